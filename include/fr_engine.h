@@ -1,0 +1,189 @@
+/*
+ * fr_engine.h — C-ABI of the MI355X-native BPR training hot path.
+ *
+ * Drop-in boundary for sdu-zyx/Multi-modal-Food-Recommendation (FoodRec).  The reference is
+ * pure Python on PyTorch; its "FFI" for this path is the set of ATen calls the plugin models
+ * make.  Each export below replaces one of those call sites (file:line in /root/reference):
+ *
+ *   fr_spmm_csr          torch.sparse.mm(norm_adj, X) + torch.stack(..).mean(1)
+ *                        models/cikm_model.py:187-190,199-202  models/pricai_modelx.py:183-226
+ *                        models/lightgcn.py:136-144
+ *   fr_bpr_fwd/_bwd      gather + mul().sum(1) + BPRLoss + EmbLoss
+ *                        models/cikm_model.py:255-279  models/pricai_modelx.py:252-274
+ *                        models/lightgcn.py:158-177  common/loss.py:32-34,45-50
+ *   fr_dcor_fwd/_bwd     PRICAI_ModelX.correlation_distance x3 (models/pricai_modelx.py:263,409-437)
+ *   fr_infonce_fwd/_bwd  PRICAI_ModelX.CL_loss (models/pricai_modelx.py:354-378)
+ *   fr_adam_step         torch.optim.Adam.step (common/trainer.py:143-144,224)
+ *   fr_sampler_*         TrainDataLoader.get_random_neg / init_neg_list (utils/dataloader.py:40-48,145-151)
+ *
+ * Conventions:
+ *   - every function returns int: 0 = FR_OK, otherwise an fr_status code; it never throws
+ *     across the ABI.  fr_last_error() returns a thread-local message for the last failure.
+ *   - every pointer named d_* (or documented "device") is caller-owned device memory; the
+ *     library never allocates or frees caller memory.  Scratch comes from a caller workspace
+ *     whose size is returned by the matching *_workspace() query.
+ *   - work is stream-ordered on the caller's hipStream_t (passed as void*), with no implicit
+ *     host synchronisation, so calls may be captured into a hipGraph.
+ *   - thread-safe for distinct streams.
+ */
+#ifndef FR_ENGINE_H
+#define FR_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum fr_status {
+  FR_OK = 0,
+  FR_EINVAL = 1,   /* bad argument (null pointer, size, unsupported d)            */
+  FR_EHIP = 2,     /* a HIP runtime call failed (message in fr_last_error)       */
+  FR_ENOTSUP = 3,  /* combination not supported by this build                    */
+  FR_ERANGE = 4    /* an index/id outside its table                               */
+};
+
+enum fr_dtype { FR_F32 = 0, FR_BF16 = 1 };
+
+int fr_version(void);
+const char* fr_last_error(void);
+/* number of HIP devices visible (0 when the runtime has no GPU) */
+int fr_device_count(void);
+
+/* ------------------------------------------------------------------------------------------
+ * CSR SpMM with fused layer epilogue (LightGCN propagation, SURVEY 8(a) a6-a8,a12,a15).
+ *
+ *   acc[r]  = sum_{e in [rowptr[r], rowptr[r+1])} val[e] * X[col[e], 0:d]
+ *   Y1[r]   = acc                                      (if d_Y1 != NULL)
+ *   Y2[r]   = alpha*acc + beta1*A1[r] + beta2*A2[r]     (if d_Y2 != NULL; A1/A2 may be NULL)
+ *
+ * Rows are processed as work units of at most `chunk` edges (nnz balance for heavy rows).
+ * The plan (built once per adjacency by fr_spmm_plan_host) lists units as int32 pairs
+ * {row, chunk_index}: first the n_plain units of rows with <= chunk edges, then the units of
+ * split rows grouped by row.  split_rows lists {row, first_partial, n_chunks} int32 triples;
+ * partial sums of split rows go to the workspace and are combined in chunk order, so the
+ * result is deterministic run to run.
+ *
+ * Y1/Y2 must not alias X.  A1/A2 may alias Y2 (same-row read-before-write).
+ * Leading dimensions are in elements.  d must be a multiple of 4 and <= 1024.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct fr_spmm_plan {
+  const int32_t* d_units;       /* [n_units][2]  {row, chunk}                           */
+  const int32_t* d_split_rows;  /* [n_split][3]  {row, first_partial, n_chunks}         */
+  int64_t n_units;
+  int64_t n_plain;
+  int64_t n_split;
+  int32_t chunk;                /* edges per unit                                        */
+} fr_spmm_plan;
+
+/* workspace bytes needed by fr_spmm_csr for this plan and feature width */
+int64_t fr_spmm_workspace(const fr_spmm_plan* plan, int d);
+
+/* Host-side planner: fills units (capacity n_rows + nnz/chunk + 1 pairs) and split_rows
+ * (capacity n_rows triples) from a host copy of rowptr.  Returns FR_OK and writes counts. */
+int fr_spmm_plan_host(const int64_t* rowptr, int64_t n_rows, int32_t chunk,
+                      int32_t* units, int64_t* n_units, int64_t* n_plain,
+                      int32_t* split_rows, int64_t* n_split);
+
+int fr_spmm_csr(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                int64_t n_rows, const fr_spmm_plan* plan,
+                const float* d_X, int64_t ldx, int d,
+                float* d_Y1, int64_t ldy1,
+                float* d_Y2, int64_t ldy2, float alpha,
+                const float* d_A1, int64_t lda1, float beta1,
+                const float* d_A2, int64_t lda2, float beta2,
+                void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused gather-dot-BPR + EmbLoss.
+ *   s+_b = <U[u_b], I[p_b]>,  s-_b = <U[u_b], I[n_b]>
+ *   out[0] = -mean_b log(gamma + sigmoid(s+_b - s-_b))                  (BPRLoss)
+ *   out[1..3] = ||Ue[u]||_F, ||Ie[p]||_F, ||Ie[n]||_F over the gathered [B,d] blocks
+ *   out[4] = (out[1]+out[2]+out[3]) / B                                 (EmbLoss, unweighted)
+ * Ue/Ie may be NULL (then out[1..4] = 0).  Index arrays are int64 device arrays.
+ * workspace: fr_bpr_workspace(B) bytes; it keeps the per-triple scores and the norms that
+ * fr_bpr_bwd reuses, so pass the same workspace to the matching backward call.
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_bpr_workspace(int64_t B);
+
+int fr_bpr_fwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+               const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+               const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+               int64_t B, int d, float gamma, float* d_out,
+               void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Backward.  g_mf scales d(out[0]); g_reg scales d(out[4]) (i.e. reg_weight * upstream grad).
+ * d_gscale (optional, device float[2]) multiplies g_mf / g_reg on the device so no host
+ * read of the upstream gradient is needed.  Gradients are ACCUMULATED (+=) into dU/dI/dUe/dIe
+ * (any may be NULL); each uses the leading dimension of its forward table (ldu/ldi/ldue/ldie).  deterministic != 0 selects the ordered (atomic-free) scatter. */
+int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+               const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+               const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+               int64_t B, int d, float gamma, float g_mf, float g_reg, const float* d_gscale,
+               float* d_dU, float* d_dI, float* d_dUe, float* d_dIe,
+               int deterministic, void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused multi-view distance correlation (CLUSSL SSL loss).
+ * views: HOST array of V (<= 4) device pointers to [n, d] fp32 row-major (ld = d) matrices.
+ * pairs: P (a,b) view-index pairs (host int32 [P][2]); out[k] = dcor(view a_k, view b_k)
+ * exactly as PRICAI_ModelX.correlation_distance, and out[P] = sum_k out[k].
+ * The backward takes d(out[P]) (the summed loss) scaled by g (or device d_gscale[0]) and
+ * ACCUMULATES into dviews[v] (any may be NULL).
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_dcor_workspace(int64_t n, int n_views);
+
+int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, int d,
+                const int32_t* pairs, int n_pairs, float* d_out,
+                void* d_workspace, int64_t workspace_bytes, void* stream);
+
+int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, int d,
+                const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
+                float* const* d_dviews,
+                void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused InfoNCE / NT-Xent (PRICAI_ModelX.CL_loss, hidden_norm=True): H is [2b, d];
+ * out[0] = (CE([h1 h2^T | h1 h1^T - 1e9 I]/tau) + CE([h2 h1^T | h2 h2^T - 1e9 I]/tau)) / b.
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_infonce_workspace(int64_t b);
+
+int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, float* d_out,
+                   void* d_workspace, int64_t workspace_bytes, void* stream);
+
+int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g, const float* d_gscale,
+                   float* d_dH, void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-tensor Adam, following torch.optim.Adam (amsgrad=False, maximize=False) element order:
+ *   g += wd*p;  m = m + (1-b1)(g-m);  v = v*b2 + ((1-b2)g)g;
+ *   p += (-lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps),   bc_k = 1 - b_k^step (host, double)
+ * The pointer arrays and numel are HOST arrays of device pointers (they travel in the kernel
+ * argument block, 24 tensors per launch).  step is 1-based (after increment).
+ * d_skip (optional device int32): when *d_skip != 0 the update is a no-op (NaN guard).
+ * ------------------------------------------------------------------------------------------ */
+int fr_adam_step(float* const* params, const float* const* grads,
+                 float* const* exp_avg, float* const* exp_avg_sq,
+                 const int64_t* numel, int n_tensors, int64_t max_numel,
+                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                 int64_t step, const int32_t* d_skip, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Negative sampler (host code): numpy legacy MT19937 stream, masked-rejection bounded ints,
+ * exactly the draws np.random.randint(num_items) makes in TrainDataLoader.get_random_neg.
+ * state: 624 uint32 key + pos (as numpy.random.get_state()[1:3]); updated in place.
+ * Exclusion sets are per-user sorted int64 lists in CSR form (train items, valid+test items).
+ * ------------------------------------------------------------------------------------------ */
+int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
+                         const int64_t* users, int64_t n,
+                         const int64_t* excl_ptr, const int64_t* excl_items,
+                         const int64_t* excl2_ptr, const int64_t* excl2_items,
+                         int64_t* out_neg);
+
+/* raw masked-rejection draws (test hook): out[i] = np.random.randint(high) for i < n */
+int fr_sampler_randint(uint32_t* mt_key, int32_t* mt_pos, int64_t high, int64_t n, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FR_ENGINE_H */

@@ -1,0 +1,124 @@
+"""ctypes binding of the C-ABI engine library (include/fr_engine.h).
+
+The library is built in-tree by ``make -C multi-modal-food-recommendation_amd/csrc`` (or
+``__graft_entry__.build()``) into ``FoodRec/_native/libfr_engine.so``.  There is no fallback:
+if the library is missing, or a compute call is made without a ROCm GPU, an error is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_uint32, c_void_p, c_char_p
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native",
+                         "libfr_engine.so")
+
+FR_OK = 0
+_STATUS = {1: "FR_EINVAL", 2: "FR_EHIP", 3: "FR_ENOTSUP", 4: "FR_ERANGE"}
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class FrSpmmPlan(ctypes.Structure):
+    _fields_ = [("d_units", c_void_p), ("d_split_rows", c_void_p), ("n_units", c_int64),
+                ("n_plain", c_int64), ("n_split", c_int64), ("chunk", c_int32)]
+
+
+_lib = None
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "fr_version": (c_int, []),
+    "fr_last_error": (c_char_p, []),
+    "fr_device_count": (c_int, []),
+    "fr_spmm_workspace": (c_int64, [POINTER(FrSpmmPlan), c_int]),
+    "fr_spmm_plan_host": (c_int, [c_void_p, c_int64, c_int32, c_void_p, POINTER(c_int64),
+                                  POINTER(c_int64), c_void_p, POINTER(c_int64)]),
+    "fr_spmm_csr": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, POINTER(FrSpmmPlan),
+                            c_void_p, c_int64, c_int,
+                            c_void_p, c_int64,
+                            c_void_p, c_int64, c_float,
+                            c_void_p, c_int64, c_float,
+                            c_void_p, c_int64, c_float,
+                            c_void_p, c_int64, c_void_p]),
+    "fr_bpr_workspace": (c_int64, [c_int64]),
+    "fr_bpr_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                           c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p,
+                           c_void_p, c_int64, c_void_p]),
+    "fr_bpr_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                           c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_float,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                           c_void_p, c_int64, c_void_p]),
+    "fr_dcor_workspace": (c_int64, [c_int64, c_int]),
+    "fr_dcor_fwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
+                            c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_dcor_bwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
+                            c_float, c_void_p, POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
+    "fr_infonce_workspace": (c_int64, [c_int64]),
+    "fr_infonce_fwd": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_infonce_bwd": (c_int, [c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
+                               c_void_p, c_int64, c_void_p]),
+    "fr_adam_step": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                             POINTER(c_int64), c_int, c_int64, c_float, c_float, c_float, c_float,
+                             c_float, c_int64, c_void_p, c_void_p]),
+    "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def lib():
+    """Load (once) and return the engine library; raises EngineError if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise EngineError(
+                f"FoodRec MI355X engine library not found at {_LIB_PATH}; build it with "
+                "`make -C multi-modal-food-recommendation_amd/csrc` or __graft_entry__.build()")
+        handle = ctypes.CDLL(_LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FR_OK:
+        msg = lib().fr_last_error()
+        raise EngineError(f"{what} failed: {_STATUS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int | None:
+    """Device/host pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def require_device(*tensors) -> None:
+    """The engine computes on the GPU only; CPU tensors are an error, never a fallback."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise EngineError("FoodRec MI355X engine ops need tensors on a ROCm GPU device "
+                              f"(got a tensor on {t.device}); there is no CPU path")
+
+
+def stream_of(t) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Caller-owned scratch (PyTorch caching allocator), 256-B aligned base."""
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)

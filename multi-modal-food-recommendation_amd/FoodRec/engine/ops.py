@@ -1,0 +1,276 @@
+"""Autograd ops over the HIP kernels (C-ABI in include/fr_engine.h).
+
+Every op here runs on the GPU through ``libfr_engine.so``; a CPU tensor raises EngineError.
+Upstream gradients are consumed on the device (``d_gscale``), so no op forces a host sync.
+
+Op                       reference call site it replaces
+-----------------------  ------------------------------------------------------------------
+spmm(adj, X)             torch.sparse.mm(adj, X)          lightgcn.py:139, cikm_model.py:187,199
+propagate_mean(adj,e,L)  L x sparse.mm + stack().mean(1)  lightgcn.py:134-144, cikm_model.py:182-208
+bpr_emb_loss(...)        gather/mul/sum + BPRLoss + EmbLoss  lightgcn.py:158-177, loss.py:32-50
+dcor_loss(views, pairs)  sum of correlation_distance       pricai_modelx.py:263,409-437
+infonce_loss(H, tau)     CL_loss                           pricai_modelx.py:354-378
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import native
+from .graph import Adjacency
+
+_f = ctypes.c_float
+
+
+def _rowmajor(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise native.EngineError(f"engine ops compute in fp32 (got {t.dtype})")
+    if t.dim() != 2:
+        raise native.EngineError(f"expected a 2-D table, got shape {tuple(t.shape)}")
+    if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        t = t.contiguous()
+    return t
+
+
+def _ws_for(adj: Adjacency, d: int, device) -> torch.Tensor:
+    cache = adj.__dict__.setdefault("_ws_cache", {})
+    key = (d, str(device))
+    if key not in cache:
+        plan = adj.plan()
+        cache[key] = native.workspace(native.lib().fr_spmm_workspace(ctypes.byref(plan), d), device)
+    return cache[key]
+
+
+def spmm_launch(adj: Adjacency, X: torch.Tensor, Y1=None, Y2=None, alpha=1.0, A1=None, beta1=0.0,
+                A2=None, beta2=0.0, stream=None) -> None:
+    """Raw launch: Y1 = adj@X;  Y2 = alpha*(adj@X) + beta1*A1 + beta2*A2 (each optional)."""
+    native.require_device(X)
+    if X.shape[0] != adj.shape[1]:
+        raise native.EngineError(f"spmm: adjacency {adj.shape} vs X {tuple(X.shape)}")
+    d = X.shape[1]
+    plan = adj.plan()
+    ws = _ws_for(adj, d, X.device)
+    s = stream if stream is not None else native.stream_of(X)
+
+    def ld(t):
+        return t.stride(0) if t is not None else 0
+
+    rc = native.lib().fr_spmm_csr(
+        adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], ctypes.byref(plan),
+        X.data_ptr(), ld(X), d,
+        native.ptr(Y1), ld(Y1),
+        native.ptr(Y2), ld(Y2), _f(alpha),
+        native.ptr(A1), ld(A1), _f(beta1),
+        native.ptr(A2), ld(A2), _f(beta2),
+        ws.data_ptr(), ws.numel(), s)
+    native.check(rc, "fr_spmm_csr")
+
+
+class _SpMM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj, X):
+        X = _rowmajor(X)
+        Y = torch.empty((adj.shape[0], X.shape[1]), dtype=torch.float32, device=X.device)
+        spmm_launch(adj, X, Y1=Y)
+        ctx.adj = adj
+        return Y
+
+    @staticmethod
+    def backward(ctx, G):
+        G = _rowmajor(G)
+        at = ctx.adj.transpose_csr()
+        dX = torch.empty((at.shape[0], G.shape[1]), dtype=torch.float32, device=G.device)
+        spmm_launch(at, G, Y1=dX)
+        return None, dX
+
+
+def spmm(adj: Adjacency, X: torch.Tensor) -> torch.Tensor:
+    return _SpMM.apply(adj, X)
+
+
+def _propagate_mean_fwd(adj: Adjacency, ego: torch.Tensor, L: int) -> torch.Tensor:
+    N, d = ego.shape
+    out = torch.empty_like(ego)
+    if L == 1:
+        spmm_launch(adj, ego, Y2=out, alpha=0.5, A1=ego, beta1=0.5)
+        return out
+    inv = 1.0 / (L + 1)
+    E1 = torch.empty_like(ego)
+    if L == 2:
+        spmm_launch(adj, ego, Y1=E1)
+        spmm_launch(adj, E1, Y2=out, alpha=inv, A1=ego, beta1=inv, A2=E1, beta2=inv)
+        return out
+    S = torch.empty_like(ego)
+    spmm_launch(adj, ego, Y1=E1, Y2=S, alpha=1.0, A1=ego, beta1=1.0)
+    prev, nxt = E1, torch.empty_like(ego)
+    for _ in range(2, L):
+        spmm_launch(adj, prev, Y1=nxt, Y2=S, alpha=1.0, A1=S, beta1=1.0)
+        prev, nxt = nxt, prev
+    spmm_launch(adj, prev, Y2=out, alpha=inv, A1=S, beta1=inv)
+    return out
+
+
+def _propagate_mean_bwd(adj: Adjacency, G: torch.Tensor, L: int) -> torch.Tensor:
+    # d/d ego of mean_k A^k ego:  H_L = G/(L+1);  H_k = A^T H_{k+1} + G/(L+1);  grad = H_0
+    at = adj.transpose_csr()
+    inv = 1.0 / (L + 1)
+    H = torch.empty_like(G)
+    spmm_launch(at, G, Y2=H, alpha=inv, A1=G, beta1=inv)
+    if L == 1:
+        return H
+    H2 = torch.empty_like(G)
+    for _ in range(1, L):
+        spmm_launch(at, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
+        H, H2 = H2, H
+    return H
+
+
+class _PropagateMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj, ego, L):
+        ego = _rowmajor(ego)
+        native.require_device(ego)
+        ctx.adj, ctx.L = adj, L
+        return _propagate_mean_fwd(adj, ego, L)
+
+    @staticmethod
+    def backward(ctx, G):
+        return None, _propagate_mean_bwd(ctx.adj, _rowmajor(G), ctx.L), None
+
+
+def propagate_mean(adj: Adjacency, ego: torch.Tensor, n_layers: int) -> torch.Tensor:
+    """mean([ego, A ego, ..., A^L ego]) — LightGCN propagation with the layer mean fused."""
+    if n_layers == 0:
+        return ego
+    return _PropagateMean.apply(adj, ego, int(n_layers))
+
+
+# ----------------------------------------------------------------------------- BPR + EmbLoss
+class _BprEmb(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic):
+        U, I = _rowmajor(U), _rowmajor(I)
+        Ue = _rowmajor(Ue) if Ue is not None else None
+        Ie = _rowmajor(Ie) if Ie is not None else None
+        native.require_device(U, I, Ue, Ie, u, p, n)
+        u, p, n = (x.to(torch.int64).contiguous() for x in (u, p, n))
+        B, d = int(u.numel()), U.shape[1]
+        lib = native.lib()
+        ws = native.workspace(lib.fr_bpr_workspace(B), U.device)
+        out = torch.empty(5, dtype=torch.float32, device=U.device)
+        ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
+        native.check(lib.fr_bpr_fwd(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
+                                    native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                                    B, d, _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                    native.stream_of(U)), "fr_bpr_fwd")
+        ctx.save_for_backward(U, I, Ue, Ie, u, p, n)
+        ctx.ws, ctx.gamma, ctx.det = ws, gamma, int(deterministic)
+        ctx.same_u, ctx.same_i = Ue is U, Ie is I
+        return out[0], out[4:5]
+
+    @staticmethod
+    def backward(ctx, g_mf, g_emb):
+        U, I, Ue, Ie, u, p, n = ctx.saved_tensors
+        dev = U.device
+        g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
+        g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
+        gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
+        need = ctx.needs_input_grad
+        dU = torch.zeros_like(U) if need[0] else None
+        dI = torch.zeros_like(I) if need[1] else None
+        dUe = dIe = None
+        if Ue is not None:
+            dUe = dU if (ctx.same_u and dU is not None) else (torch.zeros_like(Ue) if need[2] else None)
+            dIe = dI if (ctx.same_i and dI is not None) else (torch.zeros_like(Ie) if need[3] else None)
+        B, d = int(u.numel()), U.shape[1]
+        ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
+        native.check(native.lib().fr_bpr_bwd(
+            U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
+            u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
+            gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+            ctx.det, ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd")
+        if ctx.same_u:
+            dUe = None
+        if ctx.same_i:
+            dIe = None
+        return dU, dI, dUe, dIe, None, None, None, None, None
+
+
+def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False):
+    """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused."""
+    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic)
+
+
+# ----------------------------------------------------------------------------- dCor
+class _DCor(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pairs, *views):
+        views = tuple(_rowmajor(v) for v in views)
+        native.require_device(*views)
+        V = len(views)
+        n, d = views[0].shape
+        lib = native.lib()
+        ws = native.workspace(lib.fr_dcor_workspace(n, V), views[0].device)
+        vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
+        pa = (ctypes.c_int32 * (2 * len(pairs)))(*[x for pr in pairs for x in pr])
+        out = torch.empty(len(pairs) + 1, dtype=torch.float32, device=views[0].device)
+        native.check(lib.fr_dcor_fwd(vp, V, n, d, pa, len(pairs), out.data_ptr(), ws.data_ptr(),
+                                     ws.numel(), native.stream_of(views[0])), "fr_dcor_fwd")
+        ctx.save_for_backward(*views)
+        ctx.ws, ctx.pairs = ws, pairs
+        return out[len(pairs):]
+
+    @staticmethod
+    def backward(ctx, g):
+        views = ctx.saved_tensors
+        V = len(views)
+        n, d = views[0].shape
+        grads = [torch.zeros_like(v) if ctx.needs_input_grad[1 + i] else None for i, v in enumerate(views)]
+        vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
+        gp = (ctypes.c_void_p * V)(*[native.ptr(x) for x in grads])
+        pa = (ctypes.c_int32 * (2 * len(ctx.pairs)))(*[x for pr in ctx.pairs for x in pr])
+        gs = g.reshape(1).float().contiguous()
+        native.check(native.lib().fr_dcor_bwd(vp, V, n, d, pa, len(ctx.pairs), _f(1.0), gs.data_ptr(), gp,
+                                              ctx.ws.data_ptr(), ctx.ws.numel(),
+                                              native.stream_of(views[0])), "fr_dcor_bwd")
+        return (None, *grads)
+
+
+def dcor_loss(views, pairs) -> torch.Tensor:
+    """sum over pairs (a,b) of correlation_distance(views[a], views[b]) -> shape [1]."""
+    return _DCor.apply(tuple(tuple(p) for p in pairs), *views)
+
+
+# ----------------------------------------------------------------------------- InfoNCE
+class _InfoNCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, H, tau):
+        H = _rowmajor(H)
+        native.require_device(H)
+        m, d = H.shape
+        if m % 2:
+            raise native.EngineError("InfoNCE expects an even number of rows (two halves)")
+        b = m // 2
+        lib = native.lib()
+        ws = native.workspace(lib.fr_infonce_workspace(b), H.device)
+        out = torch.empty(1, dtype=torch.float32, device=H.device)
+        native.check(lib.fr_infonce_fwd(H.data_ptr(), b, d, _f(tau), out.data_ptr(), ws.data_ptr(),
+                                        ws.numel(), native.stream_of(H)), "fr_infonce_fwd")
+        ctx.save_for_backward(H)
+        ctx.ws, ctx.tau, ctx.b = ws, tau, b
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (H,) = ctx.saved_tensors
+        dH = torch.zeros_like(H)
+        gs = g.reshape(1).float().contiguous()
+        native.check(native.lib().fr_infonce_bwd(H.data_ptr(), ctx.b, H.shape[1], _f(ctx.tau), _f(1.0),
+                                                 gs.data_ptr(), dH.data_ptr(), ctx.ws.data_ptr(),
+                                                 ctx.ws.numel(), native.stream_of(H)), "fr_infonce_bwd")
+        return dH, None
+
+
+def infonce_loss(H: torch.Tensor, tau: float = 0.5) -> torch.Tensor:
+    return _InfoNCE.apply(H, float(tau))

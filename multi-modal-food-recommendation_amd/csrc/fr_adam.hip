@@ -1,0 +1,134 @@
+// Multi-tensor fused Adam — replaces torch.optim.Adam.step (common/trainer.py:143-144,224).
+//
+// One launch updates up to kMaxTensors parameter tensors (pointers travel in the kernel
+// argument block, no device-side descriptor table, so the call is graph-capturable).
+// Per element, in torch's single-tensor order (torch/optim/adam.py _single_tensor_adam):
+//   g  = grad (+ wd * p)
+//   m  = fma(1-b1, g - m, m)                       exp_avg.lerp_(grad, 1-beta1)
+//   v  = fma((1-b2) * g, g, v * b2)                exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+//   p  = p + (-step_size * m) / (sqrt(v) / bc2_sqrt + eps)
+// The fused/unfused choice of each step was matched element-for-element against torch-CPU's
+// Adam (m and v bit-identical; p differs by <= 1 ulp on ~3e-5 of elements).
+// 28 B of HBM traffic per parameter (p,m,v read+write, g read): HBM-bound, float4 vectorised.
+#include "fr_common.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace {
+
+constexpr int kMaxTensors = 24;
+constexpr int kChunk = 4096;  // elements per block
+
+struct AdamArgs {
+  float* p[kMaxTensors];
+  const float* g[kMaxTensors];
+  float* m[kMaxTensors];
+  float* v[kMaxTensors];
+  int64_t numel[kMaxTensors];
+  int32_t blk_start[kMaxTensors + 1];
+  int32_t vec4[kMaxTensors];
+  int n;
+};
+
+struct AdamHyper {
+  float w1;         // 1 - beta1
+  float beta2;
+  float one_m_b2;   // 1 - beta2
+  float neg_step;   // -lr / bias_correction1
+  float bc2_sqrt;
+  float eps;
+  float wd;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamHyper& h) {
+  if (h.wd != 0.f) g = __fadd_rn(g, __fmul_rn(h.wd, p));
+  m = fmaf(h.w1, __fsub_rn(g, m), m);
+  v = fmaf(__fmul_rn(h.one_m_b2, g), g, __fmul_rn(v, h.beta2));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), h.bc2_sqrt), h.eps);
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(h.neg_step, m), denom));
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, const int32_t* skip) {
+  if (skip && *skip) return;
+  int t = 0;
+  while (t + 1 < a.n && (int)blockIdx.x >= a.blk_start[t + 1]) ++t;
+  const int64_t base = (int64_t)(blockIdx.x - a.blk_start[t]) * kChunk;
+  const int64_t end = min(base + (int64_t)kChunk, a.numel[t]);
+  float* __restrict__ P = a.p[t];
+  const float* __restrict__ G = a.g[t];
+  float* __restrict__ M = a.m[t];
+  float* __restrict__ V = a.v[t];
+  if (a.vec4[t]) {
+    for (int64_t i = base + 4 * threadIdx.x; i + 3 < end; i += 4 * blockDim.x) {
+      float4 p = *reinterpret_cast<float4*>(P + i);
+      const float4 g = *reinterpret_cast<const float4*>(G + i);
+      float4 m = *reinterpret_cast<float4*>(M + i);
+      float4 v = *reinterpret_cast<float4*>(V + i);
+      adam_elem(p.x, g.x, m.x, v.x, h);
+      adam_elem(p.y, g.y, m.y, v.y, h);
+      adam_elem(p.z, g.z, m.z, v.z, h);
+      adam_elem(p.w, g.w, m.w, v.w, h);
+      *reinterpret_cast<float4*>(P + i) = p;
+      *reinterpret_cast<float4*>(M + i) = m;
+      *reinterpret_cast<float4*>(V + i) = v;
+    }
+    // scalar tail of the last chunk (numel % 4)
+    const int64_t tail0 = base + ((end - base) / 4) * 4;
+    for (int64_t i = tail0 + threadIdx.x; i < end; i += blockDim.x) adam_elem(P[i], G[i], M[i], V[i], h);
+  } else {
+    for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) adam_elem(P[i], G[i], M[i], V[i], h);
+  }
+}
+
+}  // namespace
+
+extern "C" int fr_adam_step(float* const* params, const float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, const int64_t* numel, int n_tensors,
+                            int64_t max_numel, float lr, float beta1, float beta2, float eps,
+                            float weight_decay, int64_t step, const int32_t* d_skip, void* stream) {
+  (void)max_numel;
+  FR_REQUIRE(n_tensors >= 0, "n_tensors < 0");
+  if (n_tensors == 0) return FR_OK;
+  FR_REQUIRE(params && grads && exp_avg && exp_avg_sq && numel, "null host array");
+  FR_REQUIRE(step >= 1, "step must be >= 1 (1-based, after increment)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // bias corrections in double, as the Python scalars in torch.optim.Adam
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  AdamHyper h;
+  h.w1 = (float)(1.0 - (double)beta1);
+  h.beta2 = beta2;
+  h.one_m_b2 = (float)(1.0 - (double)beta2);
+  h.neg_step = (float)(-((double)lr / bc1));
+  h.bc2_sqrt = (float)std::sqrt(bc2);
+  h.eps = eps;
+  h.wd = weight_decay;
+  for (int t0 = 0; t0 < n_tensors; t0 += kMaxTensors) {
+    AdamArgs a{};
+    a.n = 0;
+    int32_t blocks = 0;
+    for (int t = t0; t < std::min(n_tensors, t0 + kMaxTensors); ++t) {
+      FR_REQUIRE(numel[t] >= 0, "numel < 0");
+      if (numel[t] == 0) continue;
+      FR_REQUIRE(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t], "null tensor pointer");
+      const int k = a.n++;
+      a.p[k] = params[t];
+      a.g[k] = grads[t];
+      a.m[k] = exp_avg[t];
+      a.v[k] = exp_avg_sq[t];
+      a.numel[k] = numel[t];
+      a.vec4[k] = fr::aligned16(params[t]) && fr::aligned16(grads[t]) && fr::aligned16(exp_avg[t]) &&
+                  fr::aligned16(exp_avg_sq[t]);
+      a.blk_start[k] = blocks;
+      const int64_t nb = fr::ceil_div(numel[t], kChunk);
+      FR_REQUIRE(blocks + nb < INT32_MAX, "tensor too large for one launch");
+      blocks += (int32_t)nb;
+    }
+    a.blk_start[a.n] = blocks;
+    if (a.n == 0) continue;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, h, d_skip);
+    FR_LAUNCH_CHECK();
+  }
+  return FR_OK;
+}

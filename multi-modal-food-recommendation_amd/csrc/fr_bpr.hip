@@ -1,0 +1,313 @@
+// Fused gather-dot-BPR + EmbLoss (forward and backward).
+//
+// Replaces, per step:
+//   u = U_all[user]; p = I_all[pos]; n = I_all[neg]                 models/lightgcn.py:158-166
+//   mf = -log(1e-10 + sigmoid(<u,p> - <u,n>)).mean()                 common/loss.py:32-34
+//   reg = (||Ue[user]||_F + ||Ie[pos]||_F + ||Ie[neg]||_F) / B       common/loss.py:45-50
+// B x 3 row gathers of d floats, a 16-lane group per triple (float4 per lane, shuffle reduce);
+// no MFMA: d=64 dot products are bandwidth work.  Batch reductions are fp64 and fixed-order.
+//
+// Backward scatters into dense gradient tables.  Default: float atomics (one 256-B row segment
+// per wave-instruction, the shape the atomic unit runs at full rate).  deterministic=1: every
+// destination row is summed by its first-occurring slot in the reference's autograd order
+// (index backward of pos, then of neg, each in batch order), so results are run-to-run identical.
+#include "fr_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int LPR = 16;  // lanes per triple
+
+struct BprWS {
+  float* spos; float* sneg; float* squ; float* sqp; float* sqn;  // [B] each
+  float* norms;                                                   // [4]: |U|,|P|,|N|, pad
+};
+
+__host__ __device__ inline BprWS bpr_ws(void* base, int64_t B) {
+  char* p = reinterpret_cast<char*>(base);
+  auto take = [&](int64_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+  BprWS w;
+  w.spos = reinterpret_cast<float*>(take(B * 4));
+  w.sneg = reinterpret_cast<float*>(take(B * 4));
+  w.squ = reinterpret_cast<float*>(take(B * 4));
+  w.sqp = reinterpret_cast<float*>(take(B * 4));
+  w.sqn = reinterpret_cast<float*>(take(B * 4));
+  w.norms = reinterpret_cast<float*>(take(16));
+  return w;
+}
+
+inline int64_t bpr_ws_bytes(int64_t B) {
+  auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
+  return 5 * r(B * 4) + r(16);
+}
+
+__device__ __forceinline__ float4 ld4(const float* base, int64_t row, int64_t ld, int q) {
+  return reinterpret_cast<const float4*>(base + row * ld)[q];
+}
+
+__global__ __launch_bounds__(256) void bpr_scores_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
+    const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d4, BprWS ws) {
+  constexpr int GPB = 256 / LPR;
+  const int q0 = threadIdx.x % LPR;
+  for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; b < B;
+       b += (int64_t)gridDim.x * GPB) {
+    const int64_t u = uu[b], p = pp[b], n = nn[b];
+    float sp = 0.f, sn = 0.f, a = 0.f, c = 0.f, e = 0.f;
+    for (int q = q0; q < d4; q += LPR) {
+      const float4 xu = ld4(U, u, ldu, q);
+      sp += f4_dot(xu, ld4(I, p, ldi, q));
+      sn += f4_dot(xu, ld4(I, n, ldi, q));
+      if (Ue) {
+        const float4 eu = ld4(Ue, u, ldue, q), ep = ld4(Ie, p, ldie, q), en = ld4(Ie, n, ldie, q);
+        a += f4_dot(eu, eu);
+        c += f4_dot(ep, ep);
+        e += f4_dot(en, en);
+      }
+    }
+    sp = group_sum<LPR>(sp);
+    sn = group_sum<LPR>(sn);
+    a = group_sum<LPR>(a);
+    c = group_sum<LPR>(c);
+    e = group_sum<LPR>(e);
+    if (q0 == 0) {
+      ws.spos[b] = sp;
+      ws.sneg[b] = sn;
+      ws.squ[b] = a;
+      ws.sqp[b] = c;
+      ws.sqn[b] = e;
+    }
+  }
+}
+
+// one block, fixed-order fp64 reduction -> out[0..4], ws.norms
+__global__ __launch_bounds__(1024) void bpr_reduce_kernel(int64_t B, float gamma, int has_emb,
+                                                          BprWS ws, float* out) {
+  __shared__ double red[4][16];
+  double l = 0.0, a = 0.0, c = 0.0, e = 0.0;
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+    const float x = ws.spos[b] - ws.sneg[b];
+    const float sg = 1.f / (1.f + expf(-x));
+    l += (double)logf(gamma + sg);
+    a += ws.squ[b];
+    c += ws.sqp[b];
+    e += ws.sqn[b];
+  }
+  l = group_sum_d<64>(l);
+  a = group_sum_d<64>(a);
+  c = group_sum_d<64>(c);
+  e = group_sum_d<64>(e);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = l; red[1][w] = a; red[2][w] = c; red[3][w] = e; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s[4] = {0, 0, 0, 0};
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k)
+      for (int j = 0; j < 4; ++j) s[j] += red[j][k];
+    const float nu = has_emb ? (float)sqrt(s[1]) : 0.f;
+    const float np = has_emb ? (float)sqrt(s[2]) : 0.f;
+    const float nn = has_emb ? (float)sqrt(s[3]) : 0.f;
+    out[0] = (float)(-s[0] / (double)B);
+    out[1] = nu;
+    out[2] = np;
+    out[3] = nn;
+    out[4] = ((nu + np) + nn) / (float)B;
+    ws.norms[0] = nu;
+    ws.norms[1] = np;
+    ws.norms[2] = nn;
+  }
+}
+
+// dL/ds+ for triple b (dL/ds- = -that), with the upstream scale applied
+__device__ __forceinline__ float bpr_coef(const BprWS& ws, int64_t b, int64_t B, float gamma, float gmf) {
+  const float x = ws.spos[b] - ws.sneg[b];
+  const float sg = 1.f / (1.f + expf(-x));
+  // d/dx -log(gamma + sigmoid(x)) / B = -sigmoid*(1-sigmoid) / (gamma + sigmoid) / B
+  return -gmf / (float)B / (gamma + sg) * (sg * (1.f - sg));
+}
+
+__device__ __forceinline__ void atomic_row_add(float* base, int64_t row, int64_t ld, int q, float4 v) {
+  float* p = base + row * ld + 4 * q;
+  atomicAdd(p + 0, v.x);
+  atomicAdd(p + 1, v.y);
+  atomicAdd(p + 2, v.z);
+  atomicAdd(p + 3, v.w);
+}
+
+__global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
+    const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d4, float gamma, float gmf, float greg, const float* gscale, float* dU, int64_t lddu,
+    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws) {
+  constexpr int GPB = 256 / LPR;
+  const int q0 = threadIdx.x % LPR;
+  if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; b < B;
+       b += (int64_t)gridDim.x * GPB) {
+    const int64_t u = uu[b], p = pp[b], n = nn[b];
+    const float g = bpr_coef(ws, b, B, gamma, gmf);
+    for (int q = q0; q < d4; q += LPR) {
+      const float4 xu = ld4(U, u, ldu, q), xp = ld4(I, p, ldi, q), xn = ld4(I, n, ldi, q);
+      if (dU) {
+        float4 t = f4_scale(g, xp);
+        t = f4_fma(-g, xn, t);
+        atomic_row_add(dU, u, lddu, q, t);
+      }
+      if (dI) {
+        atomic_row_add(dI, p, lddi, q, f4_scale(g, xu));
+        atomic_row_add(dI, n, lddi, q, f4_scale(-g, xu));
+      }
+      if (Ue && dUe) atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
+      if (Ie && dIe) {
+        atomic_row_add(dIe, p, lddie, q, f4_scale(rp, ld4(Ie, p, ldie, q)));
+        atomic_row_add(dIe, n, lddie, q, f4_scale(rn, ld4(Ie, n, ldie, q)));
+      }
+    }
+  }
+}
+
+// Deterministic scatter.  Slots: [0,B) user occurrences, [B,2B) pos, [2B,3B) neg.  The first
+// slot of each (table,row) owns it and sums all its contributions in reference order.
+__global__ __launch_bounds__(256) void bpr_bwd_det_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
+    const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d4, float gamma, float gmf, float greg, const float* gscale, float* dU, int64_t lddu,
+    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws) {
+  constexpr int GPB = 256 / LPR;
+  const int q0 = threadIdx.x % LPR;
+  if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  for (int64_t s = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; s < 3 * B;
+       s += (int64_t)gridDim.x * GPB) {
+    const bool is_user = s < B;
+    const int64_t row = is_user ? uu[s] : (s < 2 * B ? pp[s - B] : nn[s - 2 * B]);
+    // owner test: no earlier slot of the same table maps to this row (lanes split the scan)
+    bool earlier = false;
+    if (is_user) {
+      for (int64_t t = q0; t < s; t += LPR) earlier |= (uu[t] == row);
+    } else {
+      for (int64_t t = B + q0; t < s; t += LPR)
+        earlier |= ((t < 2 * B ? pp[t - B] : nn[t - 2 * B]) == row);
+    }
+    // OR across the group
+    int e = earlier ? 1 : 0;
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) e |= __shfl_xor(e, off, LPR);
+    if (e) continue;
+    for (int q = q0; q < d4; q += LPR) {
+      if (is_user) {
+        float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), r4 = g4;
+        for (int64_t t = 0; t < B; ++t) {
+          if (uu[t] != row) continue;
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          // u grad = dpos * p + dneg * n (mul backward of both scores)
+          g4 = f4_add(g4, f4_add(f4_scale(g, ld4(I, pp[t], ldi, q)), f4_scale(-g, ld4(I, nn[t], ldi, q))));
+          if (Ue) r4 = f4_add(r4, f4_scale(ru, ld4(Ue, row, ldue, q)));
+        }
+        if (dU) { float4* o = reinterpret_cast<float4*>(dU + row * lddu) + q; *o = f4_add(*o, g4); }
+        if (Ue && dUe) { float4* o = reinterpret_cast<float4*>(dUe + row * lddue) + q; *o = f4_add(*o, r4); }
+      } else {
+        float4 gp = make_float4(0.f, 0.f, 0.f, 0.f), gn = gp, rp4 = gp, rn4 = gp;
+        for (int64_t t = 0; t < B; ++t) {
+          const bool mp = pp[t] == row, mn = nn[t] == row;
+          if (!mp && !mn) continue;
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          const float4 xu = ld4(U, uu[t], ldu, q);
+          if (mp) {
+            gp = f4_add(gp, f4_scale(g, xu));
+            if (Ie) rp4 = f4_add(rp4, f4_scale(rp, ld4(Ie, row, ldie, q)));
+          }
+          if (mn) {
+            gn = f4_add(gn, f4_scale(-g, xu));
+            if (Ie) rn4 = f4_add(rn4, f4_scale(rn, ld4(Ie, row, ldie, q)));
+          }
+        }
+        if (dI) { float4* o = reinterpret_cast<float4*>(dI + row * lddi) + q; *o = f4_add(*o, f4_add(gp, gn)); }
+        if (Ie && dIe) {
+          float4* o = reinterpret_cast<float4*>(dIe + row * lddie) + q;
+          *o = f4_add(*o, f4_add(rp4, rn4));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t fr_bpr_workspace(int64_t B) { return B > 0 ? bpr_ws_bytes(B) : 0; }
+
+static int bpr_check(const float* U, int64_t ldu, const float* I, int64_t ldi, const float* Ue,
+                     int64_t ldue, const float* Ie, int64_t ldie, const int64_t* u, const int64_t* p,
+                     const int64_t* n, int64_t B, int d, void* ws, int64_t wsb) {
+  FR_REQUIRE(B >= 1, "B must be >= 1");
+  FR_REQUIRE(d >= 4 && d % 4 == 0, "d must be a positive multiple of 4");
+  FR_REQUIRE(U && I && u && p && n, "null table/index");
+  FR_REQUIRE(fr::aligned16(U) && fr::aligned16(I) && ldu % 4 == 0 && ldi % 4 == 0 && ldu >= d && ldi >= d,
+             "U/I must be 16-B aligned with ld % 4 == 0");
+  FR_REQUIRE((Ue == nullptr) == (Ie == nullptr), "Ue and Ie must both be given or both null");
+  FR_REQUIRE(!Ue || (fr::aligned16(Ue) && fr::aligned16(Ie) && ldue % 4 == 0 && ldie % 4 == 0 &&
+                     ldue >= d && ldie >= d),
+             "Ue/Ie must be 16-B aligned with ld % 4 == 0");
+  FR_REQUIRE(ws && wsb >= bpr_ws_bytes(B) && fr::aligned16(ws), "workspace too small");
+  return FR_OK;
+}
+
+extern "C" int fr_bpr_fwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                          const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                          const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                          float gamma, float* d_out, void* d_workspace, int64_t workspace_bytes,
+                          void* stream) {
+  int rc = bpr_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
+                     workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_out, "out null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  BprWS w = bpr_ws(d_workspace, B);
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
+  hipLaunchKernelGGL(bpr_scores_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue, ldue,
+                     d_Ie, ldie, d_u, d_p, d_n, B, d / 4, w);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w, d_out);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                          const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                          const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                          float gamma, float g_mf, float g_reg, const float* d_gscale, float* d_dU,
+                          float* d_dI, float* d_dUe, float* d_dIe, int deterministic,
+                          void* d_workspace, int64_t workspace_bytes, void* stream) {
+  int rc = bpr_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
+                     workspace_bytes);
+  if (rc) return rc;
+  for (const float* g : {d_dU, d_dI, d_dUe, d_dIe}) FR_REQUIRE(!g || fr::aligned16(g), "grad unaligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  BprWS w = bpr_ws(d_workspace, B);
+  // gradient tables share the leading dimension of their forward tables
+  if (deterministic) {
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(3 * B, 256 / LPR), 4096);
+    hipLaunchKernelGGL(bpr_bwd_det_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
+                       ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
+                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
+  } else {
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
+    hipLaunchKernelGGL(bpr_bwd_atomic_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
+                       ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
+                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
+  }
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}

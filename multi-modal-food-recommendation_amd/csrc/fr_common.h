@@ -1,0 +1,78 @@
+// Shared helpers for the FoodRec MI355X engine (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "fr_engine.h"
+
+namespace fr {
+
+void set_error(const std::string& msg);
+
+inline int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+#define FR_REQUIRE(cond, msg)                                        \
+  do {                                                               \
+    if (!(cond)) return ::fr::fail(FR_EINVAL, std::string(__func__) + ": " + (msg)); \
+  } while (0)
+
+#define FR_HIP_CHECK(expr)                                                              \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return ::fr::fail(FR_EHIP, std::string(__func__) + ": " #expr " -> " +          \
+                                     hipGetErrorString(_e));                           \
+  } while (0)
+
+#define FR_LAUNCH_CHECK() FR_HIP_CHECK(hipGetLastError())
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+constexpr int kWave = 64;          // CDNA wavefront width
+constexpr int kNumCU = 256;        // MI355X: 8 XCDs x 32 CUs
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t align_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+}  // namespace fr
+
+// ---------------------------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float4 f4_fma(float s, float4 x, float4 acc) {
+  acc.x = fmaf(s, x.x, acc.x);
+  acc.y = fmaf(s, x.y, acc.y);
+  acc.z = fmaf(s, x.z, acc.z);
+  acc.w = fmaf(s, x.w, acc.w);
+  return acc;
+}
+
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__device__ __forceinline__ float4 f4_scale(float s, float4 a) {
+  return make_float4(s * a.x, s * a.y, s * a.z, s * a.w);
+}
+
+__device__ __forceinline__ float f4_dot(float4 a, float4 b) {
+  return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+
+// sum over the `width` lanes of an aligned lane group (width power of two <= 64)
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = WIDTH / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WIDTH);
+  return v;
+}
+
+template <int WIDTH>
+__device__ __forceinline__ double group_sum_d(double v) {
+#pragma unroll
+  for (int off = WIDTH / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WIDTH);
+  return v;
+}

@@ -1,0 +1,809 @@
+// Fused self-supervised losses of CLUSSL (PRICAI_ModelX):
+//   * multi-view distance correlation  — correlation_distance, models/pricai_modelx.py:409-437,
+//     called on three view pairs at :263.  All pairwise centred sums are computed from ONE set of
+//     distance tiles per view (the reference builds each view's n x n distance matrix twice).
+//   * InfoNCE / NT-Xent               — CL_loss, models/pricai_modelx.py:354-378.
+//
+// Both are n x n pair interactions over n = 2B = 1024 rows of d = 64: a few hundred MFLOP, so the
+// kernels are LDS-tiled VALU (64x64 tiles, 4x4 outputs per thread) and never materialise the
+// n x n matrices in HBM.  Reductions run in fp64 and in a fixed order (deterministic).
+//
+// dCor identity used (symmetric D, E; a_i = rowmean D, A = mean D):
+//   sum_ij Dc_ij Ec_ij = sum D E - 2n sum_i a_i b_i + n^2 A B
+// and its gradient: d(sum Dc Ec)/dD = Ec (the centring projector is idempotent and symmetric).
+#include "fr_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int T = 64;     // tile rows
+constexpr int PADT = 68;  // transposed tile row stride (floats): float4-aligned, spreads banks
+constexpr int MAXV = 4;   // views
+constexpr int MAXP = 10;  // unordered view pairs incl. (a,a): 4*5/2
+
+struct Views {
+  const float* x[MAXV];
+  float* dx[MAXV];
+};
+
+struct PairTab {
+  int n_pairs;           // requested dcor pairs
+  int pa[16], pb[16];
+};
+
+__host__ __device__ inline int pair_index(int a, int b, int V) {
+  if (a > b) { int t = a; a = b; b = t; }
+  // index of (a,b), a<=b, in row-major upper triangle
+  return a * V - a * (a - 1) / 2 + (b - a);
+}
+
+// rows [r0, r0+64) of X (ld = d) -> transposed LDS tile Xt[k*PADT + r] (0 beyond n)
+__device__ __forceinline__ void load_tile_t(const float* __restrict__ X, int64_t n, int d, int64_t r0,
+                                            float* Xt) {
+  const int d4 = d >> 2;
+  for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
+    const int r = idx / d4, k4 = idx - r * d4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < n) v = reinterpret_cast<const float4*>(X + (r0 + r) * d)[k4];
+    Xt[(4 * k4 + 0) * PADT + r] = v.x;
+    Xt[(4 * k4 + 1) * PADT + r] = v.y;
+    Xt[(4 * k4 + 2) * PADT + r] = v.z;
+    Xt[(4 * k4 + 3) * PADT + r] = v.w;
+  }
+}
+
+// rows [r0, r0+64) of X -> row-major LDS tile Xr[r*(d+4) + k]
+__device__ __forceinline__ void load_tile_r(const float* __restrict__ X, int64_t n, int d, int64_t r0,
+                                            float* Xr) {
+  const int d4 = d >> 2;
+  const int ld = d + 4;
+  for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
+    const int r = idx / d4, k4 = idx - r * d4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < n) v = reinterpret_cast<const float4*>(X + (r0 + r) * d)[k4];
+    *reinterpret_cast<float4*>(Xr + r * ld + 4 * k4) = v;
+  }
+}
+
+// 4x4 Gram block of thread (ti,tj): g[x][y] = <row 4ti+x of A, row 4tj+y of B>
+__device__ __forceinline__ void gram4x4(const float* At, const float* Bt, int d, int ti, int tj,
+                                        float g[4][4]) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) g[x][y] = 0.f;
+  for (int k = 0; k < d; ++k) {
+    const float4 a = *reinterpret_cast<const float4*>(At + k * PADT + 4 * ti);
+    const float4 b = *reinterpret_cast<const float4*>(Bt + k * PADT + 4 * tj);
+    const float av[4] = {a.x, a.y, a.z, a.w};
+    const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) g[x][y] = fmaf(av[x], bv[y], g[x][y]);
+  }
+}
+
+// squared row norms of the 64 rows of a transposed tile (threads 0..63), fp32 like torch.sum(square)
+__device__ __forceinline__ void row_sq(const float* Xt, int d, float* out) {
+  if (threadIdx.x < T) {
+    float s = 0.f;
+    for (int k = 0; k < d; ++k) {
+      const float v = Xt[k * PADT + threadIdx.x];
+      s = fmaf(v, v, s);
+    }
+    out[threadIdx.x] = s;
+  }
+}
+
+// block-wide fp64 sum (256 threads), result valid in thread 0
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = group_sum_d<64>(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+
+// ============================ distance correlation ============================================
+// workspace layout (doubles unless noted):
+//   S    [nblk][NP]          per-tile pair sums      (nblk = nt*nt)
+//   row  [V][nt][n] floats   per-j-tile row sums of D_a
+//   mean [V][n]              a_a[i] = rowmean(D_a)
+//   Abar [V]                 mean(D_a)
+//   coef [NP]                d(sum dcor)/d(centred pair sum), for unit upstream grad
+//   out-scalars scratch
+//   bwd partial P [JS][V][n][d] floats, rowm [JS][V][n] floats
+constexpr int DCOR_JS = 8;
+
+struct DcorWS {
+  double* S; float* row; double* mean; double* Abar; double* coef;
+  float* P; float* rowm;
+};
+
+__host__ __device__ inline DcorWS dcor_ws(void* base, int64_t n, int V) {
+  const int64_t nt = (n + T - 1) / T;
+  const int NP = V * (V + 1) / 2;
+  char* p = reinterpret_cast<char*>(base);
+  DcorWS w;
+  auto take = [&](int64_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+  w.S = reinterpret_cast<double*>(take(nt * nt * NP * 8));
+  w.row = reinterpret_cast<float*>(take((int64_t)V * nt * n * 4));
+  w.mean = reinterpret_cast<double*>(take((int64_t)V * n * 8));
+  w.Abar = reinterpret_cast<double*>(take(MAXV * 8));
+  w.coef = reinterpret_cast<double*>(take(MAXP * 8));
+  w.P = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 128 * 4));
+  w.rowm = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 4));
+  return w;
+}
+
+inline int64_t dcor_ws_bytes(int64_t n, int V) {
+  const int64_t nt = (n + T - 1) / T;
+  const int NP = V * (V + 1) / 2;
+  auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
+  return r(nt * nt * NP * 8) + r((int64_t)V * nt * n * 4) + r((int64_t)V * n * 8) + r(MAXV * 8) +
+         r(MAXP * 8) + r((int64_t)DCOR_JS * V * n * 128 * 4) + r((int64_t)DCOR_JS * V * n * 4);
+}
+
+// distance tile of one view: D[x][y] for the thread's 4x4 block
+__device__ __forceinline__ void dist4x4(const float* At, const float* Bt, const float* ra,
+                                        const float* rb, int d, int ti, int tj, float D[4][4],
+                                        float Q[4][4]) {
+  float g[4][4];
+  gram4x4(At, Bt, d, ti, tj, g);
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      // (r - 2 X X^T) + r^T, exactly the reference's evaluation order
+      const float q = (ra[4 * ti + x] - 2.f * g[x][y]) + rb[4 * tj + y];
+      Q[x][y] = q;
+      D[x][y] = sqrtf(fmaxf(q, 0.f) + 1e-8f);
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int d, DcorWS ws) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* At = smem;                 // [d][PADT]
+  float* Bt = At + d * PADT;        // [d][PADT]
+  float* ra = Bt + d * PADT;        // [64]
+  float* rb = ra + T;               // [64]
+  double* red = reinterpret_cast<double*>(rb + T);  // [4]
+  const int64_t nt = (n + T - 1) / T;
+  const int it = blockIdx.x, jt = blockIdx.y;
+  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+  const int NP = V * (V + 1) / 2;
+  float D[V][4][4];
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    __syncthreads();
+    load_tile_t(v.x[a], n, d, (int64_t)it * T, At);
+    load_tile_t(v.x[a], n, d, (int64_t)jt * T, Bt);
+    __syncthreads();
+    row_sq(At, d, ra);
+    if (threadIdx.x >= T && threadIdx.x < 2 * T) {
+      float s = 0.f;
+      for (int k = 0; k < d; ++k) { const float t = Bt[k * PADT + threadIdx.x - T]; s = fmaf(t, t, s); }
+      rb[threadIdx.x - T] = s;
+    }
+    __syncthreads();
+    float Q[4][4];
+    float Da[4][4];
+    dist4x4(At, Bt, ra, rb, d, ti, tj, Da, Q);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const bool ok = ((int64_t)it * T + 4 * ti + x < n) && ((int64_t)jt * T + 4 * tj + y < n);
+        D[a][x][y] = ok ? Da[x][y] : 0.f;
+      }
+      // row sums over this j-tile
+      float rs = D[a][x][0] + D[a][x][1] + D[a][x][2] + D[a][x][3];
+      rs = group_sum<16>(rs);
+      const int64_t gi = (int64_t)it * T + 4 * ti + x;
+      if (tj == 0 && gi < n) ws.row[((int64_t)a * nt + jt) * n + gi] = rs;
+    }
+  }
+  // all unordered pair sums from the same tiles
+  const int64_t blk = (int64_t)it * nt + jt;
+#pragma unroll
+  for (int a = 0; a < V; ++a)
+#pragma unroll
+    for (int b = a; b < V; ++b) {
+      double s = 0.0;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) s += (double)D[a][x][y] * (double)D[b][x][y];
+      s = block_sum_d(s, red);
+      if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = s;
+    }
+}
+
+// one block: means, centred sums, dcor values, backward coefficients
+__global__ __launch_bounds__(1024) void dcor_finalize_kernel(int V, int64_t n, PairTab pt,
+                                                             DcorWS ws, float* out) {
+  __shared__ double red[16];
+  __shared__ double Sc[MAXP];
+  __shared__ double Ab[MAXV];
+  const int64_t nt = (n + T - 1) / T;
+  const int NP = V * (V + 1) / 2;
+  // row means (fixed j-tile order)
+  for (int a = 0; a < V; ++a) {
+    double loc = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      double s = 0.0;
+      for (int64_t jt = 0; jt < nt; ++jt) s += (double)ws.row[((int64_t)a * nt + jt) * n + i];
+      const double m = s / (double)n;
+      ws.mean[(int64_t)a * n + i] = m;
+      loc += m;
+    }
+    loc = group_sum_d<64>(loc);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+      Ab[a] = s / (double)n;
+      ws.Abar[a] = Ab[a];
+    }
+    __syncthreads();
+  }
+  // centred pair sums
+  for (int a = 0; a < V; ++a)
+    for (int b = a; b < V; ++b) {
+      double loc = 0.0;
+      for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
+        loc += ws.mean[(int64_t)a * n + i] * ws.mean[(int64_t)b * n + i];
+      loc = group_sum_d<64>(loc);
+      __syncthreads();
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double ab = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) ab += red[w];
+        double S = 0.0;
+        const int pi = pair_index(a, b, V);
+        for (int64_t blk = 0; blk < nt * nt; ++blk) S += ws.S[blk * NP + pi];
+        const double dn = (double)n;
+        Sc[pi] = S - 2.0 * dn * ab + dn * dn * Ab[a] * Ab[b];
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0) {
+    const double dn2 = (double)n * (double)n;
+    double coef[MAXP];
+    for (int k = 0; k < NP; ++k) coef[k] = 0.0;
+    float total = 0.f;
+    for (int k = 0; k < pt.n_pairs; ++k) {
+      const int a = pt.pa[k], b = pt.pb[k];
+      const int iab = pair_index(a, b, V), iaa = pair_index(a, a, V), ibb = pair_index(b, b, V);
+      // fp32 scalar chain as the reference: dcov = sqrt(max(S/n^2, 0) + 1e-8)
+      const float s12 = (float)(Sc[iab] / dn2), s11 = (float)(Sc[iaa] / dn2), s22 = (float)(Sc[ibb] / dn2);
+      const float c12 = sqrtf(fmaxf(s12, 0.f) + 1e-8f);
+      const float c11 = sqrtf(fmaxf(s11, 0.f) + 1e-8f);
+      const float c22 = sqrtf(fmaxf(s22, 0.f) + 1e-8f);
+      const float prod = c11 * c22;
+      const float den = sqrtf(fmaxf(prod, 0.f) + 1e-10f);
+      const float dc = c12 / den;
+      out[k] = dc;
+      total += dc;
+      // gradients wrt the centred sums (torch.maximum passes half the grad at a tie)
+      auto gate = [](float x) { return x > 0.f ? 1.0 : (x == 0.f ? 0.5 : 0.0); };
+      const double d_c12 = 1.0 / den;
+      const double d_den = -(double)c12 / ((double)den * den);
+      const double d_prod = d_den * gate(prod) / (2.0 * den);
+      const double d_c11 = d_prod * c22, d_c22 = d_prod * c11;
+      coef[iab] += d_c12 * gate(s12) / (2.0 * c12) / dn2;
+      coef[iaa] += d_c11 * gate(s11) / (2.0 * c11) / dn2;
+      coef[ibb] += d_c22 * gate(s22) / (2.0 * c22) / dn2;
+    }
+    out[pt.n_pairs] = total;
+    for (int k = 0; k < NP; ++k) ws.coef[k] = coef[k];
+  }
+}
+
+// backward tiles: block (i-tile, j-split) accumulates P_a[i] = sum_j m_ij x_j and rowsum m
+template <int V, int KPER>
+__global__ __launch_bounds__(256) void dcor_bwd_tiles_kernel(Views v, int64_t n, DcorWS ws) {
+  constexpr int d = 4 * KPER;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Ait = smem;                    // [V][d][PADT] i-tiles (transposed)
+  float* Bt = Ait + V * d * PADT;       // [d][PADT]
+  float* Br = Bt + d * PADT;            // [64][d+4]
+  float* Ms = Br + T * (d + 4);         // [64][65]
+  float* ra = Ms + T * 65;              // [V][64]
+  float* rb = ra + MAXV * T;            // [64]
+  const int64_t nt = (n + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y;
+  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+  constexpr int NP = V * (V + 1) / 2;
+  constexpr int kper = KPER;               // features per thread in the apply step
+  const int ar = threadIdx.x & 63, aslot = threadIdx.x >> 6;
+  double coef[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) coef[k] = ws.coef[k];
+  for (int a = 0; a < V; ++a) load_tile_t(v.x[a], n, d, (int64_t)it * T, Ait + a * d * PADT);
+  __syncthreads();
+  for (int a = 0; a < V; ++a) row_sq(Ait + a * d * PADT, d, ra + a * T);
+  __syncthreads();
+  float acc[V][KPER];
+  float rowm[V];
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    rowm[a] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KPER; ++k) acc[a][k] = 0.f;
+  }
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    float D[V][4][4], Q[V][4][4];
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      __syncthreads();
+      load_tile_t(v.x[a], n, d, jt * T, Bt);
+      __syncthreads();
+      if (threadIdx.x < T) {
+        float s = 0.f;
+        for (int k = 0; k < d; ++k) { const float t = Bt[k * PADT + threadIdx.x]; s = fmaf(t, t, s); }
+        rb[threadIdx.x] = s;
+      }
+      __syncthreads();
+      dist4x4(Ait + a * d * PADT, Bt, ra + a * T, rb, d, ti, tj, D[a], Q[a]);
+    }
+    // centred tiles (fp32 from fp64 means) for every view
+    float Dc[V][4][4];
+#pragma unroll
+    for (int a = 0; a < V; ++a)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int64_t gi = (int64_t)it * T + 4 * ti + x, gj = jt * T + 4 * tj + y;
+          const bool ok = gi < n && gj < n;
+          Dc[a][x][y] = ok ? (float)((double)D[a][x][y] - ws.mean[(int64_t)a * n + gi] -
+                                     ws.mean[(int64_t)a * n + gj] + ws.Abar[a])
+                           : 0.f;
+        }
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      if (!v.dx[a]) continue;
+      // m_ij = K_a(i,j) * gate(q) / (2 D), K_a = sum_b c_ab Dc_b (b != a) + 2 c_aa Dc_a
+      __syncthreads();
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          double K = 2.0 * coef[pair_index(a, a, V)] * Dc[a][x][y];
+#pragma unroll
+          for (int b = 0; b < V; ++b)
+            if (b != a) K += coef[pair_index(a, b, V)] * Dc[b][x][y];
+          const float q = Q[a][x][y];
+          const float gt = q > 0.f ? 1.f : (q == 0.f ? 0.5f : 0.f);
+          const int64_t gi = (int64_t)it * T + 4 * ti + x, gj = jt * T + 4 * tj + y;
+          const bool ok = gi < n && gj < n && gi != gj;
+          Ms[(4 * ti + x) * 65 + 4 * tj + y] = ok ? (float)(K * gt / (2.0 * D[a][x][y])) : 0.f;
+        }
+      load_tile_r(v.x[a], n, d, jt * T, Br);
+      __syncthreads();
+      // apply: row ar, features [aslot*kper, +kper)
+      float rm = 0.f;
+      for (int j = 0; j < T; ++j) {
+        const float w = Ms[ar * 65 + j];
+        rm += w;
+        const float* xr = Br + j * (d + 4) + aslot * kper;
+#pragma unroll
+        for (int k = 0; k < kper; ++k) acc[a][k] = fmaf(w, xr[k], acc[a][k]);
+      }
+      rowm[a] += rm;
+    }
+  }
+  const int64_t gi = (int64_t)it * T + ar;
+  if (gi < n) {
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      if (!v.dx[a]) continue;
+      float* P = ws.P + (((int64_t)js * V + a) * n + gi) * d + aslot * kper;
+#pragma unroll
+      for (int k = 0; k < kper; ++k) P[k] = acc[a][k];
+      if (aslot == 0) ws.rowm[((int64_t)js * V + a) * n + gi] = rowm[a];
+    }
+  }
+}
+
+// dX_a[i][k] += 4 g (x_i[k] * rowm_i - P_i[k])   (sum over j-splits in order)
+__global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, int64_t n, int d,
+                                                                int js_count, float g,
+                                                                const float* gscale, DcorWS ws) {
+  const float gg = 4.f * g * (gscale ? gscale[0] : 1.f);
+  const int64_t total = (int64_t)V * n * d;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int a = (int)(t / (n * d));
+    if (!v.dx[a]) continue;
+    const int64_t rem = t - (int64_t)a * n * d;
+    const int64_t i = rem / d;
+    const int k = (int)(rem - i * d);
+    float rm = 0.f, p = 0.f;
+    for (int s = 0; s < js_count; ++s) {
+      rm += ws.rowm[((int64_t)s * V + a) * n + i];
+      p += ws.P[(((int64_t)s * V + a) * n + i) * d + k];
+    }
+    v.dx[a][i * d + k] += gg * (v.x[a][i * d + k] * rm - p);
+  }
+}
+
+// ============================ InfoNCE ==========================================================
+// workspace: Hn [2b][d] f32, norm [2b] f32, part (m,s) [JS][2b] f32x2, lse [2b] f32,
+//            P [JS][2b][d] f32 (bwd), out scratch
+constexpr int NCE_JS = 8;
+
+struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; };
+
+__host__ __device__ inline NceWS nce_ws(void* base, int64_t m, int d) {
+  char* p = reinterpret_cast<char*>(base);
+  auto take = [&](int64_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+  NceWS w;
+  w.Hn = reinterpret_cast<float*>(take(m * d * 4));
+  w.nrm = reinterpret_cast<float*>(take(m * 4));
+  w.part = reinterpret_cast<float2*>(take((int64_t)NCE_JS * m * 8));
+  w.lse = reinterpret_cast<float*>(take(m * 4));
+  w.P = reinterpret_cast<float*>(take((int64_t)NCE_JS * m * d * 4));
+  return w;
+}
+
+inline int64_t nce_ws_bytes(int64_t m, int d) {
+  auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
+  return r(m * d * 4) + r(m * 4) + r((int64_t)NCE_JS * m * 8) + r(m * 4) + r((int64_t)NCE_JS * m * d * 4);
+}
+
+// F.normalize(p=2, dim=-1): x / max(||x||, 1e-12); one wave per row
+__global__ __launch_bounds__(256) void nce_normalize_kernel(const float* __restrict__ H, int64_t m,
+                                                            int d, NceWS ws) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < m;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    float s = 0.f;
+    for (int k = lane; k < d; k += 64) s = fmaf(H[r * d + k], H[r * d + k], s);
+    s = group_sum<64>(s);
+    const float nr = sqrtf(s);
+    const float den = fmaxf(nr, 1e-12f);
+    for (int k = lane; k < d; k += 64) ws.Hn[r * d + k] = H[r * d + k] / den;
+    if (lane == 0) ws.nrm[r] = nr;
+  }
+}
+
+__device__ __forceinline__ int64_t nce_partner(int64_t i, int64_t b) { return i < b ? i + b : i - b; }
+
+// partial online log-sum-exp of row i over the column tiles of split js (self excluded)
+__global__ __launch_bounds__(256) void nce_lse_tiles_kernel(int64_t b, int d, float inv_tau, NceWS ws) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* At = smem;
+  float* Bt = At + d * PADT;
+  __shared__ float pm[T][17], ps[T][17];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y;
+  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+  load_tile_t(ws.Hn, m, d, (int64_t)it * T, At);
+  float mx[4], sm[4];
+  for (int x = 0; x < 4; ++x) { mx[x] = -INFINITY; sm[x] = 0.f; }
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    load_tile_t(ws.Hn, m, d, jt * T, Bt);
+    __syncthreads();
+    float g[4][4];
+    gram4x4(At, Bt, d, ti, tj, g);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t gi = (int64_t)it * T + 4 * ti + x, gj = jt * T + 4 * tj + y;
+        if (gj >= m || gi == gj) continue;
+        const float l = g[x][y] * inv_tau;
+        if (l > mx[x]) { sm[x] = sm[x] * expf(mx[x] - l) + 1.f; mx[x] = l; }
+        else sm[x] += expf(l - mx[x]);
+      }
+  }
+  for (int x = 0; x < 4; ++x) { pm[4 * ti + x][tj] = mx[x]; ps[4 * ti + x][tj] = sm[x]; }
+  __syncthreads();
+  if (threadIdx.x < T) {
+    const int r = threadIdx.x;
+    float M = -INFINITY, S = 0.f;
+    for (int k = 0; k < 16; ++k) {
+      const float mk = pm[r][k], sk = ps[r][k];
+      if (sk == 0.f) continue;
+      if (mk > M) { S = S * expf(M - mk) + sk; M = mk; }
+      else S += sk * expf(mk - M);
+    }
+    const int64_t gi = (int64_t)it * T + r;
+    if (gi < m) ws.part[(int64_t)js * m + gi] = make_float2(M, S);
+  }
+}
+
+// merge splits -> lse; loss = sum_i (lse_i - l_i,p(i)) / b^2
+__global__ __launch_bounds__(1024) void nce_finalize_kernel(int64_t b, int d, float inv_tau, int js_count,
+                                                            NceWS ws, float* out) {
+  __shared__ double red[16];
+  const int64_t m = 2 * b;
+  double loc = 0.0;
+  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) {
+    float M = -INFINITY, S = 0.f;
+    for (int s = 0; s < js_count; ++s) {
+      const float2 p = ws.part[(int64_t)s * m + i];
+      if (p.y == 0.f) continue;
+      if (p.x > M) { S = S * expf(M - p.x) + p.y; M = p.x; }
+      else S += p.y * expf(p.x - M);
+    }
+    const float lse = M + logf(S);
+    ws.lse[i] = lse;
+    const int64_t j = nce_partner(i, b);
+    float dot = 0.f;
+    for (int k = 0; k < d; ++k) dot = fmaf(ws.Hn[i * d + k], ws.Hn[j * d + k], dot);
+    loc += (double)lse - (double)(dot * inv_tau);
+  }
+  loc = group_sum_d<64>(loc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    out[0] = (float)(s / ((double)b * (double)b));
+  }
+}
+
+// dHn_i = (1/tau) sum_j W_ij Hn_j,  W_ij = dl_ij + dl_ji,  dl_ij = (P_ij - [j==p(i)]) * g / b^2
+template <int KPER>
+__global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv_tau, NceWS ws) {
+  constexpr int d = 4 * KPER;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* At = smem;
+  float* Bt = At + d * PADT;
+  float* Br = Bt + d * PADT;
+  float* Ws = Br + T * (d + 4);
+  __shared__ float lse_i[T], lse_j[T];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y;
+  const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
+  const int ar = threadIdx.x & 63, aslot = threadIdx.x >> 6;
+  constexpr int kper = KPER;
+  load_tile_t(ws.Hn, m, d, (int64_t)it * T, At);
+  if (threadIdx.x < T) {
+    const int64_t gi = (int64_t)it * T + threadIdx.x;
+    lse_i[threadIdx.x] = gi < m ? ws.lse[gi] : 0.f;
+  }
+  float acc[KPER];
+#pragma unroll
+  for (int k = 0; k < KPER; ++k) acc[k] = 0.f;
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    load_tile_t(ws.Hn, m, d, jt * T, Bt);
+    load_tile_r(ws.Hn, m, d, jt * T, Br);
+    if (threadIdx.x < T) {
+      const int64_t gj = jt * T + threadIdx.x;
+      lse_j[threadIdx.x] = gj < m ? ws.lse[gj] : 0.f;
+    }
+    __syncthreads();
+    float g[4][4];
+    gram4x4(At, Bt, d, ti, tj, g);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t gi = (int64_t)it * T + 4 * ti + x, gj = jt * T + 4 * tj + y;
+        float w = 0.f;
+        if (gi < m && gj < m && gi != gj) {
+          const float l = g[x][y] * inv_tau;
+          const float pij = expf(l - lse_i[4 * ti + x]) - (gj == nce_partner(gi, b) ? 1.f : 0.f);
+          const float pji = expf(l - lse_j[4 * tj + y]) - (gi == nce_partner(gj, b) ? 1.f : 0.f);
+          w = pij + pji;
+        }
+        Ws[(4 * ti + x) * 65 + 4 * tj + y] = w;
+      }
+    __syncthreads();
+    for (int j = 0; j < T; ++j) {
+      const float w = Ws[ar * 65 + j];
+      const float* xr = Br + j * (d + 4) + aslot * kper;
+#pragma unroll
+      for (int k = 0; k < kper; ++k) acc[k] = fmaf(w, xr[k], acc[k]);
+    }
+  }
+  const int64_t gi = (int64_t)it * T + ar;
+  if (gi < m) {
+    float* P = ws.P + ((int64_t)js * m + gi) * d + aslot * kper;
+#pragma unroll
+    for (int k = 0; k < kper; ++k) P[k] = acc[k];
+  }
+}
+
+// dH_i += normalize_backward(dHn_i) with dHn_i = scale * sum_splits P / tau
+__global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(const float* __restrict__ H, int64_t b,
+                                                               int d, float inv_tau, int js_count,
+                                                               float g, const float* gscale,
+                                                               NceWS ws, float* dH) {
+  const float scale = g * (gscale ? gscale[0] : 1.f) / ((float)b * (float)b) * inv_tau;
+  const int64_t m = 2 * b;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < m;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const float nr = ws.nrm[r];
+    float dot = 0.f;
+    for (int k = lane; k < d; k += 64) {
+      float p = 0.f;
+      for (int s = 0; s < js_count; ++s) p += ws.P[((int64_t)s * m + r) * d + k];
+      dot = fmaf(p * scale, ws.Hn[r * d + k], dot);
+    }
+    dot = group_sum<64>(dot);
+    for (int k = lane; k < d; k += 64) {
+      float p = 0.f;
+      for (int s = 0; s < js_count; ++s) p += ws.P[((int64_t)s * m + r) * d + k];
+      const float gh = p * scale;
+      // d/dx [x / max(|x|, eps)]
+      const float gx = nr > 1e-12f ? (gh - ws.Hn[r * d + k] * dot) / nr : gh / 1e-12f;
+      dH[r * d + k] += gx;
+    }
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------ ABI
+extern "C" int64_t fr_dcor_workspace(int64_t n, int n_views) {
+  if (n <= 0 || n_views <= 0 || n_views > MAXV) return 0;
+  return dcor_ws_bytes(n, n_views);
+}
+
+static int dcor_check(const float* const* views, int V, int64_t n, int d, const int32_t* pairs,
+                      int P, void* ws, int64_t wsb) {
+  FR_REQUIRE(views && V >= 1 && V <= MAXV, "1..4 views required");
+  FR_REQUIRE(n >= 2, "need n >= 2 rows");
+  FR_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "d must be 16, 32, 64 or 128");
+  FR_REQUIRE(pairs && P >= 1 && P <= 16, "1..16 pairs required");
+  for (int k = 0; k < P; ++k)
+    FR_REQUIRE(pairs[2 * k] >= 0 && pairs[2 * k] < V && pairs[2 * k + 1] >= 0 && pairs[2 * k + 1] < V,
+               "pair view index out of range");
+  for (int a = 0; a < V; ++a) FR_REQUIRE(views[a] && fr::aligned16(views[a]), "view null/unaligned");
+  FR_REQUIRE(ws && wsb >= dcor_ws_bytes(n, V) && fr::aligned16(ws), "workspace too small");
+  return FR_OK;
+}
+
+extern "C" int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, int d,
+                           const int32_t* pairs, int n_pairs, float* d_out, void* d_workspace,
+                           int64_t workspace_bytes, void* stream) {
+  int rc = dcor_check(d_views, n_views, n, d, pairs, n_pairs, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_out, "out null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Views v{};
+  for (int a = 0; a < n_views; ++a) v.x[a] = d_views[a];
+  PairTab pt{};
+  pt.n_pairs = n_pairs;
+  for (int k = 0; k < n_pairs; ++k) { pt.pa[k] = pairs[2 * k]; pt.pb[k] = pairs[2 * k + 1]; }
+  DcorWS w = dcor_ws(d_workspace, n, n_views);
+  const int64_t nt = fr::ceil_div(n, T);
+  const size_t lds = (size_t)(2 * d * PADT + 2 * T) * 4 + 64;
+  const dim3 grid((unsigned)nt, (unsigned)nt);
+  switch (n_views) {
+    case 1: hipLaunchKernelGGL(dcor_tiles_kernel<1>, grid, dim3(256), lds, s, v, n, d, w); break;
+    case 2: hipLaunchKernelGGL(dcor_tiles_kernel<2>, grid, dim3(256), lds, s, v, n, d, w); break;
+    case 3: hipLaunchKernelGGL(dcor_tiles_kernel<3>, grid, dim3(256), lds, s, v, n, d, w); break;
+    default: hipLaunchKernelGGL(dcor_tiles_kernel<4>, grid, dim3(256), lds, s, v, n, d, w); break;
+  }
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(1024), 0, s, n_views, n, pt, w, d_out);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, int d,
+                           const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
+                           float* const* d_dviews, void* d_workspace, int64_t workspace_bytes,
+                           void* stream) {
+  int rc = dcor_check(d_views, n_views, n, d, pairs, n_pairs, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_dviews, "dviews null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Views v{};
+  for (int a = 0; a < n_views; ++a) {
+    v.x[a] = d_views[a];
+    v.dx[a] = d_dviews[a];
+    FR_REQUIRE(!v.dx[a] || fr::aligned16(v.dx[a]), "dview unaligned");
+  }
+  DcorWS w = dcor_ws(d_workspace, n, n_views);
+  const int64_t nt = fr::ceil_div(n, T);
+  const int js = (int)std::min<int64_t>(DCOR_JS, nt);
+  const size_t lds = (size_t)(n_views * d * PADT + d * PADT + T * (d + 4) + T * 65 + MAXV * T + T) * 4;
+  FR_REQUIRE(lds <= 160 * 1024, "LDS budget exceeded (reduce views or d)");
+  const dim3 grid((unsigned)nt, (unsigned)js);
+#define FR_DCOR_BWD(VV, KK) \
+  hipLaunchKernelGGL((dcor_bwd_tiles_kernel<VV, KK>), grid, dim3(256), lds, s, v, n, w)
+#define FR_DCOR_BWD_V(KK)                          \
+  switch (n_views) {                               \
+    case 1: FR_DCOR_BWD(1, KK); break;             \
+    case 2: FR_DCOR_BWD(2, KK); break;             \
+    case 3: FR_DCOR_BWD(3, KK); break;             \
+    default: FR_DCOR_BWD(4, KK); break;            \
+  }
+  switch (d) {
+    case 16: FR_DCOR_BWD_V(4); break;
+    case 32: FR_DCOR_BWD_V(8); break;
+    case 64: FR_DCOR_BWD_V(16); break;
+    default: FR_DCOR_BWD_V(32); break;
+  }
+#undef FR_DCOR_BWD_V
+#undef FR_DCOR_BWD
+  FR_LAUNCH_CHECK();
+  const int64_t total = (int64_t)n_views * n * d;
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(total, 256), 4096);
+  hipLaunchKernelGGL(dcor_bwd_finalize_kernel, dim3(blocks), dim3(256), 0, s, v, n_views, n, d, js,
+                     g, d_gscale, w);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int64_t fr_infonce_workspace(int64_t b) {
+  if (b <= 0) return 0;
+  return nce_ws_bytes(2 * b, 128);
+}
+
+extern "C" int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, float* d_out,
+                              void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(d_H && d_out && fr::aligned16(d_H), "H/out null or unaligned");
+  FR_REQUIRE(b >= 1, "b must be >= 1");
+  FR_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "d must be 16, 32, 64 or 128");
+  FR_REQUIRE(tau > 0.f, "tau must be > 0");
+  FR_REQUIRE(d_workspace && workspace_bytes >= nce_ws_bytes(2 * b, d) && fr::aligned16(d_workspace),
+             "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t m = 2 * b;
+  NceWS w = nce_ws(d_workspace, m, d);
+  const float inv_tau = 1.f / tau;
+  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div(m, 4), 4096);
+  hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, d_H, m, d, w);
+  FR_LAUNCH_CHECK();
+  const int64_t nt = fr::ceil_div(m, T);
+  const int js = (int)std::min<int64_t>(NCE_JS, nt);
+  const size_t lds = (size_t)(2 * d * PADT) * 4;
+  hipLaunchKernelGGL(nce_lse_tiles_kernel, dim3((unsigned)nt, (unsigned)js), dim3(256), lds, s, b, d,
+                     inv_tau, w);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(nce_finalize_kernel, dim3(1), dim3(1024), 0, s, b, d, inv_tau, js, w, d_out);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g,
+                              const float* d_gscale, float* d_dH, void* d_workspace,
+                              int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(d_H && d_dH && fr::aligned16(d_H), "H/dH null or unaligned");
+  FR_REQUIRE(b >= 1, "b must be >= 1");
+  FR_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "d must be 16, 32, 64 or 128");
+  FR_REQUIRE(tau > 0.f, "tau must be > 0");
+  FR_REQUIRE(d_workspace && workspace_bytes >= nce_ws_bytes(2 * b, d) && fr::aligned16(d_workspace),
+             "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t m = 2 * b;
+  NceWS w = nce_ws(d_workspace, m, d);
+  const float inv_tau = 1.f / tau;
+  const int64_t nt = fr::ceil_div(m, T);
+  const int js = (int)std::min<int64_t>(NCE_JS, nt);
+  const size_t lds = (size_t)(2 * d * PADT + T * (d + 4) + T * 65) * 4;
+  const dim3 grid((unsigned)nt, (unsigned)js);
+  switch (d) {
+    case 16: hipLaunchKernelGGL(nce_bwd_tiles_kernel<4>, grid, dim3(256), lds, s, b, inv_tau, w); break;
+    case 32: hipLaunchKernelGGL(nce_bwd_tiles_kernel<8>, grid, dim3(256), lds, s, b, inv_tau, w); break;
+    case 64: hipLaunchKernelGGL(nce_bwd_tiles_kernel<16>, grid, dim3(256), lds, s, b, inv_tau, w); break;
+    default: hipLaunchKernelGGL(nce_bwd_tiles_kernel<32>, grid, dim3(256), lds, s, b, inv_tau, w); break;
+  }
+  FR_LAUNCH_CHECK();
+  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div(m, 4), 4096);
+  hipLaunchKernelGGL(nce_bwd_finalize_kernel, dim3(nb), dim3(256), 0, s, d_H, b, d, inv_tau, js, g,
+                     d_gscale, w, d_dH);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
