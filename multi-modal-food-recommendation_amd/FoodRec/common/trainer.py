@@ -1,0 +1,300 @@
+"""Trainer — the reference's training engine (common/trainer.py:71-474) on the MI355X engine.
+
+Same public surface and semantics: ``fit`` (epoch loop, LambdaLR per epoch, evaluation every
+``eval_step``, early stopping, checkpoint on improvement, final test on the best checkpoint),
+``_train_epoch`` (returns the per-component loss sums), ``_valid_by_user_epoch`` (sampled
+candidate Recall/NDCG@{10,20} + AUC), mirror-gradient variant (``mg``), NaN stop.
+
+What changes is the execution, not the results:
+  * triples come from FoodRec.engine.sampler.TripleSampler: the reference's exact RNG stream,
+    drawn natively per epoch, batches assembled on the device (no per-sample Python, no
+    per-step deepcopy unless ``mg``);
+  * Adam is the fused multi-tensor HIP kernel (FoodRec.engine.optim.FusedAdam);
+  * no host synchronisation inside the step loop: loss components accumulate on the device
+    and the NaN check is a device flag that turns the optimiser step into a no-op, read once
+    per epoch (the reference reads 4 .item()s and a NaN flag every step);
+  * evaluation scores every user's candidate list in one batched gather-dot on the device; the
+    ranking metrics then follow the reference's numpy code per user (same argsort tie order).
+Unchanged reference models (torch.sparse.mm users) are supported: their sparse adjacency
+attributes are swapped for HIP-backed Adjacency objects at construction.
+"""
+from __future__ import annotations
+
+import copy
+import itertools
+import math
+import os
+from logging import getLogger
+from time import time
+
+import numpy as np
+import torch
+import torch.optim as optim
+from torch.nn.utils.clip_grad import clip_grad_norm_
+
+from FoodRec.engine.graph import swap_sparse_attributes
+from FoodRec.engine.optim import FusedAdam
+from FoodRec.engine.sampler import BatchFeatures, TripleSampler
+from FoodRec.utils.utils import dict2str, early_stopping
+
+
+def get_auc_fast(rel_list, predictions, neg_num):
+    """trainer.py:49-52."""
+    neg_predictions = predictions[len(rel_list):]
+    auc_value = np.sum([np.sum(neg_predictions < predictions[idx]) for idx in rel_list])
+    return auc_value / (len(rel_list) * neg_num)
+
+
+def metrics_by_user(doc_list, rel_list):
+    """trainer.py:55-69: Recall and NDCG of a ranked list against the relevant index set."""
+    rel = set(rel_list)
+    dcg, hits = 0.0, 0.0
+    for i, doc in enumerate(doc_list):
+        if doc in rel:
+            dcg += 1 / (math.log(i + 2) / math.log(2))
+            hits += 1
+    idcg = 0.0
+    for i in range(min(len(doc_list), len(rel_list))):
+        idcg += 1 / (math.log(i + 2) / math.log(2))
+    return hits / len(rel_list), dcg / idcg
+
+
+class AbstractTrainer:
+    def __init__(self, config, model):
+        self.config = config
+        self.model = model
+
+    def fit(self, train_data):
+        raise NotImplementedError("Method [next] should be implemented.")
+
+    def evaluate(self, eval_data):
+        raise NotImplementedError("Method [next] should be implemented.")
+
+
+class Trainer(AbstractTrainer):
+    def __init__(self, config, model, mg=False):
+        super().__init__(config, model)
+        self.logger = getLogger()
+        self.learner = config["learner"]
+        self.learning_rate = config["learning_rate"]
+        self.epochs = config["epochs"]
+        self.eval_step = min(config["eval_step"], self.epochs)
+        self.test_step = min(config["test_step"] or self.epochs, self.epochs)
+        self.stopping_step = config["stopping_step"]
+        self.clip_grad_norm = config["clip_grad_norm"]
+        self.valid_metric = (config["valid_metric"] or "NDCG@20").lower()
+        self.valid_metric_bigger = config["valid_metric_bigger"]
+        self.test_batch_size = config["eval_batch_size"]
+        self.device = config["device"]
+        wd = config["weight_decay"]
+        self.weight_decay = (float(eval(wd)) if isinstance(wd, str) else float(wd)) if wd is not None else 0.0
+        self.req_training = config["req_training"]
+        self.start_epoch = 0
+        self.cur_step = 0
+        tmp = {f"{j.lower()}@{k}": 0.0 for j, k in itertools.product(config["metrics"] or [], config["topk"] or [])}
+        self.best_valid_score = -1
+        self.best_valid_result = tmp
+        self.best_test_upon_valid = tmp
+        self.train_loss_dict = {}
+        self.swapped_adjacencies = []
+        if self._on_gpu():
+            self.swapped_adjacencies = swap_sparse_attributes(model)
+        self.optimizer = self._build_optimizer()
+        sched = config["learning_rate_scheduler"] or [1.0, 50]
+        self.lr_scheduler = optim.lr_scheduler.LambdaLR(self.optimizer,
+                                                        lr_lambda=lambda e: sched[0] ** (e / sched[1]))
+        self.eval_type = config["eval_type"]
+        self.mg = mg
+        self.alpha1, self.alpha2, self.beta = config["alpha1"], config["alpha2"], config["beta"]
+        self._feats = None
+
+    def _on_gpu(self) -> bool:
+        return torch.device(self.device).type == "cuda"
+
+    def _build_optimizer(self):
+        params = self.model.parameters()
+        name = (self.learner or "adam").lower()
+        if name == "adam":
+            if self._on_gpu():
+                return FusedAdam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+            return optim.Adam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "sgd":
+            return optim.SGD(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "adagrad":
+            return optim.Adagrad(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        if name == "rmsprop":
+            return optim.RMSprop(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+        self.logger.warning("Received unrecognized optimizer, set default Adam optimizer")
+        return FusedAdam(params, lr=self.learning_rate) if self._on_gpu() else optim.Adam(params, lr=self.learning_rate)
+
+    # ------------------------------------------------------------------------------ training
+    def _features(self):
+        if self._feats is None:
+            self._feats = BatchFeatures(self.model.dataset if hasattr(self.model, "dataset") else self._dataset,
+                                        self.device)
+        return self._feats
+
+    def _opt_step(self, skip_flag):
+        if isinstance(self.optimizer, FusedAdam):
+            self.optimizer.step(skip_flag=skip_flag)
+        else:
+            self.optimizer.step()
+
+    def _train_epoch(self, train_data, epoch_idx, loss_func=None):
+        """One epoch.  ``train_data`` is a TripleSampler (engine path).  Returns
+        (per-component loss sums | tensor on NaN, per-batch losses, similarity sums)."""
+        if not self.req_training:
+            return 0.0, [], None
+        self.model.train()
+        loss_func = loss_func or self.model.calculate_loss
+        feats = self._features()
+        dev = torch.device(self.device)
+        acc = None
+        nan_flag = torch.zeros((), dtype=torch.int32, device=dev)
+        loss_batches = []
+        for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
+            interaction = feats.batch(u, p, n)
+            self.optimizer.zero_grad()
+            second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
+            losses = loss_func(interaction)
+            parts = losses if isinstance(losses, tuple) else (losses,)
+            loss = sum(parts)
+            vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
+            acc = vec if acc is None else acc + vec
+            nan_flag |= torch.isnan(loss.detach().reshape(-1)[0]).to(torch.int32)
+            if second_inter is not None:
+                (self.alpha1 * loss).backward()
+                self._opt_step(nan_flag)
+                self.optimizer.zero_grad()
+                l2 = loss_func(second_inter)
+                l2 = sum(l2) if isinstance(l2, tuple) else l2
+                nan_flag |= torch.isnan(l2.detach().reshape(-1)[0]).to(torch.int32)
+                (-1 * self.alpha2 * l2).backward()
+            else:
+                loss.backward()
+            if self.clip_grad_norm:
+                clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+            self._opt_step(nan_flag)
+            loss_batches.append(loss.detach())
+        if acc is None:
+            return 0.0, loss_batches, None
+        if int(nan_flag.item()):
+            self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
+            return torch.tensor(float("nan")), torch.tensor(0.0), None
+        total = tuple(acc.cpu().tolist())
+        return (total if len(total) > 1 else total[0]), loss_batches, None
+
+    # ------------------------------------------------------------------------------ evaluation
+    def _candidates(self, is_test):
+        """EvalByUserDataloader (dataloader.py:228-302): per user, pos + negatives with the
+        positives removed (the removal mutates the dataset lists in place, as the reference)."""
+        ds = self.model.dataset
+        if not is_test:
+            users, pos_lists, neg_lists = ds.valid_users, ds.validRatings, ds.validNegatives
+        else:
+            users, pos_lists, neg_lists = list(range(ds.num_users)), ds.testRatings, ds.testNegatives
+        all_users, all_items, lens, npos = [], [], [], []
+        for idx, user in enumerate(users):
+            pos, neg = pos_lists[idx], neg_lists[idx]
+            for item in pos:
+                if item in neg:
+                    neg.remove(item)
+            items = pos + neg
+            all_users.append(np.full(len(items), user, dtype=np.int64))
+            all_items.append(np.asarray(items, dtype=np.int64))
+            lens.append(len(items))
+            npos.append(len(pos))
+        return np.concatenate(all_users), np.concatenate(all_items), np.asarray(lens), np.asarray(npos)
+
+    @torch.no_grad()
+    def _score(self, users, items):
+        dev = torch.device(self.device)
+        batch = {"user_input": torch.from_numpy(users).to(dev), "item_input": torch.from_numpy(items).to(dev)}
+        if self.config["graph_inference_fast"]:
+            out = self.model.forward()
+            preds = self.model.inference_fast(batch, out[0], out[1])
+        else:
+            preds = self.model.inference_by_user(batch)
+        return preds.float().cpu().numpy()
+
+    def _valid_by_user_epoch(self, valid_data=None, is_test=False):
+        users, items, lens, npos = self._candidates(is_test)
+        preds = self._score(users, items)
+        neg_num = self.config["neg_sample_num"]
+        res = np.zeros((len(lens), 3, 2))
+        off = 0
+        for k, (ln, npo) in enumerate(zip(lens.tolist(), npos.tolist())):
+            pr = preds[off:off + ln].copy()
+            off += ln
+            gt = range(npo)
+            order = np.argsort(pr)[::-1]
+            auc = get_auc_fast(gt, pr, neg_num)
+            for j, topk in enumerate((10, 20)):
+                r, nd = metrics_by_user(order[:topk], gt)
+                res[k, 0, j], res[k, 1, j], res[k, 2, j] = r, nd, auc
+        recalls, ndcgs, aucs = res.mean(axis=0).tolist()
+        metrics = {"AUC": aucs[0], "Recall@10": recalls[0], "Recall@20": recalls[1],
+                   "NDCG@10": ndcgs[0], "NDCG@20": ndcgs[1]}
+        return metrics["NDCG@20"], metrics
+
+    # ------------------------------------------------------------------------------ fit
+    def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):
+        out = "epoch %d training [time: %.2fs, " % (epoch_idx, e_time - s_time)
+        if isinstance(losses, tuple):
+            out += ", ".join("train_loss%d: %.4f" % (i + 1, l) for i, l in enumerate(losses))
+        else:
+            out += "train loss: %.4f" % losses
+        return out + "]"
+
+    def fit(self, dataset, valid_data=None, test_data=None, hyper_tuple=None, saved=False, verbose=True):
+        self._dataset = dataset
+        ckpt_name = "{}-{}-{}={}.pt".format(self.config["model"], self.config["dataset"],
+                                           self.config["hyper_parameters"], hyper_tuple)
+        ckroot = self.config["ckp_root"] or "./ckp/"
+        os.makedirs(ckroot, exist_ok=True)
+        ckpt = os.path.join(ckroot, ckpt_name)
+        sampler = TripleSampler(dataset, self.config["train_batch_size"], self.device)
+        saved_once = False
+        for epoch_idx in range(self.start_epoch, self.epochs):
+            t0 = time()
+            self.model.pre_epoch_processing()
+            train_loss, _, _ = self._train_epoch(sampler, epoch_idx)
+            if torch.is_tensor(train_loss):
+                break
+            for group in self.optimizer.param_groups:
+                self.logger.info("======lr: %f" % group["lr"])
+            self.lr_scheduler.step()
+            self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
+            t1 = time()
+            post = self.model.post_epoch_processing()
+            if verbose:
+                self.logger.info(self._generate_train_loss_output(epoch_idx, t0, t1, train_loss))
+                if post is not None:
+                    self.logger.info(post)
+            if (epoch_idx + 1) % self.eval_step == 0:
+                v0 = time()
+                valid_score, valid_result = self._valid_by_user_epoch(is_test=False)
+                self.best_valid_score, self.cur_step, stop_flag, update_flag = early_stopping(
+                    valid_score, self.best_valid_score, self.cur_step, max_step=self.stopping_step,
+                    bigger=self.valid_metric_bigger)
+                v1 = time()
+                if verbose:
+                    self.logger.info("epoch %d evaluating [time: %.2fs, valid_score: %f]" % (epoch_idx, v1 - v0, valid_score))
+                    self.logger.info("valid result: \n" + dict2str(valid_result))
+                if update_flag:
+                    torch.save(self.model.state_dict(), ckpt)
+                    saved_once = True
+                    if verbose:
+                        self.logger.info("██ " + str(self.config["model"]) + "--Best validation results updated!!!")
+                    self.best_valid_result = valid_result
+                if stop_flag:
+                    if verbose:
+                        self.logger.info("+++++Finished training, best eval result in epoch %d" %
+                                         (epoch_idx - self.cur_step * self.eval_step))
+                    break
+        if saved_once:
+            self.model.load_state_dict(torch.load(ckpt, weights_only=True))
+        _, test_result = self._valid_by_user_epoch(is_test=True)
+        self.logger.info("test result: \n" + dict2str(test_result))
+        self.best_test_upon_valid = test_result
+        return self.best_valid_score, self.best_valid_result, self.best_test_upon_valid

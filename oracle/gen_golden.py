@@ -127,10 +127,10 @@ def main():
         model.eval()  # dropout off (CIKM is also configured with p = 0)
         with torch.no_grad():
             fw = model.forward()
-        out["fwd/user"] = fw[0].detach().numpy()
-        out["fwd/item"] = fw[1].detach().numpy()
+        out["fwd/user"] = fw[0].detach().numpy().copy()
+        out["fwd/item"] = fw[1].detach().numpy().copy()
         if name == "PRICAI_ModelX":
-            out["fwd/view_image"], out["fwd/view_text"], out["fwd/view_ingre"] = (x.numpy() for x in fw[2])
+            out["fwd/view_image"], out["fwd/view_text"], out["fwd/view_ingre"] = (x.numpy().copy() for x in fw[2])
         trainer.optimizer.zero_grad()
         losses = model.calculate_loss(batch)
         losses = losses if isinstance(losses, tuple) else (losses,)
