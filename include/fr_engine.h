@@ -165,7 +165,7 @@ int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g, const
 int fr_adam_step(float* const* params, const float* const* grads,
                  float* const* exp_avg, float* const* exp_avg_sq,
                  const int64_t* numel, int n_tensors, int64_t max_numel,
-                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                 double lr, double beta1, double beta2, double eps, double weight_decay,
                  int64_t step, const int32_t* d_skip, void* stream);
 
 /* ------------------------------------------------------------------------------------------

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_uint32, c_void_p, c_char_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_void_p
 
 import torch
 
@@ -63,8 +63,8 @@ _SIGS = {
     "fr_infonce_bwd": (c_int, [c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                                c_void_p, c_int64, c_void_p]),
     "fr_adam_step": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
-                             POINTER(c_int64), c_int, c_int64, c_float, c_float, c_float, c_float,
-                             c_float, c_int64, c_void_p, c_void_p]),
+                             POINTER(c_int64), c_int, c_int64, c_double, c_double, c_double, c_double,
+                             c_double, c_int64, c_void_p, c_void_p]),
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),

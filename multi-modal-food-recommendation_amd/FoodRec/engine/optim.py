@@ -59,8 +59,8 @@ class FusedAdam(torch.optim.Optimizer):
                 V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in plist])
                 N = (ctypes.c_int64 * n)(*[p.numel() for p in plist])
                 native.check(lib.fr_adam_step(
-                    P, G, M, V, N, n, max(p.numel() for p in plist), ctypes.c_float(group["lr"]),
-                    ctypes.c_float(beta1), ctypes.c_float(beta2), ctypes.c_float(group["eps"]),
-                    ctypes.c_float(group["weight_decay"]), step, native.ptr(skip_flag),
+                    P, G, M, V, N, n, max(p.numel() for p in plist), float(group["lr"]),
+                    float(beta1), float(beta2), float(group["eps"]),
+                    float(group["weight_decay"]), step, native.ptr(skip_flag),
                     native.stream_of(plist[0])), "fr_adam_step")
         return loss

@@ -1,0 +1,123 @@
+"""CLUSSL (PRICAI'24) on the MI355X engine — the reference's ``PRICAI_ModelX``
+(models/pricai_modelx.py).
+
+Parameters, construction order and state_dict keys are the reference's.  forward() runs the
+three item-side propagations (ingredient, image-cluster, text-cluster graphs; n_ri_layers each)
+and the user-item propagation (n_ui_layers) as fused HIP SpMM chains (:179-232).  The SSL term is
+the fused multi-view distance-correlation kernel: the three reference calls
+dcor(image,text) + dcor(image,ingre) + dcor(ingre,text) (:263) share one set of distance tiles.
+``ssl_mode: infonce`` switches to the (in the reference commented-out) InfoNCE form over the same
+view pairs, run by the fused InfoNCE kernel (CL_loss, :354-378).
+"""
+import torch
+import torch.nn as nn
+
+from FoodRec.common.abstract_recommender import GeneralRecommender
+from FoodRec.common.init import xavier_uniform_initialization
+from FoodRec.common.loss import BPRLoss, EmbLoss
+from FoodRec.engine import ops
+from FoodRec.models._graphs import side_adjacency, ui_adjacency
+
+# (image, text), (image, ingre), (ingre, text) with views ordered [image, text, ingre]
+_DCOR_PAIRS = ((0, 1), (0, 2), (2, 1))
+
+
+class CLUSSL(GeneralRecommender):
+    def __init__(self, config, dataset):
+        super().__init__(config, dataset)
+        self.device = config["device"]
+        self.config = config
+        self.dataset = dataset
+        self.n_ingredients = dataset.num_ingredients
+        self.n_cal_level = dataset.num_calories_level
+        self.n_health_level = len(dataset.health_level_multi_hot[0]) if config["use_health_level_multi_hot"] \
+            else dataset.num_health_level
+        self.interaction_matrix = dataset.train_coo_matrix
+        d = config["embedding_size"]
+        self.latent_dim = d
+        self.n_ri_layers = config["n_ri_layers"]
+        self.n_mm_layers = config["n_mm_layers"]
+        self.n_ui_layers = config["n_ui_layers"]
+        self.reg_weight = config["reg_weight"]
+        self.loss_cl = config["loss_cl"]
+        self.knn_k = config["knn_k"]
+        self.mm_image_weight = config["mm_image_weight"]
+        self.n_cluster = config["n_cluster"]
+        self.ssl_mode = (config["ssl_mode"] or "dcor").lower()
+        self.user_embedding = nn.Embedding(self.n_users, d)
+        self.item_embedding = nn.Embedding(self.n_items, d)
+        self.ingre_embedding = nn.Embedding(self.n_ingredients + 1, d, padding_idx=self.n_ingredients)
+        self.mf_loss = BPRLoss()
+        self.reg_loss = EmbLoss()
+        self.norm_adj_matrix = ui_adjacency(dataset, self.n_users, self.n_items, self.device)
+        self.image_norm_adj = side_adjacency(dataset.image_cluster_triples, self.n_items, self.n_cluster, self.device)
+        self.text_norm_adj = side_adjacency(dataset.text_cluster_triples, self.n_items, self.n_cluster, self.device)
+        self.ingre_norm_adj = side_adjacency(dataset.rIngre_triples, self.n_items, self.n_ingredients, self.device)
+        self.proj_ingre = nn.Linear(d, d)
+        self.proj_text = nn.Linear(d, d)
+        self.proj_image = nn.Linear(d, d)
+        self.image_prototype_embedding = nn.Embedding(self.n_cluster, d)
+        self.text_prototype_embedding = nn.Embedding(self.n_cluster, d)
+        self.apply(xavier_uniform_initialization)
+        self.v_center, self.t_center = None, None
+        if config["use_center_embedding"]:
+            import numpy as np
+            base = config["interaction_data_path"] + "mm_cluster/"
+            self.v_center = torch.tensor(np.load(base + "image_center.npy").astype(np.float32)).to(self.device)
+            self.t_center = torch.tensor(np.load(base + "text_center.npy").astype(np.float32)).to(self.device)
+            self.image_prototype_embedding = nn.Embedding.from_pretrained(self.v_center, freeze=False)
+            self.image_trs = nn.Linear(self.v_center.shape[1], d)
+            nn.init.xavier_normal_(self.image_trs.weight)
+            self.text_prototype_embedding = nn.Embedding.from_pretrained(self.t_center, freeze=False)
+            self.text_trs = nn.Linear(self.t_center.shape[1], d)
+            nn.init.xavier_normal_(self.text_trs.weight)
+
+    def _view(self, adj, side_table, n_side):
+        ego = torch.cat((self.item_embedding.weight, side_table), dim=0)
+        out = ops.propagate_mean(adj, ego, self.n_ri_layers)
+        return torch.split(out, [self.n_items, n_side])[0]
+
+    def forward(self):
+        item_ingre = self._view(self.ingre_norm_adj, self.ingre_embedding.weight[:-1, :], self.n_ingredients)
+        img_side = self.image_trs(self.image_prototype_embedding.weight) if self.v_center is not None \
+            else self.image_prototype_embedding.weight
+        item_image = self._view(self.image_norm_adj, img_side, self.n_cluster)
+        txt_side = self.text_trs(self.text_prototype_embedding.weight) if self.t_center is not None \
+            else self.text_prototype_embedding.weight
+        item_text = self._view(self.text_norm_adj, txt_side, self.n_cluster)
+        item_emb = item_ingre + item_image + item_text
+        ui = ops.propagate_mean(self.norm_adj_matrix, torch.cat([self.user_embedding.weight, item_emb], dim=0),
+                                self.n_ui_layers)
+        user_all, item_all = torch.split(ui, [self.n_users, self.n_items])
+        return user_all, item_all, (item_image, item_text, item_ingre)
+
+    def calculate_loss(self, batch_data):
+        user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
+        all_item = torch.cat([pos_item, neg_item], dim=0)
+        user_all, item_all, (v_img, v_txt, v_ing) = self.forward()
+        views = [v_img[all_item], v_txt[all_item], v_ing[all_item]]
+        mf_loss, emb = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
+                                        user, pos_item, neg_item)
+        if self.ssl_mode == "infonce":
+            cl = sum(ops.infonce_loss(torch.cat([views[a], views[b]], dim=0), 0.5) for a, b in _DCOR_PAIRS)
+        else:
+            cl = ops.dcor_loss(views, _DCOR_PAIRS)
+        return mf_loss, self.loss_cl * cl, self.reg_weight * emb
+
+    def inference_fast(self, batch_data, user_emb, item_emb):
+        return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
+
+    def inference_by_user(self, batch_data):
+        u, i, _ = self.forward()
+        return self.inference_fast(batch_data, u, i)
+
+    def CL_loss(self, hidden, hidden_norm=True, temperature=0.5):
+        if not hidden_norm:
+            raise NotImplementedError("the fused InfoNCE kernel implements hidden_norm=True")
+        return ops.infonce_loss(hidden, temperature)
+
+    def correlation_distance(self, x, y):
+        return ops.dcor_loss([x, y], [(0, 1)])
+
+
+PRICAI_ModelX = CLUSSL

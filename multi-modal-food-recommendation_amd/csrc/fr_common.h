@@ -50,6 +50,19 @@ __device__ __forceinline__ float4 f4_fma(float s, float4 x, float4 acc) {
   return acc;
 }
 
+// Correctly rounded f32 sqrt: v_sqrt_f32 is accurate to 1 ulp only; pick among s-1ulp, s, s+1ulp
+// by the sign of the fma residuals (the IEEE-exact expansion; matches x86 sqrtps bit for bit).
+__device__ __forceinline__ float sqrt_rn(float x) {
+  float s = __builtin_sqrtf(x);
+  const float s_dn = __int_as_float(__float_as_int(s) - 1);
+  const float s_up = __int_as_float(__float_as_int(s) + 1);
+  const float r_dn = fmaf(-s_dn, s, x);
+  const float r_up = fmaf(-s_up, s, x);
+  s = (r_dn <= 0.f) ? s_dn : s;
+  s = (r_up > 0.f) ? s_up : s;
+  return s;
+}
+
 __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
