@@ -1,0 +1,201 @@
+"""Benchmark: BPR training triples/sec on MI355X (BASELINE.json metric), one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload healthrec_allrecipes]
+
+Workload (N=1 line = BASELINE configs[1]): HealthRec (reference CIKM_Model) on a seeded synthetic
+Allrecipes-shaped dataset (U=68,768, I=45,630, ~677k train pairs, NI=19,987, 2048-d image /
+512-d text features, 7-bit health), d=64, B=512 triples per step per GPU.  A "step" is the
+reference's full training step on one batch: native triple sampling (exact reference RNG
+stream), forward (RI + UI SpMM propagation, ingredient Transformer, target attention, KD and
+health heads), the fused BPR/EmbLoss, backward, and the fused Adam update over all 125.7M
+parameters.  Inputs are resident in HBM before timing; the host->device copy of each batch's
+sampled indices is inside the step.
+
+N>1 (torch.distributed.run, RCCL): data-parallel replicas, each rank steps its own 512-triple
+batch and the dense gradient buffer is all-reduced over xGMI every step ("scaling": "weak";
+value = triples of all ranks / max-over-ranks time).
+
+Extra objects on the line:
+  roofline      dominant kernel (by measured time over the timed steps, HIP events on the launch
+                stream): algorithmic bytes per launch / average launch time vs 8 TB/s HBM peak
+  spmm          the propagation SpMM's own achieved GB/s (the metric's "SpMM HBM GB/s")
+  cpu_baseline  the oracle's CPU restatement of the same step (torch-CPU, oracle/cpu_backend.py)
+                timed on this host's cores on a bounded number of steps (rank 0, N=1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "multi-modal-food-recommendation_amd"), ROOT]
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="healthrec_allrecipes", choices=["healthrec_allrecipes"])
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", type=float, default=None,
+                    help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
+    return ap.parse_args()
+
+
+def build(device, batch, seed=0, dataset_seed=0):
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.dataset import FoodData
+    from FoodRec.utils.synthetic import make_synthetic
+    from FoodRec.utils.utils import get_model, init_seed
+    ds = make_synthetic("allrecipes", dataset_seed, negatives=False)
+    data = FoodData.from_synthetic(ds)
+    cfg = Config("CIKM_Model", "Allrecipes", {"use_gpu": device.type == "cuda", "seed": 999,
+                                             "train_batch_size": batch, "log_root": "/tmp/frlog/",
+                                             "ckp_root": "/tmp/frckp/"})
+    cfg["device"] = device
+    data.args_config = cfg
+    init_seed(999 + seed)
+    model = get_model("CIKM_Model")(cfg, data).to(device)
+    return cfg, data, model
+
+
+def main():
+    args = _args()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import profiling
+    from FoodRec.engine.dist import GradAllReduce
+    from FoodRec.engine.sampler import TripleSampler
+
+    cfg, data, model = build(device, args.batch)
+    trainer = Trainer(cfg, model)
+    if world > 1:
+        trainer.grad_hook = GradAllReduce(model, world)
+    np.random.seed(1000 + rank)  # each replica draws its own triple stream
+    sampler = TripleSampler(data, args.batch, device, replay_python_random=False)
+    feats = trainer._features()
+    state = trainer.new_step_state()
+    model.train()
+
+    def batches():
+        while True:
+            for t in sampler.epoch():
+                yield t
+
+    it = batches()
+    for i in range(args.warmup):
+        u, p, n = next(it)
+        trainer.train_step(feats.batch(u, p, n), i, state)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with profiling.timing() as timer:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            u, p, n = next(it)
+            trainer.train_step(feats.batch(u, p, n), args.warmup + i, state)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern = timer.summary()
+    assert not int(state["nan"].item()), "NaN loss during bench"
+
+    ms_per_step = elapsed / args.steps * 1e3
+    triples = args.batch * args.steps * world
+    value = triples / elapsed
+
+    dom_name = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
+    roofline = None
+    if dom_name is not None:
+        d = kern[dom_name]
+        achieved = d["gbps"]
+        roofline = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                    "traffic": args.traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
+                    "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / args.steps,
+                    "share_of_step": round(d["total_ms"] / (elapsed * 1e3), 3)}
+    spmm = None
+    if "spmm" in kern:
+        s = kern["spmm"]
+        spmm = {"achieved_gbps": round(s["gbps"], 1), "avg_launch_ms": round(s["avg_ms"], 4),
+                "bytes_per_launch": int(s["bytes_per_launch"]), "launches_per_step": s["launches"] / args.steps,
+                "frac_of_hbm_peak": round(s["gbps"] / HBM_PEAK_GBPS, 4),
+                "note": "Allrecipes-shape X tables (<=29 MB) are Infinity-Cache resident"}
+    kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "per_step_ms": round(v["total_ms"] / args.steps, 4),
+                   "gbps": round(v["gbps"], 1)} for k, v in kern.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {"metric": "BPR triples/sec + SpMM HBM GB/s, Allrecipes d=64, 1/2/4/8 MI355X",
+                "value": round(value, 1), "unit": "triples/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": "healthrec_allrecipes", "model": "HealthRec (CIKM_Model)",
+                           "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
+                           "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                           "parallelism": f"dp{world}" if world > 1 else "single"},
+                "roofline": roofline, "spmm": spmm, "kernels": kernels, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """Time the oracle's CPU restatement of the same step on this host (bounded sample)."""
+    import torch
+    from oracle import cpu_backend
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    with cpu_backend.installed():
+        from FoodRec.common.trainer import Trainer
+        from FoodRec.engine.sampler import TripleSampler
+        cfg, data, model = build(torch.device("cpu"), args.batch)
+        trainer = Trainer(cfg, model)
+        sampler = TripleSampler(data, args.batch, "cpu", replay_python_random=False)
+        feats = trainer._features()
+        state = trainer.new_step_state()
+        it = sampler.epoch()
+        u, p, n = next(it)
+        trainer.train_step(feats.batch(u, p, n), 0, state)  # warm-up
+        t0 = time.perf_counter()
+        k = max(1, args.cpu_baseline_steps)
+        for i in range(k):
+            u, p, n = next(it)
+            trainer.train_step(feats.batch(u, p, n), 1 + i, state)
+        dt = time.perf_counter() - t0
+    return {"value": round(args.batch * k / dt, 2), "unit": "triples/s", "cores": threads, "kind": "port",
+            "sample": f"{k} HealthRec training steps (B={args.batch}) of the torch-CPU oracle after 1 warm-up",
+            "ms_per_step": round(dt / k * 1e3, 1)}
+
+
+if __name__ == "__main__":
+    main()

@@ -107,6 +107,9 @@ class Trainer(AbstractTrainer):
         self.mg = mg
         self.alpha1, self.alpha2, self.beta = config["alpha1"], config["alpha2"], config["beta"]
         self._feats = None
+        # optional callable(model) run between backward and the optimiser step (e.g. the
+        # data-parallel gradient all-reduce of FoodRec.engine.dist)
+        self.grad_hook = None
 
     def _on_gpu(self) -> bool:
         return torch.device(self.device).type == "cuda"
@@ -140,48 +143,57 @@ class Trainer(AbstractTrainer):
         else:
             self.optimizer.step()
 
+    def train_step(self, interaction, batch_idx, state, loss_func=None):
+        """One optimisation step on one batch (the body of the reference's step loop,
+        trainer.py:177-227), with no host synchronisation.  ``state`` carries the device-side
+        loss accumulator and NaN flag across steps."""
+        loss_func = loss_func or self.model.calculate_loss
+        self.optimizer.zero_grad()
+        second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
+        losses = loss_func(interaction)
+        parts = losses if isinstance(losses, tuple) else (losses,)
+        loss = sum(parts)
+        vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
+        state["acc"] = vec if state.get("acc") is None else state["acc"] + vec
+        nan_flag = state["nan"]
+        nan_flag |= torch.isnan(loss.detach().reshape(-1)[0]).to(torch.int32)
+        if second_inter is not None:
+            (self.alpha1 * loss).backward()
+            self._opt_step(nan_flag)
+            self.optimizer.zero_grad()
+            l2 = loss_func(second_inter)
+            l2 = sum(l2) if isinstance(l2, tuple) else l2
+            nan_flag |= torch.isnan(l2.detach().reshape(-1)[0]).to(torch.int32)
+            (-1 * self.alpha2 * l2).backward()
+        else:
+            loss.backward()
+        if self.clip_grad_norm:
+            clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
+        if self.grad_hook is not None:
+            self.grad_hook(self.model)
+        self._opt_step(nan_flag)
+        return loss.detach()
+
+    def new_step_state(self):
+        return {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=torch.device(self.device))}
+
     def _train_epoch(self, train_data, epoch_idx, loss_func=None):
         """One epoch.  ``train_data`` is a TripleSampler (engine path).  Returns
         (per-component loss sums | tensor on NaN, per-batch losses, similarity sums)."""
         if not self.req_training:
             return 0.0, [], None
         self.model.train()
-        loss_func = loss_func or self.model.calculate_loss
         feats = self._features()
-        dev = torch.device(self.device)
-        acc = None
-        nan_flag = torch.zeros((), dtype=torch.int32, device=dev)
+        state = self.new_step_state()
         loss_batches = []
         for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
-            interaction = feats.batch(u, p, n)
-            self.optimizer.zero_grad()
-            second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
-            losses = loss_func(interaction)
-            parts = losses if isinstance(losses, tuple) else (losses,)
-            loss = sum(parts)
-            vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
-            acc = vec if acc is None else acc + vec
-            nan_flag |= torch.isnan(loss.detach().reshape(-1)[0]).to(torch.int32)
-            if second_inter is not None:
-                (self.alpha1 * loss).backward()
-                self._opt_step(nan_flag)
-                self.optimizer.zero_grad()
-                l2 = loss_func(second_inter)
-                l2 = sum(l2) if isinstance(l2, tuple) else l2
-                nan_flag |= torch.isnan(l2.detach().reshape(-1)[0]).to(torch.int32)
-                (-1 * self.alpha2 * l2).backward()
-            else:
-                loss.backward()
-            if self.clip_grad_norm:
-                clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
-            self._opt_step(nan_flag)
-            loss_batches.append(loss.detach())
-        if acc is None:
+            loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
+        if state["acc"] is None:
             return 0.0, loss_batches, None
-        if int(nan_flag.item()):
+        if int(state["nan"].item()):
             self.logger.info("Loss is nan at epoch: {}. Exiting.".format(epoch_idx))
             return torch.tensor(float("nan")), torch.tensor(0.0), None
-        total = tuple(acc.cpu().tolist())
+        total = tuple(state["acc"].cpu().tolist())
         return (total if len(total) > 1 else total[0]), loss_batches, None
 
     # ------------------------------------------------------------------------------ evaluation

@@ -1,0 +1,60 @@
+"""Multi-GPU: one process per GPU, torch.distributed over RCCL (backend "nccl") on xGMI.
+
+Round-1 scheme: data-parallel replicas.  Each rank trains on its own triple batch; after the
+backward pass the dense gradient buffer (every parameter that received a gradient, packed into
+one fp32 buffer) is all-reduced once per step and averaged, then every rank applies the same
+fused Adam update, so the replicas stay bit-identical.  (The row-sharded graph scheme of SURVEY
+8(e) is for the 10M-user synthetic graph; at Allrecipes shape the graph is replicated.)
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+class GradAllReduce:
+    """Trainer.grad_hook: average gradients over ranks with ONE collective per step."""
+
+    def __init__(self, model, world: int, group=None):
+        self.world = int(world)
+        self.group = group
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.flat = None
+        self.layout = None
+
+    def __call__(self, model):
+        live = [p for p in self.params if p.grad is not None]
+        if self.flat is None or self.layout != [id(p) for p in live]:
+            total = sum(p.numel() for p in live)
+            self.flat = torch.empty(total, dtype=torch.float32, device=live[0].grad.device)
+            self.layout = [id(p) for p in live]
+        off = 0
+        views = []
+        for p in live:
+            n = p.numel()
+            v = self.flat[off:off + n]
+            v.copy_(p.grad.reshape(-1))
+            views.append((p, v))
+            off += n
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.flat.mul_(1.0 / self.world)
+        for p, v in views:
+            p.grad.copy_(v.view_as(p.grad))

@@ -17,7 +17,7 @@ import ctypes
 
 import torch
 
-from . import native
+from . import native, profiling
 from .graph import Adjacency
 
 _f = ctypes.c_float
@@ -56,6 +56,18 @@ def spmm_launch(adj: Adjacency, X: torch.Tensor, Y1=None, Y2=None, alpha=1.0, A1
     def ld(t):
         return t.stride(0) if t is not None else 0
 
+    with profiling.region("spmm", spmm_bytes(adj, d, sum(x is not None for x in (Y1, Y2, A1, A2)))):
+        _spmm_call(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld)
+
+
+def spmm_bytes(adj: Adjacency, d: int, n_rowio: int = 1) -> int:
+    """Algorithmic HBM bytes of one SpMM launch (no-reuse gather model):
+    rowptr 8(N+1) + col/val 8 nnz + gathered rows 4 d nnz + 4 d N per output written / addend read."""
+    n = adj.shape[0]
+    return 8 * (n + 1) + 8 * adj.nnz + 4 * d * adj.nnz + 4 * d * n * n_rowio
+
+
+def _spmm_call(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld):
     rc = native.lib().fr_spmm_csr(
         adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], ctypes.byref(plan),
         X.data_ptr(), ld(X), d,

@@ -11,7 +11,7 @@ import ctypes
 
 import torch
 
-from . import native
+from . import native, profiling
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -58,9 +58,10 @@ class FusedAdam(torch.optim.Optimizer):
                 M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in plist])
                 V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in plist])
                 N = (ctypes.c_int64 * n)(*[p.numel() for p in plist])
-                native.check(lib.fr_adam_step(
-                    P, G, M, V, N, n, max(p.numel() for p in plist), float(group["lr"]),
-                    float(beta1), float(beta2), float(group["eps"]),
-                    float(group["weight_decay"]), step, native.ptr(skip_flag),
-                    native.stream_of(plist[0])), "fr_adam_step")
+                with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
+                    native.check(lib.fr_adam_step(
+                        P, G, M, V, N, n, max(p.numel() for p in plist), float(group["lr"]),
+                        float(beta1), float(beta2), float(group["eps"]),
+                        float(group["weight_decay"]), step, native.ptr(skip_flag),
+                        native.stream_of(plist[0])), "fr_adam_step")
         return loss

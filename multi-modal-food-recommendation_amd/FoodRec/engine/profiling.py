@@ -1,0 +1,62 @@
+"""Per-launch kernel timing with HIP events (torch.cuda.Event on the launch stream).
+
+Every engine launch goes to torch's current stream, so events recorded there bracket exactly
+that kernel (plus its launch gap).  bench.py enables this over its timed steps to report the
+dominant kernel's average duration and algorithmic bytes per launch (roofline.achieved);
+when disabled the hooks cost one attribute check.
+"""
+from __future__ import annotations
+
+import contextlib
+from collections import defaultdict
+
+import torch
+
+_ACTIVE = None
+
+
+class KernelTimer:
+    def __init__(self):
+        self.records = []  # (name, start_event, end_event, algorithmic_bytes)
+
+    @contextlib.contextmanager
+    def region(self, name: str, nbytes: int):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        try:
+            yield
+        finally:
+            e.record()
+            self.records.append((name, s, e, int(nbytes)))
+
+    def summary(self) -> dict:
+        torch.cuda.synchronize()
+        agg = defaultdict(lambda: [0, 0.0, 0])
+        for name, s, e, b in self.records:
+            a = agg[name]
+            a[0] += 1
+            a[1] += s.elapsed_time(e)
+            a[2] += b
+        return {k: {"launches": n, "total_ms": t, "avg_ms": t / n, "bytes_per_launch": b / n,
+                    "gbps": (b / n) / (t / n * 1e-3) / 1e9 if t > 0 else 0.0}
+                for k, (n, t, b) in agg.items()}
+
+
+def active():
+    return _ACTIVE
+
+
+@contextlib.contextmanager
+def timing():
+    global _ACTIVE
+    prev, _ACTIVE = _ACTIVE, KernelTimer()
+    try:
+        yield _ACTIVE
+    finally:
+        _ACTIVE = prev
+
+
+def region(name: str, nbytes: int):
+    t = _ACTIVE
+    return t.region(name, nbytes) if t is not None else contextlib.nullcontext()

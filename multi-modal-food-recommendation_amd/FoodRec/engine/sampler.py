@@ -93,14 +93,17 @@ class TripleSampler:
         return torch.randperm(self.n, generator=g)
 
     def epoch(self):
-        """Yield (u, pos, neg) int64 device tensors per batch for one epoch."""
+        """Yield (u, pos, neg) int64 device tensors per batch for one epoch.  Negatives are drawn
+        per batch (same stream as the reference's per-sample draws, in permutation order)."""
         perm = self.epoch_order().numpy()
-        negs = self._negatives(self.users[perm])
         perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
-        negs_d = torch.from_numpy(negs).to(self.device, non_blocking=True)
+        pin = self.device.type == "cuda"
         for s in range(0, self.n, self.batch_size):
+            negs = torch.from_numpy(self._negatives(self.users[perm[s:s + self.batch_size]]))
+            if pin:
+                negs = negs.pin_memory()
             idx = perm_d[s:s + self.batch_size]
-            yield self._dev_users[idx], self._dev_items[idx], negs_d[s:s + self.batch_size]
+            yield self._dev_users[idx], self._dev_items[idx], negs.to(self.device, non_blocking=True)
 
 
 class BatchFeatures:

@@ -130,7 +130,9 @@ class HealthRec(GeneralRecommender):
         health_level = torch.cat([batch_data["pos_hl_mh"], batch_data["neg_hl_mh"]], dim=0)
         ingredients = torch.cat([pos_ingre, neg_ingre], dim=0)
         ingre_num = torch.cat([batch_data["pos_ingre_num"], batch_data["neg_ingre_num"]], dim=0)
-        ingr_emb = ingr_all[ingredients]
+        # the reference indexes ingr_all[ingredients] (grad reaches the pad row too); F.embedding
+        # has the same gradient but a segmented backward instead of a duplicate-serialised one
+        ingr_emb = F.embedding(ingredients, ingr_all)
         mask = ingredients == self.n_ingredients
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
@@ -148,7 +150,7 @@ class HealthRec(GeneralRecommender):
 
         mf_loss, emb3 = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                          user, pos_item, neg_item)
-        pos_e, neg_e = item_all[pos_item], item_all[neg_item]
+        pos_e, neg_e = F.embedding(pos_item, item_all), F.embedding(neg_item, item_all)
         kd = 1 - cosine_similarity(item_know, torch.cat([pos_e, neg_e], dim=0), dim=-1).mean()
         kd = torch.max(torch.tensor(0.0, device=kd.device), kd - self.kd_threshold)
 

@@ -60,6 +60,10 @@ def _read_negatives(path: str) -> list:
     return out
 
 
+def _as_lists(x) -> list:
+    return x.tolist() if isinstance(x, np.ndarray) else [list(r) for r in x]
+
+
 def _csr_sets(users: np.ndarray, items: np.ndarray, n_users: int):
     """per-user sorted unique item lists as (ptr [n_users+1], items)."""
     key = np.unique(users.astype(np.int64) * (np.int64(items.max(initial=0)) + 1) + items)
@@ -177,16 +181,13 @@ class FoodData:
         self.num_users = int(tr_all[:, 0].max()) + 1
         self.num_items = int(tr_all[:, 1].max()) + 1
         self.trainMatrix = _TrainMatrix(self.train_pairs, (self.num_users, self.num_items))
-        self.trainList, _ = _group_consecutive(tr_all)
+        self._tr_all, self._va_all, self._te_all = tr_all, va_all, te_all
         self.testRatings, _ = _group_consecutive(te_all)
-        self.testNegatives = [list(x) for x in a["test_neg"]]
+        self.testNegatives = _as_lists(a["test_neg"])
         self.validRatings, self.valid_users = _group_consecutive(va_all)
-        self.validNegatives = [list(x) for x in a["valid_neg"]]
+        self.validNegatives = _as_lists(a["valid_neg"])
         assert len(self.testRatings) == len(self.testNegatives)
         assert len(self.validRatings) == len(self.validNegatives)
-        self.validTestRatings = {u: set() for u in range(self.num_users)}
-        for u, i in np.concatenate([va_all, te_all]).tolist():
-            self.validTestRatings.setdefault(u, set()).add(i)
         train_items = set(tr_all[:, 1].tolist())
         vt_items = set(va_all[:, 1].tolist()) | set(te_all[:, 1].tolist())
         self.cold_list = list(vt_items - train_items)
@@ -199,8 +200,6 @@ class FoodData:
         self.test_data = te_all.copy()
         for d in (self.train_data, self.valid_data, self.test_data):
             d[:, 1] += nu_all
-        self.train_user_dict, self.valid_user_dict, self.test_user_dict = (
-            self._user_dict(x) for x in (self.train_data, self.valid_data, self.test_data))
 
         self.embImage = a["image"]
         self.image_size = self.embImage.shape[1]
@@ -250,6 +249,41 @@ class FoodData:
         vt = np.concatenate([va_all, te_all])
         vt = vt[vt[:, 0] < self.num_users]
         self.excl_vt_ptr, self.excl_vt_items = _csr_sets(vt[:, 0], vt[:, 1], self.num_users)
+
+    # --- per-user Python structures of the reference API, built on first use (the engine's
+    # sampler and evaluator use the array views instead)
+    @property
+    def trainList(self):
+        if "_trainList" not in self.__dict__:
+            self._trainList, _ = _group_consecutive(self._tr_all)
+        return self._trainList
+
+    @property
+    def validTestRatings(self):
+        if "_vtr" not in self.__dict__:
+            vtr = {u: set() for u in range(self.num_users)}
+            for u, i in np.concatenate([self._va_all, self._te_all]).tolist():
+                vtr.setdefault(u, set()).add(i)
+            self._vtr = vtr
+        return self._vtr
+
+    @property
+    def train_user_dict(self):
+        if "_tud" not in self.__dict__:
+            self._tud = self._user_dict(self.train_data)
+        return self._tud
+
+    @property
+    def valid_user_dict(self):
+        if "_vud" not in self.__dict__:
+            self._vud = self._user_dict(self.valid_data)
+        return self._vud
+
+    @property
+    def test_user_dict(self):
+        if "_teud" not in self.__dict__:
+            self._teud = self._user_dict(self.test_data)
+        return self._teud
 
     @staticmethod
     def _user_dict(inter):

@@ -77,7 +77,9 @@ def _popularity(n_items: int, rng: np.random.Generator, s: float = 0.8) -> np.nd
     return p / p.sum()
 
 
-def make_synthetic(shape: str = "tiny", seed: int = 0, **overrides) -> SyntheticFood:
+def make_synthetic(shape: str = "tiny", seed: int = 0, negatives: bool = True, **overrides) -> SyntheticFood:
+    """``negatives=False`` skips the 500-per-user evaluation candidate lists (training-only
+    inputs, e.g. bench.py) — they are the slowest part to generate at Allrecipes shape."""
     cfg = dict(SHAPES[shape])
     cfg.update(overrides)
     rng = np.random.default_rng(seed)
@@ -133,36 +135,59 @@ def make_synthetic(shape: str = "tiny", seed: int = 0, **overrides) -> Synthetic
     neg = cfg["neg"]
     tr_ptr = np.concatenate([[0], np.cumsum(np.bincount(train[:, 0], minlength=U))])
 
-    def _negatives(user_ids):
+    train_keys = np.unique(train[:, 0] * I + train[:, 1])
+
+    def _negatives(user_ids, chunk=4096):
+        """neg distinct popularity^0.7 draws per user excluding its train items (vectorised)."""
         out = np.empty((len(user_ids), neg), np.int64)
-        for row, u in enumerate(user_ids):
-            own = set(train[tr_ptr[u]:tr_ptr[u + 1], 1].tolist())
-            cand = [c for c in rng.choice(I, size=3 * neg, p=p07).tolist() if c not in own]
-            cand = list(dict.fromkeys(cand))
-            while len(cand) < neg:
-                extra = [c for c in rng.choice(I, size=neg, p=p07).tolist() if c not in own]
-                cand = list(dict.fromkeys(cand + extra))
-            out[row] = cand[:neg]
+        for c0 in range(0, len(user_ids), chunk):
+            uu = np.asarray(user_ids[c0:c0 + chunk], np.int64)
+            cand = rng.choice(I, size=(len(uu), 3 * neg), p=p07)
+            key = uu[:, None] * I + cand
+            pos = np.searchsorted(train_keys, key)
+            excl = train_keys[np.minimum(pos, len(train_keys) - 1)] == key
+            order = np.argsort(cand, axis=1, kind="stable")
+            srt = np.take_along_axis(cand, order, 1)
+            dup_s = np.zeros_like(srt, dtype=bool)
+            dup_s[:, 1:] = srt[:, 1:] == srt[:, :-1]
+            dup = np.empty_like(dup_s)
+            np.put_along_axis(dup, order, dup_s, 1)
+            ok = ~excl & ~dup
+            rank = np.cumsum(ok, axis=1)
+            full = rank[:, -1] >= neg
+            sel = ok & (rank <= neg)
+            out_rows = np.where(full)[0]
+            out[c0 + out_rows] = cand[out_rows][sel[out_rows]].reshape(len(out_rows), neg)
+            for r in np.where(~full)[0]:  # rare: too few distinct candidates, top up one by one
+                u = int(uu[r])
+                own = set(train[tr_ptr[u]:tr_ptr[u + 1], 1].tolist())
+                got = list(dict.fromkeys(c for c in cand[r].tolist() if c not in own))
+                while len(got) < neg:
+                    c = int(rng.integers(I))
+                    if c not in own and c not in got:
+                        got.append(c)
+                out[c0 + r] = got[:neg]
         return out
 
-    valid_neg = _negatives(valid_users)
-    test_neg = _negatives(np.arange(U))
+    if negatives:
+        valid_neg = _negatives(valid_users)
+        test_neg = _negatives(np.arange(U))
+    else:
+        valid_neg = np.zeros((len(valid_users), 0), np.int64)
+        test_neg = np.zeros((U, 0), np.int64)
 
     # ingredients: 1..20 distinct per item, padded with NI (notebook cell 6)
     k = rng.integers(1, 21, size=I)
     k[rng.integers(I)] = 19  # guarantee at least one padded row -> max code == NI
     code = np.full((I, 20), NI, np.int64)
-    raw = np.argsort(rng.random((I, NI)), axis=1)[:, :20] if NI <= 4096 else \
-        np.stack([rng.choice(NI, 20, replace=False) for _ in range(I)])
+    raw = _distinct_rows(rng, I, NI, 20)
     mask = np.arange(20)[None, :] < k[:, None]
     code[mask] = raw[mask]
     image = rng.standard_normal((I, cfg["img"]))
     text = rng.standard_normal((I, cfg["txt"]))
     ne = min(6, C)
-    img_c = np.argsort(rng.random((I, C)), axis=1)[:, :ne] if C <= 256 else \
-        np.stack([rng.choice(C, ne, replace=False) for _ in range(I)])
-    txt_c = np.argsort(rng.random((I, C)), axis=1)[:, :ne] if C <= 256 else \
-        np.stack([rng.choice(C, ne, replace=False) for _ in range(I)])
+    img_c = _distinct_rows(rng, I, C, ne)
+    txt_c = _distinct_rows(rng, I, C, ne)
     item_ids = np.repeat(np.arange(I, dtype=np.int64), ne)
     image_cluster = np.stack([item_ids, img_c.reshape(-1)], 1)
     text_cluster = np.stack([item_ids, txt_c.reshape(-1)], 1)
@@ -170,6 +195,29 @@ def make_synthetic(shape: str = "tiny", seed: int = 0, **overrides) -> Synthetic
     return SyntheticFood(shape, U, I, NI, C, train, valid, test, valid_users.astype(np.int64),
                          valid_neg, test_neg, code, k.astype(np.int64), image, text,
                          image_cluster, text_cluster, health)
+
+
+def _distinct_rows(rng, rows: int, n: int, k: int) -> np.ndarray:
+    """[rows, k] int64, each row k distinct values of [0, n) in random order (vectorised)."""
+    if n <= 256:
+        return np.argsort(rng.random((rows, n)), axis=1)[:, :k].astype(np.int64)
+    m = 2 * k + 8
+    out = np.empty((rows, k), np.int64)
+    cand = rng.integers(0, n, size=(rows, m))
+    order = np.argsort(cand, axis=1, kind="stable")
+    srt = np.take_along_axis(cand, order, 1)
+    dup_s = np.zeros_like(srt, dtype=bool)
+    dup_s[:, 1:] = srt[:, 1:] == srt[:, :-1]
+    dup = np.empty_like(dup_s)
+    np.put_along_axis(dup, order, dup_s, 1)
+    ok = ~dup
+    rank = np.cumsum(ok, axis=1)
+    full = rank[:, -1] >= k
+    rows_ok = np.where(full)[0]
+    out[rows_ok] = cand[rows_ok][(ok & (rank <= k))[rows_ok]].reshape(len(rows_ok), k)
+    for r in np.where(~full)[0]:
+        out[r] = rng.choice(n, k, replace=False)
+    return out
 
 
 def _dedupe_sorted(pairs: np.ndarray, n_items: int) -> np.ndarray:

@@ -1,0 +1,66 @@
+"""ORACLE (test infrastructure only): torch-CPU implementations of the engine ops.
+
+``installed()`` swaps FoodRec.engine.ops' functions for the oracle's CPU restatements (torch
+sparse COO SpMM, the reference's loss formulas), so an engine model can run its training step
+on the host.  Used ONLY by bench.py's ``cpu_baseline`` leg (timed on the GPU box's host cores)
+and by CPU tests; the product never imports this module and never falls back to it.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from oracle import ops as O
+
+
+def _coo(adj):
+    t = adj.__dict__.get("_oracle_coo")
+    if t is None:
+        rows = torch.repeat_interleave(torch.arange(adj.shape[0]), (adj.rowptr[1:] - adj.rowptr[:-1]).cpu())
+        t = torch.sparse_coo_tensor(torch.stack([rows, adj.col.cpu().long()]), adj.val.cpu(), adj.shape).coalesce()
+        adj.__dict__["_oracle_coo"] = t
+    return t
+
+
+def spmm(adj, X):
+    return torch.sparse.mm(_coo(adj), X)
+
+
+def propagate_mean(adj, ego, n_layers):
+    if n_layers == 0:
+        return ego
+    return O.propagate_mean(_coo(adj), ego, n_layers)
+
+
+def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False):
+    u, p, n = U[user], I[pos], I[neg]
+    mf = O.bpr_loss((u * p).sum(1), (u * n).sum(1), gamma)
+    if Ue is None:
+        return mf, torch.zeros(1)
+    return mf, O.emb_loss(Ue[user], Ie[pos], Ie[neg])
+
+
+def dcor_loss(views, pairs):
+    return sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
+
+
+def infonce_loss(H, tau=0.5):
+    return O.cl_loss(H, tau)
+
+
+_PATCH = {"spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
+          "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
+
+
+@contextlib.contextmanager
+def installed():
+    from FoodRec.engine import ops
+    saved = {k: getattr(ops, k) for k in _PATCH}
+    for k, v in _PATCH.items():
+        setattr(ops, k, v)
+    try:
+        yield
+    finally:
+        for k, v in saved.items():
+            setattr(ops, k, v)

@@ -1,0 +1,179 @@
+"""CPU tests: host logic against the reference's goldens (no GPU, no compute kernels).
+
+Covers the dataset loader, config cascade, exact-RNG triple sampler (MT19937 stream + torch
+permutation), model init parity (state_dict bit-identical under seed 999), normalised
+adjacency construction (bit-identical to the reference's scipy build), evaluation metrics,
+and the C-ABI library exporting every symbol of include/fr_engine.h.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import golden, tiny_config, tiny_data, tiny_dir
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_dataset_digest_matches_goldens():
+    """The goldens were produced on make_synthetic('tiny', 0); a generator change must regenerate them."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gen_golden import dataset_digest
+    from FoodRec.utils.synthetic import make_synthetic
+    assert str(golden("model_LightGCN.npz")["digest"]) == dataset_digest(make_synthetic("tiny", 0))
+
+
+def test_library_exports_header_symbols():
+    from FoodRec.engine import native
+    header = open(os.path.join(ROOT, "include", "fr_engine.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(fr_\w+)\s*\(", header, re.M))
+    assert declared == set(native.EXPORTED_SYMBOLS)
+    lib = native.lib()
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.fr_version() >= 1
+
+
+def test_config_cascade_semantics():
+    from FoodRec.utils.configurator import Config
+    cfg = Config("CIKM_Model", "Allrecipes", {"learning_rate": 0.123, "use_gpu": False})
+    assert cfg["learning_rate"] == 0.123          # config_dict overrides files
+    assert cfg["train_batch_size"] == 512          # model yaml overrides overall.yaml (1024)
+    assert cfg["definitely_missing_key"] is None   # missing keys read as None
+    assert cfg["hyper_parameters"][-1] == "seed"   # seed appended
+    assert cfg["valid_metric_bigger"] is True
+    lg = Config("LightGCN", "x", {"use_gpu": False})
+    assert isinstance(lg["reg_weight"], float) and lg["reg_weight"] == 0.1   # '1e-01' is a float
+
+
+def test_dataset_matches_reference_structures():
+    g = golden("stream.npz")
+    data = tiny_data(tiny_config("LightGCN", False))
+    np.testing.assert_array_equal(data.train_pairs[:, 0], g["pos_list_order_u"])
+    np.testing.assert_array_equal(data.train_pairs[:, 1], g["pos_list_order_i"])
+    assert data.num_items == int(g["num_items"])
+    assert len(data.trainList) == data.num_users
+    assert all(isinstance(x, int) for x in data.testNegatives[0])
+
+
+def test_sampler_stream_bit_exact():
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("stream.npz")
+    cfg = tiny_config("LightGCN", False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    get_model("LightGCN")(cfg, data)          # consumes torch's RNG like quick_start
+    s = TripleSampler(data, int(g["batch_size"]))
+    np.testing.assert_array_equal(s.neg_list_post, g["neg_list_post"])
+    for ep in range(2):
+        u, p, n = (np.concatenate(x) for x in zip(*[(a.numpy(), b.numpy(), c.numpy()) for a, b, c in s.epoch()]))
+        np.testing.assert_array_equal(u, g[f"ep{ep}/u"])
+        np.testing.assert_array_equal(p, g[f"ep{ep}/p"])
+        np.testing.assert_array_equal(n, g[f"ep{ep}/n"])
+
+
+def test_randint_stream_equals_numpy():
+    from FoodRec.engine.sampler import draw_negatives
+    import ctypes
+    from FoodRec.engine import native
+    for high in (1, 2, 7, 90, 45630, 2 ** 31 + 11, 2 ** 40 + 3):
+        np.random.seed(high % 1000)
+        ref = [np.random.randint(high) for _ in range(500)]
+        np.random.seed(high % 1000)
+        st = np.random.get_state()
+        key = np.array(st[1], np.uint32)
+        pos = np.array([st[2]], np.int32)
+        out = np.empty(500, np.int64)
+        native.check(native.lib().fr_sampler_randint(key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                      pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                      high, 500, out.ctypes.data), "randint")
+        np.testing.assert_array_equal(out, ref)
+        np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
+        assert np.random.randint(1 << 30) == (lambda: (np.random.seed(high % 1000), [np.random.randint(high) for _ in range(500)], np.random.randint(1 << 30))[2])()
+
+
+@pytest.mark.parametrize("name", ["LightGCN", "BPRMF", "CIKM_Model", "PRICAI_ModelX"])
+def test_model_init_and_adjacency_bit_exact(name):
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden(f"model_{name}.npz")
+    cfg = tiny_config(name, False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    m = get_model(name)(cfg, data)
+    sd = m.state_dict()
+    assert sorted(sd) == sorted(k[3:] for k in g.files if k.startswith("sd/"))
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), g["sd/" + k], err_msg=k)
+    for attr in ("norm_adj_matrix", "ri_norm_adj", "image_norm_adj", "text_norm_adj", "ingre_norm_adj"):
+        if f"adj/{attr}/values" not in g.files:
+            continue
+        A = getattr(m, attr)
+        rows = np.repeat(np.arange(A.shape[0]), np.diff(A.rowptr.numpy()))
+        idx = g[f"adj/{attr}/indices"]
+        np.testing.assert_array_equal(rows, idx[0])
+        np.testing.assert_array_equal(A.col.numpy(), idx[1])
+        np.testing.assert_array_equal(A.val.numpy(), g[f"adj/{attr}/values"])
+        assert tuple(A.shape) == tuple(g[f"adj/{attr}/shape"])
+
+
+def test_metrics_match_reference():
+    from FoodRec.common.trainer import get_auc_fast, metrics_by_user
+    g = golden("metrics.npz")
+    for k in range(20):
+        pred, npos = g[f"u{k}/pred"], int(g[f"u{k}/npos"])
+        order = np.argsort(pred)[::-1]
+        for j, topk in enumerate((10, 20)):
+            r, nd = metrics_by_user(order[:topk], range(npos))
+            assert r == g[f"u{k}/recall"][j] and nd == g[f"u{k}/ndcg"][j]
+        assert get_auc_fast(range(npos), pred, 30) == g[f"u{k}/auc"]
+
+
+def test_oracle_pinned_against_reference_ops():
+    """The oracle's restatements reproduce the reference's own op outputs (ops.npz)."""
+    from oracle import ops as O
+    g = golden("ops.npz")
+    x = torch.tensor(g["dcor/x"], requires_grad=True)
+    y = torch.tensor(g["dcor/y"], requires_grad=True)
+    d = O.correlation_distance(x, y)
+    d.sum().backward()
+    np.testing.assert_allclose(d.detach().numpy(), g["dcor/out"], rtol=1e-6)
+    np.testing.assert_allclose(x.grad.numpy(), g["dcor/gx"], rtol=1e-5, atol=1e-7)
+    h = torch.tensor(g["cl/h"], requires_grad=True)
+    c = O.cl_loss(h)
+    c.backward()
+    np.testing.assert_allclose(c.detach().numpy(), g["cl/out"], rtol=1e-6)
+    np.testing.assert_allclose(h.grad.numpy(), g["cl/gh"], rtol=1e-5, atol=1e-8)
+    b = O.bpr_loss(torch.tensor(g["bpr/pos"]), torch.tensor(g["bpr/neg"]))
+    np.testing.assert_allclose(b.numpy(), g["bpr/out"], rtol=1e-7)
+    e = O.emb_loss(*(torch.tensor(g[f"emb/e{i}"]) for i in range(3)))
+    np.testing.assert_allclose(e.numpy(), g["emb/out"], rtol=1e-7)
+    A = golden("model_LightGCN.npz")
+    idx, val = A["adj/norm_adj_matrix/indices"], A["adj/norm_adj_matrix/values"]
+    n = int(A["adj/norm_adj_matrix/shape"][0])
+    upper = idx[0] < idx[1]
+    r, c, v = O.norm_adj_coo(n, idx[0][upper], idx[1][upper])
+    np.testing.assert_array_equal(r, idx[0])
+    np.testing.assert_array_equal(c, idx[1])
+    np.testing.assert_array_equal(v, val)
+
+
+def test_engine_refuses_cpu_tensors():
+    from FoodRec.engine import native, ops
+    with pytest.raises(native.EngineError):
+        ops.bpr_emb_loss(torch.randn(4, 8), torch.randn(4, 8), None, None,
+                         torch.zeros(2, dtype=torch.long), torch.zeros(2, dtype=torch.long),
+                         torch.zeros(2, dtype=torch.long))
+
+
+def test_safe_unpickler_refuses_code():
+    import pickle
+    from FoodRec.utils.dataset import safe_pickle_load
+    path = os.path.join(tiny_dir(), "evil.pkl")
+    with open(path, "wb") as f:
+        pickle.dump(os.getcwd, f)   # a callable: must not be reconstructed
+    with pytest.raises(pickle.UnpicklingError):
+        safe_pickle_load(path)
