@@ -47,6 +47,8 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
+    ap.add_argument("--no-spmm-10m", action="store_true",
+                    help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
     return ap.parse_args()
 
 
@@ -131,13 +133,14 @@ def main():
     value = triples / elapsed
 
     dom_name = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
+    traffic = args.traffic if args.traffic is not None else pmc_traffic(dom_name)
     roofline = None
     if dom_name is not None:
         d = kern[dom_name]
         achieved = d["gbps"]
         roofline = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": args.traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
+                    "traffic": traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
                     "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / args.steps,
                     "share_of_step": round(d["total_ms"] / (elapsed * 1e3), 3)}
     spmm = None
@@ -149,6 +152,12 @@ def main():
                 "note": "Allrecipes-shape X tables (<=29 MB) are Infinity-Cache resident"}
     kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "per_step_ms": round(v["total_ms"] / args.steps, 4),
                    "gbps": round(v["gbps"], 1)} for k, v in kern.items()}
+
+    spmm10 = None
+    if rank == 0 and not args.no_spmm_10m:
+        del trainer, model, sampler, state
+        torch.cuda.empty_cache()
+        spmm10 = spmm_at_scale(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -163,10 +172,57 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else "single"},
-                "roofline": roofline, "spmm": spmm, "kernels": kernels, "cpu_baseline": cpu}
+                "roofline": roofline, "spmm": spmm, "spmm_10m": spmm10, "kernels": kernels,
+                "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, the
+    gfx950 calibration) in a separate profiling run, committed under profiles/ (newest round)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files or kernel is None:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f).get("per_region_bytes", {}).get(kernel)
+
+
+def spmm_at_scale(device, iters=10):
+    """fr_spmm_csr on the BASELINE config-4 graph (10M users x 1M items x ~200M edges, d=64 fp32):
+    the propagation kernel in its HBM-bound regime (the Allrecipes tables fit the Infinity Cache)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from synth_graph import synth_bipartite
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency, bipartite_norm_csr_torch
+    U, I = 10_000_000, 1_000_000
+    u, i = synth_bipartite(U, I, 20.0, seed=0, device=device)
+    rp, col, val = bipartite_norm_csr_torch(U, I, u, i)
+    del u, i
+    N = U + I
+    adj = Adjacency(rp, col, val, (N, N), device=device)
+    del rp, col, val
+    X = torch.randn(N, 64, device=device)
+    Y = torch.empty_like(X)
+    ops.spmm_launch(adj, X, Y1=Y)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        ops.spmm_launch(adj, X, Y1=Y)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    b = ops.spmm_bytes(adj, 64, 1)
+    out = {"graph": "synthetic U=10M I=1M E=%d (nnz=%d, N=%d)" % (adj.nnz // 2, adj.nnz, N),
+           "avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
+           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk}
+    del adj, X, Y
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(args):

@@ -24,7 +24,7 @@ import torch
 
 from . import native
 
-DEFAULT_CHUNK = 256
+DEFAULT_CHUNK = 1024
 
 
 def _sym_keys_np(n_nodes: int, rows: np.ndarray, cols: np.ndarray) -> np.ndarray:
@@ -63,6 +63,34 @@ def sym_norm_csr_torch(n_nodes: int, rows: torch.Tensor, cols: torch.Tensor):
     rowptr = torch.zeros(n + 1, dtype=torch.int64, device=r.device)
     torch.cumsum(cnt, 0, out=rowptr[1:])
     return rowptr, c.to(torch.int32), val
+
+
+def bipartite_norm_csr_torch(n_users: int, n_items: int, u: torch.Tensor, i: torch.Tensor):
+    """Symmetric-normalised (U+I)^2 adjacency of a bipartite edge list, built on the device
+    without symmetrising through a 2E-key sort: the user block comes from the (u,i)-sorted
+    unique keys, the item block from one (i,u) sort.  Same values as sym_norm_csr_torch on
+    (u, i+U): deg counts distinct neighbours, val = fp32(deg_r^-1/2 deg_c^-1/2) in float64."""
+    U, I = int(n_users), int(n_items)
+    key = torch.unique(u.to(torch.int64) * I + i.to(torch.int64), sorted=True)
+    uu = torch.div(key, I, rounding_mode="floor")
+    ii = key - uu * I
+    del key
+    deg_u = torch.bincount(uu, minlength=U)
+    deg_i = torch.bincount(ii, minlength=I)
+    dinv = torch.pow(torch.cat([deg_u, deg_i]).to(torch.float64) + 1e-7, -0.5)
+    order = torch.argsort(ii * U + uu)
+    iu_u = uu[order]
+    del order
+    col = torch.cat([(ii + U).to(torch.int32), iu_u.to(torch.int32)])
+    row_u = uu
+    val_u = (dinv[row_u] * dinv[ii + U]).to(torch.float32)
+    del row_u
+    ii_sorted = torch.repeat_interleave(torch.arange(I, device=u.device), deg_i)
+    val_i = (dinv[ii_sorted + U] * dinv[iu_u]).to(torch.float32)
+    val = torch.cat([val_u, val_i])
+    rowptr = torch.zeros(U + I + 1, dtype=torch.int64, device=u.device)
+    torch.cumsum(torch.cat([deg_u, deg_i]), 0, out=rowptr[1:])
+    return rowptr, col, val
 
 
 def ui_edges(inter_rows, inter_cols, n_users):
