@@ -168,6 +168,16 @@ int fr_adam_step(float* const* params, const float* const* grads,
                  double lr, double beta1, double beta2, double eps, double weight_decay,
                  int64_t step, const int32_t* d_skip, void* stream);
 
+/* Device-scalar variant (graph-capturable optimiser step): each tensor's step counter lives in
+ * device memory (int64, incremented by the call before use) and the learning rate is read from
+ * d_lr (device double; NULL -> lr), so a captured step replays with the current step and lr.
+ * d_steps is a HOST array of device pointers, one per tensor. */
+int fr_adam_step_dev(float* const* params, const float* const* grads,
+                     float* const* exp_avg, float* const* exp_avg_sq,
+                     int64_t* const* d_steps, const int64_t* numel, int n_tensors,
+                     const double* d_lr, double lr, double beta1, double beta2, double eps,
+                     double weight_decay, const int32_t* d_skip, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Negative sampler (host code): numpy legacy MT19937 stream, masked-rejection bounded ints,
  * exactly the draws np.random.randint(num_items) makes in TrainDataLoader.get_random_neg.

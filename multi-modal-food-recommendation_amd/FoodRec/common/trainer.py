@@ -59,6 +59,67 @@ def metrics_by_user(doc_list, rel_list):
     return hits / len(rel_list), dcg / idcg
 
 
+class GraphedStep:
+    """Trainer.train_step captured once in a HIP graph and replayed per batch.
+
+    The batch's (u, pos, neg) ids are copied into static device buffers; the graph holds the
+    whole step: side-feature gathers, forward (HIP SpMM chains, Transformer, heads), fused
+    BPR/EmbLoss, backward, and the fused Adam update (device-side step counters and lr).  The
+    first ``warmup`` calls run eagerly on a side stream (lazy workspaces, BLAS handles), the next
+    call captures and replays.  Batches of another size (the epoch's last) run eagerly.
+    """
+
+    def __init__(self, trainer, batch_size, warmup=3):
+        self.tr = trainer
+        self.B = int(batch_size)
+        self.warmup = max(1, int(warmup))
+        dev = torch.device(trainer.device)
+        self.u = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self.p = torch.zeros_like(self.u)
+        self.n = torch.zeros_like(self.u)
+        self.graph = None
+        self.calls = 0
+        self.static_loss = None
+        # private static state: the graph writes this step's loss vector and the cumulative NaN
+        # flag here; they are folded into the caller's epoch state after each replay
+        self.gstate = {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=dev)}
+
+    def _body(self, batch_idx, state, accumulate=True):
+        feats = self.tr._features()
+        return self.tr.train_step(feats.batch(self.u, self.p, self.n), batch_idx, state, accumulate=accumulate)
+
+    def __call__(self, u, p, n, batch_idx, state):
+        if u.numel() != self.B:
+            return self.tr.train_step(self.tr._features().batch(u, p, n), batch_idx, state)
+        self.u.copy_(u, non_blocking=True)
+        self.p.copy_(p, non_blocking=True)
+        self.n.copy_(n, non_blocking=True)
+        self.calls += 1
+        if self.graph is None and self.calls <= self.warmup:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                out = self._body(batch_idx, state)
+            torch.cuda.current_stream().wait_stream(side)
+            self.n_parts = state["acc"].numel()
+            return out
+        if self.graph is None:
+            self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
+            self.tr.optimizer.zero_grad()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.static_loss = self._body(batch_idx, self.gstate, accumulate=False)
+            self.graph = g
+        self.gstate["nan"].copy_(state["nan"])
+        self.graph.replay()
+        state["nan"].copy_(self.gstate["nan"])
+        if state["acc"] is None:
+            state["acc"] = self.gstate["acc"].clone()
+        else:
+            state["acc"].add_(self.gstate["acc"])
+        return self.static_loss
+
+
 class AbstractTrainer:
     def __init__(self, config, model):
         self.config = config
@@ -110,6 +171,9 @@ class Trainer(AbstractTrainer):
         # optional callable(model) run between backward and the optimiser step (e.g. the
         # data-parallel gradient all-reduce of FoodRec.engine.dist)
         self.grad_hook = None
+        # capture the training step in a HIP graph (config key cuda_graph; GPU, single process)
+        self.use_graph = bool(config["cuda_graph"]) and self._on_gpu()
+        self._graphed = None
 
     def _on_gpu(self) -> bool:
         return torch.device(self.device).type == "cuda"
@@ -143,10 +207,10 @@ class Trainer(AbstractTrainer):
         else:
             self.optimizer.step()
 
-    def train_step(self, interaction, batch_idx, state, loss_func=None):
+    def train_step(self, interaction, batch_idx, state, loss_func=None, accumulate=True):
         """One optimisation step on one batch (the body of the reference's step loop,
         trainer.py:177-227), with no host synchronisation.  ``state`` carries the device-side
-        loss accumulator and NaN flag across steps."""
+        loss accumulator and NaN flag across steps (``accumulate=False``: overwrite, for capture)."""
         loss_func = loss_func or self.model.calculate_loss
         self.optimizer.zero_grad()
         second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
@@ -154,7 +218,12 @@ class Trainer(AbstractTrainer):
         parts = losses if isinstance(losses, tuple) else (losses,)
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
-        state["acc"] = vec if state.get("acc") is None else state["acc"] + vec
+        if state.get("acc") is None:
+            state["acc"] = vec.clone()
+        elif accumulate:
+            state["acc"].add_(vec)
+        else:
+            state["acc"].copy_(vec)
         nan_flag = state["nan"]
         nan_flag |= torch.isnan(loss.detach().reshape(-1)[0]).to(torch.int32)
         if second_inter is not None:
@@ -174,6 +243,10 @@ class Trainer(AbstractTrainer):
         self._opt_step(nan_flag)
         return loss.detach()
 
+    def graphed_step(self, batch_size: int, warmup: int = 3):
+        """A callable (u, p, n, batch_idx, state) running train_step through a captured HIP graph."""
+        return GraphedStep(self, batch_size, warmup)
+
     def new_step_state(self):
         return {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=torch.device(self.device))}
 
@@ -186,8 +259,15 @@ class Trainer(AbstractTrainer):
         feats = self._features()
         state = self.new_step_state()
         loss_batches = []
-        for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
-            loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
+        if self.use_graph and loss_func is None and not self.mg:
+            if self._graphed is None:
+                self._graphed = self.graphed_step(train_data.batch_size, int(self.config["cuda_graph_warmup"] or 3))
+            step = self._graphed
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
+                loss_batches.append(step(u, p, n, batch_idx, state))
+        else:
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
+                loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
         if state["acc"] is None:
             return 0.0, loss_batches, None
         if int(state["nan"].item()):
@@ -276,6 +356,8 @@ class Trainer(AbstractTrainer):
             for group in self.optimizer.param_groups:
                 self.logger.info("======lr: %f" % group["lr"])
             self.lr_scheduler.step()
+            if isinstance(self.optimizer, FusedAdam):
+                self.optimizer.sync_lr()
             self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
             t1 = time()
             post = self.model.post_epoch_processing()

@@ -65,6 +65,9 @@ _SIGS = {
     "fr_adam_step": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                              POINTER(c_int64), c_int, c_int64, c_double, c_double, c_double, c_double,
                              c_double, c_int64, c_void_p, c_void_p]),
+    "fr_adam_step_dev": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                                 POINTER(c_void_p), POINTER(c_int64), c_int, c_void_p, c_double, c_double,
+                                 c_double, c_double, c_double, c_void_p, c_void_p]),
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),

@@ -59,4 +59,6 @@ def timing():
 
 def region(name: str, nbytes: int):
     t = _ACTIVE
-    return t.region(name, nbytes) if t is not None else contextlib.nullcontext()
+    if t is None or torch.cuda.is_current_stream_capturing():
+        return contextlib.nullcontext()
+    return t.region(name, nbytes)

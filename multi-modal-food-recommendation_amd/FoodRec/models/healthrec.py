@@ -152,7 +152,7 @@ class HealthRec(GeneralRecommender):
                                          user, pos_item, neg_item)
         pos_e, neg_e = F.embedding(pos_item, item_all), F.embedding(neg_item, item_all)
         kd = 1 - cosine_similarity(item_know, torch.cat([pos_e, neg_e], dim=0), dim=-1).mean()
-        kd = torch.max(torch.tensor(0.0, device=kd.device), kd - self.kd_threshold)
+        kd = self.norm_loss(kd, self.kd_threshold)
 
         B = user.shape[0]
         ing_p = F.embedding(pos_ingre, self.ingre_embedding.weight, padding_idx=self.n_ingredients)
@@ -169,7 +169,13 @@ class HealthRec(GeneralRecommender):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
 
     def norm_loss(self, kd_loss, threshold):
-        return torch.max(torch.tensor(0.0, device=kd_loss.device), kd_loss - threshold)
+        # torch.max(tensor(0.), kd - thr) (cikm_model.py:304-308) with a cached device zero, so the
+        # step issues no host->device scalar copy (graph-capturable)
+        zero = self.__dict__.get("_zero")
+        if zero is None or zero.device != kd_loss.device:
+            zero = torch.zeros((), dtype=kd_loss.dtype, device=kd_loss.device)
+            self.__dict__["_zero"] = zero
+        return torch.max(zero, kd_loss - threshold)
 
 
 # the reference's names

@@ -25,6 +25,7 @@ struct AdamArgs {
   const float* g[kMaxTensors];
   float* m[kMaxTensors];
   float* v[kMaxTensors];
+  int64_t* step[kMaxTensors];   // device step counters (device-scalar mode) or null
   int64_t numel[kMaxTensors];
   int32_t blk_start[kMaxTensors + 1];
   int32_t vec4[kMaxTensors];
@@ -32,6 +33,8 @@ struct AdamArgs {
 };
 
 struct AdamHyper {
+  double lr, beta1_d, beta2_d;  // device-scalar mode recomputes neg_step / bc2_sqrt from these
+  const double* d_lr;       // device lr (device-scalar mode) or null
   float w1;         // 1 - beta1
   float beta2;
   float one_m_b2;   // 1 - beta2
@@ -49,10 +52,27 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = __fadd_rn(p, __fdiv_rn(__fmul_rn(h.neg_step, m), denom));
 }
 
+// device-scalar mode: bump each tensor's step counter once per optimiser step
+__global__ void adam_step_inc_kernel(AdamArgs a, const int32_t* skip) {
+  if (skip && *skip) return;
+  const int t = threadIdx.x;
+  if (t < a.n && a.step[t]) a.step[t][0] += 1;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
   int t = 0;
   while (t + 1 < a.n && (int)blockIdx.x >= a.blk_start[t + 1]) ++t;
+  if (a.step[t]) {
+    // step-dependent scalars from device memory (graph-replayable); same double arithmetic as
+    // the host path / torch's Python scalars
+    const double st = (double)a.step[t][0];
+    const double lr = h.d_lr ? h.d_lr[0] : h.lr;
+    const double bc1 = 1.0 - pow(h.beta1_d, st);
+    const double bc2 = 1.0 - pow(h.beta2_d, st);
+    h.neg_step = (float)(-(lr / bc1));
+    h.bc2_sqrt = (float)sqrt(bc2);
+  }
   const int64_t base = (int64_t)(blockIdx.x - a.blk_start[t]) * kChunk;
   const int64_t end = min(base + (int64_t)kChunk, a.numel[t]);
   float* __restrict__ P = a.p[t];
@@ -83,20 +103,24 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
 
 }  // namespace
 
-extern "C" int fr_adam_step(float* const* params, const float* const* grads, float* const* exp_avg,
-                            float* const* exp_avg_sq, const int64_t* numel, int n_tensors,
-                            int64_t max_numel, double lr, double beta1, double beta2, double eps,
-                            double weight_decay, int64_t step, const int32_t* d_skip, void* stream) {
-  (void)max_numel;
+static int adam_impl(float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                     int n_tensors, double lr, const double* d_lr, double beta1, double beta2,
+                     double eps, double weight_decay, int64_t step, const int32_t* d_skip,
+                     void* stream) {
   FR_REQUIRE(n_tensors >= 0, "n_tensors < 0");
   if (n_tensors == 0) return FR_OK;
   FR_REQUIRE(params && grads && exp_avg && exp_avg_sq && numel, "null host array");
-  FR_REQUIRE(step >= 1, "step must be >= 1 (1-based, after increment)");
+  FR_REQUIRE(d_steps || step >= 1, "step must be >= 1 (1-based, after increment)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // bias corrections in double, as the Python scalars in torch.optim.Adam
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double bc1 = 1.0 - std::pow(beta1, (double)(d_steps ? 1 : step));
+  const double bc2 = 1.0 - std::pow(beta2, (double)(d_steps ? 1 : step));
   AdamHyper h;
+  h.lr = lr;
+  h.beta1_d = beta1;
+  h.beta2_d = beta2;
+  h.d_lr = d_lr;
   // hyper-parameters arrive as doubles (Python floats) and are rounded to f32 where torch's
   // tensor ops round them: lerp weight 1-b1, mul_ b2, addcmul value 1-b2, eps, step size
   h.w1 = (float)(1.0 - beta1);
@@ -119,6 +143,8 @@ extern "C" int fr_adam_step(float* const* params, const float* const* grads, flo
       a.g[k] = grads[t];
       a.m[k] = exp_avg[t];
       a.v[k] = exp_avg_sq[t];
+      a.step[k] = d_steps ? d_steps[t] : nullptr;
+      FR_REQUIRE(!d_steps || d_steps[t], "null step counter");
       a.numel[k] = numel[t];
       a.vec4[k] = fr::aligned16(params[t]) && fr::aligned16(grads[t]) && fr::aligned16(exp_avg[t]) &&
                   fr::aligned16(exp_avg_sq[t]);
@@ -129,8 +155,30 @@ extern "C" int fr_adam_step(float* const* params, const float* const* grads, flo
     }
     a.blk_start[a.n] = blocks;
     if (a.n == 0) continue;
+    if (d_steps) {
+      hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, s, a, d_skip);
+      FR_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, h, d_skip);
     FR_LAUNCH_CHECK();
   }
   return FR_OK;
+}
+
+extern "C" int fr_adam_step(float* const* params, const float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, const int64_t* numel, int n_tensors,
+                            int64_t max_numel, double lr, double beta1, double beta2, double eps,
+                            double weight_decay, int64_t step, const int32_t* d_skip, void* stream) {
+  (void)max_numel;
+  return adam_impl(params, grads, exp_avg, exp_avg_sq, nullptr, numel, n_tensors, lr, nullptr, beta1,
+                   beta2, eps, weight_decay, step, d_skip, stream);
+}
+
+extern "C" int fr_adam_step_dev(float* const* params, const float* const* grads, float* const* exp_avg,
+                                float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                                int n_tensors, const double* d_lr, double lr, double beta1, double beta2,
+                                double eps, double weight_decay, const int32_t* d_skip, void* stream) {
+  FR_REQUIRE(d_steps, "d_steps (device step counters) required");
+  return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1,
+                   beta2, eps, weight_decay, 0, d_skip, stream);
 }

@@ -84,3 +84,22 @@ def test_training_matches_reference(cuda, name):
     for keys, vals, got in ((g["valid_keys"], g["valid"], bvr), (g["test_keys"], g["test"], btr)):
         for k, v in zip(keys.tolist(), vals.tolist()):
             assert abs(got[k] - v) <= 1e-3, (name, k, got[k], v)
+
+
+@pytest.mark.parametrize("name", ["LightGCN", "PRICAI_ModelX"])
+def test_graphed_training_matches_reference(cuda, name):
+    """The HIP-graph-captured step (cuda_graph=True) trains exactly like the eager one."""
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden(f"train_{name}.npz")
+    cfg = tiny_config(name, True, cuda_graph=True, cuda_graph_warmup=1)
+    data = tiny_data(cfg)
+    init_seed(999)
+    model = get_model(name)(cfg, data).to(cfg["device"])
+    tr = Trainer(cfg, model)
+    bv, bvr, btr = tr.fit(data, hyper_tuple=(999,), saved=True, verbose=False)
+    assert tr._graphed is not None and tr._graphed.graph is not None, "graph was never captured"
+    trace = np.array([tr.train_loss_dict[e] for e in sorted(tr.train_loss_dict)])
+    np.testing.assert_allclose(trace, g["train_loss"], rtol=1e-4)
+    for k, v in zip(g["test_keys"].tolist(), g["test"].tolist()):
+        assert abs(btr[k] - v) <= 1e-3, (name, k, btr[k], v)
