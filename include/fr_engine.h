@@ -193,6 +193,18 @@ int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
 /* raw masked-rejection draws (test hook): out[i] = np.random.randint(high) for i < n */
 int fr_sampler_randint(uint32_t* mt_key, int32_t* mt_pos, int64_t high, int64_t n, int64_t* out);
 
+/* ---- embedding-table backward (row scatter-add) -------------------------------------------
+ * dW[r,:] = sum of G[i,:] over positions i with idx[i] == r, r != padding_idx (-1: none); every
+ * row of dW is written (zeros where untouched).  Replaces the backward of the reference's row
+ * gathers: ingr_all[ingredients] (FoodRec/models/cikm_model.py:230), ingre_embedding(...) with
+ * padding_idx (cikm_model.py:67-68, 270-271), image_/text_embedding (cikm_model.py:83-87).
+ * Deterministic (position-ordered sums inside fixed chunks, chunk partials in chunk order); no
+ * launch shape depends on device data (graph capturable).  n <= 2^18, d % 4 == 0. */
+int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d);
+int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                     int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
+                     void* d_workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,14 @@ def _rowmajor(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def _grad_like(t: torch.Tensor) -> torch.Tensor:
+    """Zero gradient buffer with exactly ``t``'s strides (kernels write grads with the input's ld)."""
+    if t.stride(0) == t.shape[1] or t.shape[0] <= 1:
+        return torch.zeros(t.shape, dtype=t.dtype, device=t.device)
+    n = (t.shape[0] - 1) * t.stride(0) + t.shape[1]
+    return torch.zeros(n, dtype=t.dtype, device=t.device).as_strided(t.shape, t.stride())
+
+
 def _ws_for(adj: Adjacency, d: int, device) -> torch.Tensor:
     cache = adj.__dict__.setdefault("_ws_cache", {})
     key = (d, str(device))
@@ -189,12 +197,12 @@ class _BprEmb(torch.autograd.Function):
         g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
         gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
         need = ctx.needs_input_grad
-        dU = torch.zeros_like(U) if need[0] else None
-        dI = torch.zeros_like(I) if need[1] else None
+        dU = _grad_like(U) if need[0] else None
+        dI = _grad_like(I) if need[1] else None
         dUe = dIe = None
         if Ue is not None:
-            dUe = dU if (ctx.same_u and dU is not None) else (torch.zeros_like(Ue) if need[2] else None)
-            dIe = dI if (ctx.same_i and dI is not None) else (torch.zeros_like(Ie) if need[3] else None)
+            dUe = dU if (ctx.same_u and dU is not None) else (_grad_like(Ue) if need[2] else None)
+            dIe = dI if (ctx.same_i and dI is not None) else (_grad_like(Ie) if need[3] else None)
         B, d = int(u.numel()), U.shape[1]
         ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
         native.check(native.lib().fr_bpr_bwd(
@@ -212,6 +220,52 @@ class _BprEmb(torch.autograd.Function):
 def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False):
     """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused."""
     return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic)
+
+
+# ----------------------------------------------------------------------------- embedding
+def embedding_bwd_bytes(n: int, rows: int, d: int) -> int:
+    """Algorithmic HBM bytes of one fr_embedding_bwd: ids + gradient rows read, dW written."""
+    return 8 * n + 4 * n * d + 4 * rows * d
+
+
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, weight, padding_idx):
+        native.require_device(weight, idx)
+        ctx.save_for_backward(idx)
+        ctx.rows, ctx.pad = weight.shape[0], padding_idx
+        return torch.nn.functional.embedding(idx, weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        d = g.shape[-1]
+        G = g.reshape(-1, d)
+        if G.dtype != torch.float32:
+            raise native.EngineError(f"engine ops compute in fp32 (got {G.dtype})")
+        if G.stride(1) != 1 or G.stride(0) % 4 or G.data_ptr() % 16:
+            G = G.contiguous()
+        ids = idx.reshape(-1)
+        if ids.dtype != torch.int64 or not ids.is_contiguous():
+            ids = ids.to(torch.int64).contiguous()
+        n, R = int(ids.numel()), int(ctx.rows)
+        dW = torch.empty(R, d, dtype=torch.float32, device=G.device)
+        lib = native.lib()
+        ws = native.workspace(lib.fr_embedding_bwd_workspace(n, R, d), G.device)
+        with profiling.region("embedding_bwd", embedding_bwd_bytes(n, R, d)):
+            native.check(lib.fr_embedding_bwd(ids.data_ptr(), n, G.data_ptr(), G.stride(0), d, R,
+                                              -1 if ctx.pad is None else int(ctx.pad), dW.data_ptr(), d,
+                                              ws.data_ptr(), ws.numel(), native.stream_of(G)),
+                         "fr_embedding_bwd")
+        return None, dW, None
+
+
+def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int | None = None) -> torch.Tensor:
+    """``F.embedding(idx, weight, padding_idx)`` whose weight gradient is the deterministic HIP
+    scatter-add ``fr_embedding_bwd`` (rows == padding_idx receive no gradient, as in torch)."""
+    if padding_idx is not None and padding_idx < 0:
+        padding_idx += weight.shape[0]
+    return _Embedding.apply(idx, weight, padding_idx)
 
 
 # ----------------------------------------------------------------------------- dCor

@@ -96,7 +96,7 @@ class CLUSSL(GeneralRecommender):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
         all_item = torch.cat([pos_item, neg_item], dim=0)
         user_all, item_all, (v_img, v_txt, v_ing) = self.forward()
-        views = [F.embedding(all_item, v) for v in (v_img, v_txt, v_ing)]
+        views = [ops.embedding(all_item, v) for v in (v_img, v_txt, v_ing)]
         mf_loss, emb = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                         user, pos_item, neg_item)
         if self.ssl_mode == "infonce":

@@ -130,17 +130,17 @@ class HealthRec(GeneralRecommender):
         health_level = torch.cat([batch_data["pos_hl_mh"], batch_data["neg_hl_mh"]], dim=0)
         ingredients = torch.cat([pos_ingre, neg_ingre], dim=0)
         ingre_num = torch.cat([batch_data["pos_ingre_num"], batch_data["neg_ingre_num"]], dim=0)
-        # the reference indexes ingr_all[ingredients] (grad reaches the pad row too); F.embedding
-        # has the same gradient but a segmented backward instead of a duplicate-serialised one
-        ingr_emb = F.embedding(ingredients, ingr_all)
+        # the reference indexes ingr_all[ingredients] (grad reaches the pad row too); the engine
+        # gather has the same gradient through the deterministic HIP scatter-add fr_embedding_bwd
+        ingr_emb = ops.embedding(ingredients, ingr_all)
         mask = ingredients == self.n_ingredients
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
         all_item = torch.cat([pos_item, neg_item], dim=0)
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        img_q = self.image_trs(self.image_embedding(all_item)).unsqueeze(1)
-        txt_q = self.text_trs(self.text_embedding(all_item)).unsqueeze(1)
+        img_q = self.image_trs(ops.embedding(all_item, self.image_embedding.weight)).unsqueeze(1)
+        txt_q = self.text_trs(ops.embedding(all_item, self.text_embedding.weight)).unsqueeze(1)
         mm_query = torch.cat([img_q, txt_q], dim=1)
         item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)
         item_mm, _ = self.ingre_target_atten(encoded, mm_query)
@@ -150,13 +150,14 @@ class HealthRec(GeneralRecommender):
 
         mf_loss, emb3 = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                          user, pos_item, neg_item)
-        pos_e, neg_e = F.embedding(pos_item, item_all), F.embedding(neg_item, item_all)
-        kd = 1 - cosine_similarity(item_know, torch.cat([pos_e, neg_e], dim=0), dim=-1).mean()
+        # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263) as one gather
+        kd = 1 - cosine_similarity(item_know, ops.embedding(all_item, item_all), dim=-1).mean()
         kd = self.norm_loss(kd, self.kd_threshold)
 
         B = user.shape[0]
-        ing_p = F.embedding(pos_ingre, self.ingre_embedding.weight, padding_idx=self.n_ingredients)
-        ing_n = F.embedding(neg_ingre, self.ingre_embedding.weight, padding_idx=self.n_ingredients)
+        # ingre_embedding(pos) / ingre_embedding(neg) (cikm_model.py:270-271) as one gather
+        ing_pn = ops.embedding(ingredients, self.ingre_embedding.weight, padding_idx=self.n_ingredients)
+        ing_p, ing_n = ing_pn[:B], ing_pn[B:]
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         reg = emb3 + (torch.norm(ing_p) + torch.norm(ing_n)) / B
         return mf_loss, self.loss_health * health_loss, self.loss_kd * kd, self.reg_weight * reg

@@ -1,0 +1,427 @@
+// Embedding-table backward (row gather -> row scatter-add) for gfx950.
+//
+//   dW[r, :] = sum over positions i with idx[i] == r (r != padding_idx) of G[i, :]
+//
+// The reference's gathers ``ingr_all[ingredients]`` (cikm_model.py:230), ``ingre_embedding(...)``
+// with padding_idx (cikm_model.py:67-68, 270-271) and the trainable feature tables
+// ``image_embedding``/``text_embedding`` (cikm_model.py:83-87) all back-propagate through this.
+// torch's sort/unique_by_key path costs ~10 launches per call; here:
+//
+//   1. histogram of rows + zero fill of the dense gradient (one grid-stride kernel; the wave's
+//      most frequent candidate row -- the padding row of ingredient lists -- is aggregated with a
+//      ballot so the hot counter sees one atomic per wave),
+//   2. exclusive scan of the counts (one block) -> bucket starts, per-row fill cursors,
+//   3. placement of positions into buckets,
+//   4. ordering of each bucket by position: <= 32 entries with an in-register bitonic network,
+//      larger buckets with an LDS bitmap over positions (popcount ranks; exact, no comparisons),
+//   5. segmented sum over the position-ordered slots in fixed chunks of kChunk slots: segments
+//      complete inside a chunk are written straight to dW, the (at most two) cut segments of a
+//      chunk go to partial slots,
+//   6. fix-up: each row cut by chunk boundaries is summed from its partials in chunk order.
+//
+// Every step is deterministic: the result depends only on (idx, G), never on scheduling.  No
+// step's launch shape depends on device data, so the whole chain captures into a HIP graph.
+#include "fr_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int kSmall = 32;    // buckets up to this size are ordered in registers by one thread
+constexpr int kChunk = 32;    // sorted slots per segmented-sum chunk
+constexpr int LPR = 16;       // lanes per group = one DPP row; each lane owns one float4 column
+constexpr int GPB = 256 / LPR;
+constexpr int64_t kMaxPositions = 1 << 18;  // LDS bitmap of step 4: n/32 words <= 32 KiB
+
+struct EmbWS {
+  int32_t* cursor;  // [R+1]: counts, then fill cursors; [R] = number of big buckets
+  int32_t* start;   // [R+1]: bucket starts, start[R] = number of valid positions
+  int32_t* sorted;  // [n]  : positions grouped by row, ascending inside a row
+  int32_t* big;     // [n/(kSmall+1)+1]: rows whose bucket exceeds kSmall
+  float4* pf;       // [nchunks*d4]: the chunk's first segment when it began in an earlier chunk
+  float4* pl;       // [nchunks*d4]: the chunk's last segment when it continues past the chunk
+};
+
+inline int64_t r256(int64_t b) { return (b + 255) / 256 * 256; }
+
+__host__ __device__ inline int64_t n_chunks(int64_t n) { return (n + kChunk - 1) / kChunk; }
+
+inline EmbWS emb_ws(void* base, int64_t n, int64_t R, int d) {
+  char* p = reinterpret_cast<char*>(base);
+  auto take = [&](int64_t bytes) { char* r = p; p += r256(bytes); return r; };
+  EmbWS w;
+  w.cursor = reinterpret_cast<int32_t*>(take((R + 1) * 4));
+  w.start = reinterpret_cast<int32_t*>(take((R + 1) * 4));
+  w.sorted = reinterpret_cast<int32_t*>(take(std::max<int64_t>(n, 1) * 4));
+  w.big = reinterpret_cast<int32_t*>(take((n / (kSmall + 1) + 1) * 4));
+  w.pf = reinterpret_cast<float4*>(take(n_chunks(n) * (d / 4) * 16));
+  w.pl = reinterpret_cast<float4*>(take(n_chunks(n) * (d / 4) * 16));
+  return w;
+}
+
+inline int64_t emb_ws_bytes(int64_t n, int64_t R, int d) {
+  return 2 * r256((R + 1) * 4) + r256(std::max<int64_t>(n, 1) * 4) + r256((n / (kSmall + 1) + 1) * 4) +
+         2 * r256(n_chunks(n) * (d / 4) * 16);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// row of position i, or -1 when i is out of range / the padding row / an invalid id
+__device__ __forceinline__ int emb_key(const int64_t* idx, int64_t i, int64_t n, int64_t R, int64_t pad) {
+  if (i >= n) return -1;
+  const int64_t r = idx[i];
+  return (r >= 0 && r < R && r != pad) ? (int)r : -1;
+}
+
+// 1. histogram + zero fill of dW
+__global__ __launch_bounds__(256) void emb_hist_zero_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                            int64_t R, int64_t pad, int32_t* __restrict__ cnt,
+                                                            float4* __restrict__ out, int64_t ldo4, int d4) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  // wave-uniform trip count (nth is a multiple of 64), so the ballots see every lane
+  for (int64_t i0 = tid - lane; i0 < n; i0 += nth) {
+    int key = emb_key(idx, i0 + lane, n, R, pad);
+    const int m = wave_max(key);
+    const uint64_t mask = __ballot(key == m && m >= 0);
+    const int c = __popcll(mask);
+    if (c > 1) {
+      if (lane == __ffsll((unsigned long long)mask) - 1) atomicAdd(&cnt[m], c);
+      if (key == m) key = -1;
+    }
+    if (key >= 0) atomicAdd(&cnt[key], 1);
+  }
+  const int64_t total4 = R * d4;
+  for (int64_t e = tid; e < total4; e += nth) {
+    const int64_t r = e / d4;
+    out[r * ldo4 + (e - r * d4)] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// block-wide exclusive scan of one int per thread (1024 threads); returns the exclusive prefix,
+// *total = block sum.  `sh` holds >= 16 ints.
+__device__ __forceinline__ int block_excl_scan_1024(int v, int* sh, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) sh[wid] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int w = 0; w < 16; ++w) { const int t = sh[w]; sh[w] = run; run += t; }
+    sh[16] = run;
+  }
+  __syncthreads();
+  const int res = sh[wid] + inc - v;
+  *total = sh[16];
+  __syncthreads();
+  return res;
+}
+
+// 2. scan counts -> start[], cursors; list big buckets
+__global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cursor, int64_t R,
+                                                        int32_t* __restrict__ start, int32_t* __restrict__ big) {
+  __shared__ int sh[17];
+  int carry = 0;
+  for (int64_t base = 0; base < R; base += 4096) {
+    const int64_t i0 = base + 4 * (int64_t)threadIdx.x;
+    int c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = (i0 + j < R) ? cursor[i0 + j] : 0;
+    int tot;
+    int off = carry + block_excl_scan_1024(c[0] + c[1] + c[2] + c[3], sh, &tot);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j < R) {
+        start[i0 + j] = off;
+        cursor[i0 + j] = off;
+        if (c[j] > kSmall) big[atomicAdd(&cursor[R], 1)] = (int)(i0 + j);
+      }
+      off += c[j];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) start[R] = carry;
+}
+
+// 3. placement (the wave's hot row takes one cursor atomic and ranks by lane)
+__global__ __launch_bounds__(256) void emb_place_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t R,
+                                                        int64_t pad, int32_t* __restrict__ cursor,
+                                                        int32_t* __restrict__ sorted) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = tid - lane; i0 < n; i0 += nth) {
+    const int64_t i = i0 + lane;
+    int key = emb_key(idx, i, n, R, pad);
+    const int m = wave_max(key);
+    const uint64_t mask = __ballot(key == m && m >= 0);
+    const int c = __popcll(mask);
+    if (c > 1) {
+      const int leader = __ffsll((unsigned long long)mask) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&cursor[m], c);
+      base = __shfl(base, leader, 64);
+      if (key == m) {
+        sorted[base + __popcll(mask & ((1ull << lane) - 1))] = (int)i;
+        key = -1;
+      }
+    }
+    if (key >= 0) sorted[atomicAdd(&cursor[key], 1)] = (int)i;
+  }
+}
+
+// 4a. small buckets: in-register bitonic network (fully unrolled, compile-time indices)
+__global__ __launch_bounds__(256) void emb_sort_small_kernel(const int32_t* __restrict__ start, int64_t R,
+                                                             int32_t* __restrict__ sorted) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
+    const int s = start[r], c = start[r + 1] - s;
+    if (c < 2 || c > kSmall) continue;
+    int v[kSmall];
+#pragma unroll
+    for (int j = 0; j < kSmall; ++j) v[j] = j < c ? sorted[s + j] : INT32_MAX;
+#pragma unroll
+    for (int k = 2; k <= kSmall; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+        for (int i = 0; i < kSmall; ++i) {
+          const int l = i ^ j;
+          if (l > i) {
+            const int a = v[i], b = v[l];
+            const bool up = (i & k) == 0;
+            if ((a > b) == up) { v[i] = b; v[l] = a; }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kSmall; ++j)
+      if (j < c) sorted[s + j] = v[j];
+  }
+}
+
+// 4b. big buckets: one block each; positions are distinct in [0, n), so an LDS bitmap over them
+//     plus popcount prefix sums yields the ascending order directly.
+__global__ __launch_bounds__(256) void emb_sort_big_kernel(const int32_t* __restrict__ cursor_tail, int64_t n,
+                                                           const int32_t* __restrict__ big,
+                                                           const int32_t* __restrict__ start,
+                                                           int32_t* __restrict__ sorted) {
+  extern __shared__ uint32_t bm[];
+  __shared__ int sh[5];
+  if ((int)blockIdx.x >= cursor_tail[0]) return;  // block-uniform
+  const int r = big[blockIdx.x];
+  const int s = start[r], e = start[r + 1];
+  const int words = (int)((n + 31) / 32);
+  for (int w = threadIdx.x; w < words; w += 256) bm[w] = 0u;
+  __syncthreads();
+  for (int k = s + threadIdx.x; k < e; k += 256) {
+    const int p = sorted[k];
+    atomicOr(&bm[p >> 5], 1u << (p & 31));
+  }
+  __syncthreads();
+  const int per = (words + 255) / 256;
+  const int w0 = threadIdx.x * per, w1 = min(words, w0 + per);
+  int local = 0;
+  for (int w = w0; w < w1; ++w) local += __popc(bm[w]);
+  // 256-thread exclusive scan (4 waves)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) sh[wid] = inc;
+  __syncthreads();
+  int off = inc - local;
+  for (int w = 0; w < wid; ++w) off += sh[w];
+  for (int w = w0; w < w1; ++w) {
+    uint32_t bits = bm[w];
+    while (bits) {
+      const int b = __ffs(bits) - 1;
+      sorted[s + off++] = w * 32 + b;
+      bits &= bits - 1u;
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ int row_bcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);  // row_newbcast:K
+}
+
+// 5. segmented sum over the position-ordered slots, one 16-lane group per (chunk, 64-column slice)
+__global__ __launch_bounds__(256) void emb_segsum_kernel(const int64_t* __restrict__ idx,
+                                                         const int32_t* __restrict__ sorted,
+                                                         const int32_t* __restrict__ start, int64_t R,
+                                                         int64_t nchunks, const float4* __restrict__ G4,
+                                                         int64_t ldg4, int d4, float4* __restrict__ out,
+                                                         int64_t ldo4, float4* __restrict__ pf,
+                                                         float4* __restrict__ pl) {
+  const int lig = threadIdx.x % LPR;
+  const int64_t c = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  const int q = blockIdx.y * LPR + lig;
+  const bool qok = q < d4;
+  const int total = start[R];
+  const int64_t k0 = c * kChunk;
+  if (c >= nchunks || k0 >= total) return;  // group-uniform
+  const int64_t k1 = min((int64_t)total, k0 + kChunk);
+  const int64_t cend = k0 + kChunk;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int cur = -1, cs = 0, ce = 0;
+  auto flush = [&]() {
+    if (!qok) return;
+    if (cs >= k0 && ce <= cend) out[(int64_t)cur * ldo4 + q] = acc;
+    else if (cs < k0) pf[c * d4 + q] = acc;
+    else pl[c * d4 + q] = acc;
+  };
+  for (int64_t kb = k0; kb < k1; kb += LPR) {
+    // each lane fetches one slot's (position, row, bucket bounds); DPP broadcasts them
+    const int64_t my = kb + lig;
+    const int p = my < k1 ? sorted[my] : -1;
+    const int r = p >= 0 ? (int)idx[p] : -1;
+    const int rs = r >= 0 ? start[r] : 0;
+    const int re = r >= 0 ? start[r + 1] : 0;
+    int rr[LPR], ss[LPR], ee[LPR];
+    float4 x[LPR];
+#define FR_EMB_BCAST(K)                                                                   \
+    {                                                                                     \
+      const int pk = row_bcast<K>(p);                                                     \
+      rr[K] = row_bcast<K>(r);                                                            \
+      ss[K] = row_bcast<K>(rs);                                                           \
+      ee[K] = row_bcast<K>(re);                                                           \
+      x[K] = (pk >= 0 && qok) ? G4[(int64_t)pk * ldg4 + q] : make_float4(0.f, 0.f, 0.f, 0.f); \
+    }
+    FR_EMB_BCAST(0) FR_EMB_BCAST(1) FR_EMB_BCAST(2) FR_EMB_BCAST(3)
+    FR_EMB_BCAST(4) FR_EMB_BCAST(5) FR_EMB_BCAST(6) FR_EMB_BCAST(7)
+    FR_EMB_BCAST(8) FR_EMB_BCAST(9) FR_EMB_BCAST(10) FR_EMB_BCAST(11)
+    FR_EMB_BCAST(12) FR_EMB_BCAST(13) FR_EMB_BCAST(14) FR_EMB_BCAST(15)
+#undef FR_EMB_BCAST
+#pragma unroll
+    for (int k = 0; k < LPR; ++k) {
+      if (rr[k] < 0) break;  // past the chunk's last slot (uniform across the group)
+      if (rr[k] != cur) {
+        if (cur >= 0) flush();
+        cur = rr[k]; cs = ss[k]; ce = ee[k];
+        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      acc = f4_add(acc, x[k]);
+    }
+  }
+  if (cur >= 0) flush();
+}
+
+// 6. rows cut by chunk boundaries: the block of the chunk where such a row begins sums its
+//    partials (first piece, then pf of every following chunk it covers) in a fixed order.
+__global__ __launch_bounds__(256) void emb_fixup_kernel(const int64_t* __restrict__ idx,
+                                                        const int32_t* __restrict__ sorted,
+                                                        const int32_t* __restrict__ start, int64_t R, int d4,
+                                                        float4* __restrict__ out, int64_t ldo4,
+                                                        const float4* __restrict__ pf,
+                                                        const float4* __restrict__ pl) {
+  __shared__ float4 red[GPB][LPR];
+  const int lig = threadIdx.x % LPR, g = threadIdx.x / LPR;
+  const int q = blockIdx.y * LPR + lig;
+  const bool qok = q < d4;
+  const int total = start[R];
+  const int64_t c = blockIdx.x;
+  const int64_t k0 = c * kChunk;
+  if (k0 >= total) return;  // block-uniform
+  const int64_t klast = min((int64_t)total, k0 + kChunk) - 1;
+  const int r = (int)idx[sorted[klast]];
+  const int64_t s = start[r], e = start[r + 1];
+  if (!(e > k0 + kChunk && s >= k0)) return;  // no row starts here and crosses the chunk end
+  const int64_t clast = (e - 1) / kChunk;
+  // pieces: j = 0 -> pl[c] (the row starts inside chunk c), j >= 1 -> pf[c + j]
+  const int64_t np = clast - c + 1;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (qok) {
+    for (int64_t j = g; j < np; j += GPB) {
+      const float4 v = j == 0 ? pl[c * d4 + q] : pf[(c + j) * d4 + q];
+      acc = f4_add(acc, v);
+    }
+  }
+  red[g][lig] = acc;
+  __syncthreads();
+  if (g == 0 && qok) {
+    float4 t = red[0][lig];
+#pragma unroll
+    for (int k = 1; k < GPB; ++k) t = f4_add(t, red[k][lig]);
+    out[(int64_t)r * ldo4 + q] = t;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d) {
+  if (n < 0 || num_rows < 0 || d <= 0) return 0;
+  return emb_ws_bytes(n, num_rows, d);
+}
+
+extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                                int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
+                                void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(n >= 0 && n <= kMaxPositions, "n out of range [0, 2^18]");
+  FR_REQUIRE(num_rows > 0 && num_rows < INT32_MAX, "num_rows out of range");
+  FR_REQUIRE(d > 0 && d % 4 == 0, "d must be a positive multiple of 4");
+  FR_REQUIRE(ldo >= d && ldo % 4 == 0 && d_out && fr::aligned16(d_out), "bad output table");
+  FR_REQUIRE(n == 0 || (d_idx && d_grad && ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad)),
+             "bad grad / index arguments");
+  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= emb_ws_bytes(n, num_rows, d),
+             "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int d4 = d / 4;
+  const int64_t R = num_rows;
+  EmbWS w = emb_ws(d_workspace, n, R, d);
+  FR_HIP_CHECK(hipMemsetAsync(w.cursor, 0, (R + 1) * 4, s));
+  {
+    const int64_t work = std::max<int64_t>(n, R * d4);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(work, 256), (int64_t)fr::kNumCU * 8));
+    hipLaunchKernelGGL(emb_hist_zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, n, R, padding_idx,
+                       w.cursor, reinterpret_cast<float4*>(d_out), ldo / 4, d4);
+    FR_LAUNCH_CHECK();
+  }
+  if (n == 0) return FR_OK;
+  hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, w.cursor, R, w.start, w.big);
+  FR_LAUNCH_CHECK();
+  {
+    const int64_t blocks = std::min<int64_t>(fr::ceil_div(n, 256), (int64_t)fr::kNumCU * 8);
+    hipLaunchKernelGGL(emb_place_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, n, R, padding_idx,
+                       w.cursor, w.sorted);
+    FR_LAUNCH_CHECK();
+  }
+  {
+    const int64_t blocks = std::min<int64_t>(fr::ceil_div(R, 256), (int64_t)fr::kNumCU * 8);
+    hipLaunchKernelGGL(emb_sort_small_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w.start, R, w.sorted);
+    FR_LAUNCH_CHECK();
+  }
+  {
+    const int64_t max_big = n / (kSmall + 1);
+    if (max_big > 0) {
+      const size_t lds = (size_t)fr::ceil_div(n, 32) * 4;
+      hipLaunchKernelGGL(emb_sort_big_kernel, dim3((unsigned)max_big), dim3(256), lds, s, w.cursor + R, n,
+                         w.big, w.start, w.sorted);
+      FR_LAUNCH_CHECK();
+    }
+  }
+  const int64_t nch = n_chunks(n);
+  const unsigned slices = (unsigned)fr::ceil_div(d4, LPR);
+  hipLaunchKernelGGL(emb_segsum_kernel, dim3((unsigned)fr::ceil_div(nch, GPB), slices), dim3(256), 0, s, d_idx,
+                     w.sorted, w.start, R, nch, reinterpret_cast<const float4*>(d_grad), ldg / 4, d4,
+                     reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(emb_fixup_kernel, dim3((unsigned)nch, slices), dim3(256), 0, s, d_idx, w.sorted, w.start, R,
+                     d4, reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}

@@ -11,6 +11,24 @@ import scipy.sparse as sp
 import torch
 
 
+# ----------------------------------------------------------------------------- row gathers
+def embedding_bwd_f64(idx, G, num_rows: int, padding_idx=None) -> np.ndarray:
+    """Weight gradient of a row gather ``W[idx]`` / ``nn.Embedding(idx)`` in float64.
+
+    Restates the autograd of ``ingr_all_embeddings[ingredients]`` (cikm_model.py:230; index
+    backward = index_put_ accumulate) and of ``self.ingre_embedding(...)`` with
+    ``padding_idx=self.n_ingredients`` (cikm_model.py:67-68, 270-271; embedding backward leaves the
+    padding row's gradient zero): dW[r] = sum_{i : idx[i] == r, r != padding_idx} G[i].
+    """
+    idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+    G = np.asarray(G, dtype=np.float64)
+    G = G.reshape(idx.shape[0], G.shape[-1])
+    keep = idx != (-1 if padding_idx is None else int(padding_idx))
+    out = np.zeros((num_rows, G.shape[1]), np.float64)
+    np.add.at(out, idx[keep], G[keep])
+    return out
+
+
 # ----------------------------------------------------------------------------- adjacency
 def norm_adj_coo(n_nodes: int, rows, cols):
     """D^-1/2 A D^-1/2 of the symmetrised binary graph.

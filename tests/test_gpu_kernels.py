@@ -222,3 +222,96 @@ def test_cpu_tensor_is_an_error():
     from FoodRec.engine import ops
     with pytest.raises(native.EngineError):
         ops.infonce_loss(torch.randn(8, 64), 0.5)
+
+
+# ----------------------------------------------------------------------------- embedding backward
+def _emb_case(kind, seed=0):
+    """(idx, n_rows, d, padding_idx) for the edge cases of the reference's row gathers."""
+    rng = np.random.default_rng(seed)
+    if kind == "ingredients":      # HealthRec: 1024 items x 20 codes, ~half padding (the hot row)
+        R, d = 20001, 64
+        ids = rng.integers(0, R - 1, (1024, 20))
+        ids[rng.random((1024, 20)) < 0.5] = R - 1
+        return ids, R, d, None
+    if kind == "ingredients_pad":  # same ids through ingre_embedding(padding_idx=n_ingredients)
+        ids, R, d, _ = _emb_case("ingredients", seed)
+        return ids, R, d, R - 1
+    if kind == "one_row":          # every position hits one row: one big bucket over all chunks
+        return np.full(5000, 7), 50, 64, None
+    if kind == "wide":             # image/text feature tables: 2B ids, d = 2048 (32 column slices)
+        return rng.integers(0, 3000, 1024), 3000, 2048, None
+    if kind == "ragged":           # d not a multiple of 64, n not a multiple of the chunk
+        return rng.integers(0, 40, 777), 40, 20, 3
+    if kind == "few_dups":         # buckets of 2..32 (register sort) and 33+ (bitmap sort)
+        base = np.repeat(np.arange(60), rng.integers(1, 70, 60))
+        return rng.permutation(base), 64, 32, None
+    if kind == "empty":
+        return np.zeros(0, np.int64), 10, 16, None
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind", ["ingredients", "ingredients_pad", "one_row", "wide", "ragged",
+                                  "few_dups", "empty"])
+def test_embedding_bwd_matches_fp64(cuda, kind):
+    """fr_embedding_bwd vs the fp64 restatement; tolerance: |err| <= 1e-5 * sum|G| per element
+    (fp32 chunked summation of up to n terms) + 1e-6; rows with no contribution exactly zero."""
+    from FoodRec.engine import ops
+    ids, R, d, pad = _emb_case(kind)
+    g = torch.Generator().manual_seed(1)
+    W = torch.randn(R, d, generator=g).to(cuda).requires_grad_(True)
+    idx = torch.as_tensor(ids, dtype=torch.int64, device=cuda)
+    G = torch.randn(*ids.shape, d, generator=g)
+    out = ops.embedding(idx, W, padding_idx=pad)
+    ref_fwd = W.detach()[idx]
+    assert torch.equal(out.detach(), ref_fwd)
+    out.backward(G.to(cuda))
+    got = W.grad.double().cpu().numpy()
+    ref = O.embedding_bwd_f64(ids, G.numpy(), R, pad)
+    scale = O.embedding_bwd_f64(ids, np.abs(G.numpy()), R, pad)
+    assert np.all(np.abs(got - ref) <= 1e-5 * scale + 1e-6)
+    untouched = scale.sum(1) == 0
+    assert np.all(got[untouched] == 0.0)
+
+
+def test_embedding_bwd_deterministic_and_matches_torch(cuda):
+    """Two launches are bit-identical; torch's own embedding backward agrees to fp32 rounding."""
+    from FoodRec.engine import ops
+    ids, R, d, pad = _emb_case("ingredients_pad", seed=3)
+    idx = torch.as_tensor(ids, device=cuda)
+    G = torch.randn(*ids.shape, d, device=cuda)
+    grads = []
+    for _ in range(2):
+        W = torch.zeros(R, d, device=cuda, requires_grad=True)
+        ops.embedding(idx, W, padding_idx=pad).backward(G)
+        grads.append(W.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    Wt = torch.zeros(R, d, device=cuda, requires_grad=True)
+    torch.nn.functional.embedding(idx, Wt, padding_idx=pad).backward(G)
+    torch.testing.assert_close(grads[0], Wt.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_embedding_bwd_in_graph(cuda):
+    """The whole fr_embedding_bwd chain captures into a HIP graph and replays with new ids."""
+    from FoodRec.engine import ops
+    R, d = 500, 64
+    idx = torch.zeros(3000, dtype=torch.int64, device=cuda)
+    G = torch.randn(3000, d, device=cuda)
+    W = torch.zeros(R, d, device=cuda, requires_grad=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.embedding(idx, W).backward(G)  # warm-up (allocator, library load)
+    torch.cuda.current_stream().wait_stream(s)
+    W.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.embedding(idx, W).backward(G)
+    rng = np.random.default_rng(5)
+    for trial in range(3):
+        ids = rng.integers(0, R if trial else 3, 3000)  # trial 0: three hot rows
+        idx.copy_(torch.as_tensor(ids))
+        graph.replay()
+        torch.cuda.synchronize()
+        ref = O.embedding_bwd_f64(ids, G.cpu().numpy(), R)
+        scale = O.embedding_bwd_f64(ids, np.abs(G.cpu().numpy()), R)
+        assert np.all(np.abs(W.grad.double().cpu().numpy() - ref) <= 1e-5 * scale + 1e-6)
