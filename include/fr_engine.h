@@ -204,6 +204,10 @@ int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d);
 int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
                      int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
                      void* d_workspace, int64_t workspace_bytes, void* stream);
+/* byte offset, inside the workspace, of the int32 status word of the last fr_embedding_bwd on it:
+ * 0 = consistent; non-zero bits name the step that met an out-of-range index on the device and
+ * skipped that access instead of faulting (1 scan, 2 place, 4/8 bucket order, 16 segsum, 32 fix-up) */
+int64_t fr_embedding_bwd_status_offset(int64_t num_rows);
 
 #ifdef __cplusplus
 }

@@ -257,7 +257,13 @@ class _Embedding(torch.autograd.Function):
                                               -1 if ctx.pad is None else int(ctx.pad), dW.data_ptr(), d,
                                               ws.data_ptr(), ws.numel(), native.stream_of(G)),
                          "fr_embedding_bwd")
+        if _EMB_STATUS is not None:
+            off = lib.fr_embedding_bwd_status_offset(R)
+            _EMB_STATUS.append(ws[off:off + 4].view(torch.int32))
         return None, dW, None
+
+
+_EMB_STATUS = None  # test hook: a list collecting each call's device status word (0 = consistent)
 
 
 def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int | None = None) -> torch.Tensor:

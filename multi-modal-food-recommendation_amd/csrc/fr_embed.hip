@@ -33,8 +33,12 @@ constexpr int LPR = 16;       // lanes per group = one DPP row; each lane owns o
 constexpr int GPB = 256 / LPR;
 constexpr int64_t kMaxPositions = 1 << 18;  // LDS bitmap of step 4: n/32 words <= 32 KiB
 
+// Status bits (cursor[R+1]): a step found device data inconsistent with the launch (an index out
+// of range) and skipped the access instead of faulting.  Zero after every well-formed call.
+enum : int { kBadScan = 1, kBadPlace = 2, kBadSmall = 4, kBadBig = 8, kBadSegsum = 16, kBadFixup = 32 };
+
 struct EmbWS {
-  int32_t* cursor;  // [R+1]: counts, then fill cursors; [R] = number of big buckets
+  int32_t* cursor;  // [R+2]: counts, then fill cursors; [R] = number of big buckets; [R+1] = status
   int32_t* start;   // [R+1]: bucket starts, start[R] = number of valid positions
   int32_t* sorted;  // [n]  : positions grouped by row, ascending inside a row
   int32_t* big;     // [n/(kSmall+1)+1]: rows whose bucket exceeds kSmall
@@ -50,7 +54,7 @@ inline EmbWS emb_ws(void* base, int64_t n, int64_t R, int d) {
   char* p = reinterpret_cast<char*>(base);
   auto take = [&](int64_t bytes) { char* r = p; p += r256(bytes); return r; };
   EmbWS w;
-  w.cursor = reinterpret_cast<int32_t*>(take((R + 1) * 4));
+  w.cursor = reinterpret_cast<int32_t*>(take((R + 2) * 4));
   w.start = reinterpret_cast<int32_t*>(take((R + 1) * 4));
   w.sorted = reinterpret_cast<int32_t*>(take(std::max<int64_t>(n, 1) * 4));
   w.big = reinterpret_cast<int32_t*>(take((n / (kSmall + 1) + 1) * 4));
@@ -60,7 +64,7 @@ inline EmbWS emb_ws(void* base, int64_t n, int64_t R, int d) {
 }
 
 inline int64_t emb_ws_bytes(int64_t n, int64_t R, int d) {
-  return 2 * r256((R + 1) * 4) + r256(std::max<int64_t>(n, 1) * 4) + r256((n / (kSmall + 1) + 1) * 4) +
+  return r256((R + 2) * 4) + r256((R + 1) * 4) + r256(std::max<int64_t>(n, 1) * 4) + r256((n / (kSmall + 1) + 1) * 4) +
          2 * r256(n_chunks(n) * (d / 4) * 16);
 }
 
@@ -75,6 +79,13 @@ __device__ __forceinline__ int emb_key(const int64_t* idx, int64_t i, int64_t n,
   if (i >= n) return -1;
   const int64_t r = idx[i];
   return (r >= 0 && r < R && r != pad) ? (int)r : -1;
+}
+
+// 0. zero the counters (a kernel, not hipMemsetAsync: a captured memset node is not relied on to
+//    be ordered before the histogram's atomics on graph replay)
+__global__ __launch_bounds__(256) void emb_clear_kernel(int32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0;
 }
 
 // 1. histogram + zero fill of dW
@@ -129,7 +140,8 @@ __device__ __forceinline__ int block_excl_scan_1024(int v, int* sh, int* total) 
 
 // 2. scan counts -> start[], cursors; list big buckets
 __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cursor, int64_t R,
-                                                        int32_t* __restrict__ start, int32_t* __restrict__ big) {
+                                                        int32_t* __restrict__ start, int32_t* __restrict__ big,
+                                                        int64_t big_cap) {
   __shared__ int sh[17];
   int carry = 0;
   for (int64_t base = 0; base < R; base += 4096) {
@@ -144,7 +156,11 @@ __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cu
       if (i0 + j < R) {
         start[i0 + j] = off;
         cursor[i0 + j] = off;
-        if (c[j] > kSmall) big[atomicAdd(&cursor[R], 1)] = (int)(i0 + j);
+        if (c[j] > kSmall) {
+          const int b = atomicAdd(&cursor[R], 1);
+          if (b < big_cap) big[b] = (int)(i0 + j);
+          else atomicOr(&cursor[R + 1], kBadScan);
+        }
       }
       off += c[j];
     }
@@ -172,20 +188,28 @@ __global__ __launch_bounds__(256) void emb_place_kernel(const int64_t* __restric
       if (lane == leader) base = atomicAdd(&cursor[m], c);
       base = __shfl(base, leader, 64);
       if (key == m) {
-        sorted[base + __popcll(mask & ((1ull << lane) - 1))] = (int)i;
+        const int slot = base + __popcll(mask & ((1ull << lane) - 1));
+        if (slot >= 0 && slot < n) sorted[slot] = (int)i;
+        else atomicOr(&cursor[R + 1], kBadPlace);
         key = -1;
       }
     }
-    if (key >= 0) sorted[atomicAdd(&cursor[key], 1)] = (int)i;
+    if (key >= 0) {
+      const int slot = atomicAdd(&cursor[key], 1);
+      if (slot >= 0 && slot < n) sorted[slot] = (int)i;
+      else atomicOr(&cursor[R + 1], kBadPlace);
+    }
   }
 }
 
 // 4a. small buckets: in-register bitonic network (fully unrolled, compile-time indices)
 __global__ __launch_bounds__(256) void emb_sort_small_kernel(const int32_t* __restrict__ start, int64_t R,
-                                                             int32_t* __restrict__ sorted) {
+                                                             int64_t n, int32_t* __restrict__ sorted,
+                                                             int32_t* __restrict__ status) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (int64_t)gridDim.x * blockDim.x) {
     const int s = start[r], c = start[r + 1] - s;
     if (c < 2 || c > kSmall) continue;
+    if (s < 0 || s + c > n) { atomicOr(status, kBadSmall); continue; }
     int v[kSmall];
 #pragma unroll
     for (int j = 0; j < kSmall; ++j) v[j] = j < c ? sorted[s + j] : INT32_MAX;
@@ -212,21 +236,24 @@ __global__ __launch_bounds__(256) void emb_sort_small_kernel(const int32_t* __re
 
 // 4b. big buckets: one block each; positions are distinct in [0, n), so an LDS bitmap over them
 //     plus popcount prefix sums yields the ascending order directly.
-__global__ __launch_bounds__(256) void emb_sort_big_kernel(const int32_t* __restrict__ cursor_tail, int64_t n,
-                                                           const int32_t* __restrict__ big,
+__global__ __launch_bounds__(256) void emb_sort_big_kernel(int32_t* __restrict__ cursor_tail, int64_t n,
+                                                           int64_t R, const int32_t* __restrict__ big,
                                                            const int32_t* __restrict__ start,
                                                            int32_t* __restrict__ sorted) {
   extern __shared__ uint32_t bm[];
   __shared__ int sh[5];
   if ((int)blockIdx.x >= cursor_tail[0]) return;  // block-uniform
   const int r = big[blockIdx.x];
+  if (r < 0 || r >= R) { if (threadIdx.x == 0) atomicOr(&cursor_tail[1], kBadBig); return; }
   const int s = start[r], e = start[r + 1];
+  if (s < 0 || e > n || s > e) { if (threadIdx.x == 0) atomicOr(&cursor_tail[1], kBadBig); return; }
   const int words = (int)((n + 31) / 32);
   for (int w = threadIdx.x; w < words; w += 256) bm[w] = 0u;
   __syncthreads();
   for (int k = s + threadIdx.x; k < e; k += 256) {
     const int p = sorted[k];
-    atomicOr(&bm[p >> 5], 1u << (p & 31));
+    if (p >= 0 && p < n) atomicOr(&bm[p >> 5], 1u << (p & 31));
+    else atomicOr(&cursor_tail[1], kBadBig);
   }
   __syncthreads();
   const int per = (words + 255) / 256;
@@ -249,7 +276,9 @@ __global__ __launch_bounds__(256) void emb_sort_big_kernel(const int32_t* __rest
     uint32_t bits = bm[w];
     while (bits) {
       const int b = __ffs(bits) - 1;
-      sorted[s + off++] = w * 32 + b;
+      if (s + off < e) sorted[s + off] = w * 32 + b;
+      else atomicOr(&cursor_tail[1], kBadBig);
+      ++off;
       bits &= bits - 1u;
     }
   }
@@ -267,12 +296,17 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(const int64_t* __restri
                                                          int64_t nchunks, const float4* __restrict__ G4,
                                                          int64_t ldg4, int d4, float4* __restrict__ out,
                                                          int64_t ldo4, float4* __restrict__ pf,
-                                                         float4* __restrict__ pl) {
+                                                         float4* __restrict__ pl, int64_t n,
+                                                         int32_t* __restrict__ status) {
   const int lig = threadIdx.x % LPR;
   const int64_t c = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
   const int q = blockIdx.y * LPR + lig;
   const bool qok = q < d4;
-  const int total = start[R];
+  int total = start[R];
+  if (total < 0 || total > n) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) atomicOr(status, kBadSegsum);
+    total = total < 0 ? 0 : (int)n;
+  }
   const int64_t k0 = c * kChunk;
   if (c >= nchunks || k0 >= total) return;  // group-uniform
   const int64_t k1 = min((int64_t)total, k0 + kChunk);
@@ -288,8 +322,10 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(const int64_t* __restri
   for (int64_t kb = k0; kb < k1; kb += LPR) {
     // each lane fetches one slot's (position, row, bucket bounds); DPP broadcasts them
     const int64_t my = kb + lig;
-    const int p = my < k1 ? sorted[my] : -1;
-    const int r = p >= 0 ? (int)idx[p] : -1;
+    int p = my < k1 ? sorted[my] : -1;
+    if (p >= n) { atomicOr(status, kBadSegsum); p = -1; }
+    int r = p >= 0 ? (int)idx[p] : -1;
+    if (r >= R) { atomicOr(status, kBadSegsum); r = -1; }
     const int rs = r >= 0 ? start[r] : 0;
     const int re = r >= 0 ? start[r + 1] : 0;
     int rr[LPR], ss[LPR], ee[LPR];
@@ -328,7 +364,8 @@ __global__ __launch_bounds__(256) void emb_fixup_kernel(const int64_t* __restric
                                                         const int32_t* __restrict__ start, int64_t R, int d4,
                                                         float4* __restrict__ out, int64_t ldo4,
                                                         const float4* __restrict__ pf,
-                                                        const float4* __restrict__ pl) {
+                                                        const float4* __restrict__ pl, int64_t n,
+                                                        int64_t nchunks, int32_t* __restrict__ status) {
   __shared__ float4 red[GPB][LPR];
   const int lig = threadIdx.x % LPR, g = threadIdx.x / LPR;
   const int q = blockIdx.y * LPR + lig;
@@ -336,12 +373,19 @@ __global__ __launch_bounds__(256) void emb_fixup_kernel(const int64_t* __restric
   const int total = start[R];
   const int64_t c = blockIdx.x;
   const int64_t k0 = c * kChunk;
+  if (total < 0 || total > n) {  // reported by segsum; nothing here is trustworthy
+    if (threadIdx.x == 0) atomicOr(status, kBadFixup);
+    return;
+  }
   if (k0 >= total) return;  // block-uniform
   const int64_t klast = min((int64_t)total, k0 + kChunk) - 1;
-  const int r = (int)idx[sorted[klast]];
+  const int p = sorted[klast];
+  const int r = (p >= 0 && p < n) ? (int)idx[p] : -1;
+  if (r < 0 || r >= R) { if (threadIdx.x == 0) atomicOr(status, kBadFixup); return; }
   const int64_t s = start[r], e = start[r + 1];
   if (!(e > k0 + kChunk && s >= k0)) return;  // no row starts here and crosses the chunk end
   const int64_t clast = (e - 1) / kChunk;
+  if (clast >= nchunks) { if (threadIdx.x == 0) atomicOr(status, kBadFixup); return; }
   // pieces: j = 0 -> pl[c] (the row starts inside chunk c), j >= 1 -> pf[c + j]
   const int64_t np = clast - c + 1;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -368,6 +412,8 @@ extern "C" int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d
   return emb_ws_bytes(n, num_rows, d);
 }
 
+extern "C" int64_t fr_embedding_bwd_status_offset(int64_t num_rows) { return (num_rows + 1) * 4; }
+
 extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
                                 int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
                                 void* d_workspace, int64_t workspace_bytes, void* stream) {
@@ -383,7 +429,9 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   const int d4 = d / 4;
   const int64_t R = num_rows;
   EmbWS w = emb_ws(d_workspace, n, R, d);
-  FR_HIP_CHECK(hipMemsetAsync(w.cursor, 0, (R + 1) * 4, s));
+  hipLaunchKernelGGL(emb_clear_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(R + 1, 256), 1024)), dim3(256), 0,
+                     s, w.cursor, R + 2);
+  FR_LAUNCH_CHECK();
   {
     const int64_t work = std::max<int64_t>(n, R * d4);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(work, 256), (int64_t)fr::kNumCU * 8));
@@ -392,7 +440,8 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
     FR_LAUNCH_CHECK();
   }
   if (n == 0) return FR_OK;
-  hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, w.cursor, R, w.start, w.big);
+  hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, w.cursor, R, w.start, w.big,
+                     n / (kSmall + 1) + 1);
   FR_LAUNCH_CHECK();
   {
     const int64_t blocks = std::min<int64_t>(fr::ceil_div(n, 256), (int64_t)fr::kNumCU * 8);
@@ -402,14 +451,15 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   }
   {
     const int64_t blocks = std::min<int64_t>(fr::ceil_div(R, 256), (int64_t)fr::kNumCU * 8);
-    hipLaunchKernelGGL(emb_sort_small_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w.start, R, w.sorted);
+    hipLaunchKernelGGL(emb_sort_small_kernel, dim3((unsigned)blocks), dim3(256), 0, s, w.start, R, n, w.sorted,
+                       w.cursor + R + 1);
     FR_LAUNCH_CHECK();
   }
   {
     const int64_t max_big = n / (kSmall + 1);
     if (max_big > 0) {
       const size_t lds = (size_t)fr::ceil_div(n, 32) * 4;
-      hipLaunchKernelGGL(emb_sort_big_kernel, dim3((unsigned)max_big), dim3(256), lds, s, w.cursor + R, n,
+      hipLaunchKernelGGL(emb_sort_big_kernel, dim3((unsigned)max_big), dim3(256), lds, s, w.cursor + R, n, R,
                          w.big, w.start, w.sorted);
       FR_LAUNCH_CHECK();
     }
@@ -418,10 +468,10 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   const unsigned slices = (unsigned)fr::ceil_div(d4, LPR);
   hipLaunchKernelGGL(emb_segsum_kernel, dim3((unsigned)fr::ceil_div(nch, GPB), slices), dim3(256), 0, s, d_idx,
                      w.sorted, w.start, R, nch, reinterpret_cast<const float4*>(d_grad), ldg / 4, d4,
-                     reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl);
+                     reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl, n, w.cursor + R + 1);
   FR_LAUNCH_CHECK();
   hipLaunchKernelGGL(emb_fixup_kernel, dim3((unsigned)nch, slices), dim3(256), 0, s, d_idx, w.sorted, w.start, R,
-                     d4, reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl);
+                     d4, reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl, n, nch, w.cursor + R + 1);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -49,7 +49,12 @@ def infonce_loss(H, tau=0.5):
     return O.cl_loss(H, tau)
 
 
-_PATCH = {"spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
+def embedding(idx, weight, padding_idx=None):
+    # ingr_all[ingredients] / nn.Embedding(padding_idx) (cikm_model.py:230, 270-271)
+    return torch.nn.functional.embedding(idx, weight, padding_idx=padding_idx)
+
+
+_PATCH = {"embedding": embedding, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
           "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
 
 

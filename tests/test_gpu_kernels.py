@@ -261,10 +261,15 @@ def test_embedding_bwd_matches_fp64(cuda, kind):
     W = torch.randn(R, d, generator=g).to(cuda).requires_grad_(True)
     idx = torch.as_tensor(ids, dtype=torch.int64, device=cuda)
     G = torch.randn(*ids.shape, d, generator=g)
-    out = ops.embedding(idx, W, padding_idx=pad)
-    ref_fwd = W.detach()[idx]
-    assert torch.equal(out.detach(), ref_fwd)
-    out.backward(G.to(cuda))
+    ops._EMB_STATUS = []
+    try:
+        out = ops.embedding(idx, W, padding_idx=pad)
+        ref_fwd = W.detach()[idx]
+        assert torch.equal(out.detach(), ref_fwd)
+        out.backward(G.to(cuda))
+        assert [int(t) for t in ops._EMB_STATUS] == [0]
+    finally:
+        ops._EMB_STATUS = None
     got = W.grad.double().cpu().numpy()
     ref = O.embedding_bwd_f64(ids, G.numpy(), R, pad)
     scale = O.embedding_bwd_f64(ids, np.abs(G.numpy()), R, pad)
@@ -304,14 +309,20 @@ def test_embedding_bwd_in_graph(cuda):
     torch.cuda.current_stream().wait_stream(s)
     W.grad = None
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        ops.embedding(idx, W).backward(G)
+    ops._EMB_STATUS = []
+    try:
+        with torch.cuda.graph(graph):
+            ops.embedding(idx, W).backward(G)
+        (status,) = ops._EMB_STATUS
+    finally:
+        ops._EMB_STATUS = None
     rng = np.random.default_rng(5)
     for trial in range(3):
         ids = rng.integers(0, R if trial else 3, 3000)  # trial 0: three hot rows
         idx.copy_(torch.as_tensor(ids))
         graph.replay()
         torch.cuda.synchronize()
+        assert int(status) == 0, f"replay {trial}: fr_embedding_bwd status {int(status)}"
         ref = O.embedding_bwd_f64(ids, G.cpu().numpy(), R)
         scale = O.embedding_bwd_f64(ids, np.abs(G.cpu().numpy()), R)
         assert np.all(np.abs(W.grad.double().cpu().numpy() - ref) <= 1e-5 * scale + 1e-6)
