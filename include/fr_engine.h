@@ -209,6 +209,17 @@ int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64
  * skipped that access instead of faulting (1 scan, 2 place, 4/8 bucket order, 16 segsum, 32 fix-up) */
 int64_t fr_embedding_bwd_status_offset(int64_t num_rows);
 
+/* ---- Linear weight/bias gradient over many rows ---------------------------------------------
+ * dW[n,k] = sum_m dY[m,n] X[m,k] (written with row stride ldw), db[n] = sum_m dY[m,n] (d_db may
+ * be null).  Replaces the weight-gradient GEMMs of the Linear layers of the reference's ingredient
+ * Transformer (FoodRec/models/cikm_model.py:33-35, nn.TransformerEncoderLayer over 2B x 20 tokens)
+ * and of image_trs / text_trs (cikm_model.py:240-241).  Split over row slabs, slab partials summed
+ * in fixed order (deterministic).  N, K multiples of 4; dY, X 16-byte aligned. */
+int64_t fr_linear_wgrad_workspace(int64_t M, int N, int K);
+int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x, int64_t ldx, int64_t M, int N, int K,
+                    float* d_dw, int64_t ldw, float* d_db, void* d_workspace, int64_t workspace_bytes,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,9 @@ _SIGS = {
     "fr_bpr_workspace": (c_int64, [c_int64]),
     "fr_embedding_bwd_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_bwd_status_offset": (c_int64, [c_int64]),
+    "fr_linear_wgrad_workspace": (c_int64, [c_int64, c_int, c_int]),
+    "fr_linear_wgrad": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_int64,
+                                c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_embedding_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p,
                                  c_int64, c_void_p, c_int64, c_void_p]),
     "fr_bpr_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,

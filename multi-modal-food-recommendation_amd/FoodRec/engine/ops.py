@@ -274,6 +274,68 @@ def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int | None =
     return _Embedding.apply(idx, weight, padding_idx)
 
 
+# ----------------------------------------------------------------------------- Linear
+LINEAR_MIN_ROWS = 1024  # below this the library GEMM's weight gradient is already short
+
+
+def _rows_operand(t: torch.Tensor, cols: int) -> torch.Tensor:
+    t2 = t.reshape(-1, cols)
+    if t2.stride(1) != 1 or t2.stride(0) % 4 or t2.data_ptr() % 16:
+        t2 = t2.contiguous()
+    return t2
+
+
+def linear_wgrad_bytes(M: int, N: int, K: int) -> int:
+    """Algorithmic bytes of fr_linear_wgrad: dY [M,N] and X [M,K] read once, dW + db written."""
+    return 4 * (M * N + M * K + N * K + N)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, W, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        N, K = W.shape
+        need = ctx.needs_input_grad
+        gy2 = _rows_operand(gy, N)
+        dx = dW = db = None
+        if need[0]:
+            dx = torch.mm(gy2, W).view(x.shape)
+        if need[1] or (ctx.has_b and need[2]):
+            x2 = _rows_operand(x, K)
+            M = gy2.shape[0]
+            dW = torch.empty(N, K, dtype=torch.float32, device=gy.device)
+            db = torch.empty(N, dtype=torch.float32, device=gy.device) if ctx.has_b else None
+            lib = native.lib()
+            ws = native.workspace(lib.fr_linear_wgrad_workspace(M, N, K), gy.device)
+            with profiling.region("linear_wgrad", linear_wgrad_bytes(M, N, K)):
+                native.check(lib.fr_linear_wgrad(gy2.data_ptr(), gy2.stride(0), x2.data_ptr(), x2.stride(0), M,
+                                                 N, K, dW.data_ptr(), K, native.ptr(db), ws.data_ptr(),
+                                                 ws.numel(), native.stream_of(gy2)), "fr_linear_wgrad")
+            if not need[1]:
+                dW = None
+            if not need[2]:
+                db = None
+        return dx, dW, db
+
+
+def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.linear(x, W, b)``; over >= LINEAR_MIN_ROWS rows of fp32 its weight/bias gradient is the
+    split-K HIP kernel ``fr_linear_wgrad`` (the input gradient stays a library GEMM)."""
+    N, K = W.shape
+    rows = x.numel() // max(K, 1)
+    if (rows < LINEAR_MIN_ROWS or N % 4 or K % 4 or x.dtype != torch.float32 or W.dtype != torch.float32
+            or not torch.is_grad_enabled() or not (W.requires_grad or (b is not None and b.requires_grad))):
+        return torch.nn.functional.linear(x, W, b)
+    native.require_device(x, W)
+    return _Linear.apply(x, W, b)
+
+
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod

@@ -23,7 +23,7 @@ from torch.nn.functional import cosine_similarity
 from FoodRec.common.abstract_recommender import GeneralRecommender
 from FoodRec.common.init import xavier_uniform_initialization
 from FoodRec.common.loss import BPRLoss, EmbLoss
-from FoodRec.engine import ops
+from FoodRec.engine import layers, ops
 from FoodRec.models._graphs import side_adjacency, ui_adjacency
 
 
@@ -78,7 +78,7 @@ class HealthRec(GeneralRecommender):
             else dataset.num_health_level
         d = config["embedding_size"]
         # module construction order == the reference's (seeded init parity)
-        self.encoder_layer = nn.TransformerEncoderLayer(d_model=d, nhead=config["num_attention_heads"],
+        self.encoder_layer = layers.TransformerEncoderLayer(d_model=d, nhead=config["num_attention_heads"],
                                                         dim_feedforward=4 * d,
                                                         dropout=config["attention_probs_dropout_prob"],
                                                         activation=config["hidden_act"])
@@ -139,8 +139,10 @@ class HealthRec(GeneralRecommender):
 
         all_item = torch.cat([pos_item, neg_item], dim=0)
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        img_q = self.image_trs(ops.embedding(all_item, self.image_embedding.weight)).unsqueeze(1)
-        txt_q = self.text_trs(ops.embedding(all_item, self.text_embedding.weight)).unsqueeze(1)
+        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight), self.image_trs.weight,
+                           self.image_trs.bias).unsqueeze(1)
+        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight), self.text_trs.weight,
+                           self.text_trs.bias).unsqueeze(1)
         mm_query = torch.cat([img_q, txt_q], dim=1)
         item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)
         item_mm, _ = self.ingre_target_atten(encoded, mm_query)

@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int kSmall = 32;    // buckets up to this size are ordered in registers by one thread
-constexpr int kChunk = 32;    // sorted slots per segmented-sum chunk
+constexpr int kChunk = 16;    // sorted slots per segmented-sum chunk (one 16-slot batch)
 constexpr int LPR = 16;       // lanes per group = one DPP row; each lane owns one float4 column
 constexpr int GPB = 256 / LPR;
 constexpr int64_t kMaxPositions = 1 << 18;  // LDS bitmap of step 4: n/32 words <= 32 KiB
@@ -138,21 +138,35 @@ __device__ __forceinline__ int block_excl_scan_1024(int v, int* sh, int* total) 
   return res;
 }
 
-// 2. scan counts -> start[], cursors; list big buckets
+// 2. scan counts -> start[], cursors; list big buckets.  One block; each thread owns kScanPer
+//    consecutive rows (vector loads), so a 45k-row table is two block-scan rounds.
+constexpr int kScanPer = 32;
+
 __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cursor, int64_t R,
                                                         int32_t* __restrict__ start, int32_t* __restrict__ big,
                                                         int64_t big_cap) {
   __shared__ int sh[17];
   int carry = 0;
-  for (int64_t base = 0; base < R; base += 4096) {
-    const int64_t i0 = base + 4 * (int64_t)threadIdx.x;
-    int c[4];
+  for (int64_t base = 0; base < R; base += 1024 * kScanPer) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kScanPer;
+    int c[kScanPer];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = (i0 + j < R) ? cursor[i0 + j] : 0;
+    for (int j = 0; j < kScanPer; j += 4) {
+      if (i0 + j + 3 < R) {
+        const int4 v = *reinterpret_cast<const int4*>(cursor + i0 + j);
+        c[j] = v.x; c[j + 1] = v.y; c[j + 2] = v.z; c[j + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) c[j + t] = (i0 + j + t < R) ? cursor[i0 + j + t] : 0;
+      }
+    }
+    int sum = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) sum += c[j];
     int tot;
-    int off = carry + block_excl_scan_1024(c[0] + c[1] + c[2] + c[3], sh, &tot);
+    int off = carry + block_excl_scan_1024(sum, sh, &tot);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < kScanPer; ++j) {
       if (i0 + j < R) {
         start[i0 + j] = off;
         cursor[i0 + j] = off;

@@ -1,0 +1,149 @@
+// Weight/bias gradient of a Linear layer over many rows (split-K over the rows), gfx950.
+//
+//   dW[n, k] = sum_m dY[m, n] * X[m, k]        (dW = dY^T X, [N x K])
+//   db[n]    = sum_m dY[m, n]
+//
+// The HealthRec ingredient Transformer (cikm_model.py:33-35: nn.TransformerEncoder, d=64, FF 4d)
+// runs its four Linear layers over M = 2B x 20 = 20480 tokens: the weight gradients are
+// [<=256 x 20480] x [20480 x <=256] -- tiny outputs, a huge reduction.  A library GEMM tiles the
+// output and walks all 20480 rows in one workgroup per tile (~100 us each); here the rows are split
+// into slabs, one workgroup per (slab, 64x64 output tile), each thread holding a 4x4 register tile
+// fed from LDS-staged 16-row sub-tiles (double-buffered in registers), fp32 FMA (exact f32, the rate
+// f32 MFMA would give).  Slab partials are summed in slab order by a second kernel: deterministic.
+#include "fr_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int TN = 64, TK = 64;  // output tile
+constexpr int SUB = 16;          // rows per LDS sub-tile
+constexpr int kSlab = 128;       // rows per slab (split-K unit)
+
+__device__ __forceinline__ float4 ld4_masked(const float* base, int64_t ld, int64_t m, int64_t M, int c, int C) {
+  if (m < M && c < C) return *reinterpret_cast<const float4*>(base + m * ld + c);
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// grid: x = slab, y = n-tile * ktiles + k-tile.  part: [slabs][N][K], pdb: [slabs][N]
+__global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict__ dY, int64_t ldy,
+                                                         const float* __restrict__ X, int64_t ldx, int64_t M,
+                                                         int N, int K, int ktiles, float* __restrict__ part,
+                                                         float* __restrict__ pdb) {
+  __shared__ float4 As[SUB][TN / 4];
+  __shared__ float4 Bs[SUB][TK / 4];
+  const int t = threadIdx.x;
+  const int tn = t / 16, tk = t % 16;  // compute layout: 4 n x 4 k per thread
+  const int lr = t / 16, lc = t % 16;  // load layout: one float4 of one row per thread (A and B)
+  const int n0 = (blockIdx.y / ktiles) * TN, k0 = (blockIdx.y % ktiles) * TK;
+  const int64_t m0 = (int64_t)blockIdx.x * kSlab;
+  const int64_t m1 = min(M, m0 + kSlab);
+  const bool want_db = pdb != nullptr && (blockIdx.y % ktiles) == 0;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ra = ld4_masked(dY, ldy, m0 + lr, m1, n0 + lc * 4, N);
+  float4 rb = ld4_masked(X, ldx, m0 + lr, m1, k0 + lc * 4, K);
+  for (int64_t ms = m0; ms < m1; ms += SUB) {
+    As[lr][lc] = ra;
+    Bs[lr][lc] = rb;
+    __syncthreads();
+    if (ms + SUB < m1) {  // prefetch the next sub-tile while this one is consumed
+      ra = ld4_masked(dY, ldy, ms + SUB + lr, m1, n0 + lc * 4, N);
+      rb = ld4_masked(X, ldx, ms + SUB + lr, m1, k0 + lc * 4, K);
+    }
+#pragma unroll
+    for (int r = 0; r < SUB; ++r) {
+      const float4 a = As[r][tn];
+      const float4 b = Bs[r][tk];
+      const float av[4] = {a.x, a.y, a.z, a.w};
+      const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+      if (want_db && tk == 0) dbacc = f4_add(dbacc, a);
+    }
+    __syncthreads();
+  }
+  const int64_t slab = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + tn * 4 + i;
+    const int k = k0 + tk * 4;
+    if (n < N && k < K)
+      *reinterpret_cast<float4*>(part + (slab * N + n) * K + k) =
+          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+  }
+  if (want_db && tk == 0) {
+    const int n = n0 + tn * 4;
+    if (n < N) *reinterpret_cast<float4*>(pdb + slab * N + n) = dbacc;
+  }
+}
+
+// dW[n,k] = sum over slabs (in order, 4 interleaved slab lanes combined in fixed order)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t slabs, int N,
+                                                           int K, float* __restrict__ dW, int64_t ldw,
+                                                           const float* __restrict__ pdb, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int e_local = threadIdx.x % 64, g = threadIdx.x / 64;
+  const int64_t NK = (int64_t)N * K;
+  const int64_t total = NK + (db ? N : 0);
+  const int64_t e = (int64_t)blockIdx.x * 64 + e_local;
+  float s = 0.f;
+  if (e < total) {
+    const float* src = e < NK ? part + e : pdb + (e - NK);
+    const int64_t stride = e < NK ? NK : N;
+    int64_t sl = g;
+    for (; sl + 12 < slabs; sl += 16) {  // four loads in flight per lane
+      const float v0 = src[sl * stride], v1 = src[(sl + 4) * stride];
+      const float v2 = src[(sl + 8) * stride], v3 = src[(sl + 12) * stride];
+      s += v0; s += v1; s += v2; s += v3;
+    }
+    for (; sl < slabs; sl += 4) s += src[sl * stride];
+  }
+  red[g][e_local] = s;
+  __syncthreads();
+  if (g == 0 && e < total) {
+    const float r = ((red[0][e_local] + red[1][e_local]) + red[2][e_local]) + red[3][e_local];
+    if (e < NK) dW[(e / K) * ldw + (e % K)] = r;
+    else db[e - NK] = r;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t fr_linear_wgrad_workspace(int64_t M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int64_t slabs = fr::ceil_div(M, kSlab);
+  return fr::align_up(slabs * N * K * 4, 256) + fr::align_up(slabs * N * 4, 256);
+}
+
+extern "C" int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x, int64_t ldx, int64_t M, int N,
+                               int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace,
+                               int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(M > 0 && N > 0 && K > 0, "empty problem");
+  FR_REQUIRE(N % 4 == 0 && K % 4 == 0, "N and K must be multiples of 4");
+  FR_REQUIRE(d_dy && d_x && d_dw && ldy >= N && ldx >= K && ldw >= K && ldy % 4 == 0 && ldx % 4 == 0,
+             "bad operands");
+  FR_REQUIRE(fr::aligned16(d_dy) && fr::aligned16(d_x), "dY and X must be 16-byte aligned");
+  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= fr_linear_wgrad_workspace(M, N, K),
+             "workspace too small");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t slabs = fr::ceil_div(M, kSlab);
+  FR_REQUIRE(slabs < (1u << 31), "too many rows");
+  float* part = reinterpret_cast<float*>(d_workspace);
+  float* pdb = reinterpret_cast<float*>(reinterpret_cast<char*>(d_workspace) + fr::align_up(slabs * N * K * 4, 256));
+  const int ntiles = (int)fr::ceil_div(N, TN), ktiles = (int)fr::ceil_div(K, TK);
+  hipLaunchKernelGGL(wgrad_slab_kernel, dim3((unsigned)slabs, (unsigned)(ntiles * ktiles)), dim3(256), 0, s, d_dy,
+                     ldy, d_x, ldx, M, N, K, ktiles, part, d_db ? pdb : nullptr);
+  FR_LAUNCH_CHECK();
+  const int64_t total = (int64_t)N * K + (d_db ? N : 0);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)fr::ceil_div(total, 64)), dim3(256), 0, s, part, slabs, N,
+                     K, d_dw, ldw, pdb, d_db);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}

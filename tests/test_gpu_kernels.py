@@ -326,3 +326,60 @@ def test_embedding_bwd_in_graph(cuda):
         ref = O.embedding_bwd_f64(ids, G.cpu().numpy(), R)
         scale = O.embedding_bwd_f64(ids, np.abs(G.cpu().numpy()), R)
         assert np.all(np.abs(W.grad.double().cpu().numpy() - ref) <= 1e-5 * scale + 1e-6)
+
+
+# ----------------------------------------------------------------------------- Linear weight grad
+@pytest.mark.parametrize("M,N,K", [(20480, 192, 64), (20480, 64, 64), (20480, 256, 64), (20480, 64, 256),
+                                   (1024, 64, 2048), (1000, 12, 20), (77, 4, 8)])
+def test_linear_wgrad_matches_fp64(cuda, M, N, K):
+    """fr_linear_wgrad vs fp64: |err| <= 1e-5 * sum_m |dY||X| + 1e-6 (fp32 slab sums); bit-identical
+    on a second launch (fixed slab order)."""
+    from FoodRec.engine import native
+    g = torch.Generator().manual_seed(M + N + K)
+    dY = torch.randn(M, N, generator=g)
+    X = torch.randn(M, K, generator=g)
+    lib = native.lib()
+    ws = native.workspace(lib.fr_linear_wgrad_workspace(M, N, K), cuda)
+    dYg, Xg = dY.to(cuda), X.to(cuda)
+    outs = []
+    for _ in range(2):
+        dW = torch.full((N, K), float("nan"), device=cuda)
+        db = torch.full((N,), float("nan"), device=cuda)
+        native.check(lib.fr_linear_wgrad(dYg.data_ptr(), N, Xg.data_ptr(), K, M, N, K, dW.data_ptr(), K,
+                                         db.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         torch.cuda.current_stream().cuda_stream), "fr_linear_wgrad")
+        outs.append((dW.cpu(), db.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = dY.double().t() @ X.double()
+    scale = dY.double().abs().t() @ X.double().abs()
+    assert torch.all((outs[0][0].double() - ref).abs() <= 1e-5 * scale + 1e-6)
+    refb = dY.double().sum(0)
+    assert torch.all((outs[0][1].double() - refb).abs() <= 1e-5 * dY.double().abs().sum(0) + 1e-6)
+
+
+def test_engine_encoder_layer_gpu(cuda):
+    """The engine TransformerEncoderLayer at HealthRec's shape (20 x 1024 tokens, d=64) vs torch's
+    module with the same weights: outputs rel 1e-5, every gradient within 1e-4 * max|grad|."""
+    import torch.nn as nn
+    from FoodRec.engine import layers
+    torch.manual_seed(0)
+    ref = nn.TransformerEncoder(nn.TransformerEncoderLayer(64, 2, 256, dropout=0.0, activation="gelu"),
+                                num_layers=2, enable_nested_tensor=False).to(cuda)
+    torch.manual_seed(0)
+    eng = nn.TransformerEncoder(layers.TransformerEncoderLayer(64, 2, 256, dropout=0.0, activation="gelu"),
+                                num_layers=2, enable_nested_tensor=False).to(cuda)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(20, 1024, 64, generator=g).to(cuda)
+    mask = (torch.rand(1024, 20, generator=g) < 0.5).to(cuda)
+    mask[:, 0] = False
+    xr, xe = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    yr = ref(xr, src_key_padding_mask=mask)
+    ye = eng(xe, src_key_padding_mask=mask)
+    torch.testing.assert_close(ye, yr, rtol=1e-5, atol=1e-5)
+    w = torch.randn(yr.shape, generator=g).to(cuda)
+    (yr * w).sum().backward()
+    (ye * w).sum().backward()
+    pairs = [("x", xr.grad, xe.grad)] + [(n, pr.grad, pe.grad) for (n, pr), (_, pe) in
+                                         zip(ref.named_parameters(), eng.named_parameters())]
+    for name, a, b in pairs:
+        assert (a - b).abs().max() <= 1e-4 * a.abs().max() + 1e-6, name

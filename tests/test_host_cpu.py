@@ -177,3 +177,37 @@ def test_safe_unpickler_refuses_code():
         pickle.dump(os.getcwd, f)   # a callable: must not be reconstructed
     with pytest.raises(pickle.UnpicklingError):
         safe_pickle_load(path)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_engine_encoder_layer_restates_torch(act):
+    """engine.layers.TransformerEncoderLayer: same parameters/init as torch's, and its restated
+    training forward (post-norm, packed in-projection, per-head key-padding mask, SDPA) gives the
+    same outputs and gradients as torch's module (cikm_model.py:33-35 builds this layer)."""
+    import torch
+    import torch.nn as nn
+    from FoodRec.engine import layers
+    torch.manual_seed(0)
+    ref = nn.TransformerEncoder(nn.TransformerEncoderLayer(64, 2, 256, dropout=0.0, activation=act),
+                                num_layers=2, enable_nested_tensor=False)
+    torch.manual_seed(0)
+    eng = nn.TransformerEncoder(layers.TransformerEncoderLayer(64, 2, 256, dropout=0.0, activation=act),
+                                num_layers=2, enable_nested_tensor=False)
+    sr, se = ref.state_dict(), eng.state_dict()
+    assert list(sr) == list(se) and all(torch.equal(sr[k], se[k]) for k in sr)
+    for layer in eng.layers:  # force the restated path on CPU (ops.linear -> F.linear below 1024 rows)
+        layer._engine_path = lambda *a: True
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(20, 7, 64, generator=g)
+    mask = torch.rand(7, 20, generator=g) < 0.4
+    mask[:, 0] = False
+    xr, xe = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    yr = ref(xr, src_key_padding_mask=mask)
+    ye = eng(xe, src_key_padding_mask=mask)
+    torch.testing.assert_close(ye, yr, rtol=1e-6, atol=1e-6)
+    w = torch.randn(yr.shape, generator=g)
+    (yr * w).sum().backward()
+    (ye * w).sum().backward()
+    torch.testing.assert_close(xe.grad, xr.grad, rtol=1e-5, atol=1e-6)
+    for (n, pr), (_, pe) in zip(ref.named_parameters(), eng.named_parameters()):
+        torch.testing.assert_close(pe.grad, pr.grad, rtol=1e-5, atol=1e-6, msg=n)
