@@ -7,6 +7,7 @@
 // ``image_embedding``/``text_embedding`` (cikm_model.py:83-87) all back-propagate through this.
 // torch's sort/unique_by_key path costs ~10 launches per call; here:
 //
+// Batches of <= 4096 ids take a sort-free owner pass (emb_owner_kernel); larger ones:
 //   1. histogram of rows + zero fill of the dense gradient (one grid-stride kernel; the wave's
 //      most frequent candidate row -- the padding row of ingredient lists -- is aggregated with a
 //      ballot so the hot counter sees one atomic per wave),
@@ -138,49 +139,98 @@ __device__ __forceinline__ int block_excl_scan_1024(int v, int* sh, int* total) 
   return res;
 }
 
-// 2. scan counts -> start[], cursors; list big buckets.  One block; each thread owns kScanPer
-//    consecutive rows (vector loads), so a 45k-row table is two block-scan rounds.
-constexpr int kScanPer = 32;
+// 2. scan counts -> start[], cursors; list big buckets.  One block; rows pass through LDS in
+//    tiles of 8192 (coalesced global loads/stores, each thread scans 8 consecutive LDS entries).
+constexpr int kScanTile = 8192;
+
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 5); }  // LDS bank-conflict padding
 
 __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cursor, int64_t R,
                                                         int32_t* __restrict__ start, int32_t* __restrict__ big,
                                                         int64_t big_cap) {
+  __shared__ int tile[kScanTile + kScanTile / 32];
   __shared__ int sh[17];
+  const int t = threadIdx.x;
   int carry = 0;
-  for (int64_t base = 0; base < R; base += 1024 * kScanPer) {
-    const int64_t i0 = base + (int64_t)threadIdx.x * kScanPer;
-    int c[kScanPer];
+  for (int64_t base = 0; base < R; base += kScanTile) {
 #pragma unroll
-    for (int j = 0; j < kScanPer; j += 4) {
-      if (i0 + j + 3 < R) {
-        const int4 v = *reinterpret_cast<const int4*>(cursor + i0 + j);
-        c[j] = v.x; c[j + 1] = v.y; c[j + 2] = v.z; c[j + 3] = v.w;
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) c[j + t] = (i0 + j + t < R) ? cursor[i0 + j + t] : 0;
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int i = j * 1024 + t;
+      tile[scan_pad(i)] = (base + i < R) ? cursor[base + i] : 0;
     }
+    __syncthreads();
+    int c[8];
     int sum = 0;
 #pragma unroll
-    for (int j = 0; j < kScanPer; ++j) sum += c[j];
+    for (int j = 0; j < 8; ++j) { c[j] = tile[scan_pad(t * 8 + j)]; sum += c[j]; }
     int tot;
     int off = carry + block_excl_scan_1024(sum, sh, &tot);
 #pragma unroll
-    for (int j = 0; j < kScanPer; ++j) {
-      if (i0 + j < R) {
-        start[i0 + j] = off;
-        cursor[i0 + j] = off;
-        if (c[j] > kSmall) {
-          const int b = atomicAdd(&cursor[R], 1);
-          if (b < big_cap) big[b] = (int)(i0 + j);
-          else atomicOr(&cursor[R + 1], kBadScan);
-        }
+    for (int j = 0; j < 8; ++j) {
+      tile[scan_pad(t * 8 + j)] = off;
+      const int64_t row = base + t * 8 + j;
+      if (c[j] > kSmall && row < R) {
+        const int b = atomicAdd(&cursor[R], 1);
+        if (b < big_cap) big[b] = (int)row;
+        else atomicOr(&cursor[R + 1], kBadScan);
       }
       off += c[j];
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = j * 1024 + t;
+      if (base + i < R) {
+        const int v = tile[scan_pad(i)];
+        start[base + i] = v;
+        cursor[base + i] = v;
+      }
+    }
     carry += tot;
+    __syncthreads();
   }
-  if (threadIdx.x == 0) start[R] = carry;
+  if (t == 0) start[R] = carry;
+}
+
+// Small batches (n <= kOwnerMax, e.g. 2B item ids into a 45k-row feature table): no sort.  Every
+// block stages all ids in LDS; the group of position i owns row idx[i] when no earlier position
+// has it, and sums that row's positions in order (matches gathered 16 at a time, loads in flight
+// together).  dW was zero-filled by the previous launch.
+constexpr int kOwnerMax = 4096;
+
+__global__ __launch_bounds__(256) void emb_owner_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t R,
+                                                        int64_t pad, const float4* __restrict__ G4, int64_t ldg4,
+                                                        int d4, float4* __restrict__ out, int64_t ldo4) {
+  __shared__ int ids[kOwnerMax];
+  for (int64_t i = threadIdx.x; i < n; i += 256) ids[i] = emb_key(idx, i, n, R, pad);
+  __syncthreads();
+  const int lig = threadIdx.x % LPR;
+  const int gshift = (threadIdx.x & 63) & ~(LPR - 1);  // this group's bit offset in a wave ballot
+  const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  const int q = blockIdx.y * LPR + lig;
+  const bool qok = q < d4;
+  if (i >= n) return;  // group-uniform
+  const int r = ids[i];
+  if (r < 0) return;
+  bool dup = false;
+  for (int64_t j = lig; j < i; j += LPR) dup |= ids[j] == r;
+  const uint64_t dmask = __ballot(dup);
+  if ((dmask >> gshift) & 0xFFFFull) return;  // an earlier position owns this row
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t jb = i; jb < n; jb += LPR) {
+    const int64_t j = jb + lig;
+    const bool m = j < n && ids[j] == r;
+    const uint32_t mask = (uint32_t)((__ballot(m) >> gshift) & 0xFFFFull);
+    if (!mask) continue;  // group-uniform
+    float4 x[LPR];
+#pragma unroll
+    for (int k = 0; k < LPR; ++k)
+      x[k] = ((mask >> k) & 1u) && qok ? G4[(jb + k) * ldg4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < LPR; ++k)
+      if ((mask >> k) & 1u) acc = f4_add(acc, x[k]);
+  }
+  if (qok) out[(int64_t)r * ldo4 + q] = acc;
 }
 
 // 3. placement (the wave's hot row takes one cursor atomic and ranks by lane)
@@ -443,6 +493,21 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   const int d4 = d / 4;
   const int64_t R = num_rows;
   EmbWS w = emb_ws(d_workspace, n, R, d);
+  if (n <= kOwnerMax) {  // zero fill, then one owner pass: no counting sort
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(R * d4, 256), (int64_t)fr::kNumCU * 8));
+    hipLaunchKernelGGL(emb_hist_zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, (int64_t)0, R,
+                       padding_idx, w.cursor, reinterpret_cast<float4*>(d_out), ldo / 4, d4);
+    FR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(emb_clear_kernel, dim3(1), dim3(256), 0, s, w.cursor + R + 1, (int64_t)1);  // status = 0
+    FR_LAUNCH_CHECK();
+    if (n > 0) {
+      hipLaunchKernelGGL(emb_owner_kernel, dim3((unsigned)fr::ceil_div(n, GPB), (unsigned)fr::ceil_div(d4, LPR)),
+                         dim3(256), 0, s, d_idx, n, R, padding_idx, reinterpret_cast<const float4*>(d_grad),
+                         ldg / 4, d4, reinterpret_cast<float4*>(d_out), ldo / 4);
+      FR_LAUNCH_CHECK();
+    }
+    return FR_OK;
+  }
   hipLaunchKernelGGL(emb_clear_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(R + 1, 256), 1024)), dim3(256), 0,
                      s, w.cursor, R + 2);
   FR_LAUNCH_CHECK();

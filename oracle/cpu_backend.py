@@ -54,7 +54,11 @@ def embedding(idx, weight, padding_idx=None):
     return torch.nn.functional.embedding(idx, weight, padding_idx=padding_idx)
 
 
-_PATCH = {"embedding": embedding, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
+def linear(x, W, b=None):
+    return torch.nn.functional.linear(x, W, b)
+
+
+_PATCH = {"embedding": embedding, "linear": linear, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
           "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
 
 

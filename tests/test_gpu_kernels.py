@@ -238,6 +238,8 @@ def _emb_case(kind, seed=0):
         return ids, R, d, R - 1
     if kind == "one_row":          # every position hits one row: one big bucket over all chunks
         return np.full(5000, 7), 50, 64, None
+    if kind == "one_row_small":    # owner pass: one owner sums all 4000 positions
+        return np.full(4000, 7), 50, 64, None
     if kind == "wide":             # image/text feature tables: 2B ids, d = 2048 (32 column slices)
         return rng.integers(0, 3000, 1024), 3000, 2048, None
     if kind == "ragged":           # d not a multiple of 64, n not a multiple of the chunk
@@ -245,13 +247,16 @@ def _emb_case(kind, seed=0):
     if kind == "few_dups":         # buckets of 2..32 (register sort) and 33+ (bitmap sort)
         base = np.repeat(np.arange(60), rng.integers(1, 70, 60))
         return rng.permutation(base), 64, 32, None
+    if kind == "few_dups_large":   # the same bucket mix through the counting-sort chain (n > 4096)
+        base = np.repeat(np.arange(200), rng.integers(1, 70, 200))
+        return rng.permutation(base), 256, 32, None
     if kind == "empty":
         return np.zeros(0, np.int64), 10, 16, None
     raise KeyError(kind)
 
 
-@pytest.mark.parametrize("kind", ["ingredients", "ingredients_pad", "one_row", "wide", "ragged",
-                                  "few_dups", "empty"])
+@pytest.mark.parametrize("kind", ["ingredients", "ingredients_pad", "one_row", "one_row_small", "wide",
+                                  "ragged", "few_dups", "few_dups_large", "empty"])
 def test_embedding_bwd_matches_fp64(cuda, kind):
     """fr_embedding_bwd vs the fp64 restatement; tolerance: |err| <= 1e-5 * sum|G| per element
     (fp32 chunked summation of up to n terms) + 1e-6; rows with no contribution exactly zero."""
@@ -295,12 +300,13 @@ def test_embedding_bwd_deterministic_and_matches_torch(cuda):
     torch.testing.assert_close(grads[0], Wt.grad, rtol=1e-5, atol=1e-5)
 
 
-def test_embedding_bwd_in_graph(cuda):
-    """The whole fr_embedding_bwd chain captures into a HIP graph and replays with new ids."""
+@pytest.mark.parametrize("n", [3000, 6000])  # owner pass (n <= 4096) and the counting-sort chain
+def test_embedding_bwd_in_graph(cuda, n):
+    """fr_embedding_bwd captures into a HIP graph and replays with new ids."""
     from FoodRec.engine import ops
     R, d = 500, 64
-    idx = torch.zeros(3000, dtype=torch.int64, device=cuda)
-    G = torch.randn(3000, d, device=cuda)
+    idx = torch.zeros(n, dtype=torch.int64, device=cuda)
+    G = torch.randn(n, d, device=cuda)
     W = torch.zeros(R, d, device=cuda, requires_grad=True)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -318,7 +324,7 @@ def test_embedding_bwd_in_graph(cuda):
         ops._EMB_STATUS = None
     rng = np.random.default_rng(5)
     for trial in range(3):
-        ids = rng.integers(0, R if trial else 3, 3000)  # trial 0: three hot rows
+        ids = rng.integers(0, R if trial else 3, n)  # trial 0: three hot rows
         idx.copy_(torch.as_tensor(ids))
         graph.replay()
         torch.cuda.synchronize()

@@ -211,3 +211,27 @@ def test_engine_encoder_layer_restates_torch(act):
     torch.testing.assert_close(xe.grad, xr.grad, rtol=1e-5, atol=1e-6)
     for (n, pr), (_, pe) in zip(ref.named_parameters(), eng.named_parameters()):
         torch.testing.assert_close(pe.grad, pr.grad, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.parametrize("model", ["CIKM_Model", "PRICAI_ModelX", "LightGCN", "BPRMF"])
+def test_oracle_cpu_backend_covers_engine_models(model):
+    """bench.py's cpu_baseline leg runs engine models on the host through oracle.cpu_backend: every
+    engine op a model calls must have a CPU restatement there (one training step, finite losses)."""
+    import torch
+    from oracle import cpu_backend
+    from helpers import tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    with cpu_backend.installed():
+        cfg = tiny_config(model, False)
+        cfg["device"] = torch.device("cpu")
+        data = tiny_data(cfg)
+        init_seed(999)
+        m = get_model(model)(cfg, data)
+        trainer = Trainer(cfg, m)
+        sampler = TripleSampler(data, 512, "cpu", replay_python_random=False)  # 2B = 1024 rows: ops.linear's engine path
+        state = trainer.new_step_state()
+        u, p, n = next(iter(sampler.epoch()))
+        trainer.train_step(trainer._features().batch(u, p, n), 0, state)
+        assert torch.isfinite(state["acc"]).all() and int(state["nan"]) == 0
