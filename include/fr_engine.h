@@ -220,6 +220,20 @@ int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x, int64_t ld
                     float* d_dw, int64_t ldw, float* d_db, void* d_workspace, int64_t workspace_bytes,
                     void* stream);
 
+/* ---- LayerNorm over the last dimension ---------------------------------------------------------
+ * Forward writes y and per-row mean / rstd (fp32); backward writes dx and, when requested, dgamma /
+ * dbeta (deterministic block partials + ordered reduce; workspace from fr_layernorm_bwd_workspace).
+ * Replaces nn.LayerNorm in the reference's ingredient Transformer (FoodRec/models/cikm_model.py:33-35)
+ * and target_attention_layer's shared Q/K LayerNorm (cikm_model.py:326-327, 349-350).
+ * d = 4 * 2^k <= 256; gamma/beta may be null (no affine). */
+int fr_layernorm_fwd(const float* d_x, int64_t ldx, int64_t rows, int d, const float* d_gamma,
+                     const float* d_beta, float eps, float* d_y, int64_t ldy, float* d_mean, float* d_rstd,
+                     void* stream);
+int64_t fr_layernorm_bwd_workspace(int d);
+int fr_layernorm_bwd(const float* d_dy, int64_t lddy, const float* d_x, int64_t ldx, int64_t rows, int d,
+                     const float* d_mean, const float* d_rstd, const float* d_gamma, float* d_dx, int64_t lddx,
+                     float* d_dgamma, float* d_dbeta, void* d_workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

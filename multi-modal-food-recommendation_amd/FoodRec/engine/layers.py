@@ -35,8 +35,9 @@ class TransformerEncoderLayer(nn.TransformerEncoderLayer):
         kpm = F._canonical_mask(mask=src_key_padding_mask, mask_name="src_key_padding_mask",
                                 other_type=None, other_name="", target_type=src.dtype)
         x = src
-        x = self.norm1(x + self._engine_sa_block(x, kpm))
-        x = self.norm2(x + self._engine_ff_block(x))
+        n1, n2 = self.norm1, self.norm2
+        x = ops.layer_norm(x + self._engine_sa_block(x, kpm), n1.normalized_shape, n1.weight, n1.bias, n1.eps)
+        x = ops.layer_norm(x + self._engine_ff_block(x), n2.normalized_shape, n2.weight, n2.bias, n2.eps)
         return x
 
     def _engine_sa_block(self, x, kpm):

@@ -49,6 +49,11 @@ _SIGS = {
     "fr_embedding_bwd_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_bwd_status_offset": (c_int64, [c_int64]),
     "fr_linear_wgrad_workspace": (c_int64, [c_int64, c_int, c_int]),
+    "fr_layernorm_fwd": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int64,
+                                 c_void_p, c_void_p, c_void_p]),
+    "fr_layernorm_bwd_workspace": (c_int64, [c_int]),
+    "fr_layernorm_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_linear_wgrad": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_int64,
                                 c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_embedding_bwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p,

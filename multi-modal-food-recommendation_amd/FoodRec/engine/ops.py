@@ -336,6 +336,69 @@ def linear(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None = None) -> t
     return _Linear.apply(x, W, b)
 
 
+# ----------------------------------------------------------------------------- LayerNorm
+def _ln_ok(x, weight, bias, d) -> bool:
+    if not (x.is_cuda and x.dtype == torch.float32 and 4 <= d <= 256 and d % 4 == 0 and (d // 4) & (d // 4 - 1) == 0):
+        return False
+    for p in (weight, bias):
+        if p is not None and (p.dtype != torch.float32 or not p.is_contiguous() or p.data_ptr() % 16):
+            return False
+    return True
+
+
+def layernorm_bytes(rows: int, d: int, backward: bool) -> int:
+    """Algorithmic bytes: forward reads x, writes y (+ mean/rstd); backward reads dy, x (+ stats),
+    writes dx."""
+    return (12 if backward else 8) * rows * d + 8 * rows
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        d = x.shape[-1]
+        x2 = _rows_operand(x, d)
+        rows = x2.shape[0]
+        y = torch.empty(rows, d, dtype=torch.float32, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        with profiling.region("layernorm", layernorm_bytes(rows, d, False)):
+            native.check(native.lib().fr_layernorm_fwd(x2.data_ptr(), x2.stride(0), rows, d, native.ptr(weight),
+                                                       native.ptr(bias), float(eps), y.data_ptr(), d,
+                                                       mean.data_ptr(), rstd.data_ptr(), native.stream_of(x2)),
+                         "fr_layernorm_fwd")
+        ctx.save_for_backward(x2, mean, rstd, weight)
+        ctx.shape, ctx.has_bias = x.shape, bias is not None
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, mean, rstd, weight = ctx.saved_tensors
+        rows, d = x2.shape
+        gy2 = _rows_operand(gy, d)
+        need = ctx.needs_input_grad
+        dx = torch.empty(rows, d, dtype=torch.float32, device=gy.device)
+        dgamma = torch.empty(d, dtype=torch.float32, device=gy.device) if (weight is not None and need[1]) else None
+        dbeta = torch.empty(d, dtype=torch.float32, device=gy.device) if (ctx.has_bias and need[2]) else None
+        lib = native.lib()
+        ws = native.workspace(lib.fr_layernorm_bwd_workspace(d), gy.device)
+        with profiling.region("layernorm", layernorm_bytes(rows, d, True)):
+            native.check(lib.fr_layernorm_bwd(gy2.data_ptr(), gy2.stride(0), x2.data_ptr(), x2.stride(0), rows, d,
+                                              mean.data_ptr(), rstd.data_ptr(), native.ptr(weight), dx.data_ptr(), d,
+                                              native.ptr(dgamma), native.ptr(dbeta), ws.data_ptr(), ws.numel(),
+                                              native.stream_of(gy2)), "fr_layernorm_bwd")
+        return dx.view(ctx.shape), dgamma, dbeta, None
+
+
+def layer_norm(x: torch.Tensor, normalized_shape, weight=None, bias=None, eps: float = 1e-5) -> torch.Tensor:
+    """``F.layer_norm`` over the last dimension through the HIP kernels ``fr_layernorm_fwd/_bwd``
+    (other shapes / dtypes / host tensors: torch's own)."""
+    shape = tuple(normalized_shape) if not isinstance(normalized_shape, int) else (normalized_shape,)
+    d = x.shape[-1]
+    if len(shape) != 1 or shape[0] != d or not _ln_ok(x, weight, bias, d):
+        return torch.nn.functional.layer_norm(x, shape, weight, bias, eps)
+    return _LayerNorm.apply(x, weight, bias, eps)
+
+
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod

@@ -54,7 +54,9 @@ class TargetAttention(nn.Module):
         kh = torch.cat(torch.chunk(k, h, dim=2), dim=0)
         vh = torch.cat(torch.chunk(v, h, dim=2), dim=0)
         if self.atten_mode == "ln":
-            qh, kh = self.ln(qh), self.ln(kh)
+            ln = self.ln
+            qh = ops.layer_norm(qh, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
+            kh = ops.layer_norm(kh, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
         scores = torch.matmul(qh, kh.transpose(1, 2)) * (kh.shape[-1] ** (-0.5))
         if seq_ids is not None:
             lq, lk = q.shape[1], k.shape[1]

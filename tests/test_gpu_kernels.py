@@ -389,3 +389,44 @@ def test_engine_encoder_layer_gpu(cuda):
                                          zip(ref.named_parameters(), eng.named_parameters())]
     for name, a, b in pairs:
         assert (a - b).abs().max() <= 1e-4 * a.abs().max() + 1e-6, name
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("rows,d,eps,affine", [(20480, 64, 1e-5, True), (40960, 32, 1e-12, True),
+                                              (4096, 32, 1e-12, True), (777, 256, 1e-5, True),
+                                              (1000, 16, 1e-5, False), (0, 64, 1e-5, True)])
+def test_layernorm_matches_fp64(cuda, rows, d, eps, affine):
+    """ops.layer_norm (fr_layernorm_fwd/_bwd) vs float64 F.layer_norm: y and dx within 2e-5 * max,
+    dgamma/dbeta within 1e-5 * sum|terms|; deterministic (second backward bit-identical)."""
+    from FoodRec.engine import ops
+    g = torch.Generator().manual_seed(rows + d)
+    x = torch.randn(rows, d, generator=g) * 3 + 1
+    w = torch.randn(d, generator=g) if affine else None
+    b = torch.randn(d, generator=g) if affine else None
+    gy = torch.randn(rows, d, generator=g)
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True) if affine else None
+    br = b.double().requires_grad_(True) if affine else None
+    yr = torch.nn.functional.layer_norm(xr, (d,), wr, br, eps)
+    yr.backward(gy.double())
+    grads = []
+    for _ in range(2):
+        xg = x.to(cuda).requires_grad_(True)
+        wg = w.to(cuda).requires_grad_(True) if affine else None
+        bg = b.to(cuda).requires_grad_(True) if affine else None
+        y = ops.layer_norm(xg, (d,), wg, bg, eps)
+        y.backward(gy.to(cuda))
+        grads.append((y.detach().cpu(), xg.grad.cpu(), None if wg is None else wg.grad.cpu(),
+                      None if bg is None else bg.grad.cpu()))
+    for a, c in zip(grads[0], grads[1]):
+        assert (a is None and c is None) or torch.equal(a, c)
+    y, dx, dw, db = grads[0]
+    if rows == 0:
+        return
+    assert (y.double() - yr.detach()).abs().max() <= 2e-5 * yr.detach().abs().max()
+    assert (dx.double() - xr.grad).abs().max() <= 2e-5 * xr.grad.abs().max()
+    if affine:
+        xhat = torch.nn.functional.layer_norm(x.double(), (d,), None, None, eps)
+        sw = (gy.double().abs() * xhat.abs()).sum(0)
+        assert torch.all((dw.double() - wr.grad).abs() <= 1e-5 * sw + 1e-6)
+        assert torch.all((db.double() - br.grad).abs() <= 1e-5 * gy.double().abs().sum(0) + 1e-6)
