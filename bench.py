@@ -50,7 +50,7 @@ def _args():
     ap.add_argument("--eager", action="store_true", help="do not capture the step in a HIP graph")
     ap.add_argument("--kernel-steps", type=int, default=10,
                     help="eager steps of the per-kernel HIP-event timing pass (roofline)")
-    ap.add_argument("--no-spmm-10m", action="store_true",
+    ap.add_argument("--no-spmm-10m", action="store_true",  # also skips the config-4 training step
                     help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
     return ap.parse_args()
 
@@ -176,11 +176,11 @@ def main():
                           "kernel_pass": f"{ksteps} eager steps, HIP events on the launch stream",
                           "eager_ms_per_step": round(eager_elapsed / ksteps * 1e3, 4)}
 
-    spmm10 = None
+    c4 = None
     if rank == 0 and not args.no_spmm_10m:
         del trainer, model, sampler, state, graphed
         torch.cuda.empty_cache()
-        spmm10 = spmm_at_scale(device)
+        c4 = config4(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -195,7 +195,7 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else "single"},
-                "roofline": roofline, "spmm": spmm, "spmm_10m": spmm10, "kernels": kernels,
+                "roofline": roofline, "spmm": spmm, "config4_10m": c4, "kernels": kernels,
                 "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -213,37 +213,81 @@ def pmc_traffic(kernel):
         return json.load(f).get("per_region_bytes", {}).get(kernel)
 
 
-def spmm_at_scale(device, iters=10):
-    """fr_spmm_csr on the BASELINE config-4 graph (10M users x 1M items x ~200M edges, d=64 fp32):
-    the propagation kernel in its HBM-bound regime (the Allrecipes tables fit the Infinity Cache)."""
+def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4):
+    """SURVEY 8(d) algorithmic bytes of one LightGCN-ID step (no-reuse gather model)."""
+    b_spmm = 8 * (N + 1) + nnz * 8 + nnz * d * s + N * d * s
+    return 2 * L * b_spmm + 2 * (L + 1) * N * d * s + 28 * P + B * (3 * 8 + 3 * d * s) * 2, b_spmm
+
+
+def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
+    """BASELINE config 4 on one GPU: the synthetic 10M users x 1M items x ~200M interactions graph.
+    (1) fr_spmm_csr alone (the propagation kernel in its HBM-bound regime; the Allrecipes tables fit
+    the Infinity Cache), (2) the full LightGCN-ID training step (device triple sampling, 2-layer
+    propagation + layer mean, fused BPR + EmbLoss, backward, fused Adam over (U+I) x 64) timed over
+    ``steps`` steps per batch size, roofline from SURVEY 8(d)'s per-step byte model."""
     import torch
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from synth_graph import synth_bipartite
+    from FoodRec.common.trainer import Trainer
     from FoodRec.engine import ops
-    from FoodRec.engine.graph import Adjacency, bipartite_norm_csr_torch
-    U, I = 10_000_000, 1_000_000
-    u, i = synth_bipartite(U, I, 20.0, seed=0, device=device)
-    rp, col, val = bipartite_norm_csr_torch(U, I, u, i)
-    del u, i
+    from FoodRec.models.lightgcn_id import LightGCN_ID
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.interaction_graph import InteractionGraph
+    U, I, d = 10_000_000, 1_000_000, 64
+    t0 = time.perf_counter()
+    g = InteractionGraph(U, I, 20.0, seed=0, device=device)
+    build_s = time.perf_counter() - t0
+    adj = g.adj
     N = U + I
-    adj = Adjacency(rp, col, val, (N, N), device=device)
-    del rp, col, val
-    X = torch.randn(N, 64, device=device)
+    X = torch.randn(N, d, device=device)
     Y = torch.empty_like(X)
     ops.spmm_launch(adj, X, Y1=Y)
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(spmm_iters):
         ops.spmm_launch(adj, X, Y1=Y)
-    e.record()
+    ev1.record()
     torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / iters
-    b = ops.spmm_bytes(adj, 64, 1)
-    out = {"graph": "synthetic U=10M I=1M E=%d (nnz=%d, N=%d)" % (adj.nnz // 2, adj.nnz, N),
-           "avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
-           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk}
-    del adj, X, Y
+    ms = ev0.elapsed_time(ev1) / spmm_iters
+    b = ops.spmm_bytes(adj, d, 1)
+    spmm = {"avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
+            "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk}
+    del X, Y
+    torch.cuda.empty_cache()
+    cfg = Config("LightGCN_ID", "Synthetic10M", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
+                                                 "ckp_root": "/tmp/frckp/"})
+    cfg["device"] = device
+    torch.manual_seed(999)
+    model = LightGCN_ID(cfg, g)
+    trainer = Trainer(cfg, model)
+    P = sum(p.numel() for p in model.parameters())
+    steps_out = {}
+    for B in batches:
+        state = trainer.new_step_state()
+
+        def step(i):
+            u, p, n = g.triples(B)
+            trainer.train_step({"u_id": u, "pos_i_id": p, "neg_i_id": n}, i, state)
+
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(warmup + i)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        assert not int(state["nan"].item()), "NaN loss in the config-4 step"
+        bstep, _ = config4_bytes_per_step(N, adj.nnz, P, B)
+        steps_out[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
+                             "bytes_per_step": bstep, "achieved_gbps": round(bstep / dt / 1e9, 1),
+                             "roofline_frac": round(bstep / dt / 1e9 / HBM_PEAK_GBPS, 4),
+                             "roofline_triples_per_s": round(B / (bstep / (HBM_PEAK_GBPS * 1e9)), 1)}
+    out = {"graph": "synthetic U=10M I=1M E=%d (nnz=%d, N=%d), built on device in %.1f s"
+                    % (g.n_edges, adj.nnz, N, build_s),
+           "model": "LightGCN_ID (L=2, d=64, fp32, BPR + EmbLoss, Adam)", "params": P, "steps_timed": steps,
+           "spmm": spmm, "step": steps_out,
+           "byte_model": "SURVEY 8(d): 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2"}
+    del trainer, model, g, adj
     torch.cuda.empty_cache()
     return out
 

@@ -234,6 +234,15 @@ int fr_layernorm_bwd(const float* d_dy, int64_t lddy, const float* d_x, int64_t 
                      const float* d_mean, const float* d_rstd, const float* d_gamma, float* d_dx, int64_t lddx,
                      float* d_dgamma, float* d_dbeta, void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- device negative sampling over a CSR interaction graph --------------------------------------
+ * out[b] = item id uniform in [0, n_items), redrawn (counter-based RNG: seed, b, attempt) while
+ * item_base + id is in user d_users[b]'s CSR row (sorted columns); at most max_tries draws.  The
+ * reference's get_random_neg (FoodRec/utils/dataloader.py:145-151) for graphs whose exclusion lists
+ * do not fit the host sampler (BASELINE config 4, 200M interactions). */
+int fr_sample_negatives_csr(const int64_t* d_rowptr, const int32_t* d_col, int64_t n_users, const int64_t* d_users,
+                            int64_t B, int64_t n_items, int64_t item_base, uint64_t seed, int max_tries,
+                            int64_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 
 import torch
 
@@ -49,6 +49,8 @@ _SIGS = {
     "fr_embedding_bwd_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_bwd_status_offset": (c_int64, [c_int64]),
     "fr_linear_wgrad_workspace": (c_int64, [c_int64, c_int, c_int]),
+    "fr_sample_negatives_csr": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64, c_uint64,
+                                        c_int, c_void_p, c_void_p]),
     "fr_layernorm_fwd": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int64,
                                  c_void_p, c_void_p, c_void_p]),
     "fr_layernorm_bwd_workspace": (c_int64, [c_int]),

@@ -170,9 +170,12 @@ def propagate_mean(adj: Adjacency, ego: torch.Tensor, n_layers: int) -> torch.Te
 class _BprEmb(torch.autograd.Function):
     @staticmethod
     def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic):
-        U, I = _rowmajor(U), _rowmajor(I)
+        # one table for users and items (item ids offset past the users): one gradient buffer
+        alias_ui, alias_e = I is U, Ie is not None and Ie is Ue
+        U = _rowmajor(U)
+        I = U if alias_ui else _rowmajor(I)
         Ue = _rowmajor(Ue) if Ue is not None else None
-        Ie = _rowmajor(Ie) if Ie is not None else None
+        Ie = Ue if alias_e else (_rowmajor(Ie) if Ie is not None else None)
         native.require_device(U, I, Ue, Ie, u, p, n)
         u, p, n = (x.to(torch.int64).contiguous() for x in (u, p, n))
         B, d = int(u.numel()), U.shape[1]
@@ -187,6 +190,7 @@ class _BprEmb(torch.autograd.Function):
         ctx.save_for_backward(U, I, Ue, Ie, u, p, n)
         ctx.ws, ctx.gamma, ctx.det = ws, gamma, int(deterministic)
         ctx.same_u, ctx.same_i = Ue is U, Ie is I
+        ctx.alias_ui, ctx.alias_e = alias_ui, alias_e
         return out[0], out[4:5]
 
     @staticmethod
@@ -197,12 +201,14 @@ class _BprEmb(torch.autograd.Function):
         g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
         gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
         need = ctx.needs_input_grad
-        dU = _grad_like(U) if need[0] else None
-        dI = _grad_like(I) if need[1] else None
+        dU = _grad_like(U) if (need[0] or (ctx.alias_ui and need[1])) else None
+        dI = dU if ctx.alias_ui else (_grad_like(I) if need[1] else None)
         dUe = dIe = None
         if Ue is not None:
-            dUe = dU if (ctx.same_u and dU is not None) else (_grad_like(Ue) if need[2] else None)
-            dIe = dI if (ctx.same_i and dI is not None) else (_grad_like(Ie) if need[3] else None)
+            dUe = dU if (ctx.same_u and dU is not None) else (
+                _grad_like(Ue) if (need[2] or (ctx.alias_e and need[3])) else None)
+            dIe = dUe if ctx.alias_e else (dI if (ctx.same_i and dI is not None) else
+                                           (_grad_like(Ie) if need[3] else None))
         B, d = int(u.numel()), U.shape[1]
         ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
         native.check(native.lib().fr_bpr_bwd(
@@ -212,8 +218,10 @@ class _BprEmb(torch.autograd.Function):
             ctx.det, ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd")
         if ctx.same_u:
             dUe = None
-        if ctx.same_i:
+        if ctx.same_i or ctx.alias_e:
             dIe = None
+        if ctx.alias_ui:
+            dI = None
         return dU, dI, dUe, dIe, None, None, None, None, None
 
 

@@ -1,0 +1,75 @@
+"""LightGCN with ID embeddings on a synthetic interaction graph -- BASELINE config 4 (SURVEY 8(a)
+a15 template: models/lightgcn.py with the ego item rows = item_embedding).
+
+One training step: ego = [user_emb; item_emb] (one [U+I, d] table), L-layer propagation with the
+layer mean (``ops.propagate_mean``: one HIP SpMM per layer, mean in the epilogue), BPRLoss on the
+propagated rows + reg_weight * EmbLoss on the ego rows of the batch (``ops.bpr_emb_loss``, fused;
+item ids offset by U into the same table so users and items share one gradient buffer), backward
+(L SpMMs), fused Adam.  Users and items live in one parameter so no [U+I, d] concatenation is
+materialised per step; ``user_embedding`` / ``item_embedding`` are views of it, and the state_dict
+carries them under the reference LightGCN's keys.
+"""
+import torch
+from torch import nn
+
+from FoodRec.common.abstract_recommender import GeneralRecommender
+from FoodRec.engine import ops
+
+
+class _TableView:
+    """``.weight`` view of a row block of the ego table (the reference's nn.Embedding attribute)."""
+
+    def __init__(self, owner, lo, hi):
+        self._owner, self._lo, self._hi = owner, lo, hi
+
+    @property
+    def weight(self):
+        return self._owner.ego[self._lo:self._hi]
+
+
+class LightGCN_ID(GeneralRecommender):
+    def __init__(self, config, dataset):
+        super().__init__(config, dataset)
+        self.latent_dim = config["embedding_size"]
+        self.n_layers = config["n_layers"]
+        self.reg_weight = config["reg_weight"]
+        U, I, d = self.n_users, self.n_items, self.latent_dim
+        dev = torch.device(config["device"]) if config["device"] is not None else dataset.adj.rowptr.device
+        self.ego = nn.Parameter(torch.empty(U + I, d, device=dev))
+        with torch.no_grad():  # xavier_uniform_ of each nn.Embedding weight (common/init.py)
+            nn.init.xavier_uniform_(self.ego[:U])
+            nn.init.xavier_uniform_(self.ego[U:])
+        self.norm_adj_matrix = dataset.adj
+        self.user_embedding = _TableView(self, 0, U)
+        self.item_embedding = _TableView(self, U, U + I)
+
+    def state_dict(self, *args, **kwargs):
+        sd = super().state_dict(*args, **kwargs)
+        ego = sd.pop("ego")
+        sd["user_embedding.weight"] = ego[:self.n_users]
+        sd["item_embedding.weight"] = ego[self.n_users:]
+        return sd
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        sd = dict(state_dict)
+        if "user_embedding.weight" in sd:
+            sd["ego"] = torch.cat([sd.pop("user_embedding.weight"), sd.pop("item_embedding.weight")])
+        return super().load_state_dict(sd, strict=strict, assign=assign)
+
+    def forward(self):
+        out = ops.propagate_mean(self.norm_adj_matrix, self.ego, self.n_layers)
+        return out[:self.n_users], out[self.n_users:]
+
+    def calculate_loss(self, batch_data):
+        out = ops.propagate_mean(self.norm_adj_matrix, self.ego, self.n_layers)
+        U = self.n_users
+        mf, emb = ops.bpr_emb_loss(out, out, self.ego, self.ego, batch_data["u_id"], batch_data["pos_i_id"] + U,
+                                   batch_data["neg_i_id"] + U)
+        return mf, self.reg_weight * emb
+
+    def inference_fast(self, batch_data, user_emb, item_emb):
+        return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
+
+    def inference_by_user(self, batch_data):
+        user_all, item_all = self.forward()
+        return self.inference_fast(batch_data, user_all, item_all)

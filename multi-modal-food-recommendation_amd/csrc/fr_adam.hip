@@ -18,7 +18,8 @@
 namespace {
 
 constexpr int kMaxTensors = 24;
-constexpr int kChunk = 4096;  // elements per block
+constexpr int kChunk = 8192;  // elements per (tensor, chunk) work item
+constexpr int kAdamBlocks = fr::kNumCU * 5;  // persistent grid: 5 blocks/CU = the 84-VGPR occupancy
 
 struct AdamArgs {
   float* p[kMaxTensors];
@@ -59,45 +60,75 @@ __global__ void adam_step_inc_kernel(AdamArgs a, const int32_t* skip) {
   if (t < a.n && a.step[t]) a.step[t][0] += 1;
 }
 
+typedef float fv4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 nt_load4(const float* p) {
+  const fv4 v = __builtin_nontemporal_load(reinterpret_cast<const fv4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store4(float* p, float4 v) {
+  fv4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<fv4*>(p));
+}
+
+__device__ __forceinline__ void adam4(float* P, const float* G, float* M, float* V, int64_t i, const AdamHyper& h,
+                                      float4& p, float4& g, float4& m, float4& v) {
+  adam_elem(p.x, g.x, m.x, v.x, h);
+  adam_elem(p.y, g.y, m.y, v.y, h);
+  adam_elem(p.z, g.z, m.z, v.z, h);
+  adam_elem(p.w, g.w, m.w, v.w, h);
+  nt_store4(P + i, p);
+  nt_store4(M + i, m);
+  nt_store4(V + i, v);
+}
+
+// Persistent grid over the launch's (tensor, chunk) list; the step-dependent scalars are derived
+// once per tensor a block meets.  Each thread keeps two float4 quartets (p, g, m, v) in flight.
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
-  int t = 0;
-  while (t + 1 < a.n && (int)blockIdx.x >= a.blk_start[t + 1]) ++t;
-  if (a.step[t]) {
-    // step-dependent scalars from device memory (graph-replayable); same double arithmetic as
-    // the host path / torch's Python scalars
-    const double st = (double)a.step[t][0];
-    const double lr = h.d_lr ? h.d_lr[0] : h.lr;
-    const double bc1 = 1.0 - pow(h.beta1_d, st);
-    const double bc2 = 1.0 - pow(h.beta2_d, st);
-    h.neg_step = (float)(-(lr / bc1));
-    h.bc2_sqrt = (float)sqrt(bc2);
-  }
-  const int64_t base = (int64_t)(blockIdx.x - a.blk_start[t]) * kChunk;
-  const int64_t end = min(base + (int64_t)kChunk, a.numel[t]);
-  float* __restrict__ P = a.p[t];
-  const float* __restrict__ G = a.g[t];
-  float* __restrict__ M = a.m[t];
-  float* __restrict__ V = a.v[t];
-  if (a.vec4[t]) {
-    for (int64_t i = base + 4 * threadIdx.x; i + 3 < end; i += 4 * blockDim.x) {
-      float4 p = *reinterpret_cast<float4*>(P + i);
-      const float4 g = *reinterpret_cast<const float4*>(G + i);
-      float4 m = *reinterpret_cast<float4*>(M + i);
-      float4 v = *reinterpret_cast<float4*>(V + i);
-      adam_elem(p.x, g.x, m.x, v.x, h);
-      adam_elem(p.y, g.y, m.y, v.y, h);
-      adam_elem(p.z, g.z, m.z, v.z, h);
-      adam_elem(p.w, g.w, m.w, v.w, h);
-      *reinterpret_cast<float4*>(P + i) = p;
-      *reinterpret_cast<float4*>(M + i) = m;
-      *reinterpret_cast<float4*>(V + i) = v;
+  const int total = a.blk_start[a.n];
+  int t = 0, cur = -1;
+  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+    while (t + 1 < a.n && c >= a.blk_start[t + 1]) ++t;
+    if (t != cur) {
+      cur = t;
+      if (a.step[t]) {
+        // step-dependent scalars from device memory (graph-replayable); same double arithmetic
+        // as the host path / torch's Python scalars
+        const double st = (double)a.step[t][0];
+        const double lr = h.d_lr ? h.d_lr[0] : h.lr;
+        const double bc1 = 1.0 - pow(h.beta1_d, st);
+        const double bc2 = 1.0 - pow(h.beta2_d, st);
+        h.neg_step = (float)(-(lr / bc1));
+        h.bc2_sqrt = (float)sqrt(bc2);
+      }
     }
-    // scalar tail of the last chunk (numel % 4)
-    const int64_t tail0 = base + ((end - base) / 4) * 4;
-    for (int64_t i = tail0 + threadIdx.x; i < end; i += blockDim.x) adam_elem(P[i], G[i], M[i], V[i], h);
-  } else {
-    for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) adam_elem(P[i], G[i], M[i], V[i], h);
+    const int64_t base = (int64_t)(c - a.blk_start[t]) * kChunk;
+    const int64_t end = min(base + (int64_t)kChunk, a.numel[t]);
+    float* __restrict__ P = a.p[t];
+    const float* __restrict__ G = a.g[t];
+    float* __restrict__ M = a.m[t];
+    float* __restrict__ V = a.v[t];
+    if (a.vec4[t]) {
+      constexpr int64_t kStride = 4 * 256;
+      int64_t i = base + 4 * threadIdx.x;
+      for (; i + kStride + 3 < end; i += 2 * kStride) {
+        float4 p0 = nt_load4(P + i), g0 = nt_load4(G + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i);
+        const int64_t i1 = i + kStride;
+        float4 p1 = nt_load4(P + i1), g1 = nt_load4(G + i1), m1 = nt_load4(M + i1), v1 = nt_load4(V + i1);
+        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+        adam4(P, G, M, V, i1, h, p1, g1, m1, v1);
+      }
+      for (; i + 3 < end; i += kStride) {
+        float4 p0 = nt_load4(P + i), g0 = nt_load4(G + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i);
+        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+      }
+      // scalar tail of the last chunk (numel % 4)
+      const int64_t tail0 = base + ((end - base) / 4) * 4;
+      for (int64_t k = tail0 + threadIdx.x; k < end; k += blockDim.x) adam_elem(P[k], G[k], M[k], V[k], h);
+    } else {
+      for (int64_t k = base + threadIdx.x; k < end; k += blockDim.x) adam_elem(P[k], G[k], M[k], V[k], h);
+    }
   }
 }
 
@@ -159,7 +190,8 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
       hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, s, a, d_skip);
       FR_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, h, d_skip);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0, s, a, h,
+                       d_skip);
     FR_LAUNCH_CHECK();
   }
   return FR_OK;

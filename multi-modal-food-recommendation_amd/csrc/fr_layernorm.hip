@@ -16,7 +16,7 @@
 
 namespace {
 
-constexpr int kLnBlocks = 128;  // backward partial blocks
+constexpr int kLnBlocks = 256;  // backward partial blocks (one per CU)
 
 template <int LPR>
 __device__ __forceinline__ float gsum(float v) {
@@ -100,22 +100,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
-// out[e] for e in [0, 2d): sum over blocks (4 interleaved lanes, combined in fixed order)
+// out[e] for e in [0, 2d): 16 outputs per block, 16 block-lanes each summing every 16th partial
+// block (8 loads in flight), lanes combined in fixed order
 __global__ __launch_bounds__(256) void ln_param_reduce_kernel(const float* __restrict__ part, int nblocks, int d,
                                                               float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
-  const int el = threadIdx.x % 64, g = threadIdx.x / 64;
-  const int e = blockIdx.x * 64 + el;
+  __shared__ float red[16][17];
+  const int el = threadIdx.x % 16, g = threadIdx.x / 16;
+  const int e = blockIdx.x * 16 + el;
   float s = 0.f;
   if (e < 2 * d) {
     const int which = e / d, c = e % d;
-    for (int b = g; b < nblocks; b += 4) s += part[((int64_t)b * 2 + which) * d + c];
+    const float* src = part + (int64_t)which * d + c;
+    const int64_t stride = 2 * (int64_t)d;
+    int b = g;
+    for (; b + 112 < nblocks; b += 128) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = src[(int64_t)(b + 16 * k) * stride];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; b < nblocks; b += 16) s += src[(int64_t)b * stride];
   }
   red[g][el] = s;
   __syncthreads();
   if (g == 0 && e < 2 * d) {
-    const float r = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
+    float r = red[0][el];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) r += red[k][el];
     if (e < d) { if (dgamma) dgamma[e] = r; }
     else if (dbeta) dbeta[e - d] = r;
   }
@@ -199,7 +212,7 @@ extern "C" int fr_layernorm_bwd(const float* d_dy, int64_t lddy, const float* d_
   }
   FR_HIP_CHECK(e);
   if (params) {
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)fr::ceil_div(2 * d, 64)), dim3(256), 0, s, part, nblocks,
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)fr::ceil_div(2 * d, 16)), dim3(256), 0, s, part, nblocks,
                        d, d_dgamma, d_dbeta);
     FR_LAUNCH_CHECK();
   }
