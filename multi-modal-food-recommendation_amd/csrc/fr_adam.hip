@@ -17,7 +17,7 @@
 
 namespace {
 
-constexpr int kMaxTensors = 24;
+constexpr int kMaxTensors = 48;  // AdamArgs = 48 x 56 B + 4 B < the 4 KiB kernel-argument limit
 constexpr int kChunk = 8192;  // elements per (tensor, chunk) work item
 constexpr int kAdamBlocks = fr::kNumCU * 5;  // persistent grid: 5 blocks/CU = the 84-VGPR occupancy
 
