@@ -177,10 +177,13 @@ def main():
                           "eager_ms_per_step": round(eager_elapsed / ksteps * 1e3, 4)}
 
     c4 = None
-    if rank == 0 and not args.no_spmm_10m:
+    if not args.no_spmm_10m:
         del trainer, model, sampler, state, graphed
         torch.cuda.empty_cache()
-        c4 = config4(device)
+        if world == 1:
+            c4 = config4(device)
+        else:
+            c4 = config4_sharded(device, world, rank)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -288,6 +291,73 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
            "spmm": spmm, "step": steps_out,
            "byte_model": "SURVEY 8(d): 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2"}
     del trainer, model, g, adj
+    torch.cuda.empty_cache()
+    return out
+
+
+def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2):
+    """BASELINE config 4 row-sharded over the job's ranks (engine/sharded.py): users in
+    nnz-balanced blocks, items replicated, one RCCL all-reduce of the item block per propagation
+    layer (forward and backward).  Every rank builds the same graph from the same seed and keeps
+    its slice; every rank samples the same global batch.  Time = max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine.sharded import ShardedGraph, ShardedLightGCN
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.interaction_graph import synth_bipartite
+    U, I, d = 10_000_000, 1_000_000, 64
+    t0 = time.perf_counter()
+    u, i = synth_bipartite(U, I, 20.0, seed=0, device=device)
+    g = ShardedGraph(U, I, u, i, rank, world, device)
+    del u, i
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    cfg = Config("LightGCN_ID", "Synthetic10M", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
+                                                 "ckp_root": "/tmp/frckp/"})
+    cfg["device"] = device
+    model = ShardedLightGCN(g, d, 2, 0.1, group=dist.group.WORLD, seed=999)
+    trainer = Trainer(cfg, model)
+    P_local = sum(p.numel() for p in model.parameters())
+    out_steps = {}
+    for B in batches:
+        state = trainer.new_step_state()
+
+        def step(k):
+            uu, pp, nn_ = g.triples(B, 999, k)
+            trainer.train_step({"u_id": uu, "pos_i_id": pp, "neg_i_id": nn_}, k, state)
+
+        for k in range(warmup):
+            step(k)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(warmup + k)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item()) / steps
+        assert not int(state["nan"].item()), "NaN loss in the sharded config-4 step"
+        # the single-GPU byte model of the whole step (work is divided, not changed, by sharding)
+        bstep, _ = config4_bytes_per_step(U + I, 2 * g.n_edges, (U + I) * d, B)
+        out_steps[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
+                             "bytes_per_step_global": bstep,
+                             "achieved_gbps_per_gpu": round(bstep / dt / 1e9 / world, 1),
+                             "roofline_frac_per_gpu": round(bstep / dt / 1e9 / world / HBM_PEAK_GBPS, 4)}
+    nnz = torch.tensor([g.local_nnz], device=device, dtype=torch.float64)
+    nnz_all = [torch.zeros_like(nnz) for _ in range(world)]
+    dist.all_gather(nnz_all, nnz)
+    out = {"graph": "synthetic U=10M I=1M E=%d, row-sharded over %d ranks (built in %.1f s)"
+                    % (g.n_edges, world, build_s),
+           "model": "LightGCN_ID row-sharded (users in nnz-balanced blocks, items replicated)",
+           "collectives_per_step": "2L=4 all-reduces of I x d fp32 (256 MB) + 2 B x d gathers",
+           "local_params_rank0": P_local, "local_nnz_per_rank": [int(x.item()) for x in nnz_all],
+           "steps_timed": steps, "step": out_steps}
+    del trainer, model, g
     torch.cuda.empty_cache()
     return out
 

@@ -236,6 +236,33 @@ def embedding_bwd_bytes(n: int, rows: int, d: int) -> int:
     return 8 * n + 4 * n * d + 4 * rows * d
 
 
+def scatter_rows(ids: torch.Tensor, G: torch.Tensor, num_rows: int, padding_idx: int | None = None) -> torch.Tensor:
+    """Dense ``dW[num_rows, d]`` with ``dW[ids[i]] += G[i]`` for ids in [0, num_rows) other than
+    ``padding_idx`` (others skipped), zeros elsewhere -- the HIP ``fr_embedding_bwd`` (deterministic)."""
+    d = G.shape[-1]
+    G = G.reshape(-1, d)
+    if G.dtype != torch.float32:
+        raise native.EngineError(f"engine ops compute in fp32 (got {G.dtype})")
+    if G.stride(1) != 1 or G.stride(0) % 4 or G.data_ptr() % 16:
+        G = G.contiguous()
+    ids = ids.reshape(-1)
+    if ids.dtype != torch.int64 or not ids.is_contiguous():
+        ids = ids.to(torch.int64).contiguous()
+    native.require_device(G, ids)
+    n, R = int(ids.numel()), int(num_rows)
+    dW = torch.empty(R, d, dtype=torch.float32, device=G.device)
+    lib = native.lib()
+    ws = native.workspace(lib.fr_embedding_bwd_workspace(n, R, d), G.device)
+    with profiling.region("embedding_bwd", embedding_bwd_bytes(n, R, d)):
+        native.check(lib.fr_embedding_bwd(ids.data_ptr(), n, G.data_ptr(), G.stride(0), d, R,
+                                          -1 if padding_idx is None else int(padding_idx), dW.data_ptr(), d,
+                                          ws.data_ptr(), ws.numel(), native.stream_of(G)), "fr_embedding_bwd")
+    if _EMB_STATUS is not None:
+        off = lib.fr_embedding_bwd_status_offset(R)
+        _EMB_STATUS.append(ws[off:off + 4].view(torch.int32))
+    return dW
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, weight, padding_idx):
@@ -247,28 +274,7 @@ class _Embedding(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        d = g.shape[-1]
-        G = g.reshape(-1, d)
-        if G.dtype != torch.float32:
-            raise native.EngineError(f"engine ops compute in fp32 (got {G.dtype})")
-        if G.stride(1) != 1 or G.stride(0) % 4 or G.data_ptr() % 16:
-            G = G.contiguous()
-        ids = idx.reshape(-1)
-        if ids.dtype != torch.int64 or not ids.is_contiguous():
-            ids = ids.to(torch.int64).contiguous()
-        n, R = int(ids.numel()), int(ctx.rows)
-        dW = torch.empty(R, d, dtype=torch.float32, device=G.device)
-        lib = native.lib()
-        ws = native.workspace(lib.fr_embedding_bwd_workspace(n, R, d), G.device)
-        with profiling.region("embedding_bwd", embedding_bwd_bytes(n, R, d)):
-            native.check(lib.fr_embedding_bwd(ids.data_ptr(), n, G.data_ptr(), G.stride(0), d, R,
-                                              -1 if ctx.pad is None else int(ctx.pad), dW.data_ptr(), d,
-                                              ws.data_ptr(), ws.numel(), native.stream_of(G)),
-                         "fr_embedding_bwd")
-        if _EMB_STATUS is not None:
-            off = lib.fr_embedding_bwd_status_offset(R)
-            _EMB_STATUS.append(ws[off:off + 4].view(torch.int32))
-        return None, dW, None
+        return None, scatter_rows(idx, g, ctx.rows, ctx.pad), None
 
 
 _EMB_STATUS = None  # test hook: a list collecting each call's device status word (0 = consistent)

@@ -1,0 +1,240 @@
+"""Row-sharded LightGCN-ID over P GPUs: the config-4 step on 1/2/4/8 MI355X.
+
+Partition.  Users are split into P contiguous blocks balanced by interactions (nnz); rank r holds
+its users' ego rows and two CSR slices of the symmetric normalised adjacency (values with the GLOBAL
+degrees, identical to the single-GPU Adjacency's entries):
+
+  A_ui[r]  [n_r x I]  user rows of rank r -> item columns       (user -> item block)
+  A_iu[r]  [I x n_r]  item rows -> rank r's users (its transpose slice)
+
+Item tables are replicated (1M x 64 fp32 = 256 MB).
+
+Forward, layer k:   E_u^{k+1} = A_ui[r] E_i^k                     (local)
+                    E_i^{k+1} = sum_r A_iu[r] E_u^k[r]             (one RCCL all-reduce of I x d)
+the item-partial SpMM is launched first and its all-reduce overlaps the user SpMM.  The layer
+mean is fused into the last user SpMM's epilogue; the item mean is one pass after the reduce.
+
+Loss.  Every rank samples the same global batch (same seeds).  The batch's user rows (propagated
+and ego) are gathered from their owners with one B x d all-reduce (exactly one non-zero
+contribution per row), after which BPRLoss + EmbLoss over the global batch are evaluated
+redundantly on every rank on identical inputs: the item gradients come out identical everywhere
+(no dense gradient all-reduce), and each rank keeps the gradient rows of its own users.
+
+Backward mirrors the forward (H_L = G/(L+1); H_k = A^T H_{k+1} + G/(L+1)): one item all-reduce per
+layer.  Per step: 2L collectives of I x d (4 x 256 MB at config 4) + two B x d gathers.  Adam: local
+user rows, replicated item rows (bit-identical across ranks, since every rank applies the same
+all-reduced gradient).
+
+With P = 1 the step is exactly the single-GPU LightGCN_ID step (up to fp32 summation order).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from . import ops
+from .graph import DEFAULT_CHUNK, Adjacency
+
+
+def _all_reduce(t, group, async_op=False):
+    if group is None or dist.get_world_size(group) == 1:
+        return None
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+
+
+class ShardedGraph:
+    """Rank ``rank``'s slice of the bipartite interaction graph (u, i) of n_users x n_items."""
+
+    def __init__(self, n_users, n_items, u, i, rank, world, device, chunk=DEFAULT_CHUNK):
+        U, I = int(n_users), int(n_items)
+        dev = torch.device(device)
+        u = torch.as_tensor(u, dtype=torch.int64, device=dev)
+        i = torch.as_tensor(i, dtype=torch.int64, device=dev)
+        key = torch.unique(u * I + i, sorted=True)  # duplicates collapse (binary graph)
+        uu = torch.div(key, I, rounding_mode="floor")
+        ii = key - uu * I
+        # every rank keeps the sorted interaction keys: the global triple sampler below draws the
+        # same batch on every rank from them (8 B per interaction)
+        self.keys = key
+        deg_u = torch.bincount(uu, minlength=U)
+        deg_i = torch.bincount(ii, minlength=I)
+        dinv_u = torch.pow(deg_u.to(torch.float64) + 1e-7, -0.5)
+        dinv_i = torch.pow(deg_i.to(torch.float64) + 1e-7, -0.5)
+        E = int(uu.numel())
+        # nnz-balanced contiguous user blocks: block r ends at the first user whose prefix count
+        # reaches E * (r+1) / P
+        cum = torch.cumsum(deg_u, 0)
+        targets = torch.tensor([E * (r + 1) // world for r in range(world)], dtype=torch.int64, device=dev)
+        ends = torch.searchsorted(cum, targets, right=False) + 1
+        ends[-1] = U
+        bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), ends.clamp(max=U)])
+        bounds = torch.cummax(bounds, 0).values
+        self.bounds = [int(x) for x in bounds.cpu()]
+        lo, hi = self.bounds[rank], self.bounds[rank + 1]
+        self.lo, self.hi, self.n_local = lo, hi, hi - lo
+        self.n_users, self.n_items, self.n_edges = U, I, E
+        self.rank, self.world = rank, world
+        # local interactions (key order = (u, i) sorted, so user rows come out CSR-ordered)
+        a = int(torch.searchsorted(uu, torch.tensor([lo], device=dev)).item())
+        b = int(torch.searchsorted(uu, torch.tensor([hi], device=dev)).item())
+        lu, li = uu[a:b] - lo, ii[a:b]
+        del uu, ii
+        val = (dinv_u[lu + lo] * dinv_i[li]).to(torch.float32)
+        rp_u = torch.zeros(self.n_local + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(torch.bincount(lu, minlength=self.n_local), 0, out=rp_u[1:])
+        self.A_ui = Adjacency(rp_u, li.to(torch.int32), val, (self.n_local, I), device=dev, chunk=chunk,
+                              symmetric=False)
+        order = torch.argsort(li * max(self.n_local, 1) + lu)
+        rp_i = torch.zeros(I + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(torch.bincount(li, minlength=I), 0, out=rp_i[1:])
+        self.A_iu = Adjacency(rp_i, lu[order].to(torch.int32), val[order], (I, self.n_local), device=dev,
+                              chunk=chunk, symmetric=False)
+        self.local_nnz = int(lu.numel())
+
+    # ------------------------------------------------------------------ global triple sampler
+    def triples(self, batch_size: int, seed: int, epoch_step: int):
+        """Batch ``epoch_step`` of the epoch permutation seeded by ``seed`` -- identical on every rank
+        (same seeds, same keys).  Positives: interactions in permutation order (the shuffled
+        positive list); negatives: uniform items redrawn while (u, n) is an interaction
+        (get_random_neg, dataloader.py:145-151), at most 64 rounds."""
+        B = int(batch_size)
+        E = self.n_edges
+        per_epoch = E // B
+        epoch, k = divmod(int(epoch_step), per_epoch)
+        dev = self.keys.device
+        if getattr(self, "_perm_epoch", None) != (seed, epoch):
+            gen = torch.Generator(device=dev).manual_seed(seed * 1_000_003 + epoch)
+            self._perm = torch.randperm(E, device=dev, generator=gen)
+            self._perm_epoch = (seed, epoch)
+        key = self.keys[self._perm[k * B:(k + 1) * B]]
+        I = self.n_items
+        u = torch.div(key, I, rounding_mode="floor")
+        p = key - u * I
+        gen = torch.Generator(device=dev).manual_seed((seed * 7_919 + int(epoch_step)) & 0x7FFFFFFFFFFF)
+        n = torch.randint(0, I, (B,), device=dev, generator=gen)
+        for _ in range(64):  # every rank takes the same rounds (same data), so draws stay in step
+            cand = u * I + n
+            pos = torch.searchsorted(self.keys, cand).clamp_(max=E - 1)
+            hit = self.keys[pos] == cand
+            if not bool(hit.any()):
+                break
+            n = torch.where(hit, torch.randint(0, I, (B,), device=dev, generator=gen), n)
+        return u, p, n
+
+    def owner_index(self, users: torch.Tensor):
+        """(mask of batch users owned by this rank, their local row index)."""
+        own = (users >= self.lo) & (users < self.hi)
+        return own, torch.where(own, users - self.lo, torch.full_like(users, -1))
+
+
+class _ShardedPropagate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ego_u, ego_i, g: ShardedGraph, L: int, group):
+        ctx.g, ctx.L, ctx.group = g, L, group
+        inv = 1.0 / (L + 1)
+        Eu, Ei = ego_u, ego_i
+        out_u = torch.empty_like(ego_u)
+        acc_i = ego_i.clone()
+        prev_u = []
+        for k in range(L):
+            pi = torch.empty_like(ego_i)
+            ops.spmm_launch(g.A_iu, Eu, Y1=pi)                    # item partial of layer k+1
+            work = _all_reduce(pi, group, async_op=True)
+            if k == L - 1:                                        # last user layer: mean in the epilogue
+                terms = [ego_u] + prev_u
+                A1 = terms[0]
+                A2 = terms[1] if len(terms) > 1 else None
+                if len(terms) <= 2:
+                    ops.spmm_launch(g.A_ui, Ei, Y2=out_u, alpha=inv, A1=A1, beta1=inv, A2=A2, beta2=inv)
+                else:
+                    ops.spmm_launch(g.A_ui, Ei, Y1=out_u)
+                    out_u.add_(torch.stack(terms).sum(0)).mul_(inv)
+                nu = None
+            else:
+                nu = torch.empty_like(ego_u)
+                ops.spmm_launch(g.A_ui, Ei, Y1=nu)
+            if work is not None:
+                work.wait()
+            acc_i.add_(pi)
+            if nu is not None:
+                prev_u.append(nu)
+                Eu = nu
+            Ei = pi
+        out_i = acc_i.mul_(inv)
+        return out_u, out_i
+
+    @staticmethod
+    def backward(ctx, g_u, g_i):
+        g, L, group = ctx.g, ctx.L, ctx.group
+        inv = 1.0 / (L + 1)
+        g_u = g_u.contiguous() if g_u is not None else None
+        g_i = g_i.contiguous() if g_i is not None else None
+        dev_u = g_u if g_u is not None else torch.zeros(g.n_local, g_i.shape[1], device=g_i.device)
+        dev_i = g_i if g_i is not None else torch.zeros(g.n_items, g_u.shape[1], device=g_u.device)
+        Hu = dev_u * inv
+        Hi = dev_i * inv
+        for _ in range(L):
+            pi = torch.empty_like(Hi)
+            ops.spmm_launch(g.A_iu, Hu, Y1=pi)
+            work = _all_reduce(pi, group, async_op=True)
+            nHu = torch.empty_like(Hu)
+            ops.spmm_launch(g.A_ui, Hi, Y2=nHu, alpha=1.0, A1=dev_u, beta1=inv)
+            if work is not None:
+                work.wait()
+            Hi = pi.add_(dev_i, alpha=inv)
+            Hu = nHu
+        return Hu, Hi, None, None, None
+
+
+class _OwnerGather(torch.autograd.Function):
+    """rows[b] = local_table[loc[b]] on the owning rank, assembled on every rank by one all-reduce
+    (exactly one rank contributes each row).  Backward: every rank holds the full gradient of the
+    gathered rows (the loss is evaluated redundantly), so each scatters its own rows -- no
+    communication (deterministic fr_embedding_bwd; rows owned elsewhere are skipped)."""
+
+    @staticmethod
+    def forward(ctx, local_table, loc, group):
+        ctx.save_for_backward(loc)
+        ctx.n = local_table.shape[0]
+        safe = loc.clamp(min=0)
+        rows = local_table.index_select(0, safe) * (loc >= 0).unsqueeze(1).to(local_table.dtype)
+        _all_reduce(rows, group)
+        return rows
+
+    @staticmethod
+    def backward(ctx, grad):
+        (loc,) = ctx.saved_tensors
+        return ops.scatter_rows(loc, grad, ctx.n), None, None
+
+
+class ShardedLightGCN(nn.Module):
+    """LightGCN_ID's parameters and step, row-sharded.  ``ego_u``: this rank's user rows; ``ego_i``:
+    the replicated item table.  Initialised from the same seed as the single-GPU model (the full
+    user table is drawn on every rank and sliced), so P ranks start from identical global tables."""
+
+    def __init__(self, graph: ShardedGraph, d=64, n_layers=2, reg_weight=0.1, group=None, seed=999):
+        super().__init__()
+        self.g, self.L, self.reg_weight, self.group, self.d = graph, int(n_layers), float(reg_weight), group, d
+        dev = graph.A_ui.rowptr.device
+        U, I = graph.n_users, graph.n_items
+        gen = torch.Generator(device=dev).manual_seed(seed)
+        bu, bi = math.sqrt(6.0 / (U + d)), math.sqrt(6.0 / (I + d))  # xavier_uniform_ of [U,d], [I,d]
+        full_u = torch.empty(U, d, device=dev).uniform_(-bu, bu, generator=gen)
+        self.ego_u = nn.Parameter(full_u[graph.lo:graph.hi].clone())
+        del full_u
+        self.ego_i = nn.Parameter(torch.empty(I, d, device=dev).uniform_(-bi, bi, generator=gen))
+
+    def calculate_loss(self, batch):
+        u, p, n = batch["u_id"], batch["pos_i_id"], batch["neg_i_id"]
+        out_u, out_i = _ShardedPropagate.apply(self.ego_u, self.ego_i, self.g, self.L, self.group)
+        _, loc = self.g.owner_index(u)
+        out_ub = _OwnerGather.apply(out_u, loc, self.group)
+        ego_ub = _OwnerGather.apply(self.ego_u, loc, self.group)
+        B = u.numel()
+        ar = torch.arange(B, device=u.device)
+        mf, _ = ops.bpr_emb_loss(out_ub, out_i, None, None, ar, p, n)
+        reg = (torch.norm(ego_ub) + torch.norm(self.ego_i[p]) + torch.norm(self.ego_i[n])) / B
+        return mf, self.reg_weight * reg.reshape(1)

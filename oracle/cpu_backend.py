@@ -23,6 +23,31 @@ def _coo(adj):
     return t
 
 
+def spmm_launch(adj, X, Y1=None, Y2=None, alpha=1.0, A1=None, beta1=0.0, A2=None, beta2=0.0, stream=None):
+    """fr_spmm_csr's epilogue contract on torch sparse: Y1 = adj@X; Y2 = alpha*adj@X + beta1*A1 + beta2*A2."""
+    Z = torch.sparse.mm(_coo(adj), X)
+    if Y1 is not None:
+        Y1.copy_(Z)
+    if Y2 is not None:
+        r = alpha * Z
+        if A1 is not None:
+            r = r + beta1 * A1
+        if A2 is not None:
+            r = r + beta2 * A2
+        Y2.copy_(r)
+
+
+def scatter_rows(ids, G, num_rows, padding_idx=None):
+    """fr_embedding_bwd: dense row scatter-add (ids outside [0, num_rows) or == padding_idx skipped)."""
+    d = G.shape[-1]
+    G = G.reshape(-1, d)
+    ids = ids.reshape(-1).to(torch.int64)
+    keep = (ids >= 0) & (ids < num_rows)
+    if padding_idx is not None:
+        keep &= ids != padding_idx
+    return torch.zeros(num_rows, d, dtype=G.dtype).index_add_(0, ids[keep], G[keep])
+
+
 def spmm(adj, X):
     return torch.sparse.mm(_coo(adj), X)
 
@@ -58,7 +83,7 @@ def linear(x, W, b=None):
     return torch.nn.functional.linear(x, W, b)
 
 
-_PATCH = {"embedding": embedding, "linear": linear, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
+_PATCH = {"embedding": embedding, "linear": linear, "spmm_launch": spmm_launch, "scatter_rows": scatter_rows, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
           "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
 
 
