@@ -81,9 +81,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FR_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU (the driver's
+    # multi-GPU runs use RCCL, one rank per GPU)
+    backend = os.environ.get("FR_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
 
     from FoodRec.common.trainer import Trainer

@@ -235,6 +235,9 @@ class ShardedLightGCN(nn.Module):
         ego_ub = _OwnerGather.apply(self.ego_u, loc, self.group)
         B = u.numel()
         ar = torch.arange(B, device=u.device)
-        mf, _ = ops.bpr_emb_loss(out_ub, out_i, None, None, ar, p, n)
-        reg = (torch.norm(ego_ub) + torch.norm(self.ego_i[p]) + torch.norm(self.ego_i[n])) / B
+        # replicated item gradients must come out bit-identical on every rank: deterministic BPR
+        # scatter (owner slots) and deterministic row gathers for the EmbLoss item rows
+        mf, _ = ops.bpr_emb_loss(out_ub, out_i, None, None, ar, p, n, deterministic=True)
+        ego_ib = ops.embedding(torch.cat([p, n]), self.ego_i)
+        reg = (torch.norm(ego_ub) + torch.norm(ego_ib[:B]) + torch.norm(ego_ib[B:])) / B
         return mf, self.reg_weight * reg.reshape(1)

@@ -141,10 +141,11 @@ class HealthRec(GeneralRecommender):
 
         all_item = torch.cat([pos_item, neg_item], dim=0)
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight), self.image_trs.weight,
-                           self.image_trs.bias).unsqueeze(1)
-        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight), self.text_trs.weight,
-                           self.text_trs.bias).unsqueeze(1)
+        xg = self.__dict__.get("_fr_exchange_group")  # data-parallel: rows exchanged, not tables
+        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange_group=xg),
+                           self.image_trs.weight, self.image_trs.bias).unsqueeze(1)
+        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange_group=xg),
+                           self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
         mm_query = torch.cat([img_q, txt_q], dim=1)
         item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)
         item_mm, _ = self.ingre_target_atten(encoded, mm_query)
@@ -165,6 +166,11 @@ class HealthRec(GeneralRecommender):
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         reg = emb3 + (torch.norm(ing_p) + torch.norm(ing_n)) / B
         return mf_loss, self.loss_health * health_loss, self.loss_kd * kd, self.reg_weight * reg
+
+    def row_sparse_tables(self):
+        """Parameters whose only use on the training step is a row gather (engine.dist exchanges
+        their data-parallel gradient as rows)."""
+        return [getattr(self, n).weight for n in ("image_embedding", "text_embedding") if hasattr(self, n)]
 
     def inference_by_user(self, batch_data):
         user_all, item_all, _ = self.forward()
