@@ -114,7 +114,7 @@ def main():
                 yield t
 
     it = batches()
-    use_graph = world == 1 and not args.eager
+    use_graph = not args.eager  # N>1: two graphs per step, gradient collectives between them
     graphed = trainer.graphed_step(args.batch, warmup=3) if use_graph else None
 
     def do_step(i):

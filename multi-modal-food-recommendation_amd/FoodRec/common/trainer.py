@@ -120,6 +120,89 @@ class GraphedStep:
         return self.static_loss
 
 
+class GraphedDPStep(GraphedStep):
+    """Data-parallel step (Trainer.grad_hook = engine.dist.GradAllReduce) as two HIP graphs with the
+    collectives between them, so no RCCL call is ever captured:
+
+      graph A  zero_grad, forward, loss, backward (row-gathered tables stash their (ids, rows)),
+               pack the dense gradients into the flat buffer
+      eager    RowExchange all-gathers + one all-reduce of the flat buffer (hook.communicate)
+      graph B  average + unpack, scatter the tables' mean row gradients, fused Adam
+
+    The first ``warmup`` calls run the same three phases eagerly (side stream for the graphed
+    parts), which also creates the hook's static buffers before capture."""
+
+    def __init__(self, trainer, batch_size, warmup=3):
+        super().__init__(trainer, batch_size, warmup)
+        self.graph_b = None
+
+    def _part_a(self, batch_idx, state, accumulate):
+        tr = self.tr
+        feats = tr._features()
+        tr.optimizer.zero_grad()
+        losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n))
+        parts = losses if isinstance(losses, tuple) else (losses,)
+        loss = sum(parts)
+        vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
+        if state.get("acc") is None:
+            state["acc"] = vec.clone()
+        elif accumulate:
+            state["acc"].add_(vec)
+        else:
+            state["acc"].copy_(vec)
+        state["nan"] |= torch.isnan(loss.detach().reshape(-1)[0]).to(torch.int32)
+        loss.backward()
+        tr.grad_hook.pack()
+        return loss.detach()
+
+    def _part_b(self, state):
+        self.tr.grad_hook.unpack()
+        self.tr._opt_step(state["nan"])
+
+    def __call__(self, u, p, n, batch_idx, state):
+        tr = self.tr
+        if u.numel() != self.B:
+            return tr.train_step(tr._features().batch(u, p, n), batch_idx, state)
+        self.u.copy_(u, non_blocking=True)
+        self.p.copy_(p, non_blocking=True)
+        self.n.copy_(n, non_blocking=True)
+        self.calls += 1
+        hook = tr.grad_hook
+        if self.graph is None and self.calls <= self.warmup:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                out = self._part_a(batch_idx, state, True)
+            torch.cuda.current_stream().wait_stream(side)
+            hook.communicate()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self._part_b(state)
+            torch.cuda.current_stream().wait_stream(side)
+            self.n_parts = state["acc"].numel()
+            return out
+        if self.graph is None:
+            self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
+            tr.optimizer.zero_grad()
+            ga = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self.static_loss = self._part_a(batch_idx, self.gstate, False)
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, pool=ga.pool()):
+                self._part_b(self.gstate)
+            self.graph, self.graph_b = ga, gb
+        self.gstate["nan"].copy_(state["nan"])
+        self.graph.replay()
+        hook.communicate()
+        self.graph_b.replay()
+        state["nan"].copy_(self.gstate["nan"])
+        if state["acc"] is None:
+            state["acc"] = self.gstate["acc"].clone()
+        else:
+            state["acc"].add_(self.gstate["acc"])
+        return self.static_loss
+
+
 class AbstractTrainer:
     def __init__(self, config, model):
         self.config = config
@@ -244,7 +327,10 @@ class Trainer(AbstractTrainer):
         return loss.detach()
 
     def graphed_step(self, batch_size: int, warmup: int = 3):
-        """A callable (u, p, n, batch_idx, state) running train_step through a captured HIP graph."""
+        """A callable (u, p, n, batch_idx, state) running train_step through captured HIP graphs
+        (data parallel: two graphs with the gradient collectives between them)."""
+        if self.grad_hook is not None and hasattr(self.grad_hook, "communicate"):
+            return GraphedDPStep(self, batch_size, warmup)
         return GraphedStep(self, batch_size, warmup)
 
     def new_step_state(self):

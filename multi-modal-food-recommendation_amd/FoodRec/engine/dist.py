@@ -30,43 +30,100 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
+class RowExchange:
+    """Data-parallel gradient of row-gathered tables, exchanged as rows.
+
+    In backward, ``ops.embedding(..., exchange=self)`` stashes its ids and gradient rows into
+    static buffers (and gives the table no dense gradient); ``exchange()`` all-gathers every rank's
+    stash (two collectives per table, P x n x (8 + 4d) bytes); ``apply()`` sets each table's
+    gradient to the deterministic scatter (fr_embedding_bwd) of the gathered rows / P -- identical
+    on every rank and equal to the mean of the ranks' dense gradients."""
+
+    def __init__(self, group, world):
+        self.group, self.world = group, int(world)
+        self.slots = {}  # id(weight) -> dict(weight, pad, ids, G, ids_all, G_all)
+
+    def stash(self, weight, padding_idx, ids, G):
+        s = self.slots.get(id(weight))
+        if s is None or s["ids"].shape != ids.shape or s["G"].shape != G.shape:
+            s = {"weight": weight, "pad": padding_idx, "ids": torch.empty_like(ids), "G": torch.empty_like(G),
+                 "ids_all": torch.empty((self.world,) + tuple(ids.shape), dtype=ids.dtype, device=ids.device),
+                 "G_all": torch.empty((self.world,) + tuple(G.shape), dtype=G.dtype, device=G.device)}
+            self.slots[id(weight)] = s
+        s["ids"].copy_(ids)
+        s["G"].copy_(G)
+
+    def exchange(self):
+        import torch.distributed as dist
+        for s in self.slots.values():  # into views of the static buffers (graph B reads them)
+            dist.all_gather(list(s["ids_all"].unbind(0)), s["ids"], group=self.group)
+            dist.all_gather(list(s["G_all"].unbind(0)), s["G"], group=self.group)
+
+    def apply(self):
+        from . import ops
+        for s in self.slots.values():
+            w = s["weight"]
+            d = s["G"].shape[-1]
+            w.grad = ops.scatter_rows(s["ids_all"].reshape(-1), s["G_all"].reshape(-1, d) * (1.0 / self.world),
+                                      w.shape[0], s["pad"])
+
+
 class GradAllReduce:
-    """Trainer.grad_hook: average gradients over ranks with ONE collective per step.
+    """Trainer.grad_hook: average gradients over ranks with ONE dense collective per step.
 
     Parameters a model lists in ``row_sparse_tables`` (tables whose only use on the step is a row
-    gather through ``ops.embedding``) are exchanged as rows inside backward instead
-    (``model._fr_exchange_group`` is set here; see ops._EmbeddingExchanged) and are left out of the
-    dense buffer: for HealthRec that is the 45,630 x 2048 image and 45,630 x 512 text tables,
-    466 MB of the 503 MB gradient."""
+    gather through ``ops.embedding``) are exchanged as rows instead (``RowExchange``; the model's
+    ``_fr_exchange`` is set here) and are left out of the dense buffer: for HealthRec that is the
+    45,630 x 2048 image and 45,630 x 512 text tables, 466 MB of the 503 MB gradient.
+
+    ``pack()`` (copy gradients into the flat buffer) and ``unpack()`` (average, copy back, apply the
+    row exchange) are collective-free, so a graphed step captures them; ``communicate()`` issues the
+    collectives eagerly between the two graphs (Trainer.GraphedDPStep)."""
 
     def __init__(self, model, world: int, group=None):
         import torch.distributed as dist
         self.world = int(world)
         self.group = group
         sparse = {id(p) for p in getattr(model, "row_sparse_tables", lambda: [])()}
+        self.rows = None
         if sparse and self.world > 1:
-            model._fr_exchange_group = group if group is not None else dist.group.WORLD
+            self.rows = RowExchange(group if group is not None else dist.group.WORLD, self.world)
+            model._fr_exchange = self.rows
         else:
             sparse = set()
         self.params = [p for p in model.parameters() if p.requires_grad and id(p) not in sparse]
         self.flat = None
         self.layout = None
+        self.views = []
 
-    def __call__(self, model):
+    def pack(self):
         live = [p for p in self.params if p.grad is not None]
         if self.flat is None or self.layout != [id(p) for p in live]:
             total = sum(p.numel() for p in live)
             self.flat = torch.empty(total, dtype=torch.float32, device=live[0].grad.device)
             self.layout = [id(p) for p in live]
         off = 0
-        views = []
+        self.views = []
         for p in live:
             n = p.numel()
             v = self.flat[off:off + n]
             v.copy_(p.grad.reshape(-1))
-            views.append((p, v))
+            self.views.append((p, v))
             off += n
+
+    def communicate(self):
+        if self.rows is not None:
+            self.rows.exchange()
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+
+    def unpack(self):
         self.flat.mul_(1.0 / self.world)
-        for p, v in views:
+        for p, v in self.views:
             p.grad.copy_(v.view_as(p.grad))
+        if self.rows is not None:
+            self.rows.apply()
+
+    def __call__(self, model):
+        self.pack()
+        self.communicate()
+        self.unpack()

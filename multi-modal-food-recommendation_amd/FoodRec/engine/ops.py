@@ -278,50 +278,38 @@ class _Embedding(torch.autograd.Function):
 
 
 class _EmbeddingExchanged(torch.autograd.Function):
-    """Data-parallel row gather whose weight gradient is exchanged as rows, not as a dense table:
-    every rank all-gathers the (ids, gradient rows) of all ranks and scatters their mean with the
-    deterministic fr_embedding_bwd -- the same result on every rank, equal to the mean of the
-    ranks' dense gradients, for P x n x d bytes instead of a 2(P-1)/P x rows x d ring."""
+    """Data-parallel row gather: backward stashes (ids, gradient rows) in the RowExchange
+    (engine.dist) instead of producing a dense table gradient; after backward the exchange
+    all-gathers every rank's rows and scatters their mean (GradAllReduce)."""
 
     @staticmethod
-    def forward(ctx, idx, weight, padding_idx, group):
+    def forward(ctx, idx, weight, padding_idx, exchange):
         native.require_device(weight, idx)
         ctx.save_for_backward(idx)
-        ctx.rows, ctx.pad, ctx.group = weight.shape[0], padding_idx, group
+        ctx.weight, ctx.pad, ctx.exchange = weight, padding_idx, exchange
         return torch.nn.functional.embedding(idx, weight)
 
     @staticmethod
     def backward(ctx, g):
-        import torch.distributed as dist
         (idx,) = ctx.saved_tensors
         d = g.shape[-1]
-        world = dist.get_world_size(ctx.group)
-        ids = idx.reshape(-1).to(torch.int64).contiguous()
-        G = g.reshape(-1, d).contiguous()
-        ids_all = [torch.empty_like(ids) for _ in range(world)]
-        G_all = [torch.empty_like(G) for _ in range(world)]
-        dist.all_gather(ids_all, ids, group=ctx.group)
-        dist.all_gather(G_all, G, group=ctx.group)
-        G_cat = torch.cat(G_all).mul_(1.0 / world)
-        return None, scatter_rows(torch.cat(ids_all), G_cat, ctx.rows, ctx.pad), None, None
+        ctx.exchange.stash(ctx.weight, ctx.pad, idx.reshape(-1).to(torch.int64), g.reshape(-1, d))
+        return None, None, None, None
 
 
 _EMB_STATUS = None  # test hook: a list collecting each call's device status word (0 = consistent)
 
 
 def embedding(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int | None = None,
-              exchange_group=None) -> torch.Tensor:
+              exchange=None) -> torch.Tensor:
     """``F.embedding(idx, weight, padding_idx)`` whose weight gradient is the deterministic HIP
     scatter-add ``fr_embedding_bwd`` (rows == padding_idx receive no gradient, as in torch).
-    ``exchange_group`` (data-parallel training): the gradient is the mean over the group's ranks,
-    exchanged as gathered rows (see _EmbeddingExchanged); the caller leaves this weight out of the
-    dense gradient all-reduce."""
+    ``exchange`` (an engine.dist.RowExchange, data-parallel training): the table's gradient is the
+    mean over the ranks, exchanged as gathered rows after backward (see _EmbeddingExchanged)."""
     if padding_idx is not None and padding_idx < 0:
         padding_idx += weight.shape[0]
-    if exchange_group is not None:
-        import torch.distributed as dist
-        if dist.get_world_size(exchange_group) > 1:
-            return _EmbeddingExchanged.apply(idx, weight, padding_idx, exchange_group)
+    if exchange is not None:
+        return _EmbeddingExchanged.apply(idx, weight, padding_idx, exchange)
     return _Embedding.apply(idx, weight, padding_idx)
 
 

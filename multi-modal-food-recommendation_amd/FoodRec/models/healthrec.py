@@ -141,10 +141,10 @@ class HealthRec(GeneralRecommender):
 
         all_item = torch.cat([pos_item, neg_item], dim=0)
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        xg = self.__dict__.get("_fr_exchange_group")  # data-parallel: rows exchanged, not tables
-        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange_group=xg),
+        xg = self.__dict__.get("_fr_exchange")  # data-parallel: rows exchanged, not tables
+        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange=xg),
                            self.image_trs.weight, self.image_trs.bias).unsqueeze(1)
-        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange_group=xg),
+        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange=xg),
                            self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
         mm_query = torch.cat([img_q, txt_q], dim=1)
         item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)

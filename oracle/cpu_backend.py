@@ -74,7 +74,7 @@ def infonce_loss(H, tau=0.5):
     return O.cl_loss(H, tau)
 
 
-def embedding(idx, weight, padding_idx=None, exchange_group=None):
+def embedding(idx, weight, padding_idx=None, exchange=None):
     # ingr_all[ingredients] / nn.Embedding(padding_idx) (cikm_model.py:230, 270-271); the data-
     # parallel row exchange is a GPU-only optimisation of the same mean gradient (the CPU baseline
     # runs one process)

@@ -79,6 +79,24 @@ def main():
             err = (a.grad - b.grad).abs().max().item()
             if err > 1e-6 * b.grad.abs().max().item() + 1e-9:
                 fails.append(f"{name}: dense gradient err {err:.3e}")
+    # graphed data-parallel steps (GraphedDPStep) == eager data-parallel steps
+    _, _, mg = build(dev)
+    _, _, me = build(dev)
+    tg, te = Trainer(cfg, mg), Trainer(cfg, me)
+    tg.grad_hook, te.grad_hook = GradAllReduce(mg, world), GradAllReduce(me, world)
+    graphed = tg.graphed_step(256, warmup=2)
+    sg, se = tg.new_step_state(), te.new_step_state()
+    it = iter(sampler.epoch())
+    for k in range(5):
+        bu, bp, bn = next(it)
+        graphed(bu, bp, bn, k, sg)
+        te.train_step(te._features().batch(bu, bp, bn), k, se)
+    for (name, a), (_, b) in zip(mg.named_parameters(), me.named_parameters()):
+        err = (a - b).abs().max().item()
+        if err > 1e-5 * b.abs().max().item() + 1e-7:
+            fails.append(f"graphed vs eager DP step: {name} err {err:.3e}")
+    if not torch.allclose(sg["acc"], se["acc"], rtol=1e-6):
+        fails.append(f"graphed vs eager loss sums {sg['acc'].tolist()} vs {se['acc'].tolist()}")
     torch.cuda.synchronize()
     print(f"[rank {rank}/{world}] exchanged tables {len(sparse)}, flat all-reduce params "
           f"{sum(x.numel() for x in hook.params)}: " + ("PASS" if not fails else "FAIL " + "; ".join(fails)),
