@@ -86,17 +86,33 @@ def main():
     tg.grad_hook, te.grad_hook = GradAllReduce(mg, world), GradAllReduce(me, world)
     graphed = tg.graphed_step(256, warmup=2)
     sg, se = tg.new_step_state(), te.new_step_state()
-    it = iter(sampler.epoch())
+    def cycle():
+        while True:
+            yield from sampler.epoch()
+
+    it = cycle()
+    # per step, at identical parameters: losses and every gradient agree (fp32 reduction order).
+    # Parameters are re-synchronised before each step because Adam turns the ~1e-9 gradient noise
+    # of zero-gradient parameters (the key part of in_proj_bias) into +-lr updates in any mode.
     for k in range(5):
         bu, bp, bn = next(it)
+        with torch.no_grad():  # same parameters in both modes (graphs read parameter memory)
+            for a, b in zip(mg.parameters(), me.parameters()):
+                a.copy_(b)
+        before_g, before_e = sg["acc"].clone() if sg["acc"] is not None else 0, \
+            se["acc"].clone() if se["acc"] is not None else 0
         graphed(bu, bp, bn, k, sg)
         te.train_step(te._features().batch(bu, bp, bn), k, se)
-    for (name, a), (_, b) in zip(mg.named_parameters(), me.named_parameters()):
-        err = (a - b).abs().max().item()
-        if err > 1e-5 * b.abs().max().item() + 1e-7:
-            fails.append(f"graphed vs eager DP step: {name} err {err:.3e}")
-    if not torch.allclose(sg["acc"], se["acc"], rtol=1e-6):
-        fails.append(f"graphed vs eager loss sums {sg['acc'].tolist()} vs {se['acc'].tolist()}")
+        dl_g, dl_e = sg["acc"] - before_g, se["acc"] - before_e
+        if not torch.allclose(dl_g, dl_e, rtol=1e-4, atol=1e-7):
+            fails.append(f"step {k}: losses {dl_g.tolist()} vs {dl_e.tolist()}")
+        for (name, a), (_, b) in zip(mg.named_parameters(), me.named_parameters()):
+            if (a.grad is None) != (b.grad is None):
+                fails.append(f"step {k}: {name} gradient presence differs")
+            elif a.grad is not None:
+                err = (a.grad - b.grad).abs().max().item()
+                if err > 1e-3 * b.grad.abs().max().item() + 1e-6:
+                    fails.append(f"step {k}: graphed vs eager gradient {name} err {err:.3e}")
     torch.cuda.synchronize()
     print(f"[rank {rank}/{world}] exchanged tables {len(sparse)}, flat all-reduce params "
           f"{sum(x.numel() for x in hook.params)}: " + ("PASS" if not fails else "FAIL " + "; ".join(fails)),
