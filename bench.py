@@ -52,6 +52,8 @@ def _args():
                     help="eager steps of the per-kernel HIP-event timing pass (roofline)")
     ap.add_argument("--no-spmm-10m", action="store_true",  # also skips the config-4 training step
                     help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip BASELINE config 5 (d=256 bf16 tables, full-sort top-k on MFMA)")
     return ap.parse_args()
 
 
@@ -191,6 +193,9 @@ def main():
             c4 = config4(device)
         else:
             c4 = config4_sharded(device, world, rank)
+    c5 = None
+    if world == 1 and not args.no_config5:
+        c5 = config5(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -205,7 +210,7 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else "single"},
-                "roofline": roofline, "spmm": spmm, "config4_10m": c4, "kernels": kernels,
+                "roofline": roofline, "spmm": spmm, "config4_10m": c4, "config5_10m_bf16": c5, "kernels": kernels,
                 "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -223,10 +228,112 @@ def pmc_traffic(kernel):
         return json.load(f).get("per_region_bytes", {}).get(kernel)
 
 
-def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4):
-    """SURVEY 8(d) algorithmic bytes of one LightGCN-ID step (no-reuse gather model)."""
+def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4, adam=28):
+    """SURVEY 8(d) algorithmic bytes of one LightGCN-ID step (no-reuse gather model).  ``adam``:
+    bytes per parameter of the optimiser pass (28 fp32; 30 for bf16 params + fp32 master/m/v)."""
     b_spmm = 8 * (N + 1) + nnz * 8 + nnz * d * s + N * d * s
-    return 2 * L * b_spmm + 2 * (L + 1) * N * d * s + 28 * P + B * (3 * 8 + 3 * d * s) * 2, b_spmm
+    return 2 * L * b_spmm + 2 * (L + 1) * N * d * s + adam * P + B * (3 * 8 + 3 * d * s) * 2, b_spmm
+
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md; no sparsity)
+MFMA_F32_PEAK_TFLOPS = 157.3
+
+
+def config5(device, batches=(512, 8192), steps=3, warmup=2, spmm_iters=5, topk_users=32768, k=20):
+    """BASELINE config 5: the config-4 graph at d=256 with bf16 tables.  (1) fr_spmm_csr_bf16 alone
+    (HBM-bound gather, s=2), (2) the LightGCN-ID training step with bf16 tables (fp32 master + moments
+    in Adam), SURVEY 8(d) byte model with s=2 and 30 B/param Adam, (3) the fused full-sort top-k
+    (fr_topk_scores: MFMA user x item GEMM + running top-k, training items masked) for
+    ``topk_users`` users against all 1M items, as TFLOP/s of the dense score GEMM vs the bf16 peak."""
+    import torch
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import ops
+    from FoodRec.models.lightgcn_id import LightGCN_ID
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.interaction_graph import InteractionGraph
+    U, I, d = 10_000_000, 1_000_000, 256
+    t0 = time.perf_counter()
+    g = InteractionGraph(U, I, 20.0, seed=0, device=device)
+    build_s = time.perf_counter() - t0
+    adj = g.adj
+    N = U + I
+    X = torch.randn(N, d, device=device).to(torch.bfloat16)
+    Y = torch.empty_like(X)
+    ops.spmm_launch(adj, X, Y1=Y)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(spmm_iters):
+        ops.spmm_launch(adj, X, Y1=Y)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / spmm_iters
+    b = ops.spmm_bytes(adj, d, 1, 2)
+    spmm = {"avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
+            "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk}
+    del X, Y
+    torch.cuda.empty_cache()
+    cfg = Config("LightGCN_ID", "Synthetic10M", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
+                                                 "ckp_root": "/tmp/frckp/", "embedding_size": d,
+                                                 "embedding_dtype": "bf16"})
+    cfg["device"] = device
+    torch.manual_seed(999)
+    model = LightGCN_ID(cfg, g)
+    trainer = Trainer(cfg, model)
+    P = sum(p.numel() for p in model.parameters())
+    steps_out = {}
+    for B in batches:
+        state = trainer.new_step_state()
+
+        def step(i):
+            u, p, n = g.triples(B)
+            trainer.train_step({"u_id": u, "pos_i_id": p, "neg_i_id": n}, i, state)
+
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(warmup + i)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        assert not int(state["nan"].item()), "NaN loss in the config-5 step"
+        bstep, _ = config4_bytes_per_step(N, adj.nnz, P, B, d=d, s=2, adam=30)
+        steps_out[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
+                             "bytes_per_step": bstep, "achieved_gbps": round(bstep / dt / 1e9, 1),
+                             "roofline_frac": round(bstep / dt / 1e9 / HBM_PEAK_GBPS, 4),
+                             "roofline_triples_per_s": round(B / (bstep / (HBM_PEAK_GBPS * 1e9)), 1)}
+    trainer.optimizer.state.clear()
+    del trainer
+    torch.cuda.empty_cache()
+    # full-sort top-k over all items for a batch of users (propagated tables computed once)
+    with torch.no_grad():
+        tables = model.forward()
+        gen = torch.Generator(device=device).manual_seed(7)
+        users = torch.randint(0, U, (topk_users,), device=device, generator=gen)
+        model.full_sort_topk(users, k, tables=tables)
+        torch.cuda.synchronize()
+        reps = 3
+        ev0.record()
+        for _ in range(reps):
+            s_, i_, _h = model.full_sort_topk(users, k, tables=tables)
+        ev1.record()
+        torch.cuda.synchronize()
+    tk_ms = ev0.elapsed_time(ev1) / reps
+    flops = ops.topk_flops(topk_users, I, d)
+    topk = {"users": topk_users, "items": I, "k": k, "mask": "training items", "avg_call_ms": round(tk_ms, 3),
+            "flops_per_call": flops, "achieved_tflops": round(flops / tk_ms / 1e9, 1),
+            "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+            "frac": round(flops / tk_ms / 1e9 / MFMA_BF16_PEAK_TFLOPS, 4),
+            "users_per_s": round(topk_users / tk_ms * 1e3, 1),
+            "kernel": "fr_topk_scores (v_mfma_f32_32x32x16_bf16 + fused running top-k + merge)"}
+    out = {"graph": "synthetic U=10M I=1M E=%d (nnz=%d), built on device in %.1f s" % (g.n_edges, adj.nnz, build_s),
+           "model": "LightGCN_ID (L=2, d=256, bf16 tables, fp32 master/moments Adam, BPR + EmbLoss)",
+           "params": P, "steps_timed": steps, "spmm_bf16": spmm, "step": steps_out, "full_sort_topk": topk,
+           "byte_model": "SURVEY 8(d) with s=2: 2L*B_spmm + 2(L+1)*N*d*2 + 30*P + B*(3*8+3*d*2)*2"}
+    del model, g, adj, tables
+    torch.cuda.empty_cache()
+    return out
 
 
 def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):

@@ -243,6 +243,73 @@ int fr_sample_negatives_csr(const int64_t* d_rowptr, const int32_t* d_col, int64
                             int64_t B, int64_t n_items, int64_t item_base, uint64_t seed, int max_tries,
                             int64_t* d_out, void* stream);
 
+/* ==========================================================================================
+ * bf16 tables (BASELINE config 5: d=256 bf16 embeddings, fp32 arithmetic, fp32 Adam state).
+ * Tables are uint16_t bit patterns of bfloat16 (torch.bfloat16 storage), row-major, 16-B aligned
+ * rows (ld % 8 == 0).  Same semantics as the fp32 entry points; results are rounded to bf16 once
+ * per output element (round to nearest even).
+ * ========================================================================================== */
+
+/* fr_spmm_csr over bf16 X/Y1/Y2/A1/A2 (fp32 edge values and accumulation); d % 8 == 0.
+ * Replaces torch.sparse.mm(norm_adj, X) + the layer mean (models/lightgcn.py:136-144) at d=256. */
+int64_t fr_spmm_bf16_workspace(const fr_spmm_plan* plan, int d);
+int fr_spmm_csr_bf16(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                     int64_t n_rows, const fr_spmm_plan* plan,
+                     const uint16_t* d_X, int64_t ldx, int d,
+                     uint16_t* d_Y1, int64_t ldy1,
+                     uint16_t* d_Y2, int64_t ldy2, float alpha,
+                     const uint16_t* d_A1, int64_t lda1, float beta1,
+                     const uint16_t* d_A2, int64_t lda2, float beta2,
+                     void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* fr_bpr_fwd / fr_bpr_bwd over bf16 tables (models/lightgcn.py:158-177, common/loss.py:32-50).
+ * Workspace: fr_bpr_workspace(B).  The backward is the deterministic owner-slot scatter; each
+ * destination row's fp32 sum is added to the bf16 gradient row once. */
+int fr_bpr_fwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t* d_I, int64_t ldi,
+                    const uint16_t* d_Ue, int64_t ldue, const uint16_t* d_Ie, int64_t ldie,
+                    const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+                    int64_t B, int d, float gamma, float* d_out,
+                    void* d_workspace, int64_t workspace_bytes, void* stream);
+int fr_bpr_bwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t* d_I, int64_t ldi,
+                    const uint16_t* d_Ue, int64_t ldue, const uint16_t* d_Ie, int64_t ldie,
+                    const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+                    int64_t B, int d, float gamma, float g_mf, float g_reg, const float* d_gscale,
+                    uint16_t* d_dU, uint16_t* d_dI, uint16_t* d_dUe, uint16_t* d_dIe,
+                    void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
+ * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as
+ * fr_adam_step) and the bf16 parameter is re-rounded from the master.  d_step: device int64
+ * counter incremented by the call; d_lr: device double (NULL -> lr).  numel % 8 == 0. */
+int fr_adam_step_bf16(uint16_t* d_param, float* d_master, const uint16_t* d_grad,
+                      float* d_exp_avg, float* d_exp_avg_sq, int64_t* d_step, int64_t numel,
+                      const double* d_lr, double lr, double beta1, double beta2, double eps,
+                      double weight_decay, const int32_t* d_skip, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Full-sort top-k (BASELINE config 5's MFMA user x item GEMM).
+ * For each of n_users query rows U[u] (dtype FR_BF16: d in {64,128,256}; FR_F32: d in {64,128}):
+ *   score(u, i) = <U[u], I[i]> for i < n_items         (full_sort_predict, the dense MMRec form:
+ *                                                         common/abstract_recommender.py:39-50)
+ *   items (item_base + i) present in the exclusion CSR row of user id uid[u] are skipped
+ *   (history masking; d_ex_ptr NULL = no masking, the reference trainer's evaluate())
+ *   out_items[u, 0:k] / out_scores[u, 0:k] = the k best by (score desc, item id asc)
+ *                                            (torch.topk in Trainer.evaluate, trainer.py:476-503)
+ *   hits[u, j] = out_items[u, j] is in held-out CSR row uid[u] (TopKEvaluator.evaluate's
+ *                `i in pos_items`, utils/topk_evaluator.py:104-107); d_hits may be NULL.
+ * uid: device int64 [n_users] global user ids (NULL = row index).  CSR rows: int64 rowptr,
+ * int32 sorted columns; test_base / ex_base offset item ids into the CSR column space.
+ * k <= 32.  Missing entries (fewer than k admissible items) are item -1, score -inf.
+ * Never materialises the n_users x n_items score matrix.  Workspace: fr_topk_workspace.
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_topk_workspace(int64_t n_users, int64_t n_items, int k);
+int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_I, int64_t ldi,
+                   int64_t n_items, int d, int dtype, int k, const int64_t* d_uid,
+                   const int64_t* d_ex_ptr, const int32_t* d_ex_col, int64_t ex_base,
+                   const int64_t* d_test_ptr, const int32_t* d_test_col, int64_t test_base,
+                   float* d_out_scores, int64_t* d_out_items, uint8_t* d_hits,
+                   void* d_workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

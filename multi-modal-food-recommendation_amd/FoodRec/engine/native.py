@@ -82,6 +82,27 @@ _SIGS = {
     "fr_adam_step_dev": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                                  POINTER(c_void_p), POINTER(c_int64), c_int, c_void_p, c_double, c_double,
                                  c_double, c_double, c_double, c_void_p, c_void_p]),
+    "fr_spmm_bf16_workspace": (c_int64, [POINTER(FrSpmmPlan), c_int]),
+    "fr_spmm_csr_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, POINTER(FrSpmmPlan),
+                                 c_void_p, c_int64, c_int,
+                                 c_void_p, c_int64,
+                                 c_void_p, c_int64, c_float,
+                                 c_void_p, c_int64, c_float,
+                                 c_void_p, c_int64, c_float,
+                                 c_void_p, c_int64, c_void_p]),
+    "fr_bpr_fwd_bf16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p,
+                                c_void_p, c_int64, c_void_p]),
+    "fr_bpr_bwd_bf16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_float,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int64, c_void_p]),
+    "fr_adam_step_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_void_p, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
+    "fr_topk_workspace": (c_int64, [c_int64, c_int64, c_int]),
+    "fr_topk_scores": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_int,
+                               c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),

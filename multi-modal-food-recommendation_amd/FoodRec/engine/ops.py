@@ -23,14 +23,24 @@ from .graph import Adjacency
 _f = ctypes.c_float
 
 
-def _rowmajor(t: torch.Tensor) -> torch.Tensor:
-    if t.dtype != torch.float32:
-        raise native.EngineError(f"engine ops compute in fp32 (got {t.dtype})")
+def _rowmajor(t: torch.Tensor, f32_only: bool = False) -> torch.Tensor:
+    """Row-major table with 16-B aligned rows: fp32 (ld % 4 == 0) or bf16 storage (ld % 8 == 0,
+    the config-5 tables; arithmetic stays fp32 inside the kernels)."""
+    if t.dtype != torch.float32 and (f32_only or t.dtype != torch.bfloat16):
+        raise native.EngineError(f"engine tables are fp32 or bf16 (got {t.dtype})")
     if t.dim() != 2:
         raise native.EngineError(f"expected a 2-D table, got shape {tuple(t.shape)}")
-    if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+    per16 = 16 // t.element_size()
+    if t.stride(1) != 1 or t.stride(0) % per16 or t.data_ptr() % 16:
         t = t.contiguous()
     return t
+
+
+def _same_dtype(*ts) -> torch.dtype:
+    dts = {t.dtype for t in ts if t is not None}
+    if len(dts) != 1:
+        raise native.EngineError(f"mixed table dtypes {sorted(map(str, dts))}")
+    return dts.pop()
 
 
 def _grad_like(t: torch.Tensor) -> torch.Tensor:
@@ -60,19 +70,35 @@ def spmm_launch(adj: Adjacency, X: torch.Tensor, Y1=None, Y2=None, alpha=1.0, A1
     plan = adj.plan()
     ws = _ws_for(adj, d, X.device)
     s = stream if stream is not None else native.stream_of(X)
+    dt = _same_dtype(X, Y1, Y2, A1, A2)
 
     def ld(t):
         return t.stride(0) if t is not None else 0
 
-    with profiling.region("spmm", spmm_bytes(adj, d, sum(x is not None for x in (Y1, Y2, A1, A2)))):
-        _spmm_call(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld)
+    with profiling.region("spmm", spmm_bytes(adj, d, sum(x is not None for x in (Y1, Y2, A1, A2)),
+                                             X.element_size())):
+        call = _spmm_call_bf16 if dt == torch.bfloat16 else _spmm_call
+        call(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld)
 
 
-def spmm_bytes(adj: Adjacency, d: int, n_rowio: int = 1) -> int:
+def spmm_bytes(adj: Adjacency, d: int, n_rowio: int = 1, elem: int = 4) -> int:
     """Algorithmic HBM bytes of one SpMM launch (no-reuse gather model):
-    rowptr 8(N+1) + col/val 8 nnz + gathered rows 4 d nnz + 4 d N per output written / addend read."""
+    rowptr 8(N+1) + col/val 8 nnz + gathered rows s d nnz + s d N per output written / addend read
+    (s = 4 fp32, 2 bf16)."""
     n = adj.shape[0]
-    return 8 * (n + 1) + 8 * adj.nnz + 4 * d * adj.nnz + 4 * d * n * n_rowio
+    return 8 * (n + 1) + 8 * adj.nnz + elem * d * adj.nnz + elem * d * n * n_rowio
+
+
+def _spmm_call_bf16(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld):
+    rc = native.lib().fr_spmm_csr_bf16(
+        adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], ctypes.byref(plan),
+        X.data_ptr(), ld(X), d,
+        native.ptr(Y1), ld(Y1),
+        native.ptr(Y2), ld(Y2), _f(alpha),
+        native.ptr(A1), ld(A1), _f(beta1),
+        native.ptr(A2), ld(A2), _f(beta2),
+        ws.data_ptr(), ws.numel(), s)
+    native.check(rc, "fr_spmm_csr_bf16")
 
 
 def _spmm_call(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld):
@@ -91,7 +117,7 @@ class _SpMM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, adj, X):
         X = _rowmajor(X)
-        Y = torch.empty((adj.shape[0], X.shape[1]), dtype=torch.float32, device=X.device)
+        Y = torch.empty((adj.shape[0], X.shape[1]), dtype=X.dtype, device=X.device)
         spmm_launch(adj, X, Y1=Y)
         ctx.adj = adj
         return Y
@@ -100,7 +126,7 @@ class _SpMM(torch.autograd.Function):
     def backward(ctx, G):
         G = _rowmajor(G)
         at = ctx.adj.transpose_csr()
-        dX = torch.empty((at.shape[0], G.shape[1]), dtype=torch.float32, device=G.device)
+        dX = torch.empty((at.shape[0], G.shape[1]), dtype=G.dtype, device=G.device)
         spmm_launch(at, G, Y1=dX)
         return None, dX
 
@@ -179,14 +205,16 @@ class _BprEmb(torch.autograd.Function):
         native.require_device(U, I, Ue, Ie, u, p, n)
         u, p, n = (x.to(torch.int64).contiguous() for x in (u, p, n))
         B, d = int(u.numel()), U.shape[1]
+        bf16 = _same_dtype(U, I, Ue, Ie) == torch.bfloat16
         lib = native.lib()
         ws = native.workspace(lib.fr_bpr_workspace(B), U.device)
         out = torch.empty(5, dtype=torch.float32, device=U.device)
         ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
-        native.check(lib.fr_bpr_fwd(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
-                                    native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
-                                    B, d, _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(),
-                                    native.stream_of(U)), "fr_bpr_fwd")
+        fwd = lib.fr_bpr_fwd_bf16 if bf16 else lib.fr_bpr_fwd
+        native.check(fwd(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
+                         native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                         B, d, _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                         native.stream_of(U)), "fr_bpr_fwd")
         ctx.save_for_backward(U, I, Ue, Ie, u, p, n)
         ctx.ws, ctx.gamma, ctx.det = ws, gamma, int(deterministic)
         ctx.same_u, ctx.same_i = Ue is U, Ie is I
@@ -211,11 +239,18 @@ class _BprEmb(torch.autograd.Function):
                                            (_grad_like(Ie) if need[3] else None))
         B, d = int(u.numel()), U.shape[1]
         ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
-        native.check(native.lib().fr_bpr_bwd(
-            U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
-            u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
-            gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
-            ctx.det, ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd")
+        if U.dtype == torch.bfloat16:
+            native.check(native.lib().fr_bpr_bwd_bf16(
+                U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
+                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd_bf16")
+        else:
+            native.check(native.lib().fr_bpr_bwd(
+                U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
+                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                ctx.det, ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd")
         if ctx.same_u:
             dUe = None
         if ctx.same_i or ctx.alias_e:
@@ -442,7 +477,7 @@ def layer_norm(x: torch.Tensor, normalized_shape, weight=None, bias=None, eps: f
 class _DCor(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pairs, *views):
-        views = tuple(_rowmajor(v) for v in views)
+        views = tuple(_rowmajor(v, f32_only=True) for v in views)
         native.require_device(*views)
         V = len(views)
         n, d = views[0].shape
@@ -482,7 +517,7 @@ def dcor_loss(views, pairs) -> torch.Tensor:
 class _InfoNCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, H, tau):
-        H = _rowmajor(H)
+        H = _rowmajor(H, f32_only=True)
         native.require_device(H)
         m, d = H.shape
         if m % 2:
@@ -510,3 +545,63 @@ class _InfoNCE(torch.autograd.Function):
 
 def infonce_loss(H: torch.Tensor, tau: float = 0.5) -> torch.Tensor:
     return _InfoNCE.apply(H, float(tau))
+
+
+# ----------------------------------------------------------------------------- full-sort top-k
+def topk_flops(n_users: int, n_items: int, d: int) -> int:
+    """Algorithmic FLOPs of one fr_topk_scores call: the dense n_users x n_items x d score GEMM."""
+    return 2 * n_users * n_items * d
+
+
+def full_sort_topk(user_rows: torch.Tensor, item_table: torch.Tensor, k: int, user_ids=None,
+                   exclude=None, held_out=None):
+    """Top-k items per query user over ALL items, scored <user, item> on the matrix cores, with
+    the running top-k fused (the n_users x n_items score matrix is never written).
+
+    user_rows [n, d] and item_table [I, d]: both fp32 (d in {64, 128}) or both bf16
+    (d in {64, 128, 256}).  ``exclude`` / ``held_out``: optional (rowptr int64, col int32, base)
+    CSRs indexed by ``user_ids`` (int64 [n], default 0..n-1); items ``base + i`` in a user's
+    ``exclude`` row are skipped (history masking), and ``hits[u, j]`` flags top-k entries found in
+    the user's ``held_out`` row.  Order: score descending, item id ascending on ties.
+    Returns (scores f32 [n, k], items int64 [n, k], hits uint8 [n, k] or None).
+    Replaces full_sort_predict + torch.topk (common/trainer.py:476-503, topk_evaluator.py:45-66)."""
+    U = _rowmajor(user_rows)
+    It = _rowmajor(item_table)
+    dt = _same_dtype(U, It)
+    native.require_device(U, It)
+    n, d = U.shape
+    nI = It.shape[0]
+    if It.shape[1] != d:
+        raise native.EngineError(f"full_sort_topk: user d={d} vs item d={It.shape[1]}")
+    dev = U.device
+    scores = torch.empty(n, k, dtype=torch.float32, device=dev)
+    items = torch.empty(n, k, dtype=torch.int64, device=dev)
+    hits = torch.empty(n, k, dtype=torch.uint8, device=dev) if held_out is not None else None
+    if n == 0:
+        return scores, items, hits
+    lib = native.lib()
+    ws = native.workspace(lib.fr_topk_workspace(n, nI, k), dev)
+    uid = user_ids.to(device=dev, dtype=torch.int64).contiguous() if user_ids is not None else None
+
+    def csr(c):
+        if c is None:
+            return None, None, 0
+        rp, col, base = c
+        return rp, col, int(base)
+
+    ep, ec, eb = csr(exclude)
+    tp, tc, tb = csr(held_out)
+    for t in (ep, ec, tp, tc):
+        if t is not None:
+            native.require_device(t)
+    if (ep is not None and (ep.dtype != torch.int64 or ec.dtype != torch.int32)) or \
+            (tp is not None and (tp.dtype != torch.int64 or tc.dtype != torch.int32)):
+        raise native.EngineError("CSR rows must be int64 rowptr + int32 columns")
+    with profiling.region("topk", topk_flops(n, nI, d)):
+        native.check(lib.fr_topk_scores(
+            U.data_ptr(), U.stride(0), n, It.data_ptr(), It.stride(0), nI, d,
+            1 if dt == torch.bfloat16 else 0, int(k), native.ptr(uid),
+            native.ptr(ep), native.ptr(ec), eb, native.ptr(tp), native.ptr(tc), tb,
+            scores.data_ptr(), items.data_ptr(), native.ptr(hits), ws.data_ptr(), ws.numel(),
+            native.stream_of(U)), "fr_topk_scores")
+    return scores, items, hits

@@ -70,10 +70,19 @@ class FusedAdam(torch.optim.Optimizer):
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    # fp32 moments (and, for bf16 parameters, an fp32 master copy: config 5)
+                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32,
+                                                        memory_format=torch.preserve_format)
+                    if p.dtype == torch.bfloat16:
+                        st["master"] = p.detach().float()
                 elif st["step"].device != p.device or st["step"].dtype != torch.int64:
                     st["step"] = st["step"].to(device=p.device, dtype=torch.int64)
+                if p.dtype == torch.bfloat16:
+                    self._step_bf16(p, group, lib, skip_flag, gi)
+                    continue
+                if p.dtype != torch.float32:
+                    raise RuntimeError(f"FusedAdam supports fp32 and bf16 parameters (got {p.dtype})")
                 plist.append(p)
             if not plist:
                 continue
@@ -92,3 +101,18 @@ class FusedAdam(torch.optim.Optimizer):
                     float(group["eps"]), float(group["weight_decay"]), native.ptr(skip_flag),
                     native.stream_of(plist[0])), "fr_adam_step_dev")
         return loss
+
+    def _step_bf16(self, p, group, lib, skip_flag, gi):
+        """bf16 parameter: update the fp32 master with fp32 moments, re-round the parameter."""
+        st = self.state[p]
+        g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+        if g.dtype != torch.bfloat16:
+            raise RuntimeError("a bf16 parameter needs a bf16 gradient")
+        beta1, beta2 = group["betas"]
+        d_lr = self._lr_tensor(gi, group, p.device)
+        with profiling.region("adam", 30 * p.numel()):
+            native.check(lib.fr_adam_step_bf16(
+                p.data_ptr(), st["master"].data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                st["exp_avg_sq"].data_ptr(), st["step"].data_ptr(), p.numel(), d_lr.data_ptr(),
+                float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+                float(group["weight_decay"]), native.ptr(skip_flag), native.stream_of(p)), "fr_adam_step_bf16")

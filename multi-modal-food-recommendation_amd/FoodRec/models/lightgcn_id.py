@@ -8,6 +8,12 @@ item ids offset by U into the same table so users and items share one gradient b
 (L SpMMs), fused Adam.  Users and items live in one parameter so no [U+I, d] concatenation is
 materialised per step; ``user_embedding`` / ``item_embedding`` are views of it, and the state_dict
 carries them under the reference LightGCN's keys.
+
+``embedding_dtype: bf16`` (BASELINE config 5, d=256): the ego table and every propagated table are
+bf16 in HBM (half the gather bytes of the HBM-bound SpMM); SpMM / BPR arithmetic is fp32 in the
+kernels and Adam runs on an fp32 master copy with fp32 moments (``FusedAdam``).
+``full_sort_topk`` ranks all items for a batch of users on the matrix cores (MFMA) with the
+training items masked and the top-k selection fused into the GEMM.
 """
 import torch
 from torch import nn
@@ -35,10 +41,14 @@ class LightGCN_ID(GeneralRecommender):
         self.reg_weight = config["reg_weight"]
         U, I, d = self.n_users, self.n_items, self.latent_dim
         dev = torch.device(config["device"]) if config["device"] is not None else dataset.adj.rowptr.device
-        self.ego = nn.Parameter(torch.empty(U + I, d, device=dev))
+        # BASELINE config 5: bf16 tables (the optimiser keeps an fp32 master copy and fp32 moments)
+        self.table_dtype = torch.bfloat16 if str(config["embedding_dtype"] or "fp32") == "bf16" else torch.float32
+        ego = torch.empty(U + I, d, device=dev)
         with torch.no_grad():  # xavier_uniform_ of each nn.Embedding weight (common/init.py)
-            nn.init.xavier_uniform_(self.ego[:U])
-            nn.init.xavier_uniform_(self.ego[U:])
+            nn.init.xavier_uniform_(ego[:U])
+            nn.init.xavier_uniform_(ego[U:])
+        self.ego = nn.Parameter(ego.to(self.table_dtype))
+        del ego
         self.norm_adj_matrix = dataset.adj
         self.user_embedding = _TableView(self, 0, U)
         self.item_embedding = _TableView(self, U, U + I)
@@ -66,6 +76,23 @@ class LightGCN_ID(GeneralRecommender):
         mf, emb = ops.bpr_emb_loss(out, out, self.ego, self.ego, batch_data["u_id"], batch_data["pos_i_id"] + U,
                                    batch_data["neg_i_id"] + U)
         return mf, self.reg_weight * emb
+
+    def full_sort_predict(self, batch_data):
+        """Dense scores of the batch users against every item (common/abstract_recommender.py:39-50)."""
+        user_all, item_all = self.forward()
+        return torch.matmul(user_all[batch_data["u_id"]].float(), item_all.float().t())
+
+    def full_sort_topk(self, users, k, exclude_train=True, held_out=None, tables=None):
+        """Fused full-sort top-k on the matrix cores (engine.ops.full_sort_topk): scores of ``users``
+        against all items with the user's training items masked (``exclude_train``), top ``k``.
+        ``tables``: precomputed (user_all, item_all) to score several user batches per propagation."""
+        user_all, item_all = tables if tables is not None else self.forward()
+        users = users.to(device=user_all.device, dtype=torch.int64)
+        ex = None
+        if exclude_train:
+            adj = self.norm_adj_matrix
+            ex = (adj.rowptr, adj.col, self.n_users)  # user rows of the adjacency hold U + item
+        return ops.full_sort_topk(user_all[users], item_all, k, user_ids=users, exclude=ex, held_out=held_out)
 
     def inference_fast(self, batch_data, user_emb, item_emb):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)

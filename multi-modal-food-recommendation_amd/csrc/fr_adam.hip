@@ -11,6 +11,7 @@
 // Adam on MI355X (m and v bit-identical; p differs by <= 1 ulp on ~0.1% of elements).
 // 28 B of HBM traffic per parameter (p,m,v read+write, g read): HBM-bound, float4 vectorised.
 #include "fr_common.h"
+#include "fr_bf16.h"
 
 #include <algorithm>
 #include <cmath>
@@ -132,6 +133,52 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
   }
 }
 
+
+// Mixed precision (BASELINE config 5): bf16 parameter + bf16 gradient, fp32 master copy and
+// fp32 exp_avg / exp_avg_sq.  The update is adam_elem on the master; the bf16 parameter the
+// SpMM reads is the master rounded to nearest even.  30 B per parameter.
+__global__ __launch_bounds__(256) void adam_bf16_kernel(uint4* __restrict__ P16, float* __restrict__ W,
+                                                        const uint4* __restrict__ G16, float* __restrict__ M,
+                                                        float* __restrict__ V, int64_t n8, int64_t* step,
+                                                        AdamHyper h, const int32_t* skip) {
+  if (skip && *skip) return;
+  if (step) {
+    const double st = (double)step[0];
+    const double lr = h.d_lr ? h.d_lr[0] : h.lr;
+    h.neg_step = (float)(-(lr / (1.0 - pow(h.beta1_d, st))));
+    h.bc2_sqrt = (float)sqrt(1.0 - pow(h.beta2_d, st));
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float g[8], w[8], m[8], v[8];
+    fr_unpack8(G16[i], g);
+    const float4* W4 = reinterpret_cast<const float4*>(W) + 2 * i;
+    const float4* M4 = reinterpret_cast<const float4*>(M) + 2 * i;
+    const float4* V4 = reinterpret_cast<const float4*>(V) + 2 * i;
+    const float4 w0 = nt_load4(reinterpret_cast<const float*>(W4)), w1 = nt_load4(reinterpret_cast<const float*>(W4 + 1));
+    const float4 m0 = nt_load4(reinterpret_cast<const float*>(M4)), m1 = nt_load4(reinterpret_cast<const float*>(M4 + 1));
+    const float4 v0 = nt_load4(reinterpret_cast<const float*>(V4)), v1 = nt_load4(reinterpret_cast<const float*>(V4 + 1));
+    w[0] = w0.x; w[1] = w0.y; w[2] = w0.z; w[3] = w0.w; w[4] = w1.x; w[5] = w1.y; w[6] = w1.z; w[7] = w1.w;
+    m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w; m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adam_elem(w[j], g[j], m[j], v[j], h);
+    float* Wo = W + 8 * i;
+    float* Mo = M + 8 * i;
+    float* Vo = V + 8 * i;
+    nt_store4(Wo, make_float4(w[0], w[1], w[2], w[3]));
+    nt_store4(Wo + 4, make_float4(w[4], w[5], w[6], w[7]));
+    nt_store4(Mo, make_float4(m[0], m[1], m[2], m[3]));
+    nt_store4(Mo + 4, make_float4(m[4], m[5], m[6], m[7]));
+    nt_store4(Vo, make_float4(v[0], v[1], v[2], v[3]));
+    nt_store4(Vo + 4, make_float4(v[4], v[5], v[6], v[7]));
+    P16[i] = fr_pack8(w);
+  }
+}
+
+__global__ void adam_bf16_step_inc_kernel(int64_t* step, const int32_t* skip) {
+  if (skip && *skip) return;
+  if (threadIdx.x == 0) step[0] += 1;
+}
 }  // namespace
 
 static int adam_impl(float* const* params, const float* const* grads, float* const* exp_avg,
@@ -213,4 +260,37 @@ extern "C" int fr_adam_step_dev(float* const* params, const float* const* grads,
   FR_REQUIRE(d_steps, "d_steps (device step counters) required");
   return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1,
                    beta2, eps, weight_decay, 0, d_skip, stream);
+}
+
+extern "C" int fr_adam_step_bf16(uint16_t* d_param, float* d_master, const uint16_t* d_grad, float* d_exp_avg,
+                                 float* d_exp_avg_sq, int64_t* d_step, int64_t numel, const double* d_lr,
+                                 double lr, double beta1, double beta2, double eps, double weight_decay,
+                                 const int32_t* d_skip, void* stream) {
+  FR_REQUIRE(numel >= 0 && numel % 8 == 0, "numel must be a multiple of 8");
+  if (numel == 0) return FR_OK;
+  FR_REQUIRE(d_param && d_master && d_grad && d_exp_avg && d_exp_avg_sq && d_step, "null pointer");
+  for (const void* p : {(const void*)d_param, (const void*)d_master, (const void*)d_grad, (const void*)d_exp_avg,
+                        (const void*)d_exp_avg_sq})
+    FR_REQUIRE(fr::aligned16(p), "tensors must be 16-B aligned");
+  AdamHyper h;
+  h.lr = lr;
+  h.beta1_d = beta1;
+  h.beta2_d = beta2;
+  h.d_lr = d_lr;
+  h.w1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.one_m_b2 = (float)(1.0 - beta2);
+  h.neg_step = 0.f;
+  h.bc2_sqrt = 1.f;
+  h.eps = (float)eps;
+  h.wd = (float)weight_decay;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_bf16_step_inc_kernel, dim3(1), dim3(64), 0, s, d_step, d_skip);
+  FR_LAUNCH_CHECK();
+  const int64_t n8 = numel / 8;
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(n8, 256), (int64_t)fr::kNumCU * 8);
+  hipLaunchKernelGGL(adam_bf16_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(d_param), d_master,
+                     reinterpret_cast<const uint4*>(d_grad), d_exp_avg, d_exp_avg_sq, n8, d_step, h, d_skip);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
 }

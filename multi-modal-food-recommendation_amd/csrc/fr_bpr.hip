@@ -12,8 +12,10 @@
 // destination row is summed by its first-occurring slot in the reference's autograd order
 // (index backward of pos, then of neg, each in batch order), so results are run-to-run identical.
 #include "fr_common.h"
+#include "fr_bf16.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 
@@ -244,6 +246,144 @@ __global__ __launch_bounds__(256) void bpr_bwd_det_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// bf16 tables (BASELINE config 5): rows of d bf16, LPR = d/8 lanes x 16 B; fp32 arithmetic.
+// Same workspace / reduce kernel / coefficients as the fp32 path.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void ld8(const uint16_t* base, int64_t row, int64_t ld, int q, float* o) {
+  fr_unpack8(reinterpret_cast<const uint4*>(base + row * ld)[q], o);
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void bpr16_scores_kernel(
+    const uint16_t* __restrict__ U, int64_t ldu, const uint16_t* __restrict__ I, int64_t ldi,
+    const uint16_t* __restrict__ Ue, int64_t ldue, const uint16_t* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d8, BprWS ws) {
+  constexpr int GPB = 256 / L;
+  const int q0 = threadIdx.x % L;
+  for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / L; b < B; b += (int64_t)gridDim.x * GPB) {
+    const int64_t u = uu[b], p = pp[b], n = nn[b];
+    float sp = 0.f, sn = 0.f, a = 0.f, c = 0.f, e = 0.f;
+    for (int q = q0; q < d8; q += L) {
+      float xu[8], xp[8], xn[8];
+      ld8(U, u, ldu, q, xu);
+      ld8(I, p, ldi, q, xp);
+      ld8(I, n, ldi, q, xn);
+      sp += fr_dot8(xu, xp);
+      sn += fr_dot8(xu, xn);
+      if (Ue) {
+        ld8(Ue, u, ldue, q, xu);
+        ld8(Ie, p, ldie, q, xp);
+        ld8(Ie, n, ldie, q, xn);
+        a += fr_dot8(xu, xu);
+        c += fr_dot8(xp, xp);
+        e += fr_dot8(xn, xn);
+      }
+    }
+    sp = group_sum<L>(sp);
+    sn = group_sum<L>(sn);
+    a = group_sum<L>(a);
+    c = group_sum<L>(c);
+    e = group_sum<L>(e);
+    if (q0 == 0) {
+      ws.spos[b] = sp;
+      ws.sneg[b] = sn;
+      ws.squ[b] = a;
+      ws.sqp[b] = c;
+      ws.sqn[b] = e;
+    }
+  }
+}
+
+__device__ __forceinline__ void rmw_add8(uint16_t* base, int64_t row, int64_t ld, int q, const float* g) {
+  uint4* o = reinterpret_cast<uint4*>(base + row * ld) + q;
+  float cur[8];
+  fr_unpack8(*o, cur);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cur[j] += g[j];
+  *o = fr_pack8(cur);
+}
+
+// Deterministic owner-slot scatter (as bpr_bwd_det_kernel): every destination row is summed in
+// fp32 by its first slot and added to the bf16 gradient table once (one rounding per row).
+template <int L>
+__global__ __launch_bounds__(256) void bpr16_bwd_det_kernel(
+    const uint16_t* __restrict__ U, int64_t ldu, const uint16_t* __restrict__ I, int64_t ldi,
+    const uint16_t* __restrict__ Ue, int64_t ldue, const uint16_t* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d8, float gamma, float gmf, float greg, const float* gscale, uint16_t* dU,
+    uint16_t* dI, uint16_t* dUe, uint16_t* dIe, BprWS ws) {
+  constexpr int GPB = 256 / L;
+  const int q0 = threadIdx.x % L;
+  if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  for (int64_t s = (int64_t)blockIdx.x * GPB + threadIdx.x / L; s < 3 * B; s += (int64_t)gridDim.x * GPB) {
+    const bool is_user = s < B;
+    const int64_t row = is_user ? uu[s] : (s < 2 * B ? pp[s - B] : nn[s - 2 * B]);
+    bool earlier = false;
+    if (is_user) {
+      for (int64_t t = q0; t < s; t += L) earlier |= (uu[t] == row);
+    } else {
+      for (int64_t t = B + q0; t < s; t += L) earlier |= ((t < 2 * B ? pp[t - B] : nn[t - 2 * B]) == row);
+    }
+    int e = earlier ? 1 : 0;
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) e |= __shfl_xor(e, off, L);
+    if (e) continue;
+    for (int q = q0; q < d8; q += L) {
+      float g8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, x[8], y[8];
+      if (is_user) {
+        int cnt = 0;
+        for (int64_t t = 0; t < B; ++t) {
+          if (uu[t] != row) continue;
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          ld8(I, pp[t], ldi, q, x);
+          ld8(I, nn[t], ldi, q, y);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g8[j] += g * x[j] + (-g) * y[j];
+          ++cnt;
+        }
+        if (dU) rmw_add8(dU, row, ldu, q, g8);
+        if (Ue && dUe) {
+          ld8(Ue, row, ldue, q, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            for (int k = 0; k < cnt; ++k) r8[j] += ru * x[j];
+          rmw_add8(dUe, row, ldue, q, r8);
+        }
+      } else {
+        int cp = 0, cn = 0;
+        for (int64_t t = 0; t < B; ++t) {
+          const bool mp = pp[t] == row, mn = nn[t] == row;
+          if (!mp && !mn) continue;
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          ld8(U, uu[t], ldu, q, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g8[j] += (mp ? g * x[j] : 0.f) + (mn ? -g * x[j] : 0.f);
+          cp += mp;
+          cn += mn;
+        }
+        if (dI) rmw_add8(dI, row, ldi, q, g8);
+        if (Ie && dIe) {
+          ld8(Ie, row, ldie, q, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float a = 0.f, b = 0.f;
+            for (int k = 0; k < cp; ++k) a += rp * x[j];
+            for (int k = 0; k < cn; ++k) b += rn * x[j];
+            r8[j] = a + b;
+          }
+          rmw_add8(dIe, row, ldie, q, r8);
+        }
+      }
+    }
+  }
+}
 }  // namespace
 
 extern "C" int64_t fr_bpr_workspace(int64_t B) { return B > 0 ? bpr_ws_bytes(B) : 0; }
@@ -308,6 +448,77 @@ extern "C" int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64
                        ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
                        ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
   }
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+// ---- bf16 entry points -----------------------------------------------------------------------
+static int bpr16_check(const uint16_t* U, int64_t ldu, const uint16_t* I, int64_t ldi, const uint16_t* Ue,
+                       int64_t ldue, const uint16_t* Ie, int64_t ldie, const int64_t* u, const int64_t* p,
+                       const int64_t* n, int64_t B, int d, void* ws, int64_t wsb) {
+  FR_REQUIRE(B >= 1, "B must be >= 1");
+  FR_REQUIRE(d >= 8 && d % 8 == 0, "d must be a positive multiple of 8");
+  FR_REQUIRE(U && I && u && p && n, "null table/index");
+  auto ok = [d](const uint16_t* t, int64_t ld) { return fr::aligned16(t) && ld % 8 == 0 && ld >= d; };
+  FR_REQUIRE(ok(U, ldu) && ok(I, ldi), "U/I must be 16-B aligned with ld % 8 == 0");
+  FR_REQUIRE((Ue == nullptr) == (Ie == nullptr), "Ue and Ie must both be given or both null");
+  FR_REQUIRE(!Ue || (ok(Ue, ldue) && ok(Ie, ldie)), "Ue/Ie must be 16-B aligned with ld % 8 == 0");
+  FR_REQUIRE(ws && wsb >= bpr_ws_bytes(B) && fr::aligned16(ws), "workspace too small");
+  return FR_OK;
+}
+
+template <class F>
+static void bpr16_dispatch(int d8, F&& f) {
+  if (d8 >= 32) f(std::integral_constant<int, 32>{});
+  else if (d8 >= 16) f(std::integral_constant<int, 16>{});
+  else if (d8 >= 8) f(std::integral_constant<int, 8>{});
+  else if (d8 >= 4) f(std::integral_constant<int, 4>{});
+  else if (d8 >= 2) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 1>{});
+}
+
+extern "C" int fr_bpr_fwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t* d_I, int64_t ldi,
+                               const uint16_t* d_Ue, int64_t ldue, const uint16_t* d_Ie, int64_t ldie,
+                               const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                               float gamma, float* d_out, void* d_workspace, int64_t workspace_bytes,
+                               void* stream) {
+  int rc = bpr16_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
+                       workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_out, "out null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  BprWS w = bpr_ws(d_workspace, B);
+  bpr16_dispatch(d / 8, [&](auto L) {
+    constexpr int LL = decltype(L)::value;
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LL), 4096);
+    hipLaunchKernelGGL(bpr16_scores_kernel<LL>, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue, ldue,
+                       d_Ie, ldie, d_u, d_p, d_n, B, d / 8, w);
+  });
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w, d_out);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_bpr_bwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t* d_I, int64_t ldi,
+                               const uint16_t* d_Ue, int64_t ldue, const uint16_t* d_Ie, int64_t ldie,
+                               const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                               float gamma, float g_mf, float g_reg, const float* d_gscale, uint16_t* d_dU,
+                               uint16_t* d_dI, uint16_t* d_dUe, uint16_t* d_dIe, void* d_workspace,
+                               int64_t workspace_bytes, void* stream) {
+  int rc = bpr16_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
+                       workspace_bytes);
+  if (rc) return rc;
+  for (const uint16_t* g : {d_dU, d_dI, d_dUe, d_dIe}) FR_REQUIRE(!g || fr::aligned16(g), "grad unaligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  BprWS w = bpr_ws(d_workspace, B);
+  bpr16_dispatch(d / 8, [&](auto L) {
+    constexpr int LL = decltype(L)::value;
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(3 * B, 256 / LL), 4096);
+    hipLaunchKernelGGL(bpr16_bwd_det_kernel<LL>, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue, ldue,
+                       d_Ie, ldie, d_u, d_p, d_n, B, d / 8, gamma, g_mf, g_reg, d_gscale, d_dU, d_dI, d_dUe,
+                       d_dIe, w);
+  });
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -129,3 +129,35 @@ def bpr_step_reference(U_all, I_all, U_ego, I_ego, user, pos, neg, reg_weight, g
     mf = bpr_loss((u * p).sum(1), (u * n).sum(1), gamma)
     reg = reg_weight * emb_loss(U_ego[user], I_ego[pos], I_ego[neg])
     return mf, reg
+
+
+# ----------------------------------------------------------------------------- full-sort top-k
+def full_sort_topk(U: np.ndarray, I: np.ndarray, k: int, exclude=None, held_out=None):
+    """Full-sort ranking of every item for each user row of U.
+
+    Restates Trainer.evaluate (common/trainer.py:476-503): scores = full_sort_predict (the dense
+    user @ item.T of common/abstract_recommender.py:39-50), torch.topk(scores, max(topk)); with
+    the MMRec history mask (scores of ``exclude[u]`` items set to -inf before the top-k) when
+    ``exclude`` is given; hits = ``i in pos_items`` of TopKEvaluator.evaluate
+    (utils/topk_evaluator.py:104-107) against ``held_out[u]``.  Scores in float64 on the given
+    values; ties ordered by item id (a stable descending sort: torch.topk leaves tie order
+    unspecified).  Returns (scores [n,k] f64, items [n,k] int64, hits [n,k] bool or None).
+    """
+    S = np.asarray(U, np.float64) @ np.asarray(I, np.float64).T
+    n = S.shape[0]
+    if exclude is not None:
+        for u in range(n):
+            ex = np.asarray(list(exclude[u]), np.int64)
+            if ex.size:
+                S[u, ex] = -np.inf
+    order = np.argsort(-S, axis=1, kind="stable")[:, :k]
+    scores = np.take_along_axis(S, order, 1)
+    hits = None
+    if held_out is not None:
+        hits = np.array([[i in set(held_out[u]) for i in order[u]] for u in range(n)], dtype=bool)
+    return scores, order.astype(np.int64), hits
+
+
+def bf16_round(x) -> np.ndarray:
+    """float32 values rounded to bfloat16 (round to nearest even), returned as float32."""
+    return torch.as_tensor(np.asarray(x, np.float32)).to(torch.bfloat16).float().numpy()
