@@ -1,4 +1,4 @@
-// Full-sort top-k: user x item scores on the matrix cores, fused with a running per-user top-k.
+// Full-sort top-k: user x item scores on the matrix cores, fused with the top-k selection.
 //
 // Replaces, for a batch of users, full_sort_predict's  scores = user_all[u] @ item_all.T
 // (common/abstract_recommender.py:39-50, the MMRec dense form) followed by
@@ -8,22 +8,31 @@
 // TopKEvaluator.evaluate (topk_evaluator.py:104-107).  The [users x items] score matrix is never
 // written: at 32k users x 1M items it would be 128 GB of fp32.
 //
-// Score kernel (per workgroup: 8 waves x 32 users = 256 users, an item range of the split):
-//   * MFMA with A = a 32-item tile (from LDS) and B = the wave's 32 users (held in VGPRs for the
-//     whole kernel): bf16 tables -> v_mfma_f32_32x32x16_bf16 (K = 16 per instruction, fp32
-//     accumulate); fp32 tables -> v_mfma_f32_32x32x2_f32 (exact fp32 products, K = 2).
-//   * the 32x32 accumulator has the user on the lane (col = lane & 31) and 16 items in the
-//     registers, so each lane filters its own user's scores against that user's current k-th
-//     best (a register), and only candidates touch the user's sorted top-k list in LDS.
-//   * item tiles are staged global -> registers -> LDS (double buffer, one barrier per tile) with
-//     a 16-B chunk XOR swizzle so the A-fragment ds_read_b128 of 16 lanes hits 16 distinct bank
-//     slots; item rows are read once per workgroup (256 users), users once per kernel.
-//   * order is total and deterministic: score descending, item id ascending on ties (the order
-//     of a stable descending argsort), independent of tiling and split count.
-//   * XCD-aware block order: the workgroups of one XCD take consecutive (user tile, split)
-//     ids, so the user tiles sharing an item range share that XCD's L2.
-// Merge kernel: one wave per user merges the splits' sorted lists (k rounds of a wave arg-max)
-// and flags hits against the user's held-out items.
+// GEMM (every kernel below): a workgroup = 8 waves x 32 users = 256 users x an item range (split).
+//   * MFMA with A = a 32-item tile (LDS) and B = the wave's 32 users (VGPRs for the whole kernel):
+//     bf16 tables -> v_mfma_f32_32x32x16_bf16 (fp32 accumulate); fp32 tables ->
+//     v_mfma_f32_32x32x2_f32 (exact fp32 products).  The 32x32 accumulator has the user on the
+//     lane (col = lane & 31) and 16 items in registers, so selection is lane-local.
+//   * item tiles: global -> registers (one tile ahead) -> LDS (double buffer) with a 16-B chunk
+//     XOR swizzle (conflict-free ds_read_b128 A fragments); item rows read once per workgroup.
+//   * XCD-aware block order: workgroups of one XCD take consecutive (user tile, split) ids, so
+//     the user tiles sharing an item range share that XCD's L2.
+// Selection, for large item counts, in three launches (exact for any data):
+//   1. LIST kernel on a strided item sample (every s-th item, s <= 64): exact per-user top-k of
+//      the sample -> the user's threshold T_u = its k-th best admissible sample score, a lower
+//      bound of the k-th best over all items.
+//   2. APPEND kernel over all items: the GEMM plus a compare against T_u; the few scores >= T_u
+//      (expected ~k*s per user) are appended to per-(user, split, lane-half) regions.
+//   3. MERGE: per user, the top-k of its admissible candidates by (score desc, item id asc); the
+//      exclusion (history mask) is tested here, once per candidate, off the GEMM's path.
+//   A region that overflows its capacity (adversarial score orders) flags its user; flagged users
+//   are recomputed by the LIST kernel over all items and merged again (launches that exit at once
+//   when nothing is flagged), so the result never depends on the data's order.
+// LIST kernel: each lane keeps a PRIVATE sorted top-k (64-bit keys in registers) of the items it
+// sees, updated by bubble passes in which every lane with a candidate inserts at once.  Small
+// item counts use it directly (one pass + merge).
+// Order is total and deterministic: score descending, item id ascending on ties (the order of a
+// stable descending argsort), independent of tiling, splits and sampling.
 #include "fr_bf16.h"
 
 #include <algorithm>
@@ -33,6 +42,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * 64;
@@ -40,17 +50,18 @@ constexpr int kUsersPerWG = kWaves * 32;
 constexpr int kTile = 32;      // items per staged tile
 constexpr int kKMax = 32;      // largest k
 
-template <typename T, int D>
+template <typename T, int D, int NB = 1>
 struct Cfg {
   static constexpr int RB = D * (int)sizeof(T);           // bytes per row
   static constexpr int CPR = RB / 16;                       // 16-B chunks per row
   static constexpr bool BF = sizeof(T) == 2;
   static constexpr int KS = BF ? D / 16 : D / 2;            // MFMA k-steps
-  static constexpr int STAGE = kTile * RB;                  // bytes per staged tile
+  static constexpr int TILE = kTile * NB;                   // items per staged tile (NB 32-item blocks)
+  static constexpr int STAGE = TILE * RB;                   // bytes per staged tile
   static constexpr int G = CPR >= 16 ? 1 : 16 / CPR;        // rows sharing one 256-B bank row
   static constexpr int SWM = (CPR >= 16 ? 16 : CPR) - 1;
-  static constexpr int CH = (kTile * CPR + kThreads - 1) / kThreads;  // staged chunks per thread
-  static constexpr int LDS = 2 * STAGE + kUsersPerWG * kKMax * 8;
+  static constexpr int CH = (TILE * CPR + kThreads - 1) / kThreads;  // staged chunks per thread
+  static constexpr int LDS = 2 * STAGE;
 };
 
 template <typename T, int D>
@@ -59,251 +70,515 @@ __device__ __forceinline__ int swz(int r, int c) {
   return c ^ ((r / C::G) & C::SWM);
 }
 
-__device__ __forceinline__ bool better(float s, int i, float t, int ti) {
-  return s > t || (s == t && i < ti);
+// Entries are ordered by the 64-bit key (ordered score bits << 32 | ~item): higher score first,
+// lower item id first on ties.
+// fp32 -> uint32 preserving order (larger float -> larger uint; -0 < +0, NaN above +inf)
+__device__ __forceinline__ uint32_t fr_ord(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fr_unord(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-__device__ __forceinline__ bool excluded(const int64_t* __restrict__ ex_ptr, const int32_t* __restrict__ ex_col,
-                                         int64_t ex_base, int64_t urow, int64_t item) {
-  if (!ex_ptr) return false;
-  int64_t lo = ex_ptr[urow], hi = ex_ptr[urow + 1];
-  const int64_t key = ex_base + item;
+// byte offset, in a staged tile, of lane (r, h)'s A fragment for k-step s (bf16: chunk 2s+h;
+// fp32: 4 k-steps per chunk, lane half h holds the upper half of k)
+template <typename T, int D>
+__device__ __forceinline__ int a_off(int r, int h, int s) {
+  using C = Cfg<T, D>;
+  return (r * C::CPR + swz<T, D>(r, C::BF ? 2 * s + h : h * (C::CPR / 2) + s)) * 16;
+}
+
+__device__ __forceinline__ bool in_csr_row(const int32_t* __restrict__ col, int64_t lo, int64_t hi, int64_t key) {
+  const int64_t end = hi;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    const int64_t v = ex_col[mid];
-    if (v < key) lo = mid + 1;
+    if ((int64_t)col[mid] < key) lo = mid + 1;
     else hi = mid;
   }
-  return lo < ex_ptr[urow + 1] && (int64_t)ex_col[lo] == key;
+  return lo < end && (int64_t)col[lo] == key;
 }
 
-template <typename T, int D>
-__global__ __launch_bounds__(kThreads) void topk_score_kernel(
-    const T* __restrict__ Uq, int64_t ldu, int64_t n_users, const T* __restrict__ It, int64_t ldi,
-    int64_t n_items, const int64_t* __restrict__ uid, const int64_t* __restrict__ ex_ptr,
-    const int32_t* __restrict__ ex_col, int64_t ex_base, int k, int n_splits, int64_t span, int n_utiles,
-    float* __restrict__ out_s, int32_t* __restrict__ out_i) {
-  using C = Cfg<T, D>;
+__device__ __forceinline__ uint32_t bloom_hash(int64_t key) { return ((uint32_t)key * 0x9E3779B1u) >> 25; }
+
+// Per-lane exclusion test: a 128-bit Bloom signature of the user's row (registers) screens every
+// candidate; only signature hits (the row's items + ~15% false positives) bisect the CSR row.
+struct Excl {
+  uint32_t w0, w1, w2, w3;
+  int64_t lo, hi, base;
+  const int32_t* col;
+  __device__ void init(const int64_t* __restrict__ ptr, const int32_t* __restrict__ c, int64_t b, int64_t row) {
+    w0 = w1 = w2 = w3 = 0u;
+    col = c;
+    base = b;
+    lo = hi = 0;
+    if (!ptr) return;
+    lo = ptr[row];
+    hi = ptr[row + 1];
+    for (int64_t e = lo; e < hi; ++e) {
+      const uint32_t hsh = bloom_hash(c[e]);
+      const uint32_t bit = 1u << (hsh & 31u);
+      const uint32_t w = hsh >> 5;
+      w0 |= w == 0 ? bit : 0u;
+      w1 |= w == 1 ? bit : 0u;
+      w2 |= w == 2 ? bit : 0u;
+      w3 |= w == 3 ? bit : 0u;
+    }
+  }
+  __device__ __forceinline__ bool test(int64_t item) const {
+    if (lo == hi) return false;
+    const int64_t key = base + item;
+    const uint32_t hsh = bloom_hash(key);
+    const uint32_t w = hsh >> 5;
+    const uint32_t word = w == 0 ? w0 : (w == 1 ? w1 : (w == 2 ? w2 : w3));
+    if (!((word >> (hsh & 31u)) & 1u)) return false;
+    return in_csr_row(col, lo, hi, key);
+  }
+};
+
+struct ScoreArgs {
+  const void* Uq; int64_t ldu; int64_t n_users; const int32_t* urows; const int32_t* d_nu;
+  const void* It; int64_t ldi; int64_t n_items; int64_t item_mul;   // tile item i = item id i * item_mul
+  const int64_t* uid; const int64_t* ex_ptr; const int32_t* ex_col; int64_t ex_base;
+  int k; int n_splits; int64_t span; int n_utiles;
+  float* ls; int32_t* li;                                           // LIST: [slot][split][half][k]
+  const float* thr; int cap; float* cs; int32_t* ci; int32_t* cc;   // APPEND: [slot][split][half][cap], counts
+};
+
+enum { kList = 0, kAppend = 1 };
+
+template <typename T, int D, int KC, int MODE, int NB>
+__global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
+  using C = Cfg<T, D, NB>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
-  float* tks = reinterpret_cast<float*>(smem + 2 * C::STAGE);
-  int* tki = reinterpret_cast<int*>(tks + kUsersPerWG * kKMax);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int64_t n_users = a.d_nu ? (int64_t)*a.d_nu : a.n_users;
 
   // XCD-aware bijective remap (blocks are dispatched round-robin over the 8 XCDs)
-  const int total = n_utiles * n_splits;
+  const int total = a.n_utiles * a.n_splits;
   const int b = blockIdx.x, xcd = b & 7, q8 = total >> 3, r8 = total & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int ut = wg % n_utiles, sp = wg / n_utiles;
+  const int ut = wg % a.n_utiles, sp = wg / a.n_utiles;
+  if ((int64_t)ut * kUsersPerWG >= n_users) return;  // whole workgroup idle (device-sized grids)
 
-  const int64_t myu = (int64_t)ut * kUsersPerWG + wave * 32 + r;
-  const bool uvalid = myu < n_users;
-  const int64_t urow = uvalid ? myu : 0;
-  const int64_t exrow = uid ? uid[urow] : urow;
-  const int64_t i_lo = (int64_t)sp * span;
-  const int64_t i_hi = min(n_items, i_lo + span);
-  const int n_tiles = (int)((i_hi - i_lo + kTile - 1) / kTile);
+  const int64_t slot = (int64_t)ut * kUsersPerWG + wave * 32 + r;
+  const bool uvalid = slot < n_users;
+  const int64_t urow = uvalid ? (a.urows ? (int64_t)a.urows[slot] : slot) : 0;
+  const int64_t i_lo = (int64_t)sp * a.span;
+  const int64_t i_hi = min(a.n_items, i_lo + a.span);
+  const int n_tiles = (int)((i_hi - i_lo + C::TILE - 1) / C::TILE);
+  const T* __restrict__ It = reinterpret_cast<const T*>(a.It);
+  const int64_t ldi = a.ldi;
+
+  // exclusion: tested at insertion by the LIST kernel; the APPEND kernel leaves it to the merge
+  Excl ex;
+  ex.init(MODE == kList ? a.ex_ptr : nullptr, a.ex_col, a.ex_base, a.uid ? a.uid[urow] : urow);
 
   // B operand: this lane's user, held for the whole kernel
   typedef typename std::conditional<C::BF, bf16x8, float4>::type BFrag;
-  constexpr int NB = C::BF ? C::KS : C::KS / 4;
-  BFrag bf[NB];
+  constexpr int NBF = C::BF ? C::KS : C::KS / 4;
+  BFrag bf[NBF];
 #pragma unroll
-  for (int s = 0; s < NB; ++s) {
+  for (int s = 0; s < NBF; ++s) {
     if constexpr (C::BF) {
-      bf[s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(Uq) + urow * ldu + 16 * s + 8 * h);
+      bf[s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(a.Uq) + urow * a.ldu + 16 * s + 8 * h);
     } else {
-      bf[s] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Uq) + urow * ldu + h * (D / 2) + 4 * s);
+      bf[s] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.Uq) + urow * a.ldu + h * (D / 2) + 4 * s);
     }
   }
+  // make the compiler itself retire these loads here (an asm that reads them), so its counted
+  // waits inside the tile loop only ever cover the item-tile prefetch
+#pragma unroll
+  for (int s = 0; s < NBF; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[s])));
+  // APPEND: this user's threshold and this lane's region
+  const float thr_u = MODE == kAppend && uvalid ? a.thr[slot] : -INFINITY;
+  const int64_t region = (slot * a.n_splits + sp) * 2 + h;
+  int cnt = 0;
 
-  // top-k list of this lane's user (both lane halves initialise half of it)
-  const int lbase = (wave * 32 + r) * kKMax;
-  for (int j = h; j < kKMax; j += 2) {
-    tks[lbase + j] = -INFINITY;
-    tki[lbase + j] = INT32_MAX;
+  // the B-fragment / exclusion-row / threshold loads retire here, so the loop's counted waits
+  // only ever cover the item-tile prefetch
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // LIST: lane-private list of KC 64-bit keys (ordered score bits << 32 | ~item: larger key =
+  // better entry; keys are unique since item ids differ), sorted descending.  The first KC - k
+  // entries are sentinels (~0, above every real key), so the k live entries are
+  // key[KC-k .. KC-1]; empty live entries hold 0.
+  uint64_t key[KC];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) key[q] = q < KC - a.k ? ~0ull : 0ull;
+
+  // item tiles: global -> registers (one tile ahead) -> LDS (double buffer, swizzled chunks).
+  // APPEND keeps each staged chunk's row, LDS offset and global source (advanced one tile of rows
+  // per step) in registers; the register-heavy LIST kernel recomputes them per tile.
+  constexpr int NSH = MODE == kAppend ? C::CH : 1;
+  int srow[NSH], sdst[NSH];
+  const char* ssrc[NSH];
+#pragma unroll
+  for (int c = 0; c < NSH; ++c) {
+    const int x = tid + c * kThreads;
+    const int row = x / C::CPR, cc = x % C::CPR;
+    srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;  // rows past the tile never load
+    sdst[c] = (row * C::CPR + swz<T, D>(row, cc)) * 16;
+    ssrc[c] = reinterpret_cast<const char*>(It) + ((i_lo + row) * ldi) * (int64_t)sizeof(T) + cc * 16;
   }
-  float thr = -INFINITY;
-  int thr_i = INT32_MAX;
+  const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
+#define FR_LOAD_TILE(T_)                                                                            \
+  _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
+    if constexpr (MODE == kAppend) {                                                                \
+      const int64_t item = i_lo + (int64_t)(T_) * C::TILE + srow[c];                                \
+      stg[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)(T_) * tile_bytes)  \
+                           : make_uint4(0, 0, 0, 0);                                                \
+    } else {                                                                                        \
+      const int x = tid + c * kThreads;                                                             \
+      stg[c] = make_uint4(0, 0, 0, 0);                                                              \
+      if (x < C::TILE * C::CPR) {                                                                   \
+        const int row = x / C::CPR, cc = x % C::CPR;                                                \
+        const int64_t item = i_lo + (int64_t)(T_) * C::TILE + row;                                  \
+        if (item < i_hi)                                                                            \
+          stg[c] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(It) +              \
+                                                   (item * ldi) * (int64_t)sizeof(T) + cc * 16);    \
+      }                                                                                             \
+    }                                                                                               \
+  }
+#define FR_STORE_TILE(BUF_)                                                                         \
+  _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
+    if constexpr (MODE == kAppend) {                                                                \
+      if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + sdst[c]) = stg[c]; \
+    } else {                                                                                        \
+      const int x = tid + c * kThreads;                                                             \
+      if (x < C::TILE * C::CPR) {                                                                   \
+        const int row = x / C::CPR, cc = x % C::CPR;                                                \
+        *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + (row * C::CPR + swz<T, D>(row, cc)) * 16) = stg[c]; \
+      }                                                                                             \
+    }                                                                                               \
+  }
+  // A-fragment LDS offsets of this lane (row r of each 32-item block, chunk 2s+h): held in
+  // registers by the APPEND kernel, recomputed per use by the register-heavy LIST kernel
+  constexpr int NA = C::BF ? C::KS : C::KS / 4;
+  constexpr int NAH = MODE == kAppend ? NA : 1;
+  int aoff[NAH];
+#pragma unroll
+  for (int s = 0; s < NAH; ++s) aoff[s] = a_off<T, D>(r, h, s);
+#define FR_AOFF(S_) (MODE == kAppend ? aoff[(MODE == kAppend) ? (S_) : 0] : a_off<T, D>(r, h, (S_)))
 
   uint4 stg[C::CH];
-  auto load_tile = [&](int t) {
-#pragma unroll
-    for (int c = 0; c < C::CH; ++c) {
-      const int x = tid + c * kThreads;
-      stg[c] = make_uint4(0, 0, 0, 0);
-      if (x < kTile * C::CPR) {
-        const int row = x / C::CPR, cc = x % C::CPR;
-        const int64_t item = i_lo + (int64_t)t * kTile + row;
-        if (item < i_hi)
-          stg[c] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(It) + (item * ldi) * (int64_t)sizeof(T) +
-                                                   cc * 16);
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* base = smem + buf * C::STAGE;
-#pragma unroll
-    for (int c = 0; c < C::CH; ++c) {
-      const int x = tid + c * kThreads;
-      if (x < kTile * C::CPR) {
-        const int row = x / C::CPR, cc = x % C::CPR;
-        *reinterpret_cast<uint4*>(base + (row * C::CPR + swz<T, D>(row, cc)) * 16) = stg[c];
-      }
-    }
-  };
-
   if (n_tiles > 0) {
-    load_tile(0);
-    store_tile(0);
+    FR_LOAD_TILE(0)
+    FR_STORE_TILE(0)
   }
   __syncthreads();
-  if (n_tiles > 1) load_tile(1);
-
+  if (n_tiles > 1) { FR_LOAD_TILE(1) }
   for (int t = 0; t < n_tiles; ++t) {
+    // ---- scores of this tile on the matrix cores (NB independent 32-item blocks)
     const char* abuf = smem + (t & 1) * C::STAGE;
-    f32x16 acc;
+    f32x16 acc[NB];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
     if constexpr (C::BF) {
+      // the tile's A fragments are read ahead of the MFMA chains that consume them in order
+      bf16x8 af[NB][C::KS];
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(abuf + (r * C::CPR + swz<T, D>(r, 2 * s + h)) * 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bf[s], acc, 0, 0, 0);
+      for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+          af[bb][s] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + FR_AOFF(s));
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[s], acc[bb], 0, 0, 0);
+      // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight)
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int s = 0; s < NB * C::KS - 4; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     } else {
 #pragma unroll
       for (int sg = 0; sg < C::KS / 4; ++sg) {
-        const float4 a = *reinterpret_cast<const float4*>(abuf + (r * C::CPR + swz<T, D>(r, h * (C::CPR / 2) + sg)) * 16);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bf[sg].x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bf[sg].y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bf[sg].z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bf[sg].w, acc, 0, 0, 0);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+          const float4 af = *reinterpret_cast<const float4*>(abuf + bb * 32 * C::RB + FR_AOFF(sg));
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, bf[sg].x, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, bf[sg].y, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, bf[sg].z, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[sg].w, acc[bb], 0, 0, 0);
+        }
       }
     }
-    // this lane's 16 scores: user myu, items ib + (j&3) + 8(j>>2) + 4h
-    const int64_t ib = i_lo + (int64_t)t * kTile + 4 * h;
-    bool cand = false;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t item = ib + (j & 3) + 8 * (j >> 2);
-      cand |= (item < i_hi) && better(acc[j], (int)item, thr, thr_i);
-    }
-    cand = cand && uvalid;
-    if (__ballot(cand)) {
-      for (int hh = 0; hh < 2; ++hh) {
-        if (cand && h == hh) {
+    for (int bb = 0; bb < NB; ++bb) {
+      // ---- this lane's 16 scores of block bb: user `slot`, items ib + (j&3) + 8(j>>2) + 4h
+      const int64_t ib = i_lo + (int64_t)t * C::TILE + bb * 32 + 4 * h;
+      float wf;
+      if constexpr (MODE == kList) {
+        const uint32_t wsc = (uint32_t)(key[KC - 1] >> 32);
+        wf = wsc < 0x00800000u ? -INFINITY : fr_unord(wsc);  // the list's worst score (empty: -inf)
+      } else {
+        wf = thr_u;
+      }
+      const f32x16 av = acc[bb];
+      uint32_t mask = 0u;
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int64_t item = ib + (j & 3) + 8 * (j >> 2);
-            const float s = acc[j];
-            if (item < i_hi && better(s, (int)item, thr, thr_i) && !excluded(ex_ptr, ex_col, ex_base, exrow, item)) {
-              int pos = k - 1;
-              while (pos > 0) {
-                const float ps = tks[lbase + pos - 1];
-                const int pi = tki[lbase + pos - 1];
-                if (better(ps, pi, s, (int)item)) break;
-                tks[lbase + pos] = ps;
-                tki[lbase + pos] = pi;
-                --pos;
-              }
-              tks[lbase + pos] = s;
-              tki[lbase + pos] = (int)item;
-              thr = tks[lbase + k - 1];
-              thr_i = tki[lbase + k - 1];
+      for (int j = 0; j < 16; ++j) mask |= av[j] >= wf ? (1u << j) : 0u;
+      if (ib + 28 >= i_hi) {  // the split's last block: drop items past its end
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
+      }
+      if (!uvalid) mask = 0u;
+      // every lane handles its next candidate in the same pass
+      while (__ballot(mask != 0u)) {
+        const bool act = mask != 0u;
+        const int j = act ? __builtin_ctz(mask) : 0;
+        mask &= mask - 1u;
+        const float v0 = (j & 1) ? av[1] : av[0], v1 = (j & 1) ? av[3] : av[2];
+        const float v2 = (j & 1) ? av[5] : av[4], v3 = (j & 1) ? av[7] : av[6];
+        const float v4 = (j & 1) ? av[9] : av[8], v5 = (j & 1) ? av[11] : av[10];
+        const float v6 = (j & 1) ? av[13] : av[12], v7 = (j & 1) ? av[15] : av[14];
+        const float w0 = (j & 2) ? v1 : v0, w1 = (j & 2) ? v3 : v2, w2 = (j & 2) ? v5 : v4, w3 = (j & 2) ? v7 : v6;
+        const float x0 = (j & 4) ? w1 : w0, x1 = (j & 4) ? w3 : w2;
+        const float sc = (j & 8) ? x1 : x0;
+        const int64_t item = (ib + (j & 3) + 8 * (j >> 2)) * a.item_mul;
+        if constexpr (MODE == kList) {
+          const uint64_t kk = ((uint64_t)fr_ord(sc) << 32) | (uint32_t)(~(uint32_t)item);
+          if (act && kk > key[KC - 1] && !ex.test(item)) {
+            // one bubble pass: the new key sinks to its place, the old minimum falls off the end
+            uint64_t x = kk;
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+              const uint64_t cur = key[q];
+              const bool gt = x > cur;
+              key[q] = gt ? x : cur;
+              x = gt ? cur : x;
             }
           }
+        } else {
+          if (act) {
+            if (cnt < a.cap) {
+              a.cs[region * a.cap + cnt] = sc;
+              a.ci[region * a.cap + cnt] = (int32_t)item;
+            }
+            ++cnt;
+          }
         }
-        // the list is private to this wave: program order makes the other half see the inserts
-        thr = tks[lbase + k - 1];
-        thr_i = tki[lbase + k - 1];
       }
     }
-    if (t + 1 < n_tiles) store_tile((t + 1) & 1);
+    // ---- next tile into the other buffer; prefetch the one after
+    if (t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1) }
     __syncthreads();
-    if (t + 2 < n_tiles) load_tile(t + 2);
+    if (t + 2 < n_tiles) { FR_LOAD_TILE(t + 2) }
   }
+#undef FR_LOAD_TILE
+#undef FR_STORE_TILE
+#undef FR_AOFF
 
-  if (uvalid) {
-    const int64_t o = (myu * n_splits + sp) * (int64_t)k;
-    for (int j = h; j < k; j += 2) {
-      out_s[o + j] = tks[lbase + j];
-      out_i[o + j] = tki[lbase + j];
+  if (!uvalid) return;
+  if constexpr (MODE == kList) {
+    // list (slot, split, half): k unsorted entries, decoded back to (score, item)
+    const int64_t o = region * (int64_t)a.k - (KC - a.k);
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      if (q >= KC - a.k) {
+        const uint64_t kk = key[q];
+        const bool empty = kk < (1ull << 32);
+        a.ls[o + q] = empty ? -INFINITY : fr_unord((uint32_t)(kk >> 32));
+        a.li[o + q] = empty ? INT32_MAX : (int32_t)(~(uint32_t)kk);
+      }
     }
+  } else {
+    a.cc[region] = cnt;
   }
 }
 
-// One wave per user: k rounds of a wave arg-max over the heads of the n_splits sorted lists.
-__global__ __launch_bounds__(256) void topk_merge_kernel(
-    const float* __restrict__ ps, const int32_t* __restrict__ pi, int64_t n_users, int n_splits, int k,
-    const int64_t* __restrict__ uid, const int64_t* __restrict__ t_ptr, const int32_t* __restrict__ t_col,
-    int64_t t_base, float* __restrict__ out_s, int64_t* __restrict__ out_i, uint8_t* __restrict__ hits) {
+struct MergeArgs {
+  const float* ps; const int32_t* pi; const int32_t* cnt;   // regions (cnt null: every region holds k)
+  int cap; int n_regions;
+  int64_t n_users; const int32_t* d_nu; const int32_t* urows;  // slot -> output row
+  int k; const int64_t* uid; const int64_t* t_ptr; const int32_t* t_col; int64_t t_base;
+  float* out_s; int64_t* out_i; uint8_t* hits;
+  float* thr_out;                                              // write the k-th best score only
+  const int64_t* ex_ptr; const int32_t* ex_col; int64_t ex_base;  // exclusion applied here (APPEND input)
+  int32_t* flag_list; int32_t* flag_cnt;                      // overflowed users -> exact recompute
+};
+
+// One wave per user: each lane streams a strided share of the user's candidates (all regions)
+// into a private sorted register list (bubble insertion, as the LIST kernel), then k rounds of a
+// wave arg-max over the lanes' list heads emit the top-k in order (the winner lane pops its
+// head); finally the hit flags against the user's held-out CSR row.
+template <int KC>
+__global__ __launch_bounds__(256) void topk_merge_kernel(MergeArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t n_users = a.d_nu ? (int64_t)*a.d_nu : a.n_users;
   if (u >= n_users) return;
-  const int64_t base = u * n_splits * (int64_t)k;
-  int hp = 0;
-  for (int j = 0; j < k; ++j) {
-    float s = -INFINITY;
-    int i = INT32_MAX;
-    if (lane < n_splits && hp < k) {
-      s = ps[base + (int64_t)lane * k + hp];
-      i = pi[base + (int64_t)lane * k + hp];
+  const int64_t orow = a.urows ? (int64_t)a.urows[u] : u;
+  const int64_t base = u * (int64_t)a.n_regions * a.cap;
+  if (a.cnt) {
+    bool over = false;
+    for (int g = lane; g < a.n_regions; g += 64) over |= a.cnt[u * a.n_regions + g] > a.cap;
+    if (__ballot(over)) {
+      if (lane == 0) a.flag_list[atomicAdd(a.flag_cnt, 1)] = (int32_t)orow;
+      return;
     }
-    float bs = s;
-    int bi = i, bl = lane;
+  }
+  Excl ex;
+  ex.init(a.ex_ptr, a.ex_col, a.ex_base, a.uid ? a.uid[orow] : orow);
+  uint64_t key[KC];
+#pragma unroll
+  for (int q = 0; q < KC; ++q) key[q] = 0ull;
+  for (int g = 0; g < a.n_regions; ++g) {
+    const int c = a.cnt ? a.cnt[u * a.n_regions + g] : a.cap;
+    const int64_t rb = base + (int64_t)g * a.cap;
+    for (int e = lane; e < c; e += 64) {
+      const int i = a.pi[rb + e];
+      if (i == INT32_MAX) continue;
+      const uint64_t kk = ((uint64_t)fr_ord(a.ps[rb + e]) << 32) | (uint32_t)(~(uint32_t)i);
+      if (kk > key[KC - 1] && !ex.test(i)) {
+        uint64_t x = kk;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+          const uint64_t cur = key[q];
+          const bool gt = x > cur;
+          key[q] = gt ? x : cur;
+          x = gt ? cur : x;
+        }
+      }
+    }
+  }
+  for (int j = 0; j < a.k; ++j) {
+    uint64_t best = key[0];
+    int bl = lane;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-      const float os = __shfl_xor(bs, off, 64);
-      const int oi = __shfl_xor(bi, off, 64);
+      const uint64_t ob = __shfl_xor(best, off, 64);
       const int ol = __shfl_xor(bl, off, 64);
-      if (better(os, oi, bs, bi) || (os == bs && oi == bi && ol < bl)) {
-        bs = os;
-        bi = oi;
+      if (ob > best) {
+        best = ob;
         bl = ol;
       }
     }
-    if (lane == bl) ++hp;
+    if (lane == bl) {  // pop the head
+#pragma unroll
+      for (int q = 0; q < KC - 1; ++q) key[q] = key[q + 1];
+      key[KC - 1] = 0ull;
+    }
+    const bool valid = best != 0ull;
+    const float bs = valid ? fr_unord((uint32_t)(best >> 32)) : -INFINITY;
+    const int bi = valid ? (int)(~(uint32_t)best) : -1;
     if (lane == 0) {
-      const bool valid = bi != INT32_MAX;
-      out_s[u * k + j] = valid ? bs : -INFINITY;
-      out_i[u * k + j] = valid ? (int64_t)bi : -1;
-      if (hits) hits[u * k + j] = valid && excluded(t_ptr, t_col, t_base, uid ? uid[u] : u, bi) ? 1 : 0;
+      if (a.thr_out) {
+        if (j == a.k - 1) a.thr_out[orow] = bs;
+      } else {
+        a.out_s[orow * a.k + j] = bs;
+        a.out_i[orow * a.k + j] = (int64_t)bi;
+        if (a.hits) {
+          bool hit = false;
+          if (valid) {
+            const int64_t row = a.uid ? a.uid[orow] : orow;
+            hit = in_csr_row(a.t_col, a.t_ptr[row], a.t_ptr[row + 1], a.t_base + bi);
+          }
+          a.hits[orow * a.k + j] = hit ? 1 : 0;
+        }
+      }
     }
   }
 }
 
-template <typename T, int D>
-hipError_t launch_score(const void* Uq, int64_t ldu, int64_t n_users, const void* It, int64_t ldi, int64_t n_items,
-                        const int64_t* uid, const int64_t* ex_ptr, const int32_t* ex_col, int64_t ex_base, int k,
-                        int n_splits, int64_t span, float* ps, int32_t* pi, hipStream_t s) {
-  const int n_utiles = (int)fr::ceil_div(n_users, kUsersPerWG);
-  hipLaunchKernelGGL((topk_score_kernel<T, D>), dim3((unsigned)(n_utiles * n_splits)), dim3(kThreads), 0, s,
-                     reinterpret_cast<const T*>(Uq), ldu, n_users, reinterpret_cast<const T*>(It), ldi, n_items, uid,
-                     ex_ptr, ex_col, ex_base, k, n_splits, span, n_utiles, ps, pi);
+hipError_t launch_merge(const MergeArgs& m, unsigned blocks, hipStream_t s) {
+  auto kern = m.k <= 10 ? topk_merge_kernel<10> : (m.k <= 20 ? topk_merge_kernel<20> : topk_merge_kernel<32>);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, m);
   return hipGetLastError();
+}
+
+__global__ void topk_zero_kernel(int32_t* p) {
+  if (threadIdx.x == 0) p[0] = 0;
+}
+
+template <typename T, int D, int MODE>
+hipError_t launch_score_t(const ScoreArgs& a, hipStream_t s) {
+  void (*kern)(ScoreArgs);
+  if constexpr (MODE == kAppend) {
+    kern = topk_score_kernel<T, D, 1, kAppend, 2>;
+  } else {
+    kern = a.k <= 10 ? topk_score_kernel<T, D, 10, kList, 1>
+                     : (a.k <= 20 ? topk_score_kernel<T, D, 20, kList, 1> : topk_score_kernel<T, D, 32, kList, 1>);
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.n_utiles * a.n_splits)), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_score(int dtype, int d, const ScoreArgs& a, hipStream_t s) {
+  if (dtype == FR_BF16) {
+    if (d == 256) return launch_score_t<uint16_t, 256, MODE>(a, s);
+    if (d == 128) return launch_score_t<uint16_t, 128, MODE>(a, s);
+    return launch_score_t<uint16_t, 64, MODE>(a, s);
+  }
+  if (d == 128) return launch_score_t<float, 128, MODE>(a, s);
+  return launch_score_t<float, 64, MODE>(a, s);
 }
 
 void split_plan(int64_t n_users, int64_t n_items, int* n_splits, int64_t* span) {
   const int64_t n_utiles = fr::ceil_div(n_users, kUsersPerWG);
   int64_t ns = std::max<int64_t>(1, fr::ceil_div(2 * fr::kNumCU, n_utiles));
   ns = std::min<int64_t>(ns, 64);
-  ns = std::min<int64_t>(ns, std::max<int64_t>(1, n_items / (4 * kTile)));  // >= 4 tiles per split
-  int64_t sp = fr::align_up(fr::ceil_div(n_items, ns), kTile);
+  ns = std::min<int64_t>(ns, std::max<int64_t>(1, n_items / (8 * kTile)));  // >= 8 blocks per split
+  int64_t sp = fr::align_up(fr::ceil_div(n_items, ns), 2 * kTile);
   *span = sp;
   *n_splits = (int)fr::ceil_div(n_items, sp);
+}
+
+constexpr int64_t kSampledMinItems = 32768;  // below this: one exact LIST pass
+
+// The launch plan and the workspace carve-up (identical in the size query and the call).
+struct Plan {
+  bool sampled;
+  int64_t stride, n_sample;
+  int ns1, ns2, cap;
+  int64_t span1, span2;
+  int64_t off_l1, off_thr, off_cs, off_ci, off_cc, off_flag, off_l2, total;
+};
+
+Plan make_plan(int64_t n_users, int64_t n_items, int k) {
+  Plan p{};
+  p.sampled = n_items >= kSampledMinItems;
+  split_plan(n_users, n_items, &p.ns2, &p.span2);
+  auto take = [&](int64_t bytes) { const int64_t o = p.total; p.total += fr::align_up(bytes, 256); return o; };
+  if (!p.sampled) {
+    p.off_l1 = take(n_users * p.ns2 * 2 * (int64_t)k * 8);
+    return p;
+  }
+  p.stride = std::min<int64_t>(64, std::max<int64_t>(2, n_items / 4096));
+  p.n_sample = fr::ceil_div(n_items, p.stride);
+  split_plan(n_users, p.n_sample, &p.ns1, &p.span1);
+  // candidates per user ~ NegBinomial(k, 1/stride): mean k*stride, spread over 2*ns2 regions;
+  // room for ~4x the mean plus the long tail of small k (overflow only costs time: exact pass)
+  p.cap = (int)std::min<int64_t>(1 << 16, std::max<int64_t>(256, (4 * k + 32) * p.stride / (2 * p.ns2)));
+  p.off_l1 = take(n_users * p.ns1 * 2 * (int64_t)k * 8);
+  p.off_thr = take(n_users * 4);
+  const int64_t nreg = n_users * p.ns2 * 2;
+  p.off_cs = take(nreg * p.cap * 4);
+  p.off_ci = take(nreg * p.cap * 4);
+  p.off_cc = take(nreg * 4);
+  p.off_flag = take((n_users + 1) * 4);
+  p.off_l2 = take(n_users * p.ns2 * 2 * (int64_t)k * 8);
+  return p;
 }
 
 }  // namespace
 
 extern "C" int64_t fr_topk_workspace(int64_t n_users, int64_t n_items, int k) {
   if (n_users <= 0 || n_items <= 0 || k <= 0) return 0;
-  int ns;
-  int64_t span;
-  split_plan(n_users, n_items, &ns, &span);
-  return n_users * ns * (int64_t)k * 8 + 256;
+  return make_plan(n_users, n_items, k).total + 256;
 }
 
 extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_I, int64_t ldi,
@@ -315,11 +590,14 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   FR_REQUIRE(n_users >= 0 && n_items >= 0, "negative size");
   if (n_users == 0) return FR_OK;
   FR_REQUIRE(n_items > 0 && n_items < INT32_MAX, "n_items out of range");
+  FR_REQUIRE(n_users < INT32_MAX / 2, "n_users out of range");
   FR_REQUIRE(k >= 1 && k <= kKMax, "k must be in [1, 32]");
   FR_REQUIRE(d_U && d_I && d_out_scores && d_out_items, "null pointer");
   FR_REQUIRE(!d_ex_ptr || d_ex_col, "exclusion CSR incomplete");
   FR_REQUIRE(!d_hits || (d_test_ptr && d_test_col), "hits need the held-out CSR");
   FR_REQUIRE(dtype == FR_BF16 || dtype == FR_F32, "dtype must be FR_F32 or FR_BF16");
+  if (dtype == FR_BF16) FR_REQUIRE(d == 64 || d == 128 || d == 256, "bf16 supports d in {64, 128, 256}");
+  else FR_REQUIRE(d == 64 || d == 128, "fp32 supports d in {64, 128}");
   const int es = dtype == FR_BF16 ? 2 : 4;
   FR_REQUIRE(fr::aligned16(d_U) && fr::aligned16(d_I) && (ldu * es) % 16 == 0 && (ldi * es) % 16 == 0 &&
                  ldu >= d && ldi >= d,
@@ -327,26 +605,69 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   const int64_t need = fr_topk_workspace(n_users, n_items, k);
   FR_REQUIRE(d_workspace && workspace_bytes >= need && fr::aligned16(d_workspace),
              "workspace too small (need " + std::to_string(need) + " bytes)");
-  int ns;
-  int64_t span;
-  split_plan(n_users, n_items, &ns, &span);
-  float* ps = reinterpret_cast<float*>(d_workspace);
-  int32_t* pi = reinterpret_cast<int32_t*>(ps + n_users * ns * (int64_t)k);
+  const Plan p = make_plan(n_users, n_items, k);
+  char* ws = reinterpret_cast<char*>(d_workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int n_utiles = (int)fr::ceil_div(n_users, kUsersPerWG);
+  const unsigned merge_blocks = (unsigned)fr::ceil_div(n_users, 4);
+
+  ScoreArgs sa{};
+  sa.Uq = d_U; sa.ldu = ldu; sa.n_users = n_users;
+  sa.uid = d_uid; sa.ex_ptr = d_ex_ptr; sa.ex_col = d_ex_col; sa.ex_base = ex_base;
+  sa.k = k; sa.n_utiles = n_utiles;
+  MergeArgs ma{};
+  ma.n_users = n_users; ma.k = k; ma.uid = d_uid;
+  ma.t_ptr = d_test_ptr; ma.t_col = d_test_col; ma.t_base = test_base;
+  ma.out_s = d_out_scores; ma.out_i = d_out_items; ma.hits = d_hits;
   hipError_t e;
-  if (dtype == FR_BF16) {
-    if (d == 256) e = launch_score<uint16_t, 256>(d_U, ldu, n_users, d_I, ldi, n_items, d_uid, d_ex_ptr, d_ex_col, ex_base, k, ns, span, ps, pi, s);
-    else if (d == 128) e = launch_score<uint16_t, 128>(d_U, ldu, n_users, d_I, ldi, n_items, d_uid, d_ex_ptr, d_ex_col, ex_base, k, ns, span, ps, pi, s);
-    else if (d == 64) e = launch_score<uint16_t, 64>(d_U, ldu, n_users, d_I, ldi, n_items, d_uid, d_ex_ptr, d_ex_col, ex_base, k, ns, span, ps, pi, s);
-    else return fr::fail(FR_ENOTSUP, "fr_topk_scores: bf16 supports d in {64, 128, 256}");
-  } else {
-    if (d == 64) e = launch_score<float, 64>(d_U, ldu, n_users, d_I, ldi, n_items, d_uid, d_ex_ptr, d_ex_col, ex_base, k, ns, span, ps, pi, s);
-    else if (d == 128) e = launch_score<float, 128>(d_U, ldu, n_users, d_I, ldi, n_items, d_uid, d_ex_ptr, d_ex_col, ex_base, k, ns, span, ps, pi, s);
-    else return fr::fail(FR_ENOTSUP, "fr_topk_scores: fp32 supports d in {64, 128}");
+
+  // exact LIST pass over `items` (stride item_mul) then a merge into the outputs or thresholds
+  auto list_pass = [&](const void* It, int64_t ld, int64_t n_it, int64_t mul, int ns, int64_t span, char* lists,
+                       const int32_t* urows, const int32_t* d_nu, float* thr_out) -> hipError_t {
+    ScoreArgs l = sa;
+    l.It = It; l.ldi = ld; l.n_items = n_it; l.item_mul = mul; l.n_splits = ns; l.span = span;
+    l.urows = urows; l.d_nu = d_nu;
+    l.ls = reinterpret_cast<float*>(lists);
+    l.li = reinterpret_cast<int32_t*>(lists + n_users * ns * 2 * (int64_t)k * 4);
+    hipError_t err = launch_score<kList>(dtype, d, l, s);
+    if (err != hipSuccess) return err;
+    MergeArgs m = ma;
+    m.ps = l.ls; m.pi = l.li; m.cnt = nullptr; m.cap = k; m.n_regions = 2 * ns;
+    m.d_nu = d_nu; m.urows = urows; m.thr_out = thr_out;
+    return launch_merge(m, merge_blocks, s);
+  };
+
+  if (!p.sampled) {
+    e = list_pass(d_I, ldi, n_items, 1, p.ns2, p.span2, ws + p.off_l1, nullptr, nullptr, nullptr);
+    if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+    return FR_OK;
   }
+  float* thr = reinterpret_cast<float*>(ws + p.off_thr);
+  int32_t* flag_cnt = reinterpret_cast<int32_t*>(ws + p.off_flag);
+  int32_t* flag_list = flag_cnt + 1;
+  // 1. thresholds from the exact top-k of every stride-th item
+  e = list_pass(d_I, ldi * p.stride, p.n_sample, p.stride, p.ns1, p.span1, ws + p.off_l1, nullptr, nullptr, thr);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
-  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)fr::ceil_div(n_users, 4)), dim3(256), 0, s, ps, pi, n_users,
-                     ns, k, d_uid, d_test_ptr, d_test_col, test_base, d_out_scores, d_out_items, d_hits);
+  // 2. all items: GEMM + threshold, candidates appended
+  ScoreArgs ap = sa;
+  ap.It = d_I; ap.ldi = ldi; ap.n_items = n_items; ap.item_mul = 1; ap.n_splits = p.ns2; ap.span = p.span2;
+  ap.thr = thr; ap.cap = p.cap;
+  ap.cs = reinterpret_cast<float*>(ws + p.off_cs);
+  ap.ci = reinterpret_cast<int32_t*>(ws + p.off_ci);
+  ap.cc = reinterpret_cast<int32_t*>(ws + p.off_cc);
+  e = launch_score<kAppend>(dtype, d, ap, s);
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  // 3. merge the candidates; overflowed users are listed for the exact pass
+  hipLaunchKernelGGL(topk_zero_kernel, dim3(1), dim3(64), 0, s, flag_cnt);
   FR_LAUNCH_CHECK();
+  MergeArgs mc = ma;
+  mc.ps = ap.cs; mc.pi = ap.ci; mc.cnt = ap.cc; mc.cap = p.cap; mc.n_regions = 2 * p.ns2;
+  mc.flag_list = flag_list; mc.flag_cnt = flag_cnt;
+  mc.ex_ptr = d_ex_ptr; mc.ex_col = d_ex_col; mc.ex_base = ex_base;
+  e = launch_merge(mc, merge_blocks, s);
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  // 4. exact LIST pass + merge for the flagged users (grid sized for all; exits when none)
+  e = list_pass(d_I, ldi, n_items, 1, p.ns2, p.span2, ws + p.off_l2, flag_list, flag_cnt, nullptr);
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
   return FR_OK;
 }
