@@ -52,12 +52,13 @@ def _args():
                     help="eager steps of the per-kernel HIP-event timing pass (roofline)")
     ap.add_argument("--no-spmm-10m", action="store_true",  # also skips the config-4 training step
                     help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
+    ap.add_argument("--config-json", default=None, help="extra config keys for the HealthRec step (JSON)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip BASELINE config 5 (d=256 bf16 tables, full-sort top-k on MFMA)")
     return ap.parse_args()
 
 
-def build(device, batch, seed=0, dataset_seed=0):
+def build(device, batch, seed=0, dataset_seed=0, extra=None):
     from FoodRec.utils.configurator import Config
     from FoodRec.utils.dataset import FoodData
     from FoodRec.utils.synthetic import make_synthetic
@@ -66,7 +67,7 @@ def build(device, batch, seed=0, dataset_seed=0):
     data = FoodData.from_synthetic(ds)
     cfg = Config("CIKM_Model", "Allrecipes", {"use_gpu": device.type == "cuda", "seed": 999, "cuda_graph": True,
                                              "train_batch_size": batch, "log_root": "/tmp/frlog/",
-                                             "ckp_root": "/tmp/frckp/"})
+                                             "ckp_root": "/tmp/frckp/", **(extra or {})})
     cfg["device"] = device
     data.args_config = cfg
     init_seed(999 + seed)
@@ -100,7 +101,7 @@ def main():
     from FoodRec.engine.dist import GradAllReduce
     from FoodRec.engine.sampler import TripleSampler
 
-    cfg, data, model = build(device, args.batch)
+    cfg, data, model = build(device, args.batch, extra=json.loads(args.config_json) if args.config_json else None)
     trainer = Trainer(cfg, model)
     if world > 1:
         trainer.grad_hook = GradAllReduce(model, world)
