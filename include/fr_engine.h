@@ -310,6 +310,45 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
                    float* d_out_scores, int64_t* d_out_items, uint8_t* d_hits,
                    void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Fused post-norm Transformer encoder layer, training forward + backward.
+ * Replaces nn.TransformerEncoderLayer(d_model=64, nhead=2, dim_feedforward=256, dropout=p,
+ * activation=gelu|relu) of HealthRec's ingredient encoder (FoodRec/models/cikm_model.py:33-35,
+ * called at :232-238 over 2B sequences of L ingredient tokens):
+ *   x1 = LN1(x + dropout1(MHA(x, key_padding_mask)))   x2 = LN2(x1 + dropout2(FF(x1)))
+ * x / out: [n_seq, L, 64] fp32 batch-first; d_mask: [n_seq, L] additive key mask (0 / -inf,
+ * torch's canonical float form) or NULL.  L in {4, 5, 8, 10, 16, 20}.
+ * d_params (12 device pointers, torch parameter order): in_proj_weight [192,64], in_proj_bias,
+ *   out_proj.weight [64,64], out_proj.bias, norm1.weight, norm1.bias, linear1.weight [256,64],
+ *   linear1.bias, linear2.weight [64,256], linear2.bias, norm2.weight, norm2.bias.
+ * eps[2]: norm1/norm2 eps.  drop[4]: p of attention-prob dropout, dropout1, dropout (FF act),
+ * dropout2.  Masks come from a counter-based hash of (seed, *d_counter, site, element); the
+ * forward stores the counter value it used in *d_seed_out and the backward reads it back (the
+ * caller advances the counter; graph replays draw fresh masks).
+ * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), fact [T,256] (dropout(act(FF1))),
+ * y2 [T,64] (LN2 input), st1/st2 [T,2] (mean, rstd), T = n_seq * L, and dact (keep/(1-p) *
+ * act'(FF1)) as ceil(n_seq / (80 / L)) * 80 * 256 floats in the kernels' MFMA fragment layout
+ * (opaque to the caller; only fr_encoder_bwd reads it).
+ * Backward writes dx and the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
+ * gradients concatenated in d_params order); d_partials [fr_encoder_partials(n_seq, L)] floats of
+ * per-workgroup partials, summed in workgroup order (deterministic).
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_encoder_partials(int64_t n_seq, int L);
+int64_t fr_encoder_grad_numel(void);
+/* Diagnostics: enable (1) / disable (0) / keep (-1) per-phase s_memtime stamps of workgroup 0 and
+ * copy the stamp table (uint64 [2][32]: forward, backward; shader clock) to host_marks if non-NULL. */
+int fr_encoder_profile(int enable, uint64_t* host_marks);
+int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_seq, int L, const float* const* d_params,
+                   const float* eps, const float* drop, uint64_t seed, int gelu, const int64_t* d_counter,
+                   int64_t* d_seed_out, float* d_out, float* d_qkv, float* d_ctx, float* d_y1, float* d_fact,
+                   float* d_dact, float* d_y2, float* d_st1, float* d_st2, void* stream);
+int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, int64_t n_seq, int L,
+                   const float* const* d_params, const float* eps, const float* drop, uint64_t seed, int gelu,
+                   const int64_t* d_seed_in, const float* d_qkv, const float* d_ctx, const float* d_y1,
+                   const float* d_fact, const float* d_dact, const float* d_y2, const float* d_st1,
+                   const float* d_st2, float* d_dx,
+                   float* d_grad, float* d_partials, int64_t partial_floats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -473,6 +473,101 @@ def layer_norm(x: torch.Tensor, normalized_shape, weight=None, bias=None, eps: f
     return _LayerNorm.apply(x, weight, bias, eps)
 
 
+# ----------------------------------------------------------------------------- encoder layer
+ENCODER_LENGTHS = (4, 5, 8, 10, 16, 20)
+
+
+def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
+    """Algorithmic HBM bytes of one fused encoder-layer launch: the saved activations (qkv 192 +
+    ctx 64 + y1 64 + fact 256 + dact 256 + y2 64 + 4 stats floats per token) written by the
+    forward and read back by the backward, plus x/out (forward) or dout/x/dx (backward); weights are
+    L2-resident."""
+    T = n_seq * L
+    saved = 4 * T * (192 + 64 + 64 + 256 + 256 + 64 + 4)
+    return (saved + 4 * T * 64 * 3) if backward else (saved + 4 * T * 64 * 2)
+
+
+class _EncoderLayer(torch.autograd.Function):
+    """Fused nn.TransformerEncoderLayer training step (fr_encoder_fwd / fr_encoder_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, mask, cfg, *params):
+        NS, L, E = x.shape
+        T = NS * L
+        dev = x.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        out = torch.empty(NS, L, E, **f32)
+        qkv = torch.empty(T, 192, **f32)
+        cx = torch.empty(T, 64, **f32)
+        y1 = torch.empty(T, 64, **f32)
+        fact = torch.empty(T, 256, **f32)
+        dact = torch.empty(-(-NS // (80 // L)) * 80 * 256, **f32)  # per-workgroup MFMA fragment layout
+        y2 = torch.empty(T, 64, **f32)
+        st1 = torch.empty(T, 2, **f32)
+        st2 = torch.empty(T, 2, **f32)
+        seed_used = torch.empty(1, dtype=torch.int64, device=dev)
+        pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+        with profiling.region("encoder_fwd", encoder_bytes(NS, L, False)):
+            native.check(native.lib().fr_encoder_fwd(
+                x.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
+                cfg.counter.data_ptr(), seed_used.data_ptr(), out.data_ptr(), qkv.data_ptr(), cx.data_ptr(),
+                y1.data_ptr(), fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(),
+                native.stream_of(x)), "fr_encoder_fwd")
+        cfg.counter.add_(1)
+        ctx.cfg = cfg
+        ctx.has_mask = mask is not None
+        ctx.save_for_backward(x, mask if mask is not None else seed_used, qkv, cx, y1, fact, dact, y2, st1,
+                              st2, seed_used, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, mask, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used, *params = ctx.saved_tensors
+        cfg = ctx.cfg
+        NS, L, _ = x.shape
+        g = g.contiguous()
+        lib = native.lib()
+        dx = torch.empty_like(x)
+        grad = torch.empty(lib.fr_encoder_grad_numel(), dtype=torch.float32, device=x.device)
+        nparts = lib.fr_encoder_partials(NS, L)
+        part = torch.empty(nparts, dtype=torch.float32, device=x.device)
+        pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+        with profiling.region("encoder_bwd", encoder_bytes(NS, L, True)):
+            native.check(lib.fr_encoder_bwd(
+                g.data_ptr(), x.data_ptr(), mask.data_ptr() if ctx.has_mask else None, NS, L, pp, cfg.eps,
+                cfg.drop, cfg.seed, cfg.gelu, seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(),
+                fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
+                grad.data_ptr(),
+                part.data_ptr(), nparts, native.stream_of(g)), "fr_encoder_bwd")
+        grads = torch.split(grad, [p.numel() for p in params])
+        return (dx, None, None) + tuple(gr.view(p.shape) for gr, p in zip(grads, params))
+
+
+class EncoderConfig:
+    """Per-layer constants of the fused encoder: eps (2), dropout p (4), activation, the hash seed
+    and the device step counter the forward reads (advanced after every forward)."""
+
+    def __init__(self, eps, drop, gelu: bool, seed: int, device):
+        self.eps = (ctypes.c_float * 2)(*[float(e) for e in eps])
+        self.drop = (ctypes.c_float * 4)(*[float(p) for p in drop])
+        self.gelu = 1 if gelu else 0
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+
+
+def encoder_layer(x: torch.Tensor, mask, cfg: EncoderConfig, params) -> torch.Tensor:
+    """One fused post-norm encoder layer over batch-first x [n_seq, L, 64] (fp32, contiguous);
+    ``mask``: [n_seq, L] additive float key mask or None; ``params``: the 12 layer tensors in
+    torch order (see include/fr_engine.h)."""
+    native.require_device(x)
+    if x.dim() != 3 or x.shape[2] != 64 or x.shape[1] not in ENCODER_LENGTHS or x.dtype != torch.float32:
+        raise native.EngineError(f"fused encoder layer: unsupported input {tuple(x.shape)} {x.dtype}")
+    x = x.contiguous()
+    if mask is not None:
+        mask = mask.to(torch.float32).contiguous()
+    return _EncoderLayer.apply(x, mask, cfg, *params)
+
+
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod

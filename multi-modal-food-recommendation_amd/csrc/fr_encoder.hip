@@ -1,0 +1,992 @@
+// Fused post-norm Transformer encoder layer (training forward + backward), gfx950.
+//
+// HealthRec's ingredient encoder (FoodRec/models/cikm_model.py:33-35, used at :232-238) is
+// nn.TransformerEncoder over nn.TransformerEncoderLayer(d_model=64, nhead=2, dim_feedforward=256,
+// dropout=p, activation=gelu), post-norm, run on 2B sequences of 20 ingredient tokens:
+//
+//   qkv = x W_in^T + b_in                      ctx = dropout(softmax(q k^T / sqrt(32) + mask)) v
+//   x1  = LN1(x + dropout1(ctx W_o^T + b_o))   x2  = LN2(x1 + dropout2(dropout(act(x1 W1^T + b1)) W2^T + b2))
+//
+// torch runs this as ~20 forward and ~35 backward kernels per layer over [20480 x <=256] tensors,
+// each a few microseconds of launch-bound work.  Here one workgroup owns G = 80/L whole sequences
+// (80 token rows = five 16-row MFMA tiles) and keeps every intermediate in LDS: one forward and one
+// backward launch per layer, plus one ordered reduction of the per-workgroup weight-gradient partials.
+//
+// * GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 in / f32 accumulate, the f32 vector rate).  The k
+//   order inside a 16-wide chunk is permuted so each lane feeds four MFMAs from one float4 of A and
+//   one float4 of B (lane group h holds k = 4h..4h+3 of the chunk).
+// * Attention (20 x 20 per head) on the VALU: one thread per (sequence, head, query row).
+// * Dropout masks from a counter-based hash of (seed, step counter, site, element): the backward
+//   regenerates them instead of storing them; the step counter is read on the device, so a captured
+//   HIP graph draws fresh masks on every replay.
+// * Weight/bias gradients: each workgroup writes its partial sums; fr_encoder_bwd sums them in
+//   workgroup order (deterministic).
+#include "fr_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int E = 64, HEADS = 2, HD = 32, FF = 256, QKV = 3 * E;
+constexpr int ROWS = 80;                            // token rows per workgroup (5 MFMA row tiles)
+constexpr int RT = ROWS / 16;
+constexpr int LD_E = E + 4, LD_QKV = QKV + 4, LD_FF = FF + 4;
+constexpr int NT = 256;                             // threads per workgroup (4 waves)
+constexpr int BUF_D = 6400;                         // attention p'/ds buffers (2*G*H*L*L) and scratch
+
+// gradient partial layout (floats), identical to the flat gradient buffer fr_encoder_bwd writes
+constexpr int OFF_WIN = 0, OFF_BIN = OFF_WIN + QKV * E, OFF_WO = OFF_BIN + QKV, OFF_BO = OFF_WO + E * E,
+              OFF_G1 = OFF_BO + E, OFF_BE1 = OFF_G1 + E, OFF_W1 = OFF_BE1 + E, OFF_B1 = OFF_W1 + FF * E,
+              OFF_W2 = OFF_B1 + FF, OFF_B2 = OFF_W2 + E * FF, OFF_G2 = OFF_B2 + E, OFF_BE2 = OFF_G2 + E,
+              NPART = OFF_BE2 + E;
+static_assert(NPART % 4 == 0, "partials are reduced as float4");
+
+struct Weights {
+  const float *w_in, *b_in, *w_o, *b_o, *g1, *be1, *w1, *b1, *w2, *b2, *g2, *be2;
+  float eps1, eps2;
+  uint32_t thr[4];     // dropout: element kept iff hash >= thr  (sites: attn, out-proj, ff-act, ff-out)
+  float scale[4];      // 1 / (1 - p)
+  uint64_t seed;
+  int gelu;
+};
+
+struct FwdArgs {
+  Weights w;
+  const float* x;      // [NS, L, 64]
+  const float* mask;   // [NS, L] additive key mask (0 / -inf) or null
+  int64_t ns;
+  const int64_t* counter;
+  int64_t* seed_out;   // counter value used (read back by the backward)
+  float* out;          // [NS, L, 64]
+  // saved for the backward: fact = dropout(act(pre)), dact = keep * scale * act'(pre)  [T, 256];
+  // st: (mean, rstd) per token
+  float *qkv, *ctx, *y1, *fact, *dact, *y2, *st1, *st2;
+};
+
+struct BwdArgs {
+  Weights w;
+  const float* dout;
+  const float* x;
+  const float* mask;
+  int64_t ns;
+  const int64_t* seed_in;
+  const float *qkv, *ctx, *y1, *fact, *dact, *y2, *st1, *st2;
+  float* dx;
+  float* part;         // [n_wg, NPART]
+};
+
+// Phase timestamps (diagnostics, off unless fr_encoder_profile(1, ...)): workgroup 0's thread 0
+// records s_memtime (shader clock) after each barrier of the forward (kind 0) / backward (kind 1).
+__device__ int g_prof_on;
+__device__ unsigned long long g_prof[2][32];
+#define FR_MARK(kind, n)                                                       \
+  do {                                                                         \
+    if (prof && threadIdx.x == 0) g_prof[kind][n] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// per-(step, site) 32-bit hash keys: hi32(mix64(mix64(seed ^ mix64(counter + C)) + site + 1))
+struct SiteKeys {
+  uint32_t k[4];
+};
+
+__device__ __forceinline__ SiteKeys site_keys(uint64_t seed, int64_t counter) {
+  const uint64_t key = mix64(seed ^ mix64((uint64_t)counter + 0x632BE59BD9B4E019ull));
+  SiteKeys s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s.k[i] = (uint32_t)(mix64(key + (uint64_t)(i + 1)) >> 32);
+  return s;
+}
+
+// keep test for element idx: Weyl step + the lowbias32 finalizer (9 VALU ops), kept iff >= thr
+__device__ __forceinline__ bool keep(uint32_t ks, uint32_t idx, uint32_t thr) {
+  if (thr == 0u) return true;
+  uint32_t x = idx * 0x9E3779B1u + ks;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x >= thr;
+}
+
+// act(v) and act'(v): ReLU, or GELU(v) = v * Phi(v) (torch's exact-erf form).  Phi and phi share one
+// exp(-v^2/2); erf from Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), with Phi(-|v|) = q computed
+// directly (no cancellation for negative v).
+__device__ __forceinline__ float2 act_fwd_grad(float v, int gelu) {
+  if (!gelu) return make_float2(fmaxf(v, 0.f), v > 0.f ? 1.f : 0.f);
+  const float a = fabsf(v) * 0.70710678118654752f;
+  const float e = __expf(-a * a);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float q = 0.5f * poly * e;  // Phi(-|v|) = (1 - erf(|v| / sqrt 2)) / 2
+  const float cdf = v >= 0.f ? 1.f - q : q;
+  return make_float2(v * cdf, fmaf(v, e * 0.39894228040143268f, cdf));
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float comp(const float4& v, int m) {
+  return m == 0 ? v.x : (m == 1 ? v.y : (m == 2 ? v.z : v.w));
+}
+
+constexpr float kScale = 0.17677669529663688f;  // 1 / sqrt(HD)
+
+// offset of lane's float4 (4 rows of one column) of FF1 column tile (wave, c), row tile r, in the
+// fragment-layout dact buffer [n_wg][ROWS * FF]
+__device__ __forceinline__ int64_t dact_frag(int wg, int wave, int c, int r, int lane) {
+  return (int64_t)wg * (ROWS * FF) + ((((wave * 4 + c) * RT + r) * 64 + lane) << 2);
+}
+
+__device__ __forceinline__ float dot_row(const float (&q)[HD], const float* r) {
+  float d = 0.f;
+#pragma unroll
+  for (int e4 = 0; e4 < HD / 4; ++e4) {
+    const float4 v = lds4(r + 4 * e4);
+    d = fmaf(q[4 * e4], v.x, d); d = fmaf(q[4 * e4 + 1], v.y, d);
+    d = fmaf(q[4 * e4 + 2], v.z, d); d = fmaf(q[4 * e4 + 3], v.w, d);
+  }
+  return d;
+}
+
+__device__ __forceinline__ void axpy_row(float s, const float* r, float (&c)[HD]) {
+#pragma unroll
+  for (int e4 = 0; e4 < HD / 4; ++e4) {
+    const float4 v = lds4(r + 4 * e4);
+    c[4 * e4] = fmaf(s, v.x, c[4 * e4]); c[4 * e4 + 1] = fmaf(s, v.y, c[4 * e4 + 1]);
+    c[4 * e4 + 2] = fmaf(s, v.z, c[4 * e4 + 2]); c[4 * e4 + 3] = fmaf(s, v.w, c[4 * e4 + 3]);
+  }
+}
+
+// acc[r][c] (+)= A[80 x K] (LDS, lda) . W^T, W [N x K] row-major in global; column tiles c0..c0+NC-1.
+// The next chunk's W fragment is loaded before the current chunk's MFMAs (register double buffer).
+template <int NC, int K>
+__device__ __forceinline__ void gemm_xwt(const float* A, int lda, const float* __restrict__ W, int c0,
+                                         f32x4 (&acc)[RT][NC]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+  float4 bn[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) bn[c] = *reinterpret_cast<const float4*>(W + (int64_t)(16 * (c0 + c) + i) * K + 4 * h);
+#pragma unroll 4
+  for (int kc = 0; kc < K / 16; ++kc) {
+    float4 a[RT], b[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) b[c] = bn[c];
+    if (kc + 1 < K / 16) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        bn[c] = *reinterpret_cast<const float4*>(W + (int64_t)(16 * (c0 + c) + i) * K + (kc + 1) * 16 + 4 * h);
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r) a[r] = lds4(A + (16 * r + i) * lda + kc * 16 + 4 * h);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[r][c] = mfma4(comp(a[r], m), comp(b[c], m), acc[r][c]);
+  }
+}
+
+// acc[r][c] (+)= Y[80 x N] (LDS, ldy) . W, W [N x KO] row-major in global; output column tiles c0..
+template <int NC, int N, int KO>
+__device__ __forceinline__ void gemm_yw(const float* Y, int ldy, const float* __restrict__ W, int c0,
+                                        f32x4 (&acc)[RT][NC]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+  float bn[4][NC];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bn[m][c] = W[(int64_t)(4 * h + m) * KO + 16 * (c0 + c) + i];
+#pragma unroll 4
+  for (int nc = 0; nc < N / 16; ++nc) {
+    float4 a[RT];
+    float b[4][NC];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) b[m][c] = bn[m][c];
+    if (nc + 1 < N / 16) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) bn[m][c] = W[(int64_t)((nc + 1) * 16 + 4 * h + m) * KO + 16 * (c0 + c) + i];
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r) a[r] = lds4(Y + (16 * r + i) * ldy + nc * 16 + 4 * h);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[r][c] = mfma4(comp(a[r], m), b[m][c], acc[r][c]);
+  }
+}
+
+// weight-gradient partial  P[n][k] = sum_t Y[t][n] X[t][k] over the 80 rows; this wave owns
+// n-tiles n0..n0+NN-1 x k-tiles k0..k0+NK-1; written to part (row length K).
+template <int NN, int NK>
+__device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, const float* X, int ldx, int n0, int k0,
+                                            float* __restrict__ part, int K) {
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+  f32x4 acc[NN][NK];
+#pragma unroll
+  for (int a = 0; a < NN; ++a)
+#pragma unroll
+    for (int b = 0; b < NK; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tc = 0; tc < RT; ++tc) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int t = tc * 16 + 4 * h + m;
+      float ya[NN], xb[NK];
+#pragma unroll
+      for (int a = 0; a < NN; ++a) ya[a] = Y[t * ldy + 16 * (n0 + a) + i];
+#pragma unroll
+      for (int b = 0; b < NK; ++b) xb[b] = X[t * ldx + 16 * (k0 + b) + i];
+#pragma unroll
+      for (int a = 0; a < NN; ++a)
+#pragma unroll
+        for (int b = 0; b < NK; ++b) acc[a][b] = mfma4(ya[a], xb[b], acc[a][b]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < NN; ++a)
+#pragma unroll
+    for (int b = 0; b < NK; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[(16 * (n0 + a) + 4 * h + q) * K + 16 * (k0 + b) + i] = acc[a][b][q];
+}
+
+// column sums of an [80 x n] LDS tile (rows in order) -> part[0..n)
+__device__ __forceinline__ void colsum(const float* Y, int ldy, int n, float* __restrict__ part) {
+  for (int c = threadIdx.x; c < n; c += NT) {
+    float s = 0.f;
+    for (int t = 0; t < ROWS; ++t) s += Y[t * ldy + c];
+    part[c] = s;
+  }
+}
+
+// zero a [rows x cols] LDS region (cols % 4 == 0)
+__device__ __forceinline__ void lds_zero(float* p, int ld, int rows, int cols) {
+  const int per = cols / 4;
+  for (int e = threadIdx.x; e < rows * per; e += NT)
+    *reinterpret_cast<float4*>(p + (e / per) * ld + 4 * (e % per)) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// load rows [0, tv) of a [*, COLS] global tensor into LDS (ld), zero rows [tv, 80).  All loads of a
+// thread are issued before the first LDS store (unconditional addresses, rows clamped), so the
+// copy costs one memory latency, not one per row.
+template <int COLS>
+__device__ __forceinline__ void lds_load(float* p, int ld, const float* __restrict__ g, int tv) {
+  constexpr int PER = COLS / 4, ITER = ROWS * PER / NT;
+  static_assert(ROWS * PER % NT == 0, "tile / block shape");
+  float4 v[ITER];
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
+    v[k] = *reinterpret_cast<const float4*>(g + (int64_t)min(r, tv - 1) * COLS + 4 * c4);
+  }
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
+    *reinterpret_cast<float4*>(p + r * ld + 4 * c4) = r < tv ? v[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// store rows [0, tv) of an LDS tile (ld) to a [*, COLS] global tensor, float4 per thread
+template <int COLS>
+__device__ __forceinline__ void lds_store(const float* p, int ld, float* __restrict__ g, int tv) {
+  constexpr int PER = COLS / 4, ITER = ROWS * PER / NT;
+#pragma unroll
+  for (int k = 0; k < ITER; ++k) {
+    const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
+    if (r < tv) *reinterpret_cast<float4*>(g + (int64_t)r * COLS + 4 * c4) = lds4(p + r * ld + 4 * c4);
+  }
+}
+
+// LayerNorm forward over the 80 rows of an LDS [80 x 64] tile, in place; 16 lanes x float4 per row.
+// Saves y (the LN input) and (mean, rstd) for rows < tv.
+__device__ __forceinline__ void ln_rows_fwd(float* X, const float* __restrict__ g, const float* __restrict__ b,
+                                            float eps, int tv, float* __restrict__ ysave, float* __restrict__ st,
+                                            float* __restrict__ gout) {
+  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+  const float4 gg = *reinterpret_cast<const float4*>(g + 4 * l);
+  const float4 bb = *reinterpret_cast<const float4*>(b + 4 * l);
+  for (int r = grp; r < ROWS; r += NT / 16) {
+    float4 v = lds4(X + r * LD_E + 4 * l);
+    const float mean = group_sum<16>(v.x + v.y + v.z + v.w) * (1.f / E);
+    const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+    const float var = group_sum<16>(d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w) * (1.f / E);
+    const float rstd = rsqrtf(var + eps);
+    const float4 o = make_float4(fmaf(d.x * rstd, gg.x, bb.x), fmaf(d.y * rstd, gg.y, bb.y),
+                                 fmaf(d.z * rstd, gg.z, bb.z), fmaf(d.w * rstd, gg.w, bb.w));
+    *reinterpret_cast<float4*>(X + r * LD_E + 4 * l) = o;
+    if (r < tv) {
+      if (ysave) *reinterpret_cast<float4*>(ysave + (int64_t)r * E + 4 * l) = v;
+      if (gout) *reinterpret_cast<float4*>(gout + (int64_t)r * E + 4 * l) = o;
+      if (l == 0) {
+        st[2 * r] = mean;
+        st[2 * r + 1] = rstd;
+      }
+    }
+  }
+}
+
+// LayerNorm backward over the rows of an LDS [80 x 64] tile of upstream gradients, in place
+// (dY -> dX).  y: saved LN input rows (global), st: (mean, rstd).  dgamma / dbeta partials via the
+// scratch (16 row groups x 64, summed in group order) -> pg / pb.
+__device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ y, const float* __restrict__ st,
+                                            const float* __restrict__ g, int tv, float* scratch,
+                                            float* __restrict__ pg, float* __restrict__ pb) {
+  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+  constexpr int NR = ROWS / (NT / 16);
+  const float4 gg = *reinterpret_cast<const float4*>(g + 4 * l);
+  float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
+  float4 yv[NR];
+  float2 sv[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {  // issue every row's loads first (rows clamped to tv - 1)
+    const int r = min(grp + k * (NT / 16), tv - 1);
+    yv[k] = *reinterpret_cast<const float4*>(y + (int64_t)r * E + 4 * l);
+    sv[k] = *reinterpret_cast<const float2*>(st + 2 * r);
+  }
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int r = grp + k * (NT / 16);
+    if (r >= tv) break;
+    const float4 dy = lds4(D + r * LD_E + 4 * l);
+    const float4 v = yv[k];
+    const float mean = sv[k].x, rstd = sv[k].y;
+    const float4 xh = make_float4((v.x - mean) * rstd, (v.y - mean) * rstd, (v.z - mean) * rstd, (v.w - mean) * rstd);
+    const float4 gd = make_float4(dy.x * gg.x, dy.y * gg.y, dy.z * gg.z, dy.w * gg.w);
+    const float m1 = group_sum<16>(gd.x + gd.y + gd.z + gd.w) * (1.f / E);
+    const float m2 = group_sum<16>(gd.x * xh.x + gd.y * xh.y + gd.z * xh.z + gd.w * xh.w) * (1.f / E);
+    const float4 dx = make_float4(rstd * (gd.x - m1 - xh.x * m2), rstd * (gd.y - m1 - xh.y * m2),
+                                  rstd * (gd.z - m1 - xh.z * m2), rstd * (gd.w - m1 - xh.w * m2));
+    *reinterpret_cast<float4*>(D + r * LD_E + 4 * l) = dx;
+    sg = make_float4(fmaf(dy.x, xh.x, sg.x), fmaf(dy.y, xh.y, sg.y), fmaf(dy.z, xh.z, sg.z), fmaf(dy.w, xh.w, sg.w));
+    sb = f4_add(sb, dy);
+  }
+  *reinterpret_cast<float4*>(scratch + grp * E + 4 * l) = sg;
+  *reinterpret_cast<float4*>(scratch + 16 * E + grp * E + 4 * l) = sb;
+  __syncthreads();
+  if (threadIdx.x < 2 * E) {
+    const int which = threadIdx.x / E, c = threadIdx.x % E;
+    float s = 0.f;
+    for (int q = 0; q < 16; ++q) s += scratch[which * 16 * E + q * E + c];
+    (which ? pb : pg)[c] = s;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------
+template <int L>
+__global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
+  constexpr int G = ROWS / L;
+  __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];  // qkv (ctx in the q slots), then act
+  __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];   // x -> y1 -> x1 -> y2
+  constexpr int NTASK = G * HEADS * L;
+  __shared__ float SB[L * NTASK];                                   // attention score rows
+  __shared__ float MS[ROWS];                                        // key mask of the tile's tokens
+  const Weights& w = a.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int64_t seq0 = (int64_t)blockIdx.x * G;
+  const int nseq = (int)min<int64_t>(G, a.ns - seq0);
+  const int tv = nseq * L;
+  const int64_t tok0 = seq0 * L;
+  const bool prof = g_prof_on && blockIdx.x == 0;
+  FR_MARK(0, 0);
+  const int64_t counter = *a.counter;
+  const SiteKeys ks = site_keys(w.seed, counter);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.seed_out = counter;
+
+  if (threadIdx.x < ROWS) MS[threadIdx.x] = (a.mask && threadIdx.x < tv) ? a.mask[tok0 + threadIdx.x] : 0.f;
+  lds_load<E>(RB, LD_E, a.x + tok0 * E, tv);
+  __syncthreads();
+  FR_MARK(0, 1);
+
+  {  // qkv = x W_in^T + b_in  (wave: column tiles 3w..3w+2)
+    f32x4 acc[RT][3];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_xwt<3, E>(RB, LD_E, w.w_in, 3 * wave, acc);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int col = 16 * (3 * wave + c) + i16;
+      const float bias = w.b_in[col];
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * r + 4 * h4 + q;
+          RA[row * LD_QKV + col] = acc[r][c][q] + bias;
+        }
+    }
+  }
+  __syncthreads();
+  FR_MARK(0, 2);
+  lds_store<QKV>(RA, LD_QKV, a.qkv + tok0 * QKV, tv);
+  __syncthreads();  // the copy has read every q slot before attention overwrites them with ctx
+  FR_MARK(0, 20);
+
+  // attention: one thread per (sequence, head, query row); score rows in LDS as SB[j][task]
+  if (threadIdx.x < NTASK) {
+    const int g = threadIdx.x / (HEADS * L), hh = (threadIdx.x / L) % HEADS, qi = threadIdx.x % L;
+    if (g < nseq) {
+      const int rq = g * L + qi, me = threadIdx.x;
+      float q[HD];
+#pragma unroll
+      for (int e4 = 0; e4 < HD / 4; ++e4) {
+        const float4 v = lds4(RA + rq * LD_QKV + hh * HD + 4 * e4);
+        q[4 * e4] = v.x; q[4 * e4 + 1] = v.y; q[4 * e4 + 2] = v.z; q[4 * e4 + 3] = v.w;
+      }
+      float mx = -INFINITY;
+#pragma unroll 2
+      for (int j = 0; j < L; ++j) {
+        const float s = dot_row(q, RA + (g * L + j) * LD_QKV + E + hh * HD) * kScale + MS[g * L + j];
+        SB[j * NTASK + me] = s;
+        mx = fmaxf(mx, s);
+      }
+      float sum = 0.f;
+      for (int j = 0; j < L; ++j) {
+        const float e = expf(SB[j * NTASK + me] - mx);
+        SB[j * NTASK + me] = e;
+        sum += e;
+      }
+      const float inv = 1.f / sum;
+      const uint32_t base = (uint32_t)((((seq0 + g) * HEADS + hh) * L + qi) * L);
+      float c[HD];
+#pragma unroll
+      for (int e = 0; e < HD; ++e) c[e] = 0.f;
+#pragma unroll 2
+      for (int j = 0; j < L; ++j) {
+        const float p = keep(ks.k[0], base + j, w.thr[0]) ? SB[j * NTASK + me] * inv * w.scale[0] : 0.f;
+        axpy_row(p, RA + (g * L + j) * LD_QKV + 2 * E + hh * HD, c);
+      }
+#pragma unroll
+      for (int e4 = 0; e4 < HD / 4; ++e4) {
+        const float4 v = make_float4(c[4 * e4], c[4 * e4 + 1], c[4 * e4 + 2], c[4 * e4 + 3]);
+        *reinterpret_cast<float4*>(RA + rq * LD_QKV + hh * HD + 4 * e4) = v;
+        *reinterpret_cast<float4*>(a.ctx + (tok0 + rq) * E + hh * HD + 4 * e4) = v;
+      }
+    }
+  }
+  __syncthreads();
+  FR_MARK(0, 3);
+
+  {  // y1 = x + dropout1(ctx W_o^T + b_o)   (wave: column tile w); ctx rows of padded sequences are stale
+    f32x4 acc[RT][1];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_xwt<1, E>(RA, LD_QKV, w.w_o, wave, acc);
+    const int col = 16 * wave + i16;
+    const float bias = w.b_o[col];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * r + 4 * h4 + q;
+        const float o = acc[r][0][q] + bias;
+        const float d = keep(ks.k[1], (uint32_t)((tok0 + row) * E + col), w.thr[1]) ? o * w.scale[1] : 0.f;
+        RB[row * LD_E + col] += d;
+      }
+  }
+  __syncthreads();
+  FR_MARK(0, 4);
+  ln_rows_fwd(RB, w.g1, w.be1, w.eps1, tv, a.y1 + tok0 * E, a.st1 + 2 * tok0, nullptr);
+  __syncthreads();
+  FR_MARK(0, 5);
+
+  {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA  (wave: column tiles 4w..4w+3)
+    f32x4 acc[RT][4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_xwt<4, E>(RB, LD_E, w.w1, 4 * wave, acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = 16 * (4 * wave + c) + i16;
+      const float bias = w.b1[col];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        float d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * r + 4 * h4 + q;
+          const float2 fg = act_fwd_grad(acc[r][c][q] + bias, w.gelu);
+          const bool kp = keep(ks.k[2], (uint32_t)((tok0 + row) * FF + col), w.thr[2]);
+          RA[row * LD_FF + col] = kp ? fg.x * w.scale[2] : 0.f;
+          d[q] = kp ? fg.y * w.scale[2] : 0.f;
+        }
+        // dact in the MFMA fragment layout: one coalesced float4 per lane, read back the same way
+        *reinterpret_cast<float4*>(a.dact + dact_frag(blockIdx.x, wave, c, r, lane)) = make_float4(d[0], d[1], d[2], d[3]);
+      }
+    }
+  }
+  __syncthreads();
+  FR_MARK(0, 6);
+
+  {  // y2 = x1 + dropout2(act' W2^T + b2)  (wave: column tile w, K = 256)
+    f32x4 acc[RT][1];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_xwt<1, FF>(RA, LD_FF, w.w2, wave, acc);
+    const int col = 16 * wave + i16;
+    const float bias = w.b2[col];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * r + 4 * h4 + q;
+        const float o = acc[r][0][q] + bias;
+        const float d = keep(ks.k[3], (uint32_t)((tok0 + row) * E + col), w.thr[3]) ? o * w.scale[3] : 0.f;
+        RB[row * LD_E + col] += d;
+      }
+  }
+  __syncthreads();
+  FR_MARK(0, 7);
+  lds_store<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);  // act' (RA is final after the FF2 barrier)
+  ln_rows_fwd(RB, w.g2, w.be2, w.eps2, tv, a.y2 + tok0 * E, a.st2 + 2 * tok0, a.out + tok0 * E);
+  FR_MARK(0, 31);
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------------------
+template <int L>
+__global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
+  constexpr int G = ROWS / L;
+  __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];
+  __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];
+  __shared__ __attribute__((aligned(16))) float RC[ROWS * LD_E];
+  __shared__ __attribute__((aligned(16))) float RD[BUF_D];
+  static_assert(2 * G * HEADS * L * L <= BUF_D && ROWS * LD_E <= BUF_D, "attention buffers");
+  const Weights& w = a.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int64_t seq0 = (int64_t)blockIdx.x * G;
+  const int nseq = (int)min<int64_t>(G, a.ns - seq0);
+  const int tv = nseq * L;
+  const int64_t tok0 = seq0 * L;
+  const bool prof = g_prof_on && blockIdx.x == 0;
+  FR_MARK(1, 0);
+  const SiteKeys ks = site_keys(w.seed, *a.seed_in);
+  float* part = a.part + (int64_t)blockIdx.x * NPART;
+  __shared__ float MS[ROWS];
+  if (threadIdx.x < ROWS) MS[threadIdx.x] = (a.mask && threadIdx.x < tv) ? a.mask[tok0 + threadIdx.x] : 0.f;
+
+  // 1. LN2 backward: RB = dY2 (pad rows 0)
+  lds_load<E>(RB, LD_E, a.dout + tok0 * E, tv);
+  __syncthreads();
+  FR_MARK(1, 1);
+  ln_rows_bwd(RB, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, tv, RD, part + OFF_G2, part + OFF_BE2);
+
+  // 2. dG = dropout2'(dY2) -> RC;  act' (saved by the forward) -> RA
+  for (int e = threadIdx.x; e < ROWS * E; e += NT) {
+    const int r = e / E, c = e % E;
+    RC[r * LD_E + c] = keep(ks.k[3], (uint32_t)((tok0 + r) * E + c), w.thr[3]) ? RB[r * LD_E + c] * w.scale[3] : 0.f;
+  }
+  lds_load<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);
+  __syncthreads();
+  FR_MARK(1, 2);
+
+  // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 4w..4w+3);  db2
+  wgrad_tiles<4, 4>(RC, LD_E, RA, LD_FF, 0, 4 * wave, part + OFF_W2, FF);
+  colsum(RC, LD_E, E, part + OFF_B2);
+
+  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA
+    f32x4 acc[RT][4];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_yw<4, E, FF>(RC, LD_E, w.w2, 4 * wave, acc);
+    float4 pv[4][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        pv[c][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, wave, c, r, lane));
+    __syncthreads();  // every wave is done reading act' from RA
+    FR_MARK(1, 3);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = 16 * (4 * wave + c) + i16;
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * r + 4 * h4 + q;
+          RA[row * LD_FF + col] = row < tv ? acc[r][c][q] * comp(pv[c][r], q) : 0.f;
+        }
+    }
+  }
+  __syncthreads();
+  FR_MARK(1, 4);
+
+  // 5. db1; x1 = LN1(y1) recomputed -> RC
+  colsum(RA, LD_FF, FF, part + OFF_B1);
+  {
+    const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const float4 gg = *reinterpret_cast<const float4*>(w.g1 + 4 * l);
+    const float4 bb = *reinterpret_cast<const float4*>(w.be1 + 4 * l);
+    constexpr int NR = ROWS / (NT / 16);
+    float4 yv[NR];
+    float2 sv[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int r = min(grp + k * (NT / 16), tv - 1);
+      yv[k] = *reinterpret_cast<const float4*>(a.y1 + (tok0 + r) * E + 4 * l);
+      sv[k] = *reinterpret_cast<const float2*>(a.st1 + 2 * (tok0 + r));
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int r = grp + k * (NT / 16);
+      const float4 v = yv[k];
+      const float mean = sv[k].x, rstd = sv[k].y;
+      const float4 o = make_float4(fmaf((v.x - mean) * rstd, gg.x, bb.x), fmaf((v.y - mean) * rstd, gg.y, bb.y),
+                                   fmaf((v.z - mean) * rstd, gg.z, bb.z), fmaf((v.w - mean) * rstd, gg.w, bb.w));
+      *reinterpret_cast<float4*>(RC + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __syncthreads();
+  FR_MARK(1, 5);
+
+  // 6. dW1 = dpre^T x1  [256 x 64] (wave: n-tiles 4w..4w+3)
+  wgrad_tiles<4, 4>(RA, LD_FF, RC, LD_E, 4 * wave, 0, part + OFF_W1, E);
+
+  {  // 7. dX1 = dY2 + dpre W1  -> RB
+    f32x4 acc[RT][1];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_yw<1, FF, E>(RA, LD_FF, w.w1, wave, acc);
+    const int col = 16 * wave + i16;
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) RB[(16 * r + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
+  }
+  __syncthreads();
+  FR_MARK(1, 6);
+
+  // 8. LN1 backward: RB = dY1
+  ln_rows_bwd(RB, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, tv, RD, part + OFF_G1, part + OFF_BE1);
+
+  // 9. dO = dropout1'(dY1) -> RC;  ctx -> RD
+  for (int e = threadIdx.x; e < ROWS * E; e += NT) {
+    const int r = e / E, c = e % E;
+    RC[r * LD_E + c] = keep(ks.k[1], (uint32_t)((tok0 + r) * E + c), w.thr[1]) ? RB[r * LD_E + c] * w.scale[1] : 0.f;
+  }
+  lds_load<E>(RD, LD_E, a.ctx + tok0 * E, tv);
+  __syncthreads();
+  FR_MARK(1, 7);
+
+  // 10. dW_o = dO^T ctx [64 x 64] (wave: n-tile w); db_o
+  wgrad_tiles<1, 4>(RC, LD_E, RD, LD_E, wave, 0, part + OFF_WO, E);
+  colsum(RC, LD_E, E, part + OFF_BO);
+
+  {  // 11. dctx = dO W_o -> RC;  qkv -> RA
+    f32x4 acc[RT][1];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_yw<1, E, E>(RC, LD_E, w.w_o, wave, acc);
+    lds_load<QKV>(RA, LD_QKV, a.qkv + tok0 * QKV, tv);
+    __syncthreads();
+    FR_MARK(1, 8);
+    const int col = 16 * wave + i16;
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) RC[(16 * r + 4 * h4 + q) * LD_E + col] = acc[r][0][q];
+  }
+  __syncthreads();
+  FR_MARK(1, 9);
+
+  // 12. attention backward.  RD: P[j][task] (scores -> p -> p') and S[j][task] (dL/dp' -> ds*scale),
+  // task = (sequence, head, query row)
+  constexpr int NTASK = G * HEADS * L;
+  float* Pb = RD;
+  float* Sb = RD + NTASK * L;
+  const bool task = threadIdx.x < NTASK;
+  const int tg = threadIdx.x / (HEADS * L), thh = (threadIdx.x / L) % HEADS, ti = threadIdx.x % L;
+  const bool live = task && tg < nseq;
+  float dq[HD];
+  if (live) {  // phase a: query row ti
+    const int rq = tg * L + ti;
+    float q[HD], dc[HD];
+#pragma unroll
+    for (int e4 = 0; e4 < HD / 4; ++e4) {
+      const float4 v = lds4(RA + rq * LD_QKV + thh * HD + 4 * e4);
+      q[4 * e4] = v.x; q[4 * e4 + 1] = v.y; q[4 * e4 + 2] = v.z; q[4 * e4 + 3] = v.w;
+      const float4 d = lds4(RC + rq * LD_E + thh * HD + 4 * e4);
+      dc[4 * e4] = d.x; dc[4 * e4 + 1] = d.y; dc[4 * e4 + 2] = d.z; dc[4 * e4 + 3] = d.w;
+    }
+    const int me = threadIdx.x;
+    float mx = -INFINITY;
+#pragma unroll 2
+    for (int j = 0; j < L; ++j) {
+      const float* kr = RA + (tg * L + j) * LD_QKV + E + thh * HD;
+      const float s = dot_row(q, kr) * kScale + MS[tg * L + j];
+      Pb[j * NTASK + me] = s;
+      Sb[j * NTASK + me] = dot_row(dc, kr + E);    // dL/dp' = dctx . v_j
+      mx = fmaxf(mx, s);
+    }
+    float sum = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float e = expf(Pb[j * NTASK + me] - mx);
+      Pb[j * NTASK + me] = e;
+      sum += e;
+    }
+    const float inv = 1.f / sum;
+    const uint32_t base = (uint32_t)((((seq0 + tg) * HEADS + thh) * L + ti) * L);
+    float D = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float p = Pb[j * NTASK + me] * inv;
+      const bool kp = keep(ks.k[0], base + j, w.thr[0]);
+      const float dp = kp ? Sb[j * NTASK + me] * w.scale[0] : 0.f;  // dL/dp
+      Pb[j * NTASK + me] = kp ? p : -p;                              // keep bit in the sign
+      Sb[j * NTASK + me] = dp;
+      D = fmaf(p, dp, D);
+    }
+#pragma unroll
+    for (int e = 0; e < HD; ++e) dq[e] = 0.f;
+#pragma unroll 2
+    for (int j = 0; j < L; ++j) {
+      const float ps = Pb[j * NTASK + me], p = fabsf(ps);
+      const float ds = p * (Sb[j * NTASK + me] - D) * kScale;
+      Sb[j * NTASK + me] = ds;
+      Pb[j * NTASK + me] = ps > 0.f ? p * w.scale[0] : 0.f;  // p'
+      axpy_row(ds, RA + (tg * L + j) * LD_QKV + E + thh * HD, dq);
+    }
+  }
+  __syncthreads();
+  FR_MARK(1, 10);
+  if (live) {  // phase b: key row j = ti:  dk_j = sum_i ds_ij q_i,  dv_j = sum_i p'_ij dctx_i
+    const int rk = tg * L + ti;
+    float dk[HD], dv[HD];
+#pragma unroll
+    for (int e = 0; e < HD; ++e) dk[e] = dv[e] = 0.f;
+    for (int qi = 0; qi < L; ++qi) {
+      const int qt = (tg * HEADS + thh) * L + qi;
+      const float ds = Sb[ti * NTASK + qt];
+      const float pp = Pb[ti * NTASK + qt];
+      const float* qr = RA + (tg * L + qi) * LD_QKV + thh * HD;
+      const float* dr = RC + (tg * L + qi) * LD_E + thh * HD;
+#pragma unroll
+      for (int e4 = 0; e4 < HD / 4; ++e4) {
+        const float4 qv = lds4(qr + 4 * e4);
+        const float4 dd = lds4(dr + 4 * e4);
+        dk[4 * e4] = fmaf(ds, qv.x, dk[4 * e4]); dk[4 * e4 + 1] = fmaf(ds, qv.y, dk[4 * e4 + 1]);
+        dk[4 * e4 + 2] = fmaf(ds, qv.z, dk[4 * e4 + 2]); dk[4 * e4 + 3] = fmaf(ds, qv.w, dk[4 * e4 + 3]);
+        dv[4 * e4] = fmaf(pp, dd.x, dv[4 * e4]); dv[4 * e4 + 1] = fmaf(pp, dd.y, dv[4 * e4 + 1]);
+        dv[4 * e4 + 2] = fmaf(pp, dd.z, dv[4 * e4 + 2]); dv[4 * e4 + 3] = fmaf(pp, dd.w, dv[4 * e4 + 3]);
+      }
+    }
+    // k / v slots of row rk are read by no one after phase a
+#pragma unroll
+    for (int e4 = 0; e4 < HD / 4; ++e4) {
+      *reinterpret_cast<float4*>(RA + rk * LD_QKV + E + thh * HD + 4 * e4) =
+          make_float4(dk[4 * e4], dk[4 * e4 + 1], dk[4 * e4 + 2], dk[4 * e4 + 3]);
+      *reinterpret_cast<float4*>(RA + rk * LD_QKV + 2 * E + thh * HD + 4 * e4) =
+          make_float4(dv[4 * e4], dv[4 * e4 + 1], dv[4 * e4 + 2], dv[4 * e4 + 3]);
+    }
+  }
+  __syncthreads();
+  FR_MARK(1, 11);
+  if (live) {
+    const int rq = tg * L + ti;
+#pragma unroll
+    for (int e4 = 0; e4 < HD / 4; ++e4)
+      *reinterpret_cast<float4*>(RA + rq * LD_QKV + thh * HD + 4 * e4) =
+          make_float4(dq[4 * e4], dq[4 * e4 + 1], dq[4 * e4 + 2], dq[4 * e4 + 3]);
+  }
+  if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
+  lds_load<E>(RC, LD_E, a.x + tok0 * E, tv);
+  __syncthreads();
+  FR_MARK(1, 12);
+
+  // 13. db_in; dW_in = dqkv^T x [192 x 64] (wave: n-tiles 3w..3w+2)
+  colsum(RA, LD_QKV, QKV, part + OFF_BIN);
+  wgrad_tiles<3, 4>(RA, LD_QKV, RC, LD_E, 3 * wave, 0, part + OFF_WIN, E);
+
+  {  // 14. dX = dY1 + dqkv W_in
+    f32x4 acc[RT][1];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm_yw<1, QKV, E>(RA, LD_QKV, w.w_in, wave, acc);
+    const int col = 16 * wave + i16;
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * r + 4 * h4 + q;
+        if (row < tv) a.dx[(tok0 + row) * E + col] = RB[row * LD_E + col] + acc[r][0][q];
+      }
+  }
+  FR_MARK(1, 31);
+}
+
+// grad[j] = sum over workgroups of part[wg][j], in a fixed order (deterministic): a block owns 32
+// float4 columns; its 8 slices sum workgroups slice, slice+8, ... (8 loads in flight per thread),
+// then the slices are added in slice order.
+__global__ __launch_bounds__(256) void enc_reduce_kernel(const float4* __restrict__ part, int nwg,
+                                                         float4* __restrict__ grad) {
+  constexpr int COLS = 32, SL = 8, UNR = 8, N4 = NPART / 4;
+  __shared__ float4 sl[SL][COLS];
+  const int c = blockIdx.x * COLS + (threadIdx.x % COLS), slice = threadIdx.x / COLS;
+  const int cc = min(c, N4 - 1);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g0 = slice; g0 < nwg; g0 += SL * UNR) {
+    float4 v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int g = min(g0 + k * SL, nwg - 1);
+      v[k] = part[(int64_t)g * N4 + cc];
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k)
+      if (g0 + k * SL < nwg) s = f4_add(s, v[k]);
+  }
+  sl[slice][threadIdx.x % COLS] = s;
+  __syncthreads();
+  if (slice == 0 && c < N4) {
+    float4 t = sl[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < SL; ++k) t = f4_add(t, sl[k][threadIdx.x]);
+    grad[c] = t;
+  }
+}
+
+template <int L>
+int launch_fwd(const FwdArgs& a, hipStream_t s) {
+  const int64_t nwg = fr::ceil_div(a.ns, ROWS / L);
+  hipLaunchKernelGGL(enc_fwd_kernel<L>, dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+template <int L>
+int launch_bwd(const BwdArgs& a, float* grad, hipStream_t s) {
+  const int64_t nwg = fr::ceil_div(a.ns, ROWS / L);
+  hipLaunchKernelGGL(enc_bwd_kernel<L>, dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, 32)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(a.part), (int)nwg, reinterpret_cast<float4*>(grad));
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+bool supported_len(int L) { return L == 20 || L == 16 || L == 10 || L == 8 || L == 5 || L == 4; }
+
+int fill_weights(Weights& w, const float* const* p, const float* eps, const float* drop, uint64_t seed, int gelu) {
+  w.w_in = p[0]; w.b_in = p[1]; w.w_o = p[2]; w.b_o = p[3]; w.g1 = p[4]; w.be1 = p[5];
+  w.w1 = p[6]; w.b1 = p[7]; w.w2 = p[8]; w.b2 = p[9]; w.g2 = p[10]; w.be2 = p[11];
+  for (int k = 0; k < 12; ++k) FR_REQUIRE(p[k] && fr::aligned16(p[k]), "parameter pointers must be 16-byte aligned");
+  w.eps1 = eps[0];
+  w.eps2 = eps[1];
+  for (int k = 0; k < 4; ++k) {
+    FR_REQUIRE(drop[k] >= 0.f && drop[k] < 1.f, "dropout probability must be in [0, 1)");
+    const double t = (double)drop[k] * 4294967296.0;
+    w.thr[k] = drop[k] == 0.f ? 0u : (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+    w.scale[k] = 1.f / (1.f - drop[k]);
+  }
+  w.seed = seed;
+  w.gelu = gelu;
+  return FR_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t fr_encoder_partials(int64_t n_seq, int L) {
+  if (n_seq <= 0 || !supported_len(L)) return 0;
+  return fr::ceil_div(n_seq, ROWS / L) * (int64_t)NPART;
+}
+
+extern "C" int64_t fr_encoder_grad_numel(void) { return NPART; }
+
+extern "C" int fr_encoder_profile(int enable, uint64_t* host_marks) {
+  if (enable >= 0) {
+    const int on = enable ? 1 : 0;
+    FR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof_on), &on, sizeof(on)));
+  }
+  if (host_marks) FR_HIP_CHECK(hipMemcpyFromSymbol(host_marks, HIP_SYMBOL(g_prof), sizeof(g_prof)));
+  return FR_OK;
+}
+
+extern "C" int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_seq, int L,
+                              const float* const* d_params, const float* eps, const float* drop, uint64_t seed,
+                              int gelu, const int64_t* d_counter, int64_t* d_seed_out, float* d_out,
+                              float* d_qkv, float* d_ctx, float* d_y1, float* d_fact, float* d_dact, float* d_y2,
+                              float* d_st1, float* d_st2, void* stream) {
+  FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
+  FR_REQUIRE(n_seq * L * FF < (int64_t)1 << 32 && n_seq * HEADS * L * L < (int64_t)1 << 32,
+             "too many tokens for the 32-bit dropout element index");
+  FR_REQUIRE(d_x && d_out && d_counter && d_seed_out && d_qkv && d_ctx && d_y1 && d_fact && d_dact && d_y2 &&
+                 d_st1 && d_st2,
+             "null operand");
+  FR_REQUIRE(fr::aligned16(d_x) && fr::aligned16(d_out) && fr::aligned16(d_qkv) && fr::aligned16(d_ctx) &&
+                 fr::aligned16(d_y1) && fr::aligned16(d_fact) && fr::aligned16(d_dact) && fr::aligned16(d_y2),
+             "tensors must be 16-byte aligned");
+  FwdArgs a{};
+  int rc = fill_weights(a.w, d_params, eps, drop, seed, gelu);
+  if (rc) return rc;
+  a.x = d_x; a.mask = d_mask; a.ns = n_seq; a.counter = d_counter; a.seed_out = d_seed_out; a.out = d_out;
+  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.fact = d_fact; a.dact = d_dact; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (L) {
+    case 20: return launch_fwd<20>(a, s);
+    case 16: return launch_fwd<16>(a, s);
+    case 10: return launch_fwd<10>(a, s);
+    case 8: return launch_fwd<8>(a, s);
+    case 5: return launch_fwd<5>(a, s);
+    default: return launch_fwd<4>(a, s);
+  }
+}
+
+extern "C" int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, int64_t n_seq, int L,
+                              const float* const* d_params, const float* eps, const float* drop, uint64_t seed,
+                              int gelu, const int64_t* d_seed_in, const float* d_qkv, const float* d_ctx,
+                              const float* d_y1, const float* d_fact, const float* d_dact, const float* d_y2,
+                              const float* d_st1,
+                              const float* d_st2, float* d_dx, float* d_grad, float* d_partials,
+                              int64_t partial_floats, void* stream) {
+  FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
+  FR_REQUIRE(d_dout && d_x && d_seed_in && d_qkv && d_ctx && d_y1 && d_fact && d_dact && d_y2 && d_st1 && d_st2 &&
+                 d_dx &&
+                 d_grad && d_partials,
+             "null operand");
+  FR_REQUIRE(fr::aligned16(d_dout) && fr::aligned16(d_x) && fr::aligned16(d_dx) && fr::aligned16(d_grad) &&
+                 fr::aligned16(d_partials) && fr::aligned16(d_qkv) && fr::aligned16(d_ctx) && fr::aligned16(d_y1) &&
+                 fr::aligned16(d_y2),
+             "tensors must be 16-byte aligned");
+  FR_REQUIRE(partial_floats >= fr_encoder_partials(n_seq, L), "partial buffer too small");
+  BwdArgs a{};
+  int rc = fill_weights(a.w, d_params, eps, drop, seed, gelu);
+  if (rc) return rc;
+  a.dout = d_dout; a.x = d_x; a.mask = d_mask; a.ns = n_seq; a.seed_in = d_seed_in;
+  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.fact = d_fact; a.dact = d_dact; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
+  a.dx = d_dx; a.part = d_partials;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (L) {
+    case 20: return launch_bwd<20>(a, d_grad, s);
+    case 16: return launch_bwd<16>(a, d_grad, s);
+    case 10: return launch_bwd<10>(a, d_grad, s);
+    case 8: return launch_bwd<8>(a, d_grad, s);
+    case 5: return launch_bwd<5>(a, d_grad, s);
+    default: return launch_bwd<4>(a, d_grad, s);
+  }
+}

@@ -161,3 +161,66 @@ def full_sort_topk(U: np.ndarray, I: np.ndarray, k: int, exclude=None, held_out=
 def bf16_round(x) -> np.ndarray:
     """float32 values rounded to bfloat16 (round to nearest even), returned as float32."""
     return torch.as_tensor(np.asarray(x, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+# ----------------------------------------------------------------------------- encoder layer
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def encoder_keep_masks(seed: int, counter: int, n_seq: int, L: int, drop, heads: int = 2, d: int = 64,
+                       ff: int = 256):
+    """The fused encoder's dropout keep-masks (fr_encoder.hip: site_keys / keep), restated in numpy.
+    key = mix64(seed ^ mix64(counter + C)); site key k_s = hi32(mix64(key + s + 1)); element e of
+    site s is kept iff lowbias32(e * 0x9E3779B1 + k_s) >= floor(p * 2^32) (uint32 arithmetic).
+    Sites: 0 attention probs [n_seq, heads, L, L], 1 out-proj [n_seq, L, d], 2 FF activation
+    [n_seq, L, ff], 3 FF out [n_seq, L, d] (element index = row-major position).  Returns 4 float64
+    arrays of 0/1."""
+    shapes = [(n_seq, heads, L, L), (n_seq, L, d), (n_seq, L, ff), (n_seq, L, d)]
+    out = []
+    u32 = np.uint32
+    with np.errstate(over="ignore"):
+        key = _mix64(np.array([seed], np.uint64) ^ _mix64(np.array([counter], np.uint64)
+                                                          + np.uint64(0x632BE59BD9B4E019)))
+        for site, (shape, p) in enumerate(zip(shapes, drop)):
+            if p == 0:
+                out.append(np.ones(shape))
+                continue
+            thr = min(int(float(np.float32(p)) * 4294967296.0), 4294967295)
+            ks = (_mix64(key + np.uint64(site + 1)) >> np.uint64(32)).astype(u32)
+            x = np.arange(int(np.prod(shape)), dtype=np.uint64).astype(u32) * u32(0x9E3779B1) + ks
+            x ^= x >> u32(16)
+            x *= u32(0x7FEB352D)
+            x ^= x >> u32(15)
+            x *= u32(0x846CA68B)
+            x ^= x >> u32(16)
+            out.append((x >= u32(thr)).astype(np.float64).reshape(shape))
+    return out
+
+
+def encoder_layer_f64(x, mask, params, masks, drop, eps=(1e-5, 1e-5), gelu=True, heads: int = 2):
+    """nn.TransformerEncoderLayer's post-norm training forward (torch/nn/modules/transformer.py,
+    built at cikm_model.py:33-35) in float64 torch-CPU, batch-first x [n_seq, L, d], additive key
+    mask [n_seq, L] (or None), with explicit dropout keep-masks (encoder_keep_masks) scaled by
+    1/(1-p).  Differentiable: used for the gradient references."""
+    w_in, b_in, w_o, b_o, g1, be1, w1, b1, w2, b2, g2, be2 = params
+    NS, L, d = x.shape
+    hd = d // heads
+    ma, m1, mf, m2 = (torch.as_tensor(m, dtype=torch.float64) / (1.0 - p) for m, p in zip(masks, drop))
+    qkv = x @ w_in.t() + b_in
+    q, k, v = (t.reshape(NS, L, heads, hd).transpose(1, 2) for t in qkv.split(d, dim=-1))
+    s = q @ k.transpose(-1, -2) * hd ** -0.5
+    if mask is not None:
+        s = s + mask.view(NS, 1, 1, L)
+    pa = torch.softmax(s, dim=-1) * ma
+    ctx = (pa @ v).transpose(1, 2).reshape(NS, L, d)
+    y1 = x + (ctx @ w_o.t() + b_o) * m1
+    x1 = torch.nn.functional.layer_norm(y1, (d,), g1, be1, eps[0])
+    pre = x1 @ w1.t() + b1
+    f = (torch.nn.functional.gelu(pre) if gelu else torch.relu(pre)) * mf
+    y2 = x1 + (f @ w2.t() + b2) * m2
+    return torch.nn.functional.layer_norm(y2, (d,), g2, be2, eps[1])

@@ -1,0 +1,132 @@
+"""Fused Transformer encoder layer (fr_encoder_fwd / fr_encoder_bwd) vs the oracle.
+
+The layer replaces nn.TransformerEncoderLayer(64, 2, 256, dropout=p, activation=gelu) of HealthRec's
+ingredient encoder (cikm_model.py:33-35, 232-238).  Oracle: oracle.ops.encoder_layer_f64, a float64
+restatement of torch's post-norm training forward (pinned against torch's own module by
+tests/test_encoder_cpu.py), fed the kernel's dropout keep-masks regenerated on the host by
+oracle.ops.encoder_keep_masks.
+
+Tolerances (fp32 MFMA GEMMs + fp32 softmax/LayerNorm vs float64):
+  outputs              : |err| <= 2e-5 * max|ref| + 2e-6
+  dx, parameter grads  : |err| <= 1e-4 * max|ref grad| + 1e-6
+  dropout masks        : exact (the same hash)
+"""
+import pytest
+import torch
+
+from oracle import ops as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(gen, scale=0.15):
+    shapes = [(192, 64), (192,), (64, 64), (64,), (64,), (64,), (256, 64), (256,), (64, 256), (64,), (64,), (64,)]
+    ps = []
+    for k, s in enumerate(shapes):
+        t = torch.randn(s, generator=gen, dtype=torch.float64) * scale
+        if k in (4, 10):  # LayerNorm gammas around 1
+            t = 1.0 + t
+        ps.append(t)
+    return ps
+
+
+def _run(cuda, NS, L, drop, gelu=True, with_mask=True, seed=1234, counter=0):
+    from FoodRec.engine import ops
+    gen = torch.Generator().manual_seed(NS * 31 + L)
+    x = torch.randn(NS, L, 64, generator=gen, dtype=torch.float64)
+    mask = None
+    if with_mask:
+        pad = torch.rand(NS, L, generator=gen) < 0.4
+        pad[:, 0] = False
+        mask = torch.zeros(NS, L, dtype=torch.float64).masked_fill(pad, float("-inf"))
+    params = _params(gen)
+    gout = torch.randn(NS, L, 64, generator=gen, dtype=torch.float64)
+
+    cfg = ops.EncoderConfig((1e-5, 1e-5), drop, gelu, seed, cuda)
+    cfg.counter.fill_(counter)
+    xg = x.float().to(cuda).requires_grad_(True)
+    pg = [p.float().to(cuda).requires_grad_(True) for p in params]
+    out = ops.encoder_layer(xg, None if mask is None else mask.float().to(cuda), cfg, pg)
+    out.backward(gout.float().to(cuda))
+    assert int(cfg.counter.item()) == counter + 1
+
+    masks = O.encoder_keep_masks(seed, counter, NS, L, drop)
+    xr = x.clone().requires_grad_(True)
+    pr = [p.clone().requires_grad_(True) for p in params]
+    ref = O.encoder_layer_f64(xr, mask, pr, masks, drop, gelu=gelu)
+    ref.backward(gout)
+    return out, xg, pg, ref, xr, pr
+
+
+def _check(out, xg, pg, ref, xr, pr):
+    o = out.detach().double().cpu()
+    assert (o - ref.detach()).abs().max() <= 2e-5 * ref.abs().max() + 2e-6
+    names = ["x", "in_proj_weight", "in_proj_bias", "out_proj.weight", "out_proj.bias", "norm1.weight",
+             "norm1.bias", "linear1.weight", "linear1.bias", "linear2.weight", "linear2.bias", "norm2.weight",
+             "norm2.bias"]
+    for name, a, b in zip(names, [xg] + pg, [xr] + pr):
+        ga, gb = a.grad.double().cpu(), b.grad
+        assert (ga - gb).abs().max() <= 1e-4 * gb.abs().max() + 1e-6, name
+
+
+@pytest.mark.parametrize("NS,L", [(1024, 20), (1027, 20), (333, 16), (101, 8), (50, 5), (7, 20)])
+def test_encoder_layer_no_dropout(cuda, NS, L):
+    """p = 0 (the reference goldens' setting): outputs and all 13 gradients vs float64, including a
+    partial last workgroup (NS not a multiple of 80 / L)."""
+    _check(*_run(cuda, NS, L, (0.0, 0.0, 0.0, 0.0)))
+
+
+@pytest.mark.parametrize("gelu", [True, False])
+def test_encoder_layer_dropout_masks(cuda, gelu):
+    """p = 0.5 at all four sites (HealthRec's attention_probs_dropout_prob): the kernel's masks are
+    regenerated on the host from the same hash, so forward and backward match exactly-masked float64."""
+    _check(*_run(cuda, 257, 20, (0.5, 0.5, 0.5, 0.5), gelu=gelu, counter=7))
+
+
+def test_encoder_layer_mixed_dropout_no_mask(cuda):
+    _check(*_run(cuda, 96, 10, (0.1, 0.0, 0.3, 0.2), with_mask=False, seed=99, counter=3))
+
+
+def test_encoder_in_cuda_graph(cuda):
+    """Captured once, replayed twice: every replay reads the device counter, so masks differ
+    between replays and the backward of each replay uses its own forward's masks."""
+    from FoodRec.engine import ops
+    gen = torch.Generator().manual_seed(0)
+    params = [p.float().to(cuda).requires_grad_(True) for p in _params(gen)]
+    x = torch.randn(200, 20, 64, generator=gen).to(cuda).requires_grad_(True)
+    cfg = ops.EncoderConfig((1e-5, 1e-5), (0.5, 0.5, 0.5, 0.5), True, 77, cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):  # warm-up (allocator, autograd)
+            ops.encoder_layer(x, None, cfg, params).sum().backward()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    x.grad = None
+    with torch.cuda.graph(g):
+        out = ops.encoder_layer(x, None, cfg, params)
+        out.sum().backward()
+    outs, dxs = [], []
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        outs.append(out.detach().clone())
+        dxs.append(x.grad.detach().clone())
+    assert not torch.equal(outs[0], outs[1])
+    c = int(cfg.counter.item())
+    for k, (o, dx) in enumerate(zip(outs, dxs)):
+        masks = O.encoder_keep_masks(77, c - 2 + k, 200, 20, (0.5,) * 4)
+        xr = x.detach().double().cpu().requires_grad_(True)
+        pr = [p.detach().double().cpu() for p in params]
+        ref = O.encoder_layer_f64(xr, None, pr, masks, (0.5,) * 4)
+        ref.sum().backward()
+        assert (o.double().cpu() - ref.detach()).abs().max() <= 2e-5 * ref.abs().max() + 2e-6
+        assert (dx.double().cpu() - xr.grad).abs().max() <= 1e-4 * xr.grad.abs().max() + 1e-6
+
+
+def test_encoder_deterministic(cuda):
+    a = _run(cuda, 300, 20, (0.5, 0.5, 0.5, 0.5), counter=2)
+    b = _run(cuda, 300, 20, (0.5, 0.5, 0.5, 0.5), counter=2)
+    assert torch.equal(a[0], b[0])
+    for pa, pb in zip([a[1]] + a[2], [b[1]] + b[2]):
+        assert torch.equal(pa.grad, pb.grad)
