@@ -204,6 +204,13 @@ int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d);
 int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
                      int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
                      void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Row-gradient form of the same scatter (n <= 4096 positions): rmap[r] = the first position i with
+ * idx[i] == r (else -1; padding_idx rows get -1) and rows[i, :] = sum over positions j with
+ * idx[j] == r of grad[j, :] (fixed order, deterministic); rows of non-owner positions are left
+ * unwritten.  rmap: [num_rows] int32; rows: [n, d] fp32 (ld = d).  No dense table is touched. */
+int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                         int64_t num_rows, int64_t padding_idx, int32_t* d_rmap, float* d_rows, void* stream);
 /* byte offset, inside the workspace, of the int32 status word of the last fr_embedding_bwd on it:
  * 0 = consistent; non-zero bits name the step that met an out-of-range index on the device and
  * skipped that access instead of faulting (1 scan, 2 place, 4/8 bucket order, 16 segsum, 32 fix-up) */
@@ -276,6 +283,17 @@ int fr_bpr_bwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t* d_I, int64
                     int64_t B, int d, float gamma, float g_mf, float g_reg, const float* d_gscale,
                     uint16_t* d_dU, uint16_t* d_dI, uint16_t* d_dUe, uint16_t* d_dIe,
                     void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Row-gradient Adam: tensors whose gradient is g[r] = rmap[r] >= 0 ? rows[rmap[r]] : 0 (a [R, d]
+ * table gathered by rows on the step, d a power of two >= 4; rows/rmap from fr_embedding_rowgrad).
+ * Same per-element arithmetic as fr_adam_step_dev (bit-identical to the dense update with the dense
+ * zero-padded gradient) at 24 B instead of 28 B (+ the dense zero fill) per parameter.  Replaces
+ * torch.optim.Adam.step for HealthRec's image/text feature tables (cikm_model.py:83-87). */
+int fr_adam_step_rows(float* const* params, const float* const* grads, float* const* exp_avg,
+                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                      const int32_t* const* d_rmaps, const int32_t* row_dims, int n_tensors, const double* d_lr,
+                      double lr, double beta1, double beta2, double eps, double weight_decay,
+                      const int32_t* d_skip, void* stream);
 
 /* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
  * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as

@@ -257,6 +257,10 @@ class Trainer(AbstractTrainer):
         # capture the training step in a HIP graph (config key cuda_graph; GPU, single process)
         self.use_graph = bool(config["cuda_graph"]) and self._on_gpu()
         self._graphed = None
+        # row-gathered feature tables hand the optimiser (ids, rows) instead of a dense gradient
+        # (FusedAdam.row_grads; a data-parallel GradAllReduce installs its RowExchange instead)
+        if isinstance(self.optimizer, FusedAdam) and (config["row_grad_tables"] is None or config["row_grad_tables"]):
+            model._fr_exchange = self.optimizer.row_grads
 
     def _on_gpu(self) -> bool:
         return torch.device(self.device).type == "cuda"
@@ -319,6 +323,9 @@ class Trainer(AbstractTrainer):
             (-1 * self.alpha2 * l2).backward()
         else:
             loss.backward()
+        if self.clip_grad_norm or self.grad_hook is not None:
+            if isinstance(self.optimizer, FusedAdam):
+                self.optimizer.materialize_row_grads()  # dense .grad for the norm / the hook
         if self.clip_grad_norm:
             clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
         if self.grad_hook is not None:

@@ -71,10 +71,13 @@ class TransformerEncoderLayer(nn.TransformerEncoderLayer):
     def _fused_cfg(self, device):
         cfg = self.__dict__.get("_fr_encoder_cfg")
         if cfg is None or cfg.counter.device != device:
-            global _LAYER_ORDINAL
-            _LAYER_ORDINAL += 1
+            salt = self.__dict__.get("_fr_salt")  # the layer's index in its model (set by the model)
+            if salt is None:
+                global _LAYER_ORDINAL
+                _LAYER_ORDINAL += 1
+                salt = 1000 + _LAYER_ORDINAL
             # hash seed from the seeded torch state without consuming it (init parity), distinct per layer
-            seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + _LAYER_ORDINAL) & (2 ** 64 - 1)
+            seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + salt + 1) & (2 ** 64 - 1)
             cfg = ops.EncoderConfig((self.norm1.eps, self.norm2.eps),
                                     (self.self_attn.dropout, self.dropout1.p, self.dropout.p, self.dropout2.p),
                                     self.activation_relu_or_gelu == 2, seed, device)

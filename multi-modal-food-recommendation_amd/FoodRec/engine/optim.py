@@ -8,6 +8,14 @@ The step counters and the learning rate live in device memory (like torch's capt
 kernel increments each tensor's counter and derives the bias corrections on the device, so a
 whole training step (forward, backward, optimiser) can be captured in a HIP graph and replayed.
 After changing ``group['lr']`` outside of step() (LR scheduler), call :meth:`sync_lr`.
+
+Row gradients (``row_grads``): a table whose only use on the step is a row gather (HealthRec's
+45,630 x 2048 image and x 512 text tables) can hand its gradient to the optimiser as the gathered
+(ids, rows) instead of a dense zero-filled table (``ops.embedding(..., exchange=opt.row_grads)``).
+``step()`` reduces them with ``fr_embedding_rowgrad`` (a row -> slot map plus one summed row per
+distinct id) and ``fr_adam_step_rows`` applies Adam to every row with the gradient read from the
+compact rows (zero elsewhere): the same arithmetic as the dense update, bit for bit, without the
+dense table's zero fill and gradient read (8 of 32 bytes per parameter).
 """
 from __future__ import annotations
 
@@ -18,6 +26,49 @@ import torch
 from . import native, profiling
 
 
+ROW_GRAD_MAX = 4096  # positions per table per step the row-gradient reduction takes (fr_embedding_rowgrad)
+
+
+def adam_rows_bytes(numel: int, rows: int, compact: int) -> int:
+    """Algorithmic HBM bytes of the row-gradient Adam on one table: p, m, v read + written (24 B per
+    parameter), the row map (4 B per row) and the compact gradient rows (read once)."""
+    return 24 * numel + 4 * rows + 4 * compact
+
+
+class RowGrads:
+    """Pending row gradients of row-gathered tables: ``stash`` is called from the backward of
+    ``ops.embedding(..., exchange=self)``; several stashes of one table before a step (repeated
+    backward passes) accumulate, exactly as dense gradients would."""
+
+    def __init__(self):
+        self.pending = {}  # id(weight) -> [weight, padding_idx, [ids], [rows]]
+
+    def stash(self, weight, padding_idx, ids, G):
+        e = self.pending.get(id(weight))
+        if e is None:
+            self.pending[id(weight)] = [weight, padding_idx, [ids], [G]]
+        else:
+            e[2].append(ids)
+            e[3].append(G)
+
+    def clear(self):
+        self.pending.clear()
+
+    def take(self, weight):
+        e = self.pending.pop(id(weight), None)
+        if e is None:
+            return None
+        ids = e[2][0] if len(e[2]) == 1 else torch.cat(e[2])
+        G = e[3][0] if len(e[3]) == 1 else torch.cat(e[3])
+        return ids, G, e[1]
+
+
+def _row_grad_ok(p, ids, G) -> bool:
+    d = p.shape[-1] if p.dim() == 2 else 0
+    return (p.dim() == 2 and p.dtype == torch.float32 and p.is_contiguous() and d >= 4 and d & (d - 1) == 0
+            and ids.numel() <= ROW_GRAD_MAX and G.dtype == torch.float32 and p.data_ptr() % 16 == 0)
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
@@ -25,6 +76,21 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       amsgrad=False, maximize=False))
         self._d_lr = {}   # group index -> (device float64 lr, host value it holds)
+        self.row_grads = RowGrads()
+
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none=set_to_none)
+        self.row_grads.clear()
+
+    @torch.no_grad()
+    def materialize_row_grads(self):
+        """Turn pending row gradients into dense ``.grad`` tensors (accumulating), for callers that
+        read or clip gradients between backward and step."""
+        from . import ops
+        for w, pad, ids, G in list(self.row_grads.pending.values()):
+            ids, G, pad = self.row_grads.take(w)
+            dense = ops.scatter_rows(ids.reshape(-1), G.reshape(-1, w.shape[-1]), w.shape[0], pad)
+            w.grad = dense if w.grad is None else w.grad.add_(dense)
 
     def _lr_tensor(self, gi, group, device):
         t, held = self._d_lr.get(gi, (None, None))
@@ -58,11 +124,17 @@ class FusedAdam(torch.optim.Optimizer):
         lib = native.lib()
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
-            plist = []
+            plist, rows = [], []
             for p in group["params"]:
-                if p.grad is None:
+                rg = self.row_grads.take(p) if self.row_grads.pending else None
+                if rg is not None and (p.grad is not None or not _row_grad_ok(p, rg[0], rg[1])):
+                    from . import ops  # dense fallback: scatter the rows into (or onto) .grad
+                    dense = ops.scatter_rows(rg[0].reshape(-1), rg[1].reshape(-1, p.shape[-1]), p.shape[0], rg[2])
+                    p.grad = dense if p.grad is None else p.grad.add_(dense)
+                    rg = None
+                if p.grad is None and rg is None:
                     continue
-                if p.grad.is_sparse:
+                if p.grad is not None and p.grad.is_sparse:
                     raise RuntimeError("FusedAdam does not support sparse gradients")
                 native.require_device(p)
                 if not p.is_contiguous():
@@ -83,24 +155,63 @@ class FusedAdam(torch.optim.Optimizer):
                     continue
                 if p.dtype != torch.float32:
                     raise RuntimeError(f"FusedAdam supports fp32 and bf16 parameters (got {p.dtype})")
-                plist.append(p)
-            if not plist:
+                if rg is not None:
+                    rows.append((p, rg))
+                else:
+                    plist.append(p)
+            if not plist and not rows:
                 continue
-            grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in plist]
-            n = len(plist)
-            P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in plist])
-            G = (ctypes.c_void_p * n)(*[g.data_ptr() for g in grads])
-            M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in plist])
-            V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in plist])
-            S = (ctypes.c_void_p * n)(*[self.state[p]["step"].data_ptr() for p in plist])
-            N = (ctypes.c_int64 * n)(*[p.numel() for p in plist])
-            d_lr = self._lr_tensor(gi, group, plist[0].device)
-            with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
-                native.check(lib.fr_adam_step_dev(
-                    P, G, M, V, S, N, n, d_lr.data_ptr(), float(group["lr"]), float(beta1), float(beta2),
-                    float(group["eps"]), float(group["weight_decay"]), native.ptr(skip_flag),
-                    native.stream_of(plist[0])), "fr_adam_step_dev")
+            dev = (plist or [rows[0][0]])[0].device
+            d_lr = self._lr_tensor(gi, group, dev)
+            hyper = (d_lr.data_ptr(), float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
+                     float(group["weight_decay"]), native.ptr(skip_flag), torch.cuda.current_stream(dev).cuda_stream)
+            if plist:
+                with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
+                    self._launch_dense(lib, plist, hyper)
+            if rows:
+                self._launch_rows(lib, rows, hyper)
         return loss
+
+    def _arrays(self, plist, grads):
+        n = len(plist)
+        P = (ctypes.c_void_p * n)(*[p.data_ptr() for p in plist])
+        G = (ctypes.c_void_p * n)(*[g.data_ptr() for g in grads])
+        M = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg"].data_ptr() for p in plist])
+        V = (ctypes.c_void_p * n)(*[self.state[p]["exp_avg_sq"].data_ptr() for p in plist])
+        S = (ctypes.c_void_p * n)(*[self.state[p]["step"].data_ptr() for p in plist])
+        N = (ctypes.c_int64 * n)(*[p.numel() for p in plist])
+        return P, G, M, V, S, N
+
+    def _launch_dense(self, lib, plist, hyper):
+        grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in plist]
+        P, G, M, V, S, N = self._arrays(plist, grads)
+        native.check(lib.fr_adam_step_dev(P, G, M, V, S, N, len(plist), *hyper), "fr_adam_step_dev")
+
+    def _launch_rows(self, lib, rows, hyper):
+        plist, compact, maps, dims = [], [], [], []
+        for p, (ids, G, pad) in rows:
+            R, d = p.shape
+            ids = ids.reshape(-1)
+            G = G.reshape(-1, d)
+            if G.stride(1) != 1 or G.stride(0) % 4 or G.data_ptr() % 16:
+                G = G.contiguous()
+            rmap = torch.empty(R, dtype=torch.int32, device=p.device)
+            crow = torch.empty(max(ids.numel(), 1), d, dtype=torch.float32, device=p.device)
+            with profiling.region("embedding_rowgrad", 4 * R + 8 * ids.numel() + 8 * G.numel()):
+                native.check(lib.fr_embedding_rowgrad(ids.data_ptr(), ids.numel(), G.data_ptr(), G.stride(0), d, R,
+                                                      -1 if pad is None else int(pad), rmap.data_ptr(),
+                                                      crow.data_ptr(), native.stream_of(p)), "fr_embedding_rowgrad")
+            plist.append(p)
+            compact.append(crow)
+            maps.append(rmap)
+            dims.append(d)
+        P, G, M, V, S, N = self._arrays(plist, compact)
+        n = len(plist)
+        RM = (ctypes.c_void_p * n)(*[m.data_ptr() for m in maps])
+        RD = (ctypes.c_int32 * n)(*dims)
+        with profiling.region("adam_rows", sum(adam_rows_bytes(p.numel(), p.shape[0], c.numel())
+                                              for p, c in zip(plist, compact))):
+            native.check(lib.fr_adam_step_rows(P, G, M, V, S, N, RM, RD, n, *hyper), "fr_adam_step_rows")
 
     def _step_bf16(self, p, group, lib, skip_flag, gi):
         """bf16 parameter: update the fp32 master with fp32 moments, re-round the parameter."""

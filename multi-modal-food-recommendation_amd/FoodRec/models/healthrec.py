@@ -86,6 +86,8 @@ class HealthRec(GeneralRecommender):
                                                         activation=config["hidden_act"])
         self.ingr_encoder = nn.TransformerEncoder(self.encoder_layer, num_layers=config["num_hidden_layers"],
                                                   enable_nested_tensor=False)
+        for k, layer in enumerate(self.ingr_encoder.layers):  # dropout-hash salt of the fused layer
+            layer.__dict__["_fr_salt"] = k
         self.mm_target_atten = TargetAttention(d, d, config["num_attention_heads"], False, "ln", self.n_ingredients)
         self.ingre_target_atten = TargetAttention(d, d, config["num_attention_heads"], False, "ln", self.n_ingredients)
         self.health_mlp = nn.Sequential(nn.Linear(d, d), nn.ReLU(), nn.Linear(d, self.n_health_level))

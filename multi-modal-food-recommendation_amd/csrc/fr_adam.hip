@@ -18,7 +18,7 @@
 
 namespace {
 
-constexpr int kMaxTensors = 48;  // AdamArgs = 48 x 56 B + 4 B < the 4 KiB kernel-argument limit
+constexpr int kMaxTensors = 48;  // AdamArgs = 48 x 68 B + 8 B < the 4 KiB kernel-argument limit
 constexpr int kChunk = 8192;  // elements per (tensor, chunk) work item
 constexpr int kAdamBlocks = fr::kNumCU * 5;  // persistent grid: 5 blocks/CU = the 84-VGPR occupancy
 
@@ -31,6 +31,10 @@ struct AdamArgs {
   int64_t numel[kMaxTensors];
   int32_t blk_start[kMaxTensors + 1];
   int32_t vec4[kMaxTensors];
+  // row-gradient tensors (rmap != null): the parameter is a [R, 2^rshift] table whose gradient is
+  // g[r] = rmap[r] >= 0 ? G[rmap[r]] : 0 (compact rows from fr_embedding_rowgrad)
+  const int32_t* rmap[kMaxTensors];
+  int32_t rshift[kMaxTensors];
   int n;
 };
 
@@ -85,6 +89,7 @@ __device__ __forceinline__ void adam4(float* P, const float* G, float* M, float*
 
 // Persistent grid over the launch's (tensor, chunk) list; the step-dependent scalars are derived
 // once per tensor a block meets.  Each thread keeps two float4 quartets (p, g, m, v) in flight.
+template <bool ROWS>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
   const int total = a.blk_start[a.n];
@@ -110,7 +115,29 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
     const float* __restrict__ G = a.g[t];
     float* __restrict__ M = a.m[t];
     float* __restrict__ V = a.v[t];
-    if (a.vec4[t]) {
+    if constexpr (ROWS) {  // row gradient: p, m, v streamed; g from the compact rows of this step's batch
+      const int32_t* __restrict__ rm = a.rmap[t];
+      const int sh = a.rshift[t];
+      const int64_t cmask = ((int64_t)1 << sh) - 1;
+      auto grad4 = [&](int64_t i) {
+        const int32_t slot = rm[i >> sh];
+        return slot >= 0 ? *reinterpret_cast<const float4*>(G + ((int64_t)slot << sh) + (i & cmask))
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      };
+      constexpr int64_t kStride = 4 * 256;
+      int64_t i = base + 4 * threadIdx.x;
+      for (; i + kStride < end; i += 2 * kStride) {  // two quartets in flight (end - base is a multiple of 4)
+        const int64_t i1 = i + kStride;
+        float4 p0 = nt_load4(P + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i), g0 = grad4(i);
+        float4 p1 = nt_load4(P + i1), m1 = nt_load4(M + i1), v1 = nt_load4(V + i1), g1 = grad4(i1);
+        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+        adam4(P, G, M, V, i1, h, p1, g1, m1, v1);
+      }
+      for (; i < end; i += kStride) {
+        float4 p0 = nt_load4(P + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i), g0 = grad4(i);
+        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+      }
+    } else if (a.vec4[t]) {
       constexpr int64_t kStride = 4 * 256;
       int64_t i = base + 4 * threadIdx.x;
       for (; i + kStride + 3 < end; i += 2 * kStride) {
@@ -185,7 +212,7 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                      int n_tensors, double lr, const double* d_lr, double beta1, double beta2,
                      double eps, double weight_decay, int64_t step, const int32_t* d_skip,
-                     void* stream) {
+                     void* stream, const int32_t* const* rmaps = nullptr, const int32_t* row_dims = nullptr) {
   FR_REQUIRE(n_tensors >= 0, "n_tensors < 0");
   if (n_tensors == 0) return FR_OK;
   FR_REQUIRE(params && grads && exp_avg && exp_avg_sq && numel, "null host array");
@@ -208,38 +235,60 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
   h.bc2_sqrt = (float)std::sqrt(bc2);
   h.eps = (float)eps;
   h.wd = (float)weight_decay;
-  for (int t0 = 0; t0 < n_tensors; t0 += kMaxTensors) {
-    AdamArgs a{};
-    a.n = 0;
-    int32_t blocks = 0;
-    for (int t = t0; t < std::min(n_tensors, t0 + kMaxTensors); ++t) {
-      FR_REQUIRE(numel[t] >= 0, "numel < 0");
-      if (numel[t] == 0) continue;
-      FR_REQUIRE(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t], "null tensor pointer");
-      const int k = a.n++;
-      a.p[k] = params[t];
-      a.g[k] = grads[t];
-      a.m[k] = exp_avg[t];
-      a.v[k] = exp_avg_sq[t];
-      a.step[k] = d_steps ? d_steps[t] : nullptr;
-      FR_REQUIRE(!d_steps || d_steps[t], "null step counter");
-      a.numel[k] = numel[t];
-      a.vec4[k] = fr::aligned16(params[t]) && fr::aligned16(grads[t]) && fr::aligned16(exp_avg[t]) &&
-                  fr::aligned16(exp_avg_sq[t]);
-      a.blk_start[k] = blocks;
-      const int64_t nb = fr::ceil_div(numel[t], kChunk);
-      FR_REQUIRE(blocks + nb < INT32_MAX, "tensor too large for one launch");
-      blocks += (int32_t)nb;
-    }
-    a.blk_start[a.n] = blocks;
-    if (a.n == 0) continue;
-    if (d_steps) {
-      hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, s, a, d_skip);
+  // dense tensors and row-gradient tensors go to separate launches (separate register budgets)
+  for (int rows_pass = 0; rows_pass < 2; ++rows_pass) {
+    int idx[kMaxTensors];
+    int t = 0;
+    while (t < n_tensors) {
+      AdamArgs a{};
+      a.n = 0;
+      int32_t blocks = 0;
+      for (; t < n_tensors && a.n < kMaxTensors; ++t) {
+        const bool is_rows = rmaps && rmaps[t];
+        if (is_rows != (rows_pass == 1)) continue;
+        FR_REQUIRE(numel[t] >= 0, "numel < 0");
+        if (numel[t] == 0) continue;
+        FR_REQUIRE(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t], "null tensor pointer");
+        const int k = a.n++;
+        idx[k] = t;
+        a.p[k] = params[t];
+        a.g[k] = grads[t];
+        a.m[k] = exp_avg[t];
+        a.v[k] = exp_avg_sq[t];
+        a.step[k] = d_steps ? d_steps[t] : nullptr;
+        FR_REQUIRE(!d_steps || d_steps[t], "null step counter");
+        a.numel[k] = numel[t];
+        a.vec4[k] = fr::aligned16(params[t]) && fr::aligned16(grads[t]) && fr::aligned16(exp_avg[t]) &&
+                    fr::aligned16(exp_avg_sq[t]);
+        a.rmap[k] = is_rows ? rmaps[t] : nullptr;
+        a.rshift[k] = 0;
+        if (is_rows) {
+          const int32_t dd = row_dims[t];
+          FR_REQUIRE(dd >= 4 && (dd & (dd - 1)) == 0 && numel[t] % dd == 0,
+                     "row-gradient tensors need a power-of-two row width >= 4");
+          FR_REQUIRE(a.vec4[k], "row-gradient tensors must be 16-byte aligned");
+          while ((1 << a.rshift[k]) < dd) ++a.rshift[k];
+        }
+        a.blk_start[k] = blocks;
+        const int64_t nb = fr::ceil_div(numel[t], kChunk);
+        FR_REQUIRE(blocks + nb < INT32_MAX, "tensor too large for one launch");
+        blocks += (int32_t)nb;
+      }
+      a.blk_start[a.n] = blocks;
+      if (a.n == 0) continue;
+      (void)idx;
+      if (d_steps) {
+        hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, s, a, d_skip);
+        FR_LAUNCH_CHECK();
+      }
+      if (rows_pass)
+        hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0, s,
+                           a, h, d_skip);
+      else
+        hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0,
+                           s, a, h, d_skip);
       FR_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0, s, a, h,
-                       d_skip);
-    FR_LAUNCH_CHECK();
   }
   return FR_OK;
 }
@@ -260,6 +309,16 @@ extern "C" int fr_adam_step_dev(float* const* params, const float* const* grads,
   FR_REQUIRE(d_steps, "d_steps (device step counters) required");
   return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1,
                    beta2, eps, weight_decay, 0, d_skip, stream);
+}
+
+extern "C" int fr_adam_step_rows(float* const* params, const float* const* grads, float* const* exp_avg,
+                                 float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                                 const int32_t* const* d_rmaps, const int32_t* row_dims, int n_tensors,
+                                 const double* d_lr, double lr, double beta1, double beta2, double eps,
+                                 double weight_decay, const int32_t* d_skip, void* stream) {
+  FR_REQUIRE(d_steps && d_rmaps && row_dims, "d_steps, d_rmaps and row_dims required");
+  return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1, beta2, eps,
+                   weight_decay, 0, d_skip, stream, d_rmaps, row_dims);
 }
 
 extern "C" int fr_adam_step_bf16(uint16_t* d_param, float* d_master, const uint16_t* d_grad, float* d_exp_avg,

@@ -195,12 +195,20 @@ __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cu
 // Small batches (n <= kOwnerMax, e.g. 2B item ids into a 45k-row feature table): no sort.  Every
 // block stages all ids in LDS; the group of position i owns row idx[i] when no earlier position
 // has it, and sums that row's positions in order (matches gathered 16 at a time, loads in flight
-// together).  dW was zero-filled by the previous launch.
+// together).  Dense mode (rmap == null): the sum goes to dW[r], zero-filled by the previous launch.
+// Row-gradient mode: the sum goes to compact slot i (out[i]) and rmap[r] = i (rmap was filled with
+// -1 by the previous launch), the form fr_adam_step_rows consumes.
 constexpr int kOwnerMax = 4096;
+
+__global__ __launch_bounds__(256) void emb_rmap_fill_kernel(int32_t* __restrict__ rmap, int64_t R) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (int64_t)gridDim.x * blockDim.x)
+    rmap[i] = -1;
+}
 
 __global__ __launch_bounds__(256) void emb_owner_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t R,
                                                         int64_t pad, const float4* __restrict__ G4, int64_t ldg4,
-                                                        int d4, float4* __restrict__ out, int64_t ldo4) {
+                                                        int d4, float4* __restrict__ out, int64_t ldo4,
+                                                        int32_t* __restrict__ rmap) {
   __shared__ int ids[kOwnerMax];
   for (int64_t i = threadIdx.x; i < n; i += 256) ids[i] = emb_key(idx, i, n, R, pad);
   __syncthreads();
@@ -230,7 +238,12 @@ __global__ __launch_bounds__(256) void emb_owner_kernel(const int64_t* __restric
     for (int k = 0; k < LPR; ++k)
       if ((mask >> k) & 1u) acc = f4_add(acc, x[k]);
   }
-  if (qok) out[(int64_t)r * ldo4 + q] = acc;
+  if (rmap) {
+    if (blockIdx.y == 0 && lig == 0) rmap[r] = (int32_t)i;
+    if (qok) out[i * ldo4 + q] = acc;
+  } else if (qok) {
+    out[(int64_t)r * ldo4 + q] = acc;
+  }
 }
 
 // 3. placement (the wave's hot row takes one cursor atomic and ranks by lane)
@@ -503,7 +516,7 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
     if (n > 0) {
       hipLaunchKernelGGL(emb_owner_kernel, dim3((unsigned)fr::ceil_div(n, GPB), (unsigned)fr::ceil_div(d4, LPR)),
                          dim3(256), 0, s, d_idx, n, R, padding_idx, reinterpret_cast<const float4*>(d_grad),
-                         ldg / 4, d4, reinterpret_cast<float4*>(d_out), ldo / 4);
+                         ldg / 4, d4, reinterpret_cast<float4*>(d_out), ldo / 4, nullptr);
       FR_LAUNCH_CHECK();
     }
     return FR_OK;
@@ -552,5 +565,28 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   hipLaunchKernelGGL(emb_fixup_kernel, dim3((unsigned)nch, slices), dim3(256), 0, s, d_idx, w.sorted, w.start, R,
                      d4, reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl, n, nch, w.cursor + R + 1);
   FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                                    int64_t num_rows, int64_t padding_idx, int32_t* d_rmap, float* d_rows,
+                                    void* stream) {
+  FR_REQUIRE(n >= 0 && n <= kOwnerMax, "n out of range [0, 4096]");
+  FR_REQUIRE(num_rows > 0 && num_rows < INT32_MAX && d_rmap, "bad row map");
+  FR_REQUIRE(d > 0 && d % 4 == 0, "d must be a positive multiple of 4");
+  FR_REQUIRE(n == 0 || (d_idx && d_grad && d_rows && ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad) &&
+                        fr::aligned16(d_rows)),
+             "bad grad / index / row arguments");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int d4 = d / 4;
+  hipLaunchKernelGGL(emb_rmap_fill_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(num_rows, 256), 1024)),
+                     dim3(256), 0, s, d_rmap, num_rows);
+  FR_LAUNCH_CHECK();
+  if (n > 0) {
+    hipLaunchKernelGGL(emb_owner_kernel, dim3((unsigned)fr::ceil_div(n, GPB), (unsigned)fr::ceil_div(d4, LPR)),
+                       dim3(256), 0, s, d_idx, n, num_rows, padding_idx, reinterpret_cast<const float4*>(d_grad),
+                       ldg / 4, d4, reinterpret_cast<float4*>(d_rows), (int64_t)d4, d_rmap);
+    FR_LAUNCH_CHECK();
+  }
   return FR_OK;
 }

@@ -1,0 +1,130 @@
+"""Row gradients of row-gathered tables (fr_embedding_rowgrad + fr_adam_step_rows) vs the dense path.
+
+HealthRec's image / text feature tables (cikm_model.py:83-87) are only row-gathered on the step, so
+FusedAdam takes their gradient as (row -> slot map, one summed row per distinct id).  Bar: the
+parameters and both Adam moments after several steps are BIT-IDENTICAL to the dense-gradient
+update (same per-row sums in the same order, zero gradient elsewhere), and the compact rows equal
+the float64 scatter of the oracle within 1e-6 of each row's sum of |G| (fp32 summation).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(R, d, n, pad, seed):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, R, (n,), generator=g)
+    ids[: n // 10] = ids[n // 2]  # a hot row
+    if pad is not None:
+        ids[1::17] = pad
+    G = torch.randn(n, d, generator=g)
+    return ids, G
+
+
+@pytest.mark.parametrize("R,d,n,pad", [(45630, 2048, 1024, None), (45630, 512, 1024, None), (1000, 64, 4096, 7),
+                                       (300, 4, 1, None)])
+def test_rowgrad_matches_scatter(cuda, R, d, n, pad):
+    from FoodRec.engine import native
+    ids, G = _case(R, d, n, pad, 1)
+    idg, Gg = ids.to(cuda), G.to(cuda)
+    rmap = torch.empty(R, dtype=torch.int32, device=cuda)
+    rows = torch.empty(n, d, device=cuda)
+    native.check(native.lib().fr_embedding_rowgrad(idg.data_ptr(), n, Gg.data_ptr(), d, d, R,
+                                                   -1 if pad is None else pad, rmap.data_ptr(), rows.data_ptr(),
+                                                   torch.cuda.current_stream().cuda_stream), "rowgrad")
+    ref = O.embedding_bwd_f64(ids.numpy(), G.numpy(), R, pad)
+    rm = rmap.cpu().numpy()
+    present = np.unique(ids.numpy()[ids.numpy() != (-1 if pad is None else pad)])
+    assert set(np.nonzero(rm >= 0)[0].tolist()) == set(present.tolist())
+    # the slot of a row is its first position
+    first = {}
+    for i, r in enumerate(ids.numpy().tolist()):
+        first.setdefault(r, i)
+    assert all(rm[r] == first[r] for r in present.tolist())
+    got = rows.cpu().numpy()[rm[present]]
+    scale = O.embedding_bwd_f64(ids.numpy(), np.abs(G.numpy()), R, pad)[present]  # sum of |G| per row
+    assert np.all(np.abs(got - ref[present]) <= 1e-6 * scale + 1e-7)
+
+
+@pytest.mark.parametrize("d", [2048, 64])
+def test_row_adam_bit_identical_to_dense(cuda, d):
+    from FoodRec.engine import ops
+    from FoodRec.engine.optim import FusedAdam
+    R, n = 5000, 1024
+    torch.manual_seed(0)
+    w0 = torch.randn(R, d) * 0.1
+    extra = torch.randn(33, 7)  # a dense parameter in the same step
+    pa, pb = (torch.nn.Parameter(w0.clone().to(cuda)) for _ in range(2))
+    ea, eb = (torch.nn.Parameter(extra.clone().to(cuda)) for _ in range(2))
+    oa, ob = FusedAdam([pa, ea], lr=3e-3), FusedAdam([pb, eb], lr=3e-3)
+    for step in range(3):
+        ids, G = _case(R, d, n, 11, 10 + step)
+        idg, Gg = ids.to(cuda), G.to(cuda)
+        ge = torch.randn(33, 7, generator=torch.Generator().manual_seed(step)).to(cuda)
+        oa.zero_grad()
+        pa.grad = ops.scatter_rows(idg, Gg, R, 11)  # dense path
+        ea.grad = ge.clone()
+        oa.step()
+        ob.zero_grad()
+        ob.row_grads.stash(pb, 11, idg, Gg)      # row path
+        eb.grad = ge.clone()
+        ob.step()
+        assert torch.equal(pa, pb), step
+        assert torch.equal(oa.state[pa]["exp_avg"], ob.state[pb]["exp_avg"])
+        assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
+        assert torch.equal(ea, eb)
+
+
+def test_row_adam_accumulates_like_dense(cuda):
+    from FoodRec.engine import ops
+    from FoodRec.engine.optim import FusedAdam
+    R, d = 777, 128
+    torch.manual_seed(1)
+    w0 = torch.randn(R, d)
+    pa, pb = (torch.nn.Parameter(w0.clone().to(cuda)) for _ in range(2))
+    oa, ob = FusedAdam([pa], lr=1e-2), FusedAdam([pb], lr=1e-2)
+    ids1, G1 = _case(R, d, 500, None, 3)
+    ids2, G2 = _case(R, d, 300, None, 4)
+    i1, g1, i2, g2 = ids1.to(cuda), G1.to(cuda), ids2.to(cuda), G2.to(cuda)
+    oa.zero_grad()
+    pa.grad = ops.scatter_rows(torch.cat([i1, i2]), torch.cat([g1, g2]), R, None)
+    oa.step()
+    ob.zero_grad()
+    ob.row_grads.stash(pb, None, i1, g1)
+    ob.row_grads.stash(pb, None, i2, g2)
+    ob.step()
+    assert torch.equal(pa, pb)
+    assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
+
+
+def test_healthrec_step_row_vs_dense(cuda):
+    """One HealthRec training step with row_grad_tables on and off.  The image / text tables and
+    their Adam moments are bit-identical; every other parameter agrees to 1e-6 relative (the BPR
+    gradient scatter uses float atomics, so two runs differ in the last bits there)."""
+    from helpers import golden, tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("model_CIKM_Model.npz")
+    batch = {k[len("batch/"):]: torch.from_numpy(g[k]).to(cuda) for k in g.files if k.startswith("batch/")}
+    runs = []
+    for rows in (True, False):
+        cfg = tiny_config("CIKM_Model", True, row_grad_tables=rows, cuda_graph=False)
+        data = tiny_data(cfg)
+        init_seed(999)
+        model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
+        tr = Trainer(cfg, model)
+        assert (model.__dict__.get("_fr_exchange") is tr.optimizer.row_grads) == rows
+        tr.train_step(batch, 0, tr.new_step_state())
+        runs.append((model, tr.optimizer))
+    (ma, oa), (mb, ob) = runs
+    for (k, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+        if k.startswith(("image_embedding", "text_embedding")):
+            assert torch.equal(a, b), k
+            for s_ in ("exp_avg", "exp_avg_sq"):
+                assert torch.equal(oa.state[a][s_], ob.state[b][s_]), (k, s_)
+        else:
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), k

@@ -12,7 +12,9 @@ if max_steps is not None:
     args = [a for a in args if a != str(max_steps)]
 rows = list(csv.DictReader(open(args[0])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-adam = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("(anonymous namespace)::adam_kernel")]
+# one optimiser launch per step marks the step: the row-gradient Adam when present, else the dense one
+adam = ([i for i, r in enumerate(rows) if "::adam_kernel<true>" in r["Kernel_Name"]]
+        or [i for i, r in enumerate(rows) if "::adam_kernel" in r["Kernel_Name"]])
 # step groups: Adam launches of one step are back-to-back
 groups = [[adam[0]]]
 for a, b in zip(adam, adam[1:]):
