@@ -367,6 +367,30 @@ int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, i
                    const float* d_st2, float* d_dx,
                    float* d_grad, float* d_partials, int64_t partial_floats, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Fused modal fusion of HealthRec (models/cikm_model.py:245-249 with target_attention_layer,
+ * :311-369), per item i of the 2B batch items:
+ *   item_health = target_attention(Q_i, E_i, E_i, key mask ids_i == pad_id)   (mm_target_atten)
+ *   item_mm     = target_attention(E_i, Q_i, Q_i)                            (ingre_target_atten)
+ *   know[i]     = F.normalize(item_mm, dim=1).sum(1) / num[i]
+ *   hin[i]      = F.normalize(item_health, dim=1).mean(1)        (input of the health MLP)
+ * target_attention: 2 heads of 32 (chunk/cat), LayerNorm(32, eps) on the q and k heads, scores
+ * q k^T / sqrt(32), padded keys -> -(2^32 - 1), softmax, @ v.  d_enc [n, L, 64] (encoder output),
+ * d_query [n, 2, 64] (image / text projections), d_ids [n, L] int64, d_num [n] int64;
+ * d_ln: 4 device pointers {mm_target_atten.ln.weight, .bias, ingre_target_atten.ln.weight, .bias}
+ * (both with the same eps).  L in {4, 5, 8, 10, 16, 20}.
+ * Backward recomputes the forward and writes d_denc, d_dquery and d_dln (float [4][32]: the four
+ * LayerNorm parameter gradients, block partials in d_partials summed in block order).
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_modal_fusion_partials(int64_t n_items);
+int fr_modal_fusion_fwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
+                        int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, float* d_know,
+                        float* d_hin, void* stream);
+int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
+                        int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps,
+                        const float* d_dknow, const float* d_dhin, float* d_denc, float* d_dquery, float* d_dln,
+                        float* d_partials, int64_t partial_floats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

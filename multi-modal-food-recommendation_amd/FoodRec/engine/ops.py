@@ -568,6 +568,64 @@ def encoder_layer(x: torch.Tensor, mask, cfg: EncoderConfig, params) -> torch.Te
     return _EncoderLayer.apply(x, mask, cfg, *params)
 
 
+# ----------------------------------------------------------------------------- modal fusion
+def fusion_bytes(n: int, L: int, backward: bool) -> int:
+    """Algorithmic HBM bytes: encoder rows, modal queries, ids, counts read; know / hin written
+    (forward) or their gradients read and d_enc / d_query written (backward)."""
+    base = 4 * n * (L * 64 + 2 * 64) + 8 * n * (L + 1)
+    return base + (4 * n * 64 * 2) + ((4 * n * (L * 64 + 2 * 64)) if backward else 0)
+
+
+class _ModalFusion(torch.autograd.Function):
+    """fr_modal_fusion_fwd / _bwd: both HealthRec target attentions + the normalize heads."""
+
+    @staticmethod
+    def forward(ctx, enc, query, ids, num, pad_id, eps, ga, ba, gb, bb):
+        n, L, _ = enc.shape
+        know = torch.empty(n, 64, dtype=torch.float32, device=enc.device)
+        hin = torch.empty_like(know)
+        lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
+        with profiling.region("modal_fusion", fusion_bytes(n, L, False)):
+            native.check(native.lib().fr_modal_fusion_fwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(),
+                                                          num.data_ptr(), int(pad_id), n, L, lnp, float(eps),
+                                                          know.data_ptr(), hin.data_ptr(), native.stream_of(enc)),
+                         "fr_modal_fusion_fwd")
+        ctx.save_for_backward(enc, query, ids, num, ga, ba, gb, bb)
+        ctx.pad_id, ctx.eps = int(pad_id), float(eps)
+        return know, hin
+
+    @staticmethod
+    def backward(ctx, dknow, dhin):
+        enc, query, ids, num, ga, ba, gb, bb = ctx.saved_tensors
+        n, L, _ = enc.shape
+        dknow = torch.zeros(n, 64, dtype=torch.float32, device=enc.device) if dknow is None else dknow.contiguous()
+        dhin = torch.zeros(n, 64, dtype=torch.float32, device=enc.device) if dhin is None else dhin.contiguous()
+        denc = torch.empty_like(enc)
+        dq = torch.empty_like(query)
+        dln = torch.empty(4, 32, dtype=torch.float32, device=enc.device)
+        lib = native.lib()
+        nparts = lib.fr_modal_fusion_partials(n)
+        part = torch.empty(nparts, dtype=torch.float32, device=enc.device)
+        lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
+        with profiling.region("modal_fusion", fusion_bytes(n, L, True)):
+            native.check(lib.fr_modal_fusion_bwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
+                                                 ctx.pad_id, n, L, lnp, ctx.eps, dknow.data_ptr(), dhin.data_ptr(),
+                                                 denc.data_ptr(), dq.data_ptr(), dln.data_ptr(), part.data_ptr(),
+                                                 nparts, native.stream_of(enc)), "fr_modal_fusion_bwd")
+        return denc, dq, None, None, None, None, dln[0], dln[1], dln[2], dln[3]
+
+
+def modal_fusion(enc, query, ids, num, pad_id, ln_a, ln_b):
+    """HealthRec's two target attentions + F.normalize heads (cikm_model.py:245-249) fused:
+    returns (item_know [n, 64], health-MLP input [n, 64]).  ``ln_a`` / ``ln_b``: the LayerNorm(32)
+    modules of mm_target_atten / ingre_target_atten."""
+    native.require_device(enc, query, ids)
+    if ln_a.eps != ln_b.eps:
+        raise native.EngineError("modal_fusion: both target-attention LayerNorms must share eps")
+    return _ModalFusion.apply(enc.contiguous(), query.contiguous(), ids.contiguous(), num.contiguous(), pad_id,
+                              ln_a.eps, ln_a.weight, ln_a.bias, ln_b.weight, ln_b.bias)
+
+
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod

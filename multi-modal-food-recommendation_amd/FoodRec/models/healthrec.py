@@ -15,6 +15,8 @@ reference's.  Execution differs where the math allows:
   with the reference's exact quirks (F.normalize over dim=1, raw ingre_embedding for the
   encoder, padding mask constant -(2**32)+1, KD threshold via max(0, kd - thr)).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -25,6 +27,9 @@ from FoodRec.common.init import xavier_uniform_initialization
 from FoodRec.common.loss import BPRLoss, EmbLoss
 from FoodRec.engine import layers, ops
 from FoodRec.models._graphs import side_adjacency, ui_adjacency
+
+# FR_FUSED_FUSION=0 keeps the unfused (torch + engine ops) target-attention path for A/B comparisons
+FUSED_FUSION = os.environ.get("FR_FUSED_FUSION", "1") != "0"
 
 
 class TargetAttention(nn.Module):
@@ -149,10 +154,16 @@ class HealthRec(GeneralRecommender):
         txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange=xg),
                            self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
         mm_query = torch.cat([img_q, txt_q], dim=1)
-        item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)
-        item_mm, _ = self.ingre_target_atten(encoded, mm_query)
-        item_know = F.normalize(item_mm).sum(1) / ingre_num.unsqueeze(1)
-        health_pred = torch.sigmoid(self.health_mlp(F.normalize(item_health).mean(dim=1)))
+        if self._fused_fusion(encoded, mm_query):
+            # both target attentions + the normalize heads in one HIP kernel pair (fr_modal_fusion_*)
+            item_know, health_in = ops.modal_fusion(encoded, mm_query, ingredients, ingre_num, self.n_ingredients,
+                                                    self.mm_target_atten.ln, self.ingre_target_atten.ln)
+        else:
+            item_health, _ = self.mm_target_atten(mm_query, encoded, ingredients)
+            item_mm, _ = self.ingre_target_atten(encoded, mm_query)
+            item_know = F.normalize(item_mm).sum(1) / ingre_num.unsqueeze(1)
+            health_in = F.normalize(item_health).mean(dim=1)
+        health_pred = torch.sigmoid(self.health_mlp(health_in))
         health_loss = torch.sum(self.criterion(health_pred, health_level))
 
         mf_loss, emb3 = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
@@ -168,6 +179,15 @@ class HealthRec(GeneralRecommender):
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         reg = emb3 + (torch.norm(ing_p) + torch.norm(ing_n)) / B
         return mf_loss, self.loss_health * health_loss, self.loss_kd * kd, self.reg_weight * reg
+
+    def _fused_fusion(self, encoded, mm_query) -> bool:
+        """The fused modal-fusion kernels cover the reference's configuration: d=64, 2 heads, 'ln'
+        attention without projections, 2 modal queries, fp32 on the GPU."""
+        a, b = self.mm_target_atten, self.ingre_target_atten
+        return (FUSED_FUSION and encoded.is_cuda and encoded.dtype == torch.float32 and encoded.shape[-1] == 64
+                and mm_query.shape[1] == 2 and encoded.shape[1] in ops.ENCODER_LENGTHS
+                and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
+                and a.ln.eps == b.ln.eps)
 
     def row_sparse_tables(self):
         """Parameters whose only use on the training step is a row gather (engine.dist exchanges

@@ -224,3 +224,36 @@ def encoder_layer_f64(x, mask, params, masks, drop, eps=(1e-5, 1e-5), gelu=True,
     f = (torch.nn.functional.gelu(pre) if gelu else torch.relu(pre)) * mf
     y2 = x1 + (f @ w2.t() + b2) * m2
     return torch.nn.functional.layer_norm(y2, (d,), g2, be2, eps[1])
+
+
+# ----------------------------------------------------------------------------- modal fusion
+def target_attention_f64(q_in, kv_in, ln_w, ln_b, eps, num_head=2, seq_ids=None, padding_idx=None):
+    """target_attention_layer.forward with atten_mode='ln', linear_projection=False
+    (models/cikm_model.py:325-369), float64 torch-CPU: head split by chunk/cat, the module's
+    LayerNorm on the q and k heads, scores / sqrt(d/h), padded keys -> keep*s + pad*(-2**32+1),
+    softmax, @ v, heads concatenated back."""
+    Q_ = torch.cat(torch.chunk(q_in, num_head, dim=2), dim=0)
+    K_ = torch.cat(torch.chunk(kv_in, num_head, dim=2), dim=0)
+    V_ = torch.cat(torch.chunk(kv_in, num_head, dim=2), dim=0)
+    d = Q_.shape[-1]
+    Q_ = torch.nn.functional.layer_norm(Q_, (d,), ln_w, ln_b, eps)
+    K_ = torch.nn.functional.layer_norm(K_, (d,), ln_w, ln_b, eps)
+    out = torch.matmul(Q_, K_.permute(0, 2, 1)) * (K_.shape[-1] ** (-0.5))
+    if seq_ids is not None:
+        lq, lk = q_in.shape[1], kv_in.shape[1]
+        key_masks = ((seq_ids == padding_idx).double() * (-2 ** 32 + 1)).view(-1, 1, lk).repeat(num_head, lq, 1)
+        out = (seq_ids != padding_idx).double().view(-1, 1, lk).repeat(num_head, lq, 1) * out + key_masks
+    out = torch.softmax(out, dim=-1)
+    out = torch.matmul(out, V_)
+    return torch.cat(torch.chunk(out, num_head, dim=0), dim=2)
+
+
+def modal_fusion_f64(enc, query, ids, num, pad_id, ln_a, ln_b, eps=1e-12):
+    """cikm_model.py:245-249 in float64: item_health = mm_target_atten(query, enc, ids),
+    item_mm = ingre_target_atten(enc, query); returns (F.normalize(item_mm).sum(1) / num,
+    F.normalize(item_health).mean(1))."""
+    item_health = target_attention_f64(query, enc, ln_a[0], ln_a[1], eps, seq_ids=ids, padding_idx=pad_id)
+    item_mm = target_attention_f64(enc, query, ln_b[0], ln_b[1], eps)
+    know = torch.nn.functional.normalize(item_mm).sum(1) / num.unsqueeze(1)
+    hin = torch.nn.functional.normalize(item_health).mean(dim=1)
+    return know, hin
