@@ -205,12 +205,15 @@ int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64
                      int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
                      void* d_workspace, int64_t workspace_bytes, void* stream);
 
-/* Row-gradient form of the same scatter (n <= 4096 positions): rmap[r] = the first position i with
- * idx[i] == r (else -1; padding_idx rows get -1) and rows[i, :] = sum over positions j with
- * idx[j] == r of grad[j, :] (fixed order, deterministic); rows of non-owner positions are left
- * unwritten.  rmap: [num_rows] int32; rows: [n, d] fp32 (ld = d).  No dense table is touched. */
+/* Row-gradient form of the same scatter: rmap[r] = the first position i with idx[i] == r (else -1;
+ * padding_idx rows get -1) and rows[i, :] = sum over positions j with idx[j] == r of grad[j, :]
+ * (the same sums in the same order as fr_embedding_bwd, deterministic); rows of non-owner
+ * positions are left unwritten.  rmap: [num_rows] int32; rows: [n, d] fp32 (ld = d).  No dense
+ * table is touched.  Workspace: fr_embedding_rowgrad_workspace(n, num_rows, d) bytes. */
+int64_t fr_embedding_rowgrad_workspace(int64_t n, int64_t num_rows, int d);
 int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
-                         int64_t num_rows, int64_t padding_idx, int32_t* d_rmap, float* d_rows, void* stream);
+                         int64_t num_rows, int64_t padding_idx, int32_t* d_rmap, float* d_rows,
+                         void* d_workspace, int64_t workspace_bytes, void* stream);
 /* byte offset, inside the workspace, of the int32 status word of the last fr_embedding_bwd on it:
  * 0 = consistent; non-zero bits name the step that met an out-of-range index on the device and
  * skipped that access instead of faulting (1 scan, 2 place, 4/8 bucket order, 16 segsum, 32 fix-up) */

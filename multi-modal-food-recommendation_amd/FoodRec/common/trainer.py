@@ -251,16 +251,29 @@ class Trainer(AbstractTrainer):
         self.mg = mg
         self.alpha1, self.alpha2, self.beta = config["alpha1"], config["alpha2"], config["beta"]
         self._feats = None
+        # row-gathered feature tables hand the optimiser (ids, rows) instead of a dense gradient
+        # (FusedAdam.row_grads; a data-parallel GradAllReduce routes its RowExchange there too)
+        self._row_grads_on = isinstance(self.optimizer, FusedAdam) and (
+            config["row_grad_tables"] is None or bool(config["row_grad_tables"]))
+        if self._row_grads_on:
+            model._fr_exchange = self.optimizer.row_grads
         # optional callable(model) run between backward and the optimiser step (e.g. the
         # data-parallel gradient all-reduce of FoodRec.engine.dist)
         self.grad_hook = None
         # capture the training step in a HIP graph (config key cuda_graph; GPU, single process)
         self.use_graph = bool(config["cuda_graph"]) and self._on_gpu()
         self._graphed = None
-        # row-gathered feature tables hand the optimiser (ids, rows) instead of a dense gradient
-        # (FusedAdam.row_grads; a data-parallel GradAllReduce installs its RowExchange instead)
-        if isinstance(self.optimizer, FusedAdam) and (config["row_grad_tables"] is None or config["row_grad_tables"]):
-            model._fr_exchange = self.optimizer.row_grads
+
+    @property
+    def grad_hook(self):
+        return self._grad_hook
+
+    @grad_hook.setter
+    def grad_hook(self, hook):
+        self._grad_hook = hook
+        rows = getattr(hook, "rows", None)
+        if rows is not None and self._row_grads_on:
+            rows.sink = self.optimizer.row_grads
 
     def _on_gpu(self) -> bool:
         return torch.device(self.device).type == "cuda"

@@ -42,6 +42,9 @@ class RowExchange:
     def __init__(self, group, world):
         self.group, self.world = group, int(world)
         self.slots = {}  # id(weight) -> dict(weight, pad, ids, G, ids_all, G_all)
+        # optional FusedAdam.row_grads: apply() hands it the gathered mean rows (fr_adam_step_rows)
+        # instead of scattering a dense table gradient
+        self.sink = None
 
     def stash(self, weight, padding_idx, ids, G):
         s = self.slots.get(id(weight))
@@ -64,8 +67,11 @@ class RowExchange:
         for s in self.slots.values():
             w = s["weight"]
             d = s["G"].shape[-1]
-            w.grad = ops.scatter_rows(s["ids_all"].reshape(-1), s["G_all"].reshape(-1, d) * (1.0 / self.world),
-                                      w.shape[0], s["pad"])
+            rows = s["G_all"].reshape(-1, d) * (1.0 / self.world)
+            if self.sink is not None:
+                self.sink.stash(w, s["pad"], s["ids_all"].reshape(-1), rows)
+            else:
+                w.grad = ops.scatter_rows(s["ids_all"].reshape(-1), rows, w.shape[0], s["pad"])
 
 
 class GradAllReduce:

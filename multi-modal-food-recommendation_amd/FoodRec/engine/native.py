@@ -103,8 +103,9 @@ _SIGS = {
     "fr_topk_scores": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int, c_int, c_int,
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_embedding_rowgrad_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_rowgrad": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p,
-                                     c_void_p, c_void_p]),
+                                     c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_adam_step_rows": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                                   POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_int32), c_int,
                                   c_void_p, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),

@@ -26,7 +26,7 @@ import torch
 from . import native, profiling
 
 
-ROW_GRAD_MAX = 4096  # positions per table per step the row-gradient reduction takes (fr_embedding_rowgrad)
+ROW_GRAD_MAX = 1 << 18  # positions per table per step the row-gradient reduction takes (fr_embedding_rowgrad)
 
 
 def adam_rows_bytes(numel: int, rows: int, compact: int) -> int:
@@ -197,10 +197,12 @@ class FusedAdam(torch.optim.Optimizer):
                 G = G.contiguous()
             rmap = torch.empty(R, dtype=torch.int32, device=p.device)
             crow = torch.empty(max(ids.numel(), 1), d, dtype=torch.float32, device=p.device)
+            ws = native.workspace(lib.fr_embedding_rowgrad_workspace(ids.numel(), R, d), p.device)
             with profiling.region("embedding_rowgrad", 4 * R + 8 * ids.numel() + 8 * G.numel()):
                 native.check(lib.fr_embedding_rowgrad(ids.data_ptr(), ids.numel(), G.data_ptr(), G.stride(0), d, R,
                                                       -1 if pad is None else int(pad), rmap.data_ptr(),
-                                                      crow.data_ptr(), native.stream_of(p)), "fr_embedding_rowgrad")
+                                                      crow.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                      native.stream_of(p)), "fr_embedding_rowgrad")
             plist.append(p)
             compact.append(crow)
             maps.append(rmap)

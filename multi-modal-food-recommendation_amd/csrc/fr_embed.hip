@@ -7,7 +7,7 @@
 // ``image_embedding``/``text_embedding`` (cikm_model.py:83-87) all back-propagate through this.
 // torch's sort/unique_by_key path costs ~10 launches per call; here:
 //
-// Batches of <= 4096 ids take a sort-free owner pass (emb_owner_kernel); larger ones:
+// Batches of <= 4096 ids take a sort-free owner pass (emb_owner_scan/sum_kernel); larger ones:
 //   1. histogram of rows + zero fill of the dense gradient (one grid-stride kernel; the wave's
 //      most frequent candidate row -- the padding row of ingredient lists -- is aggregated with a
 //      ballot so the hot counter sees one atomic per wave),
@@ -45,6 +45,8 @@ struct EmbWS {
   int32_t* big;     // [n/(kSmall+1)+1]: rows whose bucket exceeds kSmall
   float4* pf;       // [nchunks*d4]: the chunk's first segment when it began in an earlier chunk
   float4* pl;       // [nchunks*d4]: the chunk's last segment when it continues past the chunk
+  int32_t* nxt;     // [n]  : owner path: next position with the same row (-1: none)
+  int32_t* own;     // [n]  : owner path: 1 when no earlier position has the row
 };
 
 inline int64_t r256(int64_t b) { return (b + 255) / 256 * 256; }
@@ -61,12 +63,14 @@ inline EmbWS emb_ws(void* base, int64_t n, int64_t R, int d) {
   w.big = reinterpret_cast<int32_t*>(take((n / (kSmall + 1) + 1) * 4));
   w.pf = reinterpret_cast<float4*>(take(n_chunks(n) * (d / 4) * 16));
   w.pl = reinterpret_cast<float4*>(take(n_chunks(n) * (d / 4) * 16));
+  w.nxt = reinterpret_cast<int32_t*>(take(std::max<int64_t>(n, 1) * 4));
+  w.own = reinterpret_cast<int32_t*>(take(std::max<int64_t>(n, 1) * 4));
   return w;
 }
 
 inline int64_t emb_ws_bytes(int64_t n, int64_t R, int d) {
   return r256((R + 2) * 4) + r256((R + 1) * 4) + r256(std::max<int64_t>(n, 1) * 4) + r256((n / (kSmall + 1) + 1) * 4) +
-         2 * r256(n_chunks(n) * (d / 4) * 16);
+         2 * r256(n_chunks(n) * (d / 4) * 16) + 2 * r256(std::max<int64_t>(n, 1) * 4);
 }
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(256) void emb_hist_zero_kernel(const int64_t* __res
     }
     if (key >= 0) atomicAdd(&cnt[key], 1);
   }
-  const int64_t total4 = R * d4;
+  const int64_t total4 = out ? R * d4 : 0;  // compact (row-gradient) mode: no dense table to clear
   for (int64_t e = tid; e < total4; e += nth) {
     const int64_t r = e / d4;
     out[r * ldo4 + (e - r * d4)] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -192,12 +196,13 @@ __global__ __launch_bounds__(1024) void emb_scan_kernel(int32_t* __restrict__ cu
   if (t == 0) start[R] = carry;
 }
 
-// Small batches (n <= kOwnerMax, e.g. 2B item ids into a 45k-row feature table): no sort.  Every
-// block stages all ids in LDS; the group of position i owns row idx[i] when no earlier position
-// has it, and sums that row's positions in order (matches gathered 16 at a time, loads in flight
-// together).  Dense mode (rmap == null): the sum goes to dW[r], zero-filled by the previous launch.
-// Row-gradient mode: the sum goes to compact slot i (out[i]) and rmap[r] = i (rmap was filled with
-// -1 by the previous launch), the form fr_adam_step_rows consumes.
+// Small batches (n <= kOwnerMax, e.g. 2B item ids into a 45k-row feature table): no sort.
+//   scan: one thread per position (all ids staged in LDS) finds whether it owns its row (no earlier
+//         position has it) and the next position with the same row;
+//   sum:  one thread per (owning position, float4 column) adds the row's positions along that
+//         chain, in ascending position order, and writes dW[r] (dense mode, zero-filled by the
+//         previous launch) or the compact slot rows[i] with rmap[r] = i (row-gradient mode, the
+//         form fr_adam_step_rows consumes; rmap was filled with -1 by the previous launch).
 constexpr int kOwnerMax = 4096;
 
 __global__ __launch_bounds__(256) void emb_rmap_fill_kernel(int32_t* __restrict__ rmap, int64_t R) {
@@ -205,44 +210,62 @@ __global__ __launch_bounds__(256) void emb_rmap_fill_kernel(int32_t* __restrict_
     rmap[i] = -1;
 }
 
-__global__ __launch_bounds__(256) void emb_owner_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t R,
-                                                        int64_t pad, const float4* __restrict__ G4, int64_t ldg4,
-                                                        int d4, float4* __restrict__ out, int64_t ldo4,
-                                                        int32_t* __restrict__ rmap) {
+// one wave per position: lanes compare 256 ids per step (4 x 64, ballots), stopping once an earlier
+// duplicate and the next duplicate are both found
+constexpr int kScanPerWave = 1;
+
+__global__ __launch_bounds__(256) void emb_owner_scan_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t R,
+                                                             int64_t pad, int32_t* __restrict__ nxt,
+                                                             int32_t* __restrict__ own, int32_t* __restrict__ rmap) {
   __shared__ int ids[kOwnerMax];
   for (int64_t i = threadIdx.x; i < n; i += 256) ids[i] = emb_key(idx, i, n, R, pad);
   __syncthreads();
-  const int lig = threadIdx.x % LPR;
-  const int gshift = (threadIdx.x & 63) & ~(LPR - 1);  // this group's bit offset in a wave ballot
-  const int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
-  const int q = blockIdx.y * LPR + lig;
-  const bool qok = q < d4;
-  if (i >= n) return;  // group-uniform
-  const int r = ids[i];
-  if (r < 0) return;
-  bool dup = false;
-  for (int64_t j = lig; j < i; j += LPR) dup |= ids[j] == r;
-  const uint64_t dmask = __ballot(dup);
-  if ((dmask >> gshift) & 0xFFFFull) return;  // an earlier position owns this row
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t jb = i; jb < n; jb += LPR) {
-    const int64_t j = jb + lig;
-    const bool m = j < n && ids[j] == r;
-    const uint32_t mask = (uint32_t)((__ballot(m) >> gshift) & 0xFFFFull);
-    if (!mask) continue;  // group-uniform
-    float4 x[LPR];
+  const int lane = threadIdx.x & 63;
+  const int i0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kScanPerWave;
+  for (int i = i0; i < min<int64_t>(i0 + kScanPerWave, n); ++i) {  // wave-uniform
+    const int r = ids[i];
+    bool before = false;
+    int next = -1;
+    if (r >= 0) {
+      for (int j0 = 0; j0 < n; j0 += 256) {
+        int v[4];
 #pragma unroll
-    for (int k = 0; k < LPR; ++k)
-      x[k] = ((mask >> k) & 1u) && qok ? G4[(jb + k) * ldg4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + 64 * u + lane;
+          v[u] = j < n ? ids[j] : -1;
+        }
 #pragma unroll
-    for (int k = 0; k < LPR; ++k)
-      if ((mask >> k) & 1u) acc = f4_add(acc, x[k]);
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + 64 * u + lane;
+          const bool m = v[u] == r;
+          before |= __ballot(m && j < i) != 0ull;
+          const uint64_t after = __ballot(m && j > i);
+          if (next < 0 && after) next = j0 + 64 * u + __ffsll((unsigned long long)after) - 1;
+        }
+        if (before && next >= 0) break;
+      }
+    }
+    if (lane == 0) {
+      nxt[i] = next;
+      own[i] = (r >= 0 && !before) ? 1 : 0;
+      if (r >= 0 && !before && rmap) rmap[r] = i;
+    }
   }
-  if (rmap) {
-    if (blockIdx.y == 0 && lig == 0) rmap[r] = (int32_t)i;
-    if (qok) out[i * ldo4 + q] = acc;
-  } else if (qok) {
-    out[(int64_t)r * ldo4 + q] = acc;
+}
+
+__global__ __launch_bounds__(256) void emb_owner_sum_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                            const int32_t* __restrict__ nxt,
+                                                            const int32_t* __restrict__ own,
+                                                            const float4* __restrict__ G4, int64_t ldg4, int d4,
+                                                            float4* __restrict__ out, int64_t ldo4, int compact) {
+  const int64_t total = n * d4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / d4;
+    const int q = (int)(e - i * d4);
+    if (!own[i]) continue;
+    float4 acc = f4_add(make_float4(0.f, 0.f, 0.f, 0.f), G4[i * ldg4 + q]);
+    for (int j = nxt[i]; j >= 0; j = nxt[j]) acc = f4_add(acc, G4[(int64_t)j * ldg4 + q]);
+    out[(compact ? i : idx[i]) * ldo4 + q] = acc;
   }
 }
 
@@ -374,7 +397,7 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(const int64_t* __restri
                                                          int64_t ldg4, int d4, float4* __restrict__ out,
                                                          int64_t ldo4, float4* __restrict__ pf,
                                                          float4* __restrict__ pl, int64_t n,
-                                                         int32_t* __restrict__ status) {
+                                                         int32_t* __restrict__ status, int32_t* __restrict__ rmap) {
   const int lig = threadIdx.x % LPR;
   const int64_t c = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
   const int q = blockIdx.y * LPR + lig;
@@ -391,8 +414,10 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(const int64_t* __restri
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   int cur = -1, cs = 0, ce = 0;
   auto flush = [&]() {
+    if (cs >= k0 && ce <= cend && rmap && lig == 0 && blockIdx.y == 0) rmap[cur] = sorted[cs];
     if (!qok) return;
-    if (cs >= k0 && ce <= cend) out[(int64_t)cur * ldo4 + q] = acc;
+    // row-gradient mode: the row's slot is its first (smallest) position, sorted[bucket start]
+    if (cs >= k0 && ce <= cend) out[(rmap ? (int64_t)sorted[cs] : (int64_t)cur) * ldo4 + q] = acc;
     else if (cs < k0) pf[c * d4 + q] = acc;
     else pl[c * d4 + q] = acc;
   };
@@ -442,7 +467,8 @@ __global__ __launch_bounds__(256) void emb_fixup_kernel(const int64_t* __restric
                                                         float4* __restrict__ out, int64_t ldo4,
                                                         const float4* __restrict__ pf,
                                                         const float4* __restrict__ pl, int64_t n,
-                                                        int64_t nchunks, int32_t* __restrict__ status) {
+                                                        int64_t nchunks, int32_t* __restrict__ status,
+                                                        int32_t* __restrict__ rmap) {
   __shared__ float4 red[GPB][LPR];
   const int lig = threadIdx.x % LPR, g = threadIdx.x / LPR;
   const int q = blockIdx.y * LPR + lig;
@@ -474,11 +500,12 @@ __global__ __launch_bounds__(256) void emb_fixup_kernel(const int64_t* __restric
   }
   red[g][lig] = acc;
   __syncthreads();
+  if (g == 0 && rmap && lig == 0 && blockIdx.y == 0) rmap[r] = sorted[s];
   if (g == 0 && qok) {
     float4 t = red[0][lig];
 #pragma unroll
     for (int k = 1; k < GPB; ++k) t = f4_add(t, red[k][lig]);
-    out[(int64_t)r * ldo4 + q] = t;
+    out[(rmap ? (int64_t)sorted[s] : (int64_t)r) * ldo4 + q] = t;
   }
 }
 
@@ -491,32 +518,36 @@ extern "C" int64_t fr_embedding_bwd_workspace(int64_t n, int64_t num_rows, int d
 
 extern "C" int64_t fr_embedding_bwd_status_offset(int64_t num_rows) { return (num_rows + 1) * 4; }
 
-extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
-                                int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
-                                void* d_workspace, int64_t workspace_bytes, void* stream) {
-  FR_REQUIRE(n >= 0 && n <= kMaxPositions, "n out of range [0, 2^18]");
-  FR_REQUIRE(num_rows > 0 && num_rows < INT32_MAX, "num_rows out of range");
-  FR_REQUIRE(d > 0 && d % 4 == 0, "d must be a positive multiple of 4");
-  FR_REQUIRE(ldo >= d && ldo % 4 == 0 && d_out && fr::aligned16(d_out), "bad output table");
-  FR_REQUIRE(n == 0 || (d_idx && d_grad && ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad)),
-             "bad grad / index arguments");
-  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= emb_ws_bytes(n, num_rows, d),
-             "workspace too small");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+namespace {
+
+// dense mode: out = dW [R, ldo], rmap == null.  row-gradient mode: out = compact rows [n, ldo],
+// rmap = [R] row -> slot map.  Same sums, same order, in both modes.
+int emb_bwd_impl(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d, int64_t R,
+                 int64_t padding_idx, float* d_out, int64_t ldo, int32_t* rmap, void* d_workspace, hipStream_t s) {
   const int d4 = d / 4;
-  const int64_t R = num_rows;
   EmbWS w = emb_ws(d_workspace, n, R, d);
-  if (n <= kOwnerMax) {  // zero fill, then one owner pass: no counting sort
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(R * d4, 256), (int64_t)fr::kNumCU * 8));
-    hipLaunchKernelGGL(emb_hist_zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, (int64_t)0, R,
-                       padding_idx, w.cursor, reinterpret_cast<float4*>(d_out), ldo / 4, d4);
+  float4* out4 = reinterpret_cast<float4*>(d_out);
+  if (rmap) {
+    hipLaunchKernelGGL(emb_rmap_fill_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(R, 256), 1024)), dim3(256),
+                       0, s, rmap, R);
     FR_LAUNCH_CHECK();
+  }
+  if (n <= kOwnerMax) {  // owner scan + chain sums: no counting sort
+    if (!rmap) {  // zero fill of the dense table
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(R * d4, 256), (int64_t)fr::kNumCU * 8));
+      hipLaunchKernelGGL(emb_hist_zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, (int64_t)0, R,
+                         padding_idx, w.cursor, out4, ldo / 4, d4);
+      FR_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(emb_clear_kernel, dim3(1), dim3(256), 0, s, w.cursor + R + 1, (int64_t)1);  // status = 0
     FR_LAUNCH_CHECK();
     if (n > 0) {
-      hipLaunchKernelGGL(emb_owner_kernel, dim3((unsigned)fr::ceil_div(n, GPB), (unsigned)fr::ceil_div(d4, LPR)),
-                         dim3(256), 0, s, d_idx, n, R, padding_idx, reinterpret_cast<const float4*>(d_grad),
-                         ldg / 4, d4, reinterpret_cast<float4*>(d_out), ldo / 4, nullptr);
+      hipLaunchKernelGGL(emb_owner_scan_kernel, dim3((unsigned)fr::ceil_div(n, 4 * kScanPerWave)), dim3(256), 0, s,
+                         d_idx, n, R, padding_idx, w.nxt, w.own, rmap);
+      FR_LAUNCH_CHECK();
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(n * d4, 256), (int64_t)fr::kNumCU * 8));
+      hipLaunchKernelGGL(emb_owner_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, n, w.nxt, w.own,
+                         reinterpret_cast<const float4*>(d_grad), ldg / 4, d4, out4, ldo / 4, rmap ? 1 : 0);
       FR_LAUNCH_CHECK();
     }
     return FR_OK;
@@ -525,13 +556,12 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
                      s, w.cursor, R + 2);
   FR_LAUNCH_CHECK();
   {
-    const int64_t work = std::max<int64_t>(n, R * d4);
+    const int64_t work = std::max<int64_t>(n, rmap ? 0 : R * d4);
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(work, 256), (int64_t)fr::kNumCU * 8));
     hipLaunchKernelGGL(emb_hist_zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, n, R, padding_idx,
-                       w.cursor, reinterpret_cast<float4*>(d_out), ldo / 4, d4);
+                       w.cursor, rmap ? nullptr : out4, ldo / 4, d4);
     FR_LAUNCH_CHECK();
   }
-  if (n == 0) return FR_OK;
   hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, w.cursor, R, w.start, w.big,
                      n / (kSmall + 1) + 1);
   FR_LAUNCH_CHECK();
@@ -559,34 +589,47 @@ extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_
   const int64_t nch = n_chunks(n);
   const unsigned slices = (unsigned)fr::ceil_div(d4, LPR);
   hipLaunchKernelGGL(emb_segsum_kernel, dim3((unsigned)fr::ceil_div(nch, GPB), slices), dim3(256), 0, s, d_idx,
-                     w.sorted, w.start, R, nch, reinterpret_cast<const float4*>(d_grad), ldg / 4, d4,
-                     reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl, n, w.cursor + R + 1);
+                     w.sorted, w.start, R, nch, reinterpret_cast<const float4*>(d_grad), ldg / 4, d4, out4, ldo / 4,
+                     w.pf, w.pl, n, w.cursor + R + 1, rmap);
   FR_LAUNCH_CHECK();
   hipLaunchKernelGGL(emb_fixup_kernel, dim3((unsigned)nch, slices), dim3(256), 0, s, d_idx, w.sorted, w.start, R,
-                     d4, reinterpret_cast<float4*>(d_out), ldo / 4, w.pf, w.pl, n, nch, w.cursor + R + 1);
+                     d4, out4, ldo / 4, w.pf, w.pl, n, nch, w.cursor + R + 1, rmap);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
 
+}  // namespace
+
+extern "C" int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                                int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
+                                void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(n >= 0 && n <= kMaxPositions, "n out of range [0, 2^18]");
+  FR_REQUIRE(num_rows > 0 && num_rows < INT32_MAX, "num_rows out of range");
+  FR_REQUIRE(d > 0 && d % 4 == 0, "d must be a positive multiple of 4");
+  FR_REQUIRE(ldo >= d && ldo % 4 == 0 && d_out && fr::aligned16(d_out), "bad output table");
+  FR_REQUIRE(n == 0 || (d_idx && d_grad && ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad)),
+             "bad grad / index arguments");
+  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= emb_ws_bytes(n, num_rows, d),
+             "workspace too small");
+  return emb_bwd_impl(d_idx, n, d_grad, ldg, d, num_rows, padding_idx, d_out, ldo, nullptr, d_workspace,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int64_t fr_embedding_rowgrad_workspace(int64_t n, int64_t num_rows, int d) {
+  return fr_embedding_bwd_workspace(n, num_rows, d);
+}
+
 extern "C" int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
                                     int64_t num_rows, int64_t padding_idx, int32_t* d_rmap, float* d_rows,
-                                    void* stream) {
-  FR_REQUIRE(n >= 0 && n <= kOwnerMax, "n out of range [0, 4096]");
+                                    void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(n >= 0 && n <= kMaxPositions, "n out of range [0, 2^18]");
   FR_REQUIRE(num_rows > 0 && num_rows < INT32_MAX && d_rmap, "bad row map");
   FR_REQUIRE(d > 0 && d % 4 == 0, "d must be a positive multiple of 4");
   FR_REQUIRE(n == 0 || (d_idx && d_grad && d_rows && ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad) &&
                         fr::aligned16(d_rows)),
              "bad grad / index / row arguments");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int d4 = d / 4;
-  hipLaunchKernelGGL(emb_rmap_fill_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(num_rows, 256), 1024)),
-                     dim3(256), 0, s, d_rmap, num_rows);
-  FR_LAUNCH_CHECK();
-  if (n > 0) {
-    hipLaunchKernelGGL(emb_owner_kernel, dim3((unsigned)fr::ceil_div(n, GPB), (unsigned)fr::ceil_div(d4, LPR)),
-                       dim3(256), 0, s, d_idx, n, num_rows, padding_idx, reinterpret_cast<const float4*>(d_grad),
-                       ldg / 4, d4, reinterpret_cast<float4*>(d_rows), (int64_t)d4, d_rmap);
-    FR_LAUNCH_CHECK();
-  }
-  return FR_OK;
+  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= emb_ws_bytes(n, num_rows, d),
+             "workspace too small");
+  return emb_bwd_impl(d_idx, n, d_grad, ldg, d, num_rows, padding_idx, d_rows, d, d_rmap, d_workspace,
+                      reinterpret_cast<hipStream_t>(stream));
 }

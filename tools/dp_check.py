@@ -57,6 +57,7 @@ def main():
     # dense reference
     tr = Trainer(cfg, mr)
     sum(mr.calculate_loss(tr._features().batch(u, p, n))).backward()
+    tr.optimizer.materialize_row_grads()  # dense .grad of the row-gathered tables
     for prm in mr.parameters():
         if prm.grad is not None:
             dist.all_reduce(prm.grad)
