@@ -332,6 +332,42 @@ class _EmbeddingExchanged(torch.autograd.Function):
         return None, None, None, None
 
 
+class _EmbeddingNorms(torch.autograd.Function):
+    """One gather serving two of the reference's uses of the same (table, ids): ``W[ids]`` (gradient
+    to every row, cikm_model.py:230) and the Frobenius norms of the two halves of
+    ``nn.Embedding(ids, padding_idx=pad)`` (EmbLoss over the pos / neg ingredient blocks,
+    cikm_model.py:270-279; padding positions get no gradient).  Both gradients are combined before
+    ONE deterministic scatter (fr_embedding_bwd)."""
+
+    @staticmethod
+    def forward(ctx, idx, weight, pad, half):
+        native.require_device(weight, idx)
+        E = torch.nn.functional.embedding(idx, weight)
+        Ef = E.reshape(2, -1)  # full-tensor norms of each half (a 2-output dim reduction is slow)
+        nrm = torch.stack([torch.linalg.vector_norm(Ef[0]), torch.linalg.vector_norm(Ef[1])])
+        ctx.save_for_backward(idx, E, nrm)
+        ctx.rows, ctx.pad, ctx.half = weight.shape[0], pad, half
+        return E, nrm
+
+    @staticmethod
+    def backward(ctx, gE, gn):
+        idx, E, nrm = ctx.saved_tensors
+        G = torch.zeros_like(E) if gE is None else gE
+        if gn is not None:
+            coef = (gn / nrm).view(2, 1).expand(2, ctx.half * idx.shape[-1]).reshape(idx.shape)
+            coef = torch.where(idx != ctx.pad, coef, torch.zeros((), dtype=coef.dtype, device=coef.device))
+            G = torch.addcmul(G, coef.unsqueeze(-1), E)
+        return None, scatter_rows(idx, G, ctx.rows, None), None, None
+
+
+def embedding_norms(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int, half: int):
+    """``(W[idx], stack(||Embedding(idx[:half], pad)||_F, ||Embedding(idx[half:], pad)||_F))`` with
+    one gather and one scatter (see _EmbeddingNorms).  ``idx``: [2 * half, L]."""
+    if idx.shape[0] != 2 * half:
+        raise native.EngineError(f"embedding_norms: idx has {idx.shape[0]} rows, expected 2 x {half}")
+    return _EmbeddingNorms.apply(idx, weight, int(padding_idx), int(half))
+
+
 _EMB_STATUS = None  # test hook: a list collecting each call's device status word (0 = consistent)
 
 

@@ -133,15 +133,21 @@ class LazyBatch(dict):
     """dict with the reference batch keys; side features are gathered on first access."""
 
     _LAZY = ("pos_ingre_code", "pos_ingre_num", "pos_hl_mh", "pos_img",
-             "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img")
+             "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img",
+             # engine extras: [pos; neg] stacked (one gather instead of two gathers and a cat)
+             "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh")
 
     def __init__(self, feats: BatchFeatures, u, p, n):
         super().__init__(u_id=u, pos_i_id=p, neg_i_id=n)
         self._f = feats
 
     def _make(self, key):
+        if key == "pn_i_id":
+            return torch.cat([self["pos_i_id"], self["neg_i_id"]])
         side, what = key.split("_", 1)
-        idx = self["pos_i_id"] if side == "pos" else self["neg_i_id"]
+        idx = {"pos": self["pos_i_id"], "neg": self["neg_i_id"]}.get(side)
+        if idx is None:
+            idx = self["pn_i_id"]
         f = self._f
         if what == "ingre_code":
             return f.ingre_code[idx]

@@ -133,20 +133,21 @@ class HealthRec(GeneralRecommender):
 
     def calculate_loss(self, batch_data):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
-        pos_ingre, neg_ingre = batch_data["pos_ingre_code"], batch_data["neg_ingre_code"]
         user_all, item_all, _ = self.forward()
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
-        health_level = torch.cat([batch_data["pos_hl_mh"], batch_data["neg_hl_mh"]], dim=0)
-        ingredients = torch.cat([pos_ingre, neg_ingre], dim=0)
-        ingre_num = torch.cat([batch_data["pos_ingre_num"], batch_data["neg_ingre_num"]], dim=0)
-        # the reference indexes ingr_all[ingredients] (grad reaches the pad row too); the engine
-        # gather has the same gradient through the deterministic HIP scatter-add fr_embedding_bwd
-        ingr_emb = ops.embedding(ingredients, ingr_all)
+        health_level = _pn(batch_data, "hl_mh")
+        ingredients = _pn(batch_data, "ingre_code")
+        ingre_num = _pn(batch_data, "ingre_num")
+        B = user.shape[0]
+        # ingr_all[ingredients] (grad reaches the pad row too, cikm_model.py:230) and the EmbLoss
+        # norms of ingre_embedding(pos / neg ingredients) with padding_idx (:270-279): the same
+        # gather, so one gather and one combined deterministic scatter (fr_embedding_bwd)
+        ingr_emb, ing_norms = ops.embedding_norms(ingredients, ingr_all, self.n_ingredients, B)
         mask = ingredients == self.n_ingredients
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
-        all_item = torch.cat([pos_item, neg_item], dim=0)
+        all_item = _pn(batch_data, "i_id")
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
         xg = self.__dict__.get("_fr_exchange")  # data-parallel: rows exchanged, not tables
         img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange=xg),
@@ -172,12 +173,8 @@ class HealthRec(GeneralRecommender):
         kd = 1 - cosine_similarity(item_know, ops.embedding(all_item, item_all), dim=-1).mean()
         kd = self.norm_loss(kd, self.kd_threshold)
 
-        B = user.shape[0]
-        # ingre_embedding(pos) / ingre_embedding(neg) (cikm_model.py:270-271) as one gather
-        ing_pn = ops.embedding(ingredients, self.ingre_embedding.weight, padding_idx=self.n_ingredients)
-        ing_p, ing_n = ing_pn[:B], ing_pn[B:]
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
-        reg = emb3 + (torch.norm(ing_p) + torch.norm(ing_n)) / B
+        reg = emb3 + (ing_norms[0] + ing_norms[1]) / B
         return mf_loss, self.loss_health * health_loss, self.loss_kd * kd, self.reg_weight * reg
 
     def _fused_fusion(self, encoded, mm_query) -> bool:
@@ -209,6 +206,13 @@ class HealthRec(GeneralRecommender):
             zero = torch.zeros((), dtype=kd_loss.dtype, device=kd_loss.device)
             self.__dict__["_zero"] = zero
         return torch.max(zero, kd_loss - threshold)
+
+
+def _pn(batch, what):
+    """torch.cat([batch['pos_' + what], batch['neg_' + what]]) -- read directly when the engine's
+    batch (sampler.LazyBatch) provides it stacked."""
+    v = batch.get("pn_" + what)
+    return v if v is not None else torch.cat([batch["pos_" + what], batch["neg_" + what]], dim=0)
 
 
 # the reference's names

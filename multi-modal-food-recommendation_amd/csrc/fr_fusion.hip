@@ -266,24 +266,33 @@ __global__ __launch_bounds__(64 * WAVES) void fusion_bwd_kernel(FusionArgs a) {
   a.part[(int64_t)blockIdx.x * NPARAM + threadIdx.x] = s;
 }
 
-// out[k][j] = sum over blocks (in order) of part[b][k][j] + part[b][k][j + 32], k = dgamma_a, dbeta_a,
-// dgamma_b, dbeta_b; one thread per output, 8 loads in flight
-__global__ __launch_bounds__(128) void fusion_reduce_kernel(const float* __restrict__ part, int64_t nblk,
-                                                            float* __restrict__ out) {
-  const int o = threadIdx.x, k = o / HD, j = o % HD;
+// out[k][j] = sum over blocks of part[b][k][j] + part[b][k][j + 32], k = dgamma_a, dbeta_a,
+// dgamma_b, dbeta_b.  1024 threads: 128 outputs x 8 block slices (4 loads in flight each), slices
+// added in slice order (deterministic).
+__global__ __launch_bounds__(1024) void fusion_reduce_kernel(const float* __restrict__ part, int64_t nblk,
+                                                             float* __restrict__ out) {
+  __shared__ float red[8][4 * HD];
+  const int o = threadIdx.x & 127, sl = threadIdx.x >> 7, k = o / HD, j = o % HD;
   float s = 0.f;
-  for (int64_t b0 = 0; b0 < nblk; b0 += 8) {
-    float v[8];
+  for (int64_t b0 = sl; b0 < nblk; b0 += 32) {
+    float v[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t b = min(b0 + u, nblk - 1);
+    for (int u = 0; u < 4; ++u) {
+      const int64_t b = min(b0 + 8 * u, nblk - 1);
       v[u] = part[b * NPARAM + k * D + j] + part[b * NPARAM + k * D + j + HD];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (b0 + u < nblk) s += v[u];
+    for (int u = 0; u < 4; ++u)
+      if (b0 + 8 * u < nblk) s += v[u];
   }
-  out[o] = s;
+  red[sl][o] = s;
+  __syncthreads();
+  if (sl == 0) {
+    float t = red[0][o];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[q][o];
+    out[o] = t;
+  }
 }
 
 bool supported_len(int L) { return L == 20 || L == 16 || L == 10 || L == 8 || L == 5 || L == 4; }
@@ -350,7 +359,7 @@ extern "C" int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, con
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   rc = dispatch(a, L, true, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(fusion_reduce_kernel, dim3(1), dim3(4 * HD), 0, s, d_partials, fr::ceil_div(n_items, WAVES),
+  hipLaunchKernelGGL(fusion_reduce_kernel, dim3(1), dim3(1024), 0, s, d_partials, fr::ceil_div(n_items, WAVES),
                      d_dln);
   FR_LAUNCH_CHECK();
   return FR_OK;

@@ -81,11 +81,19 @@ def embedding(idx, weight, padding_idx=None, exchange=None):
     return torch.nn.functional.embedding(idx, weight, padding_idx=padding_idx)
 
 
+def embedding_norms(idx, weight, padding_idx, half):
+    # ingr_all[ingredients] (cikm_model.py:230) and the EmbLoss norms of ingre_embedding(pos / neg)
+    # with padding_idx (cikm_model.py:270-279), as the reference computes them
+    E = torch.nn.functional.embedding(idx, weight)
+    P = torch.nn.functional.embedding(idx, weight, padding_idx=padding_idx)
+    return E, torch.stack([torch.norm(P[:half]), torch.norm(P[half:])])
+
+
 def linear(x, W, b=None):
     return torch.nn.functional.linear(x, W, b)
 
 
-_PATCH = {"embedding": embedding, "linear": linear, "spmm_launch": spmm_launch, "scatter_rows": scatter_rows, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
+_PATCH = {"embedding": embedding, "embedding_norms": embedding_norms, "linear": linear, "spmm_launch": spmm_launch, "scatter_rows": scatter_rows, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
           "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
 
 
