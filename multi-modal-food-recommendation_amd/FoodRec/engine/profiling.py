@@ -13,6 +13,7 @@ from collections import defaultdict
 import torch
 
 _ACTIVE = None
+SPIN_CYCLES = 200_000  # ~0.1 ms busy-wait before each timed region (not part of the measurement)
 
 
 class KernelTimer:
@@ -23,6 +24,10 @@ class KernelTimer:
     def region(self, name: str, nbytes: int):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
+        # keep the GPU busy while the host records the start event and launches the kernel: with
+        # a starved queue the start event would fire before the launch and count the host's
+        # launch latency as kernel time
+        torch.cuda._sleep(SPIN_CYCLES)
         s.record()
         try:
             yield
