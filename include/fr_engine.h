@@ -40,7 +40,9 @@ enum fr_status {
   FR_EINVAL = 1,   /* bad argument (null pointer, size, unsupported d)            */
   FR_EHIP = 2,     /* a HIP runtime call failed (message in fr_last_error)       */
   FR_ENOTSUP = 3,  /* combination not supported by this build                    */
-  FR_ERANGE = 4    /* an index/id outside its table                               */
+  FR_ERANGE = 4,   /* an index/id outside its table                               */
+  FR_EIO = 5,      /* a file could not be opened / mapped (message in fr_last_error) */
+  FR_EPARSE = 6    /* a malformed field in a text file (line in fr_last_error)   */
 };
 
 enum fr_dtype { FR_F32 = 0, FR_BF16 = 1 };
@@ -393,6 +395,39 @@ int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, const int64_t*
                         int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps,
                         const float* d_dknow, const float* d_dhin, float* d_denc, float* d_dquery, float* d_dln,
                         float* d_partials, int64_t partial_floats, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Host-side readers of the reference's on-disk interaction formats (no GPU).
+ *   FR_IO_NEGATIVE  data.{valid,test}.negative: "(u,i)\tn1\tn2..." per line; the first field is
+ *                   dropped, the rest are int() ids -> ragged rows (values, offsets[rows+1]).
+ *                   Replaces InteractionData.load_negative_file (utils/dataset.py:245-256).
+ *   FR_IO_RATING    data.{train,valid,test}.rating: "u\ti\trating..." -> values[rows][2] = (u, i),
+ *                   aux[rows] = float(rating) (NaN when the line has no third field; aux may be
+ *                   NULL).  Replaces the int(arr[0]), int(arr[1]), float(arr[2]) parses of
+ *                   utils/dataset.py:93-176.
+ * fr_io_open maps the file and counts rows / values in parallel byte ranges cut at line starts;
+ * the caller allocates; fr_io_fill parses into its arrays (FR_EPARSE + the 1-based line of the
+ * first malformed field, as the reference's int()/float() would raise); fr_io_close unmaps.
+ * threads <= 0: min(hardware threads, 16), and at least 4 MB of text per thread.
+ * ------------------------------------------------------------------------------------------ */
+enum fr_io_mode { FR_IO_NEGATIVE = 0, FR_IO_RATING = 1 };
+typedef struct fr_io_table fr_io_table;
+int fr_io_open(const char* path, int mode, int threads, fr_io_table** table, int64_t* rows, int64_t* values);
+int fr_io_fill(fr_io_table* table, int64_t* values, int64_t* offsets, double* aux, int64_t* bad_line);
+void fr_io_close(fr_io_table* table);
+
+/* Evaluation candidates of EvalByUserDataloader (utils/dataloader.py:228-302), host arrays:
+ * fr_io_remove_positives: for each user u and each positive p of pos[pos_off[u]:pos_off[u+1]] in
+ *   order, clears alive[] of the first still-alive occurrence of p in neg[neg_off[u]:neg_off[u+1]]
+ *   (list.remove in place; the mask persists, so repeated evaluations see the reference's mutated
+ *   lists); lens[u] = |pos_u| + alive negatives of u, *total = sum(lens).
+ * fr_io_candidates: out_items[cand_off[u]:] = pos_u followed by the alive negatives of u in file
+ *   order, out_users[...] = users[u]  (items = pos + neg).  cand_off = exclusive prefix of lens. */
+int fr_io_remove_positives(const int64_t* neg, const int64_t* neg_off, uint8_t* alive, const int64_t* pos,
+                           const int64_t* pos_off, int64_t n_users, int64_t* lens, int64_t* total, int threads);
+int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* alive, const int64_t* pos,
+                     const int64_t* pos_off, const int64_t* users, int64_t n_users, const int64_t* cand_off,
+                     int64_t* out_users, int64_t* out_items, int threads);
 
 #ifdef __cplusplus
 }

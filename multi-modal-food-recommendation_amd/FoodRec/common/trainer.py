@@ -35,6 +35,7 @@ from torch.nn.utils.clip_grad import clip_grad_norm_
 from FoodRec.engine.graph import swap_sparse_attributes
 from FoodRec.engine.optim import FusedAdam
 from FoodRec.engine.sampler import BatchFeatures, TripleSampler
+from FoodRec.utils.textio import eval_candidates
 from FoodRec.utils.utils import dict2str, early_stopping
 
 
@@ -385,24 +386,14 @@ class Trainer(AbstractTrainer):
     # ------------------------------------------------------------------------------ evaluation
     def _candidates(self, is_test):
         """EvalByUserDataloader (dataloader.py:228-302): per user, pos + negatives with the
-        positives removed (the removal mutates the dataset lists in place, as the reference)."""
+        positives removed (the removal persists in the dataset's RaggedIds, as the reference's
+        in-place list.remove does); native pass in csrc/fr_io.cpp."""
         ds = self.model.dataset
         if not is_test:
             users, pos_lists, neg_lists = ds.valid_users, ds.validRatings, ds.validNegatives
         else:
             users, pos_lists, neg_lists = list(range(ds.num_users)), ds.testRatings, ds.testNegatives
-        all_users, all_items, lens, npos = [], [], [], []
-        for idx, user in enumerate(users):
-            pos, neg = pos_lists[idx], neg_lists[idx]
-            for item in pos:
-                if item in neg:
-                    neg.remove(item)
-            items = pos + neg
-            all_users.append(np.full(len(items), user, dtype=np.int64))
-            all_items.append(np.asarray(items, dtype=np.int64))
-            lens.append(len(items))
-            npos.append(len(pos))
-        return np.concatenate(all_users), np.concatenate(all_items), np.asarray(lens), np.asarray(npos)
+        return eval_candidates(users, pos_lists, neg_lists)
 
     @torch.no_grad()
     def _score(self, users, items):

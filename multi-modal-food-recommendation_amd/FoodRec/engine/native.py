@@ -16,7 +16,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
                          "libfr_engine.so")
 
 FR_OK = 0
-_STATUS = {1: "FR_EINVAL", 2: "FR_EHIP", 3: "FR_ENOTSUP", 4: "FR_ERANGE"}
+_STATUS = {1: "FR_EINVAL", 2: "FR_EHIP", 3: "FR_ENOTSUP", 4: "FR_ERANGE", 5: "FR_EIO", 6: "FR_EPARSE"}
 
 
 class EngineError(RuntimeError):
@@ -129,6 +129,13 @@ _SIGS = {
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),
+    "fr_io_open": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
+    "fr_io_fill": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
+    "fr_io_close": (None, [c_void_p]),
+    "fr_io_remove_positives": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                       POINTER(c_int64), c_int]),
+    "fr_io_candidates": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                 c_void_p, c_void_p, c_int]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

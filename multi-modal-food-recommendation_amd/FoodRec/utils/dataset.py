@@ -20,6 +20,8 @@ from collections import defaultdict
 import numpy as np
 import scipy.sparse as sp
 
+from .textio import RaggedIds, read_negatives, read_ratings
+
 _SAFE = {
     ("builtins", "dict"), ("builtins", "list"), ("builtins", "set"), ("builtins", "tuple"),
     ("builtins", "int"), ("builtins", "float"), ("builtins", "bool"), ("builtins", "frozenset"),
@@ -44,24 +46,22 @@ def safe_pickle_load(path: str):
         return _SafeUnpickler(io.BytesIO(f.read())).load()
 
 
-def _read_pairs(path: str) -> np.ndarray:
-    """``u\\ti\\trating...`` lines -> [n,3] float64 (u, i, rating)."""
-    import pandas as pd
-    df = pd.read_csv(path, sep="\t", header=None, usecols=[0, 1, 2], dtype=np.float64)
-    return df.to_numpy()
+def _read_pairs(path: str, with_rating: bool = False):
+    """``u\ti\trating`` lines -> ([n,2] int64 (u, i), [n] float64 rating or None); native parallel
+    reader (utils/textio.py, csrc/fr_io.cpp)."""
+    return read_ratings(path, with_rating)
 
 
-def _read_negatives(path: str) -> list:
-    out = []
-    with open(path, "r") as f:
-        for line in f:
-            arr = line.rstrip("\n").split("\t")
-            out.append([int(x) for x in arr[1:] if x != ""])
-    return out
+def _read_negatives(path: str) -> RaggedIds:
+    return read_negatives(path)
 
 
-def _as_lists(x) -> list:
-    return x.tolist() if isinstance(x, np.ndarray) else [list(r) for r in x]
+def _as_ragged(x) -> RaggedIds:
+    if isinstance(x, RaggedIds):
+        return x
+    if isinstance(x, np.ndarray):
+        return RaggedIds.from_dense(x)
+    return RaggedIds.from_lists(x)
 
 
 def _csr_sets(users: np.ndarray, items: np.ndarray, n_users: int):
@@ -74,15 +74,42 @@ def _csr_sets(users: np.ndarray, items: np.ndarray, n_users: int):
     return ptr, it.astype(np.int64)
 
 
-def _group_consecutive(pairs: np.ndarray):
-    """Reference load_valid_file_as_list / load_training_file_as_list grouping (:115-155)."""
-    if len(pairs) == 0:
-        return [], []
+def _group_training(pairs: np.ndarray) -> RaggedIds:
+    """load_training_file_as_list (reference utils/dataset.py:138-155): a new list starts at a line
+    whose user exceeds the counter u_, and u_ then grows by ONE (not to that user), so a user id gap
+    inserts empty lists.  Files whose users run 0, 1, 2, ... take the vectorised path."""
+    n = len(pairs)
+    if n == 0:
+        return RaggedIds(np.zeros(0, np.int64), np.zeros(2, np.int64))  # [[]]
     u = pairs[:, 0]
-    cut = np.nonzero(u[1:] != u[:-1])[0] + 1
-    groups = np.split(pairs[:, 1], cut)
-    users = u[np.concatenate([[0], cut])]
-    return [g.tolist() for g in groups], users.tolist()
+    step = np.diff(u)
+    if u[0] == 0 and ((step == 0) | (step == 1)).all():
+        starts = np.flatnonzero(step) + 1
+    else:
+        starts, u_ = [], 0
+        for k, uk in enumerate(u.tolist()):
+            if u_ < uk:
+                starts.append(k)
+                u_ += 1
+        starts = np.asarray(starts, np.int64)
+    offsets = np.concatenate([[0], starts, [n]]).astype(np.int64)
+    return RaggedIds(pairs[:, 1], offsets)
+
+
+def _group_valid(pairs: np.ndarray):
+    """load_valid_file_as_list (reference utils/dataset.py:115-136): a new list starts when the user
+    exceeds the current list's user (a running maximum); users = each list's user, except that the
+    last entry is the final line's user.  (An empty file, where the reference's int('') raises, gives
+    no lists.)"""
+    n = len(pairs)
+    if n == 0:
+        return RaggedIds(np.zeros(0, np.int64), np.zeros(1, np.int64)), []
+    u = pairs[:, 0]
+    prev_max = np.maximum.accumulate(u)
+    starts = np.concatenate([[0], np.flatnonzero(u[1:] > prev_max[:-1]) + 1]).astype(np.int64)
+    users = u[starts].copy()
+    users[-1] = u[-1]
+    return RaggedIds(pairs[:, 1], np.append(starts, n)), users.tolist()
 
 
 class _TrainMatrix:
@@ -113,12 +140,12 @@ class FoodData:
         gp = cfg["graph_data_path"]
         ingre_path = cfg["ingre_data_path"] or ip
         a = {}
-        tr = _read_pairs(ip + "data.train.rating")
+        tr, rating = _read_pairs(ip + "data.train.rating", with_rating=True)
         # dok assignment keeps rating > 0 rows, first occurrence position (dataset.py:167-176)
-        a["train_raw"] = tr[:, :2].astype(np.int64)
-        a["train_rating_pos"] = tr[:, 2] > 0
-        a["valid"] = _read_pairs(ip + "data.valid.rating")[:, :2].astype(np.int64)
-        a["test"] = _read_pairs(ip + "data.test.rating")[:, :2].astype(np.int64)
+        a["train_raw"] = tr
+        a["train_rating_pos"] = rating > 0
+        a["valid"] = _read_pairs(ip + "data.valid.rating")[0]
+        a["test"] = _read_pairs(ip + "data.test.rating")[0]
         a["valid_neg"] = _read_negatives(ip + "data.valid.negative")
         a["test_neg"] = _read_negatives(ip + "data.test.negative")
         a["image"] = np.load(ip + "data_image_features_float.npy")
@@ -182,10 +209,11 @@ class FoodData:
         self.num_items = int(tr_all[:, 1].max()) + 1
         self.trainMatrix = _TrainMatrix(self.train_pairs, (self.num_users, self.num_items))
         self._tr_all, self._va_all, self._te_all = tr_all, va_all, te_all
-        self.testRatings, _ = _group_consecutive(te_all)
-        self.testNegatives = _as_lists(a["test_neg"])
-        self.validRatings, self.valid_users = _group_consecutive(va_all)
-        self.validNegatives = _as_lists(a["valid_neg"])
+        # per-user lists as RaggedIds (the reference's list-of-lists protocol over flat arrays)
+        self.testRatings = _group_training(te_all)
+        self.testNegatives = _as_ragged(a["test_neg"])
+        self.validRatings, self.valid_users = _group_valid(va_all)
+        self.validNegatives = _as_ragged(a["valid_neg"])
         assert len(self.testRatings) == len(self.testNegatives)
         assert len(self.validRatings) == len(self.validNegatives)
         train_items = set(tr_all[:, 1].tolist())
@@ -255,7 +283,7 @@ class FoodData:
     @property
     def trainList(self):
         if "_trainList" not in self.__dict__:
-            self._trainList, _ = _group_consecutive(self._tr_all)
+            self._trainList = _group_training(self._tr_all)
         return self._trainList
 
     @property

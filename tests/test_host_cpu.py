@@ -29,7 +29,7 @@ def test_dataset_digest_matches_goldens():
 def test_library_exports_header_symbols():
     from FoodRec.engine import native
     header = open(os.path.join(ROOT, "include", "fr_engine.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(fr_\w+)\s*\(", header, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(fr_\w+)\s*\(", header, re.M))
     assert declared == set(native.EXPORTED_SYMBOLS)
     lib = native.lib()
     for name in declared:
