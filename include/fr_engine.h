@@ -397,6 +397,28 @@ int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, const int64_t*
                         float* d_partials, int64_t partial_floats, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Fused health / KD loss head of HealthRec (models/cikm_model.py:249-264,304-308), over n items:
+ *   out[0] = w_health * sum BCE(sigmoid(W2 relu(W1 hin + b1) + b2), labels)      (health_mlp, BCELoss)
+ *   out[1] = w_kd * max(0, 1 - mean_i cos(know_i, rows_i) - kd_threshold)          (norm_loss of KD)
+ *   out[2] = 1 - mean cos - kd_threshold (saved for the backward's gate)
+ * d_hin/d_know/d_rows [n, 64] (rows = item_all[pos; neg]), d_labels [n, H] float, H <= 16,
+ * d_mlp = {W1 [64,64], b1 [64], W2 [H,64], b2 [H]} (nn.Linear layout).  The forward writes d_out
+ * from block partials summed in block order by the last block (d_partials from
+ * fr_health_kd_partials(n, 0), zero-filled once before first use; the kernel re-zeroes its ticket).
+ * The ticket is word 0 of d_partials.  The backward takes the upstream gradients of out[0] / out[1] as device scalars and writes
+ * d_dhin, d_dknow, d_drows and d_dmlp = {dW1, db1, dW2, db2} (block partials, block order).
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_health_kd_partials(int64_t n_items, int backward);
+int fr_health_kd_fwd(const float* d_hin, const float* d_know, const float* d_rows, const float* d_labels,
+                     int64_t n_items, int H, const float* const* d_mlp, float kd_threshold, float w_health,
+                     float w_kd, float* d_out, float* d_partials, int64_t partial_floats, void* stream);
+int fr_health_kd_bwd(const float* d_hin, const float* d_know, const float* d_rows, const float* d_labels,
+                     int64_t n_items, int H, const float* const* d_mlp, float kd_threshold, float w_health,
+                     float w_kd, const float* d_out, const float* d_gh, const float* d_gk, float* d_dhin,
+                     float* d_dknow, float* d_drows, float* const* d_dmlp, float* d_partials,
+                     int64_t partial_floats, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Host-side readers of the reference's on-disk interaction formats (no GPU).
  *   FR_IO_NEGATIVE  data.{valid,test}.negative: "(u,i)\tn1\tn2..." per line; the first field is
  *                   dropped, the rest are int() ids -> ragged rows (values, offsets[rows+1]).

@@ -129,6 +129,12 @@ _SIGS = {
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),
+    "fr_health_kd_partials": (c_int64, [c_int64, c_int]),
+    "fr_health_kd_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p),
+                                 c_float, c_float, c_float, c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_health_kd_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p),
+                                 c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
     "fr_io_open": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
     "fr_io_fill": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
     "fr_io_close": (None, [c_void_p]),

@@ -662,6 +662,82 @@ def modal_fusion(enc, query, ids, num, pad_id, ln_a, ln_b):
                               ln_a.eps, ln_a.weight, ln_a.bias, ln_b.weight, ln_b.bias)
 
 
+# ----------------------------------------------------------------------------- health / KD head
+_HEAD_FWD_PARTS = {}  # device -> zero-initialised forward partials (+ ticket word; the kernel re-zeroes it)
+
+
+def health_kd_bytes(n: int, H: int, backward: bool) -> int:
+    """Algorithmic HBM bytes: hin / know / rows [n, 64] and labels [n, H] read (+ their three
+    gradients written and the parameter-gradient partials written once and read once backward)."""
+    base = 4 * n * (3 * 64 + H) + 4 * (64 * 64 + 64 + H * 64 + H)
+    if not backward:
+        return base
+    nb = min((n + 3) // 4, 64)
+    return base + 4 * n * 3 * 64 + 2 * 4 * nb * (64 * 64 + 64 + 16 * 64 + 16)
+
+
+class _HealthKD(torch.autograd.Function):
+    """fr_health_kd_fwd / _bwd: HealthRec's health MLP + BCE sum and the KD cosine term, weighted."""
+
+    @staticmethod
+    def forward(ctx, hin, know, rows, labels, w1, b1, w2, b2, thr, w_h, w_k):
+        n, H = labels.shape
+        dev = hin.device
+        lib = native.lib()
+        need = lib.fr_health_kd_partials(n, 0)
+        part = _HEAD_FWD_PARTS.get(dev)
+        if part is None or part.numel() < need:
+            part = torch.zeros(max(need, 256), dtype=torch.float32, device=dev)
+            _HEAD_FWD_PARTS[dev] = part
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        mlp = (ctypes.c_void_p * 4)(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr())
+        with profiling.region("health_kd", health_kd_bytes(n, H, False)):
+            native.check(lib.fr_health_kd_fwd(hin.data_ptr(), know.data_ptr(), rows.data_ptr(), labels.data_ptr(), n, H,
+                                              mlp, float(thr), float(w_h), float(w_k), out.data_ptr(),
+                                              part.data_ptr(), part.numel(), native.stream_of(hin)),
+                         "fr_health_kd_fwd")
+        ctx.save_for_backward(hin, know, rows, labels, w1, b1, w2, b2)
+        ctx.out, ctx.cfg = out, (float(thr), float(w_h), float(w_k))
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, gh, gk):
+        hin, know, rows, labels, w1, b1, w2, b2 = ctx.saved_tensors
+        n, H = labels.shape
+        dev = hin.device
+        zero = None
+        if gh is None or gk is None:
+            zero = torch.zeros((), dtype=torch.float32, device=dev)
+        gh = zero if gh is None else gh.to(torch.float32).contiguous()
+        gk = zero if gk is None else gk.to(torch.float32).contiguous()
+        dhin, dknow, drows = torch.empty_like(hin), torch.empty_like(know), torch.empty_like(rows)
+        dw1, db1, dw2, db2 = (torch.empty_like(t) for t in (w1, b1, w2, b2))
+        lib = native.lib()
+        nparts = lib.fr_health_kd_partials(n, 1)
+        part = torch.empty(nparts, dtype=torch.float32, device=dev)
+        mlp = (ctypes.c_void_p * 4)(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr())
+        dmlp = (ctypes.c_void_p * 4)(dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr())
+        thr, w_h, w_k = ctx.cfg
+        with profiling.region("health_kd", health_kd_bytes(n, H, True)):
+            native.check(lib.fr_health_kd_bwd(hin.data_ptr(), know.data_ptr(), rows.data_ptr(), labels.data_ptr(), n, H,
+                                              mlp, thr, w_h, w_k, ctx.out.data_ptr(), gh.data_ptr(), gk.data_ptr(),
+                                              dhin.data_ptr(), dknow.data_ptr(), drows.data_ptr(), dmlp,
+                                              part.data_ptr(), nparts, native.stream_of(hin)), "fr_health_kd_bwd")
+        return dhin, dknow, drows, None, dw1, db1, dw2, db2, None, None, None
+
+
+def health_kd_loss(hin, know, rows, labels, mlp, kd_threshold, w_health, w_kd):
+    """HealthRec's loss head (cikm_model.py:249-264, 304-308) in one HIP launch per direction:
+    returns (w_health * BCELoss-sum of sigmoid(mlp(hin)) vs labels,
+             w_kd * max(0, 1 - cosine_similarity(know, rows).mean() - kd_threshold)).
+    ``mlp``: nn.Sequential(Linear(64, 64), ReLU, Linear(64, H)), H <= 16."""
+    native.require_device(hin, know, rows, labels)
+    l1, l2 = mlp[0], mlp[2]
+    return _HealthKD.apply(hin.contiguous(), know.contiguous(), rows.contiguous(),
+                           labels.to(torch.float32).contiguous(), l1.weight, l1.bias, l2.weight, l2.bias,
+                           kd_threshold, w_health, w_kd)
+
+
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod

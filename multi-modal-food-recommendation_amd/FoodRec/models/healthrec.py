@@ -30,6 +30,8 @@ from FoodRec.models._graphs import side_adjacency, ui_adjacency
 
 # FR_FUSED_FUSION=0 keeps the unfused (torch + engine ops) target-attention path for A/B comparisons
 FUSED_FUSION = os.environ.get("FR_FUSED_FUSION", "1") != "0"
+# FR_FUSED_HEAD=0 keeps the torch health-MLP / BCE / cosine loss head
+FUSED_HEAD = os.environ.get("FR_FUSED_HEAD", "1") != "0"
 
 
 class TargetAttention(nn.Module):
@@ -164,18 +166,23 @@ class HealthRec(GeneralRecommender):
             item_mm, _ = self.ingre_target_atten(encoded, mm_query)
             item_know = F.normalize(item_mm).sum(1) / ingre_num.unsqueeze(1)
             health_in = F.normalize(item_health).mean(dim=1)
-        health_pred = torch.sigmoid(self.health_mlp(health_in))
-        health_loss = torch.sum(self.criterion(health_pred, health_level))
-
         mf_loss, emb3 = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                          user, pos_item, neg_item)
         # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263) as one gather
-        kd = 1 - cosine_similarity(item_know, ops.embedding(all_item, item_all), dim=-1).mean()
-        kd = self.norm_loss(kd, self.kd_threshold)
+        item_rows = ops.embedding(all_item, item_all)
+        if self._fused_head(health_in, health_level):
+            # health MLP + BCE sum and the KD cosine term, weighted, in one HIP kernel per direction
+            health_term, kd_term = ops.health_kd_loss(health_in, item_know, item_rows, health_level, self.health_mlp,
+                                                      self.kd_threshold, self.loss_health, self.loss_kd)
+        else:
+            health_pred = torch.sigmoid(self.health_mlp(health_in))
+            health_term = self.loss_health * torch.sum(self.criterion(health_pred, health_level))
+            kd = 1 - cosine_similarity(item_know, item_rows, dim=-1).mean()
+            kd_term = self.loss_kd * self.norm_loss(kd, self.kd_threshold)
 
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         reg = emb3 + (ing_norms[0] + ing_norms[1]) / B
-        return mf_loss, self.loss_health * health_loss, self.loss_kd * kd, self.reg_weight * reg
+        return mf_loss, health_term, kd_term, self.reg_weight * reg
 
     def _fused_fusion(self, encoded, mm_query) -> bool:
         """The fused modal-fusion kernels cover the reference's configuration: d=64, 2 heads, 'ln'
@@ -185,6 +192,18 @@ class HealthRec(GeneralRecommender):
                 and mm_query.shape[1] == 2 and encoded.shape[1] in ops.ENCODER_LENGTHS
                 and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
                 and a.ln.eps == b.ln.eps)
+
+    def _fused_head(self, health_in, health_level) -> bool:
+        """The fused loss head covers health_mlp = Linear(64, 64), ReLU, Linear(64, H <= 16) with
+        BCELoss(reduction='none') summed, fp32 on the GPU."""
+        m = self.health_mlp
+        return (FUSED_HEAD and health_in.is_cuda and health_in.dtype == torch.float32 and health_in.shape[-1] == 64
+                and len(m) == 3 and isinstance(m[0], nn.Linear) and isinstance(m[1], nn.ReLU)
+                and isinstance(m[2], nn.Linear) and m[0].in_features == 64 and m[0].out_features == 64
+                and m[2].in_features == 64 and 1 <= m[2].out_features <= 16 and m[0].bias is not None
+                and m[2].bias is not None and health_level.dim() == 2
+                and health_level.shape[1] == m[2].out_features
+                and isinstance(self.criterion, nn.BCELoss) and self.criterion.weight is None)
 
     def row_sparse_tables(self):
         """Parameters whose only use on the training step is a row gather (engine.dist exchanges

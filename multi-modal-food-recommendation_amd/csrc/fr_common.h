@@ -75,11 +75,33 @@ __device__ __forceinline__ float f4_dot(float4 a, float4 b) {
   return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
 
-// sum over the `width` lanes of an aligned lane group (width power of two <= 64)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float lane_value(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// sum over the `width` lanes of an aligned lane group (width power of two <= 64), the same value
+// in every lane of the group.  Within a 16-lane DPP row the partners are swapped by VALU data-
+// parallel moves (quad_perm xor 1, xor 2; row_half_mirror; row_mirror) instead of ds_bpermute
+// round trips through the LDS crossbar; rows are combined with readlane in a fixed order.  Every
+// lane of the group must be active.
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int off = WIDTH / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WIDTH);
+  static_assert(WIDTH >= 1 && WIDTH <= 64 && (WIDTH & (WIDTH - 1)) == 0, "power-of-two group <= 64");
+  if constexpr (WIDTH >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (WIDTH >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (WIDTH >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if constexpr (WIDTH >= 16) v += dpp_mov<0x140>(v); // row_mirror
+  if constexpr (WIDTH == 32) {
+    const float lo = lane_value(v, 0) + lane_value(v, 16), hi = lane_value(v, 32) + lane_value(v, 48);
+    v = (__lane_id() & 32) ? hi : lo;
+  } else if constexpr (WIDTH == 64) {
+    v = (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
+  }
   return v;
 }
 

@@ -257,3 +257,16 @@ def modal_fusion_f64(enc, query, ids, num, pad_id, ln_a, ln_b, eps=1e-12):
     know = torch.nn.functional.normalize(item_mm).sum(1) / num.unsqueeze(1)
     hin = torch.nn.functional.normalize(item_health).mean(dim=1)
     return know, hin
+
+
+def health_kd_f64(hin, know, rows, labels, w1, b1, w2, b2, kd_threshold, w_health, w_kd):
+    """HealthRec's loss head in float64 (cikm_model.py:249-264 and norm_loss :304-308):
+    (w_health * sum BCELoss(sigmoid(Linear2(relu(Linear1(hin)))), labels),
+     w_kd * max(0, 1 - cosine_similarity(know, rows, dim=-1).mean() - kd_threshold)).
+    Inputs are float64 torch tensors (requires_grad as the test needs)."""
+    F = torch.nn.functional
+    pred = torch.sigmoid(F.linear(torch.relu(F.linear(hin, w1, b1)), w2, b2))
+    health = torch.sum(torch.nn.BCELoss(reduction="none")(pred, labels))
+    kd = 1 - F.cosine_similarity(know, rows, dim=-1).mean()
+    kd = torch.max(torch.zeros((), dtype=kd.dtype), kd - kd_threshold)
+    return w_health * health, w_kd * kd
