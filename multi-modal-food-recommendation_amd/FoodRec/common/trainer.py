@@ -34,7 +34,7 @@ from torch.nn.utils.clip_grad import clip_grad_norm_
 
 from FoodRec.engine.graph import swap_sparse_attributes
 from FoodRec.engine.optim import FusedAdam
-from FoodRec.engine.sampler import BatchFeatures, TripleSampler
+from FoodRec.engine.sampler import BatchFeatures, EvalBatch, TripleSampler
 from FoodRec.utils.textio import eval_candidates
 from FoodRec.utils.utils import dict2str, early_stopping
 
@@ -262,7 +262,9 @@ class Trainer(AbstractTrainer):
         # data-parallel gradient all-reduce of FoodRec.engine.dist)
         self.grad_hook = None
         # capture the training step in a HIP graph (config key cuda_graph; GPU, single process)
-        self.use_graph = bool(config["cuda_graph"]) and self._on_gpu()
+        # host-side batch work (SCHGN's masked-ingredient SSL draws Python's random per batch) cannot
+        # be captured: those configurations step eagerly
+        self.use_graph = bool(config["cuda_graph"]) and self._on_gpu() and not config["SCHGN_ssl"]
         self._graphed = None
 
     @property
@@ -299,7 +301,7 @@ class Trainer(AbstractTrainer):
     def _features(self):
         if self._feats is None:
             self._feats = BatchFeatures(self.model.dataset if hasattr(self.model, "dataset") else self._dataset,
-                                        self.device)
+                                        self.device, ssl=bool(self.config["SCHGN_ssl"]))
         return self._feats
 
     def _opt_step(self, skip_flag):
@@ -395,16 +397,26 @@ class Trainer(AbstractTrainer):
             users, pos_lists, neg_lists = list(range(ds.num_users)), ds.testRatings, ds.testNegatives
         return eval_candidates(users, pos_lists, neg_lists)
 
+    EVAL_CHUNK_ROWS = 1 << 18
+
     @torch.no_grad()
     def _score(self, users, items):
+        """Scores of the (user, candidate) rows.  The fast graph path gathers from one forward; the
+        per-row path (inference_by_user) runs over chunks of ``eval_chunk_rows`` rows (a model
+        attribute, else EVAL_CHUNK_ROWS), each an EvalBatch with the reference's side inputs."""
         dev = torch.device(self.device)
-        batch = {"user_input": torch.from_numpy(users).to(dev), "item_input": torch.from_numpy(items).to(dev)}
         if self.config["graph_inference_fast"]:
+            batch = {"user_input": torch.from_numpy(users).to(dev), "item_input": torch.from_numpy(items).to(dev)}
             out = self.model.forward()
-            preds = self.model.inference_fast(batch, out[0], out[1])
-        else:
-            preds = self.model.inference_by_user(batch)
-        return preds.float().cpu().numpy()
+            return self.model.inference_fast(batch, out[0], out[1]).float().cpu().numpy()
+        step = int(getattr(self.model, "eval_chunk_rows", None) or self.EVAL_CHUNK_ROWS)
+        feats = self._features()
+        parts = []
+        for s in range(0, len(users), step):
+            batch = EvalBatch(feats, torch.from_numpy(users[s:s + step]).to(dev),
+                              torch.from_numpy(items[s:s + step]).to(dev))
+            parts.append(self.model.inference_by_user(batch).float().reshape(-1).cpu())
+        return torch.cat(parts).numpy() if parts else np.zeros(0, np.float32)
 
     def _valid_by_user_epoch(self, valid_data=None, is_test=False):
         users, items, lens, npos = self._candidates(is_test)

@@ -106,17 +106,59 @@ class TripleSampler:
             yield self._dev_users[idx], self._dev_items[idx], negs.to(self.device, non_blocking=True)
 
 
+SSL_MASKED_P = 0.2   # TrainDataLoader.masked_p (dataloader.py:19)
+SSL_MAX_LEN = 20     # TrainDataLoader.max_len
+
+
+def ssl_sequences(codes: np.ndarray, nums: np.ndarray, n_ingredients: int, rnd=random):
+    """TrainDataLoader.ssl_task + utils.get_neg_ingre (dataloader.py:117-143, utils/utils.py:186-190)
+    for a batch of positives in sample order, drawing from Python's ``random`` exactly as the
+    reference's per-sample __getitem__ does: per valid ingredient one random() < 0.2 masks it
+    (token n_ingredients + 1) and draws a negative ingredient by randint rejection against the
+    recipe's own ingredients.  Returns (masked, pos, neg) int64 [B, L]."""
+    B, L = codes.shape
+    masked = codes.copy()
+    neg = codes.copy()
+    mask_tok = n_ingredients + 1
+    for b in range(B):
+        k = int(nums[b])
+        row = codes[b].tolist()
+        own = set(row[:k])
+        for t in range(min(k, L)):
+            if rnd.random() < SSL_MASKED_P:
+                masked[b, t] = mask_tok
+                j = rnd.randint(0, n_ingredients - 1)
+                while j in own:
+                    j = rnd.randint(0, n_ingredients - 1)
+                neg[b, t] = j
+    return masked, codes.copy(), neg
+
+
 class BatchFeatures:
     """Device-resident per-item side tables used to assemble the reference's batch dict
-    (dataloader.py:50-115): ingredient codes/counts, health multi-hot, image rows."""
+    (dataloader.py:50-115): ingredient codes/counts, health multi-hot, image rows, calorie levels;
+    with ``ssl`` (config SCHGN_ssl) the masked-ingredient sequences of every batch."""
 
-    def __init__(self, dataset, device):
+    def __init__(self, dataset, device, ssl: bool = False):
         self.device = torch.device(device)
         self.ingre_code = torch.from_numpy(np.asarray(dataset.ingredientCodeDict, np.int64)).to(self.device)
         self.ingre_num = torch.tensor(dataset.ingredientNum, dtype=torch.int64, device=self.device)
         self.health = None
         if getattr(dataset, "health_level_multi_hot", None) is not None:
             self.health = torch.from_numpy(dataset.health_matrix()).to(self.device)
+        self.cal = None
+        cal = getattr(dataset, "cal_level", None)
+        if cal is not None:
+            dense = np.zeros(len(dataset.ingredientNum), np.int64)
+            for i, lv in (cal.items() if isinstance(cal, dict) else enumerate(cal)):
+                if 0 <= int(i) < len(dense):
+                    dense[int(i)] = int(lv)
+            self.cal = torch.from_numpy(dense).to(self.device)
+        self.ssl = bool(ssl)
+        if self.ssl:
+            self._codes_np = np.asarray(dataset.ingredientCodeDict, np.int64)
+            self._nums_np = np.asarray(dataset.ingredientNum, np.int64)
+            self._n_ingre = int(dataset.num_ingredients)
         self._image = None
         self._ds = dataset
 
@@ -126,14 +168,20 @@ class BatchFeatures:
         return self._image
 
     def batch(self, u, p, n) -> "LazyBatch":
-        return LazyBatch(self, u, p, n)
+        b = LazyBatch(self, u, p, n)
+        if self.ssl:  # eager, like the reference's per-sample __getitem__ (the RNG stream advances per batch)
+            pi = p.cpu().numpy()
+            seqs = ssl_sequences(self._codes_np[pi], self._nums_np[pi], self._n_ingre)
+            for key, arr in zip(("masked_ingre_seq", "pos_ingre_seq", "neg_ingre_seq"), seqs):
+                b[key] = torch.from_numpy(arr).to(self.device)
+        return b
 
 
 class LazyBatch(dict):
     """dict with the reference batch keys; side features are gathered on first access."""
 
-    _LAZY = ("pos_ingre_code", "pos_ingre_num", "pos_hl_mh", "pos_img",
-             "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img",
+    _LAZY = ("pos_ingre_code", "pos_ingre_num", "pos_hl_mh", "pos_img", "pos_cl",
+             "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img", "neg_cl",
              # engine extras: [pos; neg] stacked (one gather instead of two gathers and a cat)
              "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh")
 
@@ -159,6 +207,10 @@ class LazyBatch(dict):
             return f.health[idx]
         if what == "img":
             return f.image()[idx]
+        if what == "cl":
+            if f.cal is None:
+                raise KeyError(key)
+            return f.cal[idx]
         raise KeyError(key)
 
     def __missing__(self, key):
@@ -175,10 +227,59 @@ class LazyBatch(dict):
             return default
 
     def __contains__(self, key):
-        return dict.__contains__(self, key) or (key in self._LAZY and (key not in ("pos_hl_mh", "neg_hl_mh") or self._f.health is not None))
+        if dict.__contains__(self, key):
+            return True
+        if key not in self._LAZY:
+            return False
+        if key in ("pos_hl_mh", "neg_hl_mh"):
+            return self._f.health is not None
+        if key in ("pos_cl", "neg_cl"):
+            return self._f.cal is not None
+        return True
 
     def keys(self):
         return list(dict.keys(self)) + [k for k in self._LAZY if k not in dict.keys(self) and k in self]
 
     def items(self):
         return [(k, self[k]) for k in self.keys()]
+
+
+class EvalBatch(dict):
+    """The per-user evaluation batch of EvalByUserDataloader (dataloader.py:228-302) for a chunk of
+    (user, candidate) rows: ``user_input`` / ``item_input`` plus, gathered on first access, the
+    candidates' ``img_input`` (float32), ``ingre_input``, ``ingre_num_input``, ``cal_level_input``
+    and ``health_level_input`` (the reference fills the latter with the calorie level too)."""
+
+    def __init__(self, feats: BatchFeatures, users, items):
+        super().__init__(user_input=users, item_input=items)
+        self._f = feats
+
+    def _make(self, key):
+        f, it = self._f, self["item_input"]
+        if key == "img_input":
+            return f.image()[it].to(torch.float32)
+        if key == "ingre_input":
+            return f.ingre_code[it]
+        if key == "ingre_num_input":
+            return f.ingre_num[it]
+        if key in ("cal_level_input", "health_level_input") and f.cal is not None:
+            return f.cal[it]
+        raise KeyError(key)
+
+    def __missing__(self, key):
+        v = self._make(key)
+        self[key] = v
+        return v
+
+    def get(self, key, default=None):
+        try:
+            return self[key]
+        except KeyError:
+            return default
+
+    def __contains__(self, key):
+        if dict.__contains__(self, key):
+            return True
+        if key in ("img_input", "ingre_input", "ingre_num_input"):
+            return True
+        return key in ("cal_level_input", "health_level_input") and self._f.cal is not None

@@ -195,6 +195,11 @@ class FoodData:
             a["text_cluster"] = ds.text_cluster.astype(np.float64)
         if "health" in flags:
             a["health"] = {i: row for i, row in enumerate(ds.health.tolist())}
+        if "schgn" in flags:  # SCHGN's user-recipe and recipe-calorie graphs + calorie levels
+            cal = ds.extra["cal_level"]
+            a["ur"] = np.asarray(ds.train, np.int64)
+            a["rc"] = np.stack([np.arange(ds.n_items, dtype=np.int64), cal], 1)
+            a["cal_level"] = {i: int(v) for i, v in enumerate(cal.tolist())}
         return cls(args_config, _arrays=a)
 
     # ----------------------------------------------------------------------------- build

@@ -192,9 +192,12 @@ def make_synthetic(shape: str = "tiny", seed: int = 0, negatives: bool = True, *
     image_cluster = np.stack([item_ids, img_c.reshape(-1)], 1)
     text_cluster = np.stack([item_ids, txt_c.reshape(-1)], 1)
     health = (rng.random((I, cfg["health"])) < 0.35).astype(np.int64)
+    # SCHGN's calorie level per recipe (0..5), from its own generator: the main stream (and the
+    # goldens' dataset digest) is unchanged
+    cal_level = np.random.default_rng([seed, 0xCA1]).integers(0, 6, I).astype(np.int64)
     return SyntheticFood(shape, U, I, NI, C, train, valid, test, valid_users.astype(np.int64),
                          valid_neg, test_neg, code, k.astype(np.int64), image, text,
-                         image_cluster, text_cluster, health)
+                         image_cluster, text_cluster, health, extra={"cal_level": cal_level})
 
 
 def _distinct_rows(rng, rows: int, n: int, k: int) -> np.ndarray:
@@ -274,4 +277,10 @@ def write_reference_format(ds: SyntheticFood, data_path: str, dataset: str) -> s
         pickle.dump(mat, f)
     with open(root + "graph_edge/recipe_health_level_multi_hot_dict.pkl", "wb") as f:
         pickle.dump({i: row for i, row in enumerate(ds.health.tolist())}, f)
+    # SCHGN's graphs: user-recipe (the training interactions), recipe-calorie level, level dict
+    np.savetxt(root + "graph_edge/ur_graph.txt", ds.train, fmt="%d")
+    cal = ds.extra["cal_level"]
+    np.savetxt(root + "graph_edge/rc_graph.txt", np.stack([np.arange(ds.n_items), cal], 1), fmt="%d")
+    with open(root + "graph_edge/recipe_cal_level_dict.pkl", "wb") as f:
+        pickle.dump({i: int(v) for i, v in enumerate(cal.tolist())}, f)
     return root

@@ -18,6 +18,7 @@ ENGINE_MODELS = {
     "pricai_modelx": ("FoodRec.models.clussl", "CLUSSL"),
     "clussl": ("FoodRec.models.clussl", "CLUSSL"),
     "lightgcn_id": ("FoodRec.models.lightgcn_id", "LightGCN_ID"),
+    "schgn": ("FoodRec.models.schgn", "SCHGN"),
 }
 
 
@@ -71,3 +72,12 @@ def early_stopping(value, best, cur_step, max_step, bigger=True):
 
 def dict2str(result_dict) -> str:
     return "".join(f"{k}: {v:.04f}    " for k, v in result_dict.items())
+
+
+def get_neg_ingre(ingre_set, ingre_size):
+    """utils/utils.py:186-190: an ingredient id uniform in [0, ingre_size) not in ``ingre_set``,
+    by rejection on Python's random.randint."""
+    ingre_id = random.randint(0, ingre_size - 1)
+    while ingre_id in ingre_set:
+        ingre_id = random.randint(0, ingre_size - 1)
+    return ingre_id

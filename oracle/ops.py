@@ -270,3 +270,32 @@ def health_kd_f64(hin, know, rows, labels, w1, b1, w2, b2, kd_threshold, w_healt
     kd = 1 - F.cosine_similarity(know, rows, dim=-1).mean()
     kd = torch.max(torch.zeros((), dtype=kd.dtype), kd - kd_threshold)
     return w_health * health, w_kd * kd
+
+
+def gcn_conv_f64(x, edge_index, weight, bias, edge_weight=None, improved=False):
+    """PyG GCNConv (documented semantics; PyG is not installed, parity unpinned) in float64 with
+    explicit per-edge loops: add_remaining_self_loops (fill 1 / 2 if improved; an existing loop
+    keeps its weight), deg over targets, w = deg^-1/2[src] w deg^-1/2[dst], out[dst] += w (x W^T)[src],
+    + bias.  x [N, in], edge_index [2, E] (src, dst), weight [out, in]."""
+    x = np.asarray(x, np.float64)
+    ei = np.asarray(edge_index, np.int64)
+    N = x.shape[0]
+    w_in = np.ones(ei.shape[1]) if edge_weight is None else np.asarray(edge_weight, np.float64)
+    loop_w = np.full(N, 2.0 if improved else 1.0)
+    edges = []
+    for e in range(ei.shape[1]):
+        s, d = int(ei[0, e]), int(ei[1, e])
+        if s == d:
+            loop_w[s] = w_in[e]
+        else:
+            edges.append((s, d, w_in[e]))
+    edges += [(i, i, loop_w[i]) for i in range(N)]
+    deg = np.zeros(N)
+    for s, d, w in edges:
+        deg[d] += w
+    dinv = np.where(deg > 0, deg ** -0.5, 0.0)
+    h = x @ np.asarray(weight, np.float64).T
+    out = np.zeros((N, h.shape[1]))
+    for s, d, w in edges:
+        out[d] += dinv[s] * w * dinv[d] * h[s]
+    return out + (0.0 if bias is None else np.asarray(bias, np.float64))
