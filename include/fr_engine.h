@@ -419,6 +419,25 @@ int fr_health_kd_bwd(const float* d_hin, const float* d_know, const float* d_row
                      int64_t partial_floats, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Modal projections over gathered feature rows (image_trs / text_trs of HealthRec,
+ * models/cikm_model.py:240-241: Linear(K -> 64) applied to embImage / embText rows of the batch items).
+ * fr_gather_linear_fwd: Y[i, 0:64] = X[ids[i], 0:K] W^T + b  (W [64, K] nn.Linear layout, b may be
+ *   NULL, Y rows at stride ldy: the two modalities write one [n, 2, 64] query tensor).  K a multiple of
+ *   16, X rows / W 16-byte aligned.  Deterministic.
+ * fr_rows_matmul: out[i, 0:K] = S[i, 0:64] W  -- the table gradient of a gathered Linear input as
+ *   (per-id sum of dY rows) x W (the compact rows of fr_embedding_rowgrad on dY), instead of scattering
+ *   dX = dY W (replaces the index backward of embImage[ids] feeding image_trs).
+ * fr_linear_wgrad_gather: fr_linear_wgrad with X row m read from X[ids[m]] (dW = dY^T X[ids]).
+ * ------------------------------------------------------------------------------------------ */
+int fr_gather_linear_fwd(const int64_t* d_ids, int64_t n, const float* d_x, int64_t ldx, int K, const float* d_w,
+                         const float* d_b, float* d_y, int64_t ldy, void* stream);
+int fr_rows_matmul(const float* d_s, int64_t lds, int64_t n, const float* d_w, int K, float* d_out, int64_t ldo,
+                   void* stream);
+int fr_linear_wgrad_gather(const float* d_dy, int64_t ldy, const int64_t* d_ids, const float* d_x, int64_t ldx,
+                           int64_t M, int N, int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace,
+                           int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Host-side readers of the reference's on-disk interaction formats (no GPU).
  *   FR_IO_NEGATIVE  data.{valid,test}.negative: "(u,i)\tn1\tn2..." per line; the first field is
  *                   dropped, the rest are int() ids -> ragged rows (values, offsets[rows+1]).

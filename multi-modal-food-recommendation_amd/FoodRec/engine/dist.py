@@ -46,15 +46,21 @@ class RowExchange:
         # instead of scattering a dense table gradient
         self.sink = None
 
-    def stash(self, weight, padding_idx, ids, G):
+    def stash(self, weight, padding_idx, ids, G, W=None):
         s = self.slots.get(id(weight))
-        if s is None or s["ids"].shape != ids.shape or s["G"].shape != G.shape:
-            s = {"weight": weight, "pad": padding_idx, "ids": torch.empty_like(ids), "G": torch.empty_like(G),
+        if s is None or s["ids"].shape != ids.shape or s["G"].shape != G.shape or s["W"] is not W:
+            s = {"weight": weight, "pad": padding_idx, "ids": torch.empty_like(ids),
+                 "G": torch.empty(G.shape, dtype=G.dtype, device=G.device), "W": W,
                  "ids_all": torch.empty((self.world,) + tuple(ids.shape), dtype=ids.dtype, device=ids.device),
                  "G_all": torch.empty((self.world,) + tuple(G.shape), dtype=G.dtype, device=G.device)}
             self.slots[id(weight)] = s
         s["ids"].copy_(ids)
         s["G"].copy_(G)
+
+    def stash_factored(self, weight, padding_idx, ids, dY, W):
+        """Gradient rows dY[i] W of a gathered Linear input (ops.modal_projection): only the 64-wide
+        dY rows and the ids cross the interconnect; W is replicated on every rank."""
+        self.stash(weight, padding_idx, ids, dY, W)
 
     def exchange(self):
         import torch.distributed as dist
@@ -68,10 +74,16 @@ class RowExchange:
             w = s["weight"]
             d = s["G"].shape[-1]
             rows = s["G_all"].reshape(-1, d) * (1.0 / self.world)
-            if self.sink is not None:
-                self.sink.stash(w, s["pad"], s["ids_all"].reshape(-1), rows)
+            ids = s["ids_all"].reshape(-1)
+            if s["W"] is not None:  # factored: rows are dY, the table gradient rows are dY W
+                if self.sink is not None:
+                    self.sink.stash_factored(w, s["pad"], ids, rows, s["W"])
+                else:
+                    w.grad = ops.scatter_rows(ids, rows @ s["W"], w.shape[0], s["pad"])
+            elif self.sink is not None:
+                self.sink.stash(w, s["pad"], ids, rows)
             else:
-                w.grad = ops.scatter_rows(s["ids_all"].reshape(-1), rows, w.shape[0], s["pad"])
+                w.grad = ops.scatter_rows(ids, rows, w.shape[0], s["pad"])
 
 
 class GradAllReduce:

@@ -135,6 +135,11 @@ _SIGS = {
     "fr_health_kd_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p),
                                  c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
+    "fr_gather_linear_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_int64, c_void_p]),
+    "fr_rows_matmul": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
+    "fr_linear_wgrad_gather": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int,
+                                       c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_io_open": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
     "fr_io_fill": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
     "fr_io_close": (None, [c_void_p]),

@@ -662,6 +662,127 @@ def modal_fusion(enc, query, ids, num, pad_id, ln_a, ln_b):
                               ln_a.eps, ln_a.weight, ln_a.bias, ln_b.weight, ln_b.bias)
 
 
+# ----------------------------------------------------------------------------- modal projections
+def projection_bytes(n: int, K: int, backward: bool) -> int:
+    """Algorithmic HBM bytes of one modality: the n gathered K-wide rows and W read, Y written
+    (forward); dY and the gathered rows read again for dW (backward wgrad)."""
+    return 4 * (n * K + 64 * K + n * 64) + (4 * (n * K + n * 64 + 64 * K) if backward else 0)
+
+
+def factored_rows(ids, G, width: int, R: int, pad, Ws):
+    """Row gradients of gathered Linear inputs: ``G`` holds len(Ws) adjacent 64-wide dY blocks
+    ([n, width], row stride G.stride(0)); one fr_embedding_rowgrad over them gives the row map
+    (rmap[r] = slot of id r, -1 if absent) and the per-id dY sums in ascending position order; then
+    rows_t = sums_t W_t (fr_rows_matmul).  Returns (rmap [R] int32, [rows_t [n, K_t]])."""
+    lib = native.lib()
+    ids = ids.reshape(-1)
+    n = ids.numel()
+    dev = G.device
+    rmap = torch.empty(R, dtype=torch.int32, device=dev)
+    S = torch.empty(max(n, 1), width, dtype=torch.float32, device=dev)
+    ws = native.workspace(lib.fr_embedding_rowgrad_workspace(n, R, width), dev)
+    with profiling.region("embedding_rowgrad", 4 * R + 8 * n + 8 * n * width):
+        native.check(lib.fr_embedding_rowgrad(ids.data_ptr(), n, G.data_ptr(), G.stride(0), width, R,
+                                              -1 if pad is None else int(pad), rmap.data_ptr(), S.data_ptr(),
+                                              ws.data_ptr(), ws.numel(), native.stream_of(G)), "fr_embedding_rowgrad")
+    rows = []
+    for k, W in enumerate(Ws):
+        K = W.shape[1]
+        crow = torch.empty(max(n, 1), K, dtype=torch.float32, device=dev)
+        with profiling.region("rows_matmul", 4 * (n * 64 + 64 * K + n * K)):
+            native.check(lib.fr_rows_matmul(S[:, 64 * k:].data_ptr(), width, n, W.data_ptr(), K, crow.data_ptr(), K,
+                                            native.stream_of(G)), "fr_rows_matmul")
+        rows.append(crow)
+    return rmap, rows
+
+
+def rows_to_dense(rmap, crow):
+    """The dense table gradient of (rmap, compact rows), without a host synchronisation."""
+    has = (rmap >= 0).unsqueeze(1)
+    return torch.where(has, crow[rmap.clamp(min=0).long()], torch.zeros((), dtype=crow.dtype, device=crow.device))
+
+
+class _ModalProjection(torch.autograd.Function):
+    """fr_gather_linear_fwd per modality into one [n, T, 64] tensor; backward: dW / db by
+    fr_linear_wgrad_gather, the feature tables' gradient factored as (ids, dY, W) -- stashed in the
+    row-gradient exchange (FusedAdam: compact rows = per-id sum of dY x W, fr_rows_matmul), or, with
+    no exchange, scattered densely."""
+
+    @staticmethod
+    def forward(ctx, ids, exchange, *flat):
+        T = len(flat) // 3
+        n = ids.numel()
+        dev = ids.device
+        lib = native.lib()
+        out = torch.empty(n, T, 64, dtype=torch.float32, device=dev)
+        for t in range(T):
+            X, W, b = flat[3 * t], flat[3 * t + 1], flat[3 * t + 2]
+            K = W.shape[1]
+            with profiling.region("modal_projection", projection_bytes(n, K, False)):
+                native.check(lib.fr_gather_linear_fwd(ids.data_ptr(), n, X.data_ptr(), X.stride(0), K, W.data_ptr(),
+                                                      native.ptr(b), out[:, t].data_ptr(), T * 64,
+                                                      native.stream_of(X)), "fr_gather_linear_fwd")
+        ctx.save_for_backward(ids, *flat)
+        ctx.exchange, ctx.T = exchange, T
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ids, *flat = ctx.saved_tensors
+        T, n = ctx.T, ids.numel()
+        g = g.contiguous()
+        G2 = g.view(n, T * 64)
+        lib = native.lib()
+        grads = [None, None]
+        dense = None
+        if ctx.exchange is None and any(ctx.needs_input_grad[2 + 3 * t] for t in range(T)):
+            # same kernels as the row-gradient path: dense and row modes see bit-identical table rows
+            R = flat[0].shape[0]
+            if all(flat[3 * t].shape[0] == R for t in range(T)) and (T * 64) & (T * 64 - 1) == 0:
+                rmap, crows = factored_rows(ids, G2, T * 64, R, None, [flat[3 * t + 1] for t in range(T)])
+                dense = [rows_to_dense(rmap, c) for c in crows]
+            else:
+                dense = []
+                for t in range(T):
+                    rmap, (c,) = factored_rows(ids, G2[:, 64 * t:], 64, flat[3 * t].shape[0], None, [flat[3 * t + 1]])
+                    dense.append(rows_to_dense(rmap, c))
+        for t in range(T):
+            X, W, b = flat[3 * t], flat[3 * t + 1], flat[3 * t + 2]
+            K = W.shape[1]
+            dW = torch.empty_like(W)
+            db = torch.empty_like(b) if b is not None else None
+            ws = native.workspace(lib.fr_linear_wgrad_workspace(n, 64, K), g.device)
+            dy = G2[:, 64 * t:64 * (t + 1)]
+            with profiling.region("modal_projection", projection_bytes(n, K, True)):
+                native.check(lib.fr_linear_wgrad_gather(dy.data_ptr(), G2.stride(0), ids.data_ptr(), X.data_ptr(),
+                                                        X.stride(0), n, 64, K, dW.data_ptr(), dW.stride(0),
+                                                        native.ptr(db), ws.data_ptr(), ws.numel(),
+                                                        native.stream_of(g)), "fr_linear_wgrad_gather")
+            dX = None
+            if ctx.needs_input_grad[2 + 3 * t]:
+                if ctx.exchange is not None:
+                    ctx.exchange.stash_factored(X, None, ids, dy, W)
+                else:
+                    dX = dense[t]
+            grads += [dX, dW if ctx.needs_input_grad[3 + 3 * t] else None,
+                      db if (b is not None and ctx.needs_input_grad[4 + 3 * t]) else None]
+        return tuple(grads)
+
+
+def modal_projection(ids, pairs, exchange=None):
+    """``torch.stack([lin(table[ids]) for table, lin in pairs], 1)`` -> [n, T, 64] (HealthRec's
+    mm_query, cikm_model.py:240-243), the gathers folded into the projection GEMM.  ``pairs``:
+    [(feature table [R, K], nn.Linear(K, 64)), ...]; ``exchange``: a RowGrads / RowExchange taking the
+    tables' factored row gradients (else dense table gradients)."""
+    native.require_device(ids, *[t for t, _ in pairs])
+    flat = []
+    for table, lin in pairs:
+        if lin.out_features != 64 or table.shape[1] != lin.in_features or lin.in_features % 16:
+            raise native.EngineError("modal_projection: Linear(K -> 64) with K a multiple of 16 required")
+        flat += [table, lin.weight, lin.bias]
+    return _ModalProjection.apply(ids.reshape(-1).contiguous(), exchange, *flat)
+
+
 # ----------------------------------------------------------------------------- health / KD head
 _HEAD_FWD_PARTS = {}  # device -> zero-initialised forward partials (+ ticket word; the kernel re-zeroes it)
 

@@ -41,7 +41,19 @@ class RowGrads:
     backward passes) accumulate, exactly as dense gradients would."""
 
     def __init__(self):
-        self.pending = {}  # id(weight) -> [weight, padding_idx, [ids], [rows]]
+        self.pending = {}   # id(weight) -> [weight, padding_idx, [ids], [rows]]
+        # id(weight) -> (weight, padding_idx, ids, dY [n, 64], W [64, K]): gradient rows dY[i] W of a
+        # gathered Linear input (ops.modal_projection), materialised by FusedAdam before any update
+        self.factored = {}
+
+    def stash_factored(self, weight, padding_idx, ids, dY, W):
+        if id(weight) in self.pending or id(weight) in self.factored:  # repeated backward: explicit rows
+            e = self.factored.pop(id(weight), None)
+            if e is not None:
+                self.stash(e[0], e[1], e[2], e[3] @ e[4])
+            self.stash(weight, padding_idx, ids, dY @ W)
+            return
+        self.factored[id(weight)] = (weight, padding_idx, ids, dY, W)
 
     def stash(self, weight, padding_idx, ids, G):
         e = self.pending.get(id(weight))
@@ -53,6 +65,10 @@ class RowGrads:
 
     def clear(self):
         self.pending.clear()
+        self.factored.clear()
+
+    def __bool__(self):
+        return bool(self.pending or self.factored)
 
     def take(self, weight):
         e = self.pending.pop(id(weight), None)
@@ -87,6 +103,9 @@ class FusedAdam(torch.optim.Optimizer):
         """Turn pending row gradients into dense ``.grad`` tensors (accumulating), for callers that
         read or clip gradients between backward and step."""
         from . import ops
+        for w, pad, ids, dY, W in list(self.row_grads.factored.values()):
+            self.row_grads.stash(w, pad, ids, dY @ W)
+        self.row_grads.factored.clear()
         for w, pad, ids, G in list(self.row_grads.pending.values()):
             ids, G, pad = self.row_grads.take(w)
             dense = ops.scatter_rows(ids.reshape(-1), G.reshape(-1, w.shape[-1]), w.shape[0], pad)
@@ -122,10 +141,20 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = native.lib()
+        # factored row gradients read the projection weights: materialise them before any update
+        prepared = self._prepare_factored(lib) if self.row_grads.factored else {}
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
             plist, rows = [], []
             for p in group["params"]:
+                if id(p) in prepared:
+                    rows.append((p, prepared.pop(id(p))))
+                    st = self.state[p]
+                    if len(st) == 0:
+                        st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
+                        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    continue
                 rg = self.row_grads.take(p) if self.row_grads.pending else None
                 if rg is not None and (p.grad is not None or not _row_grad_ok(p, rg[0], rg[1])):
                     from . import ops  # dense fallback: scatter the rows into (or onto) .grad
@@ -187,9 +216,48 @@ class FusedAdam(torch.optim.Optimizer):
         P, G, M, V, S, N = self._arrays(plist, grads)
         native.check(lib.fr_adam_step_dev(P, G, M, V, S, N, len(plist), *hyper), "fr_adam_step_dev")
 
+    def _prepare_factored(self, lib) -> dict:
+        """Compact rows + row map of every factored entry: one fr_embedding_rowgrad over the entries'
+        dY rows (entries with the same ids whose dY views are adjacent columns of one buffer share it),
+        then rows = (per-id sum of dY) W by fr_rows_matmul.  Entries that cannot take the row path
+        (a dense gradient already present, an unsupported table) become dense gradients."""
+        from . import ops
+        groups = {}
+        for key, (w, pad, ids, dY, W) in list(self.row_grads.factored.items()):
+            if w.grad is not None or not _row_grad_ok(w, ids, w) or dY.stride(1) != 1 or w.shape[1] != W.shape[1]:
+                dense = ops.scatter_rows(ids.reshape(-1), dY @ W, w.shape[0], pad)
+                w.grad = dense if w.grad is None else w.grad.add_(dense)
+                continue
+            groups.setdefault((id(ids), w.shape[0], pad, dY.stride(0)), []).append((w, ids, dY, W))
+        self.row_grads.factored.clear()
+        out = {}
+        for (_, R, pad, ld), ents in groups.items():
+            ents.sort(key=lambda e: e[2].data_ptr())
+            base = ents[0][2]
+            adjacent = all(e[2].data_ptr() == base.data_ptr() + 4 * 64 * k for k, e in enumerate(ents))
+            width = 64 * len(ents)
+            if not (adjacent and width & (width - 1) == 0 and ld >= width):
+                for e in ents:  # one row pass per table
+                    out.update(self._factored_rows(lib, [e], e[2], 64, R, pad))
+                continue
+            out.update(self._factored_rows(lib, ents, base, width, R, pad))
+        return out
+
+    def _factored_rows(self, lib, ents, G, width, R, pad):
+        from . import ops
+        rmap, crows = ops.factored_rows(ents[0][1], G, width, R, pad, [e[3] for e in ents])
+        return {id(e[0]): ("prepared", rmap, c) for e, c in zip(ents, crows)}
+
     def _launch_rows(self, lib, rows, hyper):
         plist, compact, maps, dims = [], [], [], []
-        for p, (ids, G, pad) in rows:
+        for p, entry in rows:
+            if entry[0] == "prepared":
+                plist.append(p)
+                compact.append(entry[2])
+                maps.append(entry[1])
+                dims.append(p.shape[1])
+                continue
+            ids, G, pad = entry
             R, d = p.shape
             ids = ids.reshape(-1)
             G = G.reshape(-1, d)

@@ -32,6 +32,8 @@ from FoodRec.models._graphs import side_adjacency, ui_adjacency
 FUSED_FUSION = os.environ.get("FR_FUSED_FUSION", "1") != "0"
 # FR_FUSED_HEAD=0 keeps the torch health-MLP / BCE / cosine loss head
 FUSED_HEAD = os.environ.get("FR_FUSED_HEAD", "1") != "0"
+# FR_FUSED_PROJECTION=0 keeps gather + ops.linear for the image / text projections
+FUSED_PROJECTION = os.environ.get("FR_FUSED_PROJECTION", "1") != "0"
 
 
 class TargetAttention(nn.Module):
@@ -152,11 +154,16 @@ class HealthRec(GeneralRecommender):
         all_item = _pn(batch_data, "i_id")
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
         xg = self.__dict__.get("_fr_exchange")  # data-parallel: rows exchanged, not tables
-        img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange=xg),
-                           self.image_trs.weight, self.image_trs.bias).unsqueeze(1)
-        txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange=xg),
-                           self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
-        mm_query = torch.cat([img_q, txt_q], dim=1)
+        if self._fused_projection(all_item):
+            # gathers folded into the projection GEMMs; the tables' gradient stays factored (dY, W)
+            mm_query = ops.modal_projection(all_item, [(self.image_embedding.weight, self.image_trs),
+                                                       (self.text_embedding.weight, self.text_trs)], exchange=xg)
+        else:
+            img_q = ops.linear(ops.embedding(all_item, self.image_embedding.weight, exchange=xg),
+                               self.image_trs.weight, self.image_trs.bias).unsqueeze(1)
+            txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange=xg),
+                               self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
+            mm_query = torch.cat([img_q, txt_q], dim=1)
         if self._fused_fusion(encoded, mm_query):
             # both target attentions + the normalize heads in one HIP kernel pair (fr_modal_fusion_*)
             item_know, health_in = ops.modal_fusion(encoded, mm_query, ingredients, ingre_num, self.n_ingredients,
@@ -192,6 +199,14 @@ class HealthRec(GeneralRecommender):
                 and mm_query.shape[1] == 2 and encoded.shape[1] in ops.ENCODER_LENGTHS
                 and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
                 and a.ln.eps == b.ln.eps)
+
+    def _fused_projection(self, ids) -> bool:
+        """Both modal tables present, fp32 on the GPU, Linear(K -> 64) with K a multiple of 16."""
+        if not (FUSED_PROJECTION and ids.is_cuda and hasattr(self, "image_embedding") and hasattr(self, "text_embedding")):
+            return False
+        return all(t.weight.dtype == torch.float32 and t.weight.is_contiguous() and lin.out_features == 64
+                   and lin.in_features % 16 == 0 and lin.bias is not None
+                   for t, lin in ((self.image_embedding, self.image_trs), (self.text_embedding, self.text_trs)))
 
     def _fused_head(self, health_in, health_level) -> bool:
         """The fused loss head covers health_mlp = Linear(64, 64), ReLU, Linear(64, H <= 16) with

@@ -26,8 +26,16 @@ __device__ __forceinline__ float4 ld4_masked(const float* base, int64_t ld, int6
 }
 
 // grid: x = slab, y = n-tile * ktiles + k-tile.  part: [slabs][N][K], pdb: [slabs][N]
+// X row m is X[ids[m]] when ids is given (gathered rows: the image / text projections)
+__device__ __forceinline__ float4 ldx4(const float* X, int64_t ldx, const int64_t* ids, int64_t m, int64_t M, int c,
+                                       int C) {
+  if (m < M && c < C) return *reinterpret_cast<const float4*>(X + (ids ? ids[m] : m) * ldx + c);
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict__ dY, int64_t ldy,
-                                                         const float* __restrict__ X, int64_t ldx, int64_t M,
+                                                         const float* __restrict__ X, int64_t ldx,
+                                                         const int64_t* __restrict__ ids, int64_t M,
                                                          int N, int K, int ktiles, float* __restrict__ part,
                                                          float* __restrict__ pdb) {
   __shared__ float4 As[SUB][TN / 4];
@@ -46,14 +54,14 @@ __global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 ra = ld4_masked(dY, ldy, m0 + lr, m1, n0 + lc * 4, N);
-  float4 rb = ld4_masked(X, ldx, m0 + lr, m1, k0 + lc * 4, K);
+  float4 rb = ldx4(X, ldx, ids, m0 + lr, m1, k0 + lc * 4, K);
   for (int64_t ms = m0; ms < m1; ms += SUB) {
     As[lr][lc] = ra;
     Bs[lr][lc] = rb;
     __syncthreads();
     if (ms + SUB < m1) {  // prefetch the next sub-tile while this one is consumed
       ra = ld4_masked(dY, ldy, ms + SUB + lr, m1, n0 + lc * 4, N);
-      rb = ld4_masked(X, ldx, ms + SUB + lr, m1, k0 + lc * 4, K);
+      rb = ldx4(X, ldx, ids, ms + SUB + lr, m1, k0 + lc * 4, K);
     }
 #pragma unroll
     for (int r = 0; r < SUB; ++r) {
@@ -122,9 +130,9 @@ extern "C" int64_t fr_linear_wgrad_workspace(int64_t M, int N, int K) {
   return fr::align_up(slabs * N * K * 4, 256) + fr::align_up(slabs * N * 4, 256);
 }
 
-extern "C" int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x, int64_t ldx, int64_t M, int N,
-                               int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace,
-                               int64_t workspace_bytes, void* stream) {
+static int wgrad_impl(const float* d_dy, int64_t ldy, const int64_t* d_ids, const float* d_x, int64_t ldx, int64_t M,
+                      int N, int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace, int64_t workspace_bytes,
+                      void* stream) {
   FR_REQUIRE(M > 0 && N > 0 && K > 0, "empty problem");
   FR_REQUIRE(N % 4 == 0 && K % 4 == 0, "N and K must be multiples of 4");
   FR_REQUIRE(d_dy && d_x && d_dw && ldy >= N && ldx >= K && ldw >= K && ldy % 4 == 0 && ldx % 4 == 0,
@@ -139,11 +147,24 @@ extern "C" int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x,
   float* pdb = reinterpret_cast<float*>(reinterpret_cast<char*>(d_workspace) + fr::align_up(slabs * N * K * 4, 256));
   const int ntiles = (int)fr::ceil_div(N, TN), ktiles = (int)fr::ceil_div(K, TK);
   hipLaunchKernelGGL(wgrad_slab_kernel, dim3((unsigned)slabs, (unsigned)(ntiles * ktiles)), dim3(256), 0, s, d_dy,
-                     ldy, d_x, ldx, M, N, K, ktiles, part, d_db ? pdb : nullptr);
+                     ldy, d_x, ldx, d_ids, M, N, K, ktiles, part, d_db ? pdb : nullptr);
   FR_LAUNCH_CHECK();
   const int64_t total = (int64_t)N * K + (d_db ? N : 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)fr::ceil_div(total, 64)), dim3(256), 0, s, part, slabs, N,
                      K, d_dw, ldw, pdb, d_db);
   FR_LAUNCH_CHECK();
   return FR_OK;
+}
+
+extern "C" int fr_linear_wgrad(const float* d_dy, int64_t ldy, const float* d_x, int64_t ldx, int64_t M, int N,
+                               int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace,
+                               int64_t workspace_bytes, void* stream) {
+  return wgrad_impl(d_dy, ldy, nullptr, d_x, ldx, M, N, K, d_dw, ldw, d_db, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_linear_wgrad_gather(const float* d_dy, int64_t ldy, const int64_t* d_ids, const float* d_x,
+                                      int64_t ldx, int64_t M, int N, int K, float* d_dw, int64_t ldw, float* d_db,
+                                      void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(d_ids, "null ids");
+  return wgrad_impl(d_dy, ldy, d_ids, d_x, ldx, M, N, K, d_dw, ldw, d_db, d_workspace, workspace_bytes, stream);
 }
