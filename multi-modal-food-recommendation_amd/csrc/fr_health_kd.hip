@@ -14,8 +14,8 @@
 // Elementwise formulas follow ATen's kernels (sigmoid 1/(1+exp(-x)); BCE with log/log1p clamped at
 // -100; BCE backward (p-y)/max((1-p)p, 1e-12); sigmoid backward g(1-p)p; cosine norms clamped at
 // 1e-8; maximum's backward halves the gradient on a tie).
-// Loss sums are per-block partials summed by the last block to finish (ticket; one fixed-order wave
-// sum); parameter gradients are per-block partials summed in a fixed order by a reduce kernel.
+// Loss sums are per-block partials summed by a one-wave finalize launch (fixed-order wave sum);
+// parameter gradients are per-block partials summed in a fixed order by a reduce kernel.
 // Item inputs are loaded one item ahead; every load loop has a compile-time trip count.
 #include "fr_common.h"
 
@@ -39,8 +39,7 @@ struct HeadArgs {
   const float *w1, *b1, *w2, *b2;  // [64,64], [64], [H,64], [H]
   float thr, wh, wk;
   float* out;           // [3]: w_h * health, w_k * kd_term, kd - thr (the gate, for the backward)
-  float* part;          // forward: [nblk, 2] after the ticket word; backward: [nblk, NPART_BWD]
-  unsigned* ticket;
+  float* part;          // forward: [nblk, 2]; backward: [nblk, NPART_BWD]
   // backward
   const float* gh;      // d loss / d out[0]  (device scalar)
   const float* gk;      // d loss / d out[1]
@@ -115,7 +114,6 @@ __global__ __launch_bounds__(64 * WAVES) void head_fwd_kernel(HeadArgs a) {
   __shared__ float sw2[HMAX * D];
   __shared__ float sb[D + HMAX];
   __shared__ float red[WAVES][2];
-  __shared__ bool last;
   stage_weights(a, sw1, sw2, sb);
   const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
   float sum_bce = 0.f, sum_cos = 0.f;
@@ -147,23 +145,21 @@ __global__ __launch_bounds__(64 * WAVES) void head_fwd_kernel(HeadArgs a) {
     for (int q = 0; q < WAVES; ++q) { sb_ += red[q][0]; sc += red[q][1]; }
     a.part[2 * blockIdx.x] = sb_;
     a.part[2 * blockIdx.x + 1] = sc;
-    __threadfence();
-    last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
   }
-  __syncthreads();
-  if (!last || w != 0) return;
-  __threadfence();
-  // gridDim.x <= 64: lane b loads block b's partials, one fixed-order wave sum each
-  const bool has = j < (int)gridDim.x;
-  const float tb = wsum(has ? __builtin_nontemporal_load(&a.part[2 * j]) : 0.f);
-  const float tc = wsum(has ? __builtin_nontemporal_load(&a.part[2 * j + 1]) : 0.f);
+}
+
+// the loss terms from the <= 64 block partials (lane b: block b), one fixed-order wave sum each
+__global__ __launch_bounds__(64) void head_final_kernel(HeadArgs a, int nblk) {
+  const int j = threadIdx.x;
+  const bool has = j < nblk;
+  const float tb = wsum(has ? a.part[2 * j] : 0.f);
+  const float tc = wsum(has ? a.part[2 * j + 1] : 0.f);
   if (j != 0) return;
   const float kd = 1.f - tc / (float)a.n;
   const float x = kd - a.thr;
   a.out[0] = a.wh * tb;
   a.out[1] = a.wk * fmaxf(0.f, x);
   a.out[2] = x;
-  *a.ticket = 0u;  // ready for the next launch (graph replays)
 }
 
 __global__ __launch_bounds__(64 * WAVES) void head_bwd_kernel(HeadArgs a) {
@@ -316,10 +312,13 @@ extern "C" int fr_health_kd_fwd(const float* d_hin, const float* d_know, const f
   if (rc) return rc;
   FR_REQUIRE(d_partials && partial_floats >= fr_health_kd_partials(n_items, 0), "partial buffer too small");
   const int nb = blocks_for(n_items);
-  // the ticket sits at a fixed offset (word 0) so launches with different grids share it
-  a.ticket = reinterpret_cast<unsigned*>(d_partials);
-  a.part = d_partials + 1;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(nb), dim3(64 * WAVES), 0, reinterpret_cast<hipStream_t>(stream), a);
+  a.part = d_partials + 1;  // word 0 is unused (kept for the partial-buffer layout)
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(nb), dim3(64 * WAVES), 0, s, a);
+  FR_LAUNCH_CHECK();
+  // a second launch instead of an in-kernel last-block reduction: a device-scope fence per block
+  // costs more than the kernel boundary
+  hipLaunchKernelGGL(head_final_kernel, dim3(1), dim3(64), 0, s, a, nb);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
