@@ -188,7 +188,7 @@ class HealthRec(GeneralRecommender):
             kd_term = self.loss_kd * self.norm_loss(kd, self.kd_threshold)
 
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
-        reg = emb3 + (ing_norms[0] + ing_norms[1]) / B
+        reg = emb3 + ing_norms.sum() / B  # (= ing_norms[0] + ing_norms[1]; sum's backward is a view, no fills)
         return mf_loss, health_term, kd_term, self.reg_weight * reg
 
     def _fused_fusion(self, encoded, mm_query) -> bool:
