@@ -111,14 +111,19 @@ def main():
     state = trainer.new_step_state()
     model.train()
 
+    use_graph = not args.eager  # N>1: two graphs per step, gradient collectives between them
+    graphed = trainer.graphed_step(args.batch, warmup=3) if use_graph else None
+    if graphed is not None:
+        # the sampler writes each batch into the graph's static inputs and the graph accumulates
+        # into its own state: no per-step copies around the replay
+        state = graphed.state
+
     def batches():
         while True:
-            for t in sampler.epoch():
+            for t in sampler.epoch(out=graphed.inputs if graphed is not None else None):
                 yield t
 
     it = batches()
-    use_graph = not args.eager  # N>1: two graphs per step, gradient collectives between them
-    graphed = trainer.graphed_step(args.batch, warmup=3) if use_graph else None
 
     def do_step(i):
         u, p, n = next(it)

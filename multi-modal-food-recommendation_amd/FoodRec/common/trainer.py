@@ -81,9 +81,19 @@ class GraphedStep:
         self.graph = None
         self.calls = 0
         self.static_loss = None
-        # private static state: the graph writes this step's loss vector and the cumulative NaN
-        # flag here; they are folded into the caller's epoch state after each replay
+        # the graph's own state: each replay adds the step's loss vector to gstate["acc"] and ORs
+        # the NaN flag into gstate["nan"].  Callers that pass this dict (``.state``) as their epoch
+        # state pay no per-step copies; any other state dict is folded in around each replay.
         self.gstate = {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=dev)}
+
+    @property
+    def state(self):
+        return self.gstate
+
+    @property
+    def inputs(self):
+        """The static (u, pos, neg) buffers: a sampler writing into them saves the per-step copies."""
+        return self.u, self.p, self.n
 
     def _body(self, batch_idx, state, accumulate=True):
         feats = self.tr._features()
@@ -92,9 +102,9 @@ class GraphedStep:
     def __call__(self, u, p, n, batch_idx, state):
         if u.numel() != self.B:
             return self.tr.train_step(self.tr._features().batch(u, p, n), batch_idx, state)
-        self.u.copy_(u, non_blocking=True)
-        self.p.copy_(p, non_blocking=True)
-        self.n.copy_(n, non_blocking=True)
+        for src, dst in ((u, self.u), (p, self.p), (n, self.n)):
+            if src is not dst:
+                dst.copy_(src, non_blocking=True)
         self.calls += 1
         if self.graph is None and self.calls <= self.warmup:
             side = torch.cuda.Stream()
@@ -104,14 +114,22 @@ class GraphedStep:
             torch.cuda.current_stream().wait_stream(side)
             self.n_parts = state["acc"].numel()
             return out
+        own = state is self.gstate
         if self.graph is None:
+            acc0 = self.gstate["acc"] if own else None  # the warm-up steps' sums when state is ours
             self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
             self.tr.optimizer.zero_grad()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.static_loss = self._body(batch_idx, self.gstate, accumulate=False)
+                self.static_loss = self._body(batch_idx, self.gstate, accumulate=True)
             self.graph = g
+            if acc0 is not None:
+                self.gstate["acc"].copy_(acc0)
+        if own:
+            self.graph.replay()
+            return self.static_loss
         self.gstate["nan"].copy_(state["nan"])
+        self.gstate["acc"].zero_()
         self.graph.replay()
         state["nan"].copy_(self.gstate["nan"])
         if state["acc"] is None:
@@ -164,9 +182,9 @@ class GraphedDPStep(GraphedStep):
         tr = self.tr
         if u.numel() != self.B:
             return tr.train_step(tr._features().batch(u, p, n), batch_idx, state)
-        self.u.copy_(u, non_blocking=True)
-        self.p.copy_(p, non_blocking=True)
-        self.n.copy_(n, non_blocking=True)
+        for src, dst in ((u, self.u), (p, self.p), (n, self.n)):
+            if src is not dst:
+                dst.copy_(src, non_blocking=True)
         self.calls += 1
         hook = tr.grad_hook
         if self.graph is None and self.calls <= self.warmup:
@@ -182,17 +200,27 @@ class GraphedDPStep(GraphedStep):
             torch.cuda.current_stream().wait_stream(side)
             self.n_parts = state["acc"].numel()
             return out
+        own = state is self.gstate
         if self.graph is None:
+            acc0 = self.gstate["acc"] if own else None
             self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
             tr.optimizer.zero_grad()
             ga = torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
-                self.static_loss = self._part_a(batch_idx, self.gstate, False)
+                self.static_loss = self._part_a(batch_idx, self.gstate, True)
             gb = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gb, pool=ga.pool()):
                 self._part_b(self.gstate)
             self.graph, self.graph_b = ga, gb
+            if acc0 is not None:
+                self.gstate["acc"].copy_(acc0)
+        if own:
+            self.graph.replay()
+            hook.communicate()
+            self.graph_b.replay()
+            return self.static_loss
         self.gstate["nan"].copy_(state["nan"])
+        self.gstate["acc"].zero_()
         self.graph.replay()
         hook.communicate()
         self.graph_b.replay()
@@ -372,7 +400,11 @@ class Trainer(AbstractTrainer):
             if self._graphed is None:
                 self._graphed = self.graphed_step(train_data.batch_size, int(self.config["cuda_graph_warmup"] or 3))
             step = self._graphed
-            for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
+            state = step.state  # the graph accumulates into its own state: reset it for this epoch
+            if state["acc"] is not None:
+                state["acc"].zero_()
+            state["nan"].zero_()
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs)):
                 loss_batches.append(step(u, p, n, batch_idx, state))
         else:
             for batch_idx, (u, p, n) in enumerate(train_data.epoch()):

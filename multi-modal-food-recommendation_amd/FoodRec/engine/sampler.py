@@ -92,9 +92,11 @@ class TripleSampler:
         g.manual_seed(seed)
         return torch.randperm(self.n, generator=g)
 
-    def epoch(self):
+    def epoch(self, out=None):
         """Yield (u, pos, neg) int64 device tensors per batch for one epoch.  Negatives are drawn
-        per batch (same stream as the reference's per-sample draws, in permutation order)."""
+        per batch (same stream as the reference's per-sample draws, in permutation order).  With
+        ``out`` = three [batch_size] device buffers (a graphed step's static inputs), full batches
+        are written into them and the buffers are yielded."""
         perm = self.epoch_order().numpy()
         perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
         pin = self.device.type == "cuda"
@@ -103,7 +105,13 @@ class TripleSampler:
             if pin:
                 negs = negs.pin_memory()
             idx = perm_d[s:s + self.batch_size]
-            yield self._dev_users[idx], self._dev_items[idx], negs.to(self.device, non_blocking=True)
+            if out is not None and idx.numel() == out[0].numel():
+                torch.index_select(self._dev_users, 0, idx, out=out[0])
+                torch.index_select(self._dev_items, 0, idx, out=out[1])
+                out[2].copy_(negs, non_blocking=True)
+                yield out
+            else:
+                yield self._dev_users[idx], self._dev_items[idx], negs.to(self.device, non_blocking=True)
 
 
 SSL_MASKED_P = 0.2   # TrainDataLoader.masked_p (dataloader.py:19)
