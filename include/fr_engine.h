@@ -124,6 +124,15 @@ int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
                int64_t B, int d, float gamma, float g_mf, float g_reg, const float* d_gscale,
                float* d_dU, float* d_dI, float* d_dUe, float* d_dIe,
                int deterministic, void* d_workspace, int64_t workspace_bytes, void* stream);
+/* fr_bpr_bwd (non-deterministic scatter) plus d_extra_i [2B, d] (row stride ld_extra): the gradient of
+ * the gathered item rows [I[pos]; I[neg]] from another consumer (HealthRec's KD term reads exactly
+ * those rows, cikm_model.py:256-263), added to the pos / neg rows inside the same scatter. */
+int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                  const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                  const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+                  int64_t B, int d, float gamma, float g_mf, float g_reg, const float* d_gscale,
+                  float* d_dU, float* d_dI, float* d_dUe, float* d_dIe, const float* d_extra_i, int64_t ld_extra,
+                  void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused multi-view distance correlation (CLUSSL SSL loss).

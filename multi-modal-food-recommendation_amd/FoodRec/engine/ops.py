@@ -195,7 +195,7 @@ def propagate_mean(adj: Adjacency, ego: torch.Tensor, n_layers: int) -> torch.Te
 # ----------------------------------------------------------------------------- BPR + EmbLoss
 class _BprEmb(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic):
+    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic, item_rows=False):
         # one table for users and items (item ids offset past the users): one gradient buffer
         alias_ui, alias_e = I is U, Ie is not None and Ie is Ue
         U = _rowmajor(U)
@@ -219,10 +219,15 @@ class _BprEmb(torch.autograd.Function):
         ctx.ws, ctx.gamma, ctx.det = ws, gamma, int(deterministic)
         ctx.same_u, ctx.same_i = Ue is U, Ie is I
         ctx.alias_ui, ctx.alias_e = alias_ui, alias_e
-        return out[0], out[4:5]
+        ctx.item_rows = bool(item_rows) and not deterministic and I.dtype == torch.float32
+        if not item_rows:
+            return out[0], out[4:5]
+        # [I[pos]; I[neg]] for another consumer; its gradient joins the backward's own scatter
+        rows = torch.index_select(I, 0, torch.cat([p, n]))
+        return out[0], out[4:5], rows
 
     @staticmethod
-    def backward(ctx, g_mf, g_emb):
+    def backward(ctx, g_mf, g_emb, g_rows=None):
         U, I, Ue, Ie, u, p, n = ctx.saved_tensors
         dev = U.device
         g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
@@ -245,6 +250,15 @@ class _BprEmb(torch.autograd.Function):
                 u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
                 gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
                 ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd_bf16")
+        elif g_rows is not None and dI is not None and ctx.item_rows:
+            g_rows = g_rows.contiguous()
+            native.check(native.lib().fr_bpr_bwd_ex(
+                U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
+                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                g_rows.data_ptr(), g_rows.stride(0), ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)),
+                "fr_bpr_bwd_ex")
+            g_rows = None
         else:
             native.check(native.lib().fr_bpr_bwd(
                 U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
@@ -255,14 +269,19 @@ class _BprEmb(torch.autograd.Function):
             dUe = None
         if ctx.same_i or ctx.alias_e:
             dIe = None
+        if g_rows is not None and dI is not None:  # not folded into the kernel (bf16 / deterministic)
+            dI.index_add_(0, torch.cat([p, n]), g_rows.to(dI.dtype))
         if ctx.alias_ui:
             dI = None
-        return dU, dI, dUe, dIe, None, None, None, None, None
+        return dU, dI, dUe, dIe, None, None, None, None, None, None
 
 
-def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False):
-    """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused."""
-    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic)
+def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False,
+                 item_rows: bool = False):
+    """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused; with
+    ``item_rows`` also the gathered [I[pos]; I[neg]] rows, whose gradient is added inside the fused
+    backward's scatter (no separate gather backward)."""
+    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic, item_rows)
 
 
 # ----------------------------------------------------------------------------- embedding

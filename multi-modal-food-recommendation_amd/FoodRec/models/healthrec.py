@@ -173,10 +173,11 @@ class HealthRec(GeneralRecommender):
             item_mm, _ = self.ingre_target_atten(encoded, mm_query)
             item_know = F.normalize(item_mm).sum(1) / ingre_num.unsqueeze(1)
             health_in = F.normalize(item_health).mean(dim=1)
-        mf_loss, emb3 = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
-                                         user, pos_item, neg_item)
-        # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263) as one gather
-        item_rows = ops.embedding(all_item, item_all)
+        # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263): the BPR kernel's own
+        # item rows; their KD gradient is added inside the BPR backward's scatter
+        mf_loss, emb3, item_rows = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight,
+                                                    self.item_embedding.weight, user, pos_item, neg_item,
+                                                    item_rows=True)
         if self._fused_head(health_in, health_level):
             # health MLP + BCE sum and the KD cosine term, weighted, in one HIP kernel per direction
             health_term, kd_term = ops.health_kd_loss(health_in, item_know, item_rows, health_level, self.health_mlp,

@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
     const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
     const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
     int64_t B, int d4, float gamma, float gmf, float greg, const float* gscale, float* dU, int64_t lddu,
-    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws) {
+    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws,
+    const float* __restrict__ extra, int64_t ldx) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
   if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
@@ -164,8 +165,13 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
         atomic_row_add(dU, u, lddu, q, t);
       }
       if (dI) {
-        atomic_row_add(dI, p, lddi, q, f4_scale(g, xu));
-        atomic_row_add(dI, n, lddi, q, f4_scale(-g, xu));
+        float4 tp = f4_scale(g, xu), tn = f4_scale(-g, xu);
+        if (extra) {  // gradient of the returned item rows [I[pos]; I[neg]] (another consumer of them)
+          tp = f4_add(tp, ld4(extra, b, ldx, q));
+          tn = f4_add(tn, ld4(extra, B + b, ldx, q));
+        }
+        atomic_row_add(dI, p, lddi, q, tp);
+        atomic_row_add(dI, n, lddi, q, tn);
       }
       if (Ue && dUe) atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
       if (Ie && dIe) {
@@ -424,12 +430,12 @@ extern "C" int fr_bpr_fwd(const float* d_U, int64_t ldu, const float* d_I, int64
   return FR_OK;
 }
 
-extern "C" int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
-                          const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
-                          const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
-                          float gamma, float g_mf, float g_reg, const float* d_gscale, float* d_dU,
-                          float* d_dI, float* d_dUe, float* d_dIe, int deterministic,
-                          void* d_workspace, int64_t workspace_bytes, void* stream) {
+static int bpr_bwd_impl(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi, const float* d_Ue,
+                        int64_t ldue, const float* d_Ie, int64_t ldie, const int64_t* d_u, const int64_t* d_p,
+                        const int64_t* d_n, int64_t B, int d, float gamma, float g_mf, float g_reg,
+                        const float* d_gscale, float* d_dU, float* d_dI, float* d_dUe, float* d_dIe,
+                        int deterministic, const float* d_extra, int64_t ldx, void* d_workspace,
+                        int64_t workspace_bytes, void* stream) {
   int rc = bpr_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
                      workspace_bytes);
   if (rc) return rc;
@@ -446,10 +452,32 @@ extern "C" int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64
     const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
     hipLaunchKernelGGL(bpr_bwd_atomic_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
                        ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
-                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
+                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w, d_extra, ldx);
   }
   FR_LAUNCH_CHECK();
   return FR_OK;
+}
+
+extern "C" int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                          const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                          const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                          float gamma, float g_mf, float g_reg, const float* d_gscale, float* d_dU,
+                          float* d_dI, float* d_dUe, float* d_dIe, int deterministic,
+                          void* d_workspace, int64_t workspace_bytes, void* stream) {
+  return bpr_bwd_impl(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, gamma, g_mf, g_reg, d_gscale,
+                      d_dU, d_dI, d_dUe, d_dIe, deterministic, nullptr, 0, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                             const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                             const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                             float gamma, float g_mf, float g_reg, const float* d_gscale, float* d_dU,
+                             float* d_dI, float* d_dUe, float* d_dIe, const float* d_extra_i, int64_t ld_extra,
+                             void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(d_extra_i && d_dI && fr::aligned16(d_extra_i) && ld_extra >= d && ld_extra % 4 == 0,
+             "extra item-row gradient [2B, d] (16-B aligned) and dI required");
+  return bpr_bwd_impl(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, gamma, g_mf, g_reg, d_gscale,
+                      d_dU, d_dI, d_dUe, d_dIe, 0, d_extra_i, ld_extra, d_workspace, workspace_bytes, stream);
 }
 
 // ---- bf16 entry points -----------------------------------------------------------------------

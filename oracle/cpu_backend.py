@@ -58,12 +58,11 @@ def propagate_mean(adj, ego, n_layers):
     return O.propagate_mean(_coo(adj), ego, n_layers)
 
 
-def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False):
+def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False, item_rows=False):
     u, p, n = U[user], I[pos], I[neg]
     mf = O.bpr_loss((u * p).sum(1), (u * n).sum(1), gamma)
-    if Ue is None:
-        return mf, torch.zeros(1)
-    return mf, O.emb_loss(Ue[user], Ie[pos], Ie[neg])
+    emb = torch.zeros(1) if Ue is None else O.emb_loss(Ue[user], Ie[pos], Ie[neg])
+    return (mf, emb, torch.cat([p, n])) if item_rows else (mf, emb)
 
 
 def dcor_loss(views, pairs):
