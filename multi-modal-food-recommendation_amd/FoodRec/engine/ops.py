@@ -195,7 +195,12 @@ def propagate_mean(adj: Adjacency, ego: torch.Tensor, n_layers: int) -> torch.Te
 # ----------------------------------------------------------------------------- BPR + EmbLoss
 class _BprEmb(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic, item_rows=False):
+    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic, item_rows=False, item_offset=None):
+        # item_offset: items are rows [item_offset:] of U (one propagated table, one gradient buffer,
+        # item ids unchanged); the kernels just see the offset base pointers
+        ctx.ioff = None if item_offset is None else int(item_offset)
+        if ctx.ioff is not None:
+            I = U[ctx.ioff:]
         # one table for users and items (item ids offset past the users): one gradient buffer
         alias_ui, alias_e = I is U, Ie is not None and Ie is Ue
         U = _rowmajor(U)
@@ -234,8 +239,12 @@ class _BprEmb(torch.autograd.Function):
         g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
         gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
         need = ctx.needs_input_grad
-        dU = _grad_like(U) if (need[0] or (ctx.alias_ui and need[1])) else None
-        dI = dU if ctx.alias_ui else (_grad_like(I) if need[1] else None)
+        if ctx.ioff is not None:
+            dU = _grad_like(U) if need[0] else None
+            dI = dU[ctx.ioff:] if dU is not None else None
+        else:
+            dU = _grad_like(U) if (need[0] or (ctx.alias_ui and need[1])) else None
+            dI = dU if ctx.alias_ui else (_grad_like(I) if need[1] else None)
         dUe = dIe = None
         if Ue is not None:
             dUe = dU if (ctx.same_u and dU is not None) else (
@@ -271,17 +280,18 @@ class _BprEmb(torch.autograd.Function):
             dIe = None
         if g_rows is not None and dI is not None:  # not folded into the kernel (bf16 / deterministic)
             dI.index_add_(0, torch.cat([p, n]), g_rows.to(dI.dtype))
-        if ctx.alias_ui:
+        if ctx.alias_ui or ctx.ioff is not None:
             dI = None
-        return dU, dI, dUe, dIe, None, None, None, None, None, None
+        return dU, dI, dUe, dIe, None, None, None, None, None, None, None
 
 
 def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False,
-                 item_rows: bool = False):
+                 item_rows: bool = False, item_offset: int | None = None):
     """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused; with
     ``item_rows`` also the gathered [I[pos]; I[neg]] rows, whose gradient is added inside the fused
-    backward's scatter (no separate gather backward)."""
-    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic, item_rows)
+    backward's scatter (no separate gather backward).  ``item_offset`` (with I None): the item table
+    is U[item_offset:] -- one [users + items] gradient buffer instead of two plus a concatenation."""
+    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic, item_rows, item_offset)
 
 
 # ----------------------------------------------------------------------------- embedding

@@ -126,18 +126,23 @@ class HealthRec(GeneralRecommender):
             self.text_trs = nn.Linear(self.t_feat.shape[1], d)
             nn.init.xavier_normal_(self.text_trs.weight)
 
-    def forward(self):
+    def _propagate(self):
+        """[users | items] after both propagations (cikm_model.py:185-205), and the discarded
+        propagated ingredients."""
         ir_ego = torch.cat((self.item_embedding.weight, self.ingre_embedding.weight[:-1, :]), dim=0)
         ir_all = ops.propagate_mean(self.ri_norm_adj, ir_ego, self.n_layers)
         item_ir, ingre_ir = torch.split(ir_all, [self.n_items, self.n_ingredients])
         ui_ego = torch.cat([self.user_embedding.weight, item_ir], dim=0)
-        ui_all = ops.propagate_mean(self.norm_adj_matrix, ui_ego, self.ui_layers)
+        return ops.propagate_mean(self.norm_adj_matrix, ui_ego, self.ui_layers), ingre_ir
+
+    def forward(self):
+        ui_all, ingre_ir = self._propagate()
         user_all, item_all = torch.split(ui_all, [self.n_users, self.n_items])
         return user_all, item_all, ingre_ir
 
     def calculate_loss(self, batch_data):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
-        user_all, item_all, _ = self.forward()
+        ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
         health_level = _pn(batch_data, "hl_mh")
         ingredients = _pn(batch_data, "ingre_code")
@@ -175,9 +180,9 @@ class HealthRec(GeneralRecommender):
             health_in = F.normalize(item_health).mean(dim=1)
         # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263): the BPR kernel's own
         # item rows; their KD gradient is added inside the BPR backward's scatter
-        mf_loss, emb3, item_rows = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight,
+        mf_loss, emb3, item_rows = ops.bpr_emb_loss(ui_all, None, self.user_embedding.weight,
                                                     self.item_embedding.weight, user, pos_item, neg_item,
-                                                    item_rows=True)
+                                                    item_rows=True, item_offset=self.n_users)
         if self._fused_head(health_in, health_level):
             # health MLP + BCE sum and the KD cosine term, weighted, in one HIP kernel per direction
             health_term, kd_term = ops.health_kd_loss(health_in, item_know, item_rows, health_level, self.health_mlp,

@@ -58,7 +58,10 @@ def propagate_mean(adj, ego, n_layers):
     return O.propagate_mean(_coo(adj), ego, n_layers)
 
 
-def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False, item_rows=False):
+def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False, item_rows=False,
+                 item_offset=None):
+    if item_offset is not None:
+        I = U[item_offset:]
     u, p, n = U[user], I[pos], I[neg]
     mf = O.bpr_loss((u * p).sum(1), (u * n).sum(1), gamma)
     emb = torch.zeros(1) if Ue is None else O.emb_loss(Ue[user], Ie[pos], Ie[neg])
