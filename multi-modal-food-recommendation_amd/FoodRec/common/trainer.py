@@ -140,16 +140,21 @@ class GraphedStep:
 
 
 class GraphedDPStep(GraphedStep):
-    """Data-parallel step (Trainer.grad_hook = engine.dist.GradAllReduce) as two HIP graphs with the
+    """Data-parallel step (Trainer.grad_hook = engine.dist.GradAllReduce) as HIP graphs with the
     collectives between them, so no RCCL call is ever captured:
 
       graph A  zero_grad, forward, loss, backward (row-gathered tables stash their (ids, rows)),
                pack the dense gradients into the flat buffer
-      eager    RowExchange all-gathers + one all-reduce of the flat buffer (hook.communicate)
-      graph B  average + unpack, scatter the tables' mean row gradients, fused Adam
+      eager    RowExchange all-gathers (64-wide rows), then the all-reduce of the flat buffer issued
+               asynchronously
+      graph B1 (row-exchanged tables + FusedAdam) the tables' mean rows and their Adam update, which
+               runs while the all-reduce is in flight
+      graph B2 after the all-reduce: average + unpack the dense gradients, dense Adam
+      (otherwise: both collectives, then one graph B: average + unpack, the tables' mean rows,
+      fused Adam)
 
-    The first ``warmup`` calls run the same three phases eagerly (side stream for the graphed
-    parts), which also creates the hook's static buffers before capture."""
+    The first ``warmup`` calls run the same phases eagerly (side stream for the graphed parts),
+    which also creates the hook's static buffers before capture."""
 
     def __init__(self, trainer, batch_size, warmup=3):
         super().__init__(trainer, batch_size, warmup)
@@ -178,6 +183,32 @@ class GraphedDPStep(GraphedStep):
         self.tr.grad_hook.unpack()
         self.tr._opt_step(state["nan"])
 
+    def _split_b(self) -> bool:
+        """Row-exchanged tables + FusedAdam: their update (graph B1) runs while the dense
+        all-reduce is in flight, the dense update (graph B2) after it."""
+        hook = self.tr.grad_hook
+        return getattr(hook, "rows", None) is not None and isinstance(self.tr.optimizer, FusedAdam)
+
+    def _part_b1(self, state):
+        self.tr.grad_hook.unpack_rows()
+        self.tr.optimizer.step(skip_flag=state["nan"], part="rows")
+
+    def _part_b2(self, state):
+        self.tr.grad_hook.unpack_dense()
+        self.tr.optimizer.step(skip_flag=state["nan"], part="dense")
+
+    def _comm_and_b(self, run_b1, run_b2, run_b):
+        hook = self.tr.grad_hook
+        if self._split_b():
+            hook.communicate_rows()
+            work = hook.communicate_dense(async_op=True)
+            run_b1()
+            work.wait()
+            run_b2()
+        else:
+            hook.communicate()
+            run_b()
+
     def __call__(self, u, p, n, batch_idx, state):
         tr = self.tr
         if u.numel() != self.B:
@@ -186,18 +217,21 @@ class GraphedDPStep(GraphedStep):
             if src is not dst:
                 dst.copy_(src, non_blocking=True)
         self.calls += 1
-        hook = tr.grad_hook
         if self.graph is None and self.calls <= self.warmup:
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 out = self._part_a(batch_idx, state, True)
             torch.cuda.current_stream().wait_stream(side)
-            hook.communicate()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                self._part_b(state)
-            torch.cuda.current_stream().wait_stream(side)
+
+            def on_side(fn):
+                def run():
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        fn(state)
+                    torch.cuda.current_stream().wait_stream(side)
+                return run
+            self._comm_and_b(on_side(self._part_b1), on_side(self._part_b2), on_side(self._part_b))
             self.n_parts = state["acc"].numel()
             return out
         own = state is self.gstate
@@ -208,22 +242,32 @@ class GraphedDPStep(GraphedStep):
             ga = torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self.static_loss = self._part_a(batch_idx, self.gstate, True)
-            gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, pool=ga.pool()):
-                self._part_b(self.gstate)
-            self.graph, self.graph_b = ga, gb
+            if self._split_b():
+                gb1, gb2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb1, pool=ga.pool()):
+                    self._part_b1(self.gstate)
+                with torch.cuda.graph(gb2, pool=ga.pool()):
+                    self._part_b2(self.gstate)
+                self.graph_b = (gb1, gb2)
+            else:
+                gb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb, pool=ga.pool()):
+                    self._part_b(self.gstate)
+                self.graph_b = (gb,)
+            self.graph = ga
             if acc0 is not None:
                 self.gstate["acc"].copy_(acc0)
+        gb = self.graph_b
+        replay_b = (lambda: gb[0].replay(), lambda: gb[1].replay(), None) if len(gb) == 2 else \
+            (None, None, lambda: gb[0].replay())
         if own:
             self.graph.replay()
-            hook.communicate()
-            self.graph_b.replay()
+            self._comm_and_b(*replay_b)
             return self.static_loss
         self.gstate["nan"].copy_(state["nan"])
         self.gstate["acc"].zero_()
         self.graph.replay()
-        hook.communicate()
-        self.graph_b.replay()
+        self._comm_and_b(*replay_b)
         state["nan"].copy_(self.gstate["nan"])
         if state["acc"] is None:
             state["acc"] = self.gstate["acc"].clone()

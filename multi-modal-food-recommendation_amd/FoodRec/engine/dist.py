@@ -130,14 +130,28 @@ class GradAllReduce:
             off += n
 
     def communicate(self):
+        self.communicate_rows()
+        self.communicate_dense()
+
+    def communicate_rows(self):
         if self.rows is not None:
             self.rows.exchange()
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+
+    def communicate_dense(self, async_op: bool = False):
+        """The flat all-reduce; with ``async_op`` the returned work's ``wait()`` orders the current
+        stream after it, so work enqueued in between (the row-table Adam update) overlaps it."""
+        return dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
     def unpack(self):
+        self.unpack_dense()
+        self.unpack_rows()
+
+    def unpack_dense(self):
         self.flat.mul_(1.0 / self.world)
         for p, v in self.views:
             p.grad.copy_(v.view_as(p.grad))
+
+    def unpack_rows(self):
         if self.rows is not None:
             self.rows.apply()
 

@@ -132,17 +132,21 @@ class FusedAdam(torch.optim.Optimizer):
                 self._d_lr[gi] = (t, float(group["lr"]))
 
     @torch.no_grad()
-    def step(self, closure=None, skip_flag: torch.Tensor | None = None):
+    def step(self, closure=None, skip_flag: torch.Tensor | None = None, part: str = "all"):
         """One Adam update.  ``skip_flag`` (device int32 scalar): when non-zero on the device the
         kernels leave every tensor (and step counter) untouched — the trainer's NaN guard
-        without a host synchronisation."""
+        without a host synchronisation.  ``part``: "rows" updates only the tables with pending row
+        gradients, "dense" only the others (a data-parallel step runs the row update while the
+        dense gradients are still being all-reduced)."""
+        if part not in ("all", "rows", "dense"):
+            raise ValueError(f"part must be all, rows or dense (got {part!r})")
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
         lib = native.lib()
         # factored row gradients read the projection weights: materialise them before any update
-        prepared = self._prepare_factored(lib) if self.row_grads.factored else {}
+        prepared = self._prepare_factored(lib) if (self.row_grads.factored and part != "dense") else {}
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
             plist, rows = [], []
@@ -155,7 +159,11 @@ class FusedAdam(torch.optim.Optimizer):
                         st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                         st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     continue
-                rg = self.row_grads.take(p) if self.row_grads.pending else None
+                if part == "dense" and (id(p) in self.row_grads.pending or id(p) in self.row_grads.factored):
+                    continue
+                rg = self.row_grads.take(p) if (self.row_grads.pending and part != "dense") else None
+                if part == "rows" and rg is None:
+                    continue
                 if rg is not None and (p.grad is not None or not _row_grad_ok(p, rg[0], rg[1])):
                     from . import ops  # dense fallback: scatter the rows into (or onto) .grad
                     dense = ops.scatter_rows(rg[0].reshape(-1), rg[1].reshape(-1, p.shape[-1]), p.shape[0], rg[2])
