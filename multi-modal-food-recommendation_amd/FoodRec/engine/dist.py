@@ -33,20 +33,27 @@ def init_from_env(backend=None):
 class RowExchange:
     """Data-parallel gradient of row-gathered tables, exchanged as rows.
 
-    In backward, ``ops.embedding(..., exchange=self)`` stashes its ids and gradient rows into
-    static buffers (and gives the table no dense gradient); ``exchange()`` all-gathers every rank's
-    stash (two collectives per table, P x n x (8 + 4d) bytes); ``apply()`` sets each table's
-    gradient to the deterministic scatter (fr_embedding_bwd) of the gathered rows / P -- identical
-    on every rank and equal to the mean of the ranks' dense gradients."""
+    In backward, ``ops.embedding(..., exchange=self)`` (or ``ops.modal_projection``, whose rows are
+    the 64-wide dY of the factored gradient) stashes its ids and gradient rows into static buffers
+    (and gives the table no dense gradient); ``exchange()`` all-gathers every rank's stash -- all
+    tables packed into one buffer, ONE collective, P x sum(n x (8 + 4d)) bytes; ``apply()`` sets
+    each table's gradient to the deterministic scatter of the gathered rows / P (or hands them to
+    FusedAdam's row gradients) -- identical on every rank and equal to the mean of the ranks' dense
+    gradients."""
 
     def __init__(self, group, world):
         self.group, self.world = group, int(world)
         self.slots = {}  # id(weight) -> dict(weight, pad, ids, G, ids_all, G_all)
+        # every slot's ids and rows packed into ONE send buffer (one all-gather per step); built at
+        # the first exchange, after which the stashes write straight into their views of it
+        self._send = self._recv = None
         # optional FusedAdam.row_grads: apply() hands it the gathered mean rows (fr_adam_step_rows)
         # instead of scattering a dense table gradient
         self.sink = None
 
     def stash(self, weight, padding_idx, ids, G, W=None):
+        ids = ids.to(torch.int64)
+        G = G.to(torch.float32)
         s = self.slots.get(id(weight))
         if s is None or s["ids"].shape != ids.shape or s["G"].shape != G.shape or s["W"] is not W:
             s = {"weight": weight, "pad": padding_idx, "ids": torch.empty_like(ids),
@@ -54,6 +61,7 @@ class RowExchange:
                  "ids_all": torch.empty((self.world,) + tuple(ids.shape), dtype=ids.dtype, device=ids.device),
                  "G_all": torch.empty((self.world,) + tuple(G.shape), dtype=G.dtype, device=G.device)}
             self.slots[id(weight)] = s
+            self._send = self._recv = None  # layout changed: repack at the next exchange
         s["ids"].copy_(ids)
         s["G"].copy_(G)
 
@@ -62,11 +70,34 @@ class RowExchange:
         dY rows and the ids cross the interconnect; W is replicated on every rank."""
         self.stash(weight, padding_idx, ids, dY, W)
 
+    def _pack(self):
+        """One float32 send buffer [ids(int64 as 2 words) | rows] per slot, and the matching
+        [world, total] receive buffer; slot tensors become views of them."""
+        layout, total = [], 0
+        for s in self.slots.values():
+            ni, ng = 2 * s["ids"].numel(), s["G"].numel()
+            ng += ng % 2  # keep every region 8-byte aligned
+            layout.append((s, total, ni, ng))
+            total += ni + ng
+        dev = next(iter(self.slots.values()))["G"].device
+        send = torch.empty(total, dtype=torch.float32, device=dev)
+        recv = torch.empty(self.world, total, dtype=torch.float32, device=dev)
+        for s, off, ni, ng in layout:
+            ids_v = send[off:off + ni].view(torch.int64).view(s["ids"].shape)
+            ids_v.copy_(s["ids"])
+            g_v = send[off + ni:off + ni + s["G"].numel()].view(s["G"].shape)
+            g_v.copy_(s["G"])
+            s["ids"], s["G"] = ids_v, g_v
+            s["ids_all"] = recv[:, off:off + ni].view(torch.int64)  # [world, n]
+            s["G_all"] = recv[:, off + ni:off + ni + s["G"].numel()]  # [world, n * d]
+        self._send, self._recv = send, recv
+
     def exchange(self):
         import torch.distributed as dist
-        for s in self.slots.values():  # into views of the static buffers (graph B reads them)
-            dist.all_gather(list(s["ids_all"].unbind(0)), s["ids"], group=self.group)
-            dist.all_gather(list(s["G_all"].unbind(0)), s["G"], group=self.group)
+        if self._send is None:
+            self._pack()
+        # one collective for every table (views of these static buffers are what graph B reads)
+        dist.all_gather(list(self._recv.unbind(0)), self._send, group=self.group)
 
     def apply(self):
         from . import ops
@@ -74,7 +105,7 @@ class RowExchange:
             w = s["weight"]
             d = s["G"].shape[-1]
             rows = s["G_all"].reshape(-1, d) * (1.0 / self.world)
-            ids = s["ids_all"].reshape(-1)
+            ids = s["ids_all"].reshape(-1).contiguous()
             if s["W"] is not None:  # factored: rows are dY, the table gradient rows are dY W
                 if self.sink is not None:
                     self.sink.stash_factored(w, s["pad"], ids, rows, s["W"])
