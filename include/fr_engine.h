@@ -447,6 +447,19 @@ int fr_linear_wgrad_gather(const float* d_dy, int64_t ldy, const int64_t* d_ids,
                            int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Ingredient gather + EmbLoss norms of its two halves (models/cikm_model.py:230, 270-279).
+ * fr_gather_norms_fwd: E[i] = W[ids[i]] (64-wide fp32 rows) and nrm[0] = ||E[:half]||_F,
+ *   nrm[1] = ||E[half:]||_F (block partials from fr_gather_norms_partials, fixed-order sums).
+ * fr_norms_bwd_coef: out[i] = G[i] + [ids[i] != pad] * (gn[h] / nrm[h]) * E[i], h = (i >= half),
+ *   gn[1] read at d_gn + gn_stride (0 for a broadcast gradient); zero where a norm is zero.
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_gather_norms_partials(int64_t n);
+int fr_gather_norms_fwd(const int64_t* d_ids, int64_t n, int64_t half, const float* d_w, int64_t ldw, float* d_e,
+                        float* d_partials, int64_t partial_floats, float* d_nrm, void* stream);
+int fr_norms_bwd_coef(const int64_t* d_ids, int64_t n, int64_t half, int64_t pad, const float* d_g, const float* d_e,
+                      const float* d_gn, int64_t gn_stride, const float* d_nrm, float* d_out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Host-side readers of the reference's on-disk interaction formats (no GPU).
  *   FR_IO_NEGATIVE  data.{valid,test}.negative: "(u,i)\tn1\tn2..." per line; the first field is
  *                   dropped, the rest are int() ids -> ragged rows (values, offsets[rows+1]).

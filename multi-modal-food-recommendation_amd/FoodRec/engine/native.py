@@ -144,6 +144,11 @@ _SIGS = {
     "fr_rows_matmul": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "fr_linear_wgrad_gather": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int,
                                        c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_gather_norms_partials": (c_int64, [c_int64]),
+    "fr_gather_norms_fwd": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                                    c_void_p, c_void_p]),
+    "fr_norms_bwd_coef": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_void_p, c_void_p, c_void_p]),
     "fr_io_open": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
     "fr_io_fill": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
     "fr_io_close": (None, [c_void_p]),

@@ -371,6 +371,24 @@ class _EmbeddingNorms(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, weight, pad, half):
         native.require_device(weight, idx)
+        n = idx.numel()
+        hp = half * idx.shape[-1]  # positions in the first half
+        ctx.fused = (weight.dtype == torch.float32 and weight.shape[1] == 64 and weight.stride(1) == 1
+                     and weight.stride(0) % 4 == 0 and weight.data_ptr() % 16 == 0 and 0 <= hp <= n and n > 0)
+        if ctx.fused:  # fr_gather_norms_fwd: gather + both halves' norms, 2 launches
+            lib = native.lib()
+            idx_c = idx.reshape(-1).contiguous()
+            E = torch.empty(idx.shape + (64,), dtype=torch.float32, device=weight.device)
+            nrm = torch.empty(2, dtype=torch.float32, device=weight.device)
+            nparts = lib.fr_gather_norms_partials(n)
+            part = torch.empty(nparts, dtype=torch.float32, device=weight.device)
+            with profiling.region("gather_norms", 8 * n + 2 * 4 * n * 64):
+                native.check(lib.fr_gather_norms_fwd(idx_c.data_ptr(), n, hp, weight.data_ptr(), weight.stride(0),
+                                                     E.data_ptr(), part.data_ptr(), nparts, nrm.data_ptr(),
+                                                     native.stream_of(weight)), "fr_gather_norms_fwd")
+            ctx.save_for_backward(idx_c, E, nrm)
+            ctx.rows, ctx.pad, ctx.half, ctx.hp = weight.shape[0], pad, half, hp
+            return E, nrm
         E = torch.nn.functional.embedding(idx, weight)
         Ef = E.reshape(2, -1)  # full-tensor norms of each half (a 2-output dim reduction is slow)
         nrm = torch.stack([torch.linalg.vector_norm(Ef[0]), torch.linalg.vector_norm(Ef[1])])
@@ -381,6 +399,17 @@ class _EmbeddingNorms(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gE, gn):
         idx, E, nrm = ctx.saved_tensors
+        if ctx.fused:
+            G = torch.zeros_like(E) if gE is None else gE.contiguous()
+            if gn is not None:
+                out = torch.empty_like(G)
+                with profiling.region("gather_norms", 8 * idx.numel() + 3 * 4 * G.numel()):
+                    native.check(native.lib().fr_norms_bwd_coef(
+                        idx.data_ptr(), idx.numel(), ctx.hp, -1 if ctx.pad is None else int(ctx.pad), G.data_ptr(),
+                        E.data_ptr(), gn.data_ptr(), gn.stride(0), nrm.data_ptr(), out.data_ptr(),
+                        native.stream_of(G)), "fr_norms_bwd_coef")
+                G = out
+            return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None), None, None
         G = torch.zeros_like(E) if gE is None else gE
         if gn is not None:
             coef = (gn / nrm).view(2, 1).expand(2, ctx.half * idx.shape[-1]).reshape(idx.shape)

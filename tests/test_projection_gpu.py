@@ -88,3 +88,31 @@ def test_factored_row_gradients_match_dense(cuda):
         dense[has] = crow[rmap[has]]
         assert set(torch.nonzero(has).flatten().tolist()) == set(ids.tolist())
         _close(dense, g_ref[t][0], 1e-5, f"factored table {t}")
+
+
+@pytest.mark.parametrize("B,L,R", [(512, 20, 5000), (3, 7, 40)])
+def test_embedding_norms_matches_float64(cuda, B, L, R):
+    """ops.embedding_norms (fr_gather_norms_fwd / fr_norms_bwd_coef): E = W[ids] and the two halves'
+    Frobenius norms (cikm_model.py:230, 270-279); gradient G + (gn_h / ||E_h||) E on non-padding
+    positions, scattered per row -- vs float64 autograd of the same expression."""
+    from FoodRec.engine import ops
+    g = torch.Generator().manual_seed(B)
+    pad = R - 1
+    ids = torch.randint(0, R, (2 * B, L), generator=g)
+    ids[:, L - 2:] = pad  # padded tails
+    W = torch.randn(R, 64, generator=g)
+    gE = torch.randn(2 * B, L, 64, generator=g)
+    for gn in (torch.randn(2, generator=g), torch.full((2,), 0.7)):
+        Wd = W.double().requires_grad_(True)
+        Ed = Wd[ids]
+        keep = (ids != pad).unsqueeze(-1).double()
+        Ek = Ed * keep + (Ed * (1 - keep)).detach()  # padding positions: value counted, no gradient
+        nrm_d = torch.stack([Ek[:B].reshape(-1).norm(), Ek[B:].reshape(-1).norm()])
+        ((Ed * gE.double()).sum() + (nrm_d * gn.double()).sum()).backward()
+        Wg = W.to(cuda).requires_grad_(True)
+        E, nrm = ops.embedding_norms(ids.to(cuda), Wg, pad, B)
+        gn_c = gn.to(cuda) if gn[0] != gn[1] else torch.tensor(0.7, device=cuda).expand(2)
+        ((E * gE.to(cuda)).sum() + (nrm * gn_c).sum()).backward()
+        _close(E.detach(), Ed.detach(), 1e-6, "E")
+        _close(nrm.detach(), nrm_d.detach(), 1e-5, "norms")
+        _close(Wg.grad, Wd.grad, 1e-5, "dW")
