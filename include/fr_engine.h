@@ -309,6 +309,35 @@ int fr_adam_step_rows(float* const* params, const float* const* grads, float* co
                       double lr, double beta1, double beta2, double eps, double weight_decay,
                       const int32_t* d_skip, void* stream);
 
+/* Row-gradient Adam with deferred zero-gradient steps (exact "lazy rows").  Same contract as
+ * fr_adam_step_rows (torch.optim.Adam.step, common/trainer.py:224, over cikm_model.py:83-87's
+ * image/text tables), but a row with no gradient this step is not touched: the step's
+ * (-lr/bc1, sqrt(bc2)) go to d_hist[t][(step % hist_cap)] and d_last[t][r] holds the step row r is
+ * current through.  A row with a gradient first replays its skipped steps with g = 0 (the dense
+ * kernel's float operations), then applies this step.  fr_adam_flush_rows brings every row up to
+ * the current step; after a flush p, exp_avg and exp_avg_sq equal fr_adam_step_rows' bit for bit.
+ * The caller flushes before any full-table read and at least every hist_cap - 1 steps.
+ * d_last: int32 [R] per tensor (zero at step 0); d_hist: float32 [hist_cap, 2] per tensor;
+ * n_tensors <= 16. */
+int fr_adam_step_rows_lazy(float* const* params, const float* const* grads, float* const* exp_avg,
+                           float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                           const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                           float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr,
+                           double lr, double beta1, double beta2, double eps, double weight_decay,
+                           const int32_t* d_skip, void* stream);
+int fr_adam_flush_rows(float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
+                       int64_t* const* d_steps, const int64_t* numel, const int32_t* row_dims,
+                       int32_t* const* d_last, float* const* d_hist, int32_t hist_cap, int n_tensors,
+                       double beta1, double beta2, double eps, double weight_decay, void* stream);
+
+/* Catch-up for a lazily updated table before a row gather (the forward of cikm_model.py:240-241's
+ * image_trs/text_trs over embImage/embText rows): rows d_ids[0..n) (duplicates allowed) replay their
+ * deferred zero-gradient steps through the current step, so the gather reads the dense-Adam values. */
+int fr_adam_catch_up_rows(float* param, float* exp_avg, float* exp_avg_sq, const int64_t* d_step,
+                          const int64_t* d_ids, int64_t n, int64_t rows, int32_t row_dim, int32_t* d_last,
+                          const float* d_hist, int32_t hist_cap, double beta1, double beta2, double eps,
+                          double weight_decay, void* stream);
+
 /* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
  * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as
  * fr_adam_step) and the bf16 parameter is re-rounded from the master.  d_step: device int64

@@ -95,6 +95,10 @@ class GraphedStep:
         """The static (u, pos, neg) buffers: a sampler writing into them saves the per-step copies."""
         return self.u, self.p, self.n
 
+    def _note(self):
+        if isinstance(self.tr.optimizer, FusedAdam):
+            self.tr.optimizer.note_replay()
+
     def _body(self, batch_idx, state, accumulate=True):
         feats = self.tr._features()
         return self.tr.train_step(feats.batch(self.u, self.p, self.n), batch_idx, state, accumulate=accumulate)
@@ -127,10 +131,12 @@ class GraphedStep:
                 self.gstate["acc"].copy_(acc0)
         if own:
             self.graph.replay()
+            self._note()
             return self.static_loss
         self.gstate["nan"].copy_(state["nan"])
         self.gstate["acc"].zero_()
         self.graph.replay()
+        self._note()
         state["nan"].copy_(self.gstate["nan"])
         if state["acc"] is None:
             state["acc"] = self.gstate["acc"].clone()
@@ -263,11 +269,13 @@ class GraphedDPStep(GraphedStep):
         if own:
             self.graph.replay()
             self._comm_and_b(*replay_b)
+            self._note()
             return self.static_loss
         self.gstate["nan"].copy_(state["nan"])
         self.gstate["acc"].zero_()
         self.graph.replay()
         self._comm_and_b(*replay_b)
+        self._note()
         state["nan"].copy_(self.gstate["nan"])
         if state["acc"] is None:
             state["acc"] = self.gstate["acc"].clone()
@@ -358,7 +366,9 @@ class Trainer(AbstractTrainer):
         name = (self.learner or "adam").lower()
         if name == "adam":
             if self._on_gpu():
-                return FusedAdam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
+                lazy = self.config["lazy_row_adam"]
+                return FusedAdam(params, lr=self.learning_rate, weight_decay=self.weight_decay,
+                                 lazy_rows=True if lazy is None else bool(lazy))
             return optim.Adam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
         if name == "sgd":
             return optim.SGD(params, lr=self.learning_rate, weight_decay=self.weight_decay)
@@ -453,6 +463,7 @@ class Trainer(AbstractTrainer):
         else:
             for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
                 loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
+        self.flush_optimizer()
         if state["acc"] is None:
             return 0.0, loss_batches, None
         if int(state["nan"].item()):
@@ -494,7 +505,14 @@ class Trainer(AbstractTrainer):
             parts.append(self.model.inference_by_user(batch).float().reshape(-1).cpu())
         return torch.cat(parts).numpy() if parts else np.zeros(0, np.float32)
 
+    def flush_optimizer(self):
+        """Apply the optimiser's deferred zero-gradient row steps (FusedAdam lazy rows) so every
+        parameter holds its dense-Adam value; called at each epoch end and before evaluation."""
+        if isinstance(self.optimizer, FusedAdam):
+            self.optimizer.flush()
+
     def _valid_by_user_epoch(self, valid_data=None, is_test=False):
+        self.flush_optimizer()
         users, items, lens, npos = self._candidates(is_test)
         preds = self._score(users, items)
         neg_num = self.config["neg_sample_num"]

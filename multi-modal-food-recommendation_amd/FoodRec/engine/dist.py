@@ -51,6 +51,12 @@ class RowExchange:
         # instead of scattering a dense table gradient
         self.sink = None
 
+    def catch_up_rows(self, weight, ids):
+        """Before this rank gathers ``ids``: the sink's lazily updating optimiser brings the rows up
+        to date (rows other ranks touch are replayed inside their own row update)."""
+        if self.sink is not None:
+            self.sink.catch_up_rows(weight, ids)
+
     def stash(self, weight, padding_idx, ids, G, W=None):
         ids = ids.to(torch.int64)
         G = G.to(torch.float32)

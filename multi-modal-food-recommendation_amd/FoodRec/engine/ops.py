@@ -348,6 +348,7 @@ class _EmbeddingExchanged(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, idx, weight, padding_idx, exchange):
+        _catch_up(exchange, weight, idx)
         native.require_device(weight, idx)
         ctx.save_for_backward(idx)
         ctx.weight, ctx.pad, ctx.exchange = weight, padding_idx, exchange
@@ -775,6 +776,7 @@ class _ModalProjection(torch.autograd.Function):
         out = torch.empty(n, T, 64, dtype=torch.float32, device=dev)
         for t in range(T):
             X, W, b = flat[3 * t], flat[3 * t + 1], flat[3 * t + 2]
+            _catch_up(exchange, X, ids)
             K = W.shape[1]
             with profiling.region("modal_projection", projection_bytes(n, K, False)):
                 native.check(lib.fr_gather_linear_fwd(ids.data_ptr(), n, X.data_ptr(), X.stride(0), K, W.data_ptr(),
@@ -825,6 +827,14 @@ class _ModalProjection(torch.autograd.Function):
             grads += [dX, dW if ctx.needs_input_grad[3 + 3 * t] else None,
                       db if (b is not None and ctx.needs_input_grad[4 + 3 * t]) else None]
         return tuple(grads)
+
+
+def _catch_up(exchange, weight, ids):
+    """A lazily updating optimiser (FusedAdam lazy rows) brings the rows about to be gathered up to
+    date first; exchanges without one (or tables without lazy state) make this a no-op."""
+    fn = getattr(exchange, "catch_up_rows", None)
+    if fn is not None:
+        fn(weight, ids)
 
 
 def modal_projection(ids, pairs, exchange=None):

@@ -45,6 +45,7 @@ class RowGrads:
         # id(weight) -> (weight, padding_idx, ids, dY [n, 64], W [64, K]): gradient rows dY[i] W of a
         # gathered Linear input (ops.modal_projection), materialised by FusedAdam before any update
         self.factored = {}
+        self.catch_up = None  # set by a FusedAdam with lazy_rows
 
     def stash_factored(self, weight, padding_idx, ids, dY, W):
         if id(weight) in self.pending or id(weight) in self.factored:  # repeated backward: explicit rows
@@ -67,6 +68,12 @@ class RowGrads:
         self.pending.clear()
         self.factored.clear()
 
+    def catch_up_rows(self, weight, ids):
+        """Called before ``weight`` is gathered at ``ids``: a lazily updating optimiser brings those
+        rows up to the current step (FusedAdam.catch_up_rows)."""
+        if self.catch_up is not None:
+            self.catch_up(weight, ids)
+
     def __bool__(self):
         return bool(self.pending or self.factored)
 
@@ -86,13 +93,84 @@ def _row_grad_ok(p, ids, G) -> bool:
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, lazy_rows=False,
+                 hist_cap=8192):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError("invalid Adam hyper-parameters")
+        if hist_cap < 4:
+            raise ValueError("hist_cap < 4")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       amsgrad=False, maximize=False))
         self._d_lr = {}   # group index -> (device float64 lr, host value it holds)
         self.row_grads = RowGrads()
+        # lazy_rows: row-gradient tables defer their zero-gradient steps (fr_adam_step_rows_lazy);
+        # flush() brings them up to date (bit-identical to the dense update).  _lazy_pending counts
+        # executed lazy steps since the last flush (graph replays report theirs via note_replay).
+        self.lazy_rows = bool(lazy_rows)
+        self.hist_cap = int(hist_cap)
+        self._lazy_pending = 0
+        self._lazy_launched = False
+        if self.lazy_rows:
+            self.row_grads.catch_up = self.catch_up_rows
+
+    @torch.no_grad()
+    def catch_up_rows(self, p, ids):
+        """Rows ``ids`` of a lazily updated table replay their deferred steps (fr_adam_catch_up_rows)
+        so a gather reads dense-Adam values.  No-op for tables without lazy state."""
+        st = self.state.get(p)
+        if not st or "lazy_last" not in st:
+            return
+        group = next(g for g in self.param_groups if any(q is p for q in g["params"]))
+        beta1, beta2 = group["betas"]
+        ids = ids.reshape(-1)
+        if ids.dtype != torch.int64:
+            ids = ids.to(torch.int64)
+        with profiling.region("adam_rows_catch_up", 28 * ids.numel() * p.shape[1] + 8 * ids.numel()):
+            native.check(native.lib().fr_adam_catch_up_rows(
+                p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), st["step"].data_ptr(),
+                ids.data_ptr(), ids.numel(), p.shape[0], p.shape[1], st["lazy_last"].data_ptr(),
+                st["lazy_hist"].data_ptr(), self.hist_cap, float(beta1), float(beta2), float(group["eps"]),
+                float(group["weight_decay"]), native.stream_of(p)), "fr_adam_catch_up_rows")
+
+    @torch.no_grad()
+    def flush(self):
+        """Bring every lazily updated table (and its moments) up to the current step.  Call before
+        reading those tables in full (evaluation, checkpoints, comparisons); cheap when nothing is
+        pending."""
+        if self._lazy_pending == 0:
+            return
+        lib = native.lib()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if "lazy_last" in self.state.get(p, {})]
+            if not ps:
+                continue
+            beta1, beta2 = group["betas"]
+            for k in range(0, len(ps), 16):
+                chunk = ps[k:k + 16]
+                n = len(chunk)
+                st = [self.state[p] for p in chunk]
+                arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+                with profiling.region("adam_rows_flush", sum(24 * p.numel() + 4 * p.shape[0] for p in chunk)):
+                    native.check(lib.fr_adam_flush_rows(
+                        arr(chunk), arr([s["exp_avg"] for s in st]), arr([s["exp_avg_sq"] for s in st]),
+                        arr([s["step"] for s in st]), (ctypes.c_int64 * n)(*[p.numel() for p in chunk]),
+                        (ctypes.c_int32 * n)(*[p.shape[1] for p in chunk]), arr([s["lazy_last"] for s in st]),
+                        arr([s["lazy_hist"] for s in st]), self.hist_cap, n, float(beta1), float(beta2),
+                        float(group["eps"]), float(group["weight_decay"]),
+                        torch.cuda.current_stream(chunk[0].device).cuda_stream), "fr_adam_flush_rows")
+        self._lazy_pending = 0
+
+    def note_replay(self):
+        """A captured step containing a lazy row update was replayed: count it, and flush before
+        the per-step history ring (hist_cap steps) could wrap."""
+        if self._lazy_launched:
+            self._lazy_pending += 1
+            if self._lazy_pending >= self.hist_cap - 2:
+                self.flush()
+
+    def state_dict(self):
+        self.flush()
+        return super().state_dict()
 
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)
@@ -202,6 +280,8 @@ class FusedAdam(torch.optim.Optimizer):
             d_lr = self._lr_tensor(gi, group, dev)
             hyper = (d_lr.data_ptr(), float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
                      float(group["weight_decay"]), native.ptr(skip_flag), torch.cuda.current_stream(dev).cuda_stream)
+            if plist and self._lazy_pending and any("lazy_last" in self.state[p] for p in plist):
+                self.flush()  # a lazily updated table takes a dense step: bring it up to date first
             if plist:
                 with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
                     self._launch_dense(lib, plist, hyper)
@@ -287,6 +367,26 @@ class FusedAdam(torch.optim.Optimizer):
         n = len(plist)
         RM = (ctypes.c_void_p * n)(*[m.data_ptr() for m in maps])
         RD = (ctypes.c_int32 * n)(*dims)
+        if self.lazy_rows and n <= 16:
+            for p in plist:
+                st = self.state[p]
+                if "lazy_last" not in st:
+                    # every row is current through the table's present step (0, or the dense steps so far)
+                    st["lazy_last"] = st["step"].to(torch.int32).expand(p.shape[0]).contiguous()
+                    st["lazy_hist"] = torch.zeros(self.hist_cap, 2, dtype=torch.float32, device=p.device)
+            LA = (ctypes.c_void_p * n)(*[self.state[p]["lazy_last"].data_ptr() for p in plist])
+            LH = (ctypes.c_void_p * n)(*[self.state[p]["lazy_hist"].data_ptr() for p in plist])
+            # algorithmic bytes: p, m, v of the touched rows (bounded by the compact rows' count) read
+            # and written, the compact gradient rows, the row map and the last-step array
+            with profiling.region("adam_rows", sum(28 * c.numel() + 8 * p.shape[0] for p, c in zip(plist, compact))):
+                native.check(lib.fr_adam_step_rows_lazy(P, G, M, V, S, N, RM, RD, LA, LH, self.hist_cap, n, *hyper),
+                             "fr_adam_step_rows_lazy")
+            self._lazy_launched = True
+            if not torch.cuda.is_current_stream_capturing():
+                self._lazy_pending += 1
+                if self._lazy_pending >= self.hist_cap - 2:
+                    self.flush()
+            return
         with profiling.region("adam_rows", sum(adam_rows_bytes(p.numel(), p.shape[0], c.numel())
                                               for p, c in zip(plist, compact))):
             native.check(lib.fr_adam_step_rows(P, G, M, V, S, N, RM, RD, n, *hyper), "fr_adam_step_rows")

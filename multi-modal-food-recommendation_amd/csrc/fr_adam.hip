@@ -206,7 +206,236 @@ __global__ void adam_bf16_step_inc_kernel(int64_t* step, const int32_t* skip) {
   if (skip && *skip) return;
   if (threadIdx.x == 0) step[0] += 1;
 }
+
+// ---- Deferred zero-gradient steps for row-gradient tables ("lazy rows", exact) ----------------
+// torch's Adam updates every row of a table each step, also rows whose gradient is zero.  For such
+// a row the step only decays (m, v) and moves p by the step's (neg_step, bc2_sqrt); those two
+// scalars depend on the step index and lr alone.  The lazy form records them per step in a ring
+// (hist[s % cap]) and keeps last[r] = the step row r is current through.  A row that receives a
+// gradient at step t first replays steps last[r]+1 .. t-1 with g = 0 (adam_elem, the same float
+// operations as the dense kernel), then applies step t; untouched rows are not read.  A flush
+// replays every row up to the current step.  Results are bit-identical to the dense update at
+// every flush point; HBM traffic per step is 24 B per parameter of the TOUCHED rows only.
+// The host flushes before any full-table read and at least every cap-1 steps.
+constexpr int kMaxLazy = 16;
+
+struct LazyArgs {
+  float* p[kMaxLazy];
+  const float* g[kMaxLazy];
+  float* m[kMaxLazy];
+  float* v[kMaxLazy];
+  int64_t* step[kMaxLazy];
+  const int32_t* rmap[kMaxLazy];
+  int32_t* last[kMaxLazy];
+  float* hist[kMaxLazy];      // [cap][2]: (neg_step, bc2_sqrt) of step s at s % cap
+  int32_t rshift[kMaxLazy];   // row width = 1 << rshift
+  int32_t row_start[kMaxLazy + 1];
+  int32_t cap;
+  int n;
+};
+
+__global__ void adam_lazy_inc_kernel(LazyArgs a, AdamHyper h, const int32_t* skip) {
+  if (skip && *skip) return;
+  const int t = threadIdx.x;
+  if (t >= a.n) return;
+  const int64_t st = a.step[t][0] + 1;
+  a.step[t][0] = st;
+  const double lr = h.d_lr ? h.d_lr[0] : h.lr;
+  const double bc1 = 1.0 - pow(h.beta1_d, (double)st);
+  const double bc2 = 1.0 - pow(h.beta2_d, (double)st);
+  float* e = a.hist[t] + 2 * (st % a.cap);
+  e[0] = (float)(-(lr / bc1));
+  e[1] = (float)sqrt(bc2);
+}
+
+// one wave per (tensor, row); FLUSH: replay through step t, no gradient; else only rows with a
+// gradient slot, replay through t-1 then apply step t with the slot's row
+template <bool FLUSH>
+__global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyper h, const int32_t* skip) {
+  if (skip && *skip) return;
+  const int lane = threadIdx.x & 63;
+  const int total = a.row_start[a.n];
+  const int waves = gridDim.x * 4;
+  int t = 0;
+  for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < total; w += waves) {
+    while (t + 1 < a.n && w >= a.row_start[t + 1]) ++t;
+    while (t > 0 && w < a.row_start[t]) --t;
+    const int64_t r = w - a.row_start[t];
+    int32_t slot = -1;
+    if constexpr (!FLUSH) {
+      slot = a.rmap[t][r];
+      if (slot < 0) continue;
+    }
+    const int64_t st = a.step[t][0];
+    const int64_t s0 = (int64_t)a.last[t][r] + 1;
+    const int64_t s_end = FLUSH ? st + 1 : st;  // replayed zero-gradient steps: [s0, s_end)
+    if (FLUSH && s0 > st) continue;
+    const float* __restrict__ hist = a.hist[t];
+    const int cap = a.cap;
+    const int width = 1 << a.rshift[t];
+    float* __restrict__ P = a.p[t] + (r << a.rshift[t]);
+    float* __restrict__ M = a.m[t] + (r << a.rshift[t]);
+    float* __restrict__ V = a.v[t] + (r << a.rshift[t]);
+    const float* __restrict__ G = FLUSH ? nullptr : a.g[t] + ((int64_t)slot << a.rshift[t]);
+    for (int q = 4 * lane; q < width; q += 4 * 64) {
+      float4 p = *reinterpret_cast<const float4*>(P + q);
+      float4 m = *reinterpret_cast<const float4*>(M + q);
+      float4 v = *reinterpret_cast<const float4*>(V + q);
+      AdamHyper hs = h;
+      for (int64_t s = s0; s < s_end; ++s) {
+        const float* e = hist + 2 * (s % cap);
+        hs.neg_step = e[0];
+        hs.bc2_sqrt = e[1];
+        adam_elem(p.x, 0.f, m.x, v.x, hs);
+        adam_elem(p.y, 0.f, m.y, v.y, hs);
+        adam_elem(p.z, 0.f, m.z, v.z, hs);
+        adam_elem(p.w, 0.f, m.w, v.w, hs);
+      }
+      if constexpr (!FLUSH) {
+        const float4 g = *reinterpret_cast<const float4*>(G + q);
+        const float* e = hist + 2 * (st % cap);
+        hs.neg_step = e[0];
+        hs.bc2_sqrt = e[1];
+        adam_elem(p.x, g.x, m.x, v.x, hs);
+        adam_elem(p.y, g.y, m.y, v.y, hs);
+        adam_elem(p.z, g.z, m.z, v.z, hs);
+        adam_elem(p.w, g.w, m.w, v.w, hs);
+      }
+      *reinterpret_cast<float4*>(P + q) = p;
+      *reinterpret_cast<float4*>(M + q) = m;
+      *reinterpret_cast<float4*>(V + q) = v;
+    }
+    if (lane == 0) a.last[t][r] = (int32_t)st;
+  }
+}
+
+// Catch-up before a gather: the rows a step is about to read (ids, duplicates allowed) replay their
+// deferred zero-gradient steps through the current step, so the forward sees dense-Adam values.
+// One wave per id; the wave whose atomicMax raises last[r] does the row, duplicates skip.
+__global__ __launch_bounds__(256) void adam_catch_up_kernel(float* __restrict__ P0, float* __restrict__ M0,
+                                                            float* __restrict__ V0, const int64_t* step,
+                                                            const int64_t* __restrict__ ids, int64_t n, int64_t R,
+                                                            int rshift, int32_t* last, const float* __restrict__ hist,
+                                                            int cap, AdamHyper h) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t r = ids[i];
+  if (r < 0 || r >= R) return;
+  const int64_t st = step[0];
+  int32_t old = 0;
+  if (lane == 0) old = atomicMax(last + r, (int32_t)st);
+  old = __shfl(old, 0, 64);
+  if ((int64_t)old >= st) return;
+  const int width = 1 << rshift;
+  float* P = P0 + (r << rshift);
+  float* M = M0 + (r << rshift);
+  float* V = V0 + (r << rshift);
+  for (int q = 4 * lane; q < width; q += 4 * 64) {
+    float4 p = *reinterpret_cast<const float4*>(P + q);
+    float4 m = *reinterpret_cast<const float4*>(M + q);
+    float4 v = *reinterpret_cast<const float4*>(V + q);
+    AdamHyper hs = h;
+    for (int64_t s = (int64_t)old + 1; s <= st; ++s) {
+      const float* e = hist + 2 * (s % cap);
+      hs.neg_step = e[0];
+      hs.bc2_sqrt = e[1];
+      adam_elem(p.x, 0.f, m.x, v.x, hs);
+      adam_elem(p.y, 0.f, m.y, v.y, hs);
+      adam_elem(p.z, 0.f, m.z, v.z, hs);
+      adam_elem(p.w, 0.f, m.w, v.w, hs);
+    }
+    *reinterpret_cast<float4*>(P + q) = p;
+    *reinterpret_cast<float4*>(M + q) = m;
+    *reinterpret_cast<float4*>(V + q) = v;
+  }
+}
 }  // namespace
+
+static int lazy_impl(bool flush, float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                     const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                     float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr, double lr,
+                     double beta1, double beta2, double eps, double weight_decay, const int32_t* d_skip,
+                     void* stream) {
+  FR_REQUIRE(n_tensors >= 0 && n_tensors <= kMaxLazy, "n_tensors out of range [0, 16]");
+  if (n_tensors == 0) return FR_OK;
+  FR_REQUIRE(params && exp_avg && exp_avg_sq && d_steps && numel && row_dims && d_last && d_hist,
+             "null host array");
+  FR_REQUIRE(flush || (grads && d_rmaps), "grads and d_rmaps required");
+  FR_REQUIRE(hist_cap >= 2, "hist_cap < 2");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  AdamHyper h{};
+  h.lr = lr;
+  h.beta1_d = beta1;
+  h.beta2_d = beta2;
+  h.d_lr = d_lr;
+  h.w1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.one_m_b2 = (float)(1.0 - beta2);
+  h.eps = (float)eps;
+  h.wd = (float)weight_decay;
+  LazyArgs a{};
+  a.n = n_tensors;
+  a.cap = hist_cap;
+  int64_t rows = 0;
+  for (int t = 0; t < n_tensors; ++t) {
+    const int32_t dd = row_dims[t];
+    FR_REQUIRE(dd >= 4 && (dd & (dd - 1)) == 0 && numel[t] % dd == 0,
+               "lazy row tensors need a power-of-two row width >= 4");
+    FR_REQUIRE(params[t] && exp_avg[t] && exp_avg_sq[t] && d_steps[t] && d_last[t] && d_hist[t],
+               "null tensor pointer");
+    FR_REQUIRE(fr::aligned16(params[t]) && fr::aligned16(exp_avg[t]) && fr::aligned16(exp_avg_sq[t]),
+               "lazy row tensors must be 16-byte aligned");
+    a.p[t] = params[t];
+    a.m[t] = exp_avg[t];
+    a.v[t] = exp_avg_sq[t];
+    a.step[t] = d_steps[t];
+    a.last[t] = d_last[t];
+    a.hist[t] = d_hist[t];
+    if (!flush) {
+      FR_REQUIRE(grads[t] && d_rmaps[t] && fr::aligned16(grads[t]), "null or misaligned gradient rows");
+      a.g[t] = grads[t];
+      a.rmap[t] = d_rmaps[t];
+    }
+    a.rshift[t] = 0;
+    while ((1 << a.rshift[t]) < dd) ++a.rshift[t];
+    a.row_start[t] = (int32_t)rows;
+    rows += numel[t] / dd;
+    FR_REQUIRE(rows < INT32_MAX, "too many rows for one launch");
+  }
+  a.row_start[n_tensors] = (int32_t)rows;
+  if (rows == 0) return FR_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(rows, 4), (int64_t)fr::kNumCU * 8);
+  if (flush) {
+    hipLaunchKernelGGL(adam_lazy_rows_kernel<true>, dim3(blocks), dim3(256), 0, s, a, h, nullptr);
+  } else {
+    hipLaunchKernelGGL(adam_lazy_inc_kernel, dim3(1), dim3(64), 0, s, a, h, d_skip);
+    FR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(adam_lazy_rows_kernel<false>, dim3(blocks), dim3(256), 0, s, a, h, d_skip);
+  }
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_adam_step_rows_lazy(float* const* params, const float* const* grads, float* const* exp_avg,
+                                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
+                                      const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                                      float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr,
+                                      double lr, double beta1, double beta2, double eps, double weight_decay,
+                                      const int32_t* d_skip, void* stream) {
+  return lazy_impl(false, params, grads, exp_avg, exp_avg_sq, d_steps, numel, d_rmaps, row_dims, d_last, d_hist,
+                   hist_cap, n_tensors, d_lr, lr, beta1, beta2, eps, weight_decay, d_skip, stream);
+}
+
+extern "C" int fr_adam_flush_rows(float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
+                                  int64_t* const* d_steps, const int64_t* numel, const int32_t* row_dims,
+                                  int32_t* const* d_last, float* const* d_hist, int32_t hist_cap, int n_tensors,
+                                  double beta1, double beta2, double eps, double weight_decay, void* stream) {
+  return lazy_impl(true, params, nullptr, exp_avg, exp_avg_sq, d_steps, numel, nullptr, row_dims, d_last, d_hist,
+                   hist_cap, n_tensors, nullptr, 0.0, beta1, beta2, eps, weight_decay, nullptr, stream);
+}
+
 
 static int adam_impl(float* const* params, const float* const* grads, float* const* exp_avg,
                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
@@ -350,6 +579,34 @@ extern "C" int fr_adam_step_bf16(uint16_t* d_param, float* d_master, const uint1
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(n8, 256), (int64_t)fr::kNumCU * 8);
   hipLaunchKernelGGL(adam_bf16_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<uint4*>(d_param), d_master,
                      reinterpret_cast<const uint4*>(d_grad), d_exp_avg, d_exp_avg_sq, n8, d_step, h, d_skip);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_adam_catch_up_rows(float* param, float* exp_avg, float* exp_avg_sq, const int64_t* d_step,
+                                     const int64_t* d_ids, int64_t n, int64_t rows, int32_t row_dim, int32_t* d_last,
+                                     const float* d_hist, int32_t hist_cap, double beta1, double beta2, double eps,
+                                     double weight_decay, void* stream) {
+  FR_REQUIRE(n >= 0 && rows >= 0, "negative size");
+  if (n == 0 || rows == 0) return FR_OK;
+  FR_REQUIRE(param && exp_avg && exp_avg_sq && d_step && d_ids && d_last && d_hist, "null pointer");
+  FR_REQUIRE(row_dim >= 4 && (row_dim & (row_dim - 1)) == 0, "row width must be a power of two >= 4");
+  FR_REQUIRE(hist_cap >= 2, "hist_cap < 2");
+  FR_REQUIRE(fr::aligned16(param) && fr::aligned16(exp_avg) && fr::aligned16(exp_avg_sq), "16-byte alignment");
+  FR_REQUIRE(rows < INT32_MAX, "too many rows");
+  AdamHyper h{};
+  h.beta1_d = beta1;
+  h.beta2_d = beta2;
+  h.w1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.one_m_b2 = (float)(1.0 - beta2);
+  h.eps = (float)eps;
+  h.wd = (float)weight_decay;
+  int rshift = 0;
+  while ((1 << rshift) < row_dim) ++rshift;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_catch_up_kernel, dim3((unsigned)fr::ceil_div(n, 4)), dim3(256), 0, s, param, exp_avg,
+                     exp_avg_sq, d_step, d_ids, n, rows, rshift, d_last, d_hist, hist_cap, h);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -149,3 +149,125 @@ def test_healthrec_step_row_vs_dense(cuda):
             assert torch.equal(a, b), k
             for s_ in ("exp_avg", "exp_avg_sq"):
                 assert torch.equal(oa.state[a][s_], ob.state[b][s_]), (k, s_)
+
+
+@pytest.mark.parametrize("wd,cap", [(0.0, 8192), (0.01, 8), (0.0, 5)])
+def test_lazy_row_adam_equals_eager_rows(cuda, wd, cap):
+    """fr_adam_step_rows_lazy (deferred zero-gradient row steps) vs fr_adam_step_rows over 23 steps
+    on two tables with sparse, repeating row sets, an lr change mid-way (LambdaLR between epochs),
+    weight decay, and a history ring small enough to force the automatic flushes: after each flush
+    p, exp_avg and exp_avg_sq are BIT-IDENTICAL to the every-row update."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(2)
+    shapes = [(613, 256), (301, 64)]
+    w0 = [torch.randn(R, d) for R, d in shapes]
+    pa = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    pb = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    oa = FusedAdam(pa, lr=3e-3, weight_decay=wd)
+    ob = FusedAdam(pb, lr=3e-3, weight_decay=wd, lazy_rows=True, hist_cap=cap)
+    for step in range(23):
+        if step == 11:
+            for o in (oa, ob):
+                o.param_groups[0]["lr"] = 1.5e-3
+                o.sync_lr()
+        oa.zero_grad()
+        ob.zero_grad()
+        for k, ((R, d), a, b) in enumerate(zip(shapes, pa, pb)):
+            n = 40 if step % 3 else 5
+            ids, G = _case(R, d, n, None, 100 * step + k)
+            # step 0 touches every row (non-zero moments everywhere), later steps a third of them:
+            # the other rows only decay, through deferred steps
+            ids = torch.arange(R) if step == 0 else ids % (R // 3)
+            G = torch.randn(R, d) if step == 0 else G
+            ids, G = ids.to(cuda), G.to(cuda)
+            oa.row_grads.stash(a, None, ids, G)
+            ob.row_grads.stash(b, None, ids, G)
+        oa.step()
+        ob.step()
+        if step in (6, 22):
+            ob.flush()
+            for a, b in zip(pa, pb):
+                assert torch.equal(a, b)
+                for s_ in ("exp_avg", "exp_avg_sq"):
+                    assert torch.equal(oa.state[a][s_], ob.state[b][s_]), s_
+    # lazy state really skipped rows between flushes
+    assert "lazy_last" in ob.state[pb[0]]
+
+
+def test_lazy_row_adam_graph_replay(cuda):
+    """The lazy update captured in a HIP graph and replayed: step counter, history ring and row
+    replays run from device state; note_replay counts the replays, flush() equals the eager rows."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(3)
+    R, d = 517, 128
+    w0 = torch.randn(R, d)
+    pa = torch.nn.Parameter(w0.clone().to(cuda))
+    pb = torch.nn.Parameter(w0.clone().to(cuda))
+    oa = FusedAdam([pa], lr=2e-3)
+    ob = FusedAdam([pb], lr=2e-3, lazy_rows=True, hist_cap=16)
+    ids_s = torch.zeros(64, dtype=torch.int64, device=cuda)
+    G_s = torch.zeros(64, d, device=cuda)
+
+    def body():
+        ob.zero_grad()
+        ob.row_grads.stash(pb, None, ids_s, G_s)
+        ob.step()
+
+    cases = [_case(R, d, 64, None, 700 + k) for k in range(20)]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ids_s.copy_(cases[0][0].to(cuda) % 100)
+        G_s.copy_(cases[0][1].to(cuda))
+        body()  # eager warm-up step (state creation)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    for k, (ids, G) in enumerate(cases):
+        oa.zero_grad()
+        oa.row_grads.stash(pa, None, ids.to(cuda) % 100, G.to(cuda))
+        oa.step()
+        if k == 0:
+            continue
+        ids_s.copy_(ids.to(cuda) % 100)
+        G_s.copy_(G.to(cuda))
+        g.replay()
+        ob.note_replay()
+    ob.flush()
+    torch.cuda.synchronize()
+    assert torch.equal(pa, pb)
+    assert torch.equal(oa.state[pa]["exp_avg"], ob.state[pb]["exp_avg"])
+    assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
+    assert int(ob.state[pb]["step"].item()) == 20
+
+
+def test_lazy_row_catch_up_before_gather(cuda):
+    """Rows read by a step (ids with duplicates) are caught up before the gather: they equal the
+    every-row update's rows right away, without a flush; the other rows are still deferred."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(4)
+    R, d = 400, 512
+    w0 = torch.randn(R, d)
+    pa = torch.nn.Parameter(w0.clone().to(cuda))
+    pb = torch.nn.Parameter(w0.clone().to(cuda))
+    oa = FusedAdam([pa], lr=4e-3)
+    ob = FusedAdam([pb], lr=4e-3, lazy_rows=True)
+    for k in range(9):
+        ids, G = _case(R, d, 50, None, 900 + k)
+        ids = torch.arange(R) if k == 0 else ids % 50  # every row has moments after step 1
+        G = torch.randn(R, d) if k == 0 else G
+        ids, G = ids.to(cuda), G.to(cuda)
+        for o, p in ((oa, pa), (ob, pb)):
+            o.zero_grad()
+            o.row_grads.stash(p, None, ids, G)
+            o.step()
+    read = torch.tensor([3, 3, 77, 391, 120, 77], dtype=torch.int64, device=cuda)  # 77+: untouched rows
+    ob.row_grads.catch_up_rows(pb, read)
+    assert torch.equal(pa[read], pb[read])
+    assert not torch.equal(pa[200:], pb[200:])  # deferred
+    ob.row_grads.catch_up_rows(pb, read)  # idempotent
+    assert torch.equal(pa[read], pb[read])
+    ob.flush()
+    assert torch.equal(pa, pb)
+    assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
