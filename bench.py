@@ -113,14 +113,17 @@ def main():
 
     use_graph = not args.eager  # N>1: two graphs per step, gradient collectives between them
     graphed = trainer.graphed_step(args.batch, warmup=3) if use_graph else None
+    feed = None
     if graphed is not None:
-        # the sampler writes each batch into the graph's static inputs and the graph accumulates
-        # into its own state: no per-step copies around the replay
+        # the sampler stages each epoch's permutation and negatives on the device and the graph
+        # gathers its own batch (DeviceFeed) and accumulates into its own state: per step the host
+        # only replays the graph
         state = graphed.state
+        feed = graphed.attach_feed(sampler)
 
     def batches():
         while True:
-            for t in sampler.epoch(out=graphed.inputs if graphed is not None else None):
+            for t in sampler.epoch(out=graphed.inputs if graphed is not None else None, feed=feed):
                 yield t
 
     it = batches()
@@ -160,6 +163,8 @@ def main():
         tk0 = time.perf_counter()
         for i in range(args.kernel_steps):
             u, p, n = next(it)
+            if feed is not None and u is graphed.inputs[0]:
+                feed.fill(u, p, n)  # eager step: gather the batch the graph would have gathered
             trainer.train_step(feats.batch(u, p, n), i, state)
         torch.cuda.synchronize()
         eager_elapsed = time.perf_counter() - tk0

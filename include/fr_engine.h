@@ -317,11 +317,13 @@ int fr_adam_step_rows(float* const* params, const float* const* grads, float* co
  * kernel's float operations), then applies this step.  fr_adam_flush_rows brings every row up to
  * the current step; after a flush p, exp_avg and exp_avg_sq equal fr_adam_step_rows' bit for bit.
  * The caller flushes before any full-table read and at least every hist_cap - 1 steps.
- * d_last: int32 [R] per tensor (zero at step 0); d_hist: float32 [hist_cap, 2] per tensor;
- * n_tensors <= 16. */
+ * d_ids[t][0..n_ids[t]): the ids whose gradient rows d_rmaps[t] maps (duplicates allowed; the
+ * kernel works per id, not per table row).  d_last: int32 [R] per tensor (zero at step 0); d_hist:
+ * float32 [hist_cap, 2] per tensor; n_tensors <= 16. */
 int fr_adam_step_rows_lazy(float* const* params, const float* const* grads, float* const* exp_avg,
                            float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
-                           const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                           const int32_t* const* d_rmaps, const int64_t* const* d_ids, const int64_t* n_ids,
+                           const int32_t* row_dims, int32_t* const* d_last,
                            float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr,
                            double lr, double beta1, double beta2, double eps, double weight_decay,
                            const int32_t* d_skip, void* stream);

@@ -85,6 +85,17 @@ class GraphedStep:
         # the NaN flag into gstate["nan"].  Callers that pass this dict (``.state``) as their epoch
         # state pay no per-step copies; any other state dict is folded in around each replay.
         self.gstate = {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=dev)}
+        self.feed = None  # engine.sampler.DeviceFeed: full batches are gathered inside the graph
+
+    def attach_feed(self, sampler):
+        """Gather full batches inside the step from ``sampler``'s staged epoch (pass the returned feed
+        to ``sampler.epoch(out=self.inputs, feed=...)``)."""
+        if self.graph is not None or self.calls:
+            raise RuntimeError("attach_feed before the first step")
+        if sampler.batch_size != self.B:
+            raise ValueError("sampler batch size differs from the graphed step's")
+        self.feed = sampler.device_feed()
+        return self.feed
 
     @property
     def state(self):
@@ -100,6 +111,8 @@ class GraphedStep:
             self.tr.optimizer.note_replay()
 
     def _body(self, batch_idx, state, accumulate=True):
+        if self.feed is not None:
+            self.feed.fill(self.u, self.p, self.n)
         feats = self.tr._features()
         return self.tr.train_step(feats.batch(self.u, self.p, self.n), batch_idx, state, accumulate=accumulate)
 
@@ -168,6 +181,8 @@ class GraphedDPStep(GraphedStep):
 
     def _part_a(self, batch_idx, state, accumulate):
         tr = self.tr
+        if self.feed is not None:
+            self.feed.fill(self.u, self.p, self.n)
         feats = tr._features()
         tr.optimizer.zero_grad()
         losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n))
@@ -458,7 +473,9 @@ class Trainer(AbstractTrainer):
             if state["acc"] is not None:
                 state["acc"].zero_()
             state["nan"].zero_()
-            for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs)):
+            if step.feed is None and hasattr(train_data, "device_feed"):
+                step.attach_feed(train_data)
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs, feed=step.feed)):
                 loss_batches.append(step(u, p, n, batch_idx, state))
         else:
             for batch_idx, (u, p, n) in enumerate(train_data.epoch()):

@@ -114,7 +114,8 @@ _SIGS = {
                                   POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_int32), c_int,
                                   c_void_p, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
     "fr_adam_step_rows_lazy": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
-                                       POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_int32),
+                                       POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_void_p),
+                                       POINTER(c_int64), POINTER(c_int32),
                                        POINTER(c_void_p), POINTER(c_void_p), c_int32, c_int, c_void_p, c_double,
                                        c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
     "fr_adam_flush_rows": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),

@@ -334,16 +334,18 @@ class FusedAdam(torch.optim.Optimizer):
     def _factored_rows(self, lib, ents, G, width, R, pad):
         from . import ops
         rmap, crows = ops.factored_rows(ents[0][1], G, width, R, pad, [e[3] for e in ents])
-        return {id(e[0]): ("prepared", rmap, c) for e, c in zip(ents, crows)}
+        ids = ents[0][1].reshape(-1)
+        return {id(e[0]): ("prepared", rmap, c, ids) for e, c in zip(ents, crows)}
 
     def _launch_rows(self, lib, rows, hyper):
-        plist, compact, maps, dims = [], [], [], []
+        plist, compact, maps, dims, idl = [], [], [], [], []
         for p, entry in rows:
             if entry[0] == "prepared":
                 plist.append(p)
                 compact.append(entry[2])
                 maps.append(entry[1])
                 dims.append(p.shape[1])
+                idl.append(entry[3])
                 continue
             ids, G, pad = entry
             R, d = p.shape
@@ -363,6 +365,7 @@ class FusedAdam(torch.optim.Optimizer):
             compact.append(crow)
             maps.append(rmap)
             dims.append(d)
+            idl.append(ids if ids.dtype == torch.int64 else ids.to(torch.int64))
         P, G, M, V, S, N = self._arrays(plist, compact)
         n = len(plist)
         RM = (ctypes.c_void_p * n)(*[m.data_ptr() for m in maps])
@@ -376,11 +379,14 @@ class FusedAdam(torch.optim.Optimizer):
                     st["lazy_hist"] = torch.zeros(self.hist_cap, 2, dtype=torch.float32, device=p.device)
             LA = (ctypes.c_void_p * n)(*[self.state[p]["lazy_last"].data_ptr() for p in plist])
             LH = (ctypes.c_void_p * n)(*[self.state[p]["lazy_hist"].data_ptr() for p in plist])
+            idl = [i if i.is_contiguous() else i.contiguous() for i in idl]
+            ID = (ctypes.c_void_p * n)(*[i.data_ptr() for i in idl])
+            NI = (ctypes.c_int64 * n)(*[i.numel() for i in idl])
             # algorithmic bytes: p, m, v of the touched rows (bounded by the compact rows' count) read
-            # and written, the compact gradient rows, the row map and the last-step array
-            with profiling.region("adam_rows", sum(28 * c.numel() + 8 * p.shape[0] for p, c in zip(plist, compact))):
-                native.check(lib.fr_adam_step_rows_lazy(P, G, M, V, S, N, RM, RD, LA, LH, self.hist_cap, n, *hyper),
-                             "fr_adam_step_rows_lazy")
+            # and written, the compact gradient rows read, the ids / map / last-step entries
+            with profiling.region("adam_rows", sum(28 * c.numel() + 16 * i.numel() for c, i in zip(compact, idl))):
+                native.check(lib.fr_adam_step_rows_lazy(P, G, M, V, S, N, RM, ID, NI, RD, LA, LH, self.hist_cap, n,
+                                                        *hyper), "fr_adam_step_rows_lazy")
             self._lazy_launched = True
             if not torch.cuda.is_current_stream_capturing():
                 self._lazy_pending += 1

@@ -92,26 +92,70 @@ class TripleSampler:
         g.manual_seed(seed)
         return torch.randperm(self.n, generator=g)
 
-    def epoch(self, out=None):
+    def device_feed(self):
+        """A DeviceFeed over this sampler's device arrays (for a graphed step that gathers its own
+        batches: see DeviceFeed)."""
+        return DeviceFeed(self._dev_users, self._dev_items, self.n, self.batch_size, self.device)
+
+    def epoch(self, out=None, feed=None):
         """Yield (u, pos, neg) int64 device tensors per batch for one epoch.  Negatives are drawn
         per batch (same stream as the reference's per-sample draws, in permutation order).  With
         ``out`` = three [batch_size] device buffers (a graphed step's static inputs), full batches
         are written into them and the buffers are yielded."""
         perm = self.epoch_order().numpy()
         perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
-        pin = self.device.type == "cuda"
+        # the whole epoch's negatives in one native call and one host->device copy: the same draws in
+        # the same order as per-batch (or the reference's per-sample) drawing, since nothing else
+        # consumes np.random during an epoch; the steps then only index device arrays
+        negs_all = torch.from_numpy(self._negatives(self.users[perm]))
+        if self.device.type == "cuda":
+            negs_all = negs_all.pin_memory()
+        negs_d = negs_all.to(self.device, non_blocking=True)
+        if feed is not None and out is not None:
+            feed.stage(perm_d, negs_d)
         for s in range(0, self.n, self.batch_size):
-            negs = torch.from_numpy(self._negatives(self.users[perm[s:s + self.batch_size]]))
-            if pin:
-                negs = negs.pin_memory()
             idx = perm_d[s:s + self.batch_size]
+            negs = negs_d[s:s + self.batch_size]
             if out is not None and idx.numel() == out[0].numel():
+                if feed is not None:  # the consumer's graph gathers this batch itself
+                    yield out
+                    continue
                 torch.index_select(self._dev_users, 0, idx, out=out[0])
                 torch.index_select(self._dev_items, 0, idx, out=out[1])
-                out[2].copy_(negs, non_blocking=True)
+                out[2].copy_(negs)
                 yield out
             else:
-                yield self._dev_users[idx], self._dev_items[idx], negs.to(self.device, non_blocking=True)
+                yield self._dev_users[idx], self._dev_items[idx], negs
+
+
+class DeviceFeed:
+    """The epoch's permutation and negatives staged in fixed device buffers plus a device batch
+    cursor, so a captured step gathers its own (u, pos, neg) batch (``fill``, inside the graph):
+    the host only replays the graph per step, no kernels between replays.  ``stage`` (once per
+    epoch, outside the graph) copies the epoch in and rewinds the cursor."""
+
+    def __init__(self, dev_users, dev_items, n, batch_size, device):
+        self.users, self.items = dev_users, dev_items
+        self.B = int(batch_size)
+        self.perm = torch.zeros(n, dtype=torch.int64, device=device)
+        self.negs = torch.zeros(n, dtype=torch.int64, device=device)
+        self.cursor = torch.zeros((), dtype=torch.int64, device=device)
+        self.offs = torch.arange(self.B, dtype=torch.int64, device=device)
+        self._pos = torch.empty(self.B, dtype=torch.int64, device=device)
+        self._idx = torch.empty(self.B, dtype=torch.int64, device=device)
+
+    def stage(self, perm_d, negs_d):
+        self.perm.copy_(perm_d)
+        self.negs.copy_(negs_d)
+        self.cursor.zero_()
+
+    def fill(self, u, p, n):
+        torch.add(self.offs, self.cursor * self.B, out=self._pos)
+        torch.index_select(self.perm, 0, self._pos, out=self._idx)
+        torch.index_select(self.users, 0, self._idx, out=u)
+        torch.index_select(self.items, 0, self._idx, out=p)
+        torch.index_select(self.negs, 0, self._pos, out=n)
+        self.cursor.add_(1)
 
 
 SSL_MASKED_P = 0.2   # TrainDataLoader.masked_p (dataloader.py:19)

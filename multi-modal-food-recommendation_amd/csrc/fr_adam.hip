@@ -228,8 +228,10 @@ struct LazyArgs {
   const int32_t* rmap[kMaxLazy];
   int32_t* last[kMaxLazy];
   float* hist[kMaxLazy];      // [cap][2]: (neg_step, bc2_sqrt) of step s at s % cap
+  const int64_t* ids[kMaxLazy];  // step: the ids whose rows carry a gradient (duplicates allowed)
+  int64_t nrows[kMaxLazy];
   int32_t rshift[kMaxLazy];   // row width = 1 << rshift
-  int32_t row_start[kMaxLazy + 1];
+  int32_t row_start[kMaxLazy + 1];  // flush: prefix over rows; step: prefix over ids
   int32_t cap;
   int n;
 };
@@ -248,8 +250,9 @@ __global__ void adam_lazy_inc_kernel(LazyArgs a, AdamHyper h, const int32_t* ski
   e[1] = (float)sqrt(bc2);
 }
 
-// one wave per (tensor, row); FLUSH: replay through step t, no gradient; else only rows with a
-// gradient slot, replay through t-1 then apply step t with the slot's row
+// FLUSH: one wave per (tensor, row), replay through step t, no gradient.  Step: one wave per
+// (tensor, id) of the step's gradient ids; the row replays through t-1, then takes step t with its
+// slot's gradient row
 template <bool FLUSH>
 __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
@@ -260,14 +263,24 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyp
   for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < total; w += waves) {
     while (t + 1 < a.n && w >= a.row_start[t + 1]) ++t;
     while (t > 0 && w < a.row_start[t]) --t;
-    const int64_t r = w - a.row_start[t];
+    const int64_t st = a.step[t][0];
+    int64_t r, s0;
     int32_t slot = -1;
-    if constexpr (!FLUSH) {
+    if constexpr (FLUSH) {
+      r = w - a.row_start[t];
+      s0 = (int64_t)a.last[t][r] + 1;
+    } else {
+      // wave per id: the wave whose atomicMax raises last[r] to st owns the row (duplicates skip)
+      r = a.ids[t][w - a.row_start[t]];
+      if (r < 0 || r >= a.nrows[t]) continue;
       slot = a.rmap[t][r];
       if (slot < 0) continue;
+      int32_t old = 0;
+      if (lane == 0) old = atomicMax(a.last[t] + r, (int32_t)st);
+      old = __shfl(old, 0, 64);
+      if ((int64_t)old >= st) continue;
+      s0 = (int64_t)old + 1;
     }
-    const int64_t st = a.step[t][0];
-    const int64_t s0 = (int64_t)a.last[t][r] + 1;
     const int64_t s_end = FLUSH ? st + 1 : st;  // replayed zero-gradient steps: [s0, s_end)
     if (FLUSH && s0 > st) continue;
     const float* __restrict__ hist = a.hist[t];
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyp
       *reinterpret_cast<float4*>(M + q) = m;
       *reinterpret_cast<float4*>(V + q) = v;
     }
-    if (lane == 0) a.last[t][r] = (int32_t)st;
+    if (FLUSH && lane == 0) a.last[t][r] = (int32_t)st;
   }
 }
 
@@ -354,7 +367,8 @@ __global__ __launch_bounds__(256) void adam_catch_up_kernel(float* __restrict__ 
 
 static int lazy_impl(bool flush, float* const* params, const float* const* grads, float* const* exp_avg,
                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
-                     const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                     const int32_t* const* d_rmaps, const int64_t* const* d_ids, const int64_t* n_ids,
+                     const int32_t* row_dims, int32_t* const* d_last,
                      float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr, double lr,
                      double beta1, double beta2, double eps, double weight_decay, const int32_t* d_skip,
                      void* stream) {
@@ -393,25 +407,32 @@ static int lazy_impl(bool flush, float* const* params, const float* const* grads
     a.step[t] = d_steps[t];
     a.last[t] = d_last[t];
     a.hist[t] = d_hist[t];
+    a.nrows[t] = numel[t] / dd;
+    a.row_start[t] = (int32_t)rows;
     if (!flush) {
       FR_REQUIRE(grads[t] && d_rmaps[t] && fr::aligned16(grads[t]), "null or misaligned gradient rows");
+      FR_REQUIRE(n_ids[t] >= 0 && (n_ids[t] == 0 || d_ids[t]), "null ids");
       a.g[t] = grads[t];
       a.rmap[t] = d_rmaps[t];
+      a.ids[t] = d_ids[t];
+      rows += n_ids[t];
+    } else {
+      rows += a.nrows[t];
     }
     a.rshift[t] = 0;
     while ((1 << a.rshift[t]) < dd) ++a.rshift[t];
-    a.row_start[t] = (int32_t)rows;
-    rows += numel[t] / dd;
     FR_REQUIRE(rows < INT32_MAX, "too many rows for one launch");
   }
   a.row_start[n_tensors] = (int32_t)rows;
-  if (rows == 0) return FR_OK;
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(rows, 4), (int64_t)fr::kNumCU * 8);
   if (flush) {
+    if (rows == 0) return FR_OK;
     hipLaunchKernelGGL(adam_lazy_rows_kernel<true>, dim3(blocks), dim3(256), 0, s, a, h, nullptr);
   } else {
+    // the step counter advances even when no row carries a gradient (dense semantics)
     hipLaunchKernelGGL(adam_lazy_inc_kernel, dim3(1), dim3(64), 0, s, a, h, d_skip);
     FR_LAUNCH_CHECK();
+    if (rows == 0) return FR_OK;
     hipLaunchKernelGGL(adam_lazy_rows_kernel<false>, dim3(blocks), dim3(256), 0, s, a, h, d_skip);
   }
   FR_LAUNCH_CHECK();
@@ -420,11 +441,14 @@ static int lazy_impl(bool flush, float* const* params, const float* const* grads
 
 extern "C" int fr_adam_step_rows_lazy(float* const* params, const float* const* grads, float* const* exp_avg,
                                       float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
-                                      const int32_t* const* d_rmaps, const int32_t* row_dims, int32_t* const* d_last,
+                                      const int32_t* const* d_rmaps, const int64_t* const* d_ids,
+                                      const int64_t* n_ids, const int32_t* row_dims, int32_t* const* d_last,
                                       float* const* d_hist, int32_t hist_cap, int n_tensors, const double* d_lr,
                                       double lr, double beta1, double beta2, double eps, double weight_decay,
                                       const int32_t* d_skip, void* stream) {
-  return lazy_impl(false, params, grads, exp_avg, exp_avg_sq, d_steps, numel, d_rmaps, row_dims, d_last, d_hist,
+  FR_REQUIRE(d_ids && n_ids, "d_ids and n_ids required");
+  return lazy_impl(false, params, grads, exp_avg, exp_avg_sq, d_steps, numel, d_rmaps, d_ids, n_ids, row_dims,
+                   d_last, d_hist,
                    hist_cap, n_tensors, d_lr, lr, beta1, beta2, eps, weight_decay, d_skip, stream);
 }
 
@@ -432,7 +456,8 @@ extern "C" int fr_adam_flush_rows(float* const* params, float* const* exp_avg, f
                                   int64_t* const* d_steps, const int64_t* numel, const int32_t* row_dims,
                                   int32_t* const* d_last, float* const* d_hist, int32_t hist_cap, int n_tensors,
                                   double beta1, double beta2, double eps, double weight_decay, void* stream) {
-  return lazy_impl(true, params, nullptr, exp_avg, exp_avg_sq, d_steps, numel, nullptr, row_dims, d_last, d_hist,
+  return lazy_impl(true, params, nullptr, exp_avg, exp_avg_sq, d_steps, numel, nullptr, nullptr, nullptr, row_dims,
+                   d_last, d_hist,
                    hist_cap, n_tensors, nullptr, 0.0, beta1, beta2, eps, weight_decay, nullptr, stream);
 }
 

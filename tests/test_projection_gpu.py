@@ -81,7 +81,7 @@ def test_factored_row_gradients_match_dense(cuda):
     assert all(p.grad is None for p in tg) and len(opt.row_grads.factored) == 2
     prepared = opt._prepare_factored(native.lib())
     for t, p in enumerate(tg):
-        tag, rmap, crow = prepared[id(p)]
+        tag, rmap, crow = prepared[id(p)][:3]
         rmap, crow = rmap.cpu().long(), crow.cpu().double()
         dense = torch.zeros(R, Ks[t], dtype=torch.float64)
         has = rmap >= 0

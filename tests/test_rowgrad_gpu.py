@@ -271,3 +271,29 @@ def test_lazy_row_catch_up_before_gather(cuda):
     ob.flush()
     assert torch.equal(pa, pb)
     assert torch.equal(oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])
+
+
+def test_device_feed_stream_bit_exact(cuda):
+    """GraphedStep's DeviceFeed (epoch staged on the device, batches gathered inside the captured
+    step) yields the reference's triple stream: the golden 2-epoch stream of dataloader.py's
+    sampler, full batches via DeviceFeed.fill, the ragged last batch as tensors."""
+    from helpers import golden, tiny_config, tiny_data
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("stream.npz")
+    cfg = tiny_config("LightGCN", False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    get_model("LightGCN")(cfg, data)
+    B = int(g["batch_size"])
+    s = TripleSampler(data, B, cuda)
+    feed = s.device_feed()
+    out = tuple(torch.zeros(B, dtype=torch.int64, device=cuda) for _ in range(3))
+    for ep in range(2):
+        got = []
+        for u, p, n in s.epoch(out=out, feed=feed):
+            if u is out[0]:
+                feed.fill(*out)
+            got.append([x.cpu().numpy().copy() for x in (u, p, n)])
+        for k, key in enumerate("upn"):
+            np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep{ep}/{key}"])
