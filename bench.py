@@ -53,6 +53,8 @@ def _args():
     ap.add_argument("--no-spmm-10m", action="store_true",  # also skips the config-4 training step
                     help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
     ap.add_argument("--config-json", default=None, help="extra config keys for the HealthRec step (JSON)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip BASELINE config 3 (CLUSSL on Foodcom-shape data, dCor and InfoNCE SSL)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip BASELINE config 5 (d=256 bf16 tables, full-sort top-k on MFMA)")
     return ap.parse_args()
@@ -199,6 +201,11 @@ def main():
                           "kernel_pass": f"{ksteps} eager steps, HIP events on the launch stream",
                           "eager_ms_per_step": round(eager_elapsed / ksteps * 1e3, 4)}
 
+    c3 = None
+    if world == 1 and not args.no_config3:
+        del graphed, state
+        c3 = config3(device)
+        graphed = state = None
     c4 = None
     if not args.no_spmm_10m:
         del trainer, model, sampler, state, graphed
@@ -224,7 +231,7 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else "single"},
-                "roofline": roofline, "spmm": spmm, "config4_10m": c4, "config5_10m_bf16": c5, "kernels": kernels,
+                "roofline": roofline, "spmm": spmm, "config3_clussl_foodcom": c3, "config4_10m": c4, "config5_10m_bf16": c5, "kernels": kernels,
                 "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -347,6 +354,79 @@ def config5(device, batches=(512, 8192), steps=3, warmup=2, spmm_iters=5, topk_u
            "byte_model": "SURVEY 8(d) with s=2: 2L*B_spmm + 2(L+1)*N*d*2 + 30*P + B*(3*8+3*d*2)*2"}
     del model, g, adj, tables
     torch.cuda.empty_cache()
+    return out
+
+
+def config3(device, steps=30, warmup=5, ssl_iters=20):
+    """BASELINE config 3 on one GPU: CLUSSL (reference PRICAI_ModelX) on a Foodcom-shaped synthetic
+    dataset (U=7,596, I=29,943, ~192k train pairs, 2,000 image / text k-means clusters, NI=4,963),
+    d=64, B=512: the full graphed training step (3 item-side propagations with n_ri_layers=2, the
+    UI propagation, BPR + EmbLoss, the SSL term, backward, Adam) with the reference's distance-
+    correlation SSL (:263) and with the InfoNCE variant (CL_loss, :354-378), plus the fused SSL
+    kernels alone (forward + backward over the three [2B, 64] views)."""
+    import numpy as np
+    import torch
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import ops
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.models.clussl import _DCOR_PAIRS
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.dataset import FoodData
+    from FoodRec.utils.synthetic import make_synthetic
+    from FoodRec.utils.utils import get_model, init_seed
+    B = 512
+    data = FoodData.from_synthetic(make_synthetic("foodcom", 0, negatives=False))
+    out = {"dataset": "Foodcom-shape synthetic (U=%d, I=%d, train=%d, clusters=2000)"
+                      % (data.n_users, data.n_items, int(data.train_coo_matrix.nnz)),
+           "model": "CLUSSL (PRICAI_ModelX), n_ri_layers=2, n_ui_layers=1, d=64", "batch": B, "steps_timed": steps}
+    for mode in ("dcor", "infonce"):
+        cfg = Config("PRICAI_ModelX", "Foodcom", {"use_gpu": True, "seed": 999, "cuda_graph": True,
+                                                  "train_batch_size": B, "ssl_mode": mode, "n_cluster": 2000,
+                                                  "log_root": "/tmp/frlog/", "ckp_root": "/tmp/frckp/"})
+        cfg["device"] = device
+        init_seed(999)
+        model = get_model("PRICAI_ModelX")(cfg, data).to(device)
+        tr = Trainer(cfg, model)
+        np.random.seed(2000)
+        sampler = TripleSampler(data, B, device, replay_python_random=False)
+        g = tr.graphed_step(B, warmup=3)
+        feed = g.attach_feed(sampler)
+        state = g.state
+        model.train()
+
+        def batches():
+            while True:
+                for t in sampler.epoch(out=g.inputs, feed=feed):
+                    yield t
+
+        it = batches()
+        for i in range(warmup):
+            g(*next(it), i, state)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            g(*next(it), warmup + i, state)
+        tr.flush_optimizer()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        assert not int(state["nan"].item()), "NaN loss in the config-3 step"
+        out[mode] = {"ms_per_step": round(dt * 1e3, 4), "triples_per_s": round(B / dt, 1)}
+        del tr, model, g, sampler, state, it
+        torch.cuda.empty_cache()
+    torch.manual_seed(0)
+    views = [torch.randn(2 * B, 64, device=device, requires_grad=True) for _ in range(3)]
+    for name, fn in (("dcor_fwd_bwd_ms", lambda: ops.dcor_loss(views, _DCOR_PAIRS).backward()),
+                     ("infonce_fwd_bwd_ms", lambda: sum(ops.infonce_loss(torch.cat([views[a], views[b]]), 0.5)
+                                                        for a, b in _DCOR_PAIRS).sum().backward())):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(ssl_iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = round(e0.elapsed_time(e1) / ssl_iters, 4)
     return out
 
 
