@@ -230,6 +230,7 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
 __global__ __launch_bounds__(1024) void dcor_finalize_kernel(int V, int64_t n, PairTab pt,
                                                              DcorWS ws, float* out) {
   __shared__ double red[16];
+  __shared__ double redS[16];
   __shared__ double Sc[MAXP];
   __shared__ double Ab[MAXV];
   const int64_t nt = (n + T - 1) / T;
@@ -259,19 +260,26 @@ __global__ __launch_bounds__(1024) void dcor_finalize_kernel(int V, int64_t n, P
   // centred pair sums
   for (int a = 0; a < V; ++a)
     for (int b = a; b < V; ++b) {
-      double loc = 0.0;
+      const int pi = pair_index(a, b, V);
+      double loc = 0.0, locS = 0.0;
       for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
         loc += ws.mean[(int64_t)a * n + i] * ws.mean[(int64_t)b * n + i];
+      // per-tile pair sums: strided over the block, then a fixed-shape tree (deterministic)
+      for (int64_t blk = threadIdx.x; blk < nt * nt; blk += blockDim.x) locS += ws.S[blk * NP + pi];
       loc = group_sum_d<64>(loc);
+      locS = group_sum_d<64>(locS);
       __syncthreads();
-      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
+      if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = loc;
+        redS[threadIdx.x >> 6] = locS;
+      }
       __syncthreads();
       if (threadIdx.x == 0) {
-        double ab = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) ab += red[w];
-        double S = 0.0;
-        const int pi = pair_index(a, b, V);
-        for (int64_t blk = 0; blk < nt * nt; ++blk) S += ws.S[blk * NP + pi];
+        double ab = 0.0, S = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+          ab += red[w];
+          S += redS[w];
+        }
         const double dn = (double)n;
         Sc[pi] = S - 2.0 * dn * ab + dn * dn * Ab[a] * Ab[b];
       }
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, 
 //            P [JS][2b][d] f32 (bwd), out scratch
 constexpr int NCE_JS = 8;
 
-struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; };
+struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; double* rowsum; };
 
 __host__ __device__ inline NceWS nce_ws(void* base, int64_t m, int d) {
   char* p = reinterpret_cast<char*>(base);
@@ -455,12 +463,14 @@ __host__ __device__ inline NceWS nce_ws(void* base, int64_t m, int d) {
   w.part = reinterpret_cast<float2*>(take((int64_t)NCE_JS * m * 8));
   w.lse = reinterpret_cast<float*>(take(m * 4));
   w.P = reinterpret_cast<float*>(take((int64_t)NCE_JS * m * d * 4));
+  w.rowsum = reinterpret_cast<double*>(take(((m + 3) / 4) * 8));
   return w;
 }
 
 inline int64_t nce_ws_bytes(int64_t m, int d) {
   auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
-  return r(m * d * 4) + r(m * 4) + r((int64_t)NCE_JS * m * 8) + r(m * 4) + r((int64_t)NCE_JS * m * d * 4);
+  return r(m * d * 4) + r(m * 4) + r((int64_t)NCE_JS * m * 8) + r(m * 4) + r((int64_t)NCE_JS * m * d * 4) +
+         r(((m + 3) / 4) * 8);
 }
 
 // F.normalize(p=2, dim=-1): x / max(||x||, 1e-12); one wave per row
@@ -526,13 +536,17 @@ __global__ __launch_bounds__(256) void nce_lse_tiles_kernel(int64_t b, int d, fl
   }
 }
 
-// merge splits -> lse; loss = sum_i (lse_i - l_i,p(i)) / b^2
-__global__ __launch_bounds__(1024) void nce_finalize_kernel(int64_t b, int d, float inv_tau, int js_count,
-                                                            NceWS ws, float* out) {
-  __shared__ double red[16];
+// merge splits -> lse; loss = sum_i (lse_i - l_i,p(i)) / b^2.  One wave per row (lanes over the
+// feature dim for the positive logit), 4 rows per block -> a per-block partial; nce_sum_kernel adds
+// the partials in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, float inv_tau, int js_count,
+                                                           NceWS ws) {
+  __shared__ double red[4];
   const int64_t m = 2 * b;
-  double loc = 0.0;
-  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wv;
+  double v = 0.0;
+  if (i < m) {
     float M = -INFINITY, S = 0.f;
     for (int s = 0; s < js_count; ++s) {
       const float2 p = ws.part[(int64_t)s * m + i];
@@ -541,12 +555,24 @@ __global__ __launch_bounds__(1024) void nce_finalize_kernel(int64_t b, int d, fl
       else S += p.y * expf(p.x - M);
     }
     const float lse = M + logf(S);
-    ws.lse[i] = lse;
     const int64_t j = nce_partner(i, b);
-    float dot = 0.f;
-    for (int k = 0; k < d; ++k) dot = fmaf(ws.Hn[i * d + k], ws.Hn[j * d + k], dot);
-    loc += (double)lse - (double)(dot * inv_tau);
+    double dp = 0.0;
+    for (int k = lane; k < d; k += 64) dp += (double)ws.Hn[i * d + k] * (double)ws.Hn[j * d + k];
+    const float dot = (float)group_sum_d<64>(dp);
+    if (lane == 0) {
+      ws.lse[i] = lse;
+      v = (double)lse - (double)(dot * inv_tau);
+    }
   }
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) ws.rowsum[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int64_t nparts, NceWS ws, float* out) {
+  __shared__ double red[16];
+  double loc = 0.0;
+  for (int64_t k = threadIdx.x; k < nparts; k += blockDim.x) loc += ws.rowsum[k];
   loc = group_sum_d<64>(loc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
   __syncthreads();
@@ -772,7 +798,10 @@ extern "C" int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, flo
   hipLaunchKernelGGL(nce_lse_tiles_kernel, dim3((unsigned)nt, (unsigned)js), dim3(256), lds, s, b, d,
                      inv_tau, w);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nce_finalize_kernel, dim3(1), dim3(1024), 0, s, b, d, inv_tau, js, w, d_out);
+  const int64_t nparts = fr::ceil_div(m, 4);
+  hipLaunchKernelGGL(nce_finalize_kernel, dim3((unsigned)nparts), dim3(256), 0, s, b, d, inv_tau, js, w);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(nce_sum_kernel, dim3(1), dim3(1024), 0, s, b, nparts, w, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
