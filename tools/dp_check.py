@@ -97,6 +97,8 @@ def main():
     # of zero-gradient parameters (the key part of in_proj_bias) into +-lr updates in any mode.
     for k in range(5):
         bu, bp, bn = next(it)
+        tg.flush_optimizer()  # lazy row Adam: every deferred row step applied before comparing/copying
+        te.flush_optimizer()
         with torch.no_grad():  # same parameters in both modes (graphs read parameter memory)
             for a, b in zip(mg.parameters(), me.parameters()):
                 a.copy_(b)
