@@ -46,6 +46,8 @@ class RowGrads:
         # gathered Linear input (ops.modal_projection), materialised by FusedAdam before any update
         self.factored = {}
         self.catch_up = None  # set by a FusedAdam with lazy_rows
+        self._prefetched = set()  # (id(weight), ids pointer, ids numel) caught up by prefetch_rows this step
+        self._side = None
 
     def stash_factored(self, weight, padding_idx, ids, dY, W):
         if id(weight) in self.pending or id(weight) in self.factored:  # repeated backward: explicit rows
@@ -67,12 +69,32 @@ class RowGrads:
     def clear(self):
         self.pending.clear()
         self.factored.clear()
+        self._prefetched.clear()
 
     def catch_up_rows(self, weight, ids):
         """Called before ``weight`` is gathered at ``ids``: a lazily updating optimiser brings those
-        rows up to the current step (FusedAdam.catch_up_rows)."""
-        if self.catch_up is not None:
+        rows up to the current step (FusedAdam.catch_up_rows).  Skipped when ``prefetch_rows``
+        already covered (weight, ids)."""
+        if self.catch_up is not None and (id(weight), ids.data_ptr(), ids.numel()) not in self._prefetched:
             self.catch_up(weight, ids)
+
+    def prefetch_rows(self, pairs):
+        """Catch up [(weight, ids), ...] on a side stream, overlapping whatever the caller runs next
+        (HealthRec: the SpMM propagation, which reads none of these tables).  Returns a callable that
+        makes the current stream wait for it; call it before the gathers.  Graph-capturable (fork /
+        join of the capture stream)."""
+        if self.catch_up is None or not pairs or not pairs[0][0].is_cuda:
+            return lambda: None
+        main = torch.cuda.current_stream(pairs[0][0].device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(pairs[0][0].device)
+        side = self._side
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            for w, ids in pairs:
+                self.catch_up(w, ids)
+                self._prefetched.add((id(w), ids.data_ptr(), ids.numel()))
+        return lambda: main.wait_stream(side)
 
     def __bool__(self):
         return bool(self.pending or self.factored)

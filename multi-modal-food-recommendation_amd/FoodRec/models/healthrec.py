@@ -142,6 +142,12 @@ class HealthRec(GeneralRecommender):
 
     def calculate_loss(self, batch_data):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
+        all_item = _pn(batch_data, "i_id")
+        xg = self.__dict__.get("_fr_exchange")  # row-gradient exchange (FusedAdam / data parallel)
+        # lazily updated image/text rows of this batch: caught up on a side stream (ALU-bound) while
+        # the propagation (memory-bound, other tables) runs
+        join = xg.prefetch_rows([(t.weight, all_item) for t in self._row_tables()]) \
+            if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) else (lambda: None)
         ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
         health_level = _pn(batch_data, "hl_mh")
@@ -156,9 +162,8 @@ class HealthRec(GeneralRecommender):
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
-        all_item = _pn(batch_data, "i_id")
+        join()
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        xg = self.__dict__.get("_fr_exchange")  # data-parallel: rows exchanged, not tables
         if self._fused_projection(all_item):
             # gathers folded into the projection GEMMs; the tables' gradient stays factored (dY, W)
             mm_query = ops.modal_projection(all_item, [(self.image_embedding.weight, self.image_trs),
@@ -205,6 +210,9 @@ class HealthRec(GeneralRecommender):
                 and mm_query.shape[1] == 2 and encoded.shape[1] in ops.ENCODER_LENGTHS
                 and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
                 and a.ln.eps == b.ln.eps)
+
+    def _row_tables(self):
+        return [getattr(self, n) for n in ("image_embedding", "text_embedding") if hasattr(self, n)]
 
     def _fused_projection(self, ids) -> bool:
         """Both modal tables present, fp32 on the GPU, Linear(K -> 64) with K a multiple of 16."""
