@@ -340,6 +340,14 @@ int fr_adam_catch_up_rows(float* param, float* exp_avg, float* exp_avg_sq, const
                           const float* d_hist, int32_t hist_cap, double beta1, double beta2, double eps,
                           double weight_decay, void* stream);
 
+/* fr_adam_catch_up_rows for up to 4 tables gathered at the same ids (HealthRec's image and text
+ * tables at the batch's items), one launch (grid.y = table). */
+int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, float* const* exp_avg,
+                                float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
+                                const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
+                                const int64_t* d_ids, int64_t n, int32_t hist_cap, double beta1, double beta2,
+                                double eps, double weight_decay, void* stream);
+
 /* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
  * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as
  * fr_adam_step) and the bf16 parameter is re-rounded from the master.  d_step: device int64

@@ -91,8 +91,14 @@ class RowGrads:
         side = self._side
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            multi = getattr(self.catch_up, "__self__", None)
+            same_ids = all(ids is pairs[0][1] for _, ids in pairs)
+            if multi is not None and same_ids and len(pairs) <= 4:
+                multi.catch_up_rows_multi([w for w, _ in pairs], pairs[0][1])
+            else:
+                for w, ids in pairs:
+                    self.catch_up(w, ids)
             for w, ids in pairs:
-                self.catch_up(w, ids)
                 self._prefetched.add((id(w), ids.data_ptr(), ids.numel()))
         return lambda: main.wait_stream(side)
 
@@ -134,6 +140,35 @@ class FusedAdam(torch.optim.Optimizer):
         self._lazy_launched = False
         if self.lazy_rows:
             self.row_grads.catch_up = self.catch_up_rows
+
+    @torch.no_grad()
+    def catch_up_rows_multi(self, ps, ids):
+        """catch_up_rows for several tables gathered at the same ids, one launch
+        (fr_adam_catch_up_rows_multi).  Tables without lazy state are skipped."""
+        ps = [p for p in ps if "lazy_last" in self.state.get(p, {})]
+        if not ps:
+            return
+        groups = {id(p): g for g in self.param_groups for p in g["params"]}
+        g0 = groups[id(ps[0])]
+        if any(groups[id(p)] is not g0 for p in ps):  # differing hyper-parameters: one launch per table
+            for p in ps:
+                self.catch_up_rows(p, ids)
+            return
+        beta1, beta2 = g0["betas"]
+        ids = ids.reshape(-1)
+        if ids.dtype != torch.int64:
+            ids = ids.to(torch.int64)
+        n = len(ps)
+        st = [self.state[p] for p in ps]
+        arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+        with profiling.region("adam_rows_catch_up", sum(28 * ids.numel() * p.shape[1] for p in ps) + 8 * ids.numel()):
+            native.check(native.lib().fr_adam_catch_up_rows_multi(
+                n, arr(ps), arr([s_["exp_avg"] for s_ in st]), arr([s_["exp_avg_sq"] for s_ in st]),
+                arr([s_["step"] for s_ in st]), (ctypes.c_int64 * n)(*[p.shape[0] for p in ps]),
+                (ctypes.c_int32 * n)(*[p.shape[1] for p in ps]), arr([s_["lazy_last"] for s_ in st]),
+                arr([s_["lazy_hist"] for s_ in st]), ids.data_ptr(), ids.numel(), self.hist_cap, float(beta1),
+                float(beta2), float(g0["eps"]), float(g0["weight_decay"]), native.stream_of(ps[0])),
+                "fr_adam_catch_up_rows_multi")
 
     @torch.no_grad()
     def catch_up_rows(self, p, ids):

@@ -325,14 +325,47 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyp
 // Catch-up before a gather: the rows a step is about to read (ids, duplicates allowed) replay their
 // deferred zero-gradient steps through the current step, so the forward sees dense-Adam values.
 // One wave per id; the wave whose atomicMax raises last[r] does the row, duplicates skip.
+constexpr int kMaxCatch = 4;
+struct CatchArgs {
+  float* p[kMaxCatch];
+  float* m[kMaxCatch];
+  float* v[kMaxCatch];
+  const int64_t* step[kMaxCatch];
+  int32_t* last[kMaxCatch];
+  const float* hist[kMaxCatch];
+  int64_t rows[kMaxCatch];
+  int32_t rshift[kMaxCatch];
+};
+
+__device__ __forceinline__ void catch_up_row(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
+                                             const int64_t* step, const int64_t* __restrict__ ids, int64_t i,
+                                             int64_t R, int rshift, int32_t* last, const float* __restrict__ hist,
+                                             int cap, const AdamHyper& h);
+
+// blockIdx.y = table: every table of the call catches up the same ids in one launch
+__global__ __launch_bounds__(256) void adam_catch_up_multi_kernel(CatchArgs a, const int64_t* __restrict__ ids,
+                                                                  int64_t n, int cap, AdamHyper h) {
+  const int t = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  catch_up_row(a.p[t], a.m[t], a.v[t], a.step[t], ids, i, a.rows[t], a.rshift[t], a.last[t], a.hist[t], cap, h);
+}
+
 __global__ __launch_bounds__(256) void adam_catch_up_kernel(float* __restrict__ P0, float* __restrict__ M0,
                                                             float* __restrict__ V0, const int64_t* step,
                                                             const int64_t* __restrict__ ids, int64_t n, int64_t R,
                                                             int rshift, int32_t* last, const float* __restrict__ hist,
                                                             int cap, AdamHyper h) {
-  const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
+  catch_up_row(P0, M0, V0, step, ids, i, R, rshift, last, hist, cap, h);
+}
+
+__device__ __forceinline__ void catch_up_row(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
+                                             const int64_t* step, const int64_t* __restrict__ ids, int64_t i,
+                                             int64_t R, int rshift, int32_t* last, const float* __restrict__ hist,
+                                             int cap, const AdamHyper& h) {
+  const int lane = threadIdx.x & 63;
   const int64_t r = ids[i];
   if (r < 0 || r >= R) return;
   const int64_t st = step[0];
@@ -632,6 +665,51 @@ extern "C" int fr_adam_catch_up_rows(float* param, float* exp_avg, float* exp_av
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(adam_catch_up_kernel, dim3((unsigned)fr::ceil_div(n, 4)), dim3(256), 0, s, param, exp_avg,
                      exp_avg_sq, d_step, d_ids, n, rows, rshift, d_last, d_hist, hist_cap, h);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, float* const* exp_avg,
+                                           float* const* exp_avg_sq, const int64_t* const* d_steps,
+                                           const int64_t* rows, const int32_t* row_dims, int32_t* const* d_last,
+                                           const float* const* d_hist, const int64_t* d_ids, int64_t n,
+                                           int32_t hist_cap, double beta1, double beta2, double eps,
+                                           double weight_decay, void* stream) {
+  FR_REQUIRE(n_tables >= 0 && n_tables <= kMaxCatch, "n_tables out of range [0, 4]");
+  FR_REQUIRE(n >= 0, "negative size");
+  if (n == 0 || n_tables == 0) return FR_OK;
+  FR_REQUIRE(params && exp_avg && exp_avg_sq && d_steps && rows && row_dims && d_last && d_hist && d_ids,
+             "null pointer");
+  FR_REQUIRE(hist_cap >= 2, "hist_cap < 2");
+  CatchArgs a{};
+  for (int t = 0; t < n_tables; ++t) {
+    FR_REQUIRE(params[t] && exp_avg[t] && exp_avg_sq[t] && d_steps[t] && d_last[t] && d_hist[t], "null tensor");
+    FR_REQUIRE(row_dims[t] >= 4 && (row_dims[t] & (row_dims[t] - 1)) == 0, "row width must be a power of two >= 4");
+    FR_REQUIRE(fr::aligned16(params[t]) && fr::aligned16(exp_avg[t]) && fr::aligned16(exp_avg_sq[t]),
+               "16-byte alignment");
+    FR_REQUIRE(rows[t] >= 0 && rows[t] < INT32_MAX, "rows out of range");
+    a.p[t] = params[t];
+    a.m[t] = exp_avg[t];
+    a.v[t] = exp_avg_sq[t];
+    a.step[t] = d_steps[t];
+    a.last[t] = d_last[t];
+    a.hist[t] = d_hist[t];
+    a.rows[t] = rows[t];
+    int sh = 0;
+    while ((1 << sh) < row_dims[t]) ++sh;
+    a.rshift[t] = sh;
+  }
+  AdamHyper h{};
+  h.beta1_d = beta1;
+  h.beta2_d = beta2;
+  h.w1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.one_m_b2 = (float)(1.0 - beta2);
+  h.eps = (float)eps;
+  h.wd = (float)weight_decay;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_catch_up_multi_kernel, dim3((unsigned)fr::ceil_div(n, 4), (unsigned)n_tables), dim3(256), 0,
+                     s, a, d_ids, n, hist_cap, h);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

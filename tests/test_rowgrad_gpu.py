@@ -297,3 +297,35 @@ def test_device_feed_stream_bit_exact(cuda):
             got.append([x.cpu().numpy().copy() for x in (u, p, n)])
         for k, key in enumerate("upn"):
             np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep{ep}/{key}"])
+
+
+def test_lazy_row_prefetch_multi(cuda):
+    """RowGrads.prefetch_rows (side stream, both tables in one fr_adam_catch_up_rows_multi launch)
+    catches the rows up exactly like per-table catch-up; the later per-table call is skipped."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(5)
+    shapes = [(300, 256), (300, 64)]
+    w0 = [torch.randn(R, d) for R, d in shapes]
+    pa = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    pb = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    oa = FusedAdam(pa, lr=4e-3)
+    ob = FusedAdam(pb, lr=4e-3, lazy_rows=True)
+    for k in range(7):
+        for o, ps in ((oa, pa), (ob, pb)):
+            o.zero_grad()
+            for t, ((R, d), p) in enumerate(zip(shapes, ps)):
+                ids, G = _case(R, d, 40, None, 1000 + 10 * k + t)
+                ids = torch.arange(R) if k == 0 else ids % 30
+                G = torch.randn(R, d, generator=torch.Generator().manual_seed(k)) if k == 0 else G
+                o.row_grads.stash(p, None, ids.to(cuda), G.to(cuda))
+            o.step()
+    ob.zero_grad()
+    read = torch.tensor([5, 250, 250, 77, 3, 299], dtype=torch.int64, device=cuda)
+    join = ob.row_grads.prefetch_rows([(p, read) for p in pb])
+    join()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a[read], b[read])
+    assert (id(pb[0]), read.data_ptr(), read.numel()) in ob.row_grads._prefetched
+    ob.flush()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
