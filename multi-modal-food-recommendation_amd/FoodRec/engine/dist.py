@@ -57,11 +57,6 @@ class RowExchange:
         if self.sink is not None:
             self.sink.catch_up_rows(weight, ids)
 
-    def prefetch_rows(self, pairs):
-        if self.sink is None:
-            return lambda: None
-        return self.sink.prefetch_rows(pairs)
-
     def stash(self, weight, padding_idx, ids, G, W=None):
         ids = ids.to(torch.int64)
         G = G.to(torch.float32)

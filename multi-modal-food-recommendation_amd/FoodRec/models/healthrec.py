@@ -145,7 +145,9 @@ class HealthRec(GeneralRecommender):
         all_item = _pn(batch_data, "i_id")
         xg = self.__dict__.get("_fr_exchange")  # row-gradient exchange (FusedAdam / data parallel)
         # lazily updated image/text rows of this batch: caught up on a side stream (ALU-bound) while
-        # the propagation (memory-bound, other tables) runs
+        # the propagation (memory-bound, other tables) runs.  Single process only: a data-parallel
+        # RowExchange has no prefetch_rows (a forked capture stream inside the DP graphs slowed the
+        # 2-rank rehearsal 16 -> 73 ms/step), its rows are caught up inline before the gather
         join = xg.prefetch_rows([(t.weight, all_item) for t in self._row_tables()]) \
             if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) else (lambda: None)
         ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
