@@ -32,6 +32,14 @@ class AbstractRecommender(nn.Module):
 
 
 class GeneralRecommender(AbstractRecommender):
+    def state_dict(self, *args, **kwargs):
+        """The training engine may hold deferred parameter updates (FusedAdam lazy rows): a trainer
+        registers its flush here so a checkpoint always holds the dense-Adam values."""
+        flush = self.__dict__.get("_fr_flush")
+        if flush is not None:
+            flush()
+        return super().state_dict(*args, **kwargs)
+
     def __init__(self, config, dataset):
         super().__init__()
         self.n_users = dataset.n_users

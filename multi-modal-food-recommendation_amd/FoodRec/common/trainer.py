@@ -340,6 +340,8 @@ class Trainer(AbstractTrainer):
         if self._on_gpu():
             self.swapped_adjacencies = swap_sparse_attributes(model)
         self.optimizer = self._build_optimizer()
+        if isinstance(self.optimizer, FusedAdam) and self.optimizer.lazy_rows:
+            model.__dict__["_fr_flush"] = self.optimizer.flush  # model.state_dict() applies deferred rows
         sched = config["learning_rate_scheduler"] or [1.0, 50]
         self.lr_scheduler = optim.lr_scheduler.LambdaLR(self.optimizer,
                                                         lr_lambda=lambda e: sched[0] ** (e / sched[1]))

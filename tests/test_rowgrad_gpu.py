@@ -329,3 +329,34 @@ def test_lazy_row_prefetch_multi(cuda):
     ob.flush()
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
+
+
+def test_healthrec_lazy_state_dict_flushes(cuda):
+    """The trainer registers its optimiser's flush on the model: model.state_dict() (a checkpoint)
+    holds the dense-Adam values of a lazily updated table, not the deferred ones."""
+    from helpers import tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    cfg = tiny_config("CIKM_Model", True, cuda_graph=False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
+    tr = Trainer(cfg, model)
+    opt = tr.optimizer
+    assert opt.lazy_rows
+    w = model.image_embedding.weight
+    R, d = w.shape
+    ref = torch.nn.Parameter(w.detach().clone())
+    from FoodRec.engine.optim import FusedAdam
+    oref = FusedAdam([ref], lr=opt.param_groups[0]["lr"])
+    for k in range(4):  # first step touches every row, later ones alternate between two row sets
+        ids = torch.arange(R, device=cuda) if k == 0 else torch.arange(k % 2, R, 2, device=cuda)
+        G = torch.randn(ids.numel(), d, device=cuda)
+        for o, p in ((opt, w), (oref, ref)):
+            o.zero_grad()
+            o.row_grads.stash(p, None, ids, G)
+            o.step()
+    raw = w.detach().clone()
+    assert not torch.equal(raw, ref)  # deferred steps pending
+    sd = model.state_dict()
+    assert torch.equal(sd["image_embedding.weight"], ref)
