@@ -32,6 +32,7 @@ import torch
 import torch.optim as optim
 from torch.nn.utils.clip_grad import clip_grad_norm_
 
+from FoodRec.engine import ops
 from FoodRec.engine.graph import swap_sparse_attributes
 from FoodRec.engine.optim import FusedAdam
 from FoodRec.engine.sampler import BatchFeatures, EvalBatch, TripleSampler
@@ -337,6 +338,7 @@ class Trainer(AbstractTrainer):
         self.best_test_upon_valid = tmp
         self.train_loss_dict = {}
         self.swapped_adjacencies = []
+        ops.set_deterministic(bool(config["deterministic"]))  # reproducible scatters (engine-wide)
         if self._on_gpu():
             self.swapped_adjacencies = swap_sparse_attributes(model)
         self.optimizer = self._build_optimizer()
@@ -361,7 +363,9 @@ class Trainer(AbstractTrainer):
         # capture the training step in a HIP graph (config key cuda_graph; GPU, single process)
         # host-side batch work (SCHGN's masked-ingredient SSL draws Python's random per batch) cannot
         # be captured: those configurations step eagerly
-        self.use_graph = bool(config["cuda_graph"]) and self._on_gpu() and not config["SCHGN_ssl"]
+        # (and only the fused Adam reads the NaN flag on the device: other optimisers step eagerly)
+        self.use_graph = (bool(config["cuda_graph"]) and self._on_gpu() and not config["SCHGN_ssl"]
+                          and isinstance(self.optimizer, FusedAdam))
         self._graphed = None
 
     @property
@@ -405,8 +409,10 @@ class Trainer(AbstractTrainer):
 
     def _opt_step(self, skip_flag):
         if isinstance(self.optimizer, FusedAdam):
-            self.optimizer.step(skip_flag=skip_flag)
-        else:
+            self.optimizer.step(skip_flag=skip_flag)  # the kernels read the NaN flag on the device
+        elif not int(skip_flag.item()):
+            # other optimisers: the reference returns before optimizer.step() at the first NaN batch
+            # (trainer.py:191-193), so the flag is read on the host before stepping
             self.optimizer.step()
 
     def train_step(self, interaction, batch_idx, state, loss_func=None, accumulate=True):

@@ -285,13 +285,25 @@ class _BprEmb(torch.autograd.Function):
         return dU, dI, dUe, dIe, None, None, None, None, None, None, None
 
 
+_DETERMINISTIC = False
+
+
+def set_deterministic(on: bool) -> None:
+    """Engine-wide run-to-run reproducible scatters (config key ``deterministic``, set by the
+    Trainer): the BPR backward scatters by owner slots instead of float atomics.  Combine with
+    ``torch.use_deterministic_algorithms(True)`` for PyTorch's own index_add_ / index_put_."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+
+
 def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False,
                  item_rows: bool = False, item_offset: int | None = None):
     """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused; with
     ``item_rows`` also the gathered [I[pos]; I[neg]] rows, whose gradient is added inside the fused
     backward's scatter (no separate gather backward).  ``item_offset`` (with I None): the item table
     is U[item_offset:] -- one [users + items] gradient buffer instead of two plus a concatenation."""
-    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic, item_rows, item_offset)
+    return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic or _DETERMINISTIC, item_rows,
+                         item_offset)
 
 
 # ----------------------------------------------------------------------------- embedding

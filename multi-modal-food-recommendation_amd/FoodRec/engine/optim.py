@@ -46,7 +46,10 @@ class RowGrads:
         # gathered Linear input (ops.modal_projection), materialised by FusedAdam before any update
         self.factored = {}
         self.catch_up = None  # set by a FusedAdam with lazy_rows
-        self._prefetched = set()  # (id(weight), ids pointer, ids numel) caught up by prefetch_rows this step
+        # (weight, ids) pairs caught up by prefetch_rows this step.  The ids tensors are held here, so
+        # their memory cannot be handed to another tensor by the caching allocator before clear():
+        # a (weight, pointer, numel) match below therefore names the same ids
+        self._prefetched = []
         self._side = None
 
     def stash_factored(self, weight, padding_idx, ids, dY, W):
@@ -75,7 +78,9 @@ class RowGrads:
         """Called before ``weight`` is gathered at ``ids``: a lazily updating optimiser brings those
         rows up to the current step (FusedAdam.catch_up_rows).  Skipped when ``prefetch_rows``
         already covered (weight, ids)."""
-        if self.catch_up is not None and (id(weight), ids.data_ptr(), ids.numel()) not in self._prefetched:
+        if self.catch_up is not None and not any(
+                w is weight and (i is ids or (i.data_ptr() == ids.data_ptr() and i.numel() == ids.numel()
+                                              and i.dtype == ids.dtype)) for w, i in self._prefetched):
             self.catch_up(weight, ids)
 
     def prefetch_rows(self, pairs):
@@ -98,8 +103,7 @@ class RowGrads:
             else:
                 for w, ids in pairs:
                     self.catch_up(w, ids)
-            for w, ids in pairs:
-                self._prefetched.add((id(w), ids.data_ptr(), ids.numel()))
+            self._prefetched.extend(pairs)
         return lambda: main.wait_stream(side)
 
     def __bool__(self):
@@ -196,26 +200,54 @@ class FusedAdam(torch.optim.Optimizer):
         pending."""
         if self._lazy_pending == 0:
             return
-        lib = native.lib()
         for group in self.param_groups:
-            ps = [p for p in group["params"] if "lazy_last" in self.state.get(p, {})]
-            if not ps:
-                continue
-            beta1, beta2 = group["betas"]
-            for k in range(0, len(ps), 16):
-                chunk = ps[k:k + 16]
-                n = len(chunk)
-                st = [self.state[p] for p in chunk]
-                arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
-                with profiling.region("adam_rows_flush", sum(24 * p.numel() + 4 * p.shape[0] for p in chunk)):
-                    native.check(lib.fr_adam_flush_rows(
-                        arr(chunk), arr([s["exp_avg"] for s in st]), arr([s["exp_avg_sq"] for s in st]),
-                        arr([s["step"] for s in st]), (ctypes.c_int64 * n)(*[p.numel() for p in chunk]),
-                        (ctypes.c_int32 * n)(*[p.shape[1] for p in chunk]), arr([s["lazy_last"] for s in st]),
-                        arr([s["lazy_hist"] for s in st]), self.hist_cap, n, float(beta1), float(beta2),
-                        float(group["eps"]), float(group["weight_decay"]),
-                        torch.cuda.current_stream(chunk[0].device).cuda_stream), "fr_adam_flush_rows")
+            self._flush_tables(group, [p for p in group["params"] if "lazy_last" in self.state.get(p, {})])
         self._lazy_pending = 0
+
+    def _flush_tables(self, group, ps):
+        """fr_adam_flush_rows over ``ps`` (tables of ``group`` with lazy state), unconditionally."""
+        if not ps:
+            return
+        lib = native.lib()
+        beta1, beta2 = group["betas"]
+        for k in range(0, len(ps), 16):
+            chunk = ps[k:k + 16]
+            n = len(chunk)
+            st = [self.state[p] for p in chunk]
+            arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+            with profiling.region("adam_rows_flush", sum(24 * p.numel() + 4 * p.shape[0] for p in chunk)):
+                native.check(lib.fr_adam_flush_rows(
+                    arr(chunk), arr([s["exp_avg"] for s in st]), arr([s["exp_avg_sq"] for s in st]),
+                    arr([s["step"] for s in st]), (ctypes.c_int64 * n)(*[p.numel() for p in chunk]),
+                    (ctypes.c_int32 * n)(*[p.shape[1] for p in chunk]), arr([s["lazy_last"] for s in st]),
+                    arr([s["lazy_hist"] for s in st]), self.hist_cap, n, float(beta1), float(beta2),
+                    float(group["eps"]), float(group["weight_decay"]),
+                    torch.cuda.current_stream(chunk[0].device).cuda_stream), "fr_adam_flush_rows")
+
+    def load_state_dict(self, state_dict):
+        """torch's loader casts every non-``step`` state tensor to the parameter's dtype and leaves
+        ``step`` where the file put it.  The per-row lazy bookkeeping is dropped (``state_dict()``
+        flushed it: every row was current), moments and bf16 masters are kept in fp32 and ``step``
+        becomes the device int64 counter the kernels read."""
+        slim = {"param_groups": state_dict["param_groups"], "state": {}}
+        keep = {}
+        for k, st in state_dict["state"].items():
+            slim["state"][k] = {n: v for n, v in st.items() if n not in ("lazy_last", "lazy_hist")}
+            keep[k] = {n: v for n, v in st.items()
+                       if n in ("exp_avg", "exp_avg_sq", "master") and torch.is_tensor(v)}
+        super().load_state_dict(slim)
+        for g_sd, group in zip(state_dict["param_groups"], self.param_groups):
+            for idx, p in zip(g_sd["params"], group["params"]):
+                st = self.state.get(p)
+                if not st:
+                    continue
+                if "step" in st:
+                    st["step"] = torch.as_tensor(st["step"]).to(device=p.device, dtype=torch.int64).reshape(())
+                for n, v in keep.get(idx, {}).items():
+                    st[n] = v.to(device=p.device, dtype=torch.float32).contiguous()
+        self._d_lr.clear()
+        self._lazy_pending = 0
+        self._lazy_launched = False
 
     def note_replay(self):
         """A captured step containing a lazy row update was replayed: count it, and flush before
@@ -337,11 +369,18 @@ class FusedAdam(torch.optim.Optimizer):
             d_lr = self._lr_tensor(gi, group, dev)
             hyper = (d_lr.data_ptr(), float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
                      float(group["weight_decay"]), native.ptr(skip_flag), torch.cuda.current_stream(dev).cuda_stream)
-            if plist and self._lazy_pending and any("lazy_last" in self.state[p] for p in plist):
-                self.flush()  # a lazily updated table takes a dense step: bring it up to date first
+            lazy_dense = [p for p in plist if "lazy_last" in self.state[p]]
+            # a lazily updated table taking a dense step (a dense .grad: more ids than the row path
+            # takes, a gradient hook, clipping): its deferred steps are replayed first and its rows
+            # are marked current through the new step afterwards, so no later replay reads a history
+            # slot this step never wrote
+            self._flush_tables(group, lazy_dense)
             if plist:
                 with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
                     self._launch_dense(lib, plist, hyper)
+            for p in lazy_dense:
+                st = self.state[p]
+                st["lazy_last"].copy_(st["step"].to(torch.int32).expand(p.shape[0]))
             if rows:
                 self._launch_rows(lib, rows, hyper)
         return loss
@@ -427,23 +466,31 @@ class FusedAdam(torch.optim.Optimizer):
         n = len(plist)
         RM = (ctypes.c_void_p * n)(*[m.data_ptr() for m in maps])
         RD = (ctypes.c_int32 * n)(*dims)
-        if self.lazy_rows and n <= 16:
+        if self.lazy_rows:
             for p in plist:
                 st = self.state[p]
                 if "lazy_last" not in st:
                     # every row is current through the table's present step (0, or the dense steps so far)
                     st["lazy_last"] = st["step"].to(torch.int32).expand(p.shape[0]).contiguous()
                     st["lazy_hist"] = torch.zeros(self.hist_cap, 2, dtype=torch.float32, device=p.device)
-            LA = (ctypes.c_void_p * n)(*[self.state[p]["lazy_last"].data_ptr() for p in plist])
-            LH = (ctypes.c_void_p * n)(*[self.state[p]["lazy_hist"].data_ptr() for p in plist])
             idl = [i if i.is_contiguous() else i.contiguous() for i in idl]
-            ID = (ctypes.c_void_p * n)(*[i.data_ptr() for i in idl])
-            NI = (ctypes.c_int64 * n)(*[i.numel() for i in idl])
-            # algorithmic bytes: p, m, v of the touched rows (bounded by the compact rows' count) read
-            # and written, the compact gradient rows read, the ids / map / last-step entries
-            with profiling.region("adam_rows", sum(28 * c.numel() + 16 * i.numel() for c, i in zip(compact, idl))):
-                native.check(lib.fr_adam_step_rows_lazy(P, G, M, V, S, N, RM, ID, NI, RD, LA, LH, self.hist_cap, n,
-                                                        *hyper), "fr_adam_step_rows_lazy")
+            for k in range(0, n, 16):  # the kernel's argument block takes 16 tables per launch
+                m = min(16, n - k)
+                sl = slice(k, k + m)
+                arr = lambda xs: (ctypes.c_void_p * m)(*[x.data_ptr() for x in xs])  # noqa: E731
+                sts = [self.state[p] for p in plist[sl]]
+                LA, LH = arr([s_["lazy_last"] for s_ in sts]), arr([s_["lazy_hist"] for s_ in sts])
+                ID = arr(idl[sl])
+                NI = (ctypes.c_int64 * m)(*[i.numel() for i in idl[sl]])
+                # algorithmic bytes: p, m, v of the touched rows (bounded by the compact rows' count)
+                # read and written, the compact gradient rows read, the ids / map / last-step entries
+                with profiling.region("adam_rows", sum(28 * c.numel() + 16 * i.numel()
+                                                       for c, i in zip(compact[sl], idl[sl]))):
+                    native.check(lib.fr_adam_step_rows_lazy(
+                        arr(plist[sl]), arr(compact[sl]), arr([s_["exp_avg"] for s_ in sts]),
+                        arr([s_["exp_avg_sq"] for s_ in sts]), arr([s_["step"] for s_ in sts]),
+                        (ctypes.c_int64 * m)(*[p.numel() for p in plist[sl]]), arr(maps[sl]), ID, NI,
+                        (ctypes.c_int32 * m)(*dims[sl]), LA, LH, self.hist_cap, m, *hyper), "fr_adam_step_rows_lazy")
             self._lazy_launched = True
             if not torch.cuda.is_current_stream_capturing():
                 self._lazy_pending += 1

@@ -283,7 +283,7 @@ class LazyBatch(dict):
             return True
         if key not in self._LAZY:
             return False
-        if key in ("pos_hl_mh", "neg_hl_mh"):
+        if key in ("pos_hl_mh", "neg_hl_mh", "pn_hl_mh"):
             return self._f.health is not None
         if key in ("pos_cl", "neg_cl"):
             return self._f.cal is not None
@@ -294,6 +294,14 @@ class LazyBatch(dict):
 
     def items(self):
         return [(k, self[k]) for k in self.keys()]
+
+    def __copy__(self):
+        """The trainer's ``second_inter`` (trainer.py:181, for --mg): the same tensors, lazy keys
+        still lazy (the reference deep-copies; nothing here mutates a batch tensor in place)."""
+        out = LazyBatch.__new__(LazyBatch)
+        dict.update(out, dict.items(self))
+        out._f = self._f
+        return out
 
 
 class EvalBatch(dict):

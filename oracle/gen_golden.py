@@ -13,6 +13,18 @@ Fixtures (all on the seeded synthetic 'tiny' dataset of FoodRec/utils/synthetic.
   train_<M>.npz     per-epoch loss trace + final valid/test metrics of Trainer.fit
   ops.npz           correlation_distance / CL_loss / BPRLoss / EmbLoss values + grads
   metrics.npz       metrics_by_user / get_auc_fast on fixed rankings
+  train_mg_LightGCN.npz  the same, trained by the reference's mirror-gradient trainer (--mg,
+                    trainer.py:195-212; mg.yaml resolved to alpha1=1, alpha2=0.1, beta=3)
+
+Fixtures at BASELINE widths (seeded synthetic data at the Allrecipes / Foodcom shapes, written in
+the reference's format and read by the reference's own loader; only small slices are stored):
+  wide_CIKM_Model_allrecipes.npz   HealthRec (p=0): first K training steps of Trainer.fit's stream
+  wide_PRICAI_ModelX_foodcom.npz   CLUSSL, 2,000 clusters: first K training steps
+    per step: the batch ids and every loss component; step 0: every gradient of the small
+    parameters, sampled rows of the large ones; init and after K Adam steps: sampled parameter rows
+
+Re-generate a subset:  python oracle/gen_golden.py --only train=CIKM_Model,mg,wide
+(sections: model, stream, train[=M1+M2], mg, ops, metrics, wide[=M1+M2])
 """
 from __future__ import annotations
 
@@ -35,6 +47,9 @@ EPOCHS = 3
 def _setup_reference():
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
     sys.dont_write_bytecode = True
+    # torch imports torch._dynamo lazily (first optimiser construction) and walks sys.modules with
+    # inspect, which cannot place the reference's namespace package 'FoodRec': import it up front
+    import torch._dynamo  # noqa: F401
     # our synthetic generator is imported BEFORE the reference takes the 'FoodRec' name
     from FoodRec.utils.synthetic import make_synthetic, write_reference_format
     for k in [k for k in sys.modules if k == "FoodRec" or k.startswith("FoodRec.")]:
@@ -57,7 +72,19 @@ def dataset_digest(ds) -> str:
     return h.hexdigest()
 
 
-def main():
+def _sections(argv):
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="model,stream,train,mg,ops,metrics,wide")
+    want = {}
+    for item in ap.parse_args(argv).only.split(","):
+        name, _, arg = item.partition("=")
+        want[name.strip()] = [a for a in arg.split("+") if a] or None
+    return want
+
+
+def main(argv=None):
+    want = _sections(argv)
     make_synthetic, write_reference_format = _setup_reference()
     import torch
     from FoodRec.utils.configurator import Config
@@ -80,13 +107,14 @@ def main():
             "use_gpu": False, "seed": [999], "epochs": EPOCHS, "eval_step": 1, "n_cluster": [12],
             "neg_sample_num": 30}
 
-    def make_config(model, extra=None):
-        cd = dict(base)
+    def make_config(model, extra=None, mg=False, root=None, dsname="Tiny", over_base=None):
+        cd = dict(base if over_base is None else over_base)
         cd.update(extra or {})
-        cfg = Config(model, "Tiny", cd)
-        cfg["interaction_data_path"] = tmp + "/Tiny/processed_dataset/"
-        cfg["graph_data_path"] = tmp + "/Tiny/processed_dataset/graph_edge/"
-        cfg["ingre_data_path"] = tmp + "/Tiny/processed_dataset/"
+        cfg = Config(model, dsname, cd, mg)
+        root = root or tmp + "/Tiny/processed_dataset/"
+        cfg["interaction_data_path"] = root
+        cfg["graph_data_path"] = root + "graph_edge/"
+        cfg["ingre_data_path"] = root
         # hyper-parameter lists resolved as quick_start.py:57-66 would for a single combo
         for k in cfg["hyper_parameters"]:
             if isinstance(cfg[k], list):
@@ -101,7 +129,7 @@ def main():
     }
 
     # ---------------------------------------------------------------- model-level goldens
-    for name, extra in models.items():
+    for name, extra in (models.items() if "model" in want else ()):
         cfg = make_config(name, extra)
         data = FoodData(cfg)
         init_seed(cfg["seed"])
@@ -146,6 +174,29 @@ def main():
         print("model", name, out["loss"])
 
     # ---------------------------------------------------------------- sampler stream
+    if "stream" in want:
+        stream_golden(make_config, FoodData, init_seed, get_model, TrainDataLoader, DataLoader, RandomSampler)
+    # ---------------------------------------------------------------- end-to-end training
+    for name in (want["train"] or ("LightGCN", "BPRMF", "PRICAI_ModelX", "CIKM_Model")) if "train" in want else ():
+        train_golden(f"train_{name}.npz", make_config(name, models[name]), name, FoodData, init_seed, get_model,
+                     Trainer)
+    if "mg" in want:
+        # the reference's --mg cascade (configurator.py:64-86 adds configs/mg.yaml; quick_start.py:54-88
+        # takes the first value of each hyper-parameter list) and Trainer(config, model, mg=True)
+        train_golden("train_mg_LightGCN.npz", make_config("LightGCN", models["LightGCN"], mg=True), "LightGCN",
+                     FoodData, init_seed, get_model, Trainer, mg=True)
+    if "wide" in want:
+        for name in want["wide"] or ("CIKM_Model", "PRICAI_ModelX"):
+            wide_golden(name, make_synthetic, write_reference_format, make_config, FoodData, init_seed, get_model,
+                        Trainer, TrainDataLoader, DataLoader, RandomSampler)
+    if "ops" in want:
+        ops_golden()
+    if "metrics" in want:
+        metrics_golden(metrics_by_user, get_auc_fast)
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+def stream_golden(make_config, FoodData, init_seed, get_model, TrainDataLoader, DataLoader, RandomSampler):
     cfg = make_config("LightGCN")
     data = FoodData(cfg)
     init_seed(cfg["seed"])
@@ -166,22 +217,140 @@ def main():
     np.savez_compressed(os.path.join(OUT, "stream.npz"), **st)
     print("stream", st["ep0/u"][:8], st["ep0/n"][:8])
 
-    # ---------------------------------------------------------------- end-to-end training
-    for name in ("LightGCN", "BPRMF", "PRICAI_ModelX"):
-        cfg = make_config(name, models[name])
-        data = FoodData(cfg)
-        init_seed(cfg["seed"])
-        model = get_model(name)(cfg, data)
-        tr = Trainer(cfg, model)
-        bv, bvr, btr = tr.fit(data, hyper_tuple=(999,), saved=True, verbose=False)
-        out = {"train_loss": np.array([tr.train_loss_dict[e] for e in sorted(tr.train_loss_dict)]),
-               "valid_keys": np.array(list(bvr.keys())), "valid": np.array(list(bvr.values())),
-               "test_keys": np.array(list(btr.keys())), "test": np.array(list(btr.values())),
-               "best_valid_score": np.array(bv)}
-        np.savez_compressed(os.path.join(OUT, f"train_{name}.npz"), **out)
-        print("train", name, out["train_loss"], btr)
 
-    # ---------------------------------------------------------------- op-level goldens
+
+def train_golden(fname, cfg, name, FoodData, init_seed, get_model, Trainer, mg=False):
+    data = FoodData(cfg)
+    init_seed(cfg["seed"])
+    model = get_model(name)(cfg, data)
+    tr = Trainer(cfg, model, mg) if mg else Trainer(cfg, model)
+    bv, bvr, btr = tr.fit(data, hyper_tuple=(999,), saved=True, verbose=False)
+    out = {"train_loss": np.array([tr.train_loss_dict[e] for e in sorted(tr.train_loss_dict)]),
+           "valid_keys": np.array(list(bvr.keys())), "valid": np.array(list(bvr.values())),
+           "test_keys": np.array(list(btr.keys())), "test": np.array(list(btr.values())),
+           "best_valid_score": np.array(bv)}
+    if mg:
+        out.update({"alpha1": np.array(cfg["alpha1"]), "alpha2": np.array(cfg["alpha2"]), "beta": np.array(cfg["beta"])})
+    np.savez_compressed(os.path.join(OUT, fname), **out)
+    print("train", fname, out["train_loss"], btr)
+
+
+WIDE = {  # model -> (synthetic shape, dataset name, training steps, config overrides)
+    "CIKM_Model": ("allrecipes", "Allrecipes", 3, {"attention_probs_dropout_prob": 0.0}),
+    "PRICAI_ModelX": ("foodcom", "Foodcom", 4, {}),
+}
+WIDE_ROWS = 48          # sampled rows per large parameter
+WIDE_BIG = 1 << 16      # parameters with more elements than this are stored as sampled rows
+
+
+def wide_digest(ds) -> str:
+    """Digest of the training inputs of a BASELINE-width synthetic dataset (not its evaluation
+    negatives: the fixtures come from negatives=False data, as bench.py uses)."""
+    h = hashlib.sha256()
+    for a in (ds.train, ds.valid, ds.test, ds.ingre_code, ds.ingre_num, ds.image_cluster, ds.text_cluster,
+              ds.health, ds.image[::997], ds.text[::997]):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def wide_rows(name, shape0, batch_ids):
+    """Rows stored for a large parameter: a fixed sample plus rows the first batch touches."""
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(name.encode()) + shape0)
+    fixed = rng.choice(shape0, size=min(WIDE_ROWS // 2, shape0), replace=False)
+    touched = np.unique(batch_ids[batch_ids < shape0])[: WIDE_ROWS // 2]
+    return np.unique(np.concatenate([fixed, touched])).astype(np.int64)
+
+
+def wide_golden(name, make_synthetic, write_reference_format, make_config, FoodData, init_seed, get_model,
+                Trainer, TrainDataLoader, DataLoader, RandomSampler):
+    """The reference's first K training steps at a BASELINE width:
+    Trainer.fit's order (init_seed -> model -> Trainer -> two TrainDataLoaders -> RandomSampler),
+    then the step loop of trainer.py:177-224 (zero_grad, calculate_loss, sum, backward, Adam)."""
+    import torch
+    shape, dsname, steps, extra = WIDE[name]
+    ds = make_synthetic(shape, 0, negatives=False)
+    digest = wide_digest(ds)
+    # the reference's .negative reader needs >= 1 candidate per line (dataset.py:245-256); the
+    # evaluation lists are not used by these fixtures
+    ds.valid_neg = np.zeros((len(ds.valid_users), 1), np.int64)
+    ds.test_neg = np.zeros((ds.n_users, 1), np.int64)
+    root = tempfile.mkdtemp(prefix=f"frwide_{shape}_")
+    write_reference_format(ds, root + "/", dsname)
+    wbase = {"data_path": root + "/", "log_root": root + "/log/", "ckp_root": root + "/ckp/", "use_gpu": False,
+             "seed": [999], "n_cluster": [ds.n_cluster]}
+    cfg = make_config(name, extra, root=root + f"/{dsname}/processed_dataset/", dsname=dsname, over_base=wbase)
+    data = FoodData(cfg)
+    init_seed(cfg["seed"])
+    model = get_model(name)(cfg, data)
+    trainer = Trainer(cfg, model)
+    pre = TrainDataLoader(cfg, data, use_neg_list=False)
+    TrainDataLoader(cfg, data, use_neg_list=True)
+    dl = DataLoader(pre, sampler=RandomSampler(pre), batch_size=cfg["train_batch_size"])
+    out = {"digest": np.array(digest), "steps": np.array(steps), "batch_size": np.array(cfg["train_batch_size"])}
+    it = iter(dl)
+    model.train()
+    rows = {}
+    for k in range(steps):
+        batch = next(it)
+        for key in ("u_id", "pos_i_id", "neg_i_id"):
+            out[f"step{k}/{key}"] = batch[key].numpy()
+        if k == 0:
+            ids = np.concatenate([batch[key].numpy() for key in ("u_id", "pos_i_id", "neg_i_id")])
+            for pn, p in model.named_parameters():
+                if p.numel() > WIDE_BIG:
+                    rows[pn] = wide_rows(pn, p.shape[0], ids)
+                    out[f"rows/{pn}"] = rows[pn]
+            for pn, v in model.state_dict().items():
+                out[f"sd0/{pn}"] = (v[torch.from_numpy(rows[pn])] if pn in rows else v).numpy().copy()
+        if k == 0:
+            _wide_f64_step(model, batch, rows, out)
+        trainer.optimizer.zero_grad()
+        losses = model.calculate_loss(batch)
+        losses = losses if isinstance(losses, tuple) else (losses,)
+        out[f"step{k}/loss"] = np.array([float(l.detach().reshape(-1)[0]) for l in losses])
+        sum(losses).backward()
+        if k == 0:
+            for pn, p in model.named_parameters():
+                if p.grad is not None:
+                    g = p.grad
+                    out[f"grad0/{pn}"] = (g[torch.from_numpy(rows[pn])] if pn in rows else g).numpy().copy()
+        trainer.optimizer.step()
+        print("wide", name, "step", k, out[f"step{k}/loss"], flush=True)
+    for pn, p in model.named_parameters():
+        v = p.detach()
+        out[f"final/{pn}"] = (v[torch.from_numpy(rows[pn])] if pn in rows else v).numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"wide_{name}_{shape}.npz"), **out)
+
+
+def _wide_f64_step(model, batch, rows, out):
+    """The same first step of the reference model evaluated in float64 (a deep copy: parameters,
+    feature tensors and adjacencies cast): ``step0/loss_f64`` and ``grad0_f64/*``.  At these widths
+    the reference's own fp32 CPU gradients carry ~1e-4 - 4e-4 relative error upstream of the health
+    head (fp32 sums over 1,024 items x 7 labels and 20,480 tokens), so the GPU is also pinned against
+    the float64 evaluation of the reference's arithmetic."""
+    import copy
+    import torch
+    m64 = copy.deepcopy(model).double()
+    for k, v in list(vars(m64).items()):
+        if torch.is_tensor(v) and v.is_floating_point():
+            setattr(m64, k, v.double())
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in batch.items()}
+    m64.train()
+    losses = m64.calculate_loss(b64)
+    losses = losses if isinstance(losses, tuple) else (losses,)
+    out["step0/loss_f64"] = np.array([float(l.detach().reshape(-1)[0]) for l in losses])
+    sum(losses).backward()
+    for pn, p in m64.named_parameters():
+        if p.grad is not None:
+            g = p.grad
+            # stored rounded to fp32 (6e-8 relative): far below the differences it is compared at
+            out[f"grad0_f64/{pn}"] = (g[torch.from_numpy(rows[pn])] if pn in rows else g).numpy().astype(np.float32)
+    del m64
+
+
+def ops_golden():
+    import torch
     from FoodRec.models.pricai_modelx import PRICAI_ModelX
     from FoodRec.common.loss import BPRLoss, EmbLoss
     g = torch.Generator().manual_seed(1234)
@@ -210,6 +379,8 @@ def main():
                 "emb/g0": es[0].grad.numpy()})
     np.savez_compressed(os.path.join(OUT, "ops.npz"), **ops)
 
+
+def metrics_golden(metrics_by_user, get_auc_fast):
     rng = np.random.default_rng(7)
     mt = {}
     for k in range(20):
@@ -228,7 +399,6 @@ def main():
         mt[f"u{k}/ndcg"] = np.array(nd)
         mt[f"u{k}/auc"] = np.array(get_auc_fast(range(n_pos), pred, 30))
     np.savez_compressed(os.path.join(OUT, "metrics.npz"), **mt)
-    print("wrote", sorted(os.listdir(OUT)))
 
 
 if __name__ == "__main__":

@@ -22,14 +22,14 @@ def tiny_dir():
     return _TMP["tiny"]
 
 
-def tiny_config(model, use_gpu, **over):
+def tiny_config(model, use_gpu, mg=False, **over):
     from FoodRec.utils.configurator import Config
     tmp = tiny_dir()
     cd = dict(BASE)
     cd.update(EXTRA.get(model, {}))
     cd.update({"data_path": tmp + "/", "log_root": tmp + "/log/", "ckp_root": tmp + "/ckp/", "use_gpu": use_gpu})
     cd.update(over)
-    cfg = Config(model, "Tiny", cd)
+    cfg = Config(model, "Tiny", cd, mg)
     root = tmp + "/Tiny/processed_dataset/"
     cfg["interaction_data_path"] = root
     cfg["graph_data_path"] = root + "graph_edge/"

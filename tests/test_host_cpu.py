@@ -235,3 +235,14 @@ def test_oracle_cpu_backend_covers_engine_models(model):
         u, p, n = next(iter(sampler.epoch()))
         trainer.train_step(trainer._features().batch(u, p, n), 0, state)
         assert torch.isfinite(state["acc"]).all() and int(state["nan"]) == 0
+
+
+@pytest.mark.parametrize("name,shape", [("CIKM_Model", "allrecipes"), ("PRICAI_ModelX", "foodcom")])
+def test_wide_goldens_match_generator(name, shape):
+    """The BASELINE-width reference fixtures (tests/golden/wide_*.npz) were produced on
+    make_synthetic(shape, 0, negatives=False), the data bench.py trains on."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gen_golden import wide_digest
+    from FoodRec.utils.synthetic import make_synthetic
+    assert str(golden(f"wide_{name}_{shape}.npz")["digest"]) == wide_digest(make_synthetic(shape, 0, negatives=False))

@@ -14,7 +14,9 @@ from helpers import golden, tiny_config, tiny_data
 pytestmark = pytest.mark.gpu
 
 MODELS = ["LightGCN", "BPRMF", "CIKM_Model", "PRICAI_ModelX"]
-TRAINED = ["LightGCN", "BPRMF", "PRICAI_ModelX"]  # dropout-free models: exact-stream training parity
+# exact-stream training parity (HealthRec with the reference's attention dropout set to 0: the
+# reference's CPU dropout masks cannot be reproduced on the device)
+TRAINED = ["LightGCN", "BPRMF", "PRICAI_ModelX", "CIKM_Model"]
 
 
 def _load_model(name, cuda):
@@ -87,7 +89,7 @@ def test_training_matches_reference(cuda, name):
             assert abs(got[k] - v) <= 1e-3, (name, k, got[k], v)
 
 
-@pytest.mark.parametrize("name", ["LightGCN", "PRICAI_ModelX"])
+@pytest.mark.parametrize("name", ["LightGCN", "PRICAI_ModelX", "CIKM_Model"])
 def test_graphed_training_matches_reference(cuda, name):
     """The HIP-graph-captured step (cuda_graph=True) trains exactly like the eager one."""
     from FoodRec.common.trainer import Trainer
@@ -104,3 +106,71 @@ def test_graphed_training_matches_reference(cuda, name):
     np.testing.assert_allclose(trace, g["train_loss"], rtol=1e-4)
     for k, v in zip(g["test_keys"].tolist(), g["test"].tolist()):
         assert abs(btr[k] - v) <= 1e-3, (name, k, btr[k], v)
+
+
+def test_mirror_gradient_training_matches_reference(cuda):
+    """--mg (trainer.py:195-212): every beta-th batch steps on alpha1*loss, recomputes the loss on
+    the same batch and back-propagates -alpha2*loss before the regular step; mg.yaml resolved to
+    its first hyper-parameter values (alpha1 1, alpha2 0.1, beta 3) as quick_start does."""
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("train_mg_LightGCN.npz")
+    cfg = tiny_config("LightGCN", True, mg=True)
+    assert (cfg["alpha1"], cfg["alpha2"], cfg["beta"]) == (float(g["alpha1"]), float(g["alpha2"]), int(g["beta"]))
+    data = tiny_data(cfg)
+    init_seed(999)
+    model = get_model("LightGCN")(cfg, data).to(cfg["device"])
+    tr = Trainer(cfg, model, mg=True)
+    bv, bvr, btr = tr.fit(data, hyper_tuple=(999,), saved=True, verbose=False)
+    trace = np.array([tr.train_loss_dict[e] for e in sorted(tr.train_loss_dict)])
+    np.testing.assert_allclose(trace, g["train_loss"], rtol=1e-4)
+    for keys, vals, got in ((g["valid_keys"], g["valid"], bvr), (g["test_keys"], g["test"], btr)):
+        for k, v in zip(keys.tolist(), vals.tolist()):
+            assert abs(got[k] - v) <= 1e-3, ("mg", k, got[k], v)
+
+
+def test_healthrec_graphed_lazy_equals_eager_dense(cuda):
+    """The HealthRec step bench.py times (captured graph, DeviceFeed batch gather, lazy row Adam with
+    the side-stream catch-up, automatic flushes of a small history ring) against the eager step with
+    the every-row Adam, over 2 epochs of 24 steps (B = 32: 23 graph replays + the ragged eager
+    batch per epoch), attention dropout 0.  Both runs are made run-to-run reproducible (config
+    ``deterministic``: owner-slot BPR scatter; torch's deterministic index_add_): Adam turns last-bit
+    noise in near-zero gradients into +-lr steps, so atomics alone would make any two runs differ.
+    Per-epoch loss sums and every parameter and Adam moment after the epochs (flushed) agree to
+    fp32 round-off (rel 1e-6)."""
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    runs = []
+    det0 = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed)
+    finally:
+        torch.use_deterministic_algorithms(det0)
+    (la, sa, oa, ma), (lb, sb, ob, mb) = runs
+    np.testing.assert_allclose(lb, la, rtol=1e-6)
+    for k in sa:
+        torch.testing.assert_close(sb[k], sa[k], rtol=1e-6, atol=1e-7, msg=k)
+    for (k, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        if pa in oa.state:
+            for s_ in ("exp_avg", "exp_avg_sq"):
+                torch.testing.assert_close(ob.state[pb][s_], oa.state[pa][s_], rtol=1e-6, atol=1e-9, msg=(k, s_))
+
+
+def _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed):
+    for graphed in (False, True):
+        cfg = tiny_config("CIKM_Model", True, train_batch_size=32, cuda_graph=graphed, cuda_graph_warmup=2,
+                          lazy_row_adam=graphed, deterministic=True)
+        data = tiny_data(cfg)
+        init_seed(999)
+        model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
+        tr = Trainer(cfg, model)
+        assert tr.optimizer.lazy_rows == graphed
+        tr.optimizer.hist_cap = 7  # ring wraps every 5 steps: automatic flushes inside the epochs
+        sampler = TripleSampler(data, 32, cfg["device"])
+        assert len(sampler) == 24
+        losses = [tr._train_epoch(sampler, e)[0] for e in range(2)]
+        if graphed:
+            assert tr._graphed is not None and tr._graphed.graph is not None
+        runs.append((np.array(losses), model.state_dict(), tr.optimizer, model))

@@ -325,7 +325,7 @@ def test_lazy_row_prefetch_multi(cuda):
     join()
     for a, b in zip(pa, pb):
         assert torch.equal(a[read], b[read])
-    assert (id(pb[0]), read.data_ptr(), read.numel()) in ob.row_grads._prefetched
+    assert any(w is pb[0] and i is read for w, i in ob.row_grads._prefetched)
     ob.flush()
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
@@ -360,3 +360,114 @@ def test_healthrec_lazy_state_dict_flushes(cuda):
     assert not torch.equal(raw, ref)  # deferred steps pending
     sd = model.state_dict()
     assert torch.equal(sd["image_embedding.weight"], ref)
+
+
+def _row_or_dense(o, p, ids, G, dense):
+    """Hand one step's gradient to ``o`` as rows (the row path) or as a dense .grad (summed on the
+    host in a fixed order, so both optimisers see the same bits)."""
+    o.zero_grad()
+    if dense:
+        p.grad = torch.zeros(p.shape).index_add_(0, ids.cpu(), G.cpu()).to(p.device)
+    else:
+        o.row_grads.stash(p, None, ids, G)
+
+
+def test_lazy_rows_interleaved_dense_steps(cuda):
+    """A lazily updated table that also takes dense steps (a dense .grad: clipping, a hook, more ids
+    than the row path takes): the deferred steps are replayed before the dense update and every row
+    is current through it afterwards.  Bit-identical to the every-row update after each flush, with
+    several lazy steps pending before each dense one (stale history slots)."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(6)
+    R, d = 257, 64
+    w0 = torch.randn(R, d)
+    pa = torch.nn.Parameter(w0.clone().to(cuda))
+    pb = torch.nn.Parameter(w0.clone().to(cuda))
+    oa = FusedAdam([pa], lr=3e-3)
+    ob = FusedAdam([pb], lr=3e-3, lazy_rows=True, hist_cap=16)
+    dense_at = {4, 5, 9, 15}
+    for k in range(18):
+        ids, G = _case(R, d, 30, None, 1300 + k)
+        ids = torch.arange(R) if k == 0 else ids % 60
+        G = torch.randn(R, d) if k == 0 else G
+        ids, G = ids.to(cuda), G.to(cuda)
+        for o, p in ((oa, pa), (ob, pb)):
+            _row_or_dense(o, p, ids, G, k in dense_at)
+            o.step()
+        if k in (5, 12, 17):
+            ob.flush()
+            assert torch.equal(pa, pb), k
+            for s_ in ("exp_avg", "exp_avg_sq"):
+                assert torch.equal(oa.state[pa][s_], ob.state[pb][s_]), (k, s_)
+    assert int(ob.state[pb]["step"].item()) == 18
+
+
+def test_lazy_rows_more_than_16_tables(cuda):
+    """More lazy tables than one launch's argument block holds (16): the row update is split into
+    launches of 16 and stays lazy for all of them (no fallback to a non-lazy update)."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(7)
+    shapes = [(97 + 3 * t, 64 if t % 2 else 128) for t in range(19)]
+    w0 = [torch.randn(R, d) for R, d in shapes]
+    pa = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    pb = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    oa = FusedAdam(pa, lr=2e-3)
+    ob = FusedAdam(pb, lr=2e-3, lazy_rows=True)
+    for k in range(6):
+        for o, ps in ((oa, pa), (ob, pb)):
+            o.zero_grad()
+            for t, ((R, d), p) in enumerate(zip(shapes, ps)):
+                ids, G = _case(R, d, 20, None, 2000 + 50 * k + t)
+                ids = torch.arange(R) if k == 0 else ids % 40
+                G = torch.randn(R, d, generator=torch.Generator().manual_seed(k * 100 + t)) if k == 0 else G
+                o.row_grads.stash(p, None, ids.to(cuda), G.to(cuda))
+            o.step()
+    assert all("lazy_last" in ob.state[p] for p in pb)
+    assert not torch.equal(pa[0], pb[0])  # rows 40+ deferred
+    ob.flush()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+        assert torch.equal(oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])
+
+
+def test_lazy_rows_state_dict_round_trip(cuda):
+    """optimizer.state_dict() -> torch.save -> torch.load -> load_state_dict() into a fresh FusedAdam,
+    then more lazy steps: bit-identical to the uninterrupted run.  (torch's loader would cast the
+    int32 per-row step index to float32 and leave 'step' on the host)"""
+    import io
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(8)
+    R, d = 300, 128
+    w0 = torch.randn(R, d)
+    pa = torch.nn.Parameter(w0.clone().to(cuda))
+    pb = torch.nn.Parameter(w0.clone().to(cuda))
+    oa = FusedAdam([pa], lr=3e-3, lazy_rows=True)
+    ob = FusedAdam([pb], lr=3e-3, lazy_rows=True)
+    cases = []
+    for k in range(10):
+        ids, G = _case(R, d, 25, None, 2500 + k)
+        cases.append(((torch.arange(R) if k == 0 else ids % 70).to(cuda),
+                      (torch.randn(R, d) if k == 0 else G).to(cuda)))
+    for k in range(10):
+        for o, p in ((oa, pa), (ob, pb)):
+            if o is ob and k == 5:
+                buf = io.BytesIO()
+                torch.save(ob.state_dict(), buf)
+                buf.seek(0)
+                sd = torch.load(buf, weights_only=True)
+                pb_new = torch.nn.Parameter(pb.detach().clone())
+                ob = FusedAdam([pb_new], lr=3e-3, lazy_rows=True)
+                ob.load_state_dict(sd)
+                st = ob.state[pb_new]
+                assert st["step"].dtype == torch.int64 and st["step"].is_cuda
+                assert "lazy_last" not in st and st["exp_avg"].dtype == torch.float32
+                pb, o, p = pb_new, ob, pb_new
+            o.zero_grad()
+            o.row_grads.stash(p, None, *cases[k])
+            o.step()
+    oa.flush()
+    ob.flush()
+    assert torch.equal(pa, pb)
+    for s_ in ("exp_avg", "exp_avg_sq"):
+        assert torch.equal(oa.state[pa][s_], ob.state[pb][s_]), s_
+    assert int(ob.state[pb]["step"].item()) == 10
