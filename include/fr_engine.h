@@ -531,6 +531,30 @@ int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* 
                      const int64_t* pos_off, const int64_t* users, int64_t n_users, const int64_t* cand_off,
                      int64_t* out_users, int64_t* out_items, int threads);
 
+/* ------------------------------------------------------------------------------------------
+ * RCCL communicator (SURVEY 8(b) fr_comm_init / fr_allreduce_f32; new work: the reference is
+ * single-process, utils/configurator.py:110-114).  One communicator per process and GPU (the
+ * calling thread's current HIP device); collectives are stream-ordered on the caller's stream.
+ * Replaces, for a host that binds only this ABI, the torch.distributed (backend "nccl" = RCCL)
+ * calls of engine/sharded.py (per-layer item all-reduce, _all_reduce) and engine/dist.py (dense
+ * gradient all-reduce, GradAllReduce.communicate_dense; row all-gather, RowExchange.exchange).
+ *   fr_comm_available      1 if an RCCL library could be resolved (the process's own copy first)
+ *   fr_comm_unique_id      rank 0 draws the 128-byte id (fr_comm_unique_id_bytes) and ships it to
+ *                          the other ranks out of band (a TCP store, a file, MPI ...)
+ *   fr_comm_init           ncclCommInitRank (collective over the world's ranks)
+ *   fr_allreduce_f32       in-place float sum of n elements
+ *   fr_allgather_f32       recv[world * n] = every rank's send[n], in rank order
+ *   fr_comm_destroy        frees the communicator (NULL is a no-op)
+ * FR_ENOTSUP when no RCCL library is present; RCCL failures -> FR_EHIP + fr_last_error.
+ * ------------------------------------------------------------------------------------------ */
+int fr_comm_available(void);
+int64_t fr_comm_unique_id_bytes(void);
+int fr_comm_unique_id(void* out, int64_t out_bytes);
+int fr_comm_init(int rank, int world, const void* unique_id, void** comm);
+int fr_allreduce_f32(void* comm, float* buf, int64_t n, void* stream);
+int fr_allgather_f32(void* comm, const float* send, float* recv, int64_t n, void* stream);
+int fr_comm_destroy(void* comm);
+
 #ifdef __cplusplus
 }
 #endif

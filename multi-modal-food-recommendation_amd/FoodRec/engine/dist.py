@@ -135,13 +135,15 @@ class GradAllReduce:
     row exchange) are collective-free, so a graphed step captures them; ``communicate()`` issues the
     collectives eagerly between the two graphs (Trainer.GraphedDPStep)."""
 
-    def __init__(self, model, world: int, group=None):
+    def __init__(self, model, world: int, group=None, exchange_rows: bool | None = None):
         import torch.distributed as dist
         self.world = int(world)
         self.group = group
         sparse = {id(p) for p in getattr(model, "row_sparse_tables", lambda: [])()}
         self.rows = None
-        if sparse and self.world > 1:
+        # exchange_rows: route the row tables through RowExchange (default: when there is more than
+        # one rank; True at world 1 exercises the exchange on a single GPU)
+        if sparse and (self.world > 1 if exchange_rows is None else exchange_rows):
             self.rows = RowExchange(group if group is not None else dist.group.WORLD, self.world)
             model._fr_exchange = self.rows
         else:

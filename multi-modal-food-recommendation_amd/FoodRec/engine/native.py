@@ -163,6 +163,13 @@ _SIGS = {
                                     c_void_p, c_void_p]),
     "fr_norms_bwd_coef": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_void_p, c_void_p]),
+    "fr_comm_available": (c_int, []),
+    "fr_comm_unique_id_bytes": (c_int64, []),
+    "fr_comm_unique_id": (c_int, [c_void_p, c_int64]),
+    "fr_comm_init": (c_int, [c_int, c_int, c_void_p, POINTER(c_void_p)]),
+    "fr_allreduce_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_allgather_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_comm_destroy": (c_int, [c_void_p]),
     "fr_io_open": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
     "fr_io_fill": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
     "fr_io_close": (None, [c_void_p]),

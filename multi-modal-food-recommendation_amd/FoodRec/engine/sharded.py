@@ -29,6 +29,7 @@ With P = 1 the step is exactly the single-GPU LightGCN_ID step (up to fp32 summa
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -39,8 +40,31 @@ from . import ops
 from .graph import DEFAULT_CHUNK, Adjacency
 
 
+_FORCE = [False]
+
+
+@contextlib.contextmanager
+def collectives_at_world_one():
+    """Issue every collective even in a one-rank group (normally skipped as the identity), so a
+    single-GPU run exercises the RCCL path (tests on a one-GPU box)."""
+    _FORCE[0] = True
+    try:
+        yield
+    finally:
+        _FORCE[0] = False
+
+
 def _all_reduce(t, group, async_op=False):
-    if group is None or dist.get_world_size(group) == 1:
+    """Sum ``t`` over ``group`` in place: a torch.distributed group (backend "nccl" = RCCL) or an
+    engine.comm.RcclComm (the C-ABI communicator).  Returns a handle with ``wait()`` for async_op."""
+    if group is None:
+        return None
+    from .comm import RcclComm
+    if isinstance(group, RcclComm):
+        if group.world == 1 and not _FORCE[0]:
+            return None
+        return group.all_reduce(t, async_op=async_op)
+    if dist.get_world_size(group) == 1 and not _FORCE[0]:
         return None
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
