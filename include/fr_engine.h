@@ -30,6 +30,7 @@
 #define FR_ENGINE_H
 
 #include <stdint.h>
+#include <stdbool.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -530,6 +531,57 @@ int fr_io_remove_positives(const int64_t* neg, const int64_t* neg_off, uint8_t* 
 int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* alive, const int64_t* pos,
                      const int64_t* pos_off, const int64_t* users, int64_t n_users, const int64_t* cand_off,
                      int64_t* out_users, int64_t* out_items, int threads);
+
+/* ------------------------------------------------------------------------------------------
+ * fr_spmm_csr_ex: fr_spmm_csr over split row tables, a column mask and a row list.
+ *   fr_tab      rows [0, split) at lo (stride ld_lo), rows [split, n) at hi (stride ld_hi, row r at
+ *               hi + (r - split) * ld_hi); hi == NULL: every row at lo.  X, Y1, Y2, A1, A2 may each
+ *               be split (one split row for the call).  HealthRec's propagation reads its ego table
+ *               as [user_embedding ; item_ir] / [item_embedding ; ingre_embedding[:-1]] and writes
+ *               its gradient into the tables' own buffers: the torch.cat / split / slice glue of
+ *               cikm_model.py:185-199 (and of their backward) disappears.
+ *   d_col_mask  optional uint8 per X row: edges to a row with mask 0 are skipped (X known zero
+ *               there: the backward of a propagation evaluated at a few rows).
+ *   rows        optional fr_rowlist: only the listed rows (ids[k][i] + off[k]) are computed, one
+ *               workgroup per listed row (d = 64; deterministic, equal to the full launch's row to
+ *               fp32 rounding); the other rows of Y are not written.  The training step needs the UI propagation only
+ *               at the batch's users and items (cikm_model.py:255-261): 3B rows instead of U + I.
+ * fr_rows_mark: mask[ids[k][i] + off[k]] = value (sets / clears a column mask from a row list).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct fr_tab {
+  const float* lo;
+  int64_t ld_lo;
+  const float* hi;
+  int64_t ld_hi;
+} fr_tab;
+typedef struct fr_rowlist {
+  const int64_t* ids[3];
+  int64_t n[3];
+  int64_t off[3];
+} fr_rowlist;
+int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                   const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
+                   const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
+                   float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, void* d_workspace,
+                   int64_t workspace_bytes, void* stream);
+int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * fr_feed_batch: one step's batch in one launch.  Replaces TrainDataLoader.__getitem__ x B +
+ * default_collate (utils/dataloader.py:50-115) as the engine stages them on the device.
+ *   feed mode (d_perm != NULL): triple i of batch *d_cursor (device) of the staged epoch:
+ *     k = perm[cursor * B + i];  u[i] = users[k];  p[i] = items[k];  n[i] = negs[cursor * B + i]
+ *     (the cursor is not advanced here);
+ *   plain mode: p, n are inputs.
+ *   Both: rows j of [p ; n]: pn[j], out_codes[j] = codes[pn[j]] ([L] int64), out_nums[j],
+ *   out_health[j] = health[pn[j]] ([H] float, optional: H = 0 and NULLs), out_mask[j][c] =
+ *   out_codes[j][c] == pad (optional, HealthRec's key-padding mask, cikm_model.py:231-232).
+ * ------------------------------------------------------------------------------------------ */
+int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* d_items, const int64_t* d_negs,
+                  const int64_t* d_cursor, int64_t B, int64_t* d_u, int64_t* d_p, int64_t* d_n,
+                  const int64_t* d_codes, int L, const int64_t* d_nums, const float* d_health, int H,
+                  int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes, int64_t* d_out_nums,
+                  float* d_out_health, bool* d_out_mask, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * RCCL communicator (SURVEY 8(b) fr_comm_init / fr_allreduce_f32; new work: the reference is

@@ -112,10 +112,13 @@ class GraphedStep:
             self.tr.optimizer.note_replay()
 
     def _body(self, batch_idx, state, accumulate=True):
-        if self.feed is not None:
-            self.feed.fill(self.u, self.p, self.n)
         feats = self.tr._features()
-        return self.tr.train_step(feats.batch(self.u, self.p, self.n), batch_idx, state, accumulate=accumulate)
+        pre = None
+        if self.feed is not None:
+            # (u, pos, neg) and the [pos; neg] item features gathered in one launch (fr_feed_batch)
+            pre = self.feed.fill(self.u, self.p, self.n, feats if not feats.ssl else None)
+        return self.tr.train_step(feats.batch(self.u, self.p, self.n, pre=pre), batch_idx, state,
+                                  accumulate=accumulate)
 
     def __call__(self, u, p, n, batch_idx, state):
         if u.numel() != self.B:
@@ -182,11 +185,12 @@ class GraphedDPStep(GraphedStep):
 
     def _part_a(self, batch_idx, state, accumulate):
         tr = self.tr
-        if self.feed is not None:
-            self.feed.fill(self.u, self.p, self.n)
         feats = tr._features()
+        pre = None
+        if self.feed is not None:
+            pre = self.feed.fill(self.u, self.p, self.n, feats if not feats.ssl else None)
         tr.optimizer.zero_grad()
-        losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n))
+        losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
         parts = losses if isinstance(losses, tuple) else (losses,)
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])

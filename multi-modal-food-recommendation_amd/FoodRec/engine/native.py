@@ -28,6 +28,15 @@ class FrSpmmPlan(ctypes.Structure):
                 ("n_plain", c_int64), ("n_split", c_int64), ("chunk", c_int32)]
 
 
+class FrTab(ctypes.Structure):
+    """fr_tab: rows [0, split) at lo, [split, n) at hi (hi NULL: all rows at lo)."""
+    _fields_ = [("lo", c_void_p), ("ld_lo", c_int64), ("hi", c_void_p), ("ld_hi", c_int64)]
+
+
+class FrRowList(ctypes.Structure):
+    _fields_ = [("ids", c_void_p * 3), ("n", c_int64 * 3), ("off", c_int64 * 3)]
+
+
 _lib = None
 
 # name -> (restype, argtypes)
@@ -45,6 +54,14 @@ _SIGS = {
                             c_void_p, c_int64, c_float,
                             c_void_p, c_int64, c_float,
                             c_void_p, c_int64, c_void_p]),
+    "fr_spmm_csr_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, POINTER(FrSpmmPlan), c_int64,
+                               POINTER(FrTab), c_int, POINTER(FrTab), POINTER(FrTab), c_float, POINTER(FrTab),
+                               c_float, POINTER(FrTab), c_float, c_void_p, POINTER(FrRowList), c_void_p, c_int64,
+                               c_void_p]),
+    "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
+    "fr_feed_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_bpr_workspace": (c_int64, [c_int64]),
     "fr_embedding_bwd_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_bwd_status_offset": (c_int64, [c_int64]),

@@ -306,6 +306,221 @@ def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, determinist
                          item_offset)
 
 
+# ----------------------------------------------------------------------------- split-table SpMM
+def _tab(lo, hi=None):
+    if lo is None:
+        return native.FrTab(None, 0, None, 0)
+    return native.FrTab(lo.data_ptr(), lo.stride(0), hi.data_ptr() if hi is not None else None,
+                        hi.stride(0) if hi is not None else 0)
+
+
+def _rowlist(segs):
+    """[(int64 ids, offset), ...] (at most 3) -> fr_rowlist."""
+    rl = native.FrRowList()
+    for k, (ids, off) in enumerate(segs):
+        rl.ids[k] = ids.data_ptr()
+        rl.n[k] = ids.numel()
+        rl.off[k] = int(off)
+    return rl
+
+
+def _check_tab(name, lo, hi, split, n, d):
+    if lo is None:
+        return
+    for t in (lo, hi):
+        if t is not None and (t.dtype != torch.float32 or t.dim() != 2 or t.shape[1] != d or t.stride(1) != 1
+                              or t.stride(0) % 4 or t.data_ptr() % 16):
+            raise native.EngineError(f"spmm_ex: {name} must be fp32 [rows, {d}] with 16-B aligned rows")
+    if hi is None and lo.shape[0] < n:
+        raise native.EngineError(f"spmm_ex: {name} has {lo.shape[0]} rows, needs {n}")
+    if hi is not None and (lo.shape[0] < split or hi.shape[0] < n - split):
+        raise native.EngineError(f"spmm_ex: {name} split at {split} does not cover {n} rows")
+
+
+def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None, Y2_hi=None, alpha=1.0,
+            A1=None, A1_hi=None, beta1=0.0, A2=None, A2_hi=None, beta2=0.0, col_mask=None, rows=None,
+            region="spmm", nbytes=None):
+    """fr_spmm_csr_ex: the fr_spmm_csr epilogue over split tables ([lo ; hi] at row ``split``), an
+    optional column mask (uint8 per X row, skipped where 0) and an optional row list
+    ([(ids, offset), ...]: only those rows of Y are computed and written)."""
+    native.require_device(X)
+    N, d = adj.shape[0], X.shape[1]
+    _check_tab("X", X, X_hi, split, adj.shape[1], d)
+    for name, lo, hi in (("Y1", Y1, Y1_hi), ("Y2", Y2, Y2_hi), ("A1", A1, A1_hi), ("A2", A2, A2_hi)):
+        _check_tab(name, lo, hi, split, N, d)
+    if col_mask is not None and (col_mask.dtype != torch.uint8 or col_mask.numel() < adj.shape[1]):
+        raise native.EngineError("spmm_ex: col_mask must be uint8 with one entry per X row")
+    plan = adj.plan()
+    ws = _ws_for(adj, d, X.device)
+    rl = _rowlist(rows) if rows is not None else None
+    if nbytes is None:
+        nbytes = spmm_bytes(adj, d, sum(x is not None for x in (Y1, Y2, A1, A2))) if rows is None else 0
+    with profiling.region(region, nbytes):
+        native.check(native.lib().fr_spmm_csr_ex(
+            adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, ctypes.byref(plan), int(split),
+            ctypes.byref(_tab(X, X_hi)), d, ctypes.byref(_tab(Y1, Y1_hi)), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha),
+            ctypes.byref(_tab(A1, A1_hi)), _f(beta1), ctypes.byref(_tab(A2, A2_hi)), _f(beta2),
+            native.ptr(col_mask), ctypes.byref(rl) if rl is not None else None, ws.data_ptr(), ws.numel(),
+            native.stream_of(X)), "fr_spmm_csr_ex")
+
+
+def rows_mark(mask: torch.Tensor, rows, value: int) -> None:
+    native.check(native.lib().fr_rows_mark(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
+                                           native.stream_of(mask)), "fr_rows_mark")
+
+
+def _prop_fwd_split(adj, lo, hi, split, L):
+    """mean([E, A E, ..., A^L E]) for E = [lo ; hi] split at ``split`` (no concatenated copy)."""
+    N, d = adj.shape[0], lo.shape[1]
+    out = torch.empty(N, d, dtype=lo.dtype, device=lo.device)
+    if L == 1:
+        spmm_ex(adj, lo, hi, split, Y2=out, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)
+        return out
+    inv = 1.0 / (L + 1)
+    E1 = torch.empty_like(out)
+    if L == 2:
+        spmm_ex(adj, lo, hi, split, Y1=E1)
+        spmm_ex(adj, E1, Y2=out, alpha=inv, A1=lo, A1_hi=hi, beta1=inv, A2=E1, beta2=inv, split=split)
+        return out
+    S = torch.empty_like(out)
+    spmm_ex(adj, lo, hi, split, Y1=E1, Y2=S, alpha=1.0, A1=lo, A1_hi=hi, beta1=1.0)
+    prev, nxt = E1, torch.empty_like(out)
+    for _ in range(2, L):
+        spmm_launch(adj, prev, Y1=nxt, Y2=S, alpha=1.0, A1=S, beta1=1.0)
+        prev, nxt = nxt, prev
+    spmm_launch(adj, prev, Y2=out, alpha=inv, A1=S, beta1=inv)
+    return out
+
+
+def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None):
+    """d/dE of mean_k A^k E (A symmetric) for upstream G, written into [out_lo ; out_hi] split at
+    ``split``.  ``col_mask``: rows where G is known to be zero (first layer only)."""
+    inv = 1.0 / (L + 1)
+    if L == 1:
+        spmm_ex(adj, G, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv, A1=G, beta1=inv, col_mask=col_mask)
+        return
+    H = torch.empty_like(G)
+    spmm_ex(adj, G, Y2=H, alpha=inv, A1=G, beta1=inv, col_mask=col_mask)
+    H2 = torch.empty_like(G) if L > 2 else None
+    for _ in range(1, L - 1):
+        spmm_launch(adj, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
+        H, H2 = H2, H
+    spmm_ex(adj, H, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=1.0, A1=G, beta1=inv)
+
+
+def _persistent(adj, key, make):
+    cache = adj.__dict__.setdefault("_persist", {})
+    t = cache.get(key)
+    if t is None:
+        t = make()
+        cache[key] = t
+    return t
+
+
+class _GraphBpr(torch.autograd.Function):
+    """HealthRec's propagation + BPR + user/item EmbLoss (cikm_model.py:182-208, 255-279) as one
+    autograd node:
+
+    forward   RI: mean over n_layers of A_RI^k [item ; ingre[:-1]]  (split-table reads, full graph)
+              UI: (ego + A_UI ego) / 2 at the batch's users and items only (row-list mode: the
+                  loss reads ui_all at u, U + pos, U + neg and nowhere else), ego = [user ; item_ir]
+              fused BPR + EmbLoss on those rows; the [pos; neg] item rows returned for the KD term
+    backward  BPR scatter into dUI (+ the KD rows' gradient); UI backward over the edges into the
+              batch rows only (column mask), written straight into d user_embedding and the item
+              block of the RI upstream gradient (its ingredient block is a persistent zero); RI
+              backward written straight into d item_embedding and d ingre_embedding[:-1]; the
+              EmbLoss ego-row gradients accumulated in place.  No concatenation, split, slice or
+              gradient-sum kernels.
+    ui_layers > 1: the UI propagation is evaluated in full (the loss rows' dependency cone spans
+    the graph) with the same split-table reads and writes."""
+
+    @staticmethod
+    def forward(ctx, user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma, det):
+        U, I = user_w.shape[0], item_w.shape[0]
+        NI = ingre_w.shape[0] - 1
+        dev = user_w.device
+        native.require_device(user_w, item_w, ingre_w, u, p, n)
+        for t in (user_w, item_w, ingre_w):
+            if t.dtype != torch.float32 or t.shape[1] != 64 or not t.is_contiguous():
+                raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
+        u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
+        ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri)       # [I + NI, 64]
+        rows = [(u, 0), (p, U), (n, U)]
+        if L_ui == 1:
+            ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
+            spmm_ex(ui_adj, user_w, ir_all, U, Y2=ui_all, alpha=0.5, A1=user_w, A1_hi=ir_all, beta1=0.5,
+                    rows=rows, region="spmm_rows")
+        else:
+            ui_all = _prop_fwd_split(ui_adj, user_w, ir_all, U, L_ui)
+        B = int(u.numel())
+        lib = native.lib()
+        ws = native.workspace(lib.fr_bpr_workspace(B), dev)
+        out = torch.empty(5, dtype=torch.float32, device=dev)
+        items = ui_all[U:]
+        native.check(lib.fr_bpr_fwd(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
+                                    item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                    _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(), native.stream_of(user_w)),
+                     "fr_bpr_fwd")
+        item_rows = torch.index_select(items, 0, pn)
+        ctx.save_for_backward(user_w, item_w, ui_all, u, p, n, pn)
+        ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
+        return out[0], out[4:5], item_rows
+
+    @staticmethod
+    def backward(ctx, g_mf, g_emb, g_rows):
+        user_w, item_w, ui_all, u, p, n, pn = ctx.saved_tensors
+        ri_adj, ui_adj, L_ri, L_ui, gamma, det, ws, U, I, NI = ctx.meta
+        dev = user_w.device
+        g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
+        g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
+        gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
+        B = int(u.numel())
+        lib = native.lib()
+        s = native.stream_of(user_w)
+        items = ui_all[U:]
+        dUI = torch.zeros(U + I, 64, dtype=torch.float32, device=dev)
+        dI = dUI[U:]
+        common = (ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
+                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(gamma), _f(1.0), _f(1.0), gscale.data_ptr())
+        with profiling.region("bpr_bwd", 0):
+            if g_rows is not None and not det:
+                g_rows = g_rows.contiguous()
+                native.check(lib.fr_bpr_bwd_ex(*common, dUI.data_ptr(), dI.data_ptr(), None, None, g_rows.data_ptr(),
+                                               g_rows.stride(0), ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd_ex")
+            else:
+                native.check(lib.fr_bpr_bwd(*common, dUI.data_ptr(), dI.data_ptr(), None, None, det, ws.data_ptr(),
+                                            ws.numel(), s), "fr_bpr_bwd")
+                if g_rows is not None:
+                    dI.index_add_(0, pn, g_rows)
+        d_user = torch.empty_like(user_w)
+        # RI upstream gradient: [d item_ir ; 0] -- the ingredient block is never written (persistent zero)
+        G_ri = _persistent(ri_adj, ("g_ri", str(dev)), lambda: torch.zeros(I + NI, 64, device=dev))
+        if L_ui == 1:
+            mask = _persistent(ui_adj, ("mask", str(dev)), lambda: torch.zeros(U + I, dtype=torch.uint8, device=dev))
+            rows = [(u, 0), (p, U), (n, U)]
+            rows_mark(mask, rows, 1)
+            _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask)
+            rows_mark(mask, rows, 0)
+        else:
+            _prop_bwd_split(ui_adj, dUI, L_ui, d_user, G_ri, U)
+        d_item = torch.empty_like(item_w)
+        d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
+        _prop_bwd_split(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
+        d_ingre[NI:].zero_()  # the padding row is not a graph node
+        # EmbLoss on the ego rows, accumulated into the propagation gradients
+        with profiling.region("bpr_bwd", 0):
+            native.check(lib.fr_bpr_bwd(*common, None, None, d_user.data_ptr(), d_item.data_ptr(), det, ws.data_ptr(),
+                                        ws.numel(), s), "fr_bpr_bwd")
+        return (d_user, d_item, d_ingre) + (None,) * 10
+
+
+def graph_bpr(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
+    """HealthRec's propagation + BPR + EmbLoss(user, pos, neg) -> (BPRLoss, EmbLoss [1],
+    [ui_items[pos]; ui_items[neg]]); see _GraphBpr."""
+    return _GraphBpr.apply(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma,
+                           _DETERMINISTIC)
+
+
 # ----------------------------------------------------------------------------- embedding
 def embedding_bwd_bytes(n: int, rows: int, d: int) -> int:
     """Algorithmic HBM bytes of one fr_embedding_bwd: ids + gradient rows read, dW written."""

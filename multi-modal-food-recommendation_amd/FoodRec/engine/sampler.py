@@ -149,13 +149,22 @@ class DeviceFeed:
         self.negs.copy_(negs_d)
         self.cursor.zero_()
 
-    def fill(self, u, p, n):
+    def fill(self, u, p, n, feats=None):
+        """Gather batch ``cursor`` into (u, p, n) and advance the cursor.  With ``feats`` (a
+        BatchFeatures on the GPU) the [pos; neg] item features are gathered in the same launch
+        (fr_feed_batch) into feats' static buffers, which are returned for ``feats.batch(..., pre=)``."""
+        if feats is not None and feats.native_ok():
+            pre = feats.pn_buffers(self.B)
+            feats.launch_feed(self, u, p, n, pre)
+            self.cursor.add_(1)
+            return pre
         torch.add(self.offs, self.cursor * self.B, out=self._pos)
         torch.index_select(self.perm, 0, self._pos, out=self._idx)
         torch.index_select(self.users, 0, self._idx, out=u)
         torch.index_select(self.items, 0, self._idx, out=p)
         torch.index_select(self.negs, 0, self._pos, out=n)
         self.cursor.add_(1)
+        return None
 
 
 SSL_MASKED_P = 0.2   # TrainDataLoader.masked_p (dataloader.py:19)
@@ -213,14 +222,60 @@ class BatchFeatures:
             self._n_ingre = int(dataset.num_ingredients)
         self._image = None
         self._ds = dataset
+        self.pad_id = int(getattr(dataset, "num_ingredients", -1) or -1)  # HealthRec's ingredient padding id
 
     def image(self):
         if self._image is None:
             self._image = torch.from_numpy(np.asarray(self._ds.embImage, np.float64)).to(self.device)
         return self._image
 
-    def batch(self, u, p, n) -> "LazyBatch":
+    # ------------------------------------------------------------------ [pos; neg] features (fr_feed_batch)
+    def native_ok(self) -> bool:
+        return self.device.type == "cuda" and self.ingre_code.dim() == 2 and self.ingre_code.shape[1] >= 1
+
+    def _pn_alloc(self, B):
+        dev = self.device
+        L = self.ingre_code.shape[1]
+        out = {"pn_i_id": torch.empty(2 * B, dtype=torch.int64, device=dev),
+               "pn_ingre_code": torch.empty(2 * B, L, dtype=torch.int64, device=dev),
+               "pn_ingre_num": torch.empty(2 * B, dtype=torch.int64, device=dev),
+               "pn_pad_mask": torch.empty(2 * B, L, dtype=torch.bool, device=dev)}
+        if self.health is not None:
+            out["pn_hl_mh"] = torch.empty(2 * B, self.health.shape[1], dtype=self.health.dtype, device=dev)
+        return out
+
+    def pn_buffers(self, B):
+        """Static [pos; neg] feature buffers for batch size B (a graphed step's inputs)."""
+        cache = self.__dict__.setdefault("_pn_static", {})
+        if B not in cache:
+            cache[B] = self._pn_alloc(B)
+        return cache[B]
+
+    def _launch(self, perm, users, items, negs, cursor, B, u, p, n, out):
+        from . import native
+        h = self.health
+        H = 0 if h is None else h.shape[1]
+        native.check(native.lib().fr_feed_batch(
+            native.ptr(perm), native.ptr(users), native.ptr(items), native.ptr(negs), native.ptr(cursor), B,
+            native.ptr(u), p.data_ptr(), n.data_ptr(), self.ingre_code.data_ptr(), self.ingre_code.shape[1],
+            self.ingre_num.data_ptr(), native.ptr(h), H, self.ingre_code.shape[0], self.pad_id,
+            out["pn_i_id"].data_ptr(), out["pn_ingre_code"].data_ptr(), out["pn_ingre_num"].data_ptr(),
+            native.ptr(out.get("pn_hl_mh")), out["pn_pad_mask"].data_ptr(), native.stream_of(p)), "fr_feed_batch")
+
+    def launch_feed(self, feed, u, p, n, out):
+        self._launch(feed.perm, feed.users, feed.items, feed.negs, feed.cursor, feed.B, u, p, n, out)
+
+    def gather_pn(self, p, n) -> dict:
+        """The [pos; neg] item features of a batch in one launch (fresh tensors)."""
+        p, n = p.to(torch.int64).contiguous(), n.to(torch.int64).contiguous()
+        out = self._pn_alloc(p.numel())
+        self._launch(None, None, None, None, None, p.numel(), None, p, n, out)
+        return out
+
+    def batch(self, u, p, n, pre=None) -> "LazyBatch":
         b = LazyBatch(self, u, p, n)
+        if pre is not None:
+            dict.update(b, pre)
         if self.ssl:  # eager, like the reference's per-sample __getitem__ (the RNG stream advances per batch)
             pi = p.cpu().numpy()
             seqs = ssl_sequences(self._codes_np[pi], self._nums_np[pi], self._n_ingre)
@@ -234,16 +289,27 @@ class LazyBatch(dict):
 
     _LAZY = ("pos_ingre_code", "pos_ingre_num", "pos_hl_mh", "pos_img", "pos_cl",
              "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img", "neg_cl",
-             # engine extras: [pos; neg] stacked (one gather instead of two gathers and a cat)
-             "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh")
+             # engine extras: [pos; neg] stacked, gathered together in one launch (fr_feed_batch), and
+             # the ingredient padding mask of the stacked codes
+             "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_mask")
 
     def __init__(self, feats: BatchFeatures, u, p, n):
         super().__init__(u_id=u, pos_i_id=p, neg_i_id=n)
         self._f = feats
 
     def _make(self, key):
+        if key.startswith("pn_") and self._f.native_ok():
+            got = self._f.gather_pn(self["pos_i_id"], self["neg_i_id"])  # every pn_ key in one launch
+            for k, v in got.items():
+                if not dict.__contains__(self, k):
+                    dict.__setitem__(self, k, v)
+            if key not in got:
+                raise KeyError(key)
+            return got[key]
         if key == "pn_i_id":
             return torch.cat([self["pos_i_id"], self["neg_i_id"]])
+        if key == "pn_pad_mask":
+            return self["pn_ingre_code"] == self._f.pad_id
         side, what = key.split("_", 1)
         idx = {"pos": self["pos_i_id"], "neg": self["neg_i_id"]}.get(side)
         if idx is None:

@@ -34,6 +34,8 @@ FUSED_FUSION = os.environ.get("FR_FUSED_FUSION", "1") != "0"
 FUSED_HEAD = os.environ.get("FR_FUSED_HEAD", "1") != "0"
 # FR_FUSED_PROJECTION=0 keeps gather + ops.linear for the image / text projections
 FUSED_PROJECTION = os.environ.get("FR_FUSED_PROJECTION", "1") != "0"
+# FR_FUSED_GRAPH=0 keeps the concatenated-ego propagation + separate BPR op (full UI propagation)
+FUSED_GRAPH = os.environ.get("FR_FUSED_GRAPH", "1") != "0"
 
 
 class TargetAttention(nn.Module):
@@ -150,7 +152,16 @@ class HealthRec(GeneralRecommender):
         # 2-rank rehearsal 16 -> 73 ms/step), its rows are caught up inline before the gather
         join = xg.prefetch_rows([(t.weight, all_item) for t in self._row_tables()]) \
             if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) else (lambda: None)
-        ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
+        fused_graph = self._fused_graph(user)
+        if fused_graph:
+            # both propagations + BPR + the user/item EmbLoss terms as one node: split-table reads and
+            # writes (no cat / split glue), the UI propagation evaluated at the batch rows only
+            mf_loss, emb3, item_rows = ops.graph_bpr(self.user_embedding.weight, self.item_embedding.weight,
+                                                     self.ingre_embedding.weight, user, pos_item, neg_item, all_item,
+                                                     self.ri_norm_adj, self.norm_adj_matrix, self.n_layers,
+                                                     self.ui_layers)
+        else:
+            ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
         health_level = _pn(batch_data, "hl_mh")
         ingredients = _pn(batch_data, "ingre_code")
@@ -160,7 +171,9 @@ class HealthRec(GeneralRecommender):
         # norms of ingre_embedding(pos / neg ingredients) with padding_idx (:270-279): the same
         # gather, so one gather and one combined deterministic scatter (fr_embedding_bwd)
         ingr_emb, ing_norms = ops.embedding_norms(ingredients, ingr_all, self.n_ingredients, B)
-        mask = ingredients == self.n_ingredients
+        mask = batch_data.get("pn_pad_mask")  # gathered with the codes (engine batch), else computed
+        if mask is None:
+            mask = ingredients == self.n_ingredients
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
@@ -187,9 +200,10 @@ class HealthRec(GeneralRecommender):
             health_in = F.normalize(item_health).mean(dim=1)
         # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263): the BPR kernel's own
         # item rows; their KD gradient is added inside the BPR backward's scatter
-        mf_loss, emb3, item_rows = ops.bpr_emb_loss(ui_all, None, self.user_embedding.weight,
-                                                    self.item_embedding.weight, user, pos_item, neg_item,
-                                                    item_rows=True, item_offset=self.n_users)
+        if not fused_graph:
+            mf_loss, emb3, item_rows = ops.bpr_emb_loss(ui_all, None, self.user_embedding.weight,
+                                                        self.item_embedding.weight, user, pos_item, neg_item,
+                                                        item_rows=True, item_offset=self.n_users)
         if self._fused_head(health_in, health_level):
             # health MLP + BCE sum and the KD cosine term, weighted, in one HIP kernel per direction
             health_term, kd_term = ops.health_kd_loss(health_in, item_know, item_rows, health_level, self.health_mlp,
@@ -212,6 +226,16 @@ class HealthRec(GeneralRecommender):
                 and mm_query.shape[1] == 2 and encoded.shape[1] in ops.ENCODER_LENGTHS
                 and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
                 and a.ln.eps == b.ln.eps)
+
+    def _fused_graph(self, ids) -> bool:
+        """ops.graph_bpr covers the GPU configuration: fp32 d=64 contiguous tables, CSR adjacencies
+        (the Trainer's swap), at least one layer of each propagation."""
+        from FoodRec.engine.graph import Adjacency
+        ws = (self.user_embedding.weight, self.item_embedding.weight, self.ingre_embedding.weight)
+        return (FUSED_GRAPH and ids.is_cuda and all(w.is_cuda and w.dtype == torch.float32 and w.shape[1] == 64
+                                                     and w.is_contiguous() for w in ws)
+                and isinstance(self.norm_adj_matrix, Adjacency) and isinstance(self.ri_norm_adj, Adjacency)
+                and self.n_layers >= 1 and self.ui_layers >= 1)
 
     def _row_tables(self):
         return [getattr(self, n) for n in ("image_embedding", "text_embedding") if hasattr(self, n)]

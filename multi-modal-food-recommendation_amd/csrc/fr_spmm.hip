@@ -39,48 +39,107 @@ __device__ __forceinline__ float bcast_f(float v) {
   return __int_as_float(bcast_i<LPR, K>(__float_as_int(v)));
 }
 
+// A row table whose rows [0, split) live at lo (stride ld) and rows [split, n) at hi (stride ldh,
+// row r at hi + (r - split) * ldh); hi == nullptr: every row at lo.  Lets a propagation read its
+// ego table as [user table ; item table] and write its gradient into the parameters' own buffers
+// (no concatenation, no split copies).
+struct Tab {
+  const float* lo; int64_t ld;
+  const float* hi; int64_t ldh;
+};
+
+__device__ __forceinline__ const float* tab_row(const Tab& t, int64_t r, int64_t split) {
+  return (t.hi != nullptr && r >= split) ? t.hi + (r - split) * t.ldh : t.lo + r * t.ld;
+}
+
 struct Epi {
-  float* Y1; int64_t ldy1;
-  float* Y2; int64_t ldy2; float alpha;
-  const float* A1; int64_t lda1; float beta1;
-  const float* A2; int64_t lda2; float beta2;
+  Tab Y1;
+  Tab Y2; float alpha;
+  Tab A1; float beta1;
+  Tab A2; float beta2;
+  int64_t split;
 };
 
 // write one row's result (float4 slot q of row r) through the fused epilogue
 __device__ __forceinline__ void epilogue(const Epi& ep, int64_t r, int q, float4 acc) {
-  if (ep.Y1) reinterpret_cast<float4*>(ep.Y1 + r * ep.ldy1)[q] = acc;
-  if (ep.Y2) {
+  if (ep.Y1.lo) reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y1, r, ep.split)))[q] = acc;
+  if (ep.Y2.lo) {
     float4 o = f4_scale(ep.alpha, acc);
-    if (ep.A1) o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(ep.A1 + r * ep.lda1)[q], o);
-    if (ep.A2) o = f4_fma(ep.beta2, reinterpret_cast<const float4*>(ep.A2 + r * ep.lda2)[q], o);
-    reinterpret_cast<float4*>(ep.Y2 + r * ep.ldy2)[q] = o;
+    if (ep.A1.lo) o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q], o);
+    if (ep.A2.lo) o = f4_fma(ep.beta2, reinterpret_cast<const float4*>(tab_row(ep.A2, r, ep.split))[q], o);
+    reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
   }
 }
 
+// X operand of the gather: [lo ; hi] split at `split` (SPLIT), columns masked by cmask (MASK:
+// an edge whose column has cmask == 0 is skipped -- its row of X is known to be zero).
+struct XSrc {
+  const float4* lo; int64_t ld4;
+  const float4* hi; int64_t ldh4;
+  int64_t split;
+  const uint8_t* cmask;
+};
+
+// a zero row for masked-out edges (d <= 1024 -> at most 256 float4); zero-initialised at load
+__device__ float4 g_zero_row[256];
+
+
 // Gather-accumulate edges [e0, e1) of one unit into acc (slot q of an LPR-lane group).
 // Rows wider than LPR float4 slots are handled by the caller's group-uniform slot loop.
-template <int LPR>
+// Plain tables broadcast the edge's column and address X from it; split tables (SPLIT) and masked
+// gathers (MASK) resolve every lane's row address once, before the broadcasts, as a float4 offset
+// from xs.lo (the hi table, or the zero row of a masked-out edge, expressed relative to lo), so the
+// 16 gathers of a batch stay branch-free.
+template <int LPR, bool SPLIT, bool MASK>
 __device__ __forceinline__ float4 gather_unit(const int32_t* __restrict__ col,
-                                              const float* __restrict__ val,
-                                              const float4* __restrict__ X4, int64_t ldx4,
+                                              const float* __restrict__ val, const XSrc& xs,
                                               int64_t e0, int64_t e1, int lig, int q) {
   // lig = lane index inside the group (edge slot of the cooperative col/val load),
   // q   = float4 slot of the row this lane gathers
+  constexpr bool OFF = SPLIT || MASK;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t e = e0; e < e1; e += LPR) {
     const int64_t my = e + lig;
     const int64_t last = e1 - 1;
     // lanes past the unit's end re-point at its last edge (cache hit) with weight 0
     const int c = __builtin_nontemporal_load(col + (my < e1 ? my : last));
-    const float v = my < e1 ? __builtin_nontemporal_load(val + my) : 0.f;
+    float v = my < e1 ? __builtin_nontemporal_load(val + my) : 0.f;
+    int64_t off = 0;  // float4 offset of this lane's X row from xs.lo (OFF mode)
+    if constexpr (OFF) {
+      if constexpr (SPLIT) {
+        off = c >= xs.split ? (xs.hi - xs.lo) + ((int64_t)c - xs.split) * xs.ldh4 : (int64_t)c * xs.ld4;
+      } else {
+        off = (int64_t)c * xs.ld4;
+      }
+      if constexpr (MASK) {
+        // one mask load per lane, then a group-uniform skip of batches that reach no marked row;
+        // the remaining masked-out edges read the (cached) zero row with weight 0
+        const bool m = my < e1 && xs.cmask[c] != 0;
+        const uint64_t bal = __ballot(m);
+        const int gbase = (threadIdx.x & 63) & ~(LPR - 1);
+        const uint64_t gmask = LPR >= 64 ? ~0ull : ((1ull << LPR) - 1ull);
+        if (((bal >> gbase) & gmask) == 0) continue;
+        if (!m) {
+          v = 0.f;
+          off = g_zero_row - xs.lo;
+        }
+      }
+    }
+    const int off_lo = (int)(uint32_t)(uint64_t)off, off_hi = (int)(uint32_t)((uint64_t)off >> 32);
     constexpr int NB = LPR < 16 ? LPR : 16;
     float4 x[NB];
     float w[NB];
-#define FR_GATHER(K)                                                         \
-    if constexpr ((K) < LPR) {                                               \
-      const int ck = bcast_i<LPR, (K)>(c);                                   \
-      w[(K)] = bcast_f<LPR, (K)>(v);                                         \
-      x[(K)] = X4[(int64_t)ck * ldx4 + q];                                   \
+#define FR_GATHER(K)                                                                        \
+    if constexpr ((K) < LPR) {                                                              \
+      w[(K)] = bcast_f<LPR, (K)>(v);                                                        \
+      if constexpr (OFF) {                                                                  \
+        const uint64_t ok = (uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_lo) |                 \
+                            ((uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_hi) << 32);          \
+        x[(K)] = xs.lo[(int64_t)ok + q];                                                    \
+      } else {                                                                              \
+        const int ck = bcast_i<LPR, (K)>(c);                                                \
+        x[(K)] = xs.lo[(int64_t)ck * xs.ld4 + q];                                           \
+      }                                                                                     \
     }
     FR_GATHER(0) FR_GATHER(1) FR_GATHER(2) FR_GATHER(3)
     FR_GATHER(4) FR_GATHER(5) FR_GATHER(6) FR_GATHER(7)
@@ -94,26 +153,30 @@ __device__ __forceinline__ float4 gather_unit(const int32_t* __restrict__ col,
       for (int k = 16; k < LPR; ++k) {
         const int lane = threadIdx.x & 63;
         const int src = (lane & ~(LPR - 1)) | k;
-        const int ck = __shfl(c, src, 64);
         const float wk = __shfl(v, src, 64);
-        acc = f4_fma(wk, X4[(int64_t)ck * ldx4 + q], acc);
+        if constexpr (OFF) {
+          const uint64_t ok = (uint64_t)(uint32_t)__shfl(off_lo, src, 64) |
+                              ((uint64_t)(uint32_t)__shfl(off_hi, src, 64) << 32);
+          acc = f4_fma(wk, xs.lo[(int64_t)ok + q], acc);
+        } else {
+          const int ck = __shfl(c, src, 64);
+          acc = f4_fma(wk, xs.lo[(int64_t)ck * xs.ld4 + q], acc);
+        }
       }
     }
   }
   return acc;
 }
 
-template <int LPR>
+template <int LPR, bool SPLIT, bool MASK>
 __global__ __launch_bounds__(256) void spmm_units_kernel(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int2* __restrict__ units, int64_t n_units,
-    int64_t n_plain, int chunk, const float* __restrict__ X, int64_t ldx, int d4, Epi ep,
+    int64_t n_plain, int chunk, XSrc xs, int d4, Epi ep,
     float4* __restrict__ partial) {
   constexpr int GPB = 256 / LPR;  // groups per block
   const int q0 = threadIdx.x % LPR;
   const int grp = threadIdx.x / LPR;
-  const float4* X4 = reinterpret_cast<const float4*>(X);
-  const int64_t ldx4 = ldx >> 2;
   for (int64_t u = (int64_t)blockIdx.x * GPB + grp; u < n_units; u += (int64_t)gridDim.x * GPB) {
     const int2 unit = units[u];
     const int64_t rs = rowptr[unit.x];
@@ -122,7 +185,7 @@ __global__ __launch_bounds__(256) void spmm_units_kernel(
     // group-uniform slot loop: every lane of the group takes part in the broadcasts
     for (int qb = 0; qb < d4; qb += LPR) {
       const int q = qb + q0;
-      const float4 acc = gather_unit<LPR>(col, val, X4, ldx4, e0, e1, q0, q < d4 ? q : d4 - 1);
+      const float4 acc = gather_unit<LPR, SPLIT, MASK>(col, val, xs, e0, e1, q0, q < d4 ? q : d4 - 1);
       if (q < d4) {
         if (u < n_plain) {
           epilogue(ep, unit.x, q, acc);
@@ -152,19 +215,85 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(const int3* __restrict_
   }
 }
 
+// Row-list mode: only the rows named by `rl` (up to three id segments, each shifted by its
+// offset; duplicates allowed -- they write identical values) are computed, one 1024-thread
+// workgroup per listed row: the row's 16-edge batches are dealt round-robin to the 64 lane groups
+// and the 64 group partials are summed in group order (deterministic; the summation order differs
+// from the full launch's, so rows agree with it to fp32 rounding).  A heavy row (an item with
+// thousands of users) costs a few batches per group instead of a serial chain.
+struct RowList {
+  const int64_t* ids[3];
+  int64_t n[3];
+  int64_t off[3];
+};
+
+constexpr int kRowThreads = 1024;
+
+template <int LPR, bool SPLIT>
+__global__ __launch_bounds__(kRowThreads) void spmm_rows_kernel(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, RowList rl, XSrc xs, int d4, Epi ep) {
+  static_assert(LPR == 16, "row-list mode is built for d = 64 (16 lanes x float4)");
+  constexpr int GPB = kRowThreads / LPR;
+  __shared__ float4 slots[GPB][LPR];
+  const int q0 = threadIdx.x % LPR;
+  const int grp = threadIdx.x / LPR;
+  int64_t idx = blockIdx.x;
+  int seg = 0;
+  while (seg < 3 && idx >= rl.n[seg]) idx -= rl.n[seg++];
+  if (seg >= 3) return;
+  const int64_t row = rl.ids[seg][idx] + rl.off[seg];
+  const int64_t rs = rowptr[row], re = rowptr[row + 1];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t e0 = rs + (int64_t)grp * LPR; e0 < re; e0 += (int64_t)GPB * LPR) {
+    const int64_t e1 = e0 + LPR < re ? e0 + LPR : re;
+    acc = f4_add(acc, gather_unit<LPR, SPLIT, false>(col, val, xs, e0, e1, q0, q0));
+  }
+  slots[grp][q0] = acc;
+  __syncthreads();
+  if (grp == 0) {
+    float4 t = slots[0][q0];
+    for (int g = 1; g < GPB; ++g) t = f4_add(t, slots[g][q0]);
+    epilogue(ep, row, q0, t);
+  }
+}
+
+__global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ mask, RowList rl, int64_t total,
+                                                        uint8_t value) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int64_t idx = i;
+    int seg = 0;
+    while (idx >= rl.n[seg]) idx -= rl.n[seg++];
+    mask[rl.ids[seg][idx] + rl.off[seg]] = value;
+  }
+}
+
+template <int LPR, bool SPLIT, bool MASK>
+hipError_t launch_units(const int64_t* rowptr, const int32_t* col, const float* val,
+                        const fr_spmm_plan* plan, const XSrc& xs, int d4, const Epi& ep,
+                        float4* partial, hipStream_t s) {
+  constexpr int GPB = 256 / LPR;
+  int64_t blocks = fr::ceil_div(plan->n_units, GPB);
+  blocks = std::min<int64_t>(blocks, (int64_t)fr::kNumCU * 64);
+  hipLaunchKernelGGL((spmm_units_kernel<LPR, SPLIT, MASK>), dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col,
+                     val, reinterpret_cast<const int2*>(plan->d_units), plan->n_units,
+                     plan->n_plain, plan->chunk, xs, d4, ep, partial);
+  return hipGetLastError();
+}
+
 template <int LPR>
 hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
-                       const fr_spmm_plan* plan, const float* X, int64_t ldx, int d, const Epi& ep,
+                       const fr_spmm_plan* plan, const XSrc& xs, int d, const Epi& ep,
                        float4* partial, hipStream_t s) {
   constexpr int GPB = 256 / LPR;
   const int d4 = d / 4;
+  const bool split = xs.hi != nullptr, mask = xs.cmask != nullptr;
   if (plan->n_units > 0) {
-    int64_t blocks = fr::ceil_div(plan->n_units, GPB);
-    blocks = std::min<int64_t>(blocks, (int64_t)fr::kNumCU * 64);
-    hipLaunchKernelGGL(spmm_units_kernel<LPR>, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col,
-                       val, reinterpret_cast<const int2*>(plan->d_units), plan->n_units,
-                       plan->n_plain, plan->chunk, X, ldx, d4, ep, partial);
-    hipError_t e = hipGetLastError();
+    hipError_t e;
+    if (split && mask) e = launch_units<LPR, true, true>(rowptr, col, val, plan, xs, d4, ep, partial, s);
+    else if (split) e = launch_units<LPR, true, false>(rowptr, col, val, plan, xs, d4, ep, partial, s);
+    else if (mask) e = launch_units<LPR, false, true>(rowptr, col, val, plan, xs, d4, ep, partial, s);
+    else e = launch_units<LPR, false, false>(rowptr, col, val, plan, xs, d4, ep, partial, s);
     if (e != hipSuccess) return e;
   }
   if (plan->n_split > 0) {
@@ -224,49 +353,131 @@ extern "C" int fr_spmm_plan_host(const int64_t* rowptr, int64_t n_rows, int32_t 
   return FR_OK;
 }
 
+namespace {
+
+Tab host_tab(const fr_tab* t) {
+  if (t == nullptr || t->lo == nullptr) return Tab{nullptr, 0, nullptr, 0};
+  return Tab{t->lo, t->ld_lo, t->hi, t->ld_hi};
+}
+
+bool tab_ok(const fr_tab* t, int d) {
+  if (t == nullptr || t->lo == nullptr) return true;
+  if (!(t->ld_lo >= d && t->ld_lo % 4 == 0 && fr::aligned16(t->lo))) return false;
+  return t->hi == nullptr || (t->ld_hi >= d && t->ld_hi % 4 == 0 && fr::aligned16(t->hi));
+}
+
+bool tab_touches(const fr_tab* t, const void* p) {
+  return t != nullptr && p != nullptr && (t->lo == p || t->hi == p);
+}
+
+int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+              const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
+              const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
+              const uint8_t* col_mask, const fr_rowlist* rows, void* d_workspace, int64_t workspace_bytes,
+              void* stream, const char* who) {
+  FR_REQUIRE(plan != nullptr, "plan is null");
+  FR_REQUIRE(d > 0 && d % 4 == 0 && d <= 1024, "d must be a positive multiple of 4, <= 1024");
+  FR_REQUIRE(n_rows >= 0, "n_rows < 0");
+  if (n_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && X && X->lo, "rowptr/X null");
+  FR_REQUIRE((Y1 && Y1->lo) || (Y2 && Y2->lo), "no output requested");
+  FR_REQUIRE(plan->n_units == 0 || (plan->d_units && d_col && d_val), "plan/col/val null");
+  FR_REQUIRE(plan->n_split == 0 || plan->d_split_rows, "split_rows null");
+  FR_REQUIRE(plan->chunk > 0, "plan chunk must be > 0");
+  FR_REQUIRE(tab_ok(X, d), "X must be 16-B aligned, ld % 4 == 0, ld >= d");
+  FR_REQUIRE(tab_ok(Y1, d) && tab_ok(Y2, d) && tab_ok(A1, d) && tab_ok(A2, d), "bad Y1/Y2/A1/A2 table");
+  FR_REQUIRE(split >= 0, "split < 0");
+  for (const fr_tab* y : {Y1, Y2})
+    FR_REQUIRE(!(y && (tab_touches(y, X->lo) || tab_touches(y, X->hi))), "outputs must not alias X");
+  const int64_t need = fr_spmm_workspace(plan, d);
+  FR_REQUIRE(rows != nullptr || plan->n_split == 0 ||
+             (d_workspace && workspace_bytes >= need && fr::aligned16(d_workspace)),
+             "workspace too small (need " + std::to_string(need) + " bytes)");
+  Epi ep{host_tab(Y1), host_tab(Y2), alpha, host_tab(A1), beta1, host_tab(A2), beta2,
+         split};
+  XSrc xs{reinterpret_cast<const float4*>(X->lo), X->ld_lo >> 2, reinterpret_cast<const float4*>(X->hi),
+          X->hi ? (X->ld_hi >> 2) : 0, X->hi ? split : INT64_MAX, col_mask};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float4* partial = reinterpret_cast<float4*>(d_workspace);
+  const int d4 = d / 4;
+  hipError_t e = hipSuccess;
+  if (rows != nullptr) {
+    FR_REQUIRE(d4 == 16, "row-list mode supports d = 64");
+    FR_REQUIRE(col_mask == nullptr, "row-list mode takes no column mask");
+    RowList rl{};
+    int64_t total = 0;
+    for (int k = 0; k < 3; ++k) {
+      FR_REQUIRE(rows->n[k] >= 0 && (rows->n[k] == 0 || rows->ids[k]), "bad row segment");
+      rl.ids[k] = rows->ids[k];
+      rl.n[k] = rows->n[k];
+      rl.off[k] = rows->off[k];
+      total += rows->n[k];
+    }
+    if (total == 0) return FR_OK;
+    if (xs.hi) {
+      hipLaunchKernelGGL((spmm_rows_kernel<16, true>), dim3((unsigned)total), dim3(kRowThreads), 0, s, d_rowptr,
+                         d_col, d_val, rl, xs, d4, ep);
+    } else {
+      hipLaunchKernelGGL((spmm_rows_kernel<16, false>), dim3((unsigned)total), dim3(kRowThreads), 0, s, d_rowptr,
+                         d_col, d_val, rl, xs, d4, ep);
+    }
+    e = hipGetLastError();
+  } else if (d4 >= 64) {
+    e = launch_spmm<64>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  } else if (d4 >= 32) {
+    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s)
+                   : launch_spmm<16>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  } else if (d4 >= 16) {
+    e = launch_spmm<16>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  } else if (d4 >= 8) {
+    e = launch_spmm<8>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  } else if (d4 >= 4) {
+    e = launch_spmm<4>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  } else {
+    e = launch_spmm<1>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+  }
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string(who) + ": " + hipGetErrorString(e));
+  return FR_OK;
+}
+
+}  // namespace
+
 extern "C" int fr_spmm_csr(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
                            int64_t n_rows, const fr_spmm_plan* plan, const float* d_X, int64_t ldx,
                            int d, float* d_Y1, int64_t ldy1, float* d_Y2, int64_t ldy2,
                            float alpha, const float* d_A1, int64_t lda1, float beta1,
                            const float* d_A2, int64_t lda2, float beta2, void* d_workspace,
                            int64_t workspace_bytes, void* stream) {
-  FR_REQUIRE(plan != nullptr, "plan is null");
-  FR_REQUIRE(d > 0 && d % 4 == 0 && d <= 1024, "d must be a positive multiple of 4, <= 1024");
-  FR_REQUIRE(n_rows >= 0, "n_rows < 0");
-  if (n_rows == 0) return FR_OK;
-  FR_REQUIRE(d_rowptr && d_X, "rowptr/X null");
-  FR_REQUIRE(d_Y1 || d_Y2, "no output requested");
-  FR_REQUIRE(plan->n_units == 0 || (plan->d_units && d_col && d_val), "plan/col/val null");
-  FR_REQUIRE(plan->n_split == 0 || plan->d_split_rows, "split_rows null");
-  FR_REQUIRE(plan->chunk > 0, "plan chunk must be > 0");
-  FR_REQUIRE(ldx >= d && ldx % 4 == 0 && fr::aligned16(d_X), "X must be 16-B aligned, ldx%4==0");
-  FR_REQUIRE(!d_Y1 || (ldy1 >= d && ldy1 % 4 == 0 && fr::aligned16(d_Y1)), "bad Y1");
-  FR_REQUIRE(!d_Y2 || (ldy2 >= d && ldy2 % 4 == 0 && fr::aligned16(d_Y2)), "bad Y2");
-  FR_REQUIRE(!d_A1 || (lda1 >= d && lda1 % 4 == 0 && fr::aligned16(d_A1)), "bad A1");
-  FR_REQUIRE(!d_A2 || (lda2 >= d && lda2 % 4 == 0 && fr::aligned16(d_A2)), "bad A2");
-  FR_REQUIRE(d_Y1 != d_X && d_Y2 != d_X, "outputs must not alias X");
-  const int64_t need = fr_spmm_workspace(plan, d);
-  FR_REQUIRE(plan->n_split == 0 || (d_workspace && workspace_bytes >= need && fr::aligned16(d_workspace)),
-             "workspace too small (need " + std::to_string(need) + " bytes)");
-  Epi ep{d_Y1, ldy1, d_Y2, ldy2, alpha, d_A1, lda1, beta1, d_A2, lda2, beta2};
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  float4* partial = reinterpret_cast<float4*>(d_workspace);
-  const int d4 = d / 4;
-  hipError_t e;
-  if (d4 >= 64) {
-    e = launch_spmm<64>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
-  } else if (d4 >= 32) {
-    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s)
-                   : launch_spmm<16>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
-  } else if (d4 >= 16) {
-    e = launch_spmm<16>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
-  } else if (d4 >= 8) {
-    e = launch_spmm<8>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
-  } else if (d4 >= 4) {
-    e = launch_spmm<4>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
-  } else {
-    e = launch_spmm<1>(d_rowptr, d_col, d_val, plan, d_X, ldx, d, ep, partial, s);
+  const fr_tab X{d_X, ldx, nullptr, 0}, Y1{d_Y1, ldy1, nullptr, 0}, Y2{d_Y2, ldy2, nullptr, 0};
+  const fr_tab A1{d_A1, lda1, nullptr, 0}, A2{d_A2, lda2, nullptr, 0};
+  return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, 0, &X, d, &Y1, &Y2, alpha, &A1, beta1, &A2, beta2,
+                   nullptr, nullptr, d_workspace, workspace_bytes, stream, "fr_spmm_csr");
+}
+
+extern "C" int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                              const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
+                              const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
+                              float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, void* d_workspace,
+                              int64_t workspace_bytes, void* stream) {
+  return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, split, X, d, Y1, Y2, alpha, A1, beta1, A2, beta2,
+                   d_col_mask, rows, d_workspace, workspace_bytes, stream, "fr_spmm_csr_ex");
+}
+
+extern "C" int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream) {
+  FR_REQUIRE(d_mask != nullptr && rows != nullptr, "null argument");
+  RowList rl{};
+  int64_t total = 0;
+  for (int k = 0; k < 3; ++k) {
+    FR_REQUIRE(rows->n[k] >= 0 && (rows->n[k] == 0 || rows->ids[k]), "bad row segment");
+    rl.ids[k] = rows->ids[k];
+    rl.n[k] = rows->n[k];
+    rl.off[k] = rows->off[k];
+    total += rows->n[k];
   }
-  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_spmm_csr: ") + hipGetErrorString(e));
+  if (total == 0) return FR_OK;
+  const int64_t blocks = std::min<int64_t>(fr::ceil_div(total, (int64_t)256), (int64_t)fr::kNumCU * 4);
+  hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     d_mask, rl, total, value);
+  FR_LAUNCH_CHECK();
   return FR_OK;
 }

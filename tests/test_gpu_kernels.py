@@ -430,3 +430,91 @@ def test_layernorm_matches_fp64(cuda, rows, d, eps, affine):
         sw = (gy.double().abs() * xhat.abs()).sum(0)
         assert torch.all((dw.double() - wr.grad).abs() <= 1e-5 * sw + 1e-6)
         assert torch.all((db.double() - br.grad).abs() <= 1e-5 * gy.double().abs().sum(0) + 1e-6)
+
+
+def test_spmm_ex_split_rows_mask_bitwise(cuda):
+    """fr_spmm_csr_ex against fr_spmm_csr on the concatenated tables: split X / A1 / Y2 ([lo ; hi]
+    at a row) and a column mask over an X that is zero outside the mask bit for bit; the row-list
+    mode (listed rows only, duplicates allowed, heavy rows spread over the workgroup) to fp32
+    rounding and run-to-run identical."""
+    from FoodRec.engine import ops
+    n, d, split = 1500, 64, 600
+    r, c = _graph(n, n, 8, heavy=[(3, 1400), (700, 900), (11, 129)], seed=21)
+    adj = _adj(n, r, c, cuda, chunk=128)
+    assert adj.n_split >= 2
+    lo = torch.randn(split, d, device=cuda)
+    hi = torch.randn(n - split + 37, d, device=cuda)   # longer than needed: only rows < n - split are read
+    X = torch.cat([lo, hi[:n - split]])
+    full = torch.empty(n, d, device=cuda)
+    ops.spmm_launch(adj, X, Y2=full, alpha=0.5, A1=X, beta1=0.5)
+    y = torch.empty(n, d, device=cuda)
+    ops.spmm_ex(adj, lo, hi, split, Y2=y, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)
+    assert torch.equal(y, full)
+    # split output
+    out_lo, out_hi = torch.empty(split, d, device=cuda), torch.empty(n - split, d, device=cuda)
+    ops.spmm_ex(adj, X, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=0.5, A1=X, beta1=0.5)
+    assert torch.equal(torch.cat([out_lo, out_hi]), full)
+    # row list: three segments with offsets and duplicates, heavy rows included
+    a = torch.tensor([3, 5, 3, 0], device=cuda)
+    b = torch.tensor([100, 200, 1], device=cuda)
+    e = torch.tensor([899, 11], device=cuda)
+    ry = torch.full((n, d), float("nan"), device=cuda)
+    ops.spmm_ex(adj, lo, hi, split, Y2=ry, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5,
+                rows=[(a, 0), (b, split), (e, 1)], region="spmm_rows")
+    listed = torch.unique(torch.cat([a, b + split, e + 1]))
+    # row-list rows: deterministic, summed in another order than the full launch (fp32 rounding)
+    torch.testing.assert_close(ry[listed], full[listed], rtol=1e-5, atol=1e-6)
+    ry2 = torch.full((n, d), float("nan"), device=cuda)
+    ops.spmm_ex(adj, lo, hi, split, Y2=ry2, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5,
+                rows=[(a, 0), (b, split), (e, 1)], region="spmm_rows")
+    assert torch.equal(ry2[listed], ry[listed])
+    others = torch.ones(n, dtype=torch.bool, device=cuda)
+    others[listed] = False
+    assert torch.isnan(ry[others]).all()
+    # column mask: X zero outside the marked rows
+    mask = torch.zeros(n, dtype=torch.uint8, device=cuda)
+    ops.rows_mark(mask, [(a, 0), (b, split)], 1)
+    assert int(mask.sum()) == len(set([3, 5, 0] + [100 + split, 200 + split, 1 + split]))
+    Xs = X * mask.unsqueeze(1).float()
+    ref = torch.empty(n, d, device=cuda)
+    ops.spmm_launch(adj, Xs, Y2=ref, alpha=0.5, A1=Xs, beta1=0.5)
+    got = torch.empty(n, d, device=cuda)
+    ops.spmm_ex(adj, Xs, Y2=got, alpha=0.5, A1=Xs, beta1=0.5, col_mask=mask)
+    assert torch.equal(got, ref)
+    ops.rows_mark(mask, [(a, 0), (b, split)], 0)
+    assert int(mask.sum()) == 0
+
+
+def test_healthrec_graph_bpr_matches_unfused(cuda):
+    """ops.graph_bpr (split-table propagation, UI rows of the batch only, masked UI backward,
+    gradients written into the parameters' buffers) against the concatenated full propagation +
+    fused BPR op it replaces: losses rel 1e-6, every gradient 1e-5 of its max."""
+    from helpers import golden, tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.models import healthrec
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("model_CIKM_Model.npz")
+    batch = {k[len("batch/"):]: torch.from_numpy(g[k]).to(cuda) for k in g.files if k.startswith("batch/")}
+    runs = []
+    for fused in (True, False):
+        healthrec.FUSED_GRAPH = fused
+        try:
+            cfg = tiny_config("CIKM_Model", True)
+            data = tiny_data(cfg)
+            init_seed(999)
+            model = get_model("CIKM_Model")(cfg, data).to(cuda)
+            tr = Trainer(cfg, model)
+            tr.optimizer.zero_grad()
+            losses = model.calculate_loss(batch)
+            sum(losses).backward()
+            tr.optimizer.materialize_row_grads()
+            runs.append(([float(x.detach().reshape(-1)[0]) for x in losses],
+                         {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}))
+        finally:
+            healthrec.FUSED_GRAPH = True
+    (la, ga), (lb, gb) = runs
+    np.testing.assert_allclose(la, lb, rtol=1e-6)
+    assert ga.keys() == gb.keys()
+    for k in ga:
+        err = (ga[k] - gb[k]).abs().max().item()
+        assert err <= 1e-5 * gb[k].abs().max().item() + 1e-9, (k, err)

@@ -471,3 +471,40 @@ def test_lazy_rows_state_dict_round_trip(cuda):
     for s_ in ("exp_avg", "exp_avg_sq"):
         assert torch.equal(oa.state[pa][s_], ob.state[pb][s_]), s_
     assert int(ob.state[pb]["step"].item()) == 10
+
+
+def test_feed_batch_one_launch_matches_gathers(cuda):
+    """fr_feed_batch (DeviceFeed.fill with the batch features): (u, pos, neg) equal to the golden
+    reference stream and to the index_select feed, and the [pos; neg] features (item ids, ingredient
+    codes, counts, health multi-hot, padding mask) equal to torch gathers of the side tables; the
+    plain-mode gather (LazyBatch pn_ keys) equal too."""
+    from helpers import golden, tiny_config, tiny_data
+    from FoodRec.engine.sampler import BatchFeatures, TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("stream.npz")
+    cfg = tiny_config("CIKM_Model", False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    get_model("LightGCN")(tiny_config("LightGCN", False), tiny_data(tiny_config("LightGCN", False)))
+    B = int(g["batch_size"])
+    s = TripleSampler(data, B, cuda)
+    feed = s.device_feed()
+    feats = BatchFeatures(data, cuda)
+    out = tuple(torch.zeros(B, dtype=torch.int64, device=cuda) for _ in range(3))
+    got = []
+    for u, p, n in s.epoch(out=out, feed=feed):
+        if u is out[0]:
+            pre = feed.fill(*out, feats)
+            assert pre is not None
+            pn = torch.cat([out[1], out[2]])
+            assert torch.equal(pre["pn_i_id"], pn)
+            assert torch.equal(pre["pn_ingre_code"], feats.ingre_code[pn])
+            assert torch.equal(pre["pn_ingre_num"], feats.ingre_num[pn])
+            assert torch.equal(pre["pn_hl_mh"], feats.health[pn])
+            assert torch.equal(pre["pn_pad_mask"], feats.ingre_code[pn] == data.num_ingredients)
+            lb = feats.batch(out[0].clone(), out[1].clone(), out[2].clone())  # plain mode (lazy keys)
+            for k in ("pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_mask"):
+                assert torch.equal(lb[k], pre[k]), k
+        got.append([x.cpu().numpy().copy() for x in (u, p, n)])
+    for k, key in enumerate("upn"):
+        np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep0/{key}"])
