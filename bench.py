@@ -57,6 +57,8 @@ def _args():
                     help="skip BASELINE config 3 (CLUSSL on Foodcom-shape data, dCor and InfoNCE SSL)")
     ap.add_argument("--no-config5", action="store_true",
                     help="skip BASELINE config 5 (d=256 bf16 tables, full-sort top-k on MFMA)")
+    ap.add_argument("--no-config1", action="store_true",
+                    help="skip BASELINE config 1 (BPRMF on Allrecipes-shape data, GPU step + CPU oracle)")
     return ap.parse_args()
 
 
@@ -129,6 +131,17 @@ def main():
                 yield t
 
     it = batches()
+    # per-epoch sampling (permutation, the epoch's negatives in one native call, H2D copy, staging)
+    # runs once per 1,323-step epoch, outside the steps: timed here on its own and amortised into
+    # `value` (epoch_sampling_ms / steps_per_epoch per step)
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    probe = sampler.epoch(out=graphed.inputs if graphed is not None else None, feed=feed)
+    next(probe)
+    torch.cuda.synchronize()
+    epoch_ms = (time.perf_counter() - te0) * 1e3
+    del probe
+    steps_per_epoch = len(sampler)
 
     def do_step(i):
         u, p, n = next(it)
@@ -173,9 +186,10 @@ def main():
     kern = timer.summary()
     ksteps = max(1, args.kernel_steps)
 
-    ms_per_step = elapsed / args.steps * 1e3
+    ms_steps = elapsed / args.steps * 1e3
+    ms_per_step = ms_steps + epoch_ms / steps_per_epoch
     triples = args.batch * args.steps * world
-    value = triples / elapsed
+    value = triples / (ms_per_step * 1e-3 * args.steps)
 
     dom_name = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
     traffic = args.traffic if args.traffic is not None else pmc_traffic(dom_name)
@@ -187,7 +201,19 @@ def main():
                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                     "traffic": traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
                     "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / ksteps,
-                    "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3)}
+                    "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3),
+                    "timing_source": "HIP events per launch on the launch stream, eager pass of "
+                                     f"{ksteps} steps right after the timed region (kernels.{dom_name})",
+                    "residency": ("the gathered X tables (<= 29 MB) sit in the 256 MB Infinity Cache (MALL): "
+                                  "this is a cache-level rate; the HBM-level SpMM roofline is config4_10m.spmm"
+                                  if dom_name == "spmm" else None)}
+    # step-level figure: algorithmic bytes of every timed region per step / the graphed step time
+    step_bytes = sum(v["bytes_per_launch"] * v["launches"] for v in kern.values()) / ksteps
+    step_fig = {"algorithmic_bytes_per_step": int(step_bytes),
+                "achieved_gbps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                "frac_of_hbm_peak": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "note": "sum over the engine's timed regions (their byte models) per step; latency-bound "
+                        "step: ~80 launches of mostly L2/MALL-resident work"}
     spmm = None
     if "spmm" in kern:
         s = kern["spmm"]
@@ -217,6 +243,9 @@ def main():
     c5 = None
     if world == 1 and not args.no_config5:
         c5 = config5(device)
+    c1 = None
+    if world == 1 and not args.no_config1:
+        c1 = config1(device, cpu=not args.no_cpu_baseline)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -231,8 +260,13 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else "single"},
-                "roofline": roofline, "spmm": spmm, "config3_clussl_foodcom": c3, "config4_10m": c4, "config5_10m_bf16": c5, "kernels": kernels,
-                "cpu_baseline": cpu}
+                "roofline": roofline, "step_bytes": step_fig,
+                "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "steps_per_epoch": steps_per_epoch,
+                                   "ms_per_step_without": round(ms_steps, 4),
+                                   "note": "value and ms_per_step include epoch_sampling.ms_per_epoch / "
+                                           "steps_per_epoch per step"},
+                "spmm": spmm, "config1_bprmf_allrecipes": c1, "config3_clussl_foodcom": c3, "config4_10m": c4,
+                "config5_10m_bf16": c5, "kernels": kernels, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -500,6 +534,38 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
            "byte_model": "SURVEY 8(d): 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2"}
     del trainer, model, g, adj
     torch.cuda.empty_cache()
+    out["spmm_beyond_mall"] = spmm_beyond_mall(device)
+    return out
+
+
+def spmm_beyond_mall(device, iters=5):
+    """The config-4 SpMM with every gathered table far beyond the 256 MB Infinity Cache: 10M users x
+    4M items (the item block of X is 1 GiB, the user block 2.56 GB), ~200M interactions, d=64 fp32 --
+    the byte model then counts DRAM traffic, not MALL hits (the 1M-item table of config 4 is the
+    MALL's size)."""
+    import torch
+    from FoodRec.engine import ops
+    from FoodRec.utils.interaction_graph import InteractionGraph
+    U, I, d = 10_000_000, 4_000_000, 64
+    g = InteractionGraph(U, I, 20.0, seed=1, device=device)
+    adj = g.adj
+    X = torch.randn(U + I, d, device=device)
+    Y = torch.empty_like(X)
+    ops.spmm_launch(adj, X, Y1=Y)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(iters):
+        ops.spmm_launch(adj, X, Y1=Y)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / iters
+    b = ops.spmm_bytes(adj, d, 1)
+    out = {"graph": "synthetic U=10M I=4M E=%d (nnz=%d)" % (g.n_edges, adj.nnz), "item_table_mb": I * d * 4 / 2**20,
+           "avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
+           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4)}
+    del X, Y, g, adj
+    torch.cuda.empty_cache()
     return out
 
 
@@ -574,6 +640,8 @@ def cpu_baseline(args):
     """Time the oracle's CPU restatement of the same step on this host (bounded sample)."""
     import torch
     from oracle import cpu_backend
+    # the GPU box gives one GPU's job a 16-CPU share of the host (OMP_NUM_THREADS=16 there); the
+    # host's total core count is reported beside it
     threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 16)
     torch.set_num_threads(threads)
     with cpu_backend.installed():
@@ -594,8 +662,86 @@ def cpu_baseline(args):
             trainer.train_step(feats.batch(u, p, n), 1 + i, state)
         dt = time.perf_counter() - t0
     return {"value": round(args.batch * k / dt, 2), "unit": "triples/s", "cores": threads, "kind": "port",
+            "host_cores_total": os.cpu_count(),
             "sample": f"{k} HealthRec training steps (B={args.batch}) of the torch-CPU oracle after 1 warm-up",
             "ms_per_step": round(dt / k * 1e3, 1)}
+
+
+def config1(device, steps=50, warmup=5, cpu=True, cpu_steps=20):
+    """BASELINE config 1: BPRMF (ID embeddings, no graph: the reference-style plugin of
+    oracle/ref_plugins) on the Allrecipes-shape synthetic data, d=64, B=1024 (overall.yaml's batch:
+    the reference ships no BPRMF.yaml), graphed training step on the GPU; beside it the torch-CPU
+    oracle of the same step on this host's CPU share (the reference's CPU trainer path)."""
+    import numpy as np
+    import torch
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.dataset import FoodData
+    from FoodRec.utils.synthetic import make_synthetic
+    from FoodRec.utils.utils import get_model, init_seed
+    from oracle import cpu_backend
+    B = 1024
+    data = FoodData.from_synthetic(make_synthetic("allrecipes", 0, negatives=False))
+
+    def make(dev):
+        cfg = Config("BPRMF", "Allrecipes", {"use_gpu": dev.type == "cuda", "seed": 999, "cuda_graph": True,
+                                             "train_batch_size": B, "reg_weight": 0.1, "log_root": "/tmp/frlog/",
+                                             "ckp_root": "/tmp/frckp/"})
+        cfg["device"] = dev
+        init_seed(999)
+        return cfg, get_model("BPRMF")(cfg, data).to(dev)
+
+    cfg, model = make(device)
+    tr = Trainer(cfg, model)
+    np.random.seed(3000)
+    sampler = TripleSampler(data, B, device, replay_python_random=False)
+    g = tr.graphed_step(B, warmup=3)
+    feed = g.attach_feed(sampler)
+    state = g.state
+    model.train()
+
+    def batches():
+        while True:
+            for t in sampler.epoch(out=g.inputs, feed=feed):
+                yield t
+
+    it = batches()
+    for i in range(warmup):
+        g(*next(it), i, state)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        g(*next(it), warmup + i, state)
+    tr.flush_optimizer()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    assert not int(state["nan"].item()), "NaN loss in the config-1 step"
+    out = {"model": "BPRMF (ID-only, no graph), d=64, B=1024", "dataset": "Allrecipes-shape synthetic",
+           "steps_timed": steps, "ms_per_step": round(dt * 1e3, 4), "triples_per_s": round(B / dt, 1)}
+    del tr, model, g, sampler, state, it
+    torch.cuda.empty_cache()
+    if cpu:
+        threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 16)
+        torch.set_num_threads(threads)
+        with cpu_backend.installed():
+            ccfg, cmodel = make(torch.device("cpu"))
+            ctr = Trainer(ccfg, cmodel)
+            cs = TripleSampler(data, B, "cpu", replay_python_random=False)
+            feats = ctr._features()
+            st = ctr.new_step_state()
+            cit = cs.epoch()
+            u, p, n = next(cit)
+            ctr.train_step(feats.batch(u, p, n), 0, st)
+            c0 = time.perf_counter()
+            for i in range(cpu_steps):
+                u, p, n = next(cit)
+                ctr.train_step(feats.batch(u, p, n), 1 + i, st)
+            cdt = (time.perf_counter() - c0) / cpu_steps
+        out["cpu_baseline"] = {"value": round(B / cdt, 1), "unit": "triples/s", "cores": threads, "kind": "port",
+                               "sample": f"{cpu_steps} BPRMF steps (B={B}) of the torch-CPU oracle after 1 warm-up",
+                               "ms_per_step": round(cdt * 1e3, 2)}
+    return out
 
 
 if __name__ == "__main__":

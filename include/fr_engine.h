@@ -217,6 +217,15 @@ int fr_embedding_bwd(const int64_t* d_idx, int64_t n, const float* d_grad, int64
                      int64_t num_rows, int64_t padding_idx, float* d_out, int64_t ldo,
                      void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* The same scatter with float atomics (run-to-run summation order not fixed; fr_embedding_bwd is
+ * the deterministic form): d_out += scatter, d = 64; rows equal to hot_row (e.g. an ingredient
+ * padding id that fills half the positions) are pre-summed per workgroup (one atomic row update per
+ * workgroup).  The caller zero-fills d_out for a plain embedding gradient.  2 launches (fill + this)
+ * instead of the sort path's 8. */
+int fr_embedding_bwd_atomic(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                            int64_t num_rows, int64_t padding_idx, int64_t hot_row, float* d_out, int64_t ldo,
+                            void* stream);
+
 /* Row-gradient form of the same scatter: rmap[r] = the first position i with idx[i] == r (else -1;
  * padding_idx rows get -1) and rows[i, :] = sum over positions j with idx[j] == r of grad[j, :]
  * (the same sums in the same order as fr_embedding_bwd, deterministic); rows of non-owner

@@ -396,11 +396,15 @@ def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None):
     """d/dE of mean_k A^k E (A symmetric) for upstream G, written into [out_lo ; out_hi] split at
     ``split``.  ``col_mask``: rows where G is known to be zero (first layer only)."""
     inv = 1.0 / (L + 1)
+    # a masked launch skips most gathers: not a full-gather (roofline) launch, timed under its own name
+    reg = "spmm_masked" if col_mask is not None else "spmm"
+    nb = 0 if col_mask is not None else None
     if L == 1:
-        spmm_ex(adj, G, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv, A1=G, beta1=inv, col_mask=col_mask)
+        spmm_ex(adj, G, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv, A1=G, beta1=inv, col_mask=col_mask,
+                region=reg, nbytes=nb)
         return
     H = torch.empty_like(G)
-    spmm_ex(adj, G, Y2=H, alpha=inv, A1=G, beta1=inv, col_mask=col_mask)
+    spmm_ex(adj, G, Y2=H, alpha=inv, A1=G, beta1=inv, col_mask=col_mask, region=reg, nbytes=nb)
     H2 = torch.empty_like(G) if L > 2 else None
     for _ in range(1, L - 1):
         spmm_launch(adj, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
@@ -527,10 +531,29 @@ def embedding_bwd_bytes(n: int, rows: int, d: int) -> int:
     return 8 * n + 4 * n * d + 4 * rows * d
 
 
-def scatter_rows(ids: torch.Tensor, G: torch.Tensor, num_rows: int, padding_idx: int | None = None) -> torch.Tensor:
+def scatter_rows(ids: torch.Tensor, G: torch.Tensor, num_rows: int, padding_idx: int | None = None,
+                 hot_row: int | None = None) -> torch.Tensor:
     """Dense ``dW[num_rows, d]`` with ``dW[ids[i]] += G[i]`` for ids in [0, num_rows) other than
-    ``padding_idx`` (others skipped), zeros elsewhere -- the HIP ``fr_embedding_bwd`` (deterministic)."""
+    ``padding_idx`` (others skipped), zeros elsewhere -- the HIP ``fr_embedding_bwd`` (deterministic
+    counting sort).  ``hot_row`` (d = 64, engine not in deterministic mode): a row id expected at many
+    positions; the scatter then runs as fr_embedding_bwd_atomic (zero fill + one launch)."""
     d = G.shape[-1]
+    if hot_row is not None and d == 64 and not _DETERMINISTIC and G.dtype == torch.float32:
+        G2 = G.reshape(-1, d)
+        if G2.stride(1) != 1 or G2.stride(0) % 4 or G2.data_ptr() % 16:
+            G2 = G2.contiguous()
+        ids2 = ids.reshape(-1)
+        if ids2.dtype != torch.int64 or not ids2.is_contiguous():
+            ids2 = ids2.to(torch.int64).contiguous()
+        native.require_device(G2, ids2)
+        n = int(ids2.numel())
+        dW = torch.zeros(int(num_rows), d, dtype=torch.float32, device=G2.device)
+        with profiling.region("embedding_bwd", embedding_bwd_bytes(n, int(num_rows), d)):
+            native.check(native.lib().fr_embedding_bwd_atomic(
+                ids2.data_ptr(), n, G2.data_ptr(), G2.stride(0), d, int(num_rows),
+                -1 if padding_idx is None else int(padding_idx), int(hot_row), dW.data_ptr(), d,
+                native.stream_of(G2)), "fr_embedding_bwd_atomic")
+        return dW
     G = G.reshape(-1, d)
     if G.dtype != torch.float32:
         raise native.EngineError(f"engine ops compute in fp32 (got {G.dtype})")
@@ -637,7 +660,7 @@ class _EmbeddingNorms(torch.autograd.Function):
                         E.data_ptr(), gn.data_ptr(), gn.stride(0), nrm.data_ptr(), out.data_ptr(),
                         native.stream_of(G)), "fr_norms_bwd_coef")
                 G = out
-            return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None), None, None
+            return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None, hot_row=ctx.pad), None, None
         G = torch.zeros_like(E) if gE is None else gE
         if gn is not None:
             coef = (gn / nrm).view(2, 1).expand(2, ctx.half * idx.shape[-1]).reshape(idx.shape)

@@ -633,3 +633,77 @@ extern "C" int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float
   return emb_bwd_impl(d_idx, n, d_grad, ldg, d, num_rows, padding_idx, d_rows, d, d_rmap, d_workspace,
                       reinterpret_cast<hipStream_t>(stream));
 }
+
+// ---------------------------------------------------------------------------------------------
+// Atomic scatter-add (run-to-run order of float additions not fixed; the deterministic counting
+// sort above is the engine's `deterministic` mode).  dW must hold the values to add onto (zeros
+// for a plain embedding gradient).  One 16-lane group per position (d = 64: float4 per lane);
+// positions of the `hot` row (HealthRec's ingredient padding id: about half of the 2B x 20
+// positions) are summed in registers, then across the workgroup in LDS, and added with one atomic
+// row update per workgroup instead of one per position.  Two launches (zero fill + this) replace
+// the eight of the sort path.
+namespace {
+
+constexpr int kAtomGroups = 16;        // 16-lane groups per 256-thread block
+constexpr int kAtomPerGroup = 8;       // positions per group per block -> 128 positions per block
+
+__global__ __launch_bounds__(256) void emb_atomic_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                         const float* __restrict__ G, int64_t ldg, int64_t R,
+                                                         int64_t pad, int64_t hot, float* __restrict__ dW,
+                                                         int64_t lddw) {
+  __shared__ float4 hot_part[kAtomGroups][16];
+  const int q = threadIdx.x & 15;
+  const int grp = threadIdx.x >> 4;
+  float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t base = (int64_t)blockIdx.x * kAtomGroups * kAtomPerGroup;
+  for (int k = 0; k < kAtomPerGroup; ++k) {
+    const int64_t i = base + (int64_t)k * kAtomGroups + grp;
+    if (i >= n) break;
+    const int64_t r = idx[i];
+    if (r < 0 || r >= R || r == pad) continue;
+    const float4 g = reinterpret_cast<const float4*>(G + i * ldg)[q];
+    if (r == hot) {
+      h = f4_add(h, g);
+    } else {
+      float* p = dW + r * lddw + 4 * q;
+      atomicAdd(p + 0, g.x);
+      atomicAdd(p + 1, g.y);
+      atomicAdd(p + 2, g.z);
+      atomicAdd(p + 3, g.w);
+    }
+  }
+  if (hot < 0 || hot >= R) return;  // block-uniform
+  hot_part[grp][q] = h;
+  __syncthreads();
+  if (grp == 0) {
+    float4 t = hot_part[0][q];
+    for (int g2 = 1; g2 < kAtomGroups; ++g2) t = f4_add(t, hot_part[g2][q]);
+    if (t.x != 0.f || t.y != 0.f || t.z != 0.f || t.w != 0.f) {
+      float* p = dW + hot * lddw + 4 * q;
+      atomicAdd(p + 0, t.x);
+      atomicAdd(p + 1, t.y);
+      atomicAdd(p + 2, t.z);
+      atomicAdd(p + 3, t.w);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int fr_embedding_bwd_atomic(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
+                                       int64_t num_rows, int64_t padding_idx, int64_t hot_row, float* d_out,
+                                       int64_t ldo, void* stream) {
+  FR_REQUIRE(d == 64, "the atomic scatter is built for d = 64");
+  FR_REQUIRE(n >= 0 && num_rows >= 1, "bad sizes");
+  if (n == 0) return FR_OK;
+  FR_REQUIRE(d_idx && d_grad && d_out, "null argument");
+  FR_REQUIRE(ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad) && ldo >= d && ldo % 4 == 0 && fr::aligned16(d_out),
+             "grad / out must be 16-B aligned with ld % 4 == 0");
+  const int64_t per_block = (int64_t)kAtomGroups * kAtomPerGroup;
+  const int64_t blocks = fr::ceil_div(n, per_block);
+  FR_REQUIRE(blocks < (int64_t)INT32_MAX, "too many positions");
+  hipLaunchKernelGGL(emb_atomic_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     d_idx, n, d_grad, ldg, num_rows, padding_idx, hot_row, d_out, ldo);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}

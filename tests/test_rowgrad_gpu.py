@@ -508,3 +508,27 @@ def test_feed_batch_one_launch_matches_gathers(cuda):
         got.append([x.cpu().numpy().copy() for x in (u, p, n)])
     for k, key in enumerate("upn"):
         np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep0/{key}"])
+
+
+@pytest.mark.parametrize("hot", [None, 19987, 5])
+def test_embedding_bwd_atomic_matches_sorted(cuda, hot):
+    """fr_embedding_bwd_atomic (float atomics, the hot row pre-summed per workgroup) against the
+    deterministic counting-sort scatter: equal to fp32 rounding (rel 1e-5 of the row scale), the
+    padding_idx row skipped, out-of-range ids ignored; HealthRec's shape ([1024 x 20] positions,
+    about half of them the padding ingredient 19987, into 19988 rows)."""
+    from FoodRec.engine import ops
+    g = torch.Generator().manual_seed(3)
+    R, n = 19988, 1024 * 20
+    ids = torch.randint(0, R - 1, (n,), generator=g)
+    ids[torch.rand(n, generator=g) < 0.5] = 19987
+    ids[7] = R + 5  # out of range: skipped by both paths
+    G = torch.randn(n, 64, generator=g)
+    idc, Gc = ids.to(cuda), G.to(cuda)
+    ref = ops.scatter_rows(idc, Gc, R, None)
+    got = ops.scatter_rows(idc, Gc, R, None, hot_row=hot)
+    scale = ops.scatter_rows(idc, Gc.abs(), R, None)
+    assert torch.all((got - ref).abs() <= 1e-5 * scale + 1e-6)
+    pad_ref = ops.scatter_rows(idc, Gc, R, 11)
+    pad_got = ops.scatter_rows(idc, Gc, R, 11, hot_row=hot)
+    assert torch.all(pad_got[11] == 0)
+    assert torch.all((pad_got - pad_ref).abs() <= 1e-5 * scale + 1e-6)
