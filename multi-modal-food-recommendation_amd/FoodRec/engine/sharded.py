@@ -72,7 +72,7 @@ def _all_reduce(t, group, async_op=False):
 class ShardedGraph:
     """Rank ``rank``'s slice of the bipartite interaction graph (u, i) of n_users x n_items."""
 
-    def __init__(self, n_users, n_items, u, i, rank, world, device, chunk=DEFAULT_CHUNK):
+    def __init__(self, n_users, n_items, u, i, rank, world, device, chunk=DEFAULT_CHUNK, item_blocks=4):
         U, I = int(n_users), int(n_items)
         dev = torch.device(device)
         u = torch.as_tensor(u, dtype=torch.int64, device=dev)
@@ -114,9 +114,31 @@ class ShardedGraph:
         order = torch.argsort(li * max(self.n_local, 1) + lu)
         rp_i = torch.zeros(I + 1, dtype=torch.int64, device=dev)
         torch.cumsum(torch.bincount(li, minlength=I), 0, out=rp_i[1:])
-        self.A_iu = Adjacency(rp_i, lu[order].to(torch.int32), val[order], (I, self.n_local), device=dev,
-                              chunk=chunk, symmetric=False)
+        col_iu, val_iu = lu[order].to(torch.int32), val[order]
+        self.A_iu = Adjacency(rp_i, col_iu, val_iu, (I, self.n_local), device=dev, chunk=chunk, symmetric=False)
+        # the transpose slice cut into nnz-balanced item-row blocks: each block's partial item rows are
+        # all-reduced as soon as they are computed, while the next block is still gathering
+        self.iu_blocks = self._row_blocks(rp_i, col_iu, val_iu, torch.cumsum(deg_i, 0), max(1, int(item_blocks)),
+                                          chunk, dev)
         self.local_nnz = int(lu.numel())
+
+    def _row_blocks(self, rp, col, val, gcum, nb, chunk, dev):
+        """[(row_lo, row_hi, Adjacency of rows [row_lo, row_hi))]: item-row blocks balanced by the GLOBAL
+        item degrees (``gcum`` = their prefix sums, the same on every rank), so every rank cuts the
+        item table at the same rows and the per-block all-reduces match across ranks."""
+        R = rp.numel() - 1
+        total = int(gcum[-1].item()) if R else 0
+        if nb == 1 or R == 0 or total == 0:
+            return [(0, R, self.A_iu)]
+        targets = torch.tensor([total * (b + 1) // nb for b in range(nb - 1)], dtype=torch.int64, device=gcum.device)
+        cuts = (torch.searchsorted(gcum, targets) + 1).clamp(0, R).cpu().tolist()
+        bounds = sorted(set([0] + [int(c) for c in cuts] + [R]))
+        out = []
+        for lo, hi in zip(bounds, bounds[1:]):
+            e0, e1 = int(rp[lo].item()), int(rp[hi].item())
+            out.append((lo, hi, Adjacency(rp[lo:hi + 1] - e0, col[e0:e1], val[e0:e1], (hi - lo, self.n_local),
+                                          device=dev, chunk=chunk, symmetric=False)))
+        return out
 
     # ------------------------------------------------------------------ global triple sampler
     def triples(self, batch_size: int, seed: int, epoch_step: int):
@@ -154,7 +176,29 @@ class ShardedGraph:
         return own, torch.where(own, users - self.lo, torch.full_like(users, -1))
 
 
+def _item_partial(g: ShardedGraph, Eu, out, group):
+    """out = A_iu[rank] Eu (this rank's contribution to every item row), one launch per item-row block,
+    each block's all-reduce issued (async) right after its launch.  Returns the pending handles."""
+    works = []
+    for lo, hi, blk in g.iu_blocks:
+        ops.spmm_launch(blk, Eu, Y1=out[lo:hi])
+        works.append(_all_reduce(out[lo:hi], group, async_op=True))
+    return works
+
+
+def _wait(works):
+    for w in works:
+        if w is not None:
+            w.wait()
+
+
 class _ShardedPropagate(torch.autograd.Function):
+    """Layer k: E_u^{k+1} = A_ui E_i^k (local) and E_i^{k+1} = sum_r A_iu[r] E_u^k[r] (all-reduce).
+    The item partial of layer k only needs E_u^k, so it is launched first, block by block with each
+    block's all-reduce issued behind it; the all-reduce of layer k is waited for only right before
+    the user SpMM of layer k + 1 needs E_i^{k+1} -- it overlaps the rest of the item partial, the
+    user SpMM of layer k and the item partial of layer k + 1.  Backward mirrors it."""
+
     @staticmethod
     def forward(ctx, ego_u, ego_i, g: ShardedGraph, L: int, group):
         ctx.g, ctx.L, ctx.group = g, L, group
@@ -163,10 +207,14 @@ class _ShardedPropagate(torch.autograd.Function):
         out_u = torch.empty_like(ego_u)
         acc_i = ego_i.clone()
         prev_u = []
+        pending = None  # (handles, table) of the previous layer's item all-reduce
         for k in range(L):
             pi = torch.empty_like(ego_i)
-            ops.spmm_launch(g.A_iu, Eu, Y1=pi)                    # item partial of layer k+1
-            work = _all_reduce(pi, group, async_op=True)
+            works = _item_partial(g, Eu, pi, group)               # E_i^{k+1}, reduce in flight
+            if pending is not None:                              # E_i^k for this layer's user SpMM
+                _wait(pending[0])
+                acc_i.add_(pending[1])
+                Ei = pending[1]
             if k == L - 1:                                        # last user layer: mean in the epilogue
                 terms = [ego_u] + prev_u
                 A1 = terms[0]
@@ -176,17 +224,14 @@ class _ShardedPropagate(torch.autograd.Function):
                 else:
                     ops.spmm_launch(g.A_ui, Ei, Y1=out_u)
                     out_u.add_(torch.stack(terms).sum(0)).mul_(inv)
-                nu = None
             else:
                 nu = torch.empty_like(ego_u)
                 ops.spmm_launch(g.A_ui, Ei, Y1=nu)
-            if work is not None:
-                work.wait()
-            acc_i.add_(pi)
-            if nu is not None:
                 prev_u.append(nu)
                 Eu = nu
-            Ei = pi
+            pending = (works, pi)
+        _wait(pending[0])
+        acc_i.add_(pending[1])
         out_i = acc_i.mul_(inv)
         return out_u, out_i
 
@@ -200,16 +245,19 @@ class _ShardedPropagate(torch.autograd.Function):
         dev_i = g_i if g_i is not None else torch.zeros(g.n_items, g_u.shape[1], device=g_u.device)
         Hu = dev_u * inv
         Hi = dev_i * inv
+        pending = None
         for _ in range(L):
             pi = torch.empty_like(Hi)
-            ops.spmm_launch(g.A_iu, Hu, Y1=pi)
-            work = _all_reduce(pi, group, async_op=True)
+            works = _item_partial(g, Hu, pi, group)
+            if pending is not None:
+                _wait(pending[0])
+                Hi = pending[1].add_(dev_i, alpha=inv)
             nHu = torch.empty_like(Hu)
             ops.spmm_launch(g.A_ui, Hi, Y2=nHu, alpha=1.0, A1=dev_u, beta1=inv)
-            if work is not None:
-                work.wait()
-            Hi = pi.add_(dev_i, alpha=inv)
+            pending = (works, pi)
             Hu = nHu
+        _wait(pending[0])
+        Hi = pending[1].add_(dev_i, alpha=inv)
         return Hu, Hi, None, None, None
 
 
