@@ -592,6 +592,11 @@ int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* 
                   int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes, int64_t* d_out_nums,
                   float* d_out_health, bool* d_out_mask, void* stream);
 
+/* fr_step_book: the training loop's per-step loss bookkeeping (common/trainer.py:183-193) on the
+ * device: acc[i] (+)= (double)*parts[i] for the n (<= 8) scalar loss components, and
+ * *nan |= isnan(sum of the parts in fp32, left to right).  One launch, no host sync. */
+int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * RCCL communicator (SURVEY 8(b) fr_comm_init / fr_allreduce_f32; new work: the reference is
  * single-process, utils/configurator.py:110-114).  One communicator per process and GPU (the

@@ -61,6 +61,16 @@ def metrics_by_user(doc_list, rel_list):
     return hits / len(rel_list), dcg / idcg
 
 
+def book_step(parts, acc, nan_flag, accumulate=True):
+    """fr_step_book over the loss parts (device float scalars): acc (+)= parts, nan |= isnan(sum)."""
+    import ctypes
+    from FoodRec.engine import native
+    n = len(parts)
+    ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in parts])
+    native.check(native.lib().fr_step_book(ptrs, n, acc.data_ptr(), int(bool(accumulate)), nan_flag.data_ptr(),
+                                           native.stream_of(acc)), "fr_step_book")
+
+
 class GraphedStep:
     """Trainer.train_step captured once in a HIP graph and replayed per batch.
 
@@ -192,6 +202,10 @@ class GraphedDPStep(GraphedStep):
         tr.optimizer.zero_grad()
         losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
         parts = losses if isinstance(losses, tuple) else (losses,)
+        if tr._book_fused(state, parts, accumulate):
+            torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
+            tr.grad_hook.pack()
+            return None
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
         if state.get("acc") is None:
@@ -428,6 +442,10 @@ class Trainer(AbstractTrainer):
         second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
         losses = loss_func(interaction)
         parts = losses if isinstance(losses, tuple) else (losses,)
+        if second_inter is None and self._book_fused(state, parts, accumulate):
+            # the loss sum is never materialised: each part back-propagates with a cached ones seed
+            torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
+            return self._finish_step(state)
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
         if state.get("acc") is None:
@@ -448,6 +466,11 @@ class Trainer(AbstractTrainer):
             (-1 * self.alpha2 * l2).backward()
         else:
             loss.backward()
+        self._finish_step(state)
+        return loss.detach()
+
+    def _finish_step(self, state):
+        """Gradient hook / clipping, then the optimiser step (common/trainer.py:215-224)."""
         if self.clip_grad_norm or self.grad_hook is not None:
             if isinstance(self.optimizer, FusedAdam):
                 self.optimizer.materialize_row_grads()  # dense .grad for the norm / the hook
@@ -455,8 +478,36 @@ class Trainer(AbstractTrainer):
             clip_grad_norm_(self.model.parameters(), **self.clip_grad_norm)
         if self.grad_hook is not None:
             self.grad_hook(self.model)
-        self._opt_step(nan_flag)
-        return loss.detach()
+        self._opt_step(state["nan"])
+        return None
+
+    def _book_fused(self, state, parts, accumulate) -> bool:
+        """Per-step loss bookkeeping in one HIP launch (fr_step_book): state['acc'] (float64 sums
+        of every loss part) and the sticky NaN flag of sum(parts).  False when it does not apply
+        (CPU, more than 8 parts, non-fp32 or non-scalar parts)."""
+        if not (len(parts) <= 8 and all(torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
+                                          and x.numel() == 1 and x.is_contiguous() and x.requires_grad
+                                          for x in parts)):
+            return False
+        if state.get("acc") is None:
+            state["acc"] = torch.zeros(len(parts), dtype=torch.float64, device=parts[0].device)
+            accumulate = False
+        elif state["acc"].numel() != len(parts):
+            return False
+        book_step(parts, state["acc"], state["nan"], accumulate)
+        return True
+
+    def _ones_like(self, parts):
+        cache = self.__dict__.setdefault("_ones_cache", {})
+        out = []
+        for x in parts:
+            key = (tuple(x.shape), x.dtype, x.device)
+            t = cache.get(key)
+            if t is None:
+                t = torch.ones(x.shape, dtype=x.dtype, device=x.device)
+                cache[key] = t
+            out.append(t)
+        return out
 
     def graphed_step(self, batch_size: int, warmup: int = 3):
         """A callable (u, p, n, batch_idx, state) running train_step through captured HIP graphs

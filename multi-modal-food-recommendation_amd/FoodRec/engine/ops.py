@@ -822,6 +822,15 @@ def layer_norm(x: torch.Tensor, normalized_shape, weight=None, bias=None, eps: f
 ENCODER_LENGTHS = (4, 5, 8, 10, 16, 20)
 
 
+def encoder_flops(n_seq: int, L: int, backward: bool) -> int:
+    """MFMA flops of one fused encoder-layer launch (d=64, FF=256): the four GEMMs per token
+    (qkv 2*64*192, out-proj 2*64*64, FF1 2*64*256, FF2 2*256*64 = 98,304 flops); the backward runs
+    both the input- and the weight-gradient GEMMs (2x).  The 20x20 attention is VALU work, not
+    counted."""
+    per_tok = 2 * 64 * 192 + 2 * 64 * 64 + 2 * 64 * 256 + 2 * 256 * 64
+    return n_seq * L * per_tok * (2 if backward else 1)
+
+
 def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
     """Algorithmic HBM bytes of one fused encoder-layer launch: the saved activations (qkv 192 +
     ctx 64 + y1 64 + fact 256 + dact 256 + y2 64 + 4 stats floats per token) written by the
