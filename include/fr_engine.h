@@ -593,9 +593,18 @@ int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* 
                   float* d_out_health, bool* d_out_mask, void* stream);
 
 /* fr_step_book: the training loop's per-step loss bookkeeping (common/trainer.py:183-193) on the
- * device: acc[i] (+)= (double)*parts[i] for the n (<= 8) scalar loss components, and
- * *nan |= isnan(sum of the parts in fp32, left to right).  One launch, no host sync. */
-int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan, void* stream);
+ * device: acc[i] (+)= (double)*parts[i] for the n (<= 8) scalar loss components,
+ * *nan |= isnan(sum of the parts in fp32, left to right), and each of the n_counters (<= 8) device
+ * int64 step counters += 1 (dropout-hash step counters, the device feed's batch cursor).  One
+ * launch, no host sync. */
+int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan,
+                 int64_t* const* d_counters, int n_counters, void* stream);
+
+/* fr_reg_combine_fwd / _bwd: HealthRec's weighted EmbLoss from its two fused pieces,
+ * out = w * (a[0] + (b[0] + ... + b[nb-1]) / B)  (cikm_model.py:267-279); backward da = g w,
+ * db[i] = g w / B.  One launch each. */
+int fr_reg_combine_fwd(const float* d_a, const float* d_b, int nb, float B, float w, float* d_out, void* stream);
+int fr_reg_combine_bwd(const float* d_g, int nb, float B, float w, float* d_da, float* d_db, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * RCCL communicator (SURVEY 8(b) fr_comm_init / fr_allreduce_f32; new work: the reference is

@@ -62,13 +62,16 @@ def metrics_by_user(doc_list, rel_list):
 
 
 def book_step(parts, acc, nan_flag, accumulate=True):
-    """fr_step_book over the loss parts (device float scalars): acc (+)= parts, nan |= isnan(sum)."""
+    """fr_step_book over the loss parts (device float scalars): acc (+)= parts, nan |= isnan(sum),
+    and the step's deferred device counters (ops.defer_increment) advanced in the same launch."""
     import ctypes
     from FoodRec.engine import native
     n = len(parts)
     ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in parts])
+    ctrs = ops.take_pending_counters()
+    cptr = (ctypes.c_void_p * max(1, len(ctrs)))(*[c.data_ptr() for c in ctrs])
     native.check(native.lib().fr_step_book(ptrs, n, acc.data_ptr(), int(bool(accumulate)), nan_flag.data_ptr(),
-                                           native.stream_of(acc)), "fr_step_book")
+                                           cptr, len(ctrs), native.stream_of(acc)), "fr_step_book")
 
 
 class GraphedStep:
@@ -124,6 +127,7 @@ class GraphedStep:
     def _body(self, batch_idx, state, accumulate=True):
         feats = self.tr._features()
         pre = None
+        ops.defer_counters(True)  # the feed cursor advances in the step's fr_step_book launch
         if self.feed is not None:
             # (u, pos, neg) and the [pos; neg] item features gathered in one launch (fr_feed_batch)
             pre = self.feed.fill(self.u, self.p, self.n, feats if not feats.ssl else None)
@@ -197,12 +201,17 @@ class GraphedDPStep(GraphedStep):
         tr = self.tr
         feats = tr._features()
         pre = None
+        ops.defer_counters(True)
         if self.feed is not None:
             pre = self.feed.fill(self.u, self.p, self.n, feats if not feats.ssl else None)
         tr.optimizer.zero_grad()
-        losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
-        parts = losses if isinstance(losses, tuple) else (losses,)
-        if tr._book_fused(state, parts, accumulate):
+        try:
+            losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
+            parts = losses if isinstance(losses, tuple) else (losses,)
+            fused = tr._book_fused(state, parts, accumulate)
+        finally:
+            ops.defer_counters(False)
+        if fused:
             torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
             tr.grad_hook.pack()
             return None
@@ -440,9 +449,14 @@ class Trainer(AbstractTrainer):
         loss_func = loss_func or self.model.calculate_loss
         self.optimizer.zero_grad()
         second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
-        losses = loss_func(interaction)
-        parts = losses if isinstance(losses, tuple) else (losses,)
-        if second_inter is None and self._book_fused(state, parts, accumulate):
+        ops.defer_counters(True)  # device step counters advance in the step's fr_step_book launch
+        try:
+            losses = loss_func(interaction)
+            parts = losses if isinstance(losses, tuple) else (losses,)
+            fused = second_inter is None and self._book_fused(state, parts, accumulate)
+        finally:
+            ops.defer_counters(False)  # (applies the increments eagerly when the step was not booked)
+        if fused:
             # the loss sum is never materialised: each part back-propagates with a cached ones seed
             torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
             return self._finish_step(state)

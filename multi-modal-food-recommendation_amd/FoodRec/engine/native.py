@@ -59,7 +59,10 @@ _SIGS = {
                                c_float, POINTER(FrTab), c_float, c_void_p, POINTER(FrRowList), c_void_p, c_int64,
                                c_void_p]),
     "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
-    "fr_step_book": (c_int, [POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
+    "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "fr_step_book": (c_int, [POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p, POINTER(c_void_p), c_int,
+                             c_void_p]),
     "fr_embedding_bwd_atomic": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_int64,
                                         c_void_p, c_int64, c_void_p]),
     "fr_feed_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

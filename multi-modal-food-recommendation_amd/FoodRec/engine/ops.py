@@ -287,6 +287,63 @@ class _BprEmb(torch.autograd.Function):
 
 _DETERMINISTIC = False
 
+# device step counters whose per-step increment is deferred to the step's fr_step_book launch
+# (Trainer._book_fused).  A counter still pending when it is about to be read again is advanced on
+# the spot, so a forward run outside a booked training step keeps the one-per-use semantics.
+_PENDING_COUNTERS = []
+_DEFER = [False]
+
+
+def defer_counters(on: bool) -> None:
+    """Inside a training step that ends in fr_step_book (Trainer) counter increments are deferred
+    to that launch; outside one they happen immediately (``defer_increment`` falls back to add_)."""
+    _DEFER[0] = bool(on)
+    if not on:
+        settle_all_counters()
+
+
+def defer_increment(counter: torch.Tensor) -> None:
+    """Advance ``counter`` (a device int64 scalar) by one at the end of this training step (or now,
+    outside a deferring step)."""
+    if not _DEFER[0]:
+        counter.add_(1)
+        return
+    for k, c in enumerate(_PENDING_COUNTERS):
+        if c is counter:
+            del _PENDING_COUNTERS[k]
+            counter.add_(1)
+            break
+    _PENDING_COUNTERS.append(counter)
+
+
+def settle_counter(counter: torch.Tensor) -> None:
+    """Apply a pending deferred increment of ``counter`` now (before it is read again)."""
+    for k, c in enumerate(_PENDING_COUNTERS):
+        if c is counter:
+            del _PENDING_COUNTERS[k]
+            counter.add_(1)
+            return
+
+
+def drop_pending(counter: torch.Tensor) -> None:
+    """Forget a pending increment (the counter is being reset)."""
+    _PENDING_COUNTERS[:] = [c for c in _PENDING_COUNTERS if c is not counter]
+
+
+def take_pending_counters(limit: int = 8) -> list:
+    """The deferred counters for fr_step_book (at most ``limit``; the rest are advanced now)."""
+    out = _PENDING_COUNTERS[:limit]
+    for c in _PENDING_COUNTERS[limit:]:
+        c.add_(1)
+    _PENDING_COUNTERS.clear()
+    return out
+
+
+def settle_all_counters() -> None:
+    for c in _PENDING_COUNTERS:
+        c.add_(1)
+    _PENDING_COUNTERS.clear()
+
 
 def set_deterministic(on: bool) -> None:
     """Engine-wide run-to-run reproducible scatters (config key ``deterministic``, set by the
@@ -523,6 +580,33 @@ def graph_bpr(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, 
     [ui_items[pos]; ui_items[neg]]); see _GraphBpr."""
     return _GraphBpr.apply(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma,
                            _DETERMINISTIC)
+
+
+class _RegCombine(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, B, w):
+        native.require_device(a, b)
+        a, b = a.contiguous(), b.contiguous()
+        out = torch.empty(1, dtype=torch.float32, device=a.device)
+        native.check(native.lib().fr_reg_combine_fwd(a.data_ptr(), b.data_ptr(), b.numel(), _f(float(B)), _f(float(w)),
+                                                     out.data_ptr(), native.stream_of(a)), "fr_reg_combine_fwd")
+        ctx.meta = (a.shape, b.shape, float(B), float(w))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        sa, sb, B, w = ctx.meta
+        g = g.contiguous()
+        da = torch.empty(sa, dtype=torch.float32, device=g.device)
+        db = torch.empty(sb, dtype=torch.float32, device=g.device)
+        native.check(native.lib().fr_reg_combine_bwd(g.data_ptr(), db.numel(), _f(B), _f(w), da.data_ptr(), db.data_ptr(),
+                                                     native.stream_of(g)), "fr_reg_combine_bwd")
+        return da, db, None, None
+
+
+def reg_combine(a, b, B, w):
+    """``w * (a + b.sum() / B)`` for a [1] and b [k] fp32 device tensors in one launch per direction."""
+    return _RegCombine.apply(a, b, B, w)
 
 
 # ----------------------------------------------------------------------------- embedding
@@ -861,13 +945,14 @@ class _EncoderLayer(torch.autograd.Function):
         st2 = torch.empty(T, 2, **f32)
         seed_used = torch.empty(1, dtype=torch.int64, device=dev)
         pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+        settle_counter(cfg.counter)  # a previous forward's increment not yet applied by a booked step
         with profiling.region("encoder_fwd", encoder_bytes(NS, L, False)):
             native.check(native.lib().fr_encoder_fwd(
                 x.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
                 cfg.counter.data_ptr(), seed_used.data_ptr(), out.data_ptr(), qkv.data_ptr(), cx.data_ptr(),
                 y1.data_ptr(), fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(),
                 native.stream_of(x)), "fr_encoder_fwd")
-        cfg.counter.add_(1)
+        defer_increment(cfg.counter)  # advanced by the step's fr_step_book (or before its next read)
         ctx.cfg = cfg
         ctx.has_mask = mask is not None
         ctx.save_for_backward(x, mask if mask is not None else seed_used, qkv, cx, y1, fact, dact, y2, st1,

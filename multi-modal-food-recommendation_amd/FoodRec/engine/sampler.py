@@ -145,6 +145,8 @@ class DeviceFeed:
         self._idx = torch.empty(self.B, dtype=torch.int64, device=device)
 
     def stage(self, perm_d, negs_d):
+        from . import ops
+        ops.drop_pending(self.cursor)
         self.perm.copy_(perm_d)
         self.negs.copy_(negs_d)
         self.cursor.zero_()
@@ -153,17 +155,19 @@ class DeviceFeed:
         """Gather batch ``cursor`` into (u, p, n) and advance the cursor.  With ``feats`` (a
         BatchFeatures on the GPU) the [pos; neg] item features are gathered in the same launch
         (fr_feed_batch) into feats' static buffers, which are returned for ``feats.batch(..., pre=)``."""
+        from . import ops
+        ops.settle_counter(self.cursor)
         if feats is not None and feats.native_ok():
             pre = feats.pn_buffers(self.B)
             feats.launch_feed(self, u, p, n, pre)
-            self.cursor.add_(1)
+            ops.defer_increment(self.cursor)  # advanced by the step's fr_step_book
             return pre
         torch.add(self.offs, self.cursor * self.B, out=self._pos)
         torch.index_select(self.perm, 0, self._pos, out=self._idx)
         torch.index_select(self.users, 0, self._idx, out=u)
         torch.index_select(self.items, 0, self._idx, out=p)
         torch.index_select(self.negs, 0, self._pos, out=n)
-        self.cursor.add_(1)
+        ops.defer_increment(self.cursor)
         return None
 
 

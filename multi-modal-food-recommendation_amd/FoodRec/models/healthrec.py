@@ -215,6 +215,8 @@ class HealthRec(GeneralRecommender):
             kd_term = self.loss_kd * self.norm_loss(kd, self.kd_threshold)
 
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
+        if emb3.is_cuda and ing_norms.is_cuda and emb3.dtype == torch.float32 and ing_norms.dtype == torch.float32:
+            return mf_loss, health_term, kd_term, ops.reg_combine(emb3, ing_norms, B, self.reg_weight)
         reg = emb3 + ing_norms.sum() / B  # (= ing_norms[0] + ing_norms[1]; sum's backward is a view, no fills)
         return mf_loss, health_term, kd_term, self.reg_weight * reg
 
