@@ -368,6 +368,9 @@ class Trainer(AbstractTrainer):
         ops.set_deterministic(bool(config["deterministic"]))  # reproducible scatters (engine-wide)
         if self._on_gpu():
             self.swapped_adjacencies = swap_sparse_attributes(model)
+            prep = getattr(model, "engine_layout", None)  # engine-native models lay out their tables
+            if callable(prep):
+                prep()
         self.optimizer = self._build_optimizer()
         if isinstance(self.optimizer, FusedAdam) and self.optimizer.lazy_rows:
             model.__dict__["_fr_flush"] = self.optimizer.flush  # model.state_dict() applies deferred rows

@@ -426,9 +426,25 @@ def rows_mark(mask: torch.Tensor, rows, value: int) -> None:
                                            native.stream_of(mask)), "fr_rows_mark")
 
 
+def _adjacent_rows(lo, hi, rows):
+    """[lo ; hi] as one [rows, d] view when hi's rows follow lo's in memory (same storage, contiguous
+    row-major: a model placed them so, e.g. HealthRec.engine_layout), else None."""
+    if not (lo.is_contiguous() and hi.is_contiguous() and lo.dim() == 2 and hi.dim() == 2
+            and lo.shape[1] == hi.shape[1] and lo.dtype == hi.dtype
+            and lo.untyped_storage().data_ptr() == hi.untyped_storage().data_ptr()
+            and hi.data_ptr() == lo.data_ptr() + lo.numel() * lo.element_size()
+            and lo.shape[0] + hi.shape[0] >= rows):
+        return None
+    return lo.as_strided((rows, lo.shape[1]), (lo.shape[1], 1))
+
+
 def _prop_fwd_split(adj, lo, hi, split, L):
     """mean([E, A E, ..., A^L E]) for E = [lo ; hi] split at ``split`` (no concatenated copy)."""
     N, d = adj.shape[0], lo.shape[1]
+    if split == lo.shape[0]:
+        one = _adjacent_rows(lo, hi, adj.shape[1])
+        if one is not None:  # the tables are one buffer already: plain gathers
+            lo, hi = one, None
     out = torch.empty(N, d, dtype=lo.dtype, device=lo.device)
     if L == 1:
         spmm_ex(adj, lo, hi, split, Y2=out, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)

@@ -229,6 +229,22 @@ class HealthRec(GeneralRecommender):
                 and all(m.num_head == 2 and m.atten_mode == "ln" and not m.linear_projection for m in (a, b))
                 and a.ln.eps == b.ln.eps)
 
+    @torch.no_grad()
+    def engine_layout(self):
+        """Place item_embedding and ingre_embedding in ONE device buffer, [items ; ingredients (+ pad)]
+        -- the RI propagation's ego table [item ; ingre[:-1]] (cikm_model.py:185) is then a plain
+        contiguous view: the first SpMM of every step gathers from one table instead of two.  Called
+        by the Trainer before the optimiser exists (the parameter objects stay the same; state_dict
+        and load_state_dict are unaffected)."""
+        iw, gw = self.item_embedding.weight, self.ingre_embedding.weight
+        if not (iw.is_cuda and gw.is_cuda and iw.dtype == gw.dtype and iw.shape[1] == gw.shape[1]):
+            return
+        if iw.is_contiguous() and gw.is_contiguous() and gw.data_ptr() == iw.data_ptr() + iw.numel() * iw.element_size():
+            return
+        big = torch.cat([iw.detach(), gw.detach()], dim=0)
+        iw.data = big[:iw.shape[0]]
+        gw.data = big[iw.shape[0]:]
+
     def _fused_graph(self, ids) -> bool:
         """ops.graph_bpr covers the GPU configuration: fp32 d=64 contiguous tables, CSR adjacencies
         (the Trainer's swap), at least one layer of each propagation."""
