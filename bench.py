@@ -196,17 +196,29 @@ def main():
     roofline = None
     if dom_name is not None:
         d = kern[dom_name]
-        achieved = d["gbps"]
-        roofline = {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
-                    "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / ksteps,
-                    "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3),
-                    "timing_source": "HIP events per launch on the launch stream, eager pass of "
-                                     f"{ksteps} steps right after the timed region (kernels.{dom_name})",
-                    "residency": ("the gathered X tables (<= 29 MB) sit in the 256 MB Infinity Cache (MALL): "
-                                  "this is a cache-level rate; the HBM-level SpMM roofline is config4_10m.spmm"
-                                  if dom_name == "spmm" else None)}
+        common = {"kernel": dom_name, "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / ksteps,
+                  "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3),
+                  "timing_source": "HIP events per launch on the launch stream, eager pass of "
+                                   f"{ksteps} steps right after the timed region (kernels.{dom_name})"}
+        if dom_name.startswith("encoder_"):
+            # the fused Transformer layer: fp32 MFMA GEMMs (v_mfma_f32_16x16x4_f32) -> an MFMA roofline
+            from FoodRec.engine import ops as _ops
+            fl = _ops.encoder_flops(2 * args.batch, 20, dom_name.endswith("bwd"))
+            tf = fl / (d["avg_ms"] * 1e-3) / 1e12
+            roofline = {**common, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
+                        "flops_per_launch": fl, "bytes_per_launch": int(d["bytes_per_launch"]),
+                        "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
+                                "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
+        else:
+            achieved = d["gbps"]
+            roofline = {**common, "bound": "hbm", "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                        "traffic": traffic, "bytes_per_launch": int(d["bytes_per_launch"]),
+                        "residency": ("the gathered X tables (<= 29 MB) sit in the 256 MB Infinity Cache (MALL): "
+                                      "this is a cache-level rate; the HBM-level SpMM roofline is config4_10m.spmm"
+                                      if dom_name == "spmm" else None)}
+    # the propagation SpMM's own figures (the metric's "SpMM HBM GB/s") are in `spmm` below
     # step-level figure: algorithmic bytes of every timed region per step / the graphed step time
     step_bytes = sum(v["bytes_per_launch"] * v["launches"] for v in kern.values()) / ksteps
     step_fig = {"algorithmic_bytes_per_step": int(step_bytes),
