@@ -6,7 +6,7 @@ sys.path[:0] = [os.path.join(ROOT, "multi-modal-food-recommendation_amd"), ROOT,
 import torch
 from FoodRec.engine import ops
 from FoodRec.engine.graph import Adjacency, bipartite_norm_csr_torch
-from synth_graph import synth_bipartite
+from FoodRec.utils.interaction_graph import synth_bipartite
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--users", type=int, default=10_000_000)
