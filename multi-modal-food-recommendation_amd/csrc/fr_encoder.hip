@@ -11,11 +11,15 @@
 // each a few microseconds of launch-bound work.  Here one workgroup owns G = 80/L whole sequences
 // (80 token rows = five 16-row MFMA tiles) and keeps every intermediate in LDS: one forward and one
 // backward launch per layer, plus one ordered reduction of the per-workgroup weight-gradient partials.
+// 8 waves per workgroup (2 per SIMD): the VALU phases between the GEMMs (attention, LayerNorm, GELU,
+// dropout hash) are latency-bound, and a second wave per SIMD is what hides that latency.
 //
 // * GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 in / f32 accumulate, the f32 vector rate).  The k
 //   order inside a 16-wide chunk is permuted so each lane feeds four MFMAs from one float4 of A and
 //   one float4 of B (lane group h holds k = 4h..4h+3 of the chunk).
-// * Attention (20 x 20 per head) on the VALU: one thread per (sequence, head, query row).
+// * Attention (20 x 20 per head) on the VALU: two adjacent lanes per (sequence, head, query row), each
+//   owning 16 of the head's 32 dimensions; partial dot products are combined by a DPP swap and the
+//   score row stays in registers.
 // * Dropout masks from a counter-based hash of (seed, step counter, site, element): the backward
 //   regenerates them instead of storing them; the step counter is read on the device, so a captured
 //   HIP graph draws fresh masks on every replay.
@@ -26,12 +30,17 @@
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int E = 64, HEADS = 2, HD = 32, FF = 256, QKV = 3 * E;
 constexpr int ROWS = 80;                            // token rows per workgroup (5 MFMA row tiles)
 constexpr int RT = ROWS / 16;
 constexpr int LD_E = E + 4, LD_QKV = QKV + 4, LD_FF = FF + 4;
-constexpr int NT = 256;                             // threads per workgroup (4 waves)
+constexpr int NT = 512;                             // threads per workgroup: 8 waves, 2 per SIMD
+// Wave w owns output column tiles by its SIMD slot sg = w & 3 (as a 4-wave layout would) and, within
+// the SIMD, one of two row-tile ranges: hf = w >> 2 takes tiles [0, RT0) or [RT0, RT).  The two waves
+// of a SIMD share its MFMA pipe and hide each other's LDS / global / transcendental latency.
+constexpr int RT0 = (RT + 1) / 2;
 constexpr int BUF_D = 6400;                         // attention p'/ds buffers (2*G*H*L*L) and scratch
 
 // gradient partial layout (floats), identical to the flat gradient buffer fr_encoder_bwd writes
@@ -44,7 +53,7 @@ static_assert(NPART % 4 == 0, "partials are reduced as float4");
 struct Weights {
   const float *w_in, *b_in, *w_o, *b_o, *g1, *be1, *w1, *b1, *w2, *b2, *g2, *be2;
   float eps1, eps2;
-  uint32_t thr[4];     // dropout: element kept iff hash >= thr  (sites: attn, out-proj, ff-act, ff-out)
+  uint32_t thr[4];     // dropout: element kept iff its 16-bit hash half >= thr  (sites: attn, out-proj, ff-act, ff-out)
   float scale[4];      // 1 / (1 - p)
   uint64_t seed;
   int gelu;
@@ -103,31 +112,81 @@ __device__ __forceinline__ SiteKeys site_keys(uint64_t seed, int64_t counter) {
   return s;
 }
 
-// keep test for element idx: Weyl step + the lowbias32 finalizer (9 VALU ops), kept iff >= thr
-__device__ __forceinline__ bool keep(uint32_t ks, uint32_t idx, uint32_t thr) {
-  if (thr == 0u) return true;
-  uint32_t x = idx * 0x9E3779B1u + ks;
+// Dropout keep test.  Elements 2m and 2m+1 of a site share one 32-bit hash of m (Weyl step + the
+// lowbias32 finalizer; its three 32-bit multiplies are quarter-rate): element e is kept iff the
+// (e & 1) half of pair_hash(k, e >> 1) is >= thr = floor(p * 2^16).
+__device__ __forceinline__ uint32_t pair_hash(uint32_t ks, uint32_t pair) {
+  uint32_t x = pair * 0x9E3779B1u + ks;
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
   x *= 0x846CA68Bu;
   x ^= x >> 16;
-  return x >= thr;
+  return x;
 }
 
-// act(v) and act'(v): ReLU, or GELU(v) = v * Phi(v) (torch's exact-erf form).  Phi and phi share one
-// exp(-v^2/2); erf from Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), with Phi(-|v|) = q computed
-// directly (no cancellation for negative v).
-__device__ __forceinline__ float2 act_fwd_grad(float v, int gelu) {
-  if (!gelu) return make_float2(fmaxf(v, 0.f), v > 0.f ? 1.f : 0.f);
-  const float a = fabsf(v) * 0.70710678118654752f;
-  const float e = __expf(-a * a);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-  const float poly =
-      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
-  const float q = 0.5f * poly * e;  // Phi(-|v|) = (1 - erf(|v| / sqrt 2)) / 2
-  const float cdf = v >= 0.f ? 1.f - q : q;
-  return make_float2(v * cdf, fmaf(v, e * 0.39894228040143268f, cdf));
+__device__ __forceinline__ bool half_keep(uint32_t h, uint32_t odd, uint32_t thr) {
+  return (odd ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+
+__device__ __forceinline__ bool keep(uint32_t ks, uint32_t idx, uint32_t thr) {
+  if (thr == 0u) return true;
+  return half_keep(pair_hash(ks, idx >> 1), idx & 1u, thr);
+}
+
+// attention site: element base + j of a score row (base = task * L); for even L the row starts on
+// a pair boundary, so j and j + 1 (j even) share a hash the compiler computes once per unrolled pair
+template <int L>
+__device__ __forceinline__ bool keep_att_l(uint32_t ks, uint32_t base, int j, uint32_t thr) {
+  if (thr == 0u) return true;
+  if constexpr (L % 2 == 0) return half_keep(pair_hash(ks, (base >> 1) + (j >> 1)), j & 1, thr);
+  return keep(ks, base + j, thr);
+}
+#define keep_att(ks, base, j, thr) keep_att_l<L>(ks, base, j, thr)
+
+__device__ __forceinline__ uint32_t pair_swap_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+
+// Keep bits of the 4 elements (rows row0 + q, q = 0..3; column col) a lane holds in an MFMA output
+// fragment of a [*, W] site (W even).  Adjacent columns are lanes 2k, 2k+1 and share each row's
+// pair hash: the even lane hashes rows 0, 1, the odd lane rows 2, 3, and they swap (2 hashes per
+// lane instead of 4).  Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t frag_keep4(uint32_t ks, int64_t tok_row0, int W, int col, uint32_t thr) {
+  if (thr == 0u) return 0xFu;
+  const uint32_t odd = col & 1;
+  const uint32_t e0 = (uint32_t)((tok_row0 + 2 * odd) * W + col);
+  const uint32_t ha = pair_hash(ks, e0 >> 1), hb = pair_hash(ks, (e0 + W) >> 1);
+  const uint32_t oa = pair_swap_u(ha), ob = pair_swap_u(hb);
+  const uint32_t h0 = odd ? oa : ha, h1 = odd ? ob : hb, h2 = odd ? ha : oa, h3 = odd ? hb : ob;
+  return (uint32_t)half_keep(h0, odd, thr) | ((uint32_t)half_keep(h1, odd, thr) << 1) |
+         ((uint32_t)half_keep(h2, odd, thr) << 2) | ((uint32_t)half_keep(h3, odd, thr) << 3);
+}
+
+// act(v) and act'(v) of two values at once: ReLU, or GELU(v) = v * Phi(v) (torch's exact-erf form).
+// Phi and phi share one exp(-v^2/2); erf from Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7), with
+// Phi(-|v|) = q computed directly (no cancellation for negative v).  The polynomial and products run
+// on packed-fp32 VALU ops (v_pk_fma_f32 / v_pk_mul_f32), exp and rcp per element.
+__device__ __forceinline__ void act_fwd_grad2(f32x2 v, int gelu, f32x2& act, f32x2& grad) {
+  if (!gelu) {
+    act = f32x2{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+    grad = f32x2{v.x > 0.f ? 1.f : 0.f, v.y > 0.f ? 1.f : 0.f};
+    return;
+  }
+  const f32x2 a = f32x2{fabsf(v.x), fabsf(v.y)} * 0.70710678118654752f;
+  const f32x2 aa = a * a;
+  const f32x2 e = f32x2{__expf(-aa.x), __expf(-aa.y)};
+  const f32x2 den = __builtin_elementwise_fma(a, f32x2{0.3275911f, 0.3275911f}, f32x2{1.f, 1.f});
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 poly = __builtin_elementwise_fma(t, f32x2{1.061405429f, 1.061405429f}, f32x2{-1.453152027f, -1.453152027f});
+  poly = __builtin_elementwise_fma(t, poly, f32x2{1.421413741f, 1.421413741f});
+  poly = __builtin_elementwise_fma(t, poly, f32x2{-0.284496736f, -0.284496736f});
+  poly = __builtin_elementwise_fma(t, poly, f32x2{0.254829592f, 0.254829592f});
+  poly = t * poly;
+  const f32x2 q = 0.5f * poly * e;
+  const f32x2 cdf = f32x2{v.x >= 0.f ? 1.f - q.x : q.x, v.y >= 0.f ? 1.f - q.y : q.y};
+  act = v * cdf;
+  grad = __builtin_elementwise_fma(v, e * 0.39894228040143268f, cdf);
 }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -141,44 +200,78 @@ __device__ __forceinline__ float comp(const float4& v, int m) {
 
 constexpr float kScale = 0.17677669529663688f;  // 1 / sqrt(HD)
 
-// offset of lane's float4 (4 rows of one column) of FF1 column tile (wave, c), row tile r, in the
-// fragment-layout dact buffer [n_wg][ROWS * FF]
-__device__ __forceinline__ int64_t dact_frag(int wg, int wave, int c, int r, int lane) {
-  return (int64_t)wg * (ROWS * FF) + ((((wave * 4 + c) * RT + r) * 64 + lane) << 2);
+
+// offset of lane's float4 (4 rows of one column) of FF1 column tile (SIMD slot sg, c), row tile r, in
+// the fragment-layout dact buffer [n_wg][ROWS * FF]
+__device__ __forceinline__ int64_t dact_frag(int wg, int sg, int c, int r, int lane) {
+  return (int64_t)wg * (ROWS * FF) + ((((sg * 4 + c) * RT + r) * 64 + lane) << 2);
 }
 
-__device__ __forceinline__ float dot_row(const float (&q)[HD], const float* r) {
-  float d = 0.f;
+// the partner lane's value (lanes 2k <-> 2k+1, DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ float pair_swap(float v) { return dpp_mov<0xB1>(v); }
+
+// 16-dimension head slices as 8 packed pairs: dot products and axpys on v_pk_fma_f32 (two lanes of
+// arithmetic per instruction); a float4 LDS load lands in two aligned register pairs
+typedef f32x2 v16[8];
+
+__device__ __forceinline__ float dot16(const v16& q, const float* r) {
+  f32x2 d = {0.f, 0.f};
 #pragma unroll
-  for (int e4 = 0; e4 < HD / 4; ++e4) {
+  for (int e4 = 0; e4 < 4; ++e4) {
     const float4 v = lds4(r + 4 * e4);
-    d = fmaf(q[4 * e4], v.x, d); d = fmaf(q[4 * e4 + 1], v.y, d);
-    d = fmaf(q[4 * e4 + 2], v.z, d); d = fmaf(q[4 * e4 + 3], v.w, d);
+    d = __builtin_elementwise_fma(q[2 * e4], f32x2{v.x, v.y}, d);
+    d = __builtin_elementwise_fma(q[2 * e4 + 1], f32x2{v.z, v.w}, d);
   }
-  return d;
+  return d.x + d.y;
 }
 
-__device__ __forceinline__ void axpy_row(float s, const float* r, float (&c)[HD]) {
+__device__ __forceinline__ void axpy16(float s, const float* r, v16& c) {
+  const f32x2 s2 = {s, s};
 #pragma unroll
-  for (int e4 = 0; e4 < HD / 4; ++e4) {
+  for (int e4 = 0; e4 < 4; ++e4) {
     const float4 v = lds4(r + 4 * e4);
-    c[4 * e4] = fmaf(s, v.x, c[4 * e4]); c[4 * e4 + 1] = fmaf(s, v.y, c[4 * e4 + 1]);
-    c[4 * e4 + 2] = fmaf(s, v.z, c[4 * e4 + 2]); c[4 * e4 + 3] = fmaf(s, v.w, c[4 * e4 + 3]);
+    c[2 * e4] = __builtin_elementwise_fma(s2, f32x2{v.x, v.y}, c[2 * e4]);
+    c[2 * e4 + 1] = __builtin_elementwise_fma(s2, f32x2{v.z, v.w}, c[2 * e4 + 1]);
   }
 }
 
-// acc[r][c] (+)= A[80 x K] (LDS, lda) . W^T, W [N x K] row-major in global; column tiles c0..c0+NC-1.
-// The next chunk's W fragment is loaded before the current chunk's MFMAs (register double buffer).
-template <int NC, int K>
+__device__ __forceinline__ void load16(const float* r, v16& v) {
+#pragma unroll
+  for (int e4 = 0; e4 < 4; ++e4) {
+    const float4 x = lds4(r + 4 * e4);
+    v[2 * e4] = f32x2{x.x, x.y};
+    v[2 * e4 + 1] = f32x2{x.z, x.w};
+  }
+}
+
+__device__ __forceinline__ void zero16(v16& v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = f32x2{0.f, 0.f};
+}
+
+__device__ __forceinline__ float4 quad16(const v16& v, int e4) {
+  return make_float4(v[2 * e4].x, v[2 * e4].y, v[2 * e4 + 1].x, v[2 * e4 + 1].y);
+}
+
+__device__ __forceinline__ void store16(float* r, const v16& v) {
+#pragma unroll
+  for (int e4 = 0; e4 < 4; ++e4) *reinterpret_cast<float4*>(r + 4 * e4) = quad16(v, e4);
+}
+
+// acc[r][c] (+)= A[rows of tiles R0..R0+NR-1] (LDS, lda) . W^T, W [N x K] row-major in global; column
+// tiles c0..c0+NC-1; acc rows beyond NR are untouched.  The next chunk's W fragment is loaded before
+// the current chunk's MFMAs (register double buffer).
+template <int NC, int K, int R0, int NR, int NA>
 __device__ __forceinline__ void gemm_xwt(const float* A, int lda, const float* __restrict__ W, int c0,
-                                         f32x4 (&acc)[RT][NC]) {
+                                         f32x4 (&acc)[NA][NC]) {
+  static_assert(NR <= NA, "accumulator rows");
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
   float4 bn[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) bn[c] = *reinterpret_cast<const float4*>(W + (int64_t)(16 * (c0 + c) + i) * K + 4 * h);
 #pragma unroll 4
   for (int kc = 0; kc < K / 16; ++kc) {
-    float4 a[RT], b[NC];
+    float4 a[NR], b[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) b[c] = bn[c];
     if (kc + 1 < K / 16) {
@@ -187,20 +280,22 @@ __device__ __forceinline__ void gemm_xwt(const float* A, int lda, const float* _
         bn[c] = *reinterpret_cast<const float4*>(W + (int64_t)(16 * (c0 + c) + i) * K + (kc + 1) * 16 + 4 * h);
     }
 #pragma unroll
-    for (int r = 0; r < RT; ++r) a[r] = lds4(A + (16 * r + i) * lda + kc * 16 + 4 * h);
+    for (int r = 0; r < NR; ++r) a[r] = lds4(A + (16 * (R0 + r) + i) * lda + kc * 16 + 4 * h);
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[r][c] = mfma4(comp(a[r], m), comp(b[c], m), acc[r][c]);
   }
 }
 
-// acc[r][c] (+)= Y[80 x N] (LDS, ldy) . W, W [N x KO] row-major in global; output column tiles c0..
-template <int NC, int N, int KO>
+// acc[r][c] (+)= Y[rows of tiles R0..R0+NR-1] (LDS, ldy) . W, W [N x KO] row-major in global; output
+// column tiles c0..
+template <int NC, int N, int KO, int R0, int NR, int NA>
 __device__ __forceinline__ void gemm_yw(const float* Y, int ldy, const float* __restrict__ W, int c0,
-                                        f32x4 (&acc)[RT][NC]) {
+                                        f32x4 (&acc)[NA][NC]) {
+  static_assert(NR <= NA, "accumulator rows");
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
   float bn[4][NC];
 #pragma unroll
@@ -209,7 +304,7 @@ __device__ __forceinline__ void gemm_yw(const float* Y, int ldy, const float* __
     for (int c = 0; c < NC; ++c) bn[m][c] = W[(int64_t)(4 * h + m) * KO + 16 * (c0 + c) + i];
 #pragma unroll 4
   for (int nc = 0; nc < N / 16; ++nc) {
-    float4 a[RT];
+    float4 a[NR];
     float b[4][NC];
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -222,15 +317,35 @@ __device__ __forceinline__ void gemm_yw(const float* Y, int ldy, const float* __
         for (int c = 0; c < NC; ++c) bn[m][c] = W[(int64_t)((nc + 1) * 16 + 4 * h + m) * KO + 16 * (c0 + c) + i];
     }
 #pragma unroll
-    for (int r = 0; r < RT; ++r) a[r] = lds4(Y + (16 * r + i) * ldy + nc * 16 + 4 * h);
+    for (int r = 0; r < NR; ++r) a[r] = lds4(Y + (16 * (R0 + r) + i) * ldy + nc * 16 + 4 * h);
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[r][c] = mfma4(comp(a[r], m), b[m][c], acc[r][c]);
   }
 }
+
+template <int NA, int NC>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[NA][NC]) {
+#pragma unroll
+  for (int r = 0; r < NA; ++r)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// this wave's row tiles: [0, RT0) for hf == 0, [RT0, RT) for hf == 1 (wave-uniform)
+#define FR_GEMM_XWT(NC, K, A, lda, W, c0, acc)                     \
+  do {                                                             \
+    if (hf == 0) gemm_xwt<NC, K, 0, RT0>(A, lda, W, c0, acc);      \
+    else gemm_xwt<NC, K, RT0, RT - RT0>(A, lda, W, c0, acc);       \
+  } while (0)
+#define FR_GEMM_YW(NC, N, KO, Y, ldy, W, c0, acc)                  \
+  do {                                                             \
+    if (hf == 0) gemm_yw<NC, N, KO, 0, RT0>(Y, ldy, W, c0, acc);   \
+    else gemm_yw<NC, N, KO, RT0, RT - RT0>(Y, ldy, W, c0, acc);    \
+  } while (0)
 
 // weight-gradient partial  P[n][k] = sum_t Y[t][n] X[t][k] over the 80 rows; this wave owns
 // n-tiles n0..n0+NN-1 x k-tiles k0..k0+NK-1; written to part (row length K).
@@ -267,12 +382,33 @@ __device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, const float
       for (int q = 0; q < 4; ++q) part[(16 * (n0 + a) + 4 * h + q) * K + 16 * (k0 + b) + i] = acc[a][b][q];
 }
 
-// column sums of an [80 x n] LDS tile (rows in order) -> part[0..n)
+// column sums of an [80 x n] LDS tile (n <= NT / 2) -> part[0..n): lanes 2c and 2c+1 sum rows
+// [0, 40) and [40, 80) of column c in order, then (first half) + (second half)
 __device__ __forceinline__ void colsum(const float* Y, int ldy, int n, float* __restrict__ part) {
-  for (int c = threadIdx.x; c < n; c += NT) {
+  const int c = threadIdx.x >> 1, hl = threadIdx.x & 1;
+  if (c < n) {
     float s = 0.f;
-    for (int t = 0; t < ROWS; ++t) s += Y[t * ldy + c];
-    part[c] = s;
+#pragma unroll 8
+    for (int t = hl * (ROWS / 2); t < (hl + 1) * (ROWS / 2); ++t) s += Y[t * ldy + c];
+    const float o = pair_swap(s);
+    if (!hl) part[c] = s + o;
+  }
+}
+
+// dst = dropout(src) over an [80 x 64] LDS tile of an E-wide site: one pair hash per two adjacent
+// columns (the pair of elements it covers)
+__device__ __forceinline__ void drop_pairs(const float* src, float* dst, uint32_t ks, int64_t tok0, uint32_t thr,
+                                           float scale) {
+  for (int e2 = threadIdx.x; e2 < ROWS * E / 2; e2 += NT) {
+    const int r = e2 / (E / 2), c = 2 * (e2 % (E / 2));
+    const float2 v = *reinterpret_cast<const float2*>(src + r * LD_E + c);
+    float2 o = make_float2(v.x * scale, v.y * scale);
+    if (thr != 0u) {
+      const uint32_t h = pair_hash(ks, (uint32_t)(((tok0 + r) * E + c) >> 1));
+      o.x = half_keep(h, 0, thr) ? o.x : 0.f;
+      o.y = half_keep(h, 1, thr) ? o.y : 0.f;
+    }
+    *reinterpret_cast<float2*>(dst + r * LD_E + c) = o;
   }
 }
 
@@ -288,29 +424,30 @@ __device__ __forceinline__ void lds_zero(float* p, int ld, int rows, int cols) {
 // copy costs one memory latency, not one per row.
 template <int COLS>
 __device__ __forceinline__ void lds_load(float* p, int ld, const float* __restrict__ g, int tv) {
-  constexpr int PER = COLS / 4, ITER = ROWS * PER / NT;
-  static_assert(ROWS * PER % NT == 0, "tile / block shape");
+  constexpr int PER = COLS / 4, TOT = ROWS * PER, ITER = (TOT + NT - 1) / NT;
   float4 v[ITER];
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
-    const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
+    const int e = min((int)threadIdx.x + k * NT, TOT - 1), r = e / PER, c4 = e % PER;
     v[k] = *reinterpret_cast<const float4*>(g + (int64_t)min(r, tv - 1) * COLS + 4 * c4);
   }
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
     const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
-    *reinterpret_cast<float4*>(p + r * ld + 4 * c4) = r < tv ? v[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (TOT % NT == 0 || e < TOT)
+      *reinterpret_cast<float4*>(p + r * ld + 4 * c4) = r < tv ? v[k] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
 // store rows [0, tv) of an LDS tile (ld) to a [*, COLS] global tensor, float4 per thread
 template <int COLS>
 __device__ __forceinline__ void lds_store(const float* p, int ld, float* __restrict__ g, int tv) {
-  constexpr int PER = COLS / 4, ITER = ROWS * PER / NT;
+  constexpr int PER = COLS / 4, TOT = ROWS * PER, ITER = (TOT + NT - 1) / NT;
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
     const int e = threadIdx.x + k * NT, r = e / PER, c4 = e % PER;
-    if (r < tv) *reinterpret_cast<float4*>(g + (int64_t)r * COLS + 4 * c4) = lds4(p + r * ld + 4 * c4);
+    if ((TOT % NT == 0 || e < TOT) && r < tv)
+      *reinterpret_cast<float4*>(g + (int64_t)r * COLS + 4 * c4) = lds4(p + r * ld + 4 * c4);
   }
 }
 
@@ -344,25 +481,25 @@ __device__ __forceinline__ void ln_rows_fwd(float* X, const float* __restrict__ 
 
 // LayerNorm backward over the rows of an LDS [80 x 64] tile of upstream gradients, in place
 // (dY -> dX).  y: saved LN input rows (global), st: (mean, rstd).  dgamma / dbeta partials via the
-// scratch (16 row groups x 64, summed in group order) -> pg / pb.
+// scratch (NT / 16 row groups x 64, summed in group order) -> pg / pb.
 __device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ y, const float* __restrict__ st,
                                             const float* __restrict__ g, int tv, float* scratch,
                                             float* __restrict__ pg, float* __restrict__ pb) {
   const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
-  constexpr int NR = ROWS / (NT / 16);
+  constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
   const float4 gg = *reinterpret_cast<const float4*>(g + 4 * l);
   float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
   float4 yv[NR];
   float2 sv[NR];
 #pragma unroll
   for (int k = 0; k < NR; ++k) {  // issue every row's loads first (rows clamped to tv - 1)
-    const int r = min(grp + k * (NT / 16), tv - 1);
+    const int r = min(grp + k * NG, tv - 1);
     yv[k] = *reinterpret_cast<const float4*>(y + (int64_t)r * E + 4 * l);
     sv[k] = *reinterpret_cast<const float2*>(st + 2 * r);
   }
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
-    const int r = grp + k * (NT / 16);
+    const int r = grp + k * NG;
     if (r >= tv) break;
     const float4 dy = lds4(D + r * LD_E + 4 * l);
     const float4 v = yv[k];
@@ -378,12 +515,13 @@ __device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ 
     sb = f4_add(sb, dy);
   }
   *reinterpret_cast<float4*>(scratch + grp * E + 4 * l) = sg;
-  *reinterpret_cast<float4*>(scratch + 16 * E + grp * E + 4 * l) = sb;
+  *reinterpret_cast<float4*>(scratch + NG * E + grp * E + 4 * l) = sb;
   __syncthreads();
   if (threadIdx.x < 2 * E) {
     const int which = threadIdx.x / E, c = threadIdx.x % E;
     float s = 0.f;
-    for (int q = 0; q < 16; ++q) s += scratch[which * 16 * E + q * E + c];
+#pragma unroll 8
+    for (int q = 0; q < NG; ++q) s += scratch[which * NG * E + q * E + c];
     (which ? pb : pg)[c] = s;
   }
   __syncthreads();
@@ -395,13 +533,15 @@ __device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ 
 template <int L>
 __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   constexpr int G = ROWS / L;
+  constexpr int NTASK = G * HEADS * L;
+  static_assert(2 * NTASK <= NT, "two lanes per attention task");
   __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];  // qkv (ctx in the q slots), then act
   __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];   // x -> y1 -> x1 -> y2
-  constexpr int NTASK = G * HEADS * L;
   __shared__ float SB[L * NTASK];                                   // attention score rows
   __shared__ float MS[ROWS];                                        // key mask of the tile's tokens
   const Weights& w = a.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int sg = wave & 3, hf = wave >> 2, r0 = hf ? RT0 : 0, nr = hf ? RT - RT0 : RT0;
   const int64_t seq0 = (int64_t)blockIdx.x * G;
   const int nseq = (int)min<int64_t>(G, a.ns - seq0);
   const int tv = nseq * L;
@@ -417,24 +557,20 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();
   FR_MARK(0, 1);
 
-  {  // qkv = x W_in^T + b_in  (wave: column tiles 3w..3w+2)
-    f32x4 acc[RT][3];
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_xwt<3, E>(RB, LD_E, w.w_in, 3 * wave, acc);
+  {  // qkv = x W_in^T + b_in  (SIMD slot sg: column tiles 3sg..3sg+2)
+    f32x4 acc[RT0][3];
+    zero_acc(acc);
+    FR_GEMM_XWT(3, E, RB, LD_E, w.w_in, 3 * sg, acc);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const int col = 16 * (3 * wave + c) + i16;
+      const int col = 16 * (3 * sg + c) + i16;
       const float bias = w.b_in[col];
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < RT0; ++r) {
+        if (r >= nr) break;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int row = 16 * r + 4 * h4 + q;
-          RA[row * LD_QKV + col] = acc[r][c][q] + bias;
-        }
+        for (int q = 0; q < 4; ++q) RA[(16 * (r0 + r) + 4 * h4 + q) * LD_QKV + col] = acc[r][c][q] + bias;
+      }
     }
   }
   __syncthreads();
@@ -443,67 +579,66 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();  // the copy has read every q slot before attention overwrites them with ctx
   FR_MARK(0, 20);
 
-  // attention: one thread per (sequence, head, query row); score rows in LDS as SB[j][task]
-  if (threadIdx.x < NTASK) {
-    const int g = threadIdx.x / (HEADS * L), hh = (threadIdx.x / L) % HEADS, qi = threadIdx.x % L;
-    if (g < nseq) {
-      const int rq = g * L + qi, me = threadIdx.x;
-      float q[HD];
-#pragma unroll
-      for (int e4 = 0; e4 < HD / 4; ++e4) {
-        const float4 v = lds4(RA + rq * LD_QKV + hh * HD + 4 * e4);
-        q[4 * e4] = v.x; q[4 * e4 + 1] = v.y; q[4 * e4 + 2] = v.z; q[4 * e4 + 3] = v.w;
-      }
+  // attention: lanes 2t, 2t+1 own task t = (sequence, head, query row), dimensions [16 hl, 16 hl + 16);
+  // score rows in LDS as SB[j][task]
+  {
+    const int t = threadIdx.x >> 1, hl = threadIdx.x & 1;
+    const int g = t / (HEADS * L), hh = (t / L) % HEADS, qi = t % L;
+    if (t < NTASK && g < nseq) {  // both lanes of a pair take the same branch
+      const int rq = g * L + qi, dof = hh * HD + 16 * hl;
+      v16 q;
+      load16(RA + rq * LD_QKV + dof, q);
+      float* sr = SB + t;  // score row j at sr[j * NTASK] (both lanes write the same value)
       float mx = -INFINITY;
 #pragma unroll 2
       for (int j = 0; j < L; ++j) {
-        const float s = dot_row(q, RA + (g * L + j) * LD_QKV + E + hh * HD) * kScale + MS[g * L + j];
-        SB[j * NTASK + me] = s;
-        mx = fmaxf(mx, s);
+        const float d = dot16(q, RA + (g * L + j) * LD_QKV + E + dof);
+        const float sj = (d + pair_swap(d)) * kScale + MS[g * L + j];
+        sr[j * NTASK] = sj;
+        mx = fmaxf(mx, sj);
       }
       float sum = 0.f;
+#pragma unroll 4
       for (int j = 0; j < L; ++j) {
-        const float e = expf(SB[j * NTASK + me] - mx);
-        SB[j * NTASK + me] = e;
+        const float e = expf(sr[j * NTASK] - mx);
+        sr[j * NTASK] = e;
         sum += e;
       }
-      const float inv = 1.f / sum;
+      const float pin = w.scale[0] / sum;
       const uint32_t base = (uint32_t)((((seq0 + g) * HEADS + hh) * L + qi) * L);
-      float c[HD];
-#pragma unroll
-      for (int e = 0; e < HD; ++e) c[e] = 0.f;
+      v16 c;
+      zero16(c);
 #pragma unroll 2
       for (int j = 0; j < L; ++j) {
-        const float p = keep(ks.k[0], base + j, w.thr[0]) ? SB[j * NTASK + me] * inv * w.scale[0] : 0.f;
-        axpy_row(p, RA + (g * L + j) * LD_QKV + 2 * E + hh * HD, c);
+        const float p = keep_att(ks.k[0], base, j, w.thr[0]) ? sr[j * NTASK] * pin : 0.f;
+        axpy16(p, RA + (g * L + j) * LD_QKV + 2 * E + dof, c);
       }
+      store16(RA + rq * LD_QKV + dof, c);
+      float* go = a.ctx + (tok0 + rq) * E + dof;
 #pragma unroll
-      for (int e4 = 0; e4 < HD / 4; ++e4) {
-        const float4 v = make_float4(c[4 * e4], c[4 * e4 + 1], c[4 * e4 + 2], c[4 * e4 + 3]);
-        *reinterpret_cast<float4*>(RA + rq * LD_QKV + hh * HD + 4 * e4) = v;
-        *reinterpret_cast<float4*>(a.ctx + (tok0 + rq) * E + hh * HD + 4 * e4) = v;
-      }
+      for (int e4 = 0; e4 < 4; ++e4) *reinterpret_cast<float4*>(go + 4 * e4) = quad16(c, e4);
     }
   }
   __syncthreads();
   FR_MARK(0, 3);
 
-  {  // y1 = x + dropout1(ctx W_o^T + b_o)   (wave: column tile w); ctx rows of padded sequences are stale
-    f32x4 acc[RT][1];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_xwt<1, E>(RA, LD_QKV, w.w_o, wave, acc);
-    const int col = 16 * wave + i16;
+  {  // y1 = x + dropout1(ctx W_o^T + b_o)   (column tile sg); ctx rows of padded sequences are stale
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_XWT(1, E, RA, LD_QKV, w.w_o, sg, acc);
+    const int col = 16 * sg + i16;
     const float bias = w.b_o[col];
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
+      const int row0 = 16 * (r0 + r) + 4 * h4;
+      const uint32_t kb = frag_keep4(ks.k[1], tok0 + row0, E, col, w.thr[1]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 16 * r + 4 * h4 + q;
         const float o = acc[r][0][q] + bias;
-        const float d = keep(ks.k[1], (uint32_t)((tok0 + row) * E + col), w.thr[1]) ? o * w.scale[1] : 0.f;
-        RB[row * LD_E + col] += d;
+        RB[(row0 + q) * LD_E + col] += ((kb >> q) & 1u) ? o * w.scale[1] : 0.f;
       }
+    }
   }
   __syncthreads();
   FR_MARK(0, 4);
@@ -511,52 +646,60 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();
   FR_MARK(0, 5);
 
-  {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA  (wave: column tiles 4w..4w+3)
-    f32x4 acc[RT][4];
+  {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA.  Column split (wave: tiles 4sg + 2hf, +1;
+     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue
+    f32x4 acc[RT][2];
+    zero_acc(acc);
+    gemm_xwt<2, E, 0, RT>(RB, LD_E, w.w1, 4 * sg + 2 * hf, acc);
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_xwt<4, E>(RB, LD_E, w.w1, 4 * wave, acc);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int col = 16 * (4 * wave + c) + i16;
+    for (int cc = 0; cc < 2; ++cc) {
+      const int c = 2 * hf + cc;  // column tile within the SIMD slot's four (dact fragment index)
+      const int col = 16 * (4 * sg + c) + i16;
       const float bias = w.b1[col];
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
+        const int row0 = 16 * r + 4 * h4;
+        const uint32_t kb = frag_keep4(ks.k[2], tok0 + row0, FF, col, w.thr[2]);
         float d[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int row = 16 * r + 4 * h4 + q;
-          const float2 fg = act_fwd_grad(acc[r][c][q] + bias, w.gelu);
-          const bool kp = keep(ks.k[2], (uint32_t)((tok0 + row) * FF + col), w.thr[2]);
-          RA[row * LD_FF + col] = kp ? fg.x * w.scale[2] : 0.f;
-          d[q] = kp ? fg.y * w.scale[2] : 0.f;
+        for (int q2 = 0; q2 < 2; ++q2) {
+          f32x2 av, gv;
+          act_fwd_grad2(f32x2{acc[r][cc][2 * q2], acc[r][cc][2 * q2 + 1]} + bias, w.gelu, av, gv);
+          av = av * w.scale[2];
+          gv = gv * w.scale[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int q = 2 * q2 + u;
+            const bool kp = (kb >> q) & 1u;
+            RA[(row0 + q) * LD_FF + col] = kp ? av[u] : 0.f;
+            d[q] = kp ? gv[u] : 0.f;
+          }
         }
         // dact in the MFMA fragment layout: one coalesced float4 per lane, read back the same way
-        *reinterpret_cast<float4*>(a.dact + dact_frag(blockIdx.x, wave, c, r, lane)) = make_float4(d[0], d[1], d[2], d[3]);
+        *reinterpret_cast<float4*>(a.dact + dact_frag(blockIdx.x, sg, c, r, lane)) = make_float4(d[0], d[1], d[2], d[3]);
       }
     }
   }
   __syncthreads();
   FR_MARK(0, 6);
 
-  {  // y2 = x1 + dropout2(act' W2^T + b2)  (wave: column tile w, K = 256)
-    f32x4 acc[RT][1];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_xwt<1, FF>(RA, LD_FF, w.w2, wave, acc);
-    const int col = 16 * wave + i16;
+  {  // y2 = x1 + dropout2(act' W2^T + b2)  (column tile sg, K = 256)
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_XWT(1, FF, RA, LD_FF, w.w2, sg, acc);
+    const int col = 16 * sg + i16;
     const float bias = w.b2[col];
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
+      const int row0 = 16 * (r0 + r) + 4 * h4;
+      const uint32_t kb = frag_keep4(ks.k[3], tok0 + row0, E, col, w.thr[3]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 16 * r + 4 * h4 + q;
         const float o = acc[r][0][q] + bias;
-        const float d = keep(ks.k[3], (uint32_t)((tok0 + row) * E + col), w.thr[3]) ? o * w.scale[3] : 0.f;
-        RB[row * LD_E + col] += d;
+        RB[(row0 + q) * LD_E + col] += ((kb >> q) & 1u) ? o * w.scale[3] : 0.f;
       }
+    }
   }
   __syncthreads();
   FR_MARK(0, 7);
@@ -571,13 +714,17 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
 template <int L>
 __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   constexpr int G = ROWS / L;
+  constexpr int NTASK = G * HEADS * L;
+  static_assert(2 * NTASK <= NT, "two lanes per attention task");
   __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];
   __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];
   __shared__ __attribute__((aligned(16))) float RC[ROWS * LD_E];
   __shared__ __attribute__((aligned(16))) float RD[BUF_D];
-  static_assert(2 * G * HEADS * L * L <= BUF_D && ROWS * LD_E <= BUF_D, "attention buffers");
+  static_assert(2 * G * HEADS * L * L <= BUF_D && ROWS * LD_E <= BUF_D && 2 * (NT / 16) * E <= BUF_D,
+                "attention / LayerNorm scratch");
   const Weights& w = a.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int sg = wave & 3, hf = wave >> 2, r0 = hf ? RT0 : 0, nr = hf ? RT - RT0 : RT0;
   const int64_t seq0 = (int64_t)blockIdx.x * G;
   const int nseq = (int)min<int64_t>(G, a.ns - seq0);
   const int tv = nseq * L;
@@ -596,42 +743,37 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   ln_rows_bwd(RB, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, tv, RD, part + OFF_G2, part + OFF_BE2);
 
   // 2. dG = dropout2'(dY2) -> RC;  act' (saved by the forward) -> RA
-  for (int e = threadIdx.x; e < ROWS * E; e += NT) {
-    const int r = e / E, c = e % E;
-    RC[r * LD_E + c] = keep(ks.k[3], (uint32_t)((tok0 + r) * E + c), w.thr[3]) ? RB[r * LD_E + c] * w.scale[3] : 0.f;
-  }
+  drop_pairs(RB, RC, ks.k[3], tok0, w.thr[3], w.scale[3]);
   lds_load<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);
   __syncthreads();
   FR_MARK(1, 2);
 
-  // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 4w..4w+3);  db2
-  wgrad_tiles<4, 4>(RC, LD_E, RA, LD_FF, 0, 4 * wave, part + OFF_W2, FF);
+  // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 2w, 2w+1);  db2
+  wgrad_tiles<4, 2>(RC, LD_E, RA, LD_FF, 0, 2 * wave, part + OFF_W2, FF);
   colsum(RC, LD_E, E, part + OFF_B2);
 
-  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA
-    f32x4 acc[RT][4];
+  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA  (wave: column tiles
+     // 4sg + 2hf, +1; every row tile)
+    f32x4 acc[RT][2];
+    zero_acc(acc);
+    gemm_yw<2, E, FF, 0, RT>(RC, LD_E, w.w2, 4 * sg + 2 * hf, acc);
+    float4 pv[2][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_yw<4, E, FF>(RC, LD_E, w.w2, 4 * wave, acc);
-    float4 pv[4][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
       for (int r = 0; r < RT; ++r)
-        pv[c][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, wave, c, r, lane));
+        pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, sg, 2 * hf + cc, r, lane));
     __syncthreads();  // every wave is done reading act' from RA
     FR_MARK(1, 3);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int col = 16 * (4 * wave + c) + i16;
+    for (int cc = 0; cc < 2; ++cc) {
+      const int col = 16 * (4 * sg + 2 * hf + cc) + i16;
 #pragma unroll
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = 16 * r + 4 * h4 + q;
-          RA[row * LD_FF + col] = row < tv ? acc[r][c][q] * comp(pv[c][r], q) : 0.f;
+          RA[row * LD_FF + col] = row < tv ? acc[r][cc][q] * comp(pv[cc][r], q) : 0.f;
         }
     }
   }
@@ -644,18 +786,19 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
     const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
     const float4 gg = *reinterpret_cast<const float4*>(w.g1 + 4 * l);
     const float4 bb = *reinterpret_cast<const float4*>(w.be1 + 4 * l);
-    constexpr int NR = ROWS / (NT / 16);
+    constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
     float4 yv[NR];
     float2 sv[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
-      const int r = min(grp + k * (NT / 16), tv - 1);
+      const int r = min(grp + k * NG, tv - 1);
       yv[k] = *reinterpret_cast<const float4*>(a.y1 + (tok0 + r) * E + 4 * l);
       sv[k] = *reinterpret_cast<const float2*>(a.st1 + 2 * (tok0 + r));
     }
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
-      const int r = grp + k * (NT / 16);
+      const int r = grp + k * NG;
+      if (r >= ROWS) break;
       const float4 v = yv[k];
       const float mean = sv[k].x, rstd = sv[k].y;
       const float4 o = make_float4(fmaf((v.x - mean) * rstd, gg.x, bb.x), fmaf((v.y - mean) * rstd, gg.y, bb.y),
@@ -666,19 +809,20 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   __syncthreads();
   FR_MARK(1, 5);
 
-  // 6. dW1 = dpre^T x1  [256 x 64] (wave: n-tiles 4w..4w+3)
-  wgrad_tiles<4, 4>(RA, LD_FF, RC, LD_E, 4 * wave, 0, part + OFF_W1, E);
+  // 6. dW1 = dpre^T x1  [256 x 64] (wave: n-tiles 2w, 2w+1)
+  wgrad_tiles<2, 4>(RA, LD_FF, RC, LD_E, 2 * wave, 0, part + OFF_W1, E);
 
   {  // 7. dX1 = dY2 + dpre W1  -> RB
-    f32x4 acc[RT][1];
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_YW(1, FF, E, RA, LD_FF, w.w1, sg, acc);
+    const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_yw<1, FF, E>(RA, LD_FF, w.w1, wave, acc);
-    const int col = 16 * wave + i16;
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) RB[(16 * r + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
+      for (int q = 0; q < 4; ++q) RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
+    }
   }
   __syncthreads();
   FR_MARK(1, 6);
@@ -687,155 +831,133 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   ln_rows_bwd(RB, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, tv, RD, part + OFF_G1, part + OFF_BE1);
 
   // 9. dO = dropout1'(dY1) -> RC;  ctx -> RD
-  for (int e = threadIdx.x; e < ROWS * E; e += NT) {
-    const int r = e / E, c = e % E;
-    RC[r * LD_E + c] = keep(ks.k[1], (uint32_t)((tok0 + r) * E + c), w.thr[1]) ? RB[r * LD_E + c] * w.scale[1] : 0.f;
-  }
+  drop_pairs(RB, RC, ks.k[1], tok0, w.thr[1], w.scale[1]);
   lds_load<E>(RD, LD_E, a.ctx + tok0 * E, tv);
   __syncthreads();
   FR_MARK(1, 7);
 
-  // 10. dW_o = dO^T ctx [64 x 64] (wave: n-tile w); db_o
-  wgrad_tiles<1, 4>(RC, LD_E, RD, LD_E, wave, 0, part + OFF_WO, E);
+  // 10. dW_o = dO^T ctx [64 x 64] (wave: n-tile sg, k-tiles 2hf, 2hf+1); db_o
+  wgrad_tiles<1, 2>(RC, LD_E, RD, LD_E, sg, 2 * hf, part + OFF_WO, E);
   colsum(RC, LD_E, E, part + OFF_BO);
 
   {  // 11. dctx = dO W_o -> RC;  qkv -> RA
-    f32x4 acc[RT][1];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_yw<1, E, E>(RC, LD_E, w.w_o, wave, acc);
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_YW(1, E, E, RC, LD_E, w.w_o, sg, acc);
     lds_load<QKV>(RA, LD_QKV, a.qkv + tok0 * QKV, tv);
     __syncthreads();
     FR_MARK(1, 8);
-    const int col = 16 * wave + i16;
+    const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) RC[(16 * r + 4 * h4 + q) * LD_E + col] = acc[r][0][q];
+      for (int q = 0; q < 4; ++q) RC[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] = acc[r][0][q];
+    }
   }
   __syncthreads();
   FR_MARK(1, 9);
 
-  // 12. attention backward.  RD: P[j][task] (scores -> p -> p') and S[j][task] (dL/dp' -> ds*scale),
-  // task = (sequence, head, query row)
-  constexpr int NTASK = G * HEADS * L;
+  // 12. attention backward.  RD: P[j][task] (scores -> p -> p') and S[j][task] (dL/dp' -> ds * scale),
+  // task = (sequence, head, query row); lanes 2t, 2t+1 own task t's dimensions [16 hl, 16 hl + 16)
   float* Pb = RD;
   float* Sb = RD + NTASK * L;
-  const bool task = threadIdx.x < NTASK;
-  const int tg = threadIdx.x / (HEADS * L), thh = (threadIdx.x / L) % HEADS, ti = threadIdx.x % L;
-  const bool live = task && tg < nseq;
-  float dq[HD];
+  const int tt = threadIdx.x >> 1, hl = threadIdx.x & 1;
+  const int tg = tt / (HEADS * L), thh = (tt / L) % HEADS, ti = tt % L;
+  const bool live = tt < NTASK && tg < nseq;  // the same for both lanes of a pair
+  const int dof = thh * HD + 16 * hl;
+  v16 dq;
   if (live) {  // phase a: query row ti
     const int rq = tg * L + ti;
-    float q[HD], dc[HD];
-#pragma unroll
-    for (int e4 = 0; e4 < HD / 4; ++e4) {
-      const float4 v = lds4(RA + rq * LD_QKV + thh * HD + 4 * e4);
-      q[4 * e4] = v.x; q[4 * e4 + 1] = v.y; q[4 * e4 + 2] = v.z; q[4 * e4 + 3] = v.w;
-      const float4 d = lds4(RC + rq * LD_E + thh * HD + 4 * e4);
-      dc[4 * e4] = d.x; dc[4 * e4 + 1] = d.y; dc[4 * e4 + 2] = d.z; dc[4 * e4 + 3] = d.w;
-    }
-    const int me = threadIdx.x;
+    v16 q, dc;
+    load16(RA + rq * LD_QKV + dof, q);
+    load16(RC + rq * LD_E + dof, dc);
+    float* pr = Pb + tt;  // both lanes of the pair write the same values
+    float* sr = Sb + tt;
     float mx = -INFINITY;
 #pragma unroll 2
     for (int j = 0; j < L; ++j) {
-      const float* kr = RA + (tg * L + j) * LD_QKV + E + thh * HD;
-      const float s = dot_row(q, kr) * kScale + MS[tg * L + j];
-      Pb[j * NTASK + me] = s;
-      Sb[j * NTASK + me] = dot_row(dc, kr + E);    // dL/dp' = dctx . v_j
-      mx = fmaxf(mx, s);
+      const float* kr = RA + (tg * L + j) * LD_QKV + E + dof;
+      const float d1 = dot16(q, kr), d2 = dot16(dc, kr + E);   // q . k_j,  dctx . v_j (= dL/dp')
+      const float sj = (d1 + pair_swap(d1)) * kScale + MS[tg * L + j];
+      pr[j * NTASK] = sj;
+      sr[j * NTASK] = d2 + pair_swap(d2);
+      mx = fmaxf(mx, sj);
     }
     float sum = 0.f;
+#pragma unroll 4
     for (int j = 0; j < L; ++j) {
-      const float e = expf(Pb[j * NTASK + me] - mx);
-      Pb[j * NTASK + me] = e;
+      const float e = expf(pr[j * NTASK] - mx);
+      pr[j * NTASK] = e;
       sum += e;
     }
     const float inv = 1.f / sum;
     const uint32_t base = (uint32_t)((((seq0 + tg) * HEADS + thh) * L + ti) * L);
     float D = 0.f;
+#pragma unroll 4
     for (int j = 0; j < L; ++j) {
-      const float p = Pb[j * NTASK + me] * inv;
-      const bool kp = keep(ks.k[0], base + j, w.thr[0]);
-      const float dp = kp ? Sb[j * NTASK + me] * w.scale[0] : 0.f;  // dL/dp
-      Pb[j * NTASK + me] = kp ? p : -p;                              // keep bit in the sign
-      Sb[j * NTASK + me] = dp;
-      D = fmaf(p, dp, D);
+      const float p = pr[j * NTASK] * inv;
+      const bool kp = keep_att(ks.k[0], base, j, w.thr[0]);
+      const float dpj = kp ? sr[j * NTASK] * w.scale[0] : 0.f;  // dL/dp
+      pr[j * NTASK] = kp ? p : -p;                               // keep bit in the sign
+      sr[j * NTASK] = dpj;
+      D = fmaf(p, dpj, D);
     }
-#pragma unroll
-    for (int e = 0; e < HD; ++e) dq[e] = 0.f;
+    zero16(dq);
 #pragma unroll 2
     for (int j = 0; j < L; ++j) {
-      const float ps = Pb[j * NTASK + me], p = fabsf(ps);
-      const float ds = p * (Sb[j * NTASK + me] - D) * kScale;
-      Sb[j * NTASK + me] = ds;
-      Pb[j * NTASK + me] = ps > 0.f ? p * w.scale[0] : 0.f;  // p'
-      axpy_row(ds, RA + (tg * L + j) * LD_QKV + E + thh * HD, dq);
+      const float ps = pr[j * NTASK], p = fabsf(ps);
+      const float ds = p * (sr[j * NTASK] - D) * kScale;
+      axpy16(ds, RA + (tg * L + j) * LD_QKV + E + dof, dq);
+      sr[j * NTASK] = ds;
+      pr[j * NTASK] = ps > 0.f ? p * w.scale[0] : 0.f;  // p'
     }
   }
   __syncthreads();
   FR_MARK(1, 10);
   if (live) {  // phase b: key row j = ti:  dk_j = sum_i ds_ij q_i,  dv_j = sum_i p'_ij dctx_i
     const int rk = tg * L + ti;
-    float dk[HD], dv[HD];
-#pragma unroll
-    for (int e = 0; e < HD; ++e) dk[e] = dv[e] = 0.f;
+    v16 dk, dv;
+    zero16(dk);
+    zero16(dv);
+#pragma unroll 4
     for (int qi = 0; qi < L; ++qi) {
       const int qt = (tg * HEADS + thh) * L + qi;
       const float ds = Sb[ti * NTASK + qt];
       const float pp = Pb[ti * NTASK + qt];
-      const float* qr = RA + (tg * L + qi) * LD_QKV + thh * HD;
-      const float* dr = RC + (tg * L + qi) * LD_E + thh * HD;
-#pragma unroll
-      for (int e4 = 0; e4 < HD / 4; ++e4) {
-        const float4 qv = lds4(qr + 4 * e4);
-        const float4 dd = lds4(dr + 4 * e4);
-        dk[4 * e4] = fmaf(ds, qv.x, dk[4 * e4]); dk[4 * e4 + 1] = fmaf(ds, qv.y, dk[4 * e4 + 1]);
-        dk[4 * e4 + 2] = fmaf(ds, qv.z, dk[4 * e4 + 2]); dk[4 * e4 + 3] = fmaf(ds, qv.w, dk[4 * e4 + 3]);
-        dv[4 * e4] = fmaf(pp, dd.x, dv[4 * e4]); dv[4 * e4 + 1] = fmaf(pp, dd.y, dv[4 * e4 + 1]);
-        dv[4 * e4 + 2] = fmaf(pp, dd.z, dv[4 * e4 + 2]); dv[4 * e4 + 3] = fmaf(pp, dd.w, dv[4 * e4 + 3]);
-      }
+      axpy16(ds, RA + (tg * L + qi) * LD_QKV + dof, dk);
+      axpy16(pp, RC + (tg * L + qi) * LD_E + dof, dv);
     }
     // k / v slots of row rk are read by no one after phase a
-#pragma unroll
-    for (int e4 = 0; e4 < HD / 4; ++e4) {
-      *reinterpret_cast<float4*>(RA + rk * LD_QKV + E + thh * HD + 4 * e4) =
-          make_float4(dk[4 * e4], dk[4 * e4 + 1], dk[4 * e4 + 2], dk[4 * e4 + 3]);
-      *reinterpret_cast<float4*>(RA + rk * LD_QKV + 2 * E + thh * HD + 4 * e4) =
-          make_float4(dv[4 * e4], dv[4 * e4 + 1], dv[4 * e4 + 2], dv[4 * e4 + 3]);
-    }
+    store16(RA + rk * LD_QKV + E + dof, dk);
+    store16(RA + rk * LD_QKV + 2 * E + dof, dv);
   }
   __syncthreads();
   FR_MARK(1, 11);
-  if (live) {
-    const int rq = tg * L + ti;
-#pragma unroll
-    for (int e4 = 0; e4 < HD / 4; ++e4)
-      *reinterpret_cast<float4*>(RA + rq * LD_QKV + thh * HD + 4 * e4) =
-          make_float4(dq[4 * e4], dq[4 * e4 + 1], dq[4 * e4 + 2], dq[4 * e4 + 3]);
-  }
+  if (live) store16(RA + (tg * L + ti) * LD_QKV + dof, dq);
   if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
   lds_load<E>(RC, LD_E, a.x + tok0 * E, tv);
   __syncthreads();
   FR_MARK(1, 12);
 
-  // 13. db_in; dW_in = dqkv^T x [192 x 64] (wave: n-tiles 3w..3w+2)
+  // 13. db_in; dW_in = dqkv^T x [192 x 64] (wave: n-tiles 3sg..3sg+2, k-tiles 2hf, 2hf+1)
   colsum(RA, LD_QKV, QKV, part + OFF_BIN);
-  wgrad_tiles<3, 4>(RA, LD_QKV, RC, LD_E, 3 * wave, 0, part + OFF_WIN, E);
+  wgrad_tiles<3, 2>(RA, LD_QKV, RC, LD_E, 3 * sg, 2 * hf, part + OFF_WIN, E);
 
   {  // 14. dX = dY1 + dqkv W_in
-    f32x4 acc[RT][1];
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_YW(1, QKV, E, RA, LD_QKV, w.w_in, sg, acc);
+    const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r) acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    gemm_yw<1, QKV, E>(RA, LD_QKV, w.w_in, wave, acc);
-    const int col = 16 * wave + i16;
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 16 * r + 4 * h4 + q;
+        const int row = 16 * (r0 + r) + 4 * h4 + q;
         if (row < tv) a.dx[(tok0 + row) * E + col] = RB[row * LD_E + col] + acc[r][0][q];
       }
+    }
   }
   FR_MARK(1, 31);
 }
@@ -900,8 +1022,8 @@ int fill_weights(Weights& w, const float* const* p, const float* eps, const floa
   w.eps2 = eps[1];
   for (int k = 0; k < 4; ++k) {
     FR_REQUIRE(drop[k] >= 0.f && drop[k] < 1.f, "dropout probability must be in [0, 1)");
-    const double t = (double)drop[k] * 4294967296.0;
-    w.thr[k] = drop[k] == 0.f ? 0u : (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+    const double t = (double)drop[k] * 65536.0;
+    w.thr[k] = drop[k] == 0.f ? 0u : (uint32_t)(t >= 65535.0 ? 65535.0 : t);
     w.scale[k] = 1.f / (1.f - drop[k]);
   }
   w.seed = seed;

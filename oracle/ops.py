@@ -175,8 +175,9 @@ def _mix64(z: np.ndarray) -> np.ndarray:
 def encoder_keep_masks(seed: int, counter: int, n_seq: int, L: int, drop, heads: int = 2, d: int = 64,
                        ff: int = 256):
     """The fused encoder's dropout keep-masks (fr_encoder.hip: site_keys / keep), restated in numpy.
-    key = mix64(seed ^ mix64(counter + C)); site key k_s = hi32(mix64(key + s + 1)); element e of
-    site s is kept iff lowbias32(e * 0x9E3779B1 + k_s) >= floor(p * 2^32) (uint32 arithmetic).
+    key = mix64(seed ^ mix64(counter + C)); site key k_s = hi32(mix64(key + s + 1)); elements 2m and
+    2m+1 of site s share h = lowbias32(m * 0x9E3779B1 + k_s) (uint32 arithmetic), and element e is
+    kept iff the (e & 1) 16-bit half of h (low half for even e) is >= floor(p * 2^16).
     Sites: 0 attention probs [n_seq, heads, L, L], 1 out-proj [n_seq, L, d], 2 FF activation
     [n_seq, L, ff], 3 FF out [n_seq, L, d] (element index = row-major position).  Returns 4 float64
     arrays of 0/1."""
@@ -190,15 +191,17 @@ def encoder_keep_masks(seed: int, counter: int, n_seq: int, L: int, drop, heads:
             if p == 0:
                 out.append(np.ones(shape))
                 continue
-            thr = min(int(float(np.float32(p)) * 4294967296.0), 4294967295)
+            thr = min(int(float(np.float32(p)) * 65536.0), 65535)
             ks = (_mix64(key + np.uint64(site + 1)) >> np.uint64(32)).astype(u32)
-            x = np.arange(int(np.prod(shape)), dtype=np.uint64).astype(u32) * u32(0x9E3779B1) + ks
+            e = np.arange(int(np.prod(shape)), dtype=np.uint64).astype(u32)
+            x = (e >> u32(1)) * u32(0x9E3779B1) + ks
             x ^= x >> u32(16)
             x *= u32(0x7FEB352D)
             x ^= x >> u32(15)
             x *= u32(0x846CA68B)
             x ^= x >> u32(16)
-            out.append((x >= u32(thr)).astype(np.float64).reshape(shape))
+            half = np.where(e & u32(1), x >> u32(16), x & u32(0xFFFF))
+            out.append((half >= u32(thr)).astype(np.float64).reshape(shape))
     return out
 
 
