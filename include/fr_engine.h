@@ -114,10 +114,19 @@ int fr_bpr_fwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
                const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
                int64_t B, int d, float gamma, float* d_out,
                void* d_workspace, int64_t workspace_bytes, void* stream);
+/* fr_bpr_fwd that also writes the gathered item rows [I[p] ; I[n]] to d_rows ([2B, d], row stride
+ * ld_rows; NULL: not written) -- the torch.cat([item_all[pos], item_all[neg]]) HealthRec's KD
+ * term reads (cikm_model.py:256-257, 263) without a separate index_select launch. */
+int fr_bpr_fwd_rows(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                    const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                    const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+                    int64_t B, int d, float gamma, float* d_out, float* d_rows, int64_t ld_rows,
+                    void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* Backward.  g_mf scales d(out[0]); g_reg scales d(out[4]) (i.e. reg_weight * upstream grad).
  * d_gscale (optional, device float[2]) multiplies g_mf / g_reg on the device so no host
- * read of the upstream gradient is needed.  Gradients are ACCUMULATED (+=) into dU/dI/dUe/dIe
+ * read of the upstream gradient is needed (d_gscale[1] is read only when dUe or dIe is given, so
+ * a BPR-only backward may pass a single device float).  Gradients are ACCUMULATED (+=) into dU/dI/dUe/dIe
  * (any may be NULL); each uses the leading dimension of its forward table (ldu/ldi/ldue/ldie).  deterministic != 0 selects the ordered (atomic-free) scatter. */
 int fr_bpr_bwd(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
                const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
@@ -555,7 +564,12 @@ int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* 
  *               workgroup per listed row (d = 64; deterministic, equal to the full launch's row to
  *               fp32 rounding); the other rows of Y are not written.  The training step needs the UI propagation only
  *               at the batch's users and items (cikm_model.py:255-261): 3B rows instead of U + I.
+ *   d_a1_gate   optional uint8 per output row: A1's row r is read only where a1_gate[r] != 0 and
+ *               counts as zero elsewhere (A1 = the upstream gradient itself, valid only at the
+ *               marked rows: no zero fill of the rest of it is needed).
  * fr_rows_mark: mask[ids[k][i] + off[k]] = value (sets / clears a column mask from a row list).
+ * fr_rows_mark_zero: the same, and rows ids[k][i] + off[k] of Z ([*, d], stride ldz) set to 0
+ *               (the batch rows of an upstream gradient about to be accumulated into).
  * ------------------------------------------------------------------------------------------ */
 typedef struct fr_tab {
   const float* lo;
@@ -571,9 +585,25 @@ typedef struct fr_rowlist {
 int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
                    const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
                    const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
-                   float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, void* d_workspace,
-                   int64_t workspace_bytes, void* stream);
+                   float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, const uint8_t* d_a1_gate,
+                   void* d_workspace, int64_t workspace_bytes, void* stream);
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
+int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
+                      void* stream);
+
+/* fr_graph_bpr_finish: the tail of HealthRec's fused propagation + BPR backward (engine
+ * ops.graph_bpr), after both propagation backwards have written dUe (user_embedding's gradient)
+ * and dIe (item_embedding's):
+ *   mask[u_b] = mask[U + p_b] = mask[U + n_b] = 0   (clears the column mask; d_mask may be NULL),
+ *   dUe[u_b] += r_u Ue[u_b], dIe[p_b] += r_p Ie[p_b], dIe[n_b] += r_n Ie[n_b]   (float atomics)
+ *     with r_x = g_reg * d_greg[0] / B / ||.||_F of block x (the norms fr_bpr_fwd left in the
+ *     workspace): EmbLoss(u_ego, pos_ego, neg_ego)'s gradient, cikm_model.py:273-279;
+ *   d_zero[0 .. zero_n) = 0   (ingre_embedding's padding row, not a graph node).
+ * One launch instead of three (unmark, EmbLoss scatter, padding-row fill). */
+int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t ldue, const float* d_Ie,
+                        int64_t ldie, const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B,
+                        int d, float g_reg, const float* d_greg, float* d_dUe, float* d_dIe,
+                        float* d_zero, int zero_n, void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * fr_feed_batch: one step's batch in one launch.  Replaces TrainDataLoader.__getitem__ x B +
@@ -583,14 +613,15 @@ int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* s
  *     (the cursor is not advanced here);
  *   plain mode: p, n are inputs.
  *   Both: rows j of [p ; n]: pn[j], out_codes[j] = codes[pn[j]] ([L] int64), out_nums[j],
- *   out_health[j] = health[pn[j]] ([H] float, optional: H = 0 and NULLs), out_mask[j][c] =
- *   out_codes[j][c] == pad (optional, HealthRec's key-padding mask, cikm_model.py:231-232).
+ *   out_health[j] = health[pn[j]] ([H] float, optional: H = 0 and NULLs), out_kpm[j][c] =
+ *   -inf where out_codes[j][c] == pad, else 0 (optional: HealthRec's key-padding mask,
+ *   cikm_model.py:231-232, in the additive float form the encoder layer consumes).
  * ------------------------------------------------------------------------------------------ */
 int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* d_items, const int64_t* d_negs,
                   const int64_t* d_cursor, int64_t B, int64_t* d_u, int64_t* d_p, int64_t* d_n,
                   const int64_t* d_codes, int L, const int64_t* d_nums, const float* d_health, int H,
                   int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes, int64_t* d_out_nums,
-                  float* d_out_health, bool* d_out_mask, void* stream);
+                  float* d_out_health, float* d_out_kpm, void* stream);
 
 /* fr_step_book: the training loop's per-step loss bookkeeping (common/trainer.py:183-193) on the
  * device: acc[i] (+)= (double)*parts[i] for the n (<= 8) scalar loss components,

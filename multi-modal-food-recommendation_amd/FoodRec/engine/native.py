@@ -56,9 +56,16 @@ _SIGS = {
                             c_void_p, c_int64, c_void_p]),
     "fr_spmm_csr_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, POINTER(FrSpmmPlan), c_int64,
                                POINTER(FrTab), c_int, POINTER(FrTab), POINTER(FrTab), c_float, POINTER(FrTab),
-                               c_float, POINTER(FrTab), c_float, c_void_p, POINTER(FrRowList), c_void_p, c_int64,
-                               c_void_p]),
+                               c_float, POINTER(FrTab), c_float, c_void_p, POINTER(FrRowList), c_void_p, c_void_p,
+                               c_int64, c_void_p]),
     "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
+    "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p]),
+    "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                    c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_void_p, c_int64, c_void_p]),
+    "fr_bpr_fwd_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_int64,
+                                c_void_p, c_int64, c_void_p]),
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "fr_step_book": (c_int, [POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p, POINTER(c_void_p), c_int,

@@ -396,10 +396,11 @@ def _check_tab(name, lo, hi, split, n, d):
 
 def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None, Y2_hi=None, alpha=1.0,
             A1=None, A1_hi=None, beta1=0.0, A2=None, A2_hi=None, beta2=0.0, col_mask=None, rows=None,
-            region="spmm", nbytes=None):
+            a1_gate=None, region="spmm", nbytes=None):
     """fr_spmm_csr_ex: the fr_spmm_csr epilogue over split tables ([lo ; hi] at row ``split``), an
-    optional column mask (uint8 per X row, skipped where 0) and an optional row list
-    ([(ids, offset), ...]: only those rows of Y are computed and written)."""
+    optional column mask (uint8 per X row, skipped where 0), an optional row list
+    ([(ids, offset), ...]: only those rows of Y are computed and written) and an optional A1 row
+    gate (uint8 per output row: A1 read only where set, zero elsewhere)."""
     native.require_device(X)
     N, d = adj.shape[0], X.shape[1]
     _check_tab("X", X, X_hi, split, adj.shape[1], d)
@@ -407,6 +408,8 @@ def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
         _check_tab(name, lo, hi, split, N, d)
     if col_mask is not None and (col_mask.dtype != torch.uint8 or col_mask.numel() < adj.shape[1]):
         raise native.EngineError("spmm_ex: col_mask must be uint8 with one entry per X row")
+    if a1_gate is not None and (a1_gate.dtype != torch.uint8 or a1_gate.numel() < N):
+        raise native.EngineError("spmm_ex: a1_gate must be uint8 with one entry per output row")
     plan = adj.plan()
     ws = _ws_for(adj, d, X.device)
     rl = _rowlist(rows) if rows is not None else None
@@ -417,13 +420,19 @@ def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, ctypes.byref(plan), int(split),
             ctypes.byref(_tab(X, X_hi)), d, ctypes.byref(_tab(Y1, Y1_hi)), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha),
             ctypes.byref(_tab(A1, A1_hi)), _f(beta1), ctypes.byref(_tab(A2, A2_hi)), _f(beta2),
-            native.ptr(col_mask), ctypes.byref(rl) if rl is not None else None, ws.data_ptr(), ws.numel(),
-            native.stream_of(X)), "fr_spmm_csr_ex")
+            native.ptr(col_mask), ctypes.byref(rl) if rl is not None else None, native.ptr(a1_gate), ws.data_ptr(),
+            ws.numel(), native.stream_of(X)), "fr_spmm_csr_ex")
 
 
-def rows_mark(mask: torch.Tensor, rows, value: int) -> None:
-    native.check(native.lib().fr_rows_mark(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
-                                           native.stream_of(mask)), "fr_rows_mark")
+def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = None) -> None:
+    """mask[row] = value at the listed rows; with ``zero`` ([*, d] fp32), those rows of it set to 0."""
+    if zero is None:
+        native.check(native.lib().fr_rows_mark(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
+                                               native.stream_of(mask)), "fr_rows_mark")
+        return
+    native.check(native.lib().fr_rows_mark_zero(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
+                                                zero.data_ptr(), zero.stride(0), zero.shape[1],
+                                                native.stream_of(mask)), "fr_rows_mark_zero")
 
 
 def _adjacent_rows(lo, hi, rows):
@@ -465,16 +474,17 @@ def _prop_fwd_split(adj, lo, hi, split, L):
     return out
 
 
-def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None):
+def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None, gate=False):
     """d/dE of mean_k A^k E (A symmetric) for upstream G, written into [out_lo ; out_hi] split at
-    ``split``.  ``col_mask``: rows where G is known to be zero (first layer only)."""
+    ``split``.  ``col_mask``: rows where G is known to be zero (first layer only); ``gate`` (L = 1):
+    G is only valid at those rows (not zero-filled elsewhere), so its residual read is gated too."""
     inv = 1.0 / (L + 1)
     # a masked launch skips most gathers: not a full-gather (roofline) launch, timed under its own name
     reg = "spmm_masked" if col_mask is not None else "spmm"
     nb = 0 if col_mask is not None else None
     if L == 1:
         spmm_ex(adj, G, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv, A1=G, beta1=inv, col_mask=col_mask,
-                region=reg, nbytes=nb)
+                a1_gate=col_mask if gate else None, region=reg, nbytes=nb)
         return
     H = torch.empty_like(G)
     spmm_ex(adj, G, Y2=H, alpha=inv, A1=G, beta1=inv, col_mask=col_mask, region=reg, nbytes=nb)
@@ -534,11 +544,11 @@ class _GraphBpr(torch.autograd.Function):
         ws = native.workspace(lib.fr_bpr_workspace(B), dev)
         out = torch.empty(5, dtype=torch.float32, device=dev)
         items = ui_all[U:]
-        native.check(lib.fr_bpr_fwd(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
-                                    item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
-                                    _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(), native.stream_of(user_w)),
-                     "fr_bpr_fwd")
-        item_rows = torch.index_select(items, 0, pn)
+        item_rows = torch.empty(2 * B, 64, dtype=torch.float32, device=dev)  # [items[p] ; items[n]] (= items[pn])
+        native.check(lib.fr_bpr_fwd_rows(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
+                                         item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                         _f(gamma), out.data_ptr(), item_rows.data_ptr(), 64, ws.data_ptr(), ws.numel(),
+                                         native.stream_of(user_w)), "fr_bpr_fwd_rows")
         ctx.save_for_backward(user_w, item_w, ui_all, u, p, n, pn)
         ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
         return out[0], out[4:5], item_rows
@@ -548,6 +558,8 @@ class _GraphBpr(torch.autograd.Function):
         user_w, item_w, ui_all, u, p, n, pn = ctx.saved_tensors
         ri_adj, ui_adj, L_ri, L_ui, gamma, det, ws, U, I, NI = ctx.meta
         dev = user_w.device
+        if not det and L_ui == 1 and g_rows is not None and g_mf is not None and g_emb is not None:
+            return _GraphBpr._backward_fast(ctx, g_mf, g_emb, g_rows)
         g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
         g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
         gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
@@ -588,6 +600,49 @@ class _GraphBpr(torch.autograd.Function):
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_bpr_bwd(*common, None, None, d_user.data_ptr(), d_item.data_ptr(), det, ws.data_ptr(),
                                         ws.numel(), s), "fr_bpr_bwd")
+        return (d_user, d_item, d_ingre) + (None,) * 10
+
+    @staticmethod
+    def _backward_fast(ctx, g_mf, g_emb, g_rows):
+        """Float-atomic path for one UI layer, 7 launches: mark the batch rows in the column mask and
+        zero them in the persistent UI upstream gradient (no full fill: its other rows are never
+        read, the masked backward gates its residual read by the same mask); the BPR scatter (+ the
+        KD rows' gradient) with g_mf read on the device; the masked UI backward (+ split-row fixup)
+        into d user_embedding and the item block of the RI upstream gradient; the RI backward into
+        d item_embedding and d ingre_embedding[:-1]; fr_graph_bpr_finish: unmark, the ego rows'
+        EmbLoss gradient, the padding row's zero."""
+        user_w, item_w, ui_all, u, p, n, pn = ctx.saved_tensors
+        ri_adj, ui_adj, L_ri, L_ui, gamma, det, ws, U, I, NI = ctx.meta
+        dev = user_w.device
+        B = int(u.numel())
+        lib = native.lib()
+        s = native.stream_of(user_w)
+        items = ui_all[U:]
+        g_mf = g_mf.float().contiguous()
+        g_emb = g_emb.float().contiguous()
+        g_rows = g_rows.contiguous()
+        dUI = _persistent(ui_adj, ("g_ui", str(dev)), lambda: torch.empty(U + I, 64, device=dev))
+        mask = _persistent(ui_adj, ("mask", str(dev)), lambda: torch.zeros(U + I, dtype=torch.uint8, device=dev))
+        rows = [(u, 0), (p, U), (n, U)]
+        rows_mark(mask, rows, 1, zero=dUI)
+        with profiling.region("bpr_bwd", 0):
+            native.check(lib.fr_bpr_bwd_ex(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
+                                           item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                           _f(gamma), _f(1.0), _f(0.0), g_mf.data_ptr(), dUI.data_ptr(),
+                                           dUI[U:].data_ptr(), None, None, g_rows.data_ptr(), g_rows.stride(0),
+                                           ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd_ex")
+        d_user = torch.empty_like(user_w)
+        G_ri = _persistent(ri_adj, ("g_ri", str(dev)), lambda: torch.zeros(I + NI, 64, device=dev))
+        _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
+        d_item = torch.empty_like(item_w)
+        d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
+        _prop_bwd_split(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
+        with profiling.region("bpr_bwd", 0):
+            native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
+                                                 u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),
+                                                 g_emb.data_ptr(), d_user.data_ptr(), d_item.data_ptr(),
+                                                 d_ingre[NI:].data_ptr(), 64, ws.data_ptr(), ws.numel(), s),
+                         "fr_graph_bpr_finish")
         return (d_user, d_item, d_ingre) + (None,) * 10
 
 

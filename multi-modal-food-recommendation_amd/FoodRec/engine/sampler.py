@@ -243,7 +243,7 @@ class BatchFeatures:
         out = {"pn_i_id": torch.empty(2 * B, dtype=torch.int64, device=dev),
                "pn_ingre_code": torch.empty(2 * B, L, dtype=torch.int64, device=dev),
                "pn_ingre_num": torch.empty(2 * B, dtype=torch.int64, device=dev),
-               "pn_pad_mask": torch.empty(2 * B, L, dtype=torch.bool, device=dev)}
+               "pn_pad_kpm": torch.empty(2 * B, L, dtype=torch.float32, device=dev)}
         if self.health is not None:
             out["pn_hl_mh"] = torch.empty(2 * B, self.health.shape[1], dtype=self.health.dtype, device=dev)
         return out
@@ -264,7 +264,7 @@ class BatchFeatures:
             native.ptr(u), p.data_ptr(), n.data_ptr(), self.ingre_code.data_ptr(), self.ingre_code.shape[1],
             self.ingre_num.data_ptr(), native.ptr(h), H, self.ingre_code.shape[0], self.pad_id,
             out["pn_i_id"].data_ptr(), out["pn_ingre_code"].data_ptr(), out["pn_ingre_num"].data_ptr(),
-            native.ptr(out.get("pn_hl_mh")), out["pn_pad_mask"].data_ptr(), native.stream_of(p)), "fr_feed_batch")
+            native.ptr(out.get("pn_hl_mh")), out["pn_pad_kpm"].data_ptr(), native.stream_of(p)), "fr_feed_batch")
 
     def launch_feed(self, feed, u, p, n, out):
         self._launch(feed.perm, feed.users, feed.items, feed.negs, feed.cursor, feed.B, u, p, n, out)
@@ -294,8 +294,9 @@ class LazyBatch(dict):
     _LAZY = ("pos_ingre_code", "pos_ingre_num", "pos_hl_mh", "pos_img", "pos_cl",
              "neg_ingre_code", "neg_ingre_num", "neg_hl_mh", "neg_img", "neg_cl",
              # engine extras: [pos; neg] stacked, gathered together in one launch (fr_feed_batch), and
-             # the ingredient padding mask of the stacked codes
-             "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_mask")
+             # the ingredient key-padding mask of the stacked codes in the additive float form
+             # (-inf at padding, 0 elsewhere) the Transformer layer consumes as it is
+             "pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_kpm")
 
     def __init__(self, feats: BatchFeatures, u, p, n):
         super().__init__(u_id=u, pos_i_id=p, neg_i_id=n)
@@ -312,8 +313,10 @@ class LazyBatch(dict):
             return got[key]
         if key == "pn_i_id":
             return torch.cat([self["pos_i_id"], self["neg_i_id"]])
-        if key == "pn_pad_mask":
-            return self["pn_ingre_code"] == self._f.pad_id
+        if key == "pn_pad_kpm":
+            codes = self["pn_ingre_code"]
+            return torch.zeros(codes.shape, dtype=torch.float32, device=codes.device).masked_fill_(
+                codes == self._f.pad_id, float("-inf"))
         side, what = key.split("_", 1)
         idx = {"pos": self["pos_i_id"], "neg": self["neg_i_id"]}.get(side)
         if idx is None:

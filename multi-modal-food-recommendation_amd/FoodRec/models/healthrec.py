@@ -171,7 +171,7 @@ class HealthRec(GeneralRecommender):
         # norms of ingre_embedding(pos / neg ingredients) with padding_idx (:270-279): the same
         # gather, so one gather and one combined deterministic scatter (fr_embedding_bwd)
         ingr_emb, ing_norms = ops.embedding_norms(ingredients, ingr_all, self.n_ingredients, B)
-        mask = batch_data.get("pn_pad_mask")  # gathered with the codes (engine batch), else computed
+        mask = batch_data.get("pn_pad_kpm")  # additive key mask gathered with the codes (engine batch), else computed
         if mask is None:
             mask = ingredients == self.n_ingredients
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)

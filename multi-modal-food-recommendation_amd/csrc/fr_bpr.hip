@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void bpr_scores_kernel(
     const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
     const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
     const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
-    int64_t B, int d4, BprWS ws) {
+    int64_t B, int d4, BprWS ws, float* __restrict__ rows_out, int64_t ldr) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
   for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; b < B;
@@ -60,9 +60,13 @@ __global__ __launch_bounds__(256) void bpr_scores_kernel(
     const int64_t u = uu[b], p = pp[b], n = nn[b];
     float sp = 0.f, sn = 0.f, a = 0.f, c = 0.f, e = 0.f;
     for (int q = q0; q < d4; q += LPR) {
-      const float4 xu = ld4(U, u, ldu, q);
-      sp += f4_dot(xu, ld4(I, p, ldi, q));
-      sn += f4_dot(xu, ld4(I, n, ldi, q));
+      const float4 xu = ld4(U, u, ldu, q), xp = ld4(I, p, ldi, q), xn = ld4(I, n, ldi, q);
+      sp += f4_dot(xu, xp);
+      sn += f4_dot(xu, xn);
+      if (rows_out) {  // [I[pos]; I[neg]] for another consumer of those rows
+        reinterpret_cast<float4*>(rows_out + b * ldr)[q] = xp;
+        reinterpret_cast<float4*>(rows_out + (B + b) * ldr)[q] = xn;
+      }
       if (Ue) {
         const float4 eu = ld4(Ue, u, ldue, q), ep = ld4(Ie, p, ldie, q), en = ld4(Ie, n, ldie, q);
         a += f4_dot(eu, eu);
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
     const float* __restrict__ extra, int64_t ldx) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
-  if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
+  if (gscale) { gmf *= gscale[0]; if (dUe || dIe) greg *= gscale[1]; }
   const float inv_b = 1.f / (float)B;
   const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
   const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
@@ -182,6 +186,39 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
   }
 }
 
+// The tail of HealthRec's fused propagation backward (fr_graph_bpr_finish): clear the batch rows'
+// column-mask bytes (users at u, items at U + pos / U + neg), add the EmbLoss gradient of the ego
+// rows (the same per-row terms and float atomics as bpr_bwd_atomic_kernel's dUe / dIe branch, with
+// g_reg scaled by d_greg[0]) and zero `zero_n` floats at `zero` (the padding row).
+__global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
+    uint8_t* __restrict__ mask, int64_t U, const float* __restrict__ Ue, int64_t ldue,
+    const float* __restrict__ Ie, int64_t ldie, const int64_t* __restrict__ uu, const int64_t* __restrict__ pp,
+    const int64_t* __restrict__ nn, int64_t B, int d4, float greg, const float* greg_dev, float* dUe,
+    int64_t lddue, float* dIe, int64_t lddie, BprWS ws, float* __restrict__ zero, int zero_n) {
+  constexpr int GPB = 256 / LPR;
+  const int q0 = threadIdx.x % LPR;
+  if (greg_dev) greg *= greg_dev[0];
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k < zero_n; k += 256) zero[k] = 0.f;
+  for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; b < B; b += (int64_t)gridDim.x * GPB) {
+    const int64_t u = uu[b], p = pp[b], n = nn[b];
+    if (mask && q0 == 0) {
+      mask[u] = 0;
+      mask[U + p] = 0;
+      mask[U + n] = 0;
+    }
+    for (int q = q0; q < d4; q += LPR) {
+      atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
+      atomic_row_add(dIe, p, lddie, q, f4_scale(rp, ld4(Ie, p, ldie, q)));
+      atomic_row_add(dIe, n, lddie, q, f4_scale(rn, ld4(Ie, n, ldie, q)));
+    }
+  }
+}
+
 // Deterministic scatter.  Slots: [0,B) user occurrences, [B,2B) pos, [2B,3B) neg.  The first
 // slot of each (table,row) owns it and sums all its contributions in reference order.
 __global__ __launch_bounds__(256) void bpr_bwd_det_kernel(
@@ -192,7 +229,7 @@ __global__ __launch_bounds__(256) void bpr_bwd_det_kernel(
     float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
-  if (gscale) { gmf *= gscale[0]; greg *= gscale[1]; }
+  if (gscale) { gmf *= gscale[0]; if (dUe || dIe) greg *= gscale[1]; }
   const float inv_b = 1.f / (float)B;
   const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
   const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
@@ -415,15 +452,25 @@ extern "C" int fr_bpr_fwd(const float* d_U, int64_t ldu, const float* d_I, int64
                           const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
                           float gamma, float* d_out, void* d_workspace, int64_t workspace_bytes,
                           void* stream) {
+  return fr_bpr_fwd_rows(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, gamma, d_out, nullptr, 0,
+                         d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_bpr_fwd_rows(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                               const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                               const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                               float gamma, float* d_out, float* d_rows, int64_t ld_rows, void* d_workspace,
+                               int64_t workspace_bytes, void* stream) {
   int rc = bpr_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
                      workspace_bytes);
   if (rc) return rc;
   FR_REQUIRE(d_out, "out null");
+  FR_REQUIRE(!d_rows || (fr::aligned16(d_rows) && ld_rows >= d && ld_rows % 4 == 0), "rows output [2B, d] unaligned");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   BprWS w = bpr_ws(d_workspace, B);
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
   hipLaunchKernelGGL(bpr_scores_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue, ldue,
-                     d_Ie, ldie, d_u, d_p, d_n, B, d / 4, w);
+                     d_Ie, ldie, d_u, d_p, d_n, B, d / 4, w, d_rows, ld_rows);
   FR_LAUNCH_CHECK();
   hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w, d_out);
   FR_LAUNCH_CHECK();
@@ -478,6 +525,26 @@ extern "C" int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, in
              "extra item-row gradient [2B, d] (16-B aligned) and dI required");
   return bpr_bwd_impl(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, gamma, g_mf, g_reg, d_gscale,
                       d_dU, d_dI, d_dUe, d_dIe, 0, d_extra_i, ld_extra, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t ldue, const float* d_Ie,
+                                   int64_t ldie, const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B,
+                                   int d, float g_reg, const float* d_greg, float* d_dUe, float* d_dIe,
+                                   float* d_zero, int zero_n, void* d_workspace, int64_t workspace_bytes,
+                                   void* stream) {
+  FR_REQUIRE(B >= 1 && d >= 4 && d % 4 == 0 && U >= 0 && zero_n >= 0, "bad sizes");
+  FR_REQUIRE(d_Ue && d_Ie && d_u && d_p && d_n && d_dUe && d_dIe && (zero_n == 0 || d_zero), "null argument");
+  FR_REQUIRE(fr::aligned16(d_Ue) && fr::aligned16(d_Ie) && fr::aligned16(d_dUe) && fr::aligned16(d_dIe) &&
+                 ldue % 4 == 0 && ldie % 4 == 0 && ldue >= d && ldie >= d,
+             "tables must be 16-B aligned with ld % 4 == 0");
+  FR_REQUIRE(d_workspace && workspace_bytes >= bpr_ws_bytes(B) && fr::aligned16(d_workspace), "workspace too small");
+  BprWS w = bpr_ws(d_workspace, B);
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
+  hipLaunchKernelGGL(graph_bpr_finish_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_mask,
+                     U, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, g_reg, d_greg, d_dUe, ldue, d_dIe, ldie, w,
+                     d_zero, zero_n);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
 }
 
 // ---- bf16 entry points -----------------------------------------------------------------------

@@ -5,7 +5,7 @@
 // as the engine runs them on the device: the DeviceFeed gathers of (u, pos, neg) from the epoch's
 // staged permutation and negatives (4 index_select + 1 add), then the LazyBatch gathers of the
 // item features of [pos; neg] (torch.cat + ingredient codes / counts / health multi-hot gathers)
-// and HealthRec's key-padding mask (codes == pad).  Ten small launches -> one.
+// and HealthRec's key-padding mask (codes == pad) as the additive float mask the encoder takes.  Ten small launches -> one.
 //
 // Mapping: one thread per (batch row j in [0, 2B), column c in [0, W)), W = max(L, H, 1); every
 // thread resolves its row's item id itself (two cached loads), so there is no cross-block
@@ -39,7 +39,7 @@ struct FeedArgs {
   int64_t* out_codes;     // [2B, L]
   int64_t* out_nums;      // [2B]
   float* out_health;      // [2B, H] or null
-  bool* out_mask;         // [2B, L] or null
+  float* out_kpm;         // [2B, L] additive key mask (-inf at padding, 0 elsewhere) or null
 };
 
 __global__ __launch_bounds__(256) void feed_batch_kernel(FeedArgs a, int64_t B) {
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void feed_batch_kernel(FeedArgs a, int64_t B) 
     if (c < a.L) {
       const int64_t code = a.codes[item * a.L + c];
       a.out_codes[j * a.L + c] = code;
-      if (a.out_mask) a.out_mask[j * a.L + c] = code == a.pad;
+      if (a.out_kpm) a.out_kpm[j * a.L + c] = code == a.pad ? -INFINITY : 0.f;
     }
     if (a.health && c < a.H) a.out_health[j * a.H + c] = a.health[item * a.H + c];
   }
@@ -87,7 +87,7 @@ extern "C" int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, cons
                              const int64_t* d_negs, const int64_t* d_cursor, int64_t B, int64_t* d_u, int64_t* d_p,
                              int64_t* d_n, const int64_t* d_codes, int L, const int64_t* d_nums, const float* d_health,
                              int H, int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes,
-                             int64_t* d_out_nums, float* d_out_health, bool* d_out_mask, void* stream) {
+                             int64_t* d_out_nums, float* d_out_health, float* d_out_kpm, void* stream) {
   FR_REQUIRE(B >= 1 && L >= 1 && L <= 1024 && H >= 0 && H <= 1024 && n_items >= 1, "bad sizes");
   FR_REQUIRE(d_p && d_n && d_codes && d_nums && d_pn && d_out_codes && d_out_nums, "null argument");
   FR_REQUIRE(!d_perm || (d_users && d_items && d_negs && d_cursor && d_u), "feed mode needs perm/users/items/negs/"
@@ -95,7 +95,7 @@ extern "C" int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, cons
   FR_REQUIRE((d_health == nullptr) == (d_out_health == nullptr) && (H == 0) == (d_health == nullptr),
              "health table and output go together (H > 0)");
   FeedArgs a{d_perm, d_users, d_items, d_negs, d_cursor, d_u, d_p, d_n, d_codes, d_nums, d_health, n_items, L, H,
-             L > H ? L : (H > 0 ? H : 1), pad, d_pn, d_out_codes, d_out_nums, d_out_health, d_out_mask};
+             L > H ? L : (H > 0 ? H : 1), pad, d_pn, d_out_codes, d_out_nums, d_out_health, d_out_kpm};
   const int64_t total = 2 * B * a.W;
   const int64_t blocks = std::min<int64_t>(fr::ceil_div(total, (int64_t)256), (int64_t)fr::kNumCU * 8);
   hipLaunchKernelGGL(feed_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),

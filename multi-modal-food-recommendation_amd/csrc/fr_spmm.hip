@@ -58,6 +58,7 @@ struct Epi {
   Tab A1; float beta1;
   Tab A2; float beta2;
   int64_t split;
+  const uint8_t* a1_gate;  // A1 row r is read only where a1_gate[r] != 0 (else it counts as zero)
 };
 
 // write one row's result (float4 slot q of row r) through the fused epilogue
@@ -65,7 +66,8 @@ __device__ __forceinline__ void epilogue(const Epi& ep, int64_t r, int q, float4
   if (ep.Y1.lo) reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y1, r, ep.split)))[q] = acc;
   if (ep.Y2.lo) {
     float4 o = f4_scale(ep.alpha, acc);
-    if (ep.A1.lo) o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q], o);
+    if (ep.A1.lo && (ep.a1_gate == nullptr || ep.a1_gate[r] != 0))
+      o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q], o);
     if (ep.A2.lo) o = f4_fma(ep.beta2, reinterpret_cast<const float4*>(tab_row(ep.A2, r, ep.split))[q], o);
     reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
   }
@@ -258,13 +260,19 @@ __global__ __launch_bounds__(kRowThreads) void spmm_rows_kernel(
   }
 }
 
+// mask[row] = value at the listed rows; with Z, also Z[row][0..d) = 0 (16 lanes x float4 per row)
 __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ mask, RowList rl, int64_t total,
-                                                        uint8_t value) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    int64_t idx = i;
+                                                        uint8_t value, float4* __restrict__ Z, int64_t ldz4, int d4) {
+  const int per = Z ? 16 : 1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total * per; i += (int64_t)gridDim.x * 256) {
+    int64_t idx = i / per;
+    const int q = (int)(i % per);
     int seg = 0;
     while (idx >= rl.n[seg]) idx -= rl.n[seg++];
-    mask[rl.ids[seg][idx] + rl.off[seg]] = value;
+    const int64_t row = rl.ids[seg][idx] + rl.off[seg];
+    if (q == 0) mask[row] = value;
+    if (Z)
+      for (int c = q; c < d4; c += 16) Z[row * ldz4 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -373,8 +381,8 @@ bool tab_touches(const fr_tab* t, const void* p) {
 int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
               const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
               const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
-              const uint8_t* col_mask, const fr_rowlist* rows, void* d_workspace, int64_t workspace_bytes,
-              void* stream, const char* who) {
+              const uint8_t* col_mask, const fr_rowlist* rows, const uint8_t* a1_gate, void* d_workspace,
+              int64_t workspace_bytes, void* stream, const char* who) {
   FR_REQUIRE(plan != nullptr, "plan is null");
   FR_REQUIRE(d > 0 && d % 4 == 0 && d <= 1024, "d must be a positive multiple of 4, <= 1024");
   FR_REQUIRE(n_rows >= 0, "n_rows < 0");
@@ -394,7 +402,7 @@ int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
              (d_workspace && workspace_bytes >= need && fr::aligned16(d_workspace)),
              "workspace too small (need " + std::to_string(need) + " bytes)");
   Epi ep{host_tab(Y1), host_tab(Y2), alpha, host_tab(A1), beta1, host_tab(A2), beta2,
-         split};
+         split, a1_gate};
   XSrc xs{reinterpret_cast<const float4*>(X->lo), X->ld_lo >> 2, reinterpret_cast<const float4*>(X->hi),
           X->hi ? (X->ld_hi >> 2) : 0, X->hi ? split : INT64_MAX, col_mask};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -451,20 +459,27 @@ extern "C" int fr_spmm_csr(const int64_t* d_rowptr, const int32_t* d_col, const 
   const fr_tab X{d_X, ldx, nullptr, 0}, Y1{d_Y1, ldy1, nullptr, 0}, Y2{d_Y2, ldy2, nullptr, 0};
   const fr_tab A1{d_A1, lda1, nullptr, 0}, A2{d_A2, lda2, nullptr, 0};
   return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, 0, &X, d, &Y1, &Y2, alpha, &A1, beta1, &A2, beta2,
-                   nullptr, nullptr, d_workspace, workspace_bytes, stream, "fr_spmm_csr");
+                   nullptr, nullptr, nullptr, d_workspace, workspace_bytes, stream, "fr_spmm_csr");
 }
 
 extern "C" int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
                               const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
                               const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
-                              float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, void* d_workspace,
-                              int64_t workspace_bytes, void* stream) {
+                              float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows,
+                              const uint8_t* d_a1_gate, void* d_workspace, int64_t workspace_bytes, void* stream) {
   return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, split, X, d, Y1, Y2, alpha, A1, beta1, A2, beta2,
-                   d_col_mask, rows, d_workspace, workspace_bytes, stream, "fr_spmm_csr_ex");
+                   d_col_mask, rows, d_a1_gate, d_workspace, workspace_bytes, stream, "fr_spmm_csr_ex");
 }
 
 extern "C" int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream) {
+  return fr_rows_mark_zero(d_mask, rows, value, nullptr, 0, 0, stream);
+}
+
+extern "C" int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
+                                 void* stream) {
   FR_REQUIRE(d_mask != nullptr && rows != nullptr, "null argument");
+  FR_REQUIRE(!d_Z || (d > 0 && d % 4 == 0 && ldz >= d && ldz % 4 == 0 && fr::aligned16(d_Z)),
+             "Z must be 16-B aligned with d % 4 == 0 and ld >= d");
   RowList rl{};
   int64_t total = 0;
   for (int k = 0; k < 3; ++k) {
@@ -475,9 +490,10 @@ extern "C" int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t val
     total += rows->n[k];
   }
   if (total == 0) return FR_OK;
-  const int64_t blocks = std::min<int64_t>(fr::ceil_div(total, (int64_t)256), (int64_t)fr::kNumCU * 4);
+  const int64_t work = total * (d_Z ? 16 : 1);
+  const int64_t blocks = std::min<int64_t>(fr::ceil_div(work, (int64_t)256), (int64_t)fr::kNumCU * 4);
   hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     d_mask, rl, total, value);
+                     d_mask, rl, total, value, reinterpret_cast<float4*>(d_Z), ldz / 4, d / 4);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -501,9 +501,10 @@ def test_feed_batch_one_launch_matches_gathers(cuda):
             assert torch.equal(pre["pn_ingre_code"], feats.ingre_code[pn])
             assert torch.equal(pre["pn_ingre_num"], feats.ingre_num[pn])
             assert torch.equal(pre["pn_hl_mh"], feats.health[pn])
-            assert torch.equal(pre["pn_pad_mask"], feats.ingre_code[pn] == data.num_ingredients)
+            assert torch.equal(pre["pn_pad_kpm"] == float("-inf"), feats.ingre_code[pn] == data.num_ingredients)
+            assert torch.all((pre["pn_pad_kpm"] == 0) | (pre["pn_pad_kpm"] == float("-inf")))
             lb = feats.batch(out[0].clone(), out[1].clone(), out[2].clone())  # plain mode (lazy keys)
-            for k in ("pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_mask"):
+            for k in ("pn_i_id", "pn_ingre_code", "pn_ingre_num", "pn_hl_mh", "pn_pad_kpm"):
                 assert torch.equal(lb[k], pre[k]), k
         got.append([x.cpu().numpy().copy() for x in (u, p, n)])
     for k, key in enumerate("upn"):

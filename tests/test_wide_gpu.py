@@ -88,6 +88,13 @@ def _check_init(g, model):
 
 
 def _check_grads(g, model, opt):
+    """Step-0 gradients against the reference run in fp32 (grad0/) and in float64 (grad0_f64/).
+    At this batch one hidden unit of HealthRec's health MLP (health_mlp.0, row 56) sits on its ReLU
+    boundary for one sample: fp32 rounding decides the side, and the reference's own fp32 and
+    float64 runs land on opposite sides (their health_mlp.0.weight gradients differ by 1.1e-3 in
+    that row only, and the flip propagates upstream into the encoder).  A correct fp32 engine lands
+    on one side or the other, so each gradient must be within (5e-4 max, 1e-4 norm) of ONE of the
+    two references, and within (2e-3, 1e-3) of the fp32 one in every case."""
     opt.materialize_row_grads()
     checked = 0
     for k, p in model.named_parameters():
@@ -95,11 +102,15 @@ def _check_grads(g, model, opt):
             continue
         assert p.grad is not None, k
         got = _rows(g, k, p.grad).cpu().numpy().astype(np.float64)
-        for key, tol_max, tol_norm in (("grad0_f64/", 5e-4, 1e-4), ("grad0/", 2e-3, 1e-3)):
+        close = []
+        for key in ("grad0_f64/", "grad0/"):
             ref = g[key + k].astype(np.float64)
-            err = np.abs(got - ref).max()
-            assert err <= tol_max * np.abs(ref).max() + 1e-8, (key, k, err, np.abs(ref).max())
-            assert np.linalg.norm(got - ref) <= tol_norm * np.linalg.norm(ref) + 1e-8, (key, k)
+            err, nerr = np.abs(got - ref).max(), np.linalg.norm(got - ref)
+            close.append(err <= 5e-4 * np.abs(ref).max() + 1e-8 and nerr <= 1e-4 * np.linalg.norm(ref) + 1e-8)
+            if key == "grad0/":
+                assert err <= 2e-3 * np.abs(ref).max() + 1e-8, (key, k, err, np.abs(ref).max())
+                assert nerr <= 1e-3 * np.linalg.norm(ref) + 1e-8, (key, k)
+        assert any(close), (k, "not within (5e-4, 1e-4) of the fp32 or the float64 reference")
         checked += 1
     assert checked >= 3
 
