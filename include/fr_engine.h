@@ -503,6 +503,24 @@ int fr_rows_matmul(const float* d_s, int64_t lds, int64_t n, const float* d_w, i
 int fr_linear_wgrad_gather(const float* d_dy, int64_t ldy, const int64_t* d_ids, const float* d_x, int64_t ldx,
                            int64_t M, int N, int K, float* d_dw, int64_t ldw, float* d_db, void* d_workspace,
                            int64_t workspace_bytes, void* stream);
+/* The same three for several tables (<= 4) at the same ids in one launch each (blockIdx.z = table):
+ * HealthRec's image and text projections share the batch's item ids.
+ *   fr_gather_linear_fwd_multi: table t writes Y[i, 64 t .. 64 t + 64) (ldy >= 64 n_tab); d_b may be NULL
+ *     (or hold NULL entries);
+ *   fr_rows_matmul_multi: out_t[i, 0:K_t] = S[i, 64 t .. 64 t + 64) W_t (lds >= 64 n_tab);
+ *   fr_linear_wgrad_gather_multi: dW_t = dY_t^T X_t[ids], db_t = colsum dY_t, dY_t = columns
+ *     [N t, N t + N) of dY; workspace fr_linear_wgrad_gather_multi_workspace(M, N, n_tab, K).
+ * Host arrays of per-table pointers / sizes; results bit-identical to the per-table calls. */
+int fr_gather_linear_fwd_multi(const int64_t* d_ids, int64_t n, int n_tab, const float* const* d_x, const int64_t* ldx,
+                               const int* K, const float* const* d_w, const float* const* d_b, float* d_y, int64_t ldy,
+                               void* stream);
+int fr_rows_matmul_multi(const float* d_s, int64_t lds, int64_t n, int n_tab, const float* const* d_w, const int* K,
+                         float* const* d_out, const int64_t* ldo, void* stream);
+int64_t fr_linear_wgrad_gather_multi_workspace(int64_t M, int N, int n_tab, const int* K);
+int fr_linear_wgrad_gather_multi(const float* d_dy, int64_t ldy, const int64_t* d_ids, int64_t M, int N, int n_tab,
+                                 const float* const* d_x, const int64_t* ldx, const int* K, float* const* d_dw,
+                                 const int64_t* ldw, float* const* d_db, void* d_workspace, int64_t workspace_bytes,
+                                 void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Ingredient gather + EmbLoss norms of its two halves (models/cikm_model.py:230, 270-279).

@@ -186,6 +186,15 @@ _SIGS = {
     "fr_gather_linear_fwd": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                      c_int64, c_void_p]),
     "fr_rows_matmul": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int, c_void_p, c_int64, c_void_p]),
+    "fr_gather_linear_fwd_multi": (c_int, [c_void_p, c_int64, c_int, POINTER(c_void_p), POINTER(c_int64),
+                                           POINTER(c_int), POINTER(c_void_p), POINTER(c_void_p), c_void_p, c_int64,
+                                           c_void_p]),
+    "fr_rows_matmul_multi": (c_int, [c_void_p, c_int64, c_int64, c_int, POINTER(c_void_p), POINTER(c_int),
+                                     POINTER(c_void_p), POINTER(c_int64), c_void_p]),
+    "fr_linear_wgrad_gather_multi_workspace": (c_int64, [c_int64, c_int, c_int, POINTER(c_int)]),
+    "fr_linear_wgrad_gather_multi": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, POINTER(c_void_p),
+                                             POINTER(c_int64), POINTER(c_int), POINTER(c_void_p), POINTER(c_int64),
+                                             POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
     "fr_linear_wgrad_gather": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int,
                                        c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_gather_norms_partials": (c_int64, [c_int64]),

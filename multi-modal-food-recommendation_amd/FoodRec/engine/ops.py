@@ -1159,14 +1159,16 @@ def factored_rows(ids, G, width: int, R: int, pad, Ws):
         native.check(lib.fr_embedding_rowgrad(ids.data_ptr(), n, G.data_ptr(), G.stride(0), width, R,
                                               -1 if pad is None else int(pad), rmap.data_ptr(), S.data_ptr(),
                                               ws.data_ptr(), ws.numel(), native.stream_of(G)), "fr_embedding_rowgrad")
-    rows = []
-    for k, W in enumerate(Ws):
-        K = W.shape[1]
-        crow = torch.empty(max(n, 1), K, dtype=torch.float32, device=dev)
-        with profiling.region("rows_matmul", 4 * (n * 64 + 64 * K + n * K)):
-            native.check(lib.fr_rows_matmul(S[:, 64 * k:].data_ptr(), width, n, W.data_ptr(), K, crow.data_ptr(), K,
-                                            native.stream_of(G)), "fr_rows_matmul")
-        rows.append(crow)
+    rows = [torch.empty(max(n, 1), W.shape[1], dtype=torch.float32, device=dev) for W in Ws]
+    if n == 0:
+        return rmap, rows
+    T = len(Ws)
+    nb = sum(4 * (n * 64 + 64 * W.shape[1] + n * W.shape[1]) for W in Ws)
+    with profiling.region("rows_matmul", nb):  # every table in one launch (blockIdx.z = table)
+        native.check(lib.fr_rows_matmul_multi(
+            S.data_ptr(), width, n, T, (ctypes.c_void_p * T)(*[W.data_ptr() for W in Ws]),
+            (ctypes.c_int * T)(*[W.shape[1] for W in Ws]), (ctypes.c_void_p * T)(*[c.data_ptr() for c in rows]),
+            (ctypes.c_int64 * T)(*[c.shape[1] for c in rows]), native.stream_of(G)), "fr_rows_matmul_multi")
     return rmap, rows
 
 
@@ -1189,14 +1191,16 @@ class _ModalProjection(torch.autograd.Function):
         dev = ids.device
         lib = native.lib()
         out = torch.empty(n, T, 64, dtype=torch.float32, device=dev)
-        for t in range(T):
-            X, W, b = flat[3 * t], flat[3 * t + 1], flat[3 * t + 2]
+        Xs, Ws, bs = flat[0::3], flat[1::3], flat[2::3]
+        for X in Xs:
             _catch_up(exchange, X, ids)
-            K = W.shape[1]
-            with profiling.region("modal_projection", projection_bytes(n, K, False)):
-                native.check(lib.fr_gather_linear_fwd(ids.data_ptr(), n, X.data_ptr(), X.stride(0), K, W.data_ptr(),
-                                                      native.ptr(b), out[:, t].data_ptr(), T * 64,
-                                                      native.stream_of(X)), "fr_gather_linear_fwd")
+        nb = sum(projection_bytes(n, W.shape[1], False) for W in Ws)
+        with profiling.region("modal_projection", nb):  # every modality in one launch (blockIdx.z = table)
+            native.check(lib.fr_gather_linear_fwd_multi(
+                ids.data_ptr(), n, T, (ctypes.c_void_p * T)(*[X.data_ptr() for X in Xs]),
+                (ctypes.c_int64 * T)(*[X.stride(0) for X in Xs]), (ctypes.c_int * T)(*[W.shape[1] for W in Ws]),
+                (ctypes.c_void_p * T)(*[W.data_ptr() for W in Ws]), (ctypes.c_void_p * T)(*[native.ptr(b) for b in bs]),
+                out.data_ptr(), T * 64, native.stream_of(ids)), "fr_gather_linear_fwd_multi")
         ctx.save_for_backward(ids, *flat)
         ctx.exchange, ctx.T = exchange, T
         return out
@@ -1221,18 +1225,22 @@ class _ModalProjection(torch.autograd.Function):
                 for t in range(T):
                     rmap, (c,) = factored_rows(ids, G2[:, 64 * t:], 64, flat[3 * t].shape[0], None, [flat[3 * t + 1]])
                     dense.append(rows_to_dense(rmap, c))
+        Xs, Ws, bs = flat[0::3], flat[1::3], flat[2::3]
+        dWs = [torch.empty_like(W) for W in Ws]
+        dbs = [torch.empty_like(b) if b is not None else None for b in bs]
+        Ks = (ctypes.c_int * T)(*[W.shape[1] for W in Ws])
+        ws = native.workspace(lib.fr_linear_wgrad_gather_multi_workspace(n, 64, T, Ks), g.device)
+        nb = sum(projection_bytes(n, W.shape[1], True) for W in Ws)
+        with profiling.region("modal_projection", nb):  # dW / db of every modality: one slab + one reduce launch
+            native.check(lib.fr_linear_wgrad_gather_multi(
+                G2.data_ptr(), G2.stride(0), ids.data_ptr(), n, 64, T, (ctypes.c_void_p * T)(*[X.data_ptr() for X in Xs]),
+                (ctypes.c_int64 * T)(*[X.stride(0) for X in Xs]), Ks, (ctypes.c_void_p * T)(*[d.data_ptr() for d in dWs]),
+                (ctypes.c_int64 * T)(*[d.stride(0) for d in dWs]), (ctypes.c_void_p * T)(*[native.ptr(d) for d in dbs]),
+                ws.data_ptr(), ws.numel(), native.stream_of(g)), "fr_linear_wgrad_gather_multi")
         for t in range(T):
             X, W, b = flat[3 * t], flat[3 * t + 1], flat[3 * t + 2]
-            K = W.shape[1]
-            dW = torch.empty_like(W)
-            db = torch.empty_like(b) if b is not None else None
-            ws = native.workspace(lib.fr_linear_wgrad_workspace(n, 64, K), g.device)
+            dW, db = dWs[t], dbs[t]
             dy = G2[:, 64 * t:64 * (t + 1)]
-            with profiling.region("modal_projection", projection_bytes(n, K, True)):
-                native.check(lib.fr_linear_wgrad_gather(dy.data_ptr(), G2.stride(0), ids.data_ptr(), X.data_ptr(),
-                                                        X.stride(0), n, 64, K, dW.data_ptr(), dW.stride(0),
-                                                        native.ptr(db), ws.data_ptr(), ws.numel(),
-                                                        native.stream_of(g)), "fr_linear_wgrad_gather")
             dX = None
             if ctx.needs_input_grad[2 + 3 * t]:
                 if ctx.exchange is not None:

@@ -58,13 +58,6 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = __fadd_rn(p, __fdiv_rn(__fmul_rn(h.neg_step, m), denom));
 }
 
-// device-scalar mode: bump each tensor's step counter once per optimiser step
-__global__ void adam_step_inc_kernel(AdamArgs a, const int32_t* skip) {
-  if (skip && *skip) return;
-  const int t = threadIdx.x;
-  if (t < a.n && a.step[t]) a.step[t][0] += 1;
-}
-
 typedef float fv4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float4 nt_load4(const float* p) {
@@ -87,6 +80,30 @@ __device__ __forceinline__ void adam4(float* P, const float* G, float* M, float*
   nt_store4(V + i, v);
 }
 
+// Device-scalar mode bumps the step counters in the launch itself: every block derives its
+// scalars from step + 1, and the block that arrives last (every other block has finished, so has
+// read the counters) writes step + 1 back.  Arrival is two-level so that hundreds of blocks do not
+// serialise on one atomic word: block b takes a ticket on shard b % 8 (the blocks of one XCD), the
+// last arrival of a shard takes a ticket on the top word, the last of those is the grid's last.
+// Each last arrival resets its word for the next launch.  One ticket set per kernel kind: launches
+// of a kind run one at a time on the caller's stream.  (1-D grids.)
+__device__ unsigned g_adam_ticket[2][9];
+
+__device__ __forceinline__ bool last_block(unsigned* ticket) {
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x, sh = blockIdx.x % 8;
+    const unsigned in_shard = (G + 7 - sh) / 8, shards = G < 8 ? G : 8;
+    bool top = atomicAdd(&ticket[sh], 1u) == in_shard - 1;
+    if (top) atomicExch(&ticket[sh], 0u);
+    last = top && atomicAdd(&ticket[8], 1u) == shards - 1;
+    if (last) atomicExch(&ticket[8], 0u);
+  }
+  __syncthreads();
+  return last;
+}
+
 // Persistent grid over the launch's (tensor, chunk) list; the step-dependent scalars are derived
 // once per tensor a block meets.  Each thread keeps two float4 quartets (p, g, m, v) in flight.
 template <bool ROWS>
@@ -101,7 +118,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
       if (a.step[t]) {
         // step-dependent scalars from device memory (graph-replayable); same double arithmetic
         // as the host path / torch's Python scalars
-        const double st = (double)a.step[t][0];
+        const double st = (double)(a.step[t][0] + 1);  // this step (the counter is bumped at the end)
         const double lr = h.d_lr ? h.d_lr[0] : h.lr;
         const double bc1 = 1.0 - pow(h.beta1_d, st);
         const double bc2 = 1.0 - pow(h.beta2_d, st);
@@ -158,6 +175,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
       for (int64_t k = base + threadIdx.x; k < end; k += blockDim.x) adam_elem(P[k], G[k], M[k], V[k], h);
     }
   }
+  if (a.step[0] && last_block(g_adam_ticket[ROWS ? 1 : 0]) && threadIdx.x < a.n && a.step[threadIdx.x])
+    a.step[threadIdx.x][0] += 1;
 }
 
 
@@ -236,18 +255,24 @@ struct LazyArgs {
   int n;
 };
 
+// (neg_step, bc2_sqrt) of step st: the values the history ring keeps for it
+__device__ __forceinline__ float2 lazy_scalars(const AdamHyper& h, int64_t st) {
+  const double lr = h.d_lr ? h.d_lr[0] : h.lr;
+  const double bc1 = 1.0 - pow(h.beta1_d, (double)st);
+  const double bc2 = 1.0 - pow(h.beta2_d, (double)st);
+  return make_float2((float)(-(lr / bc1)), (float)sqrt(bc2));
+}
+
 __global__ void adam_lazy_inc_kernel(LazyArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
   const int t = threadIdx.x;
   if (t >= a.n) return;
   const int64_t st = a.step[t][0] + 1;
   a.step[t][0] = st;
-  const double lr = h.d_lr ? h.d_lr[0] : h.lr;
-  const double bc1 = 1.0 - pow(h.beta1_d, (double)st);
-  const double bc2 = 1.0 - pow(h.beta2_d, (double)st);
-  float* e = a.hist[t] + 2 * (st % a.cap);
-  e[0] = (float)(-(lr / bc1));
-  e[1] = (float)sqrt(bc2);
+  const float2 e = lazy_scalars(h, st);
+  float* hp = a.hist[t] + 2 * (st % a.cap);
+  hp[0] = e.x;
+  hp[1] = e.y;
 }
 
 // FLUSH: one wave per (tensor, row), replay through step t, no gradient.  Step: one wave per
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyp
   for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < total; w += waves) {
     while (t + 1 < a.n && w >= a.row_start[t + 1]) ++t;
     while (t > 0 && w < a.row_start[t]) --t;
-    const int64_t st = a.step[t][0];
+    const int64_t st = a.step[t][0];  // step mode: this step (adam_lazy_inc_kernel has advanced the counter)
     int64_t r, s0;
     int32_t slot = -1;
     if constexpr (FLUSH) {
@@ -564,10 +589,7 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
       a.blk_start[a.n] = blocks;
       if (a.n == 0) continue;
       (void)idx;
-      if (d_steps) {
-        hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, s, a, d_skip);
-        FR_LAUNCH_CHECK();
-      }
+      // device-scalar mode: the kernel's last block advances the step counters
       if (rows_pass)
         hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0, s,
                            a, h, d_skip);

@@ -210,6 +210,68 @@ __global__ __launch_bounds__(256) void emb_rmap_fill_kernel(int32_t* __restrict_
     rmap[i] = -1;
 }
 
+// Row-gradient mode for up to kOneBlock positions: the owner pass in ONE workgroup (replaces the
+// rmap fill, status clear and owner scan launches of the owner path; emb_owner_sum_kernel then sums):
+//   1. status = 0; rmap[0 .. R) = -1 (stores drained before the barrier, so the owners' later
+//      rmap stores land after them);
+//   2. keys (row << 12 | position; invalid rows and the padding row -> max) bitonic-sorted in LDS:
+//      equal rows become runs in ascending position;
+//   3. per sorted element: own[pos] = first of its run (then rmap[row] = pos), nxt[pos] = the next
+//      position of the run or -1 -- the chains emb_owner_sum_kernel walks, as the owner scan builds.
+constexpr int kOneBlock = 1024;  // one key per thread
+constexpr int kOneThreads = 1024;
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__global__ __launch_bounds__(kOneThreads) void emb_owner_one_kernel(const int64_t* __restrict__ idx, int n, int64_t R,
+                                                                    int64_t pad, int32_t* __restrict__ nxt,
+                                                                    int32_t* __restrict__ own,
+                                                                    int32_t* __restrict__ rmap,
+                                                                    int32_t* __restrict__ status) {
+  __shared__ uint64_t key[kOneBlock];
+  const int t = threadIdx.x;
+  if (t == 0) status[0] = 0;
+  for (int64_t r = t; r < R; r += kOneThreads) rmap[r] = -1;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  const int rk = emb_key(idx, t, n, R, pad);
+  uint64_t v = (t < n && rk >= 0) ? (((uint64_t)rk << 12) | (uint64_t)t) : ~0ull;
+  // bitonic sort, one key per thread: partner distances below 64 exchange in registers (lane
+  // shuffles), the larger ones through LDS
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t o;
+      if (j >= 64) {  // block-uniform
+        key[t] = v;
+        __syncthreads();
+        o = key[t ^ j];
+        __syncthreads();
+      } else {
+        o = shfl_xor_u64(v, j);
+      }
+      const bool keep_min = ((t & j) == 0) == ((t & k) == 0);
+      v = keep_min ? (o < v ? o : v) : (o > v ? o : v);
+    }
+  }
+  key[t] = v;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rmap fill has reached L2
+  __syncthreads();
+  if (t < n) {
+    if (v != ~0ull) {  // invalid / padding positions sort last: no owner, no chain
+      const int pos = (int)(v & 0xFFF);
+      const bool first = t == 0 || (key[t - 1] >> 12) != (v >> 12);
+      const bool more = t + 1 < n && key[t + 1] != ~0ull && (key[t + 1] >> 12) == (v >> 12);
+      own[pos] = first ? 1 : 0;
+      nxt[pos] = more ? (int32_t)(key[t + 1] & 0xFFF) : -1;
+      if (first) rmap[v >> 12] = pos;
+    }
+    if (rk < 0) own[t] = 0;  // a position with an invalid row is never an owner
+  }
+}
+
 // one wave per position: lanes compare 256 ids per step (4 x 64, ballots), stopping once an earlier
 // duplicate and the next duplicate are both found
 constexpr int kScanPerWave = 1;
@@ -527,6 +589,16 @@ int emb_bwd_impl(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t l
   const int d4 = d / 4;
   EmbWS w = emb_ws(d_workspace, n, R, d);
   float4* out4 = reinterpret_cast<float4*>(d_out);
+  if (rmap && n > 0 && n <= kOneBlock) {  // one workgroup: fill, sort, owners; then the chain sums
+    hipLaunchKernelGGL(emb_owner_one_kernel, dim3(1), dim3(kOneThreads), 0, s, d_idx, (int)n, R, padding_idx, w.nxt,
+                       w.own, rmap, w.cursor + R + 1);
+    FR_LAUNCH_CHECK();
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(n * d4, 256), (int64_t)fr::kNumCU * 8));
+    hipLaunchKernelGGL(emb_owner_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, n, w.nxt, w.own,
+                       reinterpret_cast<const float4*>(d_grad), ldg / 4, d4, out4, ldo / 4, 1);
+    FR_LAUNCH_CHECK();
+    return FR_OK;
+  }
   if (rmap) {
     hipLaunchKernelGGL(emb_rmap_fill_kernel, dim3((unsigned)std::min<int64_t>(fr::ceil_div(R, 256), 1024)), dim3(256),
                        0, s, rmap, R);

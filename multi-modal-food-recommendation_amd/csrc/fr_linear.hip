@@ -33,20 +33,19 @@ __device__ __forceinline__ float4 ldx4(const float* X, int64_t ldx, const int64_
   return make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-__global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict__ dY, int64_t ldy,
-                                                         const float* __restrict__ X, int64_t ldx,
-                                                         const int64_t* __restrict__ ids, int64_t M,
-                                                         int N, int K, int ktiles, float* __restrict__ part,
-                                                         float* __restrict__ pdb) {
+__device__ __forceinline__ void wgrad_slab(const float* __restrict__ dY, int64_t ldy, const float* __restrict__ X,
+                                           int64_t ldx, const int64_t* __restrict__ ids, int64_t M, int N, int K,
+                                           int ktiles, float* __restrict__ part, float* __restrict__ pdb,
+                                           const int bx, const int by) {
   __shared__ float4 As[SUB][TN / 4];
   __shared__ float4 Bs[SUB][TK / 4];
   const int t = threadIdx.x;
   const int tn = t / 16, tk = t % 16;  // compute layout: 4 n x 4 k per thread
   const int lr = t / 16, lc = t % 16;  // load layout: one float4 of one row per thread (A and B)
-  const int n0 = (blockIdx.y / ktiles) * TN, k0 = (blockIdx.y % ktiles) * TK;
-  const int64_t m0 = (int64_t)blockIdx.x * kSlab;
+  const int n0 = (by / ktiles) * TN, k0 = (by % ktiles) * TK;
+  const int64_t m0 = (int64_t)bx * kSlab;
   const int64_t m1 = min(M, m0 + kSlab);
-  const bool want_db = pdb != nullptr && (blockIdx.y % ktiles) == 0;
+  const bool want_db = pdb != nullptr && (by % ktiles) == 0;
   float acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -77,7 +76,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict
     }
     __syncthreads();
   }
-  const int64_t slab = blockIdx.x;
+  const int64_t slab = bx;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + tn * 4 + i;
@@ -92,15 +91,49 @@ __global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict
   }
 }
 
+__global__ __launch_bounds__(256) void wgrad_slab_kernel(const float* __restrict__ dY, int64_t ldy,
+                                                         const float* __restrict__ X, int64_t ldx,
+                                                         const int64_t* __restrict__ ids, int64_t M,
+                                                         int N, int K, int ktiles, float* __restrict__ part,
+                                                         float* __restrict__ pdb) {
+  wgrad_slab(dY, ldy, X, ldx, ids, M, N, K, ktiles, part, pdb, blockIdx.x, blockIdx.y);
+}
+
+// several gathered-input Linears over the same ids and rows (HealthRec's image / text projections):
+// blockIdx.z = table, its own (N x K_t) tiles, partial slabs and reduction
+constexpr int kMaxWg = 4;
+struct WgTabs {
+  const float* dy[kMaxWg];
+  const float* X[kMaxWg];
+  int64_t ldx[kMaxWg];
+  int K[kMaxWg];
+  int ktiles[kMaxWg];
+  int tiles[kMaxWg];
+  float* part[kMaxWg];
+  float* pdb[kMaxWg];
+  float* dW[kMaxWg];
+  int64_t ldw[kMaxWg];
+  float* db[kMaxWg];
+  int64_t red_start[kMaxWg + 1];  // reduce: first block of table t
+};
+
+__global__ __launch_bounds__(256) void wgrad_slab_multi_kernel(int64_t ldy, const int64_t* __restrict__ ids,
+                                                               int64_t M, int N, WgTabs T) {
+  const int t = blockIdx.z;
+  if ((int)blockIdx.y >= T.tiles[t]) return;
+  wgrad_slab(T.dy[t], ldy, T.X[t], T.ldx[t], ids, M, N, T.K[t], T.ktiles[t], T.part[t], T.pdb[t], blockIdx.x,
+             blockIdx.y);
+}
+
 // dW[n,k] = sum over slabs (in order, 4 interleaved slab lanes combined in fixed order)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t slabs, int N,
-                                                           int K, float* __restrict__ dW, int64_t ldw,
-                                                           const float* __restrict__ pdb, float* __restrict__ db) {
+__device__ __forceinline__ void wgrad_reduce(const float* __restrict__ part, int64_t slabs, int N, int K,
+                                             float* __restrict__ dW, int64_t ldw, const float* __restrict__ pdb,
+                                             float* __restrict__ db, int64_t bx) {
   __shared__ float red[4][64];
   const int e_local = threadIdx.x % 64, g = threadIdx.x / 64;
   const int64_t NK = (int64_t)N * K;
   const int64_t total = NK + (db ? N : 0);
-  const int64_t e = (int64_t)blockIdx.x * 64 + e_local;
+  const int64_t e = bx * 64 + e_local;
   float s = 0.f;
   if (e < total) {
     const float* src = e < NK ? part + e : pdb + (e - NK);
@@ -120,6 +153,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     if (e < NK) dW[(e / K) * ldw + (e % K)] = r;
     else db[e - NK] = r;
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int64_t slabs, int N,
+                                                           int K, float* __restrict__ dW, int64_t ldw,
+                                                           const float* __restrict__ pdb, float* __restrict__ db) {
+  wgrad_reduce(part, slabs, N, K, dW, ldw, pdb, db, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_multi_kernel(int64_t slabs, int N, int n_tab, WgTabs T) {
+  int t = 0;
+  while (t + 1 < n_tab && (int64_t)blockIdx.x >= T.red_start[t + 1]) ++t;
+  wgrad_reduce(T.part[t], slabs, N, T.K[t], T.dW[t], T.ldw[t], T.pdb[t], T.db[t], blockIdx.x - T.red_start[t]);
 }
 
 }  // namespace
@@ -167,4 +212,58 @@ extern "C" int fr_linear_wgrad_gather(const float* d_dy, int64_t ldy, const int6
                                       void* d_workspace, int64_t workspace_bytes, void* stream) {
   FR_REQUIRE(d_ids, "null ids");
   return wgrad_impl(d_dy, ldy, d_ids, d_x, ldx, M, N, K, d_dw, ldw, d_db, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int64_t fr_linear_wgrad_gather_multi_workspace(int64_t M, int N, int n_tab, const int* K) {
+  if (M <= 0 || N <= 0 || n_tab < 1 || n_tab > kMaxWg || !K) return 0;
+  int64_t b = 0;
+  for (int t = 0; t < n_tab; ++t) b += fr_linear_wgrad_workspace(M, N, K[t]);
+  return b;
+}
+
+extern "C" int fr_linear_wgrad_gather_multi(const float* d_dy, int64_t ldy, const int64_t* d_ids, int64_t M, int N,
+                                            int n_tab, const float* const* d_x, const int64_t* ldx, const int* K,
+                                            float* const* d_dw, const int64_t* ldw, float* const* d_db,
+                                            void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(M > 0 && N > 0 && N % 4 == 0 && n_tab >= 1 && n_tab <= kMaxWg, "bad sizes (1..4 tables)");
+  FR_REQUIRE(d_dy && d_ids && d_x && ldx && K && d_dw && ldw && ldy >= N * n_tab && ldy % 4 == 0 &&
+                 fr::aligned16(d_dy),
+             "bad operands (dY holds the tables' N-wide blocks side by side)");
+  FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) &&
+                 workspace_bytes >= fr_linear_wgrad_gather_multi_workspace(M, N, n_tab, K),
+             "workspace too small");
+  const int64_t slabs = fr::ceil_div(M, kSlab);
+  FR_REQUIRE(slabs < (1u << 31), "too many rows");
+  WgTabs T{};
+  char* w = reinterpret_cast<char*>(d_workspace);
+  int max_tiles = 0;
+  int64_t blocks = 0;
+  for (int t = 0; t < n_tab; ++t) {
+    FR_REQUIRE(K[t] > 0 && K[t] % 4 == 0 && d_x[t] && d_dw[t] && ldx[t] >= K[t] && ldx[t] % 4 == 0 && ldw[t] >= K[t] &&
+                   fr::aligned16(d_x[t]),
+               "bad table operands");
+    T.dy[t] = d_dy + (int64_t)t * N;
+    T.X[t] = d_x[t];
+    T.ldx[t] = ldx[t];
+    T.K[t] = K[t];
+    T.ktiles[t] = (int)fr::ceil_div(K[t], TK);
+    T.tiles[t] = (int)fr::ceil_div(N, TN) * T.ktiles[t];
+    T.part[t] = reinterpret_cast<float*>(w);
+    T.pdb[t] = (d_db && d_db[t]) ? reinterpret_cast<float*>(w + fr::align_up(slabs * N * K[t] * 4, 256)) : nullptr;
+    w += fr_linear_wgrad_workspace(M, N, K[t]);
+    T.dW[t] = d_dw[t];
+    T.ldw[t] = ldw[t];
+    T.db[t] = d_db ? d_db[t] : nullptr;
+    T.red_start[t] = blocks;
+    blocks += fr::ceil_div((int64_t)N * K[t] + (T.db[t] ? N : 0), 64);
+    max_tiles = std::max(max_tiles, T.tiles[t]);
+  }
+  T.red_start[n_tab] = blocks;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(wgrad_slab_multi_kernel, dim3((unsigned)slabs, (unsigned)max_tiles, (unsigned)n_tab), dim3(256),
+                     0, s, ldy, d_ids, M, N, T);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slabs, N, n_tab, T);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
 }

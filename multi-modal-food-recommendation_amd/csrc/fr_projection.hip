@@ -31,11 +31,10 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // One workgroup per (16-row tile, 16-column tile): its four waves take contiguous quarters of K
 // (loads of four 16-wide chunks issued before their sixteen MFMAs), then the four partial tiles are
 // added in wave order through LDS and the bias added: no cross-workgroup traffic, deterministic.
-__global__ __launch_bounds__(64 * WAVES) void gather_linear_kernel(const int64_t* __restrict__ ids, int64_t n,
-                                                                   const float* __restrict__ X, int64_t ldx, int K,
-                                                                   const float* __restrict__ W,
-                                                                   const float* __restrict__ b, float* __restrict__ Y,
-                                                                   int64_t ldy) {
+__device__ __forceinline__ void gather_linear_tile(const int64_t* __restrict__ ids, int64_t n,
+                                                   const float* __restrict__ X, int64_t ldx, int K,
+                                                   const float* __restrict__ W, const float* __restrict__ b,
+                                                   float* __restrict__ Y, int64_t ldy) {
   __shared__ float red[WAVES][256];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = l & 15, h = l >> 4;
@@ -77,11 +76,36 @@ __global__ __launch_bounds__(64 * WAVES) void gather_linear_kernel(const int64_t
   }
 }
 
+__global__ __launch_bounds__(64 * WAVES) void gather_linear_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                   const float* __restrict__ X, int64_t ldx, int K,
+                                                                   const float* __restrict__ W,
+                                                                   const float* __restrict__ b, float* __restrict__ Y,
+                                                                   int64_t ldy) {
+  gather_linear_tile(ids, n, X, ldx, K, W, b, Y, ldy);
+}
+
+// several tables at the same ids in one launch: blockIdx.z = table, its 64 output columns at 64 t
+constexpr int kMaxProj = 4;
+struct ProjTabs {
+  const float* X[kMaxProj];
+  int64_t ldx[kMaxProj];
+  int K[kMaxProj];
+  const float* W[kMaxProj];
+  const float* b[kMaxProj];
+};
+
+__global__ __launch_bounds__(64 * WAVES) void gather_linear_multi_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                         ProjTabs P, float* __restrict__ Y,
+                                                                         int64_t ldy) {
+  const int t = blockIdx.z;
+  gather_linear_tile(ids, n, P.X[t], P.ldx[t], P.K[t], P.W[t], P.b[t], Y + (int64_t)t * D, ldy);
+}
+
 // out[i, c] = sum_k S[i, k] W[k, c] for k < 64: 16 rows x 256 columns per workgroup, wave w the
 // columns 64w..64w+63 as four 16x16 MFMA tiles over 16 k-steps.
-__global__ __launch_bounds__(64 * WAVES) void rows_matmul_kernel(const float* __restrict__ S, int64_t lds, int64_t n,
-                                                                 const float* __restrict__ W, int K,
-                                                                 float* __restrict__ out, int64_t ldo) {
+__device__ __forceinline__ void rows_matmul_tile(const float* __restrict__ S, int64_t lds, int64_t n,
+                                                 const float* __restrict__ W, int K, float* __restrict__ out,
+                                                 int64_t ldo) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = l & 15, h = l >> 4;
   const int64_t i0 = (int64_t)blockIdx.x * 16;
@@ -120,6 +144,27 @@ __global__ __launch_bounds__(64 * WAVES) void rows_matmul_kernel(const float* __
   }
 }
 
+__global__ __launch_bounds__(64 * WAVES) void rows_matmul_kernel(const float* __restrict__ S, int64_t lds, int64_t n,
+                                                                 const float* __restrict__ W, int K,
+                                                                 float* __restrict__ out, int64_t ldo) {
+  rows_matmul_tile(S, lds, n, W, K, out, ldo);
+}
+
+struct RowTabs {
+  const float* W[kMaxProj];
+  int K[kMaxProj];
+  float* out[kMaxProj];
+  int64_t ldo[kMaxProj];
+};
+
+// blockIdx.z = table t: S's 64-column block t times W_t; column blocks past K_t exit
+__global__ __launch_bounds__(64 * WAVES) void rows_matmul_multi_kernel(const float* __restrict__ S, int64_t lds,
+                                                                       int64_t n, RowTabs T) {
+  const int t = blockIdx.z;
+  if ((int)blockIdx.y * 256 >= T.K[t]) return;
+  rows_matmul_tile(S + (int64_t)t * D, lds, n, T.W[t], T.K[t], T.out[t], T.ldo[t]);
+}
+
 }  // namespace
 
 extern "C" int fr_gather_linear_fwd(const int64_t* d_ids, int64_t n, const float* d_x, int64_t ldx, int K,
@@ -142,6 +187,51 @@ extern "C" int fr_rows_matmul(const float* d_s, int64_t lds, int64_t n, const fl
   FR_REQUIRE(d_s && d_w && d_out && lds >= D && ldo >= K, "bad operands");
   hipLaunchKernelGGL(rows_matmul_kernel, dim3((unsigned)fr::ceil_div(n, 16), (unsigned)fr::ceil_div(K, 256)),
                      dim3(64 * WAVES), 0, reinterpret_cast<hipStream_t>(stream), d_s, lds, n, d_w, K, d_out, ldo);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_gather_linear_fwd_multi(const int64_t* d_ids, int64_t n, int n_tab, const float* const* d_x,
+                                          const int64_t* ldx, const int* K, const float* const* d_w,
+                                          const float* const* d_b, float* d_y, int64_t ldy, void* stream) {
+  FR_REQUIRE(n > 0 && n_tab >= 1 && n_tab <= kMaxProj, "n > 0 and 1..4 tables required");
+  FR_REQUIRE(d_ids && d_x && ldx && K && d_w && d_y && ldy >= D * n_tab, "null operand or ldy < 64 * tables");
+  ProjTabs P{};
+  for (int t = 0; t < n_tab; ++t) {
+    FR_REQUIRE(K[t] > 0 && K[t] % 16 == 0 && ldx[t] >= K[t] && ldx[t] % 4 == 0 && d_x[t] && d_w[t] &&
+                   fr::aligned16(d_x[t]) && fr::aligned16(d_w[t]),
+               "table X rows / W must be 16-byte aligned, K a multiple of 16, ldx >= K");
+    P.X[t] = d_x[t];
+    P.ldx[t] = ldx[t];
+    P.K[t] = K[t];
+    P.W[t] = d_w[t];
+    P.b[t] = d_b ? d_b[t] : nullptr;
+  }
+  const int64_t tiles = fr::ceil_div(n, 16);
+  FR_REQUIRE(tiles < (1ll << 31), "too many rows");
+  hipLaunchKernelGGL(gather_linear_multi_kernel, dim3((unsigned)tiles, D / 16, (unsigned)n_tab), dim3(64 * WAVES), 0,
+                     reinterpret_cast<hipStream_t>(stream), d_ids, n, P, d_y, ldy);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_rows_matmul_multi(const float* d_s, int64_t lds, int64_t n, int n_tab, const float* const* d_w,
+                                    const int* K, float* const* d_out, const int64_t* ldo, void* stream) {
+  FR_REQUIRE(n > 0 && n_tab >= 1 && n_tab <= kMaxProj, "n > 0 and 1..4 tables required");
+  FR_REQUIRE(d_s && d_w && K && d_out && ldo && lds >= D * n_tab, "null operand or lds < 64 * tables");
+  RowTabs T{};
+  int kmax = 0;
+  for (int t = 0; t < n_tab; ++t) {
+    FR_REQUIRE(K[t] > 0 && d_w[t] && d_out[t] && ldo[t] >= K[t], "bad table operands");
+    T.W[t] = d_w[t];
+    T.K[t] = K[t];
+    T.out[t] = d_out[t];
+    T.ldo[t] = ldo[t];
+    kmax = std::max(kmax, K[t]);
+  }
+  hipLaunchKernelGGL(rows_matmul_multi_kernel,
+                     dim3((unsigned)fr::ceil_div(n, 16), (unsigned)fr::ceil_div(kmax, 256), (unsigned)n_tab),
+                     dim3(64 * WAVES), 0, reinterpret_cast<hipStream_t>(stream), d_s, lds, n, T);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
