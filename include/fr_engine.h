@@ -331,14 +331,18 @@ int fr_adam_step_rows(float* const* params, const float* const* grads, float* co
 /* Row-gradient Adam with deferred zero-gradient steps (exact "lazy rows").  Same contract as
  * fr_adam_step_rows (torch.optim.Adam.step, common/trainer.py:224, over cikm_model.py:83-87's
  * image/text tables), but a row with no gradient this step is not touched: the step's
- * (-lr/bc1, sqrt(bc2)) go to d_hist[t][(step % hist_cap)] and d_last[t][r] holds the step row r is
+ * (-lr/bc1, sqrt(bc2), and as a double in floats 2-3 RN64(1 / sqrt(bc2)_f32)) go to
+ * d_hist[t][(step % hist_cap)] and d_last[t][r] holds the step row r is
  * current through.  A row with a gradient first replays its skipped steps with g = 0 (the dense
  * kernel's float operations), then applies this step.  fr_adam_flush_rows brings every row up to
  * the current step; after a flush p, exp_avg and exp_avg_sq equal fr_adam_step_rows' bit for bit.
  * The caller flushes before any full-table read and at least every hist_cap - 1 steps.
  * d_ids[t][0..n_ids[t]): the ids whose gradient rows d_rmaps[t] maps (duplicates allowed; the
  * kernel works per id, not per table row).  d_last: int32 [R] per tensor (zero at step 0); d_hist:
- * float32 [hist_cap, 2] per tensor; n_tensors <= 16. */
+ * float32 [hist_cap, 4] per tensor (16-byte aligned); n_tensors <= 16.  Deferred zero-gradient steps
+ * are replayed with the division by sqrt(bc2) as RN32(double(s) * that reciprocal): bit-identical to
+ * the dense step (a quotient of two fp32 numbers is never within 2^-49 of an fp32 rounding
+ * boundary; the double product is within 2^-52). */
 int fr_adam_step_rows_lazy(float* const* params, const float* const* grads, float* const* exp_avg,
                            float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                            const int32_t* const* d_rmaps, const int64_t* const* d_ids, const int64_t* n_ids,

@@ -472,7 +472,8 @@ class FusedAdam(torch.optim.Optimizer):
                 if "lazy_last" not in st:
                     # every row is current through the table's present step (0, or the dense steps so far)
                     st["lazy_last"] = st["step"].to(torch.int32).expand(p.shape[0]).contiguous()
-                    st["lazy_hist"] = torch.zeros(self.hist_cap, 2, dtype=torch.float32, device=p.device)
+                    # per step: neg_step, bc2_sqrt (fp32) and RN64(1 / bc2_sqrt) (a double in floats 2-3)
+                    st["lazy_hist"] = torch.zeros(self.hist_cap, 4, dtype=torch.float32, device=p.device)
             idl = [i if i.is_contiguous() else i.contiguous() for i in idl]
             for k in range(0, n, 16):  # the kernel's argument block takes 16 tables per launch
                 m = min(16, n - k)

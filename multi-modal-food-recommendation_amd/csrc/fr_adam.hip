@@ -246,7 +246,7 @@ struct LazyArgs {
   int64_t* step[kMaxLazy];
   const int32_t* rmap[kMaxLazy];
   int32_t* last[kMaxLazy];
-  float* hist[kMaxLazy];      // [cap][2]: (neg_step, bc2_sqrt) of step s at s % cap
+  float* hist[kMaxLazy];      // [cap][4]: (neg_step, bc2_sqrt, double 1 / bc2_sqrt) of step s at s % cap
   const int64_t* ids[kMaxLazy];  // step: the ids whose rows carry a gradient (duplicates allowed)
   int64_t nrows[kMaxLazy];
   int32_t rshift[kMaxLazy];   // row width = 1 << rshift
@@ -270,9 +270,92 @@ __global__ void adam_lazy_inc_kernel(LazyArgs a, AdamHyper h, const int32_t* ski
   const int64_t st = a.step[t][0] + 1;
   a.step[t][0] = st;
   const float2 e = lazy_scalars(h, st);
-  float* hp = a.hist[t] + 2 * (st % a.cap);
+  float* hp = a.hist[t] + 4 * (st % a.cap);  // kHist = 4: neg_step, bc2_sqrt, RN64(1 / bc2_sqrt)
   hp[0] = e.x;
   hp[1] = e.y;
+  *reinterpret_cast<double*>(hp + 2) = 1.0 / (double)e.y;
+}
+
+
+// ---- deferred zero-gradient steps, bit-identical to adam_elem(g = 0) and cheaper ---------------
+// History ring entry of step s (4 floats at hist + 4 (s % cap)): neg_step, bc2_sqrt (the fp32 scalars
+// adam_elem uses) and, as a double in floats 2-3, RN64(1 / bc2_sqrt) for the division below.
+constexpr int kHist = 4;
+// With g = 0 (and no weight decay) a step is  m = fma(w1, -m, m);  v = v * beta2;
+// p += (neg_step * m) / (sqrt_rn(v) / bc2_sqrt + eps).  The division by the step's constant bc2_sqrt
+// is done as RN32(double(s) * RN64(1 / bc2_sqrt)): the double product is within 2^-52 (relative) of
+// s / bc2_sqrt, and a quotient of two fp32 numbers lies at least 2^-49 (relative) from every fp32
+// rounding boundary (it is never a midpoint: that would need a 25-bit odd significand dividing a
+// 24-bit one), so the rounded result equals the correctly rounded fp32 quotient (s >= sqrt of the
+// smallest subnormal, so the quotient is a normal number).  One double reciprocal per step, shared
+// by all of a lane's elements; the elementwise products and sums on packed-fp32 ops.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void zero_step2(float& p0, float& p1, float& m0, float& m1, float& v0, float& v1, float ns,
+                                           double rc, const AdamHyper& h) {
+#pragma clang fp contract(off)
+  pf2 m = {m0, m1}, v = {v0, v1};
+  const pf2 w1 = {h.w1, h.w1}, b2 = {h.beta2, h.beta2};
+  m = __builtin_elementwise_fma(w1, -m, m);
+  v = v * b2;
+  const float q0 = (float)((double)sqrt_rn(v.x) * rc), q1 = (float)((double)sqrt_rn(v.y) * rc);
+  const pf2 den = pf2{q0, q1} + pf2{h.eps, h.eps};
+  const pf2 u = pf2{ns, ns} * m;
+  const pf2 p = pf2{p0, p1} + pf2{__fdiv_rn(u.x, den.x), __fdiv_rn(u.y, den.y)};
+  p0 = p.x; p1 = p.y; m0 = m.x; m1 = m.y; v0 = v.x; v1 = v.y;
+}
+
+// steps [s0, s1) with g = 0 on one float4 of a row
+__device__ __forceinline__ void zero_steps4(float4& p, float4& m, float4& v, const float* __restrict__ hist, int cap,
+                                            int64_t s0, int64_t s1, const AdamHyper& h) {
+  if (h.wd != 0.f) {  // weight decay makes g' = wd p nonzero: the general element step
+    AdamHyper hs = h;
+    for (int64_t s = s0; s < s1; ++s) {
+      const float* e = hist + kHist * (s % cap);
+      hs.neg_step = e[0];
+      hs.bc2_sqrt = e[1];
+      adam_elem(p.x, 0.f, m.x, v.x, hs);
+      adam_elem(p.y, 0.f, m.y, v.y, hs);
+      adam_elem(p.z, 0.f, m.z, v.z, hs);
+      adam_elem(p.w, 0.f, m.w, v.w, hs);
+    }
+    return;
+  }
+  for (int64_t s = s0; s < s1; ++s) {
+    const float* e = hist + kHist * (s % cap);
+    const float ns = e[0];
+    const double rc = *reinterpret_cast<const double*>(e + 2);
+    zero_step2(p.x, p.y, m.x, m.y, v.x, v.y, ns, rc, h);
+    zero_step2(p.z, p.w, m.z, m.w, v.z, v.w, ns, rc, h);
+  }
+}
+
+// one row of `width` floats at P / M / V, lane-strided float4 chunks: zero steps [s0, s1), then (G
+// non-null) step `st` with gradient row G
+__device__ __forceinline__ void replay_row(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                                           const float* __restrict__ G, int width, int lane,
+                                           const float* __restrict__ hist, int cap, int64_t s0, int64_t s1,
+                                           int64_t st, const AdamHyper& h) {
+  for (int q = 4 * lane; q < width; q += 4 * 64) {
+    float4 p = *reinterpret_cast<const float4*>(P + q);
+    float4 m = *reinterpret_cast<const float4*>(M + q);
+    float4 v = *reinterpret_cast<const float4*>(V + q);
+    zero_steps4(p, m, v, hist, cap, s0, s1, h);
+    if (G) {
+      AdamHyper hs = h;
+      const float* e = hist + kHist * (st % cap);
+      hs.neg_step = e[0];
+      hs.bc2_sqrt = e[1];
+      const float4 g = *reinterpret_cast<const float4*>(G + q);
+      adam_elem(p.x, g.x, m.x, v.x, hs);
+      adam_elem(p.y, g.y, m.y, v.y, hs);
+      adam_elem(p.z, g.z, m.z, v.z, hs);
+      adam_elem(p.w, g.w, m.w, v.w, hs);
+    }
+    *reinterpret_cast<float4*>(P + q) = p;
+    *reinterpret_cast<float4*>(M + q) = m;
+    *reinterpret_cast<float4*>(V + q) = v;
+  }
 }
 
 // FLUSH: one wave per (tensor, row), replay through step t, no gradient.  Step: one wave per
@@ -308,41 +391,11 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(LazyArgs a, AdamHyp
     }
     const int64_t s_end = FLUSH ? st + 1 : st;  // replayed zero-gradient steps: [s0, s_end)
     if (FLUSH && s0 > st) continue;
-    const float* __restrict__ hist = a.hist[t];
-    const int cap = a.cap;
-    const int width = 1 << a.rshift[t];
     float* __restrict__ P = a.p[t] + (r << a.rshift[t]);
     float* __restrict__ M = a.m[t] + (r << a.rshift[t]);
     float* __restrict__ V = a.v[t] + (r << a.rshift[t]);
     const float* __restrict__ G = FLUSH ? nullptr : a.g[t] + ((int64_t)slot << a.rshift[t]);
-    for (int q = 4 * lane; q < width; q += 4 * 64) {
-      float4 p = *reinterpret_cast<const float4*>(P + q);
-      float4 m = *reinterpret_cast<const float4*>(M + q);
-      float4 v = *reinterpret_cast<const float4*>(V + q);
-      AdamHyper hs = h;
-      for (int64_t s = s0; s < s_end; ++s) {
-        const float* e = hist + 2 * (s % cap);
-        hs.neg_step = e[0];
-        hs.bc2_sqrt = e[1];
-        adam_elem(p.x, 0.f, m.x, v.x, hs);
-        adam_elem(p.y, 0.f, m.y, v.y, hs);
-        adam_elem(p.z, 0.f, m.z, v.z, hs);
-        adam_elem(p.w, 0.f, m.w, v.w, hs);
-      }
-      if constexpr (!FLUSH) {
-        const float4 g = *reinterpret_cast<const float4*>(G + q);
-        const float* e = hist + 2 * (st % cap);
-        hs.neg_step = e[0];
-        hs.bc2_sqrt = e[1];
-        adam_elem(p.x, g.x, m.x, v.x, hs);
-        adam_elem(p.y, g.y, m.y, v.y, hs);
-        adam_elem(p.z, g.z, m.z, v.z, hs);
-        adam_elem(p.w, g.w, m.w, v.w, hs);
-      }
-      *reinterpret_cast<float4*>(P + q) = p;
-      *reinterpret_cast<float4*>(M + q) = m;
-      *reinterpret_cast<float4*>(V + q) = v;
-    }
+    replay_row(P, M, V, G, 1 << a.rshift[t], lane, a.hist[t], a.cap, s0, s_end, st, h);
     if (FLUSH && lane == 0) a.last[t][r] = (int32_t)st;
   }
 }
@@ -398,28 +451,8 @@ __device__ __forceinline__ void catch_up_row(float* __restrict__ P0, float* __re
   if (lane == 0) old = atomicMax(last + r, (int32_t)st);
   old = __shfl(old, 0, 64);
   if ((int64_t)old >= st) return;
-  const int width = 1 << rshift;
-  float* P = P0 + (r << rshift);
-  float* M = M0 + (r << rshift);
-  float* V = V0 + (r << rshift);
-  for (int q = 4 * lane; q < width; q += 4 * 64) {
-    float4 p = *reinterpret_cast<const float4*>(P + q);
-    float4 m = *reinterpret_cast<const float4*>(M + q);
-    float4 v = *reinterpret_cast<const float4*>(V + q);
-    AdamHyper hs = h;
-    for (int64_t s = (int64_t)old + 1; s <= st; ++s) {
-      const float* e = hist + 2 * (s % cap);
-      hs.neg_step = e[0];
-      hs.bc2_sqrt = e[1];
-      adam_elem(p.x, 0.f, m.x, v.x, hs);
-      adam_elem(p.y, 0.f, m.y, v.y, hs);
-      adam_elem(p.z, 0.f, m.z, v.z, hs);
-      adam_elem(p.w, 0.f, m.w, v.w, hs);
-    }
-    *reinterpret_cast<float4*>(P + q) = p;
-    *reinterpret_cast<float4*>(M + q) = m;
-    *reinterpret_cast<float4*>(V + q) = v;
-  }
+  replay_row(P0 + (r << rshift), M0 + (r << rshift), V0 + (r << rshift), nullptr, 1 << rshift, lane, hist, cap,
+             (int64_t)old + 1, st + 1, st, h);
 }
 }  // namespace
 
