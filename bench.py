@@ -163,6 +163,9 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         do_step(args.warmup + i)
+    t_submit = time.perf_counter() - t0  # host time to issue the steps (graph replays): < elapsed when GPU-bound
+    torch.cuda.synchronize()
+    t_steps = time.perf_counter() - t0
     # the deferred zero-gradient row steps of the lazily updated tables (FusedAdam lazy rows) are
     # applied inside the timed region: every parameter holds its dense-Adam value when it closes
     trainer.flush_optimizer()
@@ -280,6 +283,9 @@ def main():
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
                                    "ms_per_step_without": round(ms_steps, 4),
+                                   "host_submit_ms_per_step": round(t_submit / args.steps * 1e3, 4),
+                                   "steps_ms_per_step": round(t_steps / args.steps * 1e3, 4),
+                                   "lazy_flush_ms_per_step": round((elapsed - t_steps) / args.steps * 1e3, 4),
                                    "note": "value and ms_per_step include epoch_sampling.ms_per_epoch (the median "
                                            "of three epochs' sampling) / steps_per_epoch per step"},
                 "spmm": spmm, "config1_bprmf_allrecipes": c1, "config3_clussl_foodcom": c3, "config4_10m": c4,
