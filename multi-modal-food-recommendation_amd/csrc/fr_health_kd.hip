@@ -16,15 +16,18 @@
 // 1e-8; maximum's backward halves the gradient on a tie).
 // Loss sums are per-block partials summed by a one-wave finalize launch (fixed-order wave sum);
 // parameter gradients are per-block partials summed in a fixed order by a reduce kernel.
-// Item inputs are loaded one item ahead; every load loop has a compile-time trip count.
+// Forward item inputs are loaded one item ahead; every load loop has a compile-time trip count.
 #include "fr_common.h"
 
 namespace {
 
 constexpr int D = 64;
 constexpr int HMAX = 16;
-constexpr int WAVES = 4;          // waves per block
-constexpr int MAX_BLOCKS = 64;    // grid cap: bounds the parameter-gradient partials
+constexpr int WAVES = 8;          // forward: waves per block (2 per SIMD), up to 128 blocks
+constexpr int BWAVES = 4;         // backward: 4 waves per block (its 64 dW1 accumulators per lane need the
+                                  // full register file), up to 256 blocks
+constexpr int MAX_BLOCKS = 128;   // forward grid cap (1024 items: one per wave)
+constexpr int MAX_BLOCKS_BWD = 256;  // backward grid cap: bounds the parameter-gradient partials
 constexpr int W1S = D + 1;        // padded LDS row stride of W1
 constexpr float kCosEps = 1e-8f;  // cosine_similarity eps
 constexpr int NPART_BWD = D * D + D + HMAX * D + HMAX;  // dW1, db1, dW2 (HMAX rows), db2
@@ -55,8 +58,9 @@ __device__ __forceinline__ float bcast(float v, int lane) {
 
 // W1 (padded), b1, W2, b2 into LDS
 // (compile-time trip counts: every thread's loads are in flight together)
+template <int NW>
 __device__ __forceinline__ void stage_weights(const HeadArgs& a, float* sw1, float* sw2, float* sb) {
-  constexpr int T = 64 * WAVES;
+  constexpr int T = 64 * NW;
   float v1[D * D / T], v2[HMAX * D / T];
 #pragma unroll
   for (int u = 0; u < D * D / T; ++u) v1[u] = a.w1[threadIdx.x + u * T];
@@ -94,12 +98,13 @@ __device__ __forceinline__ ItemIn load_item(const HeadArgs& a, int64_t i, int j)
   return x;
 }
 
-// z1 = W1 h + b1 for lane j (row j of W1), h broadcast by readlane
+// z1 = W1 h + b1 for lane j (row j of W1), h broadcast by readlane; four interleaved partial sums
+// (k mod 4) keep the dependent FMA chain 16 long instead of 64
 __device__ __forceinline__ float layer1(const float* sw1, const float* sb, float h, int j) {
-  float z = 0.f;
+  float z[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < D; ++k) z = fmaf(sw1[j * W1S + k], bcast(h, k), z);
-  return z + sb[j];
+  for (int k = 0; k < D; ++k) z[k & 3] = fmaf(sw1[j * W1S + k], bcast(h, k), z[k & 3]);
+  return ((z[0] + z[1]) + (z[2] + z[3])) + sb[j];
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
@@ -114,7 +119,7 @@ __global__ __launch_bounds__(64 * WAVES) void head_fwd_kernel(HeadArgs a) {
   __shared__ float sw2[HMAX * D];
   __shared__ float sb[D + HMAX];
   __shared__ float red[WAVES][2];
-  stage_weights(a, sw1, sw2, sb);
+  stage_weights<WAVES>(a, sw1, sw2, sb);
   const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
   float sum_bce = 0.f, sum_cos = 0.f;
   const int64_t stride = (int64_t)gridDim.x * WAVES;
@@ -148,12 +153,17 @@ __global__ __launch_bounds__(64 * WAVES) void head_fwd_kernel(HeadArgs a) {
   }
 }
 
-// the loss terms from the <= 64 block partials (lane b: block b), one fixed-order wave sum each
+// the loss terms from the <= 128 block partials (lane j: blocks j, j + 64 in that order), one
+// fixed-order wave sum each
 __global__ __launch_bounds__(64) void head_final_kernel(HeadArgs a, int nblk) {
   const int j = threadIdx.x;
-  const bool has = j < nblk;
-  const float tb = wsum(has ? a.part[2 * j] : 0.f);
-  const float tc = wsum(has ? a.part[2 * j + 1] : 0.f);
+  float sb_ = 0.f, sc = 0.f;
+  for (int b = j; b < nblk; b += 64) {
+    sb_ += a.part[2 * b];
+    sc += a.part[2 * b + 1];
+  }
+  const float tb = wsum(sb_);
+  const float tc = wsum(sc);
   if (j != 0) return;
   const float kd = 1.f - tc / (float)a.n;
   const float x = kd - a.thr;
@@ -162,12 +172,12 @@ __global__ __launch_bounds__(64) void head_final_kernel(HeadArgs a, int nblk) {
   a.out[2] = x;
 }
 
-__global__ __launch_bounds__(64 * WAVES) void head_bwd_kernel(HeadArgs a) {
+__global__ __launch_bounds__(64 * BWAVES) void head_bwd_kernel(HeadArgs a) {
   __shared__ float sw1[D * W1S];
   __shared__ float sw2[HMAX * D];
   __shared__ float sb[D + HMAX];
   __shared__ float comb[D * D + D + HMAX * D + HMAX];
-  stage_weights(a, sw1, sw2, sb);
+  stage_weights<BWAVES>(a, sw1, sw2, sb);
   const int j = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float gh = *a.gh * a.wh;
   // maximum(0, x) backward for x: g where x > 0, g / 2 on a tie, 0 below
@@ -181,11 +191,9 @@ __global__ __launch_bounds__(64 * WAVES) void head_bwd_kernel(HeadArgs a) {
   float gb1 = 0.f, gw2[HMAX], gb2[HMAX];
 #pragma unroll
   for (int t = 0; t < HMAX; ++t) { gw2[t] = 0.f; gb2[t] = 0.f; }
-  const int64_t stride = (int64_t)gridDim.x * WAVES;
-  int64_t i = (int64_t)blockIdx.x * WAVES + w;
-  ItemIn cur = load_item(a, i, j);
-  for (; i < a.n; i += stride) {
-    const ItemIn nxt = load_item(a, i + stride, j);
+  const int64_t stride = (int64_t)gridDim.x * BWAVES;
+  for (int64_t i = (int64_t)blockIdx.x * BWAVES + w; i < a.n; i += stride) {
+    const ItemIn cur = load_item(a, i, j);  // one item per wave at n <= 1024: no prefetch registers
     // health branch
     const float h = cur.h;
     const float z1 = layer1(sw1, sb, h, j);
@@ -226,10 +234,9 @@ __global__ __launch_bounds__(64 * WAVES) void head_bwd_kernel(HeadArgs a) {
     const float c = wsum(kh * rh);
     a.dknow[i * D + j] = dc * (rh - c * kh) / n1;
     a.drows[i * D + j] = dc * (kh - c * rh) / n2;
-    cur = nxt;
   }
   // combine the waves' accumulators in wave order, then one partial per block
-  for (int q = 0; q < WAVES; ++q) {
+  for (int q = 0; q < BWAVES; ++q) {
     if (w == q) {
 #pragma unroll
       for (int k = 0; k < D; ++k) comb[k * D + j] = (q ? comb[k * D + j] : 0.f) + gw1[k];
@@ -251,22 +258,22 @@ __global__ __launch_bounds__(64 * WAVES) void head_bwd_kernel(HeadArgs a) {
 }
 
 // sums the per-block partials into dW1, db1, dW2, db2: 32 outputs x 8 block slices per workgroup,
-// each thread's <= 8 loads in flight (nblk <= 64), slices added in slice order (deterministic)
+// each thread's <= 32 loads in flight (nblk <= 256), slices added in slice order (deterministic)
 __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restrict__ part, int nblk, int H,
                                                           float* __restrict__ dw1, float* __restrict__ db1,
                                                           float* __restrict__ dw2, float* __restrict__ db2) {
   __shared__ float red[8][32];
   const int o = threadIdx.x & 31, sl = threadIdx.x >> 5;
   const int e = blockIdx.x * 32 + o;
-  float v[MAX_BLOCKS / 8];
+  float v[MAX_BLOCKS_BWD / 8];
 #pragma unroll
-  for (int u = 0; u < MAX_BLOCKS / 8; ++u) {
+  for (int u = 0; u < MAX_BLOCKS_BWD / 8; ++u) {
     const int b = sl + 8 * u;
     v[u] = (b < nblk && e < NPART_BWD) ? part[(int64_t)b * NPART_BWD + e] : 0.f;
   }
   float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < MAX_BLOCKS / 8; ++u) s += v[u];
+  for (int u = 0; u < MAX_BLOCKS_BWD / 8; ++u) s += v[u];
   red[sl][o] = s;
   __syncthreads();
   if (sl != 0 || e >= NPART_BWD) return;
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
 }
 
 int blocks_for(int64_t n) { return (int)std::min<int64_t>(fr::ceil_div(n, WAVES), MAX_BLOCKS); }
+int bwd_blocks_for(int64_t n) { return (int)std::min<int64_t>(fr::ceil_div(n, BWAVES), MAX_BLOCKS_BWD); }
 
 int common_args(HeadArgs& a, const float* hin, const float* know, const float* rows, const float* labels, int64_t n,
                 int H, const float* const* mlp, float thr, float wh, float wk, float* out) {
@@ -300,8 +308,7 @@ int common_args(HeadArgs& a, const float* hin, const float* know, const float* r
 
 extern "C" int64_t fr_health_kd_partials(int64_t n_items, int backward) {
   if (n_items <= 0) return 0;
-  const int64_t nb = blocks_for(n_items);
-  return backward ? nb * NPART_BWD : 1 + 2 * nb;  // forward: the ticket word, then 2 floats per block
+  return backward ? bwd_blocks_for(n_items) * NPART_BWD : 1 + 2 * blocks_for(n_items);  // forward: the ticket word, then 2 floats per block
 }
 
 extern "C" int fr_health_kd_fwd(const float* d_hin, const float* d_know, const float* d_rows, const float* d_labels,
@@ -337,8 +344,8 @@ extern "C" int fr_health_kd_bwd(const float* d_hin, const float* d_know, const f
   FR_REQUIRE(partial_floats >= fr_health_kd_partials(n_items, 1), "partial buffer too small");
   a.gh = d_gh; a.gk = d_gk; a.dhin = d_dhin; a.dknow = d_dknow; a.drows = d_drows; a.part = d_partials;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int nb = blocks_for(n_items);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(64 * WAVES), 0, s, a);
+  const int nb = bwd_blocks_for(n_items);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(64 * BWAVES), 0, s, a);
   FR_LAUNCH_CHECK();
   hipLaunchKernelGGL(head_reduce_kernel, dim3(fr::ceil_div(NPART_BWD, 32)), dim3(256), 0, s, d_partials, nb, H,
                      d_dmlp[0], d_dmlp[1], d_dmlp[2], d_dmlp[3]);
