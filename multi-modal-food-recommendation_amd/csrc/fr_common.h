@@ -87,8 +87,19 @@ __device__ __forceinline__ float lane_value(float v, int lane) {
 // sum over the `width` lanes of an aligned lane group (width power of two <= 64), the same value
 // in every lane of the group.  Within a 16-lane DPP row the partners are swapped by VALU data-
 // parallel moves (quad_perm xor 1, xor 2; row_half_mirror; row_mirror) instead of ds_bpermute
-// round trips through the LDS crossbar; rows are combined with readlane in a fixed order.  Every
-// lane of the group must be active.
+// round trips through the LDS crossbar; rows are then combined by gfx950's lane-swap moves:
+// v_permlane16_swap on (v, v) gives every lane of rows 2k / 2k+1 the pair (row 2k, row 2k+1),
+// v_permlane32_swap likewise the two 32-lane halves -- (row0 + row1) + (row2 + row3) in every lane,
+// in a fixed order.  Every lane of the group must be active.
+__device__ __forceinline__ float swap16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // (even row) + (odd row) in both rows
+}
+__device__ __forceinline__ float swap32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // (lanes 0-31) + (lanes 32-63) in both halves
+}
+
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {
   static_assert(WIDTH >= 1 && WIDTH <= 64 && (WIDTH & (WIDTH - 1)) == 0, "power-of-two group <= 64");
@@ -96,12 +107,8 @@ __device__ __forceinline__ float group_sum(float v) {
   if constexpr (WIDTH >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
   if constexpr (WIDTH >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
   if constexpr (WIDTH >= 16) v += dpp_mov<0x140>(v); // row_mirror
-  if constexpr (WIDTH == 32) {
-    const float lo = lane_value(v, 0) + lane_value(v, 16), hi = lane_value(v, 32) + lane_value(v, 48);
-    v = (__lane_id() & 32) ? hi : lo;
-  } else if constexpr (WIDTH == 64) {
-    v = (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
-  }
+  if constexpr (WIDTH >= 32) v = swap16_sum(v);
+  if constexpr (WIDTH == 64) v = swap32_sum(v);
   return v;
 }
 
