@@ -198,7 +198,8 @@ def main():
     triples = args.batch * args.steps * world
     value = triples / (ms_per_step * 1e-3 * args.steps)
 
-    dom_name = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
+    # dominance by median launch x launches: one launch stretched by a host stall does not move it
+    dom_name = max(kern, key=lambda k: kern[k]["median_ms"] * kern[k]["launches"]) if kern else None
     traffic = args.traffic if args.traffic is not None else pmc_traffic(dom_name)
     roofline = None
     if dom_name is not None:

@@ -591,7 +591,15 @@ int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* 
  *               marked rows: no zero fill of the rest of it is needed).
  * fr_rows_mark: mask[ids[k][i] + off[k]] = value (sets / clears a column mask from a row list).
  * fr_rows_mark_zero: the same, and rows ids[k][i] + off[k] of Z ([*, d], stride ldz) set to 0
- *               (the batch rows of an upstream gradient about to be accumulated into).
+ *               (the batch rows of an upstream gradient about to be accumulated into); with
+ *               d_bits, also bit (row & 31) of d_bits[row >> 5] set (value != 0) or cleared.
+ * fr_spmm_sparse_upstream: Y2 = alpha * A X + beta1 * gate(X), d = 64, for an X that is non-zero
+ *               only at the rows whose bit is set in d_bits (ceil(n_rows / 32) words; n_rows <=
+ *               262,144): X is read only there, gate(X) = X at marked rows and 0 elsewhere.  One
+ *               workgroup per 128 rows scans its edge range against the bitmask staged in LDS and
+ *               gathers only the marked columns; every row of Y2 (split at `split`) is written.
+ *               The summation order of a row's hits is run-to-run variable (LDS float atomics):
+ *               the deterministic mode uses fr_spmm_csr_ex with d_col_mask / d_a1_gate instead.
  * ------------------------------------------------------------------------------------------ */
 typedef struct fr_tab {
   const float* lo;
@@ -611,12 +619,16 @@ int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d
                    void* d_workspace, int64_t workspace_bytes, void* stream);
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
-                      void* stream);
+                      uint32_t* d_bits, void* stream);
+int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                            const uint32_t* d_bits, const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2,
+                            float alpha, const fr_tab* A1, float beta1, void* stream);
 
 /* fr_graph_bpr_finish: the tail of HealthRec's fused propagation + BPR backward (engine
  * ops.graph_bpr), after both propagation backwards have written dUe (user_embedding's gradient)
  * and dIe (item_embedding's):
- *   mask[u_b] = mask[U + p_b] = mask[U + n_b] = 0   (clears the column mask; d_mask may be NULL),
+ *   mask[u_b] = mask[U + p_b] = mask[U + n_b] = 0   (clears the column mask; d_mask may be NULL;
+ *     with d_bits, the same rows' bits of that bitmask cleared too),
  *   dUe[u_b] += r_u Ue[u_b], dIe[p_b] += r_p Ie[p_b], dIe[n_b] += r_n Ie[n_b]   (float atomics)
  *     with r_x = g_reg * d_greg[0] / B / ||.||_F of block x (the norms fr_bpr_fwd left in the
  *     workspace): EmbLoss(u_ego, pos_ego, neg_ego)'s gradient, cikm_model.py:273-279;
@@ -625,7 +637,8 @@ int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, fl
 int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t ldue, const float* d_Ie,
                         int64_t ldie, const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B,
                         int d, float g_reg, const float* d_greg, float* d_dUe, float* d_dIe,
-                        float* d_zero, int zero_n, void* d_workspace, int64_t workspace_bytes, void* stream);
+                        float* d_zero, int zero_n, uint32_t* d_bits, void* d_workspace, int64_t workspace_bytes,
+                        void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * fr_feed_batch: one step's batch in one launch.  Replaces TrainDataLoader.__getitem__ x B +

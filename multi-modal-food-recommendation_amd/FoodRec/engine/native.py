@@ -59,10 +59,13 @@ _SIGS = {
                                c_float, POINTER(FrTab), c_float, c_void_p, POINTER(FrRowList), c_void_p, c_void_p,
                                c_int64, c_void_p]),
     "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
-    "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p]),
+    "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p,
+                                  c_void_p]),
+    "fr_spmm_sparse_upstream": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64,
+                                        POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p]),
     "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                    c_void_p, c_int64, c_void_p]),
+                                    c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_bpr_fwd_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                 c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_int64,
                                 c_void_p, c_int64, c_void_p]),

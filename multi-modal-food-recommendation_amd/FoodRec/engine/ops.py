@@ -424,15 +424,40 @@ def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
             ws.numel(), native.stream_of(X)), "fr_spmm_csr_ex")
 
 
-def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = None) -> None:
-    """mask[row] = value at the listed rows; with ``zero`` ([*, d] fp32), those rows of it set to 0."""
-    if zero is None:
+def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = None,
+              bits: torch.Tensor | None = None) -> None:
+    """mask[row] = value at the listed rows; with ``zero`` ([*, d] fp32), those rows of it set to 0;
+    with ``bits`` (int32 words, bit row & 31 of word row >> 5), those bits set / cleared."""
+    if zero is None and bits is None:
         native.check(native.lib().fr_rows_mark(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
                                                native.stream_of(mask)), "fr_rows_mark")
         return
     native.check(native.lib().fr_rows_mark_zero(mask.data_ptr(), ctypes.byref(_rowlist(rows)), int(value),
-                                                zero.data_ptr(), zero.stride(0), zero.shape[1],
+                                                native.ptr(zero), zero.stride(0) if zero is not None else 0,
+                                                zero.shape[1] if zero is not None else 0, native.ptr(bits),
                                                 native.stream_of(mask)), "fr_rows_mark_zero")
+
+
+SPARSE_UPSTREAM_MAX_ROWS = 262144
+
+
+def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, Y2_hi=None, split=0,
+                         alpha=1.0, beta1=0.0, region="spmm_masked"):
+    """fr_spmm_sparse_upstream: Y2 = alpha A X + beta1 gate(X) for an X that is non-zero only at the
+    rows set in ``bits`` (int32 words); X is read only there.  d = 64; float-atomic summation order
+    (non-deterministic mode only)."""
+    native.require_device(X, bits)
+    N = adj.shape[0]
+    if adj.shape[1] != N or X.shape[1] != 64 or X.shape[0] < N or N > SPARSE_UPSTREAM_MAX_ROWS:
+        raise native.EngineError("spmm_sparse_upstream: square adjacency, X [rows, 64], rows <= 262,144")
+    if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32:
+        raise native.EngineError("spmm_sparse_upstream: bits must be int32 with ceil(rows / 32) words")
+    _check_tab("Y2", Y2, Y2_hi, split, N, 64)
+    with profiling.region(region, 0):
+        native.check(native.lib().fr_spmm_sparse_upstream(
+            adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, bits.data_ptr(), X.data_ptr(),
+            X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha), ctypes.byref(_tab(X)), _f(beta1),
+            native.stream_of(X)), "fr_spmm_sparse_upstream")
 
 
 def _adjacent_rows(lo, hi, rows):
@@ -604,11 +629,12 @@ class _GraphBpr(torch.autograd.Function):
 
     @staticmethod
     def _backward_fast(ctx, g_mf, g_emb, g_rows):
-        """Float-atomic path for one UI layer, 7 launches: mark the batch rows in the column mask and
-        zero them in the persistent UI upstream gradient (no full fill: its other rows are never
-        read, the masked backward gates its residual read by the same mask); the BPR scatter (+ the
-        KD rows' gradient) with g_mf read on the device; the masked UI backward (+ split-row fixup)
-        into d user_embedding and the item block of the RI upstream gradient; the RI backward into
+        """Float-atomic path for one UI layer: mark the batch rows in the column mask and its bitmask
+        and zero them in the persistent UI upstream gradient (no full fill: its other rows are never
+        read, the backward gates its residual read by the same mask); the BPR scatter (+ the KD rows'
+        gradient) with g_mf read on the device; the UI backward from those rows only
+        (fr_spmm_sparse_upstream: edge scan against the bitmask, gathers at the marked columns) into
+        d user_embedding and the item block of the RI upstream gradient; the RI backward into
         d item_embedding and d ingre_embedding[:-1]; fr_graph_bpr_finish: unmark, the ego rows'
         EmbLoss gradient, the padding row's zero."""
         user_w, item_w, ui_all, u, p, n, pn = ctx.saved_tensors
@@ -623,8 +649,11 @@ class _GraphBpr(torch.autograd.Function):
         g_rows = g_rows.contiguous()
         dUI = _persistent(ui_adj, ("g_ui", str(dev)), lambda: torch.empty(U + I, 64, device=dev))
         mask = _persistent(ui_adj, ("mask", str(dev)), lambda: torch.zeros(U + I, dtype=torch.uint8, device=dev))
+        sparse = U + I <= SPARSE_UPSTREAM_MAX_ROWS
+        bits = (_persistent(ui_adj, ("bits", str(dev)),
+                            lambda: torch.zeros((U + I + 31) // 32, dtype=torch.int32, device=dev)) if sparse else None)
         rows = [(u, 0), (p, U), (n, U)]
-        rows_mark(mask, rows, 1, zero=dUI)
+        rows_mark(mask, rows, 1, zero=dUI, bits=bits)
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_bpr_bwd_ex(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
                                            item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
@@ -633,7 +662,10 @@ class _GraphBpr(torch.autograd.Function):
                                            ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd_ex")
         d_user = torch.empty_like(user_w)
         G_ri = _persistent(ri_adj, ("g_ri", str(dev)), lambda: torch.zeros(I + NI, 64, device=dev))
-        _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
+        if sparse:
+            spmm_sparse_upstream(ui_adj, bits, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5)
+        else:
+            _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
         d_item = torch.empty_like(item_w)
         d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
         _prop_bwd_split(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
@@ -641,7 +673,8 @@ class _GraphBpr(torch.autograd.Function):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),
                                                  g_emb.data_ptr(), d_user.data_ptr(), d_item.data_ptr(),
-                                                 d_ingre[NI:].data_ptr(), 64, ws.data_ptr(), ws.numel(), s),
+                                                 d_ingre[NI:].data_ptr(), 64, native.ptr(bits), ws.data_ptr(),
+                                                 ws.numel(), s),
                          "fr_graph_bpr_finish")
         return (d_user, d_item, d_ingre) + (None,) * 10
 

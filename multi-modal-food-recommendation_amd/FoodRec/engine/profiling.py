@@ -37,15 +37,18 @@ class KernelTimer:
 
     def summary(self) -> dict:
         torch.cuda.synchronize()
-        agg = defaultdict(lambda: [0, 0.0, 0])
+        agg = defaultdict(lambda: [0, 0.0, 0, []])
         for name, s, e, b in self.records:
             a = agg[name]
+            ms = s.elapsed_time(e)
             a[0] += 1
-            a[1] += s.elapsed_time(e)
+            a[1] += ms
             a[2] += b
-        return {k: {"launches": n, "total_ms": t, "avg_ms": t / n, "bytes_per_launch": b / n,
-                    "gbps": (b / n) / (t / n * 1e-3) / 1e9 if t > 0 else 0.0}
-                for k, (n, t, b) in agg.items()}
+            a[3].append(ms)
+        # median_ms: robust to a launch stretched by a host stall between its events (dominance)
+        return {k: {"launches": n, "total_ms": t, "avg_ms": t / n, "median_ms": sorted(v)[len(v) // 2],
+                    "bytes_per_launch": b / n, "gbps": (b / n) / (t / n * 1e-3) / 1e9 if t > 0 else 0.0}
+                for k, (n, t, b, v) in agg.items()}
 
 
 def active():

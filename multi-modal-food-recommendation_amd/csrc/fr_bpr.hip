@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
     uint8_t* __restrict__ mask, int64_t U, const float* __restrict__ Ue, int64_t ldue,
     const float* __restrict__ Ie, int64_t ldie, const int64_t* __restrict__ uu, const int64_t* __restrict__ pp,
     const int64_t* __restrict__ nn, int64_t B, int d4, float greg, const float* greg_dev, float* dUe,
-    int64_t lddue, float* dIe, int64_t lddie, BprWS ws, float* __restrict__ zero, int zero_n) {
+    int64_t lddue, float* dIe, int64_t lddie, BprWS ws, float* __restrict__ zero, int zero_n,
+    uint32_t* __restrict__ bits) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
   if (greg_dev) greg *= greg_dev[0];
@@ -210,6 +211,11 @@ __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
       mask[u] = 0;
       mask[U + p] = 0;
       mask[U + n] = 0;
+    }
+    if (bits && q0 == 0) {
+      atomicAnd(bits + (u >> 5), ~(1u << (u & 31)));
+      atomicAnd(bits + ((U + p) >> 5), ~(1u << ((U + p) & 31)));
+      atomicAnd(bits + ((U + n) >> 5), ~(1u << ((U + n) & 31)));
     }
     for (int q = q0; q < d4; q += LPR) {
       atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
@@ -530,8 +536,8 @@ extern "C" int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, in
 extern "C" int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t ldue, const float* d_Ie,
                                    int64_t ldie, const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B,
                                    int d, float g_reg, const float* d_greg, float* d_dUe, float* d_dIe,
-                                   float* d_zero, int zero_n, void* d_workspace, int64_t workspace_bytes,
-                                   void* stream) {
+                                   float* d_zero, int zero_n, uint32_t* d_bits, void* d_workspace,
+                                   int64_t workspace_bytes, void* stream) {
   FR_REQUIRE(B >= 1 && d >= 4 && d % 4 == 0 && U >= 0 && zero_n >= 0, "bad sizes");
   FR_REQUIRE(d_Ue && d_Ie && d_u && d_p && d_n && d_dUe && d_dIe && (zero_n == 0 || d_zero), "null argument");
   FR_REQUIRE(fr::aligned16(d_Ue) && fr::aligned16(d_Ie) && fr::aligned16(d_dUe) && fr::aligned16(d_dIe) &&
@@ -542,7 +548,7 @@ extern "C" int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
   hipLaunchKernelGGL(graph_bpr_finish_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_mask,
                      U, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, g_reg, d_greg, d_dUe, ldue, d_dIe, ldie, w,
-                     d_zero, zero_n);
+                     d_zero, zero_n, d_bits);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -260,9 +260,11 @@ __global__ __launch_bounds__(kRowThreads) void spmm_rows_kernel(
   }
 }
 
-// mask[row] = value at the listed rows; with Z, also Z[row][0..d) = 0 (16 lanes x float4 per row)
+// mask[row] = value at the listed rows; with Z, also Z[row][0..d) = 0 (16 lanes x float4 per row);
+// with bits, bit `row` of the bitmask set (value != 0) or cleared
 __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ mask, RowList rl, int64_t total,
-                                                        uint8_t value, float4* __restrict__ Z, int64_t ldz4, int d4) {
+                                                        uint8_t value, float4* __restrict__ Z, int64_t ldz4, int d4,
+                                                        uint32_t* __restrict__ bits) {
   const int per = Z ? 16 : 1;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total * per; i += (int64_t)gridDim.x * 256) {
     int64_t idx = i / per;
@@ -271,8 +273,161 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ ma
     while (idx >= rl.n[seg]) idx -= rl.n[seg++];
     const int64_t row = rl.ids[seg][idx] + rl.off[seg];
     if (q == 0) mask[row] = value;
+    if (q == 0 && bits) {
+      if (value) atomicOr(bits + (row >> 5), 1u << (row & 31));
+      else atomicAnd(bits + (row >> 5), ~(1u << (row & 31)));
+    }
     if (Z)
       for (int c = q; c < d4; c += 16) Z[row * ldz4 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Sparse-upstream mode (fr_spmm_sparse_upstream): Y2 = alpha * A X + beta1 * gate(X) where X is
+// non-zero only at the rows set in a bitmask (the batch rows of a propagation's upstream
+// gradient; the rest of X is never read).  One workgroup per 64 consecutive rows:
+//   * the bitmask is staged in LDS;
+//   * the block's edge range is scanned in coalesced 1024-edge rounds; the edges whose column is
+//     marked ("hits") are compacted in edge order (wave ballots + a prefix over the 16 wave-slices
+//     of the round), so the hit list is sorted by row;
+//   * each 16-lane group (float4 column slot per lane) walks a contiguous slice of the hits,
+//     gathers X at the hit columns (four in flight), sums each row's run in registers and adds it
+//     to the block's LDS row accumulator once per run -- LDS float atomics per run, not per hit
+//     (a per-hit add serialises: consecutive hits share a row);
+//   * every row is written once: alpha * acc + beta1 * X (X read at marked rows only).
+// Work: one column + value load per edge, one 256-B gather per hit.  A row split over group slices
+// or rounds gets several adds in a run-to-run variable order (the deterministic mode keeps the
+// column-masked gather).  d = 64.
+constexpr int kSpRows = 64;
+constexpr int kSpRound = 1024;
+constexpr int kSpMaxWords = 8192;  // bitmask in LDS (dynamic, ceil(n / 32) words): up to 262,144 rows
+
+__global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const float* __restrict__ val, int64_t n_rows,
+                                                          const uint32_t* __restrict__ bits, int nwords,
+                                                          const float4* __restrict__ X, int64_t ldx4, Epi ep) {
+  constexpr int KS = kSpRound / 256;  // edges per thread per round
+  extern __shared__ uint32_t sbits[];
+  __shared__ float4 acc[kSpRows][16];
+  __shared__ int64_t srp[kSpRows + 1];
+  __shared__ int hit_c[kSpRound];    // (edge - round base) << 18 | column (columns < 2^18)
+  __shared__ float hit_v[kSpRound];  // the edge's value
+  __shared__ int cnt[KS * 4];        // hits per (k, wave) slice of the round
+  const int t = threadIdx.x, q = t & 15, lane = t & 63, wave = t >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
+  const int nr = (int)min<int64_t>(kSpRows, n_rows - r0);
+  {  // stage the bitmask: 16-B loads, all in flight before the LDS stores
+    const int n4 = nwords >> 2;
+    const uint4* b4 = reinterpret_cast<const uint4*>(bits);
+#pragma unroll 8
+    for (int w = t; w < n4; w += 256) reinterpret_cast<uint4*>(sbits)[w] = b4[w];
+    if (t < (nwords & 3)) sbits[(n4 << 2) + t] = bits[(n4 << 2) + t];
+  }
+  for (int i = t; i < kSpRows * 16; i += 256) acc[i >> 4][i & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = t; i <= nr; i += 256) srp[i] = rowptr[r0 + i];
+  __syncthreads();
+  const int64_t e0 = srp[0], e1 = srp[nr];
+  for (int64_t base = e0; base < e1; base += kSpRound) {
+    // scan: coalesced column and value loads (edge base + k * 256 + t), hit flags by wave ballot
+    int cs[KS];
+    float vs[KS];
+    uint64_t bal[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int64_t e = base + k * 256 + t;
+      cs[k] = e < e1 ? __builtin_nontemporal_load(col + e) : -1;
+      vs[k] = e < e1 ? __builtin_nontemporal_load(val + e) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int c = cs[k];
+      bal[k] = __ballot(c >= 0 && ((sbits[c >> 5] >> (c & 31)) & 1u));
+      if (lane == 0) cnt[k * 4 + wave] = __popcll(bal[k]);
+    }
+    __syncthreads();
+    // ordered compaction: slice (k, wave) starts after every earlier slice's hits
+    int nh = 0, off[KS];
+#pragma unroll
+    for (int j = 0; j < KS * 4; ++j) {
+      const int cj = cnt[j];
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        if (j == k * 4 + wave) off[k] = nh;
+      nh += cj;
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if ((bal[k] >> lane) & 1ull) {
+        const int slot = off[k] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
+        hit_c[slot] = (k * 256 + t) << 18 | cs[k];
+        hit_v[slot] = vs[k];
+      }
+    }
+    __syncthreads();
+    // accumulate: group g walks hits [g nh / 16, (g + 1) nh / 16) in row order
+    const int g = t >> 4;
+    const int h_lo = (g * nh) >> 4, h_hi = ((g + 1) * nh) >> 4;
+    if (h_lo < h_hi) {
+      int rl = 0;
+      {  // row of the first hit: srp[rl] <= e < srp[rl + 1]
+        const int64_t e = base + (hit_c[h_lo] >> 18);
+        int hi = nr;
+        while (hi - rl > 1) {
+          const int mid = (rl + hi) >> 1;
+          if (srp[mid] <= e) rl = mid; else hi = mid;
+        }
+      }
+      int cur = rl;
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int h0 = h_lo; h0 < h_hi; h0 += 4) {
+        float4 x[4];
+        float v[4];
+        int eo[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int h = min(h0 + j, h_hi - 1);
+          const int hc = hit_c[h];
+          eo[j] = hc >> 18;
+          v[j] = hit_v[h];
+          x[j] = X[(int64_t)(hc & 0x3FFFF) * ldx4 + q];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (h0 + j < h_hi) {
+            const int64_t e = base + eo[j];
+            while (srp[rl + 1] <= e) ++rl;
+            if (rl != cur) {
+              float* a = reinterpret_cast<float*>(&acc[cur][q]);
+              atomicAdd(a + 0, sum.x);
+              atomicAdd(a + 1, sum.y);
+              atomicAdd(a + 2, sum.z);
+              atomicAdd(a + 3, sum.w);
+              sum = make_float4(0.f, 0.f, 0.f, 0.f);
+              cur = rl;
+            }
+            sum = f4_fma(v[j], x[j], sum);
+          }
+        }
+      }
+      float* a = reinterpret_cast<float*>(&acc[cur][q]);
+      atomicAdd(a + 0, sum.x);
+      atomicAdd(a + 1, sum.y);
+      atomicAdd(a + 2, sum.z);
+      atomicAdd(a + 3, sum.w);
+    }
+    __syncthreads();
+  }
+  // write every row: Y2 = alpha * acc + beta1 * A1 (A1 read only at marked rows)
+  for (int i = t; i < nr * 16; i += 256) {
+    const int rl = i >> 4;
+    const int64_t r = r0 + rl;
+    float4 o = f4_scale(ep.alpha, acc[rl][q]);
+    if (ep.A1.lo && ((sbits[r >> 5] >> (r & 31)) & 1u))
+      o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q], o);
+    reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
   }
 }
 
@@ -472,11 +627,11 @@ extern "C" int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, con
 }
 
 extern "C" int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream) {
-  return fr_rows_mark_zero(d_mask, rows, value, nullptr, 0, 0, stream);
+  return fr_rows_mark_zero(d_mask, rows, value, nullptr, 0, 0, nullptr, stream);
 }
 
 extern "C" int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
-                                 void* stream) {
+                                 uint32_t* d_bits, void* stream) {
   FR_REQUIRE(d_mask != nullptr && rows != nullptr, "null argument");
   FR_REQUIRE(!d_Z || (d > 0 && d % 4 == 0 && ldz >= d && ldz % 4 == 0 && fr::aligned16(d_Z)),
              "Z must be 16-B aligned with d % 4 == 0 and ld >= d");
@@ -493,7 +648,29 @@ extern "C" int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_
   const int64_t work = total * (d_Z ? 16 : 1);
   const int64_t blocks = std::min<int64_t>(fr::ceil_div(work, (int64_t)256), (int64_t)fr::kNumCU * 4);
   hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     d_mask, rl, total, value, reinterpret_cast<float4*>(d_Z), ldz / 4, d / 4);
+                     d_mask, rl, total, value, reinterpret_cast<float4*>(d_Z), ldz / 4, d / 4, d_bits);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                       int64_t n_rows, const uint32_t* d_bits, const float* d_X, int64_t ldx,
+                                       int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
+                                       void* stream) {
+  FR_REQUIRE(n_rows >= 0 && n_rows <= (int64_t)kSpMaxWords * 32, "n_rows out of range (<= 262,144)");
+  if (n_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && d_col && d_val && d_bits && d_X && Y2 && Y2->lo, "null operand");
+  FR_REQUIRE(fr::aligned16(d_bits), "bits must be 16-B aligned");
+  FR_REQUIRE(ldx >= 64 && ldx % 4 == 0 && fr::aligned16(d_X) && tab_ok(Y2, 64) && tab_ok(A1, 64),
+             "X / Y2 / A1 must be 16-B aligned fp32 [*, 64] tables");
+  FR_REQUIRE(!(tab_touches(Y2, d_X)), "Y2 must not alias X");
+  Epi ep{Tab{nullptr, 0, nullptr, 0}, host_tab(Y2), alpha, host_tab(A1), beta1, Tab{nullptr, 0, nullptr, 0}, 0.f,
+         split, nullptr};
+  const int nwords = (int)fr::ceil_div(n_rows, 32);
+  hipLaunchKernelGGL(spmm_sparse_kernel, dim3((unsigned)fr::ceil_div(n_rows, kSpRows)), dim3(256),
+                     (size_t)nwords * sizeof(uint32_t),
+                     reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
+                     reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

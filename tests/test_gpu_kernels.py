@@ -485,6 +485,39 @@ def test_spmm_ex_split_rows_mask_bitwise(cuda):
     assert int(mask.sum()) == 0
 
 
+@pytest.mark.parametrize("frac", [0.01, 0.6])
+def test_spmm_sparse_upstream(cuda, frac):
+    """fr_spmm_sparse_upstream against fr_spmm_csr over the zero-filled upstream: X is garbage (NaN)
+    outside the marked rows and never read there; heavy rows span several 1024-edge scan rounds;
+    split output; bitmask set and cleared by fr_rows_mark_zero.  Float-atomic order: fp32 rounding."""
+    from FoodRec.engine import ops
+    n, d, split = 1500, 64, 600
+    r, c = _graph(n, n, 8, heavy=[(3, 1400), (700, 900), (11, 129)], seed=23)
+    adj = _adj(n, r, c, cuda, chunk=128)
+    g = torch.Generator().manual_seed(int(frac * 100))
+    marked = torch.unique(torch.randint(0, n, (max(1, int(frac * n)),), generator=g)).to(cuda)
+    marked = torch.cat([marked, torch.tensor([3, 700, n - 1], device=cuda)])
+    mask = torch.zeros(n, dtype=torch.uint8, device=cuda)
+    bits = torch.zeros((n + 31) // 32, dtype=torch.int32, device=cuda)
+    X = torch.full((n, d), float("nan"), device=cuda)
+    ops.rows_mark(mask, [(marked, 0)], 1, zero=X, bits=bits)
+    keep = mask.bool()
+    X[keep] = torch.randn(int(keep.sum()), d, device=cuda)
+    want = torch.tensor([sum(1 << b for b in range(32) if w * 32 + b < n and bool(keep[w * 32 + b]))
+                         for w in range(bits.numel())], dtype=torch.int64)
+    assert torch.equal(bits.cpu().to(torch.int64) & 0xFFFFFFFF, want)
+    Xz = torch.where(keep.unsqueeze(1), X, torch.zeros_like(X))
+    ref = torch.empty(n, d, device=cuda)
+    ops.spmm_launch(adj, Xz, Y2=ref, alpha=0.5, A1=Xz, beta1=0.5)
+    lo, hi = torch.full((split, d), 7.0, device=cuda), torch.full((n - split, d), 7.0, device=cuda)
+    ops.spmm_sparse_upstream(adj, bits, X, lo, hi, split, alpha=0.5, beta1=0.5)
+    got = torch.cat([lo, hi])
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    ops.rows_mark(mask, [(marked, 0)], 0, bits=bits)
+    assert int(mask.sum()) == 0 and int(bits.abs().sum()) == 0
+
+
 def test_healthrec_graph_bpr_matches_unfused(cuda):
     """ops.graph_bpr (split-table propagation, UI rows of the batch only, masked UI backward,
     gradients written into the parameters' buffers) against the concatenated full propagation +

@@ -1,5 +1,6 @@
-"""Masked UI-backward SpMM of the HealthRec step in isolation: A1 gate on/off, the upstream buffer
-zero-filled or left uninitialised outside the batch rows."""
+"""UI-backward SpMM of the HealthRec step in isolation: the column-masked gather (fr_spmm_csr_ex
+with col_mask + a1_gate) against fr_spmm_sparse_upstream, for no marked rows, uniform batch rows and
+degree-biased positives (items drawn through random training edges, as the sampler's positives are)."""
 import os
 import sys
 R = os.path.join(os.path.dirname(__file__), "..", "..")
@@ -12,33 +13,47 @@ dev = torch.device("cuda:0")
 cfg, data, model = bench.build(dev, 512)
 adj = model.norm_adj_matrix
 U, I = model.n_users, model.n_items
+B = 512
 torch.manual_seed(0)
-u = torch.randint(0, U, (512,), device=dev)
-p = torch.randint(0, I, (512,), device=dev)
-n = torch.randint(0, I, (512,), device=dev)
-rows = [(u, 0), (p, U), (n, U)]
-mask = torch.zeros(U + I, dtype=torch.uint8, device=dev)
-ops.rows_mark(mask, rows, 1)
-d_user = torch.empty(U, 64, device=dev)
-G_ri = torch.zeros(I + 20000, 64, device=dev)
-for init in ("zeros", "garbage", "nan"):
-    G = torch.zeros(U + I, 64, device=dev) if init == "zeros" else \
-        torch.full((U + I, 64), float("nan") if init == "nan" else 1e-39, device=dev)
-    G[u] = torch.randn(512, 64, device=dev)
-    G[U + p] = torch.randn(512, 64, device=dev)
-    G[U + n] = torch.randn(512, 64, device=dev)
-    for gate in (False, True):
-        if init != "zeros" and not gate:
-            continue
-        f = lambda: ops.spmm_ex(adj, G, Y2=d_user, Y2_hi=G_ri, split=U, alpha=0.5, A1=G, beta1=0.5, col_mask=mask,
-                                a1_gate=mask if gate else None, nbytes=0)
-        for _ in range(5):
-            f()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(50):
-            f()
-        e.record()
-        torch.cuda.synchronize()
-        print(f"init={init:8s} gate={gate}: {s.elapsed_time(e) / 50 * 1e3:.1f} us   nan_out={bool(torch.isnan(d_user).any())}")
+rp = adj.rowptr
+user_edges = int(rp[U])
+
+
+def timed(f, reps=50):
+    for _ in range(5):
+        f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+for case in ("none", "uniform", "biased"):
+    u = torch.randint(0, U, (B,), device=dev)
+    if case == "biased":
+        ed = torch.randint(0, user_edges, (B,), device=dev)
+        p = adj.col[ed].long() - U
+    else:
+        p = torch.randint(0, I, (B,), device=dev)
+    n = torch.randint(0, I, (B,), device=dev)
+    rows = [(u, 0), (p, U), (n, U)] if case != "none" else [(u[:0], 0)]
+    mask = torch.zeros(U + I, dtype=torch.uint8, device=dev)
+    bits = torch.zeros((U + I + 31) // 32, dtype=torch.int32, device=dev)
+    G = torch.zeros(U + I, 64, device=dev)
+    ops.rows_mark(mask, rows, 1, zero=G, bits=bits)
+    keep = mask.bool()
+    G[keep] = torch.randn(int(keep.sum()), 64, device=dev)
+    hits = int(keep[adj.col.long()].sum())
+    d_user = torch.empty(U, 64, device=dev)
+    G_ri = torch.zeros(I + 20000, 64, device=dev)
+    t_mask = timed(lambda: ops.spmm_ex(adj, G, Y2=d_user, Y2_hi=G_ri, split=U, alpha=0.5, A1=G, beta1=0.5,
+                                       col_mask=mask, a1_gate=mask, nbytes=0))
+    ref = torch.cat([d_user, G_ri[:I]]).clone()
+    t_sp = timed(lambda: ops.spmm_sparse_upstream(adj, bits, G, d_user, G_ri, U, alpha=0.5, beta1=0.5))
+    err = float((torch.cat([d_user, G_ri[:I]]) - ref).abs().max())
+    print(f"{case:8s} marked={int(keep.sum()):5d} hits={hits:7d} of {adj.nnz}: masked gather {t_mask:6.1f} us, "
+          f"sparse upstream {t_sp:6.1f} us  (max diff {err:.2e})")
