@@ -370,6 +370,20 @@ int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, float* const
                                 const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
                                 const int64_t* d_ids, int64_t n, int32_t hist_cap, double beta1, double beta2,
                                 double eps, double weight_decay, void* stream);
+/* Diagnostic: n random operand sets through the replay kernels' rounding shortcuts, on the device,
+ * against the compiler's IEEE fp32 division and sqrt.  d_bad (3 device counters, accumulated):
+ * in-range division mismatches, in-range sqrt mismatches, full-range sqrt_rn mismatches. */
+int fr_adam_rounding_selftest(int64_t n, uint64_t seed, unsigned long long* d_bad, void* stream);
+
+/* Background slice of a flush (no reference counterpart: the reference's torch.optim.Adam updates
+ * every row every step, common/trainer.py:143-144,224).  At device step counter st, rows
+ * [R s / K, R (s + 1) / K), s = st % n_slices, of every table replay their deferred zero-gradient
+ * steps through st; rows already current skip.  One launch per step bounds every row's backlog by
+ * n_slices steps; bit-identical to the dense update like every lazy-row replay. */
+int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
+                           const int64_t* const* d_steps, const int64_t* rows, const int32_t* row_dims,
+                           int32_t* const* d_last, const float* const* d_hist, int32_t n_slices, int32_t hist_cap,
+                           double beta1, double beta2, double eps, double weight_decay, void* stream);
 
 /* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
  * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as

@@ -418,8 +418,10 @@ class Trainer(AbstractTrainer):
         if name == "adam":
             if self._on_gpu():
                 lazy = self.config["lazy_row_adam"]
+                slices = self.config["lazy_row_slices"]
                 return FusedAdam(params, lr=self.learning_rate, weight_decay=self.weight_decay,
-                                 lazy_rows=True if lazy is None else bool(lazy))
+                                 lazy_rows=True if lazy is None else bool(lazy),
+                                 lazy_slices=0 if slices is None else int(slices))
             return optim.Adam(params, lr=self.learning_rate, weight_decay=self.weight_decay)
         if name == "sgd":
             return optim.SGD(params, lr=self.learning_rate, weight_decay=self.weight_decay)

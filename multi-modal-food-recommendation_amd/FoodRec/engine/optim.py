@@ -46,6 +46,8 @@ class RowGrads:
         # gathered Linear input (ops.modal_projection), materialised by FusedAdam before any update
         self.factored = {}
         self.catch_up = None  # set by a FusedAdam with lazy_rows
+        self.catch_up_slice = None  # set by a FusedAdam with lazy_rows and lazy_slices > 0
+        self._bg_join = None  # joins the background slice replay into the main stream
         # (weight, ids) pairs caught up by prefetch_rows this step.  The ids tensors are held here, so
         # their memory cannot be handed to another tensor by the caching allocator before clear():
         # a (weight, pointer, numel) match below therefore names the same ids
@@ -70,6 +72,7 @@ class RowGrads:
             e[3].append(G)
 
     def clear(self):
+        self.join_background()
         self.pending.clear()
         self.factored.clear()
         self._prefetched.clear()
@@ -104,7 +107,22 @@ class RowGrads:
                 for w, ids in pairs:
                     self.catch_up(w, ids)
             self._prefetched.extend(pairs)
-        return lambda: main.wait_stream(side)
+            caught = torch.cuda.Event()
+            caught.record(side)
+            if self.catch_up_slice is not None and self._bg_join is None:
+                # then one row slice of the lazily updated tables replays its backlog behind the
+                # catch-up (the batch's rows are current by then and skip), overlapping the rest of
+                # the step; joined before the optimiser touches any lazy state (join_background)
+                self.catch_up_slice([w for w, _ in pairs])
+                self._bg_join = lambda: main.wait_stream(side)
+        return lambda: main.wait_event(caught)
+
+    def join_background(self):
+        """Make the current stream wait for the background slice replay (before any optimiser
+        kernel reads or advances the lazy step counters / history)."""
+        if self._bg_join is not None:
+            j, self._bg_join = self._bg_join, None
+            j()
 
     def __bool__(self):
         return bool(self.pending or self.factored)
@@ -126,7 +144,7 @@ def _row_grad_ok(p, ids, G) -> bool:
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, lazy_rows=False,
-                 hist_cap=8192):
+                 hist_cap=8192, lazy_slices=0):
         if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError("invalid Adam hyper-parameters")
         if hist_cap < 4:
@@ -142,8 +160,13 @@ class FusedAdam(torch.optim.Optimizer):
         self.hist_cap = int(hist_cap)
         self._lazy_pending = 0
         self._lazy_launched = False
+        self.lazy_slices = int(lazy_slices)
+        if self.lazy_slices < 0:
+            raise ValueError("lazy_slices < 0")
         if self.lazy_rows:
             self.row_grads.catch_up = self.catch_up_rows
+            if self.lazy_slices:
+                self.row_grads.catch_up_slice = self.catch_up_slice
 
     @torch.no_grad()
     def catch_up_rows_multi(self, ps, ids):
@@ -175,6 +198,33 @@ class FusedAdam(torch.optim.Optimizer):
                 "fr_adam_catch_up_rows_multi")
 
     @torch.no_grad()
+    def catch_up_slice(self, ps):
+        """One background slice (fr_adam_catch_up_slice): rows [R s / K, R (s + 1) / K) of the lazily
+        updated tables ``ps``, s = device step counter mod K = ``lazy_slices``, replay their backlog
+        through the current step.  Tables without lazy state are skipped."""
+        ps = [p for p in ps if "lazy_last" in self.state.get(p, {})]
+        groups = {id(p): g for g in self.param_groups for p in g["params"]}
+        by_group = {}
+        for p in ps:
+            by_group.setdefault(id(groups[id(p)]), (groups[id(p)], []))[1].append(p)
+        for group, tabs in by_group.values():
+            beta1, beta2 = group["betas"]
+            for k in range(0, len(tabs), 4):
+                chunk = tabs[k:k + 4]
+                n = len(chunk)
+                st = [self.state[p] for p in chunk]
+                arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+                rows = sum(-(-p.shape[0] // self.lazy_slices) * p.shape[1] for p in chunk)
+                with profiling.region("adam_rows_slice", 24 * rows):
+                    native.check(native.lib().fr_adam_catch_up_slice(
+                        n, arr(chunk), arr([s_["exp_avg"] for s_ in st]), arr([s_["exp_avg_sq"] for s_ in st]),
+                        arr([s_["step"] for s_ in st]), (ctypes.c_int64 * n)(*[p.shape[0] for p in chunk]),
+                        (ctypes.c_int32 * n)(*[p.shape[1] for p in chunk]), arr([s_["lazy_last"] for s_ in st]),
+                        arr([s_["lazy_hist"] for s_ in st]), self.lazy_slices, self.hist_cap, float(beta1),
+                        float(beta2), float(group["eps"]), float(group["weight_decay"]),
+                        native.stream_of(chunk[0])), "fr_adam_catch_up_slice")
+
+    @torch.no_grad()
     def catch_up_rows(self, p, ids):
         """Rows ``ids`` of a lazily updated table replay their deferred steps (fr_adam_catch_up_rows)
         so a gather reads dense-Adam values.  No-op for tables without lazy state."""
@@ -198,6 +248,7 @@ class FusedAdam(torch.optim.Optimizer):
         """Bring every lazily updated table (and its moments) up to the current step.  Call before
         reading those tables in full (evaluation, checkpoints, comparisons); cheap when nothing is
         pending."""
+        self.row_grads.join_background()
         if self._lazy_pending == 0:
             return
         for group in self.param_groups:
@@ -312,6 +363,7 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = native.lib()
+        self.row_grads.join_background()
         # factored row gradients read the projection weights: materialise them before any update
         prepared = self._prepare_factored(lib) if (self.row_grads.factored and part != "dense") else {}
         for gi, group in enumerate(self.param_groups):

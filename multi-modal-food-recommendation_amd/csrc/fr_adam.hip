@@ -290,7 +290,37 @@ constexpr int kHist = 4;
 // smallest subnormal, so the quotient is a normal number).  One double reciprocal per step, shared
 // by all of a lane's elements; the elementwise products and sums on packed-fp32 ops.
 typedef float pf2 __attribute__((ext_vector_type(2)));
+constexpr int KC = 2;  // float4 chunks of a row a lane replays together (replay_row)
 
+// Correctly rounded a / b without the range handling of the general expansion: the compiler's fp32
+// division is v_div_scale (x2), v_rcp, the Newton / Markstein fma chain, v_div_fmas, v_div_fixup;
+// for |a| in {0} U [2^-40, 2^40] and b in [2^-40, 2^40] the scale steps are the identity (no
+// exponent gap >= 96, no denormal operand or result) and the fix-up passes the value through, so the
+// fma chain alone returns the same bits.  Callers guarantee the range (replay_row's row check).
+__device__ __forceinline__ float div_rn_inrange(float a, float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float e = fmaf(-b, y0, 1.0f);
+  const float y1 = fmaf(e, y0, y0);
+  const float q0 = a * y1;
+  const float r0 = fmaf(-b, q0, a);
+  const float q1 = fmaf(r0, y1, q0);
+  const float r1 = fmaf(-b, q1, a);
+  return fmaf(r1, y1, q1);
+}
+
+// Correctly rounded sqrt for x in {0} U [2^-96, inf): v_sqrt_f32 (1 ulp) + the residual selection of
+// sqrt_rn without its small-input scaling
+__device__ __forceinline__ float sqrt_rn_inrange(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float s_dn = __int_as_float(__float_as_int(s) - 1);
+  const float s_up = __int_as_float(__float_as_int(s) + 1);
+  const float r_dn = fmaf(-s_dn, s, x);
+  const float r_up = fmaf(-s_up, s, x);
+  s = (r_dn <= 0.f) ? s_dn : s;
+  return (r_up > 0.f) ? s_up : s;
+}
+
+template <bool INRANGE>
 __device__ __forceinline__ void zero_step2(float& p0, float& p1, float& m0, float& m1, float& v0, float& v1, float ns,
                                            double rc, const AdamHyper& h) {
 #pragma clang fp contract(off)
@@ -298,63 +328,146 @@ __device__ __forceinline__ void zero_step2(float& p0, float& p1, float& m0, floa
   const pf2 w1 = {h.w1, h.w1}, b2 = {h.beta2, h.beta2};
   m = __builtin_elementwise_fma(w1, -m, m);
   v = v * b2;
-  const float q0 = (float)((double)sqrt_rn(v.x) * rc), q1 = (float)((double)sqrt_rn(v.y) * rc);
+  const float r0 = INRANGE ? sqrt_rn_inrange(v.x) : sqrt_rn(v.x), r1 = INRANGE ? sqrt_rn_inrange(v.y) : sqrt_rn(v.y);
+  const float q0 = (float)((double)r0 * rc), q1 = (float)((double)r1 * rc);
   const pf2 den = pf2{q0, q1} + pf2{h.eps, h.eps};
   const pf2 u = pf2{ns, ns} * m;
-  const pf2 p = pf2{p0, p1} + pf2{__fdiv_rn(u.x, den.x), __fdiv_rn(u.y, den.y)};
+  const pf2 d = INRANGE ? pf2{div_rn_inrange(u.x, den.x), div_rn_inrange(u.y, den.y)}
+                        : pf2{__fdiv_rn(u.x, den.x), __fdiv_rn(u.y, den.y)};
+  const pf2 p = pf2{p0, p1} + d;
   p0 = p.x; p1 = p.y; m0 = m.x; m1 = m.y; v0 = v.x; v1 = v.y;
 }
 
-// steps [s0, s1) with g = 0 on one float4 of a row
-__device__ __forceinline__ void zero_steps4(float4& p, float4& m, float4& v, const float* __restrict__ hist, int cap,
-                                            int64_t s0, int64_t s1, const AdamHyper& h) {
-  if (h.wd != 0.f) {  // weight decay makes g' = wd p nonzero: the general element step
-    AdamHyper hs = h;
-    for (int64_t s = s0; s < s1; ++s) {
-      const float* e = hist + kHist * (s % cap);
-      hs.neg_step = e[0];
-      hs.bc2_sqrt = e[1];
-      adam_elem(p.x, 0.f, m.x, v.x, hs);
-      adam_elem(p.y, 0.f, m.y, v.y, hs);
-      adam_elem(p.z, 0.f, m.z, v.z, hs);
-      adam_elem(p.w, 0.f, m.w, v.w, hs);
-    }
-    return;
-  }
+// Zero steps [s0, s1) on KC float4 chunks of a lane (ring index of s0 = i0)
+template <bool INRANGE>
+__device__ __forceinline__ void zero_steps(float4 (&p)[KC], float4 (&m)[KC], float4 (&v)[KC],
+                                           const float* __restrict__ hist, int cap, int i0, int64_t s0, int64_t s1,
+                                           const AdamHyper& h) {
+  int idx = i0;
   for (int64_t s = s0; s < s1; ++s) {
-    const float* e = hist + kHist * (s % cap);
+    const float* e = hist + kHist * idx;
     const float ns = e[0];
     const double rc = *reinterpret_cast<const double*>(e + 2);
-    zero_step2(p.x, p.y, m.x, m.y, v.x, v.y, ns, rc, h);
-    zero_step2(p.z, p.w, m.z, m.w, v.z, v.w, ns, rc, h);
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      zero_step2<INRANGE>(p[c].x, p[c].y, m[c].x, m[c].y, v[c].x, v[c].y, ns, rc, h);
+      zero_step2<INRANGE>(p[c].z, p[c].w, m[c].z, m[c].w, v[c].z, v[c].w, ns, rc, h);
+    }
+    if (++idx == cap) idx = 0;
   }
 }
 
+// Range bounds for the in-range sqrt / division forms over zero steps [s0, s1) (wave-uniform, once
+// per row): m and v only decay over zero steps (|m| by 1 - w1, v by beta2 per step, each rounding
+// within 2^-24 relative), so with m_keep / v_keep = half the decay over n steps, bounds at the start
+// cover every step; |neg_step| by the replayed entries' min / max, 1 / bc2_sqrt by their max.
+struct ReplayRange {
+  float ns_lo, ns_hi, m_keep, v_keep;
+  bool ok;
+};
+
+__device__ __forceinline__ ReplayRange replay_range(const float* __restrict__ hist, int cap, int i0, int64_t s0,
+                                                    int64_t s1, const AdamHyper& h) {
+  ReplayRange r{INFINITY, 0.f, 0.f, 0.f, false};
+  double rc_hi = 0.0;
+  int idx = i0;
+  for (int64_t s = s0; s < s1; ++s) {
+    const float* e = hist + kHist * idx;
+    r.ns_lo = fminf(r.ns_lo, fabsf(e[0]));
+    r.ns_hi = fmaxf(r.ns_hi, fabsf(e[0]));
+    rc_hi = fmax(rc_hi, *reinterpret_cast<const double*>(e + 2));
+    if (++idx == cap) idx = 0;
+  }
+  const float n = (float)(s1 - s0);
+  r.m_keep = 0.5f * __builtin_amdgcn_exp2f(n * __builtin_amdgcn_logf(1.0f - h.w1));
+  r.v_keep = 0.5f * __builtin_amdgcn_exp2f(n * __builtin_amdgcn_logf(h.beta2));
+  r.ok = h.eps >= 0x1p-40f && h.eps <= 1.0f && rc_hi <= 0x1p+10 && r.ns_hi <= 0x1p+10f && r.m_keep > 0.f &&
+         r.v_keep > 0.f;
+  return r;
+}
+
+// Wave-uniform: do these chunks keep u = neg_step * m in {0} U [2^-40, 2^40], v in {0} U [2^-96, 2^50]
+// (so den = sqrt(v) / bc2_sqrt + eps lies in [2^-40, 2^40]) at every replayed step?
+__device__ __forceinline__ bool chunks_in_range(const float4 (&m)[KC], const float4 (&v)[KC], const ReplayRange& r) {
+  bool ok = r.ok;
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const float mm[4] = {m[c].x, m[c].y, m[c].z, m[c].w}, vv[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float am = fabsf(mm[k]);
+      ok &= (am == 0.f) | ((am * r.m_keep * r.ns_lo >= 0x1p-40f) & (am * r.ns_hi <= 0x1p+30f));
+      ok &= ((vv[k] == 0.f) | (vv[k] * r.v_keep >= 0x1p-96f)) & (vv[k] <= 0x1p+50f);
+    }
+  }
+  return __all(ok);
+}
+
 // one row of `width` floats at P / M / V, lane-strided float4 chunks: zero steps [s0, s1), then (G
-// non-null) step `st` with gradient row G
+// non-null) step `st` with gradient row G.  Steps run in the outer loop over up to KC of the lane's
+// chunks held in registers, so a step's history entry is read once per KC chunks; its ring index
+// advances by one per step (no division), and s0 / s1 are wave-uniform (scalar loop).
+
 __device__ __forceinline__ void replay_row(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
                                            const float* __restrict__ G, int width, int lane,
                                            const float* __restrict__ hist, int cap, int64_t s0, int64_t s1,
                                            int64_t st, const AdamHyper& h) {
-  for (int q = 4 * lane; q < width; q += 4 * 64) {
-    float4 p = *reinterpret_cast<const float4*>(P + q);
-    float4 m = *reinterpret_cast<const float4*>(M + q);
-    float4 v = *reinterpret_cast<const float4*>(V + q);
-    zero_steps4(p, m, v, hist, cap, s0, s1, h);
-    if (G) {
-      AdamHyper hs = h;
-      const float* e = hist + kHist * (st % cap);
-      hs.neg_step = e[0];
-      hs.bc2_sqrt = e[1];
-      const float4 g = *reinterpret_cast<const float4*>(G + q);
-      adam_elem(p.x, g.x, m.x, v.x, hs);
-      adam_elem(p.y, g.y, m.y, v.y, hs);
-      adam_elem(p.z, g.z, m.z, v.z, hs);
-      adam_elem(p.w, g.w, m.w, v.w, hs);
+  s0 = __builtin_amdgcn_readfirstlane((int)s0);  // step indices fit in int32 (the last[] entries do)
+  s1 = __builtin_amdgcn_readfirstlane((int)s1);
+  const int i0 = s0 < s1 ? (int)(s0 % cap) : 0;
+  const ReplayRange rr = (s0 < s1 && h.wd == 0.f) ? replay_range(hist, cap, i0, s0, s1, h) : ReplayRange{};
+  for (int q0 = 4 * lane; q0 < width; q0 += 4 * 64 * KC) {
+    float4 p[KC], m[KC], v[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int q = q0 + 4 * 64 * c;
+      if (q < width) {
+        p[c] = *reinterpret_cast<const float4*>(P + q);
+        m[c] = *reinterpret_cast<const float4*>(M + q);
+        v[c] = *reinterpret_cast<const float4*>(V + q);
+      } else {
+        p[c] = m[c] = v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
-    *reinterpret_cast<float4*>(P + q) = p;
-    *reinterpret_cast<float4*>(M + q) = m;
-    *reinterpret_cast<float4*>(V + q) = v;
+    if (h.wd != 0.f) {  // weight decay makes g' = wd p nonzero: the general element step
+      AdamHyper hs = h;
+      int idx = i0;
+      for (int64_t s = s0; s < s1; ++s) {
+        const float* e = hist + kHist * idx;
+        hs.neg_step = e[0];
+        hs.bc2_sqrt = e[1];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          adam_elem(p[c].x, 0.f, m[c].x, v[c].x, hs);
+          adam_elem(p[c].y, 0.f, m[c].y, v[c].y, hs);
+          adam_elem(p[c].z, 0.f, m[c].z, v[c].z, hs);
+          adam_elem(p[c].w, 0.f, m[c].w, v[c].w, hs);
+        }
+        if (++idx == cap) idx = 0;
+      }
+    } else if (s0 < s1) {
+      if (chunks_in_range(m, v, rr)) zero_steps<true>(p, m, v, hist, cap, i0, s0, s1, h);
+      else zero_steps<false>(p, m, v, hist, cap, i0, s0, s1, h);
+    }
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int q = q0 + 4 * 64 * c;
+      if (q >= width) continue;
+      if (G) {
+        AdamHyper hs = h;
+        const float* e = hist + kHist * (int)(st % cap);
+        hs.neg_step = e[0];
+        hs.bc2_sqrt = e[1];
+        const float4 g = *reinterpret_cast<const float4*>(G + q);
+        adam_elem(p[c].x, g.x, m[c].x, v[c].x, hs);
+        adam_elem(p[c].y, g.y, m[c].y, v[c].y, hs);
+        adam_elem(p[c].z, g.z, m[c].z, v[c].z, hs);
+        adam_elem(p[c].w, g.w, m[c].w, v[c].w, hs);
+      }
+      *reinterpret_cast<float4*>(P + q) = p[c];
+      *reinterpret_cast<float4*>(M + q) = m[c];
+      *reinterpret_cast<float4*>(V + q) = v[c];
+    }
   }
 }
 
@@ -439,14 +552,38 @@ __global__ __launch_bounds__(256) void adam_catch_up_kernel(float* __restrict__ 
   catch_up_row(P0, M0, V0, step, ids, i, R, rshift, last, hist, cap, h);
 }
 
+__device__ __forceinline__ void catch_up_at(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
+                                            int64_t st, int64_t r, int rshift, int32_t* last,
+                                            const float* __restrict__ hist, int cap, const AdamHyper& h);
+
 __device__ __forceinline__ void catch_up_row(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
                                              const int64_t* step, const int64_t* __restrict__ ids, int64_t i,
                                              int64_t R, int rshift, int32_t* last, const float* __restrict__ hist,
                                              int cap, const AdamHyper& h) {
-  const int lane = threadIdx.x & 63;
   const int64_t r = ids[i];
   if (r < 0 || r >= R) return;
-  const int64_t st = step[0];
+  catch_up_at(P0, M0, V0, step[0], r, rshift, last, hist, cap, h);
+}
+
+// Background slice of a flush: at step counter st, rows [R s / K, R (s + 1) / K) of every table
+// with s = st % K replay their deferred steps through st (the rows the step's own catch-up already
+// claimed are current and skip).  Issued once per step, it bounds every row's backlog by K steps,
+// so the flush that a full-table read needs costs K / 2 steps per row instead of the whole run's;
+// the work is the same replay the flush would do, moved to a stream that overlaps the step.
+__global__ __launch_bounds__(256) void adam_catch_up_slice_kernel(CatchArgs a, int nslices, int cap, AdamHyper h) {
+  const int t = blockIdx.y;
+  const int64_t st = a.step[t][0], R = a.rows[t];
+  const int64_t s = st % nslices;
+  const int64_t lo = R * s / nslices, hi = R * (s + 1) / nslices;
+  const int64_t r = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= hi) return;
+  catch_up_at(a.p[t], a.m[t], a.v[t], st, r, a.rshift[t], a.last[t], a.hist[t], cap, h);
+}
+
+__device__ __forceinline__ void catch_up_at(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
+                                            int64_t st, int64_t r, int rshift, int32_t* last,
+                                            const float* __restrict__ hist, int cap, const AdamHyper& h) {
+  const int lane = threadIdx.x & 63;
   int32_t old = 0;
   if (lane == 0) old = atomicMax(last + r, (int32_t)st);
   old = __shfl(old, 0, 64);
@@ -724,19 +861,14 @@ extern "C" int fr_adam_catch_up_rows(float* param, float* exp_avg, float* exp_av
   return FR_OK;
 }
 
-extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, float* const* exp_avg,
-                                           float* const* exp_avg_sq, const int64_t* const* d_steps,
-                                           const int64_t* rows, const int32_t* row_dims, int32_t* const* d_last,
-                                           const float* const* d_hist, const int64_t* d_ids, int64_t n,
-                                           int32_t hist_cap, double beta1, double beta2, double eps,
-                                           double weight_decay, void* stream) {
-  FR_REQUIRE(n_tables >= 0 && n_tables <= kMaxCatch, "n_tables out of range [0, 4]");
-  FR_REQUIRE(n >= 0, "negative size");
-  if (n == 0 || n_tables == 0) return FR_OK;
-  FR_REQUIRE(params && exp_avg && exp_avg_sq && d_steps && rows && row_dims && d_last && d_hist && d_ids,
-             "null pointer");
+// CatchArgs + hyper-parameters of a multi-table catch-up launch (tables of one parameter group)
+static int catch_args(int n_tables, float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
+                      const int64_t* const* d_steps, const int64_t* rows, const int32_t* row_dims,
+                      int32_t* const* d_last, const float* const* d_hist, int32_t hist_cap, double beta1,
+                      double beta2, double eps, double weight_decay, CatchArgs& a, AdamHyper& h) {
+  FR_REQUIRE(params && exp_avg && exp_avg_sq && d_steps && rows && row_dims && d_last && d_hist, "null pointer");
   FR_REQUIRE(hist_cap >= 2, "hist_cap < 2");
-  CatchArgs a{};
+  a = CatchArgs{};
   for (int t = 0; t < n_tables; ++t) {
     FR_REQUIRE(params[t] && exp_avg[t] && exp_avg_sq[t] && d_steps[t] && d_last[t] && d_hist[t], "null tensor");
     FR_REQUIRE(row_dims[t] >= 4 && (row_dims[t] & (row_dims[t] - 1)) == 0, "row width must be a power of two >= 4");
@@ -754,7 +886,7 @@ extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, f
     while ((1 << sh) < row_dims[t]) ++sh;
     a.rshift[t] = sh;
   }
-  AdamHyper h{};
+  h = AdamHyper{};
   h.beta1_d = beta1;
   h.beta2_d = beta2;
   h.w1 = (float)(1.0 - beta1);
@@ -762,9 +894,98 @@ extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, f
   h.one_m_b2 = (float)(1.0 - beta2);
   h.eps = (float)eps;
   h.wd = (float)weight_decay;
+  return FR_OK;
+}
+
+extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, float* const* exp_avg,
+                                           float* const* exp_avg_sq, const int64_t* const* d_steps,
+                                           const int64_t* rows, const int32_t* row_dims, int32_t* const* d_last,
+                                           const float* const* d_hist, const int64_t* d_ids, int64_t n,
+                                           int32_t hist_cap, double beta1, double beta2, double eps,
+                                           double weight_decay, void* stream) {
+  FR_REQUIRE(n_tables >= 0 && n_tables <= kMaxCatch, "n_tables out of range [0, 4]");
+  FR_REQUIRE(n >= 0, "negative size");
+  if (n == 0 || n_tables == 0) return FR_OK;
+  FR_REQUIRE(d_ids, "null ids");
+  CatchArgs a;
+  AdamHyper h;
+  const int rc = catch_args(n_tables, params, exp_avg, exp_avg_sq, d_steps, rows, row_dims, d_last, d_hist, hist_cap,
+                            beta1, beta2, eps, weight_decay, a, h);
+  if (rc != FR_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(adam_catch_up_multi_kernel, dim3((unsigned)fr::ceil_div(n, 4), (unsigned)n_tables), dim3(256), 0,
                      s, a, d_ids, n, hist_cap, h);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp_avg,
+                                      float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
+                                      const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
+                                      int32_t n_slices, int32_t hist_cap, double beta1, double beta2, double eps,
+                                      double weight_decay, void* stream) {
+  FR_REQUIRE(n_tables >= 0 && n_tables <= kMaxCatch, "n_tables out of range [0, 4]");
+  FR_REQUIRE(n_slices >= 1, "n_slices < 1");
+  if (n_tables == 0) return FR_OK;
+  CatchArgs a;
+  AdamHyper h;
+  const int rc = catch_args(n_tables, params, exp_avg, exp_avg_sq, d_steps, rows, row_dims, d_last, d_hist, hist_cap,
+                            beta1, beta2, eps, weight_decay, a, h);
+  if (rc != FR_OK) return rc;
+  int64_t most = 0;
+  for (int t = 0; t < n_tables; ++t) most = std::max<int64_t>(most, fr::ceil_div(rows[t], (int64_t)n_slices));
+  if (most == 0) return FR_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_catch_up_slice_kernel, dim3((unsigned)fr::ceil_div(most, 4), (unsigned)n_tables), dim3(256),
+                     0, s, a, n_slices, hist_cap, h);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+// ---- self-test of the rounding shortcuts (diagnostic; tests/test_rowgrad_gpu.py) ---------------
+namespace {
+__device__ __forceinline__ uint32_t st_hash(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+// reference sqrt: the correctly rounded double root rounded to fp32 (double rounding is innocuous
+// for sqrt from 53 >= 2 * 24 + 2 bits)
+__device__ __forceinline__ float st_ref_sqrt(float x) { return (float)__dsqrt_rn((double)x); }
+
+// a float with random significand and exponent uniform in [e_lo, e_hi] (both inclusive, unbiased
+// exponents), random sign if sgn
+__device__ __forceinline__ float st_rand(uint64_t key, int e_lo, int e_hi, bool sgn) {
+  const uint32_t h = st_hash(key);
+  const int e = e_lo + (int)(st_hash(key ^ 0x5851F42D4C957F2Dull) % (uint32_t)(e_hi - e_lo + 1));
+  const uint32_t bits = ((uint32_t)(e + 127) << 23) | (h & 0x7FFFFFu) | (sgn ? (h & 0x80000000u) : 0u);
+  return __uint_as_float(bits);
+}
+
+// per element i: div_rn_inrange(a, b) vs the compiler's IEEE division over the documented range;
+// sqrt_rn_inrange(x) for x in [2^-96, 2^127] and sqrt_rn(x) for x over every positive float
+// (denormals included) vs the compiler's correctly rounded sqrt.  Mismatch counts -> bad[0..2].
+__global__ void rounding_selftest_kernel(int64_t n, uint64_t seed, unsigned long long* bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = seed * 0x9E3779B97F4A7C15ull + (uint64_t)i * 4;
+  float a = st_rand(k, -40, 39, true);
+  if ((i & 255) == 0) a = 0.f;
+  const float b = st_rand(k + 1, -40, 39, false);
+  if (__float_as_uint(div_rn_inrange(a, b)) != __float_as_uint(__fdiv_rn(a, b))) atomicAdd(bad, 1ull);
+  const float x = st_rand(k + 2, -96, 127, false);
+  if (__float_as_uint(sqrt_rn_inrange(x)) != __float_as_uint(st_ref_sqrt(x))) atomicAdd(bad + 1, 1ull);
+  const float y = __uint_as_float(st_hash(k + 3) & 0x7F7FFFFFu);  // any finite non-negative float
+  if (__float_as_uint(sqrt_rn(y)) != __float_as_uint(st_ref_sqrt(y))) atomicAdd(bad + 2, 1ull);
+}
+}  // namespace
+
+extern "C" int fr_adam_rounding_selftest(int64_t n, uint64_t seed, unsigned long long* d_bad, void* stream) {
+  FR_REQUIRE(n >= 0 && d_bad, "bad arguments");
+  if (n == 0) return FR_OK;
+  hipLaunchKernelGGL(rounding_selftest_kernel, dim3((unsigned)fr::ceil_div(n, (int64_t)256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), n, seed, d_bad);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -52,15 +52,20 @@ __device__ __forceinline__ float4 f4_fma(float s, float4 x, float4 acc) {
 
 // Correctly rounded f32 sqrt: v_sqrt_f32 is accurate to 1 ulp only; pick among s-1ulp, s, s+1ulp
 // by the sign of the fma residuals (the IEEE-exact expansion; matches x86 sqrtps bit for bit).
+// Inputs below 2^-96 are scaled by 2^32 first (exact; v_sqrt_f32's 1-ulp bound holds for normal
+// inputs) and the root by 2^-16 after (exact: the root is a normal number).  The bare instruction is
+// used directly: the compiler's own correctly rounded sqrt expansion would repeat the selection.
 __device__ __forceinline__ float sqrt_rn(float x) {
-  float s = __builtin_sqrtf(x);
+  const bool tiny = x < 0x1p-96f;
+  const float xs = tiny ? x * 0x1p+32f : x;
+  float s = __builtin_amdgcn_sqrtf(xs);
   const float s_dn = __int_as_float(__float_as_int(s) - 1);
   const float s_up = __int_as_float(__float_as_int(s) + 1);
-  const float r_dn = fmaf(-s_dn, s, x);
-  const float r_up = fmaf(-s_up, s, x);
+  const float r_dn = fmaf(-s_dn, s, xs);
+  const float r_up = fmaf(-s_up, s, xs);
   s = (r_dn <= 0.f) ? s_dn : s;
   s = (r_up > 0.f) ? s_up : s;
-  return s;
+  return tiny ? s * 0x1p-16f : s;
 }
 
 __device__ __forceinline__ float4 f4_add(float4 a, float4 b) {

@@ -533,3 +533,56 @@ def test_embedding_bwd_atomic_matches_sorted(cuda, hot):
     pad_got = ops.scatter_rows(idc, Gc, R, 11, hot_row=hot)
     assert torch.all(pad_got[11] == 0)
     assert torch.all((pad_got - pad_ref).abs() <= 1e-5 * scale + 1e-6)
+
+
+@pytest.mark.parametrize("slices", [1, 3, 8])
+def test_lazy_rows_background_slices(cuda, slices):
+    """Background slice replay (fr_adam_catch_up_slice, issued by prefetch_rows behind the batch's
+    catch-up on the side stream and joined before the optimiser step): each step one slice of
+    every table replays its backlog.  Without any flush, every row is current within ``slices``
+    steps; after a flush the tables, moments and step counters are bit-identical to the every-row
+    update.  Two tables of different widths in one launch, rows gathered before the step."""
+    from FoodRec.engine.optim import FusedAdam
+    torch.manual_seed(8)
+    shapes = [(1001, 128), (1001, 32)]
+    w0 = [torch.randn(R, d) for R, d in shapes]
+    pa = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    pb = [torch.nn.Parameter(w.clone().to(cuda)) for w in w0]
+    oa = FusedAdam(pa, lr=3e-3)
+    ob = FusedAdam(pb, lr=3e-3, lazy_rows=True, lazy_slices=slices)
+    for k in range(14):
+        ids, _ = _case(1001, 4, 40, None, 3100 + k)
+        ids = ids.to(cuda)
+        Gs = [torch.randn(40, d, generator=torch.Generator().manual_seed(3200 + 7 * k + d)).to(cuda)
+              for _, d in shapes]
+        for o, ps in ((oa, pa), (ob, pb)):
+            o.zero_grad()
+            join = o.row_grads.prefetch_rows([(p, ids) for p in ps])
+            join()
+            for p, G in zip(ps, Gs):
+                o.row_grads.stash(p, None, ids, G)
+            o.step()
+        if k >= slices:  # every row replayed within the last `slices` steps (before this step)
+            for p in pb:
+                st = ob.state[p]
+                lag = int(st["step"].item()) - int(st["lazy_last"].min().item())
+                assert lag <= slices, (k, lag)
+        if k in (6, 13):
+            ob.flush()
+            for a_, b_ in zip(pa, pb):
+                assert torch.equal(a_, b_), k
+                for s_ in ("exp_avg", "exp_avg_sq"):
+                    assert torch.equal(oa.state[a_][s_], ob.state[b_][s_]), (k, s_)
+
+
+def test_rounding_shortcuts_bit_exact(cuda):
+    """The lazy-row replay's in-range forms (v_rcp + fma chain division without the scale / fix-up
+    steps, bare v_sqrt_f32 + residual selection) and sqrt_rn's small-input scaling return the IEEE
+    correctly rounded fp32 result: 2^24 random operand sets per form on the device, zero mismatches
+    (division vs __fdiv_rn; sqrt vs the correctly rounded double root, denormals included)."""
+    from FoodRec.engine import native
+    bad = torch.zeros(3, dtype=torch.int64, device=cuda)
+    for seed in (1, 2):
+        native.check(native.lib().fr_adam_rounding_selftest(1 << 23, seed, bad.data_ptr(),
+                                                            native.stream_of(bad)), "fr_adam_rounding_selftest")
+    assert bad.tolist() == [0, 0, 0]
