@@ -431,6 +431,80 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pipelined plain mode (d = 64, every row a plain unit, X one table, no column mask): the shape of
+// HealthRec's RI propagation (65,617 rows of <= 45 edges).  There a group's unit is one batch of
+// <= 16 edges and the general kernel pays four dependent memory trips per row (unit entry ->
+// rowptr -> col / val -> gathers, then the epilogue addends); here a 16-lane group walks rows
+// r, r + G, ... with the next row's rowptr pair, the current row's epilogue addends and the next
+// batch's col / val all issued before the current batch's 16 gathers are consumed, so a row costs
+// about one exposed trip.  Edge order and FMA order are those of gather_unit (bit-identical rows).
+__device__ __forceinline__ void load_batch(const int32_t* __restrict__ col, const float* __restrict__ val, int64_t e,
+                                           int64_t e1, int lig, int& c, float& v) {
+  const int64_t my = e + lig;
+  c = my < e1 ? __builtin_nontemporal_load(col + my) : 0;  // lanes past the end: row 0, weight 0
+  v = my < e1 ? __builtin_nontemporal_load(val + my) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const float* __restrict__ val, int64_t n_rows,
+                                                           const float4* __restrict__ X, int64_t ldx4, Epi ep) {
+  constexpr int LPR = 16, GPB = 256 / LPR;
+  const int q = threadIdx.x % LPR;
+  const int64_t G = (int64_t)gridDim.x * GPB;
+  int64_t r = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  if (r >= n_rows) return;
+  int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
+  int c;
+  float v;
+  load_batch(col, val, e0, e1, q, c, v);
+  const bool has_a1 = ep.Y2.lo && ep.A1.lo, has_a2 = ep.Y2.lo && ep.A2.lo;
+  while (true) {
+    const int64_t rn = r + G;
+    int64_t ne0 = 0, ne1 = 0;
+    if (rn < n_rows) {
+      ne0 = rowptr[rn];
+      ne1 = rowptr[rn + 1];
+    }
+    float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1;
+    if (has_a1 && (ep.a1_gate == nullptr || ep.a1_gate[r] != 0))
+      a1 = reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q];
+    if (has_a2) a2 = reinterpret_cast<const float4*>(tab_row(ep.A2, r, ep.split))[q];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = e0; e < e1; e += LPR) {
+      float4 x[LPR];
+      float w[LPR];
+#define FR_PG(K)                                     \
+      {                                              \
+        w[(K)] = bcast_f<LPR, (K)>(v);               \
+        const int ck = bcast_i<LPR, (K)>(c);         \
+        x[(K)] = X[(int64_t)ck * ldx4 + q];          \
+      }
+      FR_PG(0) FR_PG(1) FR_PG(2) FR_PG(3) FR_PG(4) FR_PG(5) FR_PG(6) FR_PG(7)
+      FR_PG(8) FR_PG(9) FR_PG(10) FR_PG(11) FR_PG(12) FR_PG(13) FR_PG(14) FR_PG(15)
+#undef FR_PG
+      // the next batch of this row, else the next row's first batch, in flight during the gathers
+      if (e + LPR < e1) load_batch(col, val, e + LPR, e1, q, c, v);
+      else if (rn < n_rows) load_batch(col, val, ne0, ne1, q, c, v);
+#pragma unroll
+      for (int k = 0; k < LPR; ++k) acc = f4_fma(w[k], x[k], acc);
+    }
+    if (e0 == e1 && rn < n_rows) load_batch(col, val, ne0, ne1, q, c, v);  // empty row
+    if (ep.Y1.lo) reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y1, r, ep.split)))[q] = acc;
+    if (ep.Y2.lo) {
+      float4 o = f4_scale(ep.alpha, acc);
+      if (has_a1) o = f4_fma(ep.beta1, a1, o);
+      if (has_a2) o = f4_fma(ep.beta2, a2, o);
+      reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
+    }
+    if (rn >= n_rows) break;
+    r = rn;
+    e0 = ne0;
+    e1 = ne1;
+  }
+}
+
 template <int LPR, bool SPLIT, bool MASK>
 hipError_t launch_units(const int64_t* rowptr, const int32_t* col, const float* val,
                         const fr_spmm_plan* plan, const XSrc& xs, int d4, const Epi& ep,
@@ -445,12 +519,23 @@ hipError_t launch_units(const int64_t* rowptr, const int32_t* col, const float* 
 }
 
 template <int LPR>
-hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
+hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
                        const fr_spmm_plan* plan, const XSrc& xs, int d, const Epi& ep,
                        float4* partial, hipStream_t s) {
   constexpr int GPB = 256 / LPR;
   const int d4 = d / 4;
   const bool split = xs.hi != nullptr, mask = xs.cmask != nullptr;
+  if constexpr (LPR == 16) {
+    // every row one plain unit, in row order (the planner's plain units are the rows of degree <=
+    // chunk, ascending): the pipelined row walk, ~2 rows per group
+    if (!split && !mask && d4 == 16 && plan->n_split == 0 && plan->n_units == n_rows && plan->n_plain == n_rows) {
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(n_rows, 2 * GPB),
+                                                                    (int64_t)fr::kNumCU * 16));
+      hipLaunchKernelGGL(spmm_plain16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col, val,
+                         n_rows, xs.lo, xs.ld4, ep);
+      return hipGetLastError();
+    }
+  }
   if (plan->n_units > 0) {
     hipError_t e;
     if (split && mask) e = launch_units<LPR, true, true>(rowptr, col, val, plan, xs, d4, ep, partial, s);
@@ -586,18 +671,18 @@ int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
     }
     e = hipGetLastError();
   } else if (d4 >= 64) {
-    e = launch_spmm<64>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = launch_spmm<64>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   } else if (d4 >= 32) {
-    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s)
-                   : launch_spmm<16>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s)
+                   : launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   } else if (d4 >= 16) {
-    e = launch_spmm<16>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   } else if (d4 >= 8) {
-    e = launch_spmm<8>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = launch_spmm<8>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   } else if (d4 >= 4) {
-    e = launch_spmm<4>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = launch_spmm<4>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   } else {
-    e = launch_spmm<1>(d_rowptr, d_col, d_val, plan, xs, d, ep, partial, s);
+    e = launch_spmm<1>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
   }
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string(who) + ": " + hipGetErrorString(e));
   return FR_OK;

@@ -68,6 +68,45 @@ def test_spmm_epilogue_and_ld(cuda):
     np.testing.assert_allclose(Y2.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("n,max_deg,ldx", [(65617, 45, 64), (37, 33, 96), (5000, 16, 64)])
+def test_spmm_plain_rows_pipelined(cuda, n, max_deg, ldx):
+    """Every row a plain unit (the RI propagation's shape): the pipelined row walk
+    (spmm_plain16_kernel) vs float64, with the full epilogue (Y1, Y2 = alpha acc + beta1 A1 +
+    beta2 A2), empty rows, rows of exactly 16 / 32 edges, a strided X; rows of <= 16 edges are
+    bit-identical to the general unit kernel (the same adjacency planned with chunk 16, which
+    splits the longer rows and so takes the general path)."""
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency
+    rng = np.random.default_rng(n)
+    deg = rng.integers(0, max_deg + 1, n)
+    deg[: min(n, 3)] = [0, 16, min(32, max_deg)][: min(n, 3)]
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = rng.integers(0, n, rowptr[-1]).astype(np.int32)
+    val = rng.standard_normal(rowptr[-1]).astype(np.float32)
+    a = Adjacency(rowptr, col, val, (n, n), chunk=64, symmetric=False, device=cuda)
+    b = Adjacency(rowptr, col, val, (n, n), chunk=16, symmetric=False, device=cuda)
+    assert a.n_units == n and a.n_split == 0 and (max_deg <= 16 or b.n_split > 0)
+    big = torch.randn(n, ldx, device=cuda)
+    X = big[:, :64]
+    A1, A2 = torch.randn(n, 64, device=cuda), torch.randn(n, 64, device=cuda)
+    out = {}
+    for name, adj in (("a", a), ("b", b)):
+        Y1, Y2 = torch.empty(n, 64, device=cuda), torch.empty(n, 64, device=cuda)
+        ops.spmm_launch(adj, X, Y1=Y1, Y2=Y2, alpha=0.5, A1=A1, beta1=0.25, A2=A2, beta2=-1.5)
+        out[name] = (Y1.cpu(), Y2.cpu())
+    rows = np.repeat(np.arange(n), deg)
+    acc = np.zeros((n, 64))
+    np.add.at(acc, rows, val[:, None].astype(np.float64) * X.double().cpu().numpy()[col])
+    scale = np.zeros((n, 64))
+    np.add.at(scale, rows, np.abs(val[:, None]).astype(np.float64) * np.abs(X.double().cpu().numpy()[col]))
+    Y1, Y2 = out["a"]
+    assert np.all(np.abs(Y1.numpy() - acc) <= 2e-6 * scale + 1e-6)
+    want = 0.5 * acc + 0.25 * A1.double().cpu().numpy() - 1.5 * A2.double().cpu().numpy()
+    assert np.all(np.abs(Y2.numpy() - want) <= 2e-6 * scale + 2e-6 * np.abs(want) + 1e-6)
+    short = torch.as_tensor(deg <= 16)
+    assert torch.equal(Y1[short], out["b"][0][short]) and torch.equal(Y2[short], out["b"][1][short])
+
+
 def test_spmm_deterministic(cuda):
     from FoodRec.engine import ops
     n = 2000
