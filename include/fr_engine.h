@@ -631,6 +631,15 @@ int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, const float* d
                    const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
                    float beta2, const uint8_t* d_col_mask, const fr_rowlist* rows, const uint8_t* d_a1_gate,
                    void* d_workspace, int64_t workspace_bytes, void* stream);
+/* fr_spmm_csr_range: fr_spmm_csr_ex (no mask, no row list) over output rows [row_lo, row_hi) only;
+ * the other rows of Y1 / Y2 are not written.  For a bipartite graph whose rows [0, s) connect only
+ * to [s, n) (HealthRec's RI graph, cikm_model.py:136-180 at :185-208): the last propagation layer
+ * is needed at the item rows only and the first backward layer of an item-only upstream gradient
+ * is non-zero at the ingredient rows only. */
+int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                      const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
+                      const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
+                      int64_t row_lo, int64_t row_hi, void* d_workspace, int64_t workspace_bytes, void* stream);
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
                       uint32_t* d_bits, void* stream);

@@ -137,6 +137,18 @@ class Adjacency:
         self.chunk = auto_chunk(self.nnz) if chunk is None else int(chunk)
         self._build_plan(rp.cpu())
         self._t = None
+        self.bipartite_split = None  # see mark_bipartite
+        self.nnz_below_split = 0
+
+    def mark_bipartite(self, split: int):
+        """Declare that rows [0, split) have columns in [split, n) only and vice versa (a
+        [[0, R], [R^T, 0]] graph such as the recipe-ingredient adjacency): the propagation then
+        skips the output rows a layer is known not to need or to be zero at (ops.graph_bpr)."""
+        split = int(split)
+        if not 0 < split < self.shape[0] or self.shape[0] != self.shape[1]:
+            raise ValueError("mark_bipartite: split must lie inside a square adjacency")
+        self.bipartite_split = split
+        self.nnz_below_split = int(self.rowptr[split].item())
 
     # ------------------------------------------------------------------ construction helpers
     @classmethod

@@ -157,6 +157,24 @@ def _propagate_mean_fwd(adj: Adjacency, ego: torch.Tensor, L: int) -> torch.Tens
     return out
 
 
+def _prop_bwd_bipartite2(adj, G, out_lo, out_hi, split):
+    """_prop_bwd_split for L = 2 on a bipartite adjacency split at ``split`` (adj.mark_bipartite)
+    when G is zero at rows [split, n) (HealthRec's RI upstream gradient: the ingredient rows of the
+    propagation are discarded).  With A = [[0, R], [R^T, 0]] and G = [g ; 0]:
+      H   = (A G + G) / 3     = [g / 3 ; R^T g / 3]
+      out = A H + G / 3       = [R (R^T g / 3) + g / 3 ; R^T g / 3]
+    so the ingredient rows of the result equal those of H: one launch over rows [split, n) writes
+    them (into out_hi) and the item rows read them there -- two half-graph launches instead of two
+    full ones.  The item rows are the full form's sums in the same order (the skipped products are
+    exact zeros); the ingredient rows apply the 1/3 after the sum instead of to each term (a
+    rounding-level difference)."""
+    inv = 1.0 / 3.0
+    N = adj.shape[0]
+    spmm_range(adj, G, split, N, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv)
+    # item rows read X only at ingredient columns (X lo is never read: G stands in for it)
+    spmm_range(adj, G, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=G, beta1=inv)
+
+
 def _propagate_mean_bwd(adj: Adjacency, G: torch.Tensor, L: int) -> torch.Tensor:
     # d/d ego of mean_k A^k ego:  H_L = G/(L+1);  H_k = A^T H_{k+1} + G/(L+1);  grad = H_0
     at = adj.transpose_csr()
@@ -424,6 +442,36 @@ def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
             ws.numel(), native.stream_of(X)), "fr_spmm_csr_ex")
 
 
+def spmm_range(adj: Adjacency, X, row_lo: int, row_hi: int, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
+               Y2_hi=None, alpha=1.0, A1=None, A1_hi=None, beta1=0.0, A2=None, A2_hi=None, beta2=0.0,
+               region="spmm", nbytes=None):
+    """fr_spmm_csr_range: spmm_ex (no mask, no row list) over output rows [row_lo, row_hi) only."""
+    native.require_device(X)
+    N, d = adj.shape[0], X.shape[1]
+    _check_tab("X", X, X_hi, split, adj.shape[1], d)
+    if not 0 <= row_lo <= row_hi <= N:
+        raise native.EngineError(f"spmm_range: rows [{row_lo}, {row_hi}) outside [0, {N})")
+    for name, lo, hi in (("Y1", Y1, Y1_hi), ("Y2", Y2, Y2_hi), ("A1", A1, A1_hi), ("A2", A2, A2_hi)):
+        _check_tab(name, lo, hi, split, row_hi if hi is None else N, d)  # rows are addressed absolutely
+    plan = adj.plan()
+    ws = _ws_for(adj, d, X.device)
+    if nbytes is None:
+        nnz = adj.nnz
+        if adj.bipartite_split is not None and (row_lo, row_hi) == (0, adj.bipartite_split):
+            nnz = adj.nnz_below_split
+        elif adj.bipartite_split is not None and (row_lo, row_hi) == (adj.bipartite_split, N):
+            nnz = adj.nnz - adj.nnz_below_split
+        rows = row_hi - row_lo
+        nio = sum(x is not None for x in (Y1, Y2, A1, A2))
+        nbytes = 8 * (rows + 1) + 8 * nnz + 4 * d * nnz + 4 * d * rows * nio
+    with profiling.region(region, nbytes):
+        native.check(native.lib().fr_spmm_csr_range(
+            adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, ctypes.byref(plan), int(split),
+            ctypes.byref(_tab(X, X_hi)), d, ctypes.byref(_tab(Y1, Y1_hi)), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha),
+            ctypes.byref(_tab(A1, A1_hi)), _f(beta1), ctypes.byref(_tab(A2, A2_hi)), _f(beta2), int(row_lo),
+            int(row_hi), ws.data_ptr(), ws.numel(), native.stream_of(X)), "fr_spmm_csr_range")
+
+
 def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = None,
               bits: torch.Tensor | None = None) -> None:
     """mask[row] = value at the listed rows; with ``zero`` ([*, d] fp32), those rows of it set to 0;
@@ -472,22 +520,32 @@ def _adjacent_rows(lo, hi, rows):
     return lo.as_strided((rows, lo.shape[1]), (lo.shape[1], 1))
 
 
-def _prop_fwd_split(adj, lo, hi, split, L):
-    """mean([E, A E, ..., A^L E]) for E = [lo ; hi] split at ``split`` (no concatenated copy)."""
+def _prop_fwd_split(adj, lo, hi, split, L, lo_rows_only=False):
+    """mean([E, A E, ..., A^L E]) for E = [lo ; hi] split at ``split`` (no concatenated copy).
+    ``lo_rows_only`` (a bipartite adjacency split at ``split``, adj.mark_bipartite): only rows
+    [0, split) of the mean are wanted -- the last layer is evaluated there only (half its edges);
+    the other rows of the result are left unwritten."""
     N, d = adj.shape[0], lo.shape[1]
     if split == lo.shape[0]:
         one = _adjacent_rows(lo, hi, adj.shape[1])
         if one is not None:  # the tables are one buffer already: plain gathers
             lo, hi = one, None
     out = torch.empty(N, d, dtype=lo.dtype, device=lo.device)
+    last = (0, split) if lo_rows_only and adj.bipartite_split == split else None
     if L == 1:
-        spmm_ex(adj, lo, hi, split, Y2=out, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)
+        if last is not None:
+            spmm_range(adj, lo, *last, X_hi=hi, split=split, Y2=out, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)
+        else:
+            spmm_ex(adj, lo, hi, split, Y2=out, alpha=0.5, A1=lo, A1_hi=hi, beta1=0.5)
         return out
     inv = 1.0 / (L + 1)
     E1 = torch.empty_like(out)
     if L == 2:
         spmm_ex(adj, lo, hi, split, Y1=E1)
-        spmm_ex(adj, E1, Y2=out, alpha=inv, A1=lo, A1_hi=hi, beta1=inv, A2=E1, beta2=inv, split=split)
+        if last is not None:
+            spmm_range(adj, E1, *last, Y2=out, alpha=inv, A1=lo, A1_hi=hi, beta1=inv, A2=E1, beta2=inv, split=split)
+        else:
+            spmm_ex(adj, E1, Y2=out, alpha=inv, A1=lo, A1_hi=hi, beta1=inv, A2=E1, beta2=inv, split=split)
         return out
     S = torch.empty_like(out)
     spmm_ex(adj, lo, hi, split, Y1=E1, Y2=S, alpha=1.0, A1=lo, A1_hi=hi, beta1=1.0)
@@ -495,7 +553,10 @@ def _prop_fwd_split(adj, lo, hi, split, L):
     for _ in range(2, L):
         spmm_launch(adj, prev, Y1=nxt, Y2=S, alpha=1.0, A1=S, beta1=1.0)
         prev, nxt = nxt, prev
-    spmm_launch(adj, prev, Y2=out, alpha=inv, A1=S, beta1=inv)
+    if last is not None:
+        spmm_range(adj, prev, *last, Y2=out, alpha=inv, A1=S, beta1=inv)
+    else:
+        spmm_launch(adj, prev, Y2=out, alpha=inv, A1=S, beta1=inv)
     return out
 
 
@@ -518,6 +579,18 @@ def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None, gate=False)
         spmm_launch(adj, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
         H, H2 = H2, H
     spmm_ex(adj, H, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=1.0, A1=G, beta1=inv)
+
+
+def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split):
+    """The RI backward of graph_bpr (G zero at the ingredient rows): the half-graph form on a
+    bipartite adjacency with two layers, _prop_bwd_split otherwise."""
+    if L == 2 and adj.bipartite_split == split and not _RI_FULL_GRAPH:
+        _prop_bwd_bipartite2(adj, G, out_lo, out_hi, split)
+    else:
+        _prop_bwd_split(adj, G, L, out_lo, out_hi, split)
+
+
+_RI_FULL_GRAPH = False  # test hook: True runs the full-graph RI launches
 
 
 def _persistent(adj, key, make):
@@ -556,7 +629,8 @@ class _GraphBpr(torch.autograd.Function):
             if t.dtype != torch.float32 or t.shape[1] != 64 or not t.is_contiguous():
                 raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
         u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
-        ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri)       # [I + NI, 64]
+        # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
+        ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
         rows = [(u, 0), (p, U), (n, U)]
         if L_ui == 1:
             ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
@@ -619,7 +693,7 @@ class _GraphBpr(torch.autograd.Function):
             _prop_bwd_split(ui_adj, dUI, L_ui, d_user, G_ri, U)
         d_item = torch.empty_like(item_w)
         d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
-        _prop_bwd_split(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
+        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
         d_ingre[NI:].zero_()  # the padding row is not a graph node
         # EmbLoss on the ego rows, accumulated into the propagation gradients
         with profiling.region("bpr_bwd", 0):
@@ -668,7 +742,7 @@ class _GraphBpr(torch.autograd.Function):
             _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
         d_item = torch.empty_like(item_w)
         d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
-        _prop_bwd_split(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
+        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),

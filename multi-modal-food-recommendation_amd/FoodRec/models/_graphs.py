@@ -22,4 +22,7 @@ def side_adjacency(triples, n_items, n_side, device, chunk=DEFAULT_CHUNK) -> Adj
     t = np.asarray(triples)
     rows = t[:, 1].astype(np.int64) + n_items
     cols = t[:, 0].astype(np.int64)
-    return Adjacency.sym_normalized(n_items + n_side, rows, cols, device=device, chunk=chunk)
+    adj = Adjacency.sym_normalized(n_items + n_side, rows, cols, device=device, chunk=chunk)
+    # items connect only to side nodes and side nodes only to items
+    adj.mark_bipartite(n_items)
+    return adj

@@ -175,12 +175,13 @@ __global__ __launch_bounds__(256) void spmm_units_kernel(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int2* __restrict__ units, int64_t n_units,
     int64_t n_plain, int chunk, XSrc xs, int d4, Epi ep,
-    float4* __restrict__ partial) {
+    float4* __restrict__ partial, int64_t row_lo, int64_t row_hi) {
   constexpr int GPB = 256 / LPR;  // groups per block
   const int q0 = threadIdx.x % LPR;
   const int grp = threadIdx.x / LPR;
   for (int64_t u = (int64_t)blockIdx.x * GPB + grp; u < n_units; u += (int64_t)gridDim.x * GPB) {
     const int2 unit = units[u];
+    if (unit.x < row_lo || unit.x >= row_hi) continue;  // row range (group-uniform)
     const int64_t rs = rowptr[unit.x];
     const int64_t e0 = rs + (int64_t)unit.y * chunk;
     const int64_t e1 = min(rowptr[unit.x + 1], e0 + (int64_t)chunk);
@@ -203,12 +204,14 @@ __global__ __launch_bounds__(256) void spmm_units_kernel(
 template <int LPR>
 __global__ __launch_bounds__(256) void spmm_fixup_kernel(const int3* __restrict__ split_rows,
                                                          int64_t n_split, int d4, Epi ep,
-                                                         const float4* __restrict__ partial) {
+                                                         const float4* __restrict__ partial, int64_t row_lo,
+                                                         int64_t row_hi) {
   constexpr int GPB = 256 / LPR;
   const int q0 = threadIdx.x % LPR;
   const int grp = threadIdx.x / LPR;
   for (int64_t s = (int64_t)blockIdx.x * GPB + grp; s < n_split; s += (int64_t)gridDim.x * GPB) {
     const int3 sr = split_rows[s];
+    if (sr.x < row_lo || sr.x >= row_hi) continue;
     for (int q = q0; q < d4; q += LPR) {
       float4 acc = partial[(int64_t)sr.y * d4 + q];
       for (int k = 1; k < sr.z; ++k) acc = f4_add(acc, partial[((int64_t)sr.y + k) * d4 + q]);
@@ -448,12 +451,14 @@ __device__ __forceinline__ void load_batch(const int32_t* __restrict__ col, cons
 
 __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __restrict__ rowptr,
                                                            const int32_t* __restrict__ col,
-                                                           const float* __restrict__ val, int64_t n_rows,
-                                                           const float4* __restrict__ X, int64_t ldx4, Epi ep) {
+                                                           const float* __restrict__ val, int64_t row_lo,
+                                                           int64_t n_rows, const float4* __restrict__ X,
+                                                           int64_t ldx4, Epi ep) {
+  // rows [row_lo, n_rows)
   constexpr int LPR = 16, GPB = 256 / LPR;
   const int q = threadIdx.x % LPR;
   const int64_t G = (int64_t)gridDim.x * GPB;
-  int64_t r = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  int64_t r = row_lo + (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
   if (r >= n_rows) return;
   int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
   int c;
@@ -508,20 +513,20 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
 template <int LPR, bool SPLIT, bool MASK>
 hipError_t launch_units(const int64_t* rowptr, const int32_t* col, const float* val,
                         const fr_spmm_plan* plan, const XSrc& xs, int d4, const Epi& ep,
-                        float4* partial, hipStream_t s) {
+                        float4* partial, hipStream_t s, int64_t row_lo, int64_t row_hi) {
   constexpr int GPB = 256 / LPR;
   int64_t blocks = fr::ceil_div(plan->n_units, GPB);
   blocks = std::min<int64_t>(blocks, (int64_t)fr::kNumCU * 64);
   hipLaunchKernelGGL((spmm_units_kernel<LPR, SPLIT, MASK>), dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col,
                      val, reinterpret_cast<const int2*>(plan->d_units), plan->n_units,
-                     plan->n_plain, plan->chunk, xs, d4, ep, partial);
+                     plan->n_plain, plan->chunk, xs, d4, ep, partial, row_lo, row_hi);
   return hipGetLastError();
 }
 
 template <int LPR>
 hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
                        const fr_spmm_plan* plan, const XSrc& xs, int d, const Epi& ep,
-                       float4* partial, hipStream_t s) {
+                       float4* partial, hipStream_t s, int64_t row_lo, int64_t row_hi) {
   constexpr int GPB = 256 / LPR;
   const int d4 = d / 4;
   const bool split = xs.hi != nullptr, mask = xs.cmask != nullptr;
@@ -529,26 +534,27 @@ hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* v
     // every row one plain unit, in row order (the planner's plain units are the rows of degree <=
     // chunk, ascending): the pipelined row walk, ~2 rows per group
     if (!split && !mask && d4 == 16 && plan->n_split == 0 && plan->n_units == n_rows && plan->n_plain == n_rows) {
-      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(n_rows, 2 * GPB),
+      if (row_hi <= row_lo) return hipSuccess;
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(row_hi - row_lo, 2 * GPB),
                                                                     (int64_t)fr::kNumCU * 16));
       hipLaunchKernelGGL(spmm_plain16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col, val,
-                         n_rows, xs.lo, xs.ld4, ep);
+                         row_lo, row_hi, xs.lo, xs.ld4, ep);
       return hipGetLastError();
     }
   }
   if (plan->n_units > 0) {
     hipError_t e;
-    if (split && mask) e = launch_units<LPR, true, true>(rowptr, col, val, plan, xs, d4, ep, partial, s);
-    else if (split) e = launch_units<LPR, true, false>(rowptr, col, val, plan, xs, d4, ep, partial, s);
-    else if (mask) e = launch_units<LPR, false, true>(rowptr, col, val, plan, xs, d4, ep, partial, s);
-    else e = launch_units<LPR, false, false>(rowptr, col, val, plan, xs, d4, ep, partial, s);
+    if (split && mask) e = launch_units<LPR, true, true>(rowptr, col, val, plan, xs, d4, ep, partial, s, row_lo, row_hi);
+    else if (split) e = launch_units<LPR, true, false>(rowptr, col, val, plan, xs, d4, ep, partial, s, row_lo, row_hi);
+    else if (mask) e = launch_units<LPR, false, true>(rowptr, col, val, plan, xs, d4, ep, partial, s, row_lo, row_hi);
+    else e = launch_units<LPR, false, false>(rowptr, col, val, plan, xs, d4, ep, partial, s, row_lo, row_hi);
     if (e != hipSuccess) return e;
   }
   if (plan->n_split > 0) {
     int64_t blocks = std::min<int64_t>(fr::ceil_div(plan->n_split, GPB), (int64_t)fr::kNumCU * 16);
     hipLaunchKernelGGL(spmm_fixup_kernel<LPR>, dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const int3*>(plan->d_split_rows), plan->n_split, d4, ep,
-                       partial);
+                       partial, row_lo, row_hi);
     return hipGetLastError();
   }
   return hipSuccess;
@@ -622,7 +628,8 @@ int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
               const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
               const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
               const uint8_t* col_mask, const fr_rowlist* rows, const uint8_t* a1_gate, void* d_workspace,
-              int64_t workspace_bytes, void* stream, const char* who) {
+              int64_t workspace_bytes, void* stream, const char* who, int64_t row_lo = 0,
+              int64_t row_hi = -1) {
   FR_REQUIRE(plan != nullptr, "plan is null");
   FR_REQUIRE(d > 0 && d % 4 == 0 && d <= 1024, "d must be a positive multiple of 4, <= 1024");
   FR_REQUIRE(n_rows >= 0, "n_rows < 0");
@@ -635,6 +642,9 @@ int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
   FR_REQUIRE(tab_ok(X, d), "X must be 16-B aligned, ld % 4 == 0, ld >= d");
   FR_REQUIRE(tab_ok(Y1, d) && tab_ok(Y2, d) && tab_ok(A1, d) && tab_ok(A2, d), "bad Y1/Y2/A1/A2 table");
   FR_REQUIRE(split >= 0, "split < 0");
+  if (row_hi < 0) row_hi = n_rows;
+  FR_REQUIRE(row_lo >= 0 && row_lo <= row_hi && row_hi <= n_rows, "row range out of [0, n_rows]");
+  FR_REQUIRE(rows == nullptr || (row_lo == 0 && row_hi == n_rows), "a row list takes no row range");
   for (const fr_tab* y : {Y1, Y2})
     FR_REQUIRE(!(y && (tab_touches(y, X->lo) || tab_touches(y, X->hi))), "outputs must not alias X");
   const int64_t need = fr_spmm_workspace(plan, d);
@@ -671,18 +681,18 @@ int spmm_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
     }
     e = hipGetLastError();
   } else if (d4 >= 64) {
-    e = launch_spmm<64>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = launch_spmm<64>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   } else if (d4 >= 32) {
-    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s)
-                   : launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = (d4 == 32) ? launch_spmm<32>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi)
+                   : launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   } else if (d4 >= 16) {
-    e = launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = launch_spmm<16>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   } else if (d4 >= 8) {
-    e = launch_spmm<8>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = launch_spmm<8>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   } else if (d4 >= 4) {
-    e = launch_spmm<4>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = launch_spmm<4>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   } else {
-    e = launch_spmm<1>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s);
+    e = launch_spmm<1>(d_rowptr, d_col, d_val, n_rows, plan, xs, d, ep, partial, s, row_lo, row_hi);
   }
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string(who) + ": " + hipGetErrorString(e));
   return FR_OK;
@@ -709,6 +719,15 @@ extern "C" int fr_spmm_csr_ex(const int64_t* d_rowptr, const int32_t* d_col, con
                               const uint8_t* d_a1_gate, void* d_workspace, int64_t workspace_bytes, void* stream) {
   return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, split, X, d, Y1, Y2, alpha, A1, beta1, A2, beta2,
                    d_col_mask, rows, d_a1_gate, d_workspace, workspace_bytes, stream, "fr_spmm_csr_ex");
+}
+
+extern "C" int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                                 const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
+                                 const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2,
+                                 float beta2, int64_t row_lo, int64_t row_hi, void* d_workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  return spmm_impl(d_rowptr, d_col, d_val, n_rows, plan, split, X, d, Y1, Y2, alpha, A1, beta1, A2, beta2, nullptr,
+                   nullptr, nullptr, d_workspace, workspace_bytes, stream, "fr_spmm_csr_range", row_lo, row_hi);
 }
 
 extern "C" int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream) {

@@ -107,6 +107,38 @@ def test_spmm_plain_rows_pipelined(cuda, n, max_deg, ldx):
     assert torch.equal(Y1[short], out["b"][0][short]) and torch.equal(Y2[short], out["b"][1][short])
 
 
+def test_bipartite_half_graph_propagation(cuda):
+    """HealthRec's RI propagation on a bipartite adjacency (models/_graphs.side_adjacency marks it):
+    the last forward layer over the item rows only (fr_spmm_csr_range) equals the full launch's
+    item rows bit for bit; the two-layer backward of an item-only upstream gradient in two
+    half-graph launches (ops._prop_bwd_bipartite2) equals the full form within fp32 rounding, and
+    its item rows bit for bit."""
+    from FoodRec.engine import ops
+    from FoodRec.models._graphs import side_adjacency
+    rng = np.random.default_rng(5)
+    I, NI = 3000, 700
+    triples = np.stack([rng.integers(0, I, 20000), rng.integers(0, NI, 20000)], 1)
+    adj = side_adjacency(triples, I, NI, cuda)
+    assert adj.bipartite_split == I
+    item = torch.randn(I, 64, device=cuda)
+    ingre = torch.randn(NI + 1, 64, device=cuda)
+    full = ops._prop_fwd_split(adj, item, ingre, I, 2)
+    half = ops._prop_fwd_split(adj, item, ingre, I, 2, lo_rows_only=True)
+    assert torch.equal(full[:I], half[:I])
+    G = torch.zeros(I + NI, 64, device=cuda)
+    G[:I] = torch.randn(I, 64, device=cuda)
+    outs = []
+    for fast in (False, True):
+        d_item, d_ingre = torch.empty(I, 64, device=cuda), torch.full((NI + 1, 64), 7.0, device=cuda)
+        (ops._prop_bwd_bipartite2 if fast else
+         lambda *a: ops._prop_bwd_split(a[0], a[1], 2, *a[2:]))(adj, G, d_item, d_ingre, I)
+        outs.append((d_item.cpu(), d_ingre.cpu()))
+    (a_item, a_ing), (b_item, b_ing) = outs
+    assert torch.equal(a_item, b_item)
+    torch.testing.assert_close(b_ing[:NI], a_ing[:NI], rtol=2e-6, atol=1e-7)
+    assert torch.all(b_ing[NI:] == 7.0)  # the padding row is not written
+
+
 def test_spmm_deterministic(cuda):
     from FoodRec.engine import ops
     n = 2000
