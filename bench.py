@@ -216,6 +216,9 @@ def main():
             roofline = {**common, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
                         "flops_per_launch": fl, "bytes_per_launch": int(d["bytes_per_launch"]),
+                        "region_kernels": ("enc_bwd_kernel<20> + enc_reduce_kernel (the ordered weight-gradient "
+                                           "reduction): the two launches of one fr_encoder_bwd call"
+                                           if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
         else:
