@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
 }
 
 // ---------------------------------------------------------------------------------------------
-// Pipelined plain mode (d = 64, every row a plain unit, X one table, no column mask): the shape of
+// Pipelined plain mode (d = 64, every row a plain unit, no column mask; X one table or split): the shape of
 // HealthRec's RI propagation (65,617 rows of <= 45 edges).  There a group's unit is one batch of
 // <= 16 edges and the general kernel pays four dependent memory trips per row (unit entry ->
 // rowptr -> col / val -> gathers, then the epilogue addends); here a 16-lane group walks rows
@@ -449,11 +449,11 @@ __device__ __forceinline__ void load_batch(const int32_t* __restrict__ col, cons
   v = my < e1 ? __builtin_nontemporal_load(val + my) : 0.f;
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __restrict__ rowptr,
                                                            const int32_t* __restrict__ col,
                                                            const float* __restrict__ val, int64_t row_lo,
-                                                           int64_t n_rows, const float4* __restrict__ X,
-                                                           int64_t ldx4, Epi ep) {
+                                                           int64_t n_rows, XSrc xs, Epi ep) {
   // rows [row_lo, n_rows)
   constexpr int LPR = 16, GPB = 256 / LPR;
   const int q = threadIdx.x % LPR;
@@ -480,11 +480,23 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
     for (int64_t e = e0; e < e1; e += LPR) {
       float4 x[LPR];
       float w[LPR];
-#define FR_PG(K)                                     \
-      {                                              \
-        w[(K)] = bcast_f<LPR, (K)>(v);               \
-        const int ck = bcast_i<LPR, (K)>(c);         \
-        x[(K)] = X[(int64_t)ck * ldx4 + q];          \
+      // SPLIT: each lane's X row as a float4 offset from xs.lo (the hi table relative to it), the
+      // 64-bit offsets broadcast in two halves (as gather_unit's OFF mode)
+      int64_t off = 0;
+      if constexpr (SPLIT)
+        off = c >= xs.split ? (xs.hi - xs.lo) + ((int64_t)c - xs.split) * xs.ldh4 : (int64_t)c * xs.ld4;
+      const int off_lo = (int)(uint32_t)(uint64_t)off, off_hi = (int)(uint32_t)((uint64_t)off >> 32);
+#define FR_PG(K)                                                                           \
+      {                                                                                    \
+        w[(K)] = bcast_f<LPR, (K)>(v);                                                     \
+        if constexpr (SPLIT) {                                                             \
+          const uint64_t ok = (uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_lo) |              \
+                              ((uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_hi) << 32);       \
+          x[(K)] = xs.lo[(int64_t)ok + q];                                                 \
+        } else {                                                                           \
+          const int ck = bcast_i<LPR, (K)>(c);                                             \
+          x[(K)] = xs.lo[(int64_t)ck * xs.ld4 + q];                                        \
+        }                                                                                  \
       }
       FR_PG(0) FR_PG(1) FR_PG(2) FR_PG(3) FR_PG(4) FR_PG(5) FR_PG(6) FR_PG(7)
       FR_PG(8) FR_PG(9) FR_PG(10) FR_PG(11) FR_PG(12) FR_PG(13) FR_PG(14) FR_PG(15)
@@ -533,12 +545,16 @@ hipError_t launch_spmm(const int64_t* rowptr, const int32_t* col, const float* v
   if constexpr (LPR == 16) {
     // every row one plain unit, in row order (the planner's plain units are the rows of degree <=
     // chunk, ascending): the pipelined row walk, ~2 rows per group
-    if (!split && !mask && d4 == 16 && plan->n_split == 0 && plan->n_units == n_rows && plan->n_plain == n_rows) {
+    if (!mask && d4 == 16 && plan->n_split == 0 && plan->n_units == n_rows && plan->n_plain == n_rows) {
       if (row_hi <= row_lo) return hipSuccess;
       const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(row_hi - row_lo, 2 * GPB),
                                                                     (int64_t)fr::kNumCU * 16));
-      hipLaunchKernelGGL(spmm_plain16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col, val,
-                         row_lo, row_hi, xs.lo, xs.ld4, ep);
+      if (split)
+        hipLaunchKernelGGL(spmm_plain16_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col, val,
+                           row_lo, row_hi, xs, ep);
+      else
+        hipLaunchKernelGGL(spmm_plain16_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, rowptr, col, val,
+                           row_lo, row_hi, xs, ep);
       return hipGetLastError();
     }
   }
