@@ -157,22 +157,68 @@ def _propagate_mean_fwd(adj: Adjacency, ego: torch.Tensor, L: int) -> torch.Tens
     return out
 
 
-def _prop_bwd_bipartite2(adj, G, out_lo, out_hi, split):
+def _prop_bwd_bipartite2(adj, g, out_lo, out_hi, split):
     """_prop_bwd_split for L = 2 on a bipartite adjacency split at ``split`` (adj.mark_bipartite)
-    when G is zero at rows [split, n) (HealthRec's RI upstream gradient: the ingredient rows of the
-    propagation are discarded).  With A = [[0, R], [R^T, 0]] and G = [g ; 0]:
+    for an upstream gradient G = [g ; 0], zero at rows [split, n) (HealthRec's RI graph and CLUSSL's
+    modality graphs: the side rows of the propagation are discarded).  ``g``: the rows [0, split)
+    of G.  With A = [[0, R], [R^T, 0]]:
       H   = (A G + G) / 3     = [g / 3 ; R^T g / 3]
       out = A H + G / 3       = [R (R^T g / 3) + g / 3 ; R^T g / 3]
-    so the ingredient rows of the result equal those of H: one launch over rows [split, n) writes
-    them (into out_hi) and the item rows read them there -- two half-graph launches instead of two
-    full ones.  The item rows are the full form's sums in the same order (the skipped products are
-    exact zeros); the ingredient rows apply the 1/3 after the sum instead of to each term (a
-    rounding-level difference)."""
+    so the side rows of the result equal those of H: one launch over rows [split, n) writes them
+    (into out_hi) and the item rows read them there -- two half-graph launches instead of two full
+    ones.  The item rows are the full form's sums in the same order (the skipped products are exact
+    zeros); the side rows apply the 1/3 after the sum instead of to each term (a rounding-level
+    difference)."""
     inv = 1.0 / 3.0
     N = adj.shape[0]
-    spmm_range(adj, G, split, N, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=inv)
-    # item rows read X only at ingredient columns (X lo is never read: G stands in for it)
-    spmm_range(adj, G, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=G, beta1=inv)
+    # side rows gather item columns only: X = [g ; (never read)]
+    pad = _persistent(adj, ("bwd_pad", str(g.device)), lambda: torch.zeros(N - split, g.shape[1], device=g.device))
+    spmm_range(adj, g, split, N, X_hi=pad, split=split, Y2=out_lo, Y2_hi=out_hi, alpha=inv)
+    # item rows gather side columns only: X = [(never read) ; out_hi]
+    spmm_range(adj, g, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=g, beta1=inv)
+
+
+class _PropagateLo(torch.autograd.Function):
+    """split(mean_k A^k [lo ; hi], [split, n - split])[0] on a bipartite adjacency split at
+    ``split = lo.shape[0]``: the reference's propagate-then-keep-the-item-rows
+    (pricai_modelx.py:183-226, cikm_model.py:185-208) without the concatenation, the split or the
+    side rows the result does not contain (_prop_fwd_split(lo_rows_only), _prop_bwd_bipartite2)."""
+
+    @staticmethod
+    def forward(ctx, adj, lo, hi, L):
+        native.require_device(lo, hi)
+        split = lo.shape[0]
+        ctx.adj, ctx.L, ctx.split, ctx.hi_rows = adj, L, split, hi.shape[0]
+        return _prop_fwd_split(adj, lo, hi, split, L, lo_rows_only=True)[:split]
+
+    @staticmethod
+    def backward(ctx, g):
+        adj, L, split = ctx.adj, ctx.L, ctx.split
+        g = _rowmajor(g)
+        N, d = adj.shape[0], g.shape[1]
+        d_lo = torch.empty(split, d, dtype=g.dtype, device=g.device)
+        d_hi = torch.empty(ctx.hi_rows, d, dtype=g.dtype, device=g.device)
+        if ctx.hi_rows > N - split:
+            d_hi[N - split:].zero_()  # rows past the graph (e.g. a padding row) get no gradient
+        if L == 2:
+            _prop_bwd_bipartite2(adj, g, d_lo, d_hi, split)
+        else:
+            G = torch.zeros(N, d, dtype=g.dtype, device=g.device)
+            G[:split] = g
+            _prop_bwd_split(adj, G, L, d_lo, d_hi, split)
+        return None, d_lo, d_hi, None
+
+
+def propagate_lo(adj: Adjacency, lo: torch.Tensor, hi: torch.Tensor, n_layers: int) -> torch.Tensor:
+    """Rows [0, len(lo)) of mean([E, A E, ..., A^L E]), E = [lo ; hi], for an adjacency marked
+    bipartite at len(lo) (fp32, d = 64 on the GPU); otherwise the full propagation, split."""
+    split = lo.shape[0]
+    if (n_layers >= 1 and lo.is_cuda and getattr(adj, "bipartite_split", None) == split
+            and lo.dtype == torch.float32 and hi.dtype == torch.float32 and lo.shape[1] == 64 == hi.shape[1]
+            and hi.shape[0] >= adj.shape[0] - split):
+        return _PropagateLo.apply(adj, lo, hi, int(n_layers))
+    out = propagate_mean(adj, torch.cat([lo, hi[:adj.shape[0] - split]], dim=0), n_layers)
+    return out[:split]
 
 
 def _propagate_mean_bwd(adj: Adjacency, G: torch.Tensor, L: int) -> torch.Tensor:
@@ -585,7 +631,7 @@ def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split):
     """The RI backward of graph_bpr (G zero at the ingredient rows): the half-graph form on a
     bipartite adjacency with two layers, _prop_bwd_split otherwise."""
     if L == 2 and adj.bipartite_split == split and not _RI_FULL_GRAPH:
-        _prop_bwd_bipartite2(adj, G, out_lo, out_hi, split)
+        _prop_bwd_bipartite2(adj, G[:split], out_lo, out_hi, split)
     else:
         _prop_bwd_split(adj, G, L, out_lo, out_hi, split)
 

@@ -74,9 +74,9 @@ class CLUSSL(GeneralRecommender):
             nn.init.xavier_normal_(self.text_trs.weight)
 
     def _view(self, adj, side_table, n_side):
-        ego = torch.cat((self.item_embedding.weight, side_table), dim=0)
-        out = ops.propagate_mean(adj, ego, self.n_ri_layers)
-        return torch.split(out, [self.n_items, n_side])[0]
+        # split(propagate(cat(item, side)))[0] (pricai_modelx.py:183-226): on the GPU the item rows
+        # only, on the bipartite item-side graph (ops.propagate_lo: half-graph last layer and backward)
+        return ops.propagate_lo(adj, self.item_embedding.weight, side_table[:n_side], self.n_ri_layers)
 
     def forward(self):
         item_ingre = self._view(self.ingre_norm_adj, self.ingre_embedding.weight[:-1, :], self.n_ingredients)

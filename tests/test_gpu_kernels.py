@@ -130,13 +130,44 @@ def test_bipartite_half_graph_propagation(cuda):
     outs = []
     for fast in (False, True):
         d_item, d_ingre = torch.empty(I, 64, device=cuda), torch.full((NI + 1, 64), 7.0, device=cuda)
-        (ops._prop_bwd_bipartite2 if fast else
-         lambda *a: ops._prop_bwd_split(a[0], a[1], 2, *a[2:]))(adj, G, d_item, d_ingre, I)
+        if fast:
+            ops._prop_bwd_bipartite2(adj, G[:I], d_item, d_ingre, I)
+        else:
+            ops._prop_bwd_split(adj, G, 2, d_item, d_ingre, I)
         outs.append((d_item.cpu(), d_ingre.cpu()))
     (a_item, a_ing), (b_item, b_ing) = outs
     assert torch.equal(a_item, b_item)
     torch.testing.assert_close(b_ing[:NI], a_ing[:NI], rtol=2e-6, atol=1e-7)
     assert torch.all(b_ing[NI:] == 7.0)  # the padding row is not written
+
+
+@pytest.mark.parametrize("L", [1, 2, 3])
+def test_propagate_lo_matches_full(cuda, L):
+    """ops.propagate_lo (CLUSSL's modality views: item rows of the propagation over a bipartite
+    item-side graph, no concatenation or split) vs split(propagate_mean(cat(item, side)))[0]:
+    values and both tables' gradients (side rows beyond the graph: zero gradient)."""
+    from FoodRec.engine import ops
+    from FoodRec.models._graphs import side_adjacency
+    rng = np.random.default_rng(L)
+    I, NS = 2500, 400
+    triples = np.stack([rng.integers(0, I, 9000), rng.integers(0, NS, 9000)], 1)
+    adj = side_adjacency(triples, I, NS, cuda)
+    lo0, hi0 = torch.randn(I, 64, device=cuda), torch.randn(NS + 1, 64, device=cuda)
+    g = torch.randn(I, 64, device=cuda)
+    res = []
+    for fast in (False, True):
+        lo, hi = lo0.clone().requires_grad_(True), hi0.clone().requires_grad_(True)
+        if fast:
+            out = ops.propagate_lo(adj, lo, hi, L)
+        else:
+            out = ops.propagate_mean(adj, torch.cat([lo, hi[:NS]]), L)[:I]
+        (out * g).sum().backward()
+        res.append((out.detach(), lo.grad, hi.grad))
+    (a, ga_lo, ga_hi), (b, gb_lo, gb_hi) = res
+    assert torch.equal(a, b)
+    torch.testing.assert_close(gb_lo, ga_lo, rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(gb_hi, ga_hi, rtol=2e-6, atol=1e-7)
+    assert torch.all(gb_hi[NS:] == 0)
 
 
 def test_spmm_deterministic(cuda):
