@@ -317,6 +317,20 @@ def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4, adam=28):
     return 2 * L * b_spmm + 2 * (L + 1) * N * d * s + adam * P + B * (3 * 8 + 3 * d * s) * 2, b_spmm
 
 
+def config4_bytes_rows(N, nnz, P, B, deg_rows, d=64, s=4, adam=28):
+    """Algorithmic bytes of the LightGCN-ID step as the engine runs it (L = 2, ops.propagate_rows):
+    layer 1 over the full graph; layer 2 only at the 3B loss rows (their edges: ``deg_rows`` = the sum
+    of their degrees); BPR + EmbLoss with a dense zero-filled gradient table; the backward's first
+    layer as the sparse-upstream launch (all col/val scanned, X gathered at the hits, H written in
+    full); its second layer over the full graph (+ the G addend); Adam over every parameter."""
+    b_full = 8 * (N + 1) + nnz * 8 + nnz * d * s + N * d * s
+    rows = 3 * B
+    fwd = b_full + 16 * rows + deg_rows * (8 + d * s) + rows * d * s * 3
+    loss = B * (3 * 8 + 3 * d * s) * 2 + N * d * s  # + the dense gradient table's zero fill
+    bwd = (8 * (N + 1) + 8 * nnz + deg_rows * d * s + N * d * s + rows * d * s) + (b_full + N * d * s)
+    return fwd + loss + bwd + adam * P
+
+
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md; no sparsity)
 MFMA_F32_PEAK_TFLOPS = 157.3
 
@@ -549,16 +563,32 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         assert not int(state["nan"].item()), "NaN loss in the config-4 step"
-        bstep, _ = config4_bytes_per_step(N, adj.nnz, P, B)
+        # the loss rows' degree sum, averaged over 8 sampled batches (same sampler)
+        deg = adj.rowptr[1:] - adj.rowptr[:-1]
+        dsum = 0
+        for _ in range(8):
+            u, p, n = g.triples(B)
+            dsum += int(torch.cat([deg[u], deg[p + U], deg[n + U]]).sum().item())
+        del deg
+        deg_rows = dsum // 8
+        bstep = config4_bytes_rows(N, adj.nnz, P, B, deg_rows)
+        dense_eq, _ = config4_bytes_per_step(N, adj.nnz, P, B)
         steps_out[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
-                             "bytes_per_step": bstep, "achieved_gbps": round(bstep / dt / 1e9, 1),
+                             "bytes_per_step": bstep, "loss_rows_degree_sum": deg_rows,
+                             "achieved_gbps": round(bstep / dt / 1e9, 1),
                              "roofline_frac": round(bstep / dt / 1e9 / HBM_PEAK_GBPS, 4),
-                             "roofline_triples_per_s": round(B / (bstep / (HBM_PEAK_GBPS * 1e9)), 1)}
+                             "roofline_triples_per_s": round(B / (bstep / (HBM_PEAK_GBPS * 1e9)), 1),
+                             "survey_8d_dense_bytes": dense_eq,
+                             "survey_8d_dense_roofline_triples_per_s":
+                                 round(B / (dense_eq / (HBM_PEAK_GBPS * 1e9)), 1)}
     out = {"graph": "synthetic U=10M I=1M E=%d (nnz=%d, N=%d), built on device in %.1f s"
                     % (g.n_edges, adj.nnz, N, build_s),
            "model": "LightGCN_ID (L=2, d=64, fp32, BPR + EmbLoss, Adam)", "params": P, "steps_timed": steps,
            "spmm": spmm, "step": steps_out,
-           "byte_model": "SURVEY 8(d): 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2"}
+           "byte_model": "config4_bytes_rows: full layer 1 + layer 2 at the 3B loss rows (their edges) + "
+                         "BPR/EmbLoss with a dense zero-filled gradient + sparse-upstream backward layer (col/val "
+                         "scan, hits, H write) + full backward layer + 28*P Adam; survey_8d_dense_bytes = SURVEY "
+                         "8(d)'s 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2 (every layer over the full graph)"}
     del trainer, model, g, adj
     torch.cuda.empty_cache()
     out["spmm_beyond_mall"] = spmm_beyond_mall(device)

@@ -209,6 +209,72 @@ class _PropagateLo(torch.autograd.Function):
         return None, d_lo, d_hi, None
 
 
+class _PropagateRows(torch.autograd.Function):
+    """mean_k A^k ego where the caller reads the result at the listed rows only (a BPR loss reads
+    the propagated table at its batch's users and items, lightgcn.py:134-147 + :149-168): the last
+    layer is evaluated there only (row-list launch), and the backward of an upstream gradient that is
+    non-zero only at those rows starts with the sparse-upstream launch (edges scanned against a
+    bitmask of the rows, X gathered only there).  The result is valid at the listed rows only.
+    Float-atomic summation in the sparse launch: not for the deterministic mode."""
+
+    @staticmethod
+    def forward(ctx, adj, ego, L, rows):
+        ego = _rowmajor(ego)
+        native.require_device(ego)
+        out = torch.empty_like(ego)  # valid at the listed rows
+        inv = 1.0 / (L + 1)
+        if L == 1:
+            spmm_ex(adj, ego, Y2=out, alpha=0.5, A1=ego, beta1=0.5, rows=rows, region="spmm_rows")
+        elif L == 2:
+            E1 = torch.empty_like(ego)
+            spmm_launch(adj, ego, Y1=E1)
+            spmm_ex(adj, E1, Y2=out, alpha=inv, A1=ego, beta1=inv, A2=E1, beta2=inv, rows=rows, region="spmm_rows")
+        else:
+            S, E1 = torch.empty_like(ego), torch.empty_like(ego)
+            spmm_launch(adj, ego, Y1=E1, Y2=S, alpha=1.0, A1=ego, beta1=1.0)
+            prev, nxt = E1, torch.empty_like(ego)
+            for _ in range(2, L):
+                spmm_launch(adj, prev, Y1=nxt, Y2=S, alpha=1.0, A1=S, beta1=1.0)
+                prev, nxt = nxt, prev
+            spmm_ex(adj, prev, Y2=out, alpha=inv, A1=S, beta1=inv, rows=rows, region="spmm_rows")
+        ctx.adj, ctx.L, ctx.rows = adj, L, rows
+        return out
+
+    @staticmethod
+    def backward(ctx, G):
+        adj, L, rows = ctx.adj, ctx.L, ctx.rows
+        G = _rowmajor(G)
+        at = adj.transpose_csr()
+        N, dev = at.shape[0], G.device
+        bits = _persistent(at, ("rows_bits", str(dev)), lambda: torch.zeros((N + 31) // 32, dtype=torch.int32, device=dev))
+        mask = _persistent(at, ("rows_mask", str(dev)), lambda: torch.zeros(N, dtype=torch.uint8, device=dev))
+        rows_mark(mask, rows, 1, bits=bits)
+        inv = 1.0 / (L + 1)
+        H = torch.empty_like(G)
+        # H_L = (A^T G + G) / (L + 1): G is zero outside the rows -> gathered only there
+        spmm_sparse_upstream(at, bits, G, H, alpha=0.5 if L == 1 else inv, beta1=0.5 if L == 1 else inv)
+        rows_mark(mask, rows, 0, bits=bits)
+        if L == 1:
+            return None, H, None, None
+        H2 = torch.empty_like(G)
+        for _ in range(1, L):
+            spmm_launch(at, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
+            H, H2 = H2, H
+        return None, H, None, None
+
+
+def propagate_rows(adj: Adjacency, ego: torch.Tensor, n_layers: int, rows) -> torch.Tensor:
+    """mean([ego, A ego, ..., A^L ego]) evaluated at the listed rows only ([(ids, offset), ...], up
+    to three segments) -- the table is valid there and nowhere else; the gradient flowing back must
+    be zero outside those rows (a BPR / EmbLoss on them).  fp32, d = 64 on the GPU, non-deterministic
+    mode; otherwise the full propagate_mean."""
+    if (n_layers >= 1 and ego.is_cuda and ego.dtype == torch.float32 and ego.shape[1] == 64 and not _DETERMINISTIC
+            and adj.shape[0] == adj.shape[1] and 1 <= len(rows) <= 3):
+        rows = [(ids.reshape(-1).to(torch.int64).contiguous(), int(off)) for ids, off in rows]
+        return _PropagateRows.apply(adj, ego, int(n_layers), rows)
+    return propagate_mean(adj, ego, n_layers)
+
+
 def propagate_lo(adj: Adjacency, lo: torch.Tensor, hi: torch.Tensor, n_layers: int) -> torch.Tensor:
     """Rows [0, len(lo)) of mean([E, A E, ..., A^L E]), E = [lo ; hi], for an adjacency marked
     bipartite at len(lo) (fp32, d = 64 on the GPU); otherwise the full propagation, split."""
@@ -532,7 +598,7 @@ def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = 
                                                 native.stream_of(mask)), "fr_rows_mark_zero")
 
 
-SPARSE_UPSTREAM_MAX_ROWS = 262144
+SPARSE_UPSTREAM_MAX_ROWS = 262144  # HealthRec's UI backward: bitmask in LDS up to here
 
 
 def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, Y2_hi=None, split=0,
@@ -542,8 +608,8 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
     (non-deterministic mode only)."""
     native.require_device(X, bits)
     N = adj.shape[0]
-    if adj.shape[1] != N or X.shape[1] != 64 or X.shape[0] < N or N > SPARSE_UPSTREAM_MAX_ROWS:
-        raise native.EngineError("spmm_sparse_upstream: square adjacency, X [rows, 64], rows <= 262,144")
+    if adj.shape[1] != N or X.shape[1] != 64 or X.shape[0] < N:
+        raise native.EngineError("spmm_sparse_upstream: square adjacency, X [rows, 64]")
     if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32:
         raise native.EngineError("spmm_sparse_upstream: bits must be int32 with ceil(rows / 32) words")
     _check_tab("Y2", Y2, Y2_hi, split, N, 64)

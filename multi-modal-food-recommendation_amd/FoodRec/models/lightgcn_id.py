@@ -71,10 +71,12 @@ class LightGCN_ID(GeneralRecommender):
         return out[:self.n_users], out[self.n_users:]
 
     def calculate_loss(self, batch_data):
-        out = ops.propagate_mean(self.norm_adj_matrix, self.ego, self.n_layers)
         U = self.n_users
-        mf, emb = ops.bpr_emb_loss(out, out, self.ego, self.ego, batch_data["u_id"], batch_data["pos_i_id"] + U,
-                                   batch_data["neg_i_id"] + U)
+        u, p, n = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
+        # the loss reads the propagated table at the batch's users and items only: the last layer is
+        # evaluated there and the backward starts from those rows (ops.propagate_rows)
+        out = ops.propagate_rows(self.norm_adj_matrix, self.ego, self.n_layers, [(u, 0), (p, U), (n, U)])
+        mf, emb = ops.bpr_emb_loss(out, out, self.ego, self.ego, u, p + U, n + U)
         return mf, self.reg_weight * emb
 
     def full_sort_predict(self, batch_data):

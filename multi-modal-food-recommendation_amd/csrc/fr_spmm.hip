@@ -306,27 +306,32 @@ constexpr int kSpRows = 64;
 constexpr int kSpRound = 1024;
 constexpr int kSpMaxWords = 8192;  // bitmask in LDS (dynamic, ceil(n / 32) words): up to 262,144 rows
 
+// GBITS: the bitmask is read from global memory (L2-resident: ceil(n / 32) words, 1.4 MB at 11M
+// rows) instead of being staged in LDS -- graphs beyond 262,144 rows (config 4).
+template <bool GBITS>
 __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int64_t n_rows,
                                                           const uint32_t* __restrict__ bits, int nwords,
                                                           const float4* __restrict__ X, int64_t ldx4, Epi ep) {
   constexpr int KS = kSpRound / 256;  // edges per thread per round
-  extern __shared__ uint32_t sbits[];
+  extern __shared__ uint32_t sbits_dyn[];
+  const uint32_t* sbits = GBITS ? bits : sbits_dyn;
   __shared__ float4 acc[kSpRows][16];
   __shared__ int64_t srp[kSpRows + 1];
-  __shared__ int hit_c[kSpRound];    // (edge - round base) << 18 | column (columns < 2^18)
-  __shared__ float hit_v[kSpRound];  // the edge's value
+  __shared__ int hit_c[kSpRound];    // the edge's column
+  __shared__ short hit_e[kSpRound];  // its offset in the round
+  __shared__ float hit_v[kSpRound];  // its value
   __shared__ int cnt[KS * 4];        // hits per (k, wave) slice of the round
   const int t = threadIdx.x, q = t & 15, lane = t & 63, wave = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
   const int nr = (int)min<int64_t>(kSpRows, n_rows - r0);
-  {  // stage the bitmask: 16-B loads, all in flight before the LDS stores
+  if constexpr (!GBITS) {  // stage the bitmask: 16-B loads, all in flight before the LDS stores
     const int n4 = nwords >> 2;
     const uint4* b4 = reinterpret_cast<const uint4*>(bits);
 #pragma unroll 8
-    for (int w = t; w < n4; w += 256) reinterpret_cast<uint4*>(sbits)[w] = b4[w];
-    if (t < (nwords & 3)) sbits[(n4 << 2) + t] = bits[(n4 << 2) + t];
+    for (int w = t; w < n4; w += 256) reinterpret_cast<uint4*>(sbits_dyn)[w] = b4[w];
+    if (t < (nwords & 3)) sbits_dyn[(n4 << 2) + t] = bits[(n4 << 2) + t];
   }
   for (int i = t; i < kSpRows * 16; i += 256) acc[i >> 4][i & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i = t; i <= nr; i += 256) srp[i] = rowptr[r0 + i];
@@ -365,7 +370,8 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
       if ((bal[k] >> lane) & 1ull) {
         const int slot = off[k] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
-        hit_c[slot] = (k * 256 + t) << 18 | cs[k];
+        hit_c[slot] = cs[k];
+        hit_e[slot] = (short)(k * 256 + t);
         hit_v[slot] = vs[k];
       }
     }
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
     if (h_lo < h_hi) {
       int rl = 0;
       {  // row of the first hit: srp[rl] <= e < srp[rl + 1]
-        const int64_t e = base + (hit_c[h_lo] >> 18);
+        const int64_t e = base + hit_e[h_lo];
         int hi = nr;
         while (hi - rl > 1) {
           const int mid = (rl + hi) >> 1;
@@ -392,10 +398,9 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int h = min(h0 + j, h_hi - 1);
-          const int hc = hit_c[h];
-          eo[j] = hc >> 18;
+          eo[j] = hit_e[h];
           v[j] = hit_v[h];
-          x[j] = X[(int64_t)(hc & 0x3FFFF) * ldx4 + q];
+          x[j] = X[(int64_t)hit_c[h] * ldx4 + q];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -777,7 +782,7 @@ extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d
                                        int64_t n_rows, const uint32_t* d_bits, const float* d_X, int64_t ldx,
                                        int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
                                        void* stream) {
-  FR_REQUIRE(n_rows >= 0 && n_rows <= (int64_t)kSpMaxWords * 32, "n_rows out of range (<= 262,144)");
+  FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX, "n_rows out of range");
   if (n_rows == 0) return FR_OK;
   FR_REQUIRE(d_rowptr && d_col && d_val && d_bits && d_X && Y2 && Y2->lo, "null operand");
   FR_REQUIRE(fr::aligned16(d_bits), "bits must be 16-B aligned");
@@ -787,10 +792,14 @@ extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d
   Epi ep{Tab{nullptr, 0, nullptr, 0}, host_tab(Y2), alpha, host_tab(A1), beta1, Tab{nullptr, 0, nullptr, 0}, 0.f,
          split, nullptr};
   const int nwords = (int)fr::ceil_div(n_rows, 32);
-  hipLaunchKernelGGL(spmm_sparse_kernel, dim3((unsigned)fr::ceil_div(n_rows, kSpRows)), dim3(256),
-                     (size_t)nwords * sizeof(uint32_t),
-                     reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
-                     reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
+  const dim3 grid((unsigned)fr::ceil_div(n_rows, kSpRows));
+  if (nwords <= kSpMaxWords)  // bitmask staged in LDS
+    hipLaunchKernelGGL(spmm_sparse_kernel<false>, grid, dim3(256), (size_t)nwords * sizeof(uint32_t),
+                       reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
+                       reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
+  else
+    hipLaunchKernelGGL(spmm_sparse_kernel<true>, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_rowptr,
+                       d_col, d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -170,6 +170,38 @@ def test_propagate_lo_matches_full(cuda, L):
     assert torch.all(gb_hi[NS:] == 0)
 
 
+@pytest.mark.parametrize("N,L", [(3000, 2), (300_000, 2), (300_000, 1), (5000, 3)])
+def test_propagate_rows_matches_full(cuda, N, L):
+    """ops.propagate_rows (LightGCN_ID's loss rows: last layer at the batch rows, backward from the
+    sparse upstream gradient) vs propagate_mean: the listed rows' values and the ego gradient of a
+    loss on those rows (duplicate ids included).  N > 262,144 exercises the sparse launch with its
+    bitmask in L2 instead of LDS."""
+    from FoodRec.engine import ops
+    rng = np.random.default_rng(N + L)
+    r, c = _graph(N, N, 4, heavy=[(5, 3000)], seed=N)
+    adj = _adj(N, r, c, cuda, chunk=256)
+    ego0 = torch.randn(N, 64, device=cuda)
+    U = N // 2
+    u = torch.as_tensor(rng.integers(0, U, 200), device=cuda)
+    p = torch.as_tensor(rng.integers(0, N - U, 200), device=cuda)
+    n = torch.as_tensor(rng.integers(0, N - U, 200), device=cuda)
+    u[:3] = 5  # the heavy row
+    u[:10] = u[10]  # duplicates
+    idx = torch.cat([u, p + U, n + U])
+    w = torch.randn(idx.numel(), 64, device=cuda)
+    res = []
+    for fast in (False, True):
+        ego = ego0.clone().requires_grad_(True)
+        out = (ops.propagate_rows(adj, ego, L, [(u, 0), (p, U), (n, U)]) if fast
+               else ops.propagate_mean(adj, ego, L))
+        rows = out[idx]
+        (rows * w).sum().backward()
+        res.append((rows.detach(), ego.grad))
+    (a, ga), (b, gb) = res
+    torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gb, ga, rtol=1e-5, atol=1e-6 * float(ga.abs().max()))
+
+
 def test_spmm_deterministic(cuda):
     from FoodRec.engine import ops
     n = 2000
