@@ -261,6 +261,9 @@ def main():
         torch.cuda.empty_cache()
         if world == 1:
             c4 = config4(device)
+            # the row-sharded step at P = 1 (no collectives): the denominator of the N-GPU runs'
+            # config4_10m line (the driver's multi-GPU bench runs config4_sharded at P = N)
+            c4["sharded_p1"] = config4_sharded(device, 1, 0)
         else:
             c4 = config4_sharded(device, world, rank)
     c5 = None
@@ -647,9 +650,13 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
     cfg = Config("LightGCN_ID", "Synthetic10M", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
                                                  "ckp_root": "/tmp/frckp/"})
     cfg["device"] = device
-    model = ShardedLightGCN(g, d, 2, 0.1, group=dist.group.WORLD, seed=999)
+    dist_on = world > 1 or (dist.is_available() and dist.is_initialized())
+    sync = (lambda: dist.barrier()) if dist_on else (lambda: None)  # noqa: E731
+    model = ShardedLightGCN(g, d, 2, 0.1, group=dist.group.WORLD if dist_on else None, seed=999)
     trainer = Trainer(cfg, model)
     P_local = sum(p.numel() for p in model.parameters())
+    deg_u = g.A_ui.rowptr[1:] - g.A_ui.rowptr[:-1]   # this rank's users (global degrees)
+    deg_i = g.A_iu.rowptr[1:] - g.A_iu.rowptr[:-1]   # items, this rank's share of their degrees
     out_steps = {}
     for B in batches:
         state = trainer.new_step_state()
@@ -661,31 +668,47 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
         for k in range(warmup):
             step(k)
         torch.cuda.synchronize()
-        dist.barrier()
+        sync()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(steps):
             step(warmup + k)
         torch.cuda.synchronize()
-        dist.barrier()
+        sync()
         torch.cuda.synchronize()
         t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if dist_on:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item()) / steps
         assert not int(state["nan"].item()), "NaN loss in the sharded config-4 step"
+        # global degree sum of the loss rows (owned users' degrees + every rank's share of the items')
+        ds = torch.zeros(1, dtype=torch.float64, device=device)
+        for k in range(4):
+            uu, pp, nn_ = g.triples(B, 999, 1000 + k)
+            own, loc = g.owner_index(uu)
+            ds += (deg_u[loc[own]].sum() + deg_i[pp].sum() + deg_i[nn_].sum()).double()
+        if dist_on:
+            dist.all_reduce(ds)
+        deg_rows = int(ds.item() / 4)
         # the single-GPU byte model of the whole step (work is divided, not changed, by sharding)
-        bstep, _ = config4_bytes_per_step(U + I, 2 * g.n_edges, (U + I) * d, B)
+        bstep = config4_bytes_rows(U + I, 2 * g.n_edges, (U + I) * d, B, deg_rows)
         out_steps[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
-                             "bytes_per_step_global": bstep,
+                             "bytes_per_step_global": bstep, "loss_rows_degree_sum": deg_rows,
                              "achieved_gbps_per_gpu": round(bstep / dt / 1e9 / world, 1),
                              "roofline_frac_per_gpu": round(bstep / dt / 1e9 / world / HBM_PEAK_GBPS, 4)}
     nnz = torch.tensor([g.local_nnz], device=device, dtype=torch.float64)
-    nnz_all = [torch.zeros_like(nnz) for _ in range(world)]
-    dist.all_gather(nnz_all, nnz)
+    if dist_on:
+        nnz_all = [torch.zeros_like(nnz) for _ in range(world)]
+        dist.all_gather(nnz_all, nnz)
+    else:
+        nnz_all = [nnz]
     out = {"graph": "synthetic U=10M I=1M E=%d, row-sharded over %d ranks (built in %.1f s)"
                     % (g.n_edges, world, build_s),
-           "model": "LightGCN_ID row-sharded (users in nnz-balanced blocks, items replicated)",
-           "collectives_per_step": "2L=4 all-reduces of I x d fp32 (256 MB) + 2 B x d gathers",
+           "model": "LightGCN_ID row-sharded (users in nnz-balanced blocks, items replicated), rows form",
+           "collectives_per_step": "3 all-reduces of I x d fp32 (256 MB; the forward's and the last backward "
+                                   "layer's cut into item-row blocks) + one of the 2B batch item rows + 2 B x d "
+                                   "owner gathers",
+           "byte_model": "config4_bytes_rows (the single-GPU step's algorithmic bytes)",
            "local_params_rank0": P_local, "local_nnz_per_rank": [int(x.item()) for x in nnz_all],
            "steps_timed": steps, "step": out_steps}
     del trainer, model, g

@@ -644,6 +644,12 @@ int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
                       uint32_t* d_bits, void* stream);
+/* fr_spmm_sparse_upstream over a rectangular slice [n_rows x n_cols] (the row-sharded config-4
+ * step's A_ui / A_iu, engine/sharded.py): the bitmask (ceil(n_cols / 32) words, read from L2) marks
+ * the non-zero rows of X (the slice's columns); A1 is read at every output row (no gate). */
+int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                                 int64_t n_cols, const uint32_t* d_bits, const float* d_X, int64_t ldx,
+                                 const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, void* stream);
 int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
                             const uint32_t* d_bits, const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2,
                             float alpha, const fr_tab* A1, float beta1, void* stream);

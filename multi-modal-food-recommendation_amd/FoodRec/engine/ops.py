@@ -620,6 +620,24 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
             native.stream_of(X)), "fr_spmm_sparse_upstream")
 
 
+def spmm_sparse_rect(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, alpha=1.0, A1=None, beta1=0.0,
+                     region="spmm_masked"):
+    """fr_spmm_sparse_upstream_rect: Y2 = alpha A X + beta1 A1 over a rectangular [rows x cols]
+    slice, X non-zero only at the rows of X marked in ``bits`` (int32 words over cols) and read only
+    there; A1 (optional) read at every row.  d = 64; float-atomic summation order."""
+    native.require_device(X, bits)
+    R, C = adj.shape
+    if X.shape[1] != 64 or X.shape[0] < C or bits.dtype != torch.int32 or bits.numel() < (C + 31) // 32:
+        raise native.EngineError("spmm_sparse_rect: X [cols, 64] and int32 bits over the columns required")
+    _check_tab("Y2", Y2, None, 0, R, 64)
+    _check_tab("A1", A1, None, 0, R, 64)
+    with profiling.region(region, 0):
+        native.check(native.lib().fr_spmm_sparse_upstream_rect(
+            adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), R, C, bits.data_ptr(), X.data_ptr(),
+            X.stride(0), ctypes.byref(_tab(Y2)), _f(alpha), ctypes.byref(_tab(A1)), _f(beta1),
+            native.stream_of(X)), "fr_spmm_sparse_upstream_rect")
+
+
 def _adjacent_rows(lo, hi, rows):
     """[lo ; hi] as one [rows, d] view when hi's rows follow lo's in memory (same storage, contiguous
     row-major: a model placed them so, e.g. HealthRec.engine_layout), else None."""

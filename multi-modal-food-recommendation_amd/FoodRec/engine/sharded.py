@@ -261,6 +261,83 @@ class _ShardedPropagate(torch.autograd.Function):
         return Hu, Hi, None, None, None
 
 
+def _marks(g, key, n, dev):
+    """Persistent (uint8 mask, int32 bitmask) over ``n`` rows, kept on the graph (all clear between uses)."""
+    cache = g.__dict__.setdefault("_marks", {})
+    m = cache.get(key)
+    if m is None:
+        m = (torch.zeros(n, dtype=torch.uint8, device=dev), torch.zeros((n + 31) // 32, dtype=torch.int32, device=dev))
+        cache[key] = m
+    return m
+
+
+class _ShardedPropagateRows(torch.autograd.Function):
+    """_ShardedPropagate (L = 2) for a loss that reads the propagated tables at the batch rows only
+    (the rows form of ops.propagate_rows, single-GPU config 4):
+      forward   layer 1 in full (item partial + all-reduce, user SpMM); layer 2 only at this rank's
+                batch users (row list; users owned elsewhere carry id -1) and at the batch items (row
+                list on the transpose slice, the 2B partial rows all-reduced: 2B x d instead of I x d);
+      backward  the first layer from the sparse upstream gradients (users: A_ui at the batch items'
+                columns, items: A_iu at this rank's batch users' columns, then one full item
+                all-reduce), the second in full as before.
+    Collectives per step: 3 item all-reduces of I x d (was 4) + one of 2B x d.  Results are valid at
+    the batch rows only."""
+
+    @staticmethod
+    def forward(ctx, ego_u, ego_i, g: ShardedGraph, group, loc, p, n):
+        inv = 1.0 / 3.0
+        ctx.g, ctx.group = g, group
+        pi1 = torch.empty_like(ego_i)
+        works = _item_partial(g, ego_u, pi1, group)               # E_i^1, reduce in flight
+        E1u = torch.empty_like(ego_u)
+        ops.spmm_launch(g.A_ui, ego_i, Y1=E1u)                   # E_u^1 (local)
+        _wait(works)
+        out_u = torch.empty_like(ego_u)                           # valid at this rank's batch users
+        ops.spmm_ex(g.A_ui, pi1, Y2=out_u, alpha=inv, A1=ego_u, beta1=inv, A2=E1u, beta2=inv, rows=[(loc, 0)],
+                    region="spmm_rows")
+        pi2 = torch.empty_like(ego_i)                             # valid at the batch items
+        ops.spmm_ex(g.A_iu, E1u, Y1=pi2, rows=[(p, 0), (n, 0)], region="spmm_rows")
+        pn = torch.cat([p, n])
+        part = pi2.index_select(0, pn)
+        _all_reduce(part, group)
+        out_i = torch.empty_like(ego_i)                           # valid at the batch items
+        out_i.index_copy_(0, pn, (ego_i.index_select(0, pn) + pi1.index_select(0, pn) + part) * inv)
+        ctx.save_for_backward(loc, p, n)
+        return out_u, out_i
+
+    @staticmethod
+    def backward(ctx, g_u, g_i):
+        g, group = ctx.g, ctx.group
+        loc, p, n = ctx.saved_tensors
+        inv = 1.0 / 3.0
+        dev = loc.device
+        g_u = g_u.contiguous() if g_u is not None else torch.zeros(g.n_local, 64, device=dev)
+        g_i = g_i.contiguous() if g_i is not None else torch.zeros(g.n_items, 64, device=dev)
+        # items of the first backward layer: this rank's A_iu at its batch users, then the full reduce
+        mu, bu = _marks(g, "users", g.n_local, dev)
+        ops.rows_mark(mu, [(loc, 0)], 1, bits=bu)
+        piH = torch.empty_like(g_i)
+        ops.spmm_sparse_rect(g.A_iu, bu, g_u, piH, alpha=1.0)
+        ops.rows_mark(mu, [(loc, 0)], 0, bits=bu)
+        work = _all_reduce(piH, group, async_op=True)
+        # users of the first backward layer (local): A_ui at the batch items' columns
+        mi, bi = _marks(g, "items", g.n_items, dev)
+        ops.rows_mark(mi, [(p, 0), (n, 0)], 1, bits=bi)
+        Hu = torch.empty_like(g_u)
+        ops.spmm_sparse_rect(g.A_ui, bi, g_i, Hu, alpha=inv, A1=g_u, beta1=inv)
+        ops.rows_mark(mi, [(p, 0), (n, 0)], 0, bits=bi)
+        _wait([work])
+        Hi = piH.mul_(inv).add_(g_i, alpha=inv)
+        # second layer in full
+        pi = torch.empty_like(g_i)
+        works = _item_partial(g, Hu, pi, group)
+        d_u = torch.empty_like(g_u)
+        ops.spmm_launch(g.A_ui, Hi, Y2=d_u, alpha=1.0, A1=g_u, beta1=inv)
+        _wait(works)
+        d_i = pi.add_(g_i, alpha=inv)
+        return d_u, d_i, None, None, None, None, None
+
+
 class _OwnerGather(torch.autograd.Function):
     """rows[b] = local_table[loc[b]] on the owning rank, assembled on every rank by one all-reduce
     (exactly one rank contributes each row).  Backward: every rank holds the full gradient of the
@@ -301,8 +378,14 @@ class ShardedLightGCN(nn.Module):
 
     def calculate_loss(self, batch):
         u, p, n = batch["u_id"], batch["pos_i_id"], batch["neg_i_id"]
-        out_u, out_i = _ShardedPropagate.apply(self.ego_u, self.ego_i, self.g, self.L, self.group)
         _, loc = self.g.owner_index(u)
+        if self.L == 2 and self.ego_u.is_cuda and self.d == 64 and not ops._DETERMINISTIC:
+            # the loss reads the propagated tables at the batch rows only (rows form)
+            p, n = p.to(torch.int64).contiguous(), n.to(torch.int64).contiguous()
+            out_u, out_i = _ShardedPropagateRows.apply(self.ego_u, self.ego_i, self.g, self.group,
+                                                       loc.contiguous(), p, n)
+        else:
+            out_u, out_i = _ShardedPropagate.apply(self.ego_u, self.ego_i, self.g, self.L, self.group)
         out_ub = _OwnerGather.apply(out_u, loc, self.group)
         ego_ub = _OwnerGather.apply(self.ego_u, loc, self.group)
         B = u.numel()

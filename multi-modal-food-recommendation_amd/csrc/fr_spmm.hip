@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kRowThreads) void spmm_rows_kernel(
   int64_t idx = blockIdx.x;
   int seg = 0;
   while (seg < 3 && idx >= rl.n[seg]) idx -= rl.n[seg++];
-  if (seg >= 3) return;
+  if (seg >= 3 || rl.ids[seg][idx] < 0) return;  // a negative id: no row (e.g. a batch user owned elsewhere)
   const int64_t row = rl.ids[seg][idx] + rl.off[seg];
   const int64_t rs = rowptr[row], re = rowptr[row + 1];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -274,6 +274,7 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ ma
     const int q = (int)(i % per);
     int seg = 0;
     while (idx >= rl.n[seg]) idx -= rl.n[seg++];
+    if (rl.ids[seg][idx] < 0) continue;  // negative ids name no row
     const int64_t row = rl.ids[seg][idx] + rl.off[seg];
     if (q == 0) mask[row] = value;
     if (q == 0 && bits) {
@@ -308,7 +309,9 @@ constexpr int kSpMaxWords = 8192;  // bitmask in LDS (dynamic, ceil(n / 32) word
 
 // GBITS: the bitmask is read from global memory (L2-resident: ceil(n / 32) words, 1.4 MB at 11M
 // rows) instead of being staged in LDS -- graphs beyond 262,144 rows (config 4).
-template <bool GBITS>
+// UNGATED (a rectangular slice: the bitmask marks X's rows, i.e. columns, not output rows): A1 is
+// read at every output row.
+template <bool GBITS, bool UNGATED = false>
 __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int64_t n_rows,
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
     const int rl = i >> 4;
     const int64_t r = r0 + rl;
     float4 o = f4_scale(ep.alpha, acc[rl][q]);
-    if (ep.A1.lo && ((sbits[r >> 5] >> (r & 31)) & 1u))
+    if (ep.A1.lo && (UNGATED || ((sbits[r >> 5] >> (r & 31)) & 1u)))
       o = f4_fma(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q], o);
     reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
   }
@@ -774,6 +777,28 @@ extern "C" int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_
   const int64_t blocks = std::min<int64_t>(fr::ceil_div(work, (int64_t)256), (int64_t)fr::kNumCU * 4);
   hipLaunchKernelGGL(rows_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      d_mask, rl, total, value, reinterpret_cast<float4*>(d_Z), ldz / 4, d / 4, d_bits);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                            int64_t n_rows, int64_t n_cols, const uint32_t* d_bits, const float* d_X,
+                                            int64_t ldx, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
+                                            void* stream) {
+  FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX && n_cols >= 0 && n_cols < (int64_t)INT32_MAX,
+             "n_rows / n_cols out of range");
+  if (n_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && d_col && d_val && d_bits && d_X && Y2 && Y2->lo, "null operand");
+  FR_REQUIRE(fr::aligned16(d_bits), "bits must be 16-B aligned");
+  FR_REQUIRE(ldx >= 64 && ldx % 4 == 0 && fr::aligned16(d_X) && tab_ok(Y2, 64) && tab_ok(A1, 64),
+             "X / Y2 / A1 must be 16-B aligned fp32 [*, 64] tables");
+  FR_REQUIRE(!(tab_touches(Y2, d_X)), "Y2 must not alias X");
+  Epi ep{Tab{nullptr, 0, nullptr, 0}, host_tab(Y2), alpha, host_tab(A1), beta1, Tab{nullptr, 0, nullptr, 0}, 0.f,
+         0, nullptr};
+  const int nwords = (int)fr::ceil_div(std::max<int64_t>(n_cols, 1), 32);
+  hipLaunchKernelGGL((spmm_sparse_kernel<true, true>), dim3((unsigned)fr::ceil_div(n_rows, kSpRows)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
+                     reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
