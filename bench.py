@@ -320,15 +320,18 @@ def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4, adam=28):
     return 2 * L * b_spmm + 2 * (L + 1) * N * d * s + adam * P + B * (3 * 8 + 3 * d * s) * 2, b_spmm
 
 
-def config4_bytes_rows(N, nnz, P, B, deg_rows, d=64, s=4, adam=28):
+def config4_bytes_rows(N, nnz, P, B, deg_rows, layer1=None, d=64, s=4, adam=28):
     """Algorithmic bytes of the LightGCN-ID step as the engine runs it (L = 2, ops.propagate_rows):
-    layer 1 over the full graph; layer 2 only at the 3B loss rows (their edges: ``deg_rows`` = the sum
-    of their degrees); BPR + EmbLoss with a dense zero-filled gradient table; the backward's first
-    layer as the sparse-upstream launch (all col/val scanned, X gathered at the hits, H written in
-    full); its second layer over the full graph (+ the G addend); Adam over every parameter."""
+    layer 1 over the full graph, or (``layer1`` = (rows, edges) it covers) over the user block plus
+    the items layer 2 reads; layer 2 only at the 3B loss rows (their edges: ``deg_rows`` = the sum of
+    their degrees); BPR + EmbLoss with a dense zero-filled gradient table; the backward's first layer
+    as the sparse-upstream launch (all col/val scanned, X gathered at the hits, H written in full);
+    its second layer over the full graph (+ the G addend); Adam over every parameter."""
     b_full = 8 * (N + 1) + nnz * 8 + nnz * d * s + N * d * s
+    l1_rows, l1_edges = layer1 if layer1 is not None else (N, nnz)
+    b_l1 = 8 * (l1_rows + 1) + l1_edges * 8 + l1_edges * d * s + l1_rows * d * s
     rows = 3 * B
-    fwd = b_full + 16 * rows + deg_rows * (8 + d * s) + rows * d * s * 3
+    fwd = b_l1 + 16 * rows + deg_rows * (8 + d * s) + rows * d * s * 3
     loss = B * (3 * 8 + 3 * d * s) * 2 + N * d * s  # + the dense gradient table's zero fill
     bwd = (8 * (N + 1) + 8 * nnz + deg_rows * d * s + N * d * s + rows * d * s) + (b_full + N * d * s)
     return fwd + loss + bwd + adam * P
@@ -568,16 +571,21 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
         assert not int(state["nan"].item()), "NaN loss in the config-4 step"
         # the loss rows' degree sum, averaged over 8 sampled batches (same sampler)
         deg = adj.rowptr[1:] - adj.rowptr[:-1]
-        dsum = 0
+        dsum = l1r = l1e = 0
         for _ in range(8):
             u, p, n = g.triples(B)
             dsum += int(torch.cat([deg[u], deg[p + U], deg[n + U]]).sum().item())
+            S = ops._bipartite_layer1_rows(adj, [(u, 0), (p, U), (n, U)], U)  # layer 1's item rows
+            l1r += int(S.numel())
+            l1e += int(deg[S].sum().item())
         del deg
         deg_rows = dsum // 8
-        bstep = config4_bytes_rows(N, adj.nnz, P, B, deg_rows)
+        layer1 = (U + l1r // 8, adj.nnz_below_split + l1e // 8)
+        bstep = config4_bytes_rows(N, adj.nnz, P, B, deg_rows, layer1)
         dense_eq, _ = config4_bytes_per_step(N, adj.nnz, P, B)
         steps_out[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
                              "bytes_per_step": bstep, "loss_rows_degree_sum": deg_rows,
+                             "layer1_rows_edges": list(layer1),
                              "achieved_gbps": round(bstep / dt / 1e9, 1),
                              "roofline_frac": round(bstep / dt / 1e9 / HBM_PEAK_GBPS, 4),
                              "roofline_triples_per_s": round(B / (bstep / (HBM_PEAK_GBPS * 1e9)), 1),
@@ -682,16 +690,26 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
         dt = float(t.item()) / steps
         assert not int(state["nan"].item()), "NaN loss in the sharded config-4 step"
         # global degree sum of the loss rows (owned users' degrees + every rank's share of the items')
-        ds = torch.zeros(1, dtype=torch.float64, device=device)
+        from FoodRec.engine.sharded import _neighbour_items
+        ds = torch.zeros(3, dtype=torch.float64, device=device)  # loss rows' degrees, |S|, S's degrees
         for k in range(4):
             uu, pp, nn_ = g.triples(B, 999, 1000 + k)
             own, loc = g.owner_index(uu)
-            ds += (deg_u[loc[own]].sum() + deg_i[pp].sum() + deg_i[nn_].sum()).double()
+            flags = torch.zeros(I, dtype=torch.float32, device=device)
+            flags[_neighbour_items(g, loc)] = 1.0
+            flags[torch.cat([pp, nn_])] = 1.0
+            if dist_on:
+                dist.all_reduce(flags)
+            S = torch.nonzero(flags > 0).reshape(-1)
+            ds[0] += (deg_u[loc[own]].sum() + deg_i[pp].sum() + deg_i[nn_].sum()).double()
+            ds[1] += float(S.numel()) / (world if dist_on else 1)
+            ds[2] += deg_i[S].sum().double()
         if dist_on:
             dist.all_reduce(ds)
-        deg_rows = int(ds.item() / 4)
+        deg_rows = int(ds[0].item() / 4)
+        layer1 = (U + int(ds[1].item() / 4), g.n_edges + int(ds[2].item() / 4))
         # the single-GPU byte model of the whole step (work is divided, not changed, by sharding)
-        bstep = config4_bytes_rows(U + I, 2 * g.n_edges, (U + I) * d, B, deg_rows)
+        bstep = config4_bytes_rows(U + I, 2 * g.n_edges, (U + I) * d, B, deg_rows, layer1)
         out_steps[str(B)] = {"ms_per_step": round(dt * 1e3, 3), "triples_per_s": round(B / dt, 1),
                              "bytes_per_step_global": bstep, "loss_rows_degree_sum": deg_rows,
                              "achieved_gbps_per_gpu": round(bstep / dt / 1e9 / world, 1),

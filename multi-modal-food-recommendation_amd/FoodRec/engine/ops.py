@@ -227,7 +227,17 @@ class _PropagateRows(torch.autograd.Function):
             spmm_ex(adj, ego, Y2=out, alpha=0.5, A1=ego, beta1=0.5, rows=rows, region="spmm_rows")
         elif L == 2:
             E1 = torch.empty_like(ego)
-            spmm_launch(adj, ego, Y1=E1)
+            s = adj.bipartite_split
+            if s is not None:
+                # layer 1 is read at the loss rows R and their neighbours: the [0, s) block in full (the
+                # neighbours of R's high rows span it) and the [s, n) block only at R's high rows and
+                # the neighbours of its low rows (fewer rows than the block)
+                S = _bipartite_layer1_rows(adj, rows, s)
+                spmm_range(adj, ego, 0, s, Y1=E1)
+                if S.numel():
+                    spmm_ex(adj, ego, Y1=E1, rows=[(S, 0)], region="spmm_rows")
+            else:
+                spmm_launch(adj, ego, Y1=E1)
             spmm_ex(adj, E1, Y2=out, alpha=inv, A1=ego, beta1=inv, A2=E1, beta2=inv, rows=rows, region="spmm_rows")
         else:
             S, E1 = torch.empty_like(ego), torch.empty_like(ego)
@@ -261,6 +271,23 @@ class _PropagateRows(torch.autograd.Function):
             spmm_launch(at, H, Y2=H2, alpha=1.0, A1=G, beta1=inv)
             H, H2 = H2, H
         return None, H, None, None
+
+
+def _bipartite_layer1_rows(adj: Adjacency, rows, s: int) -> torch.Tensor:
+    """Rows >= s of a bipartite adjacency (split s) that a row-list layer 2 at ``rows`` reads layer 1
+    at: the listed rows >= s and the columns of the listed rows < s (sorted, unique)."""
+    ids = torch.cat([ids + off for ids, off in rows])
+    lo = ids[ids < s]
+    hi = ids[ids >= s]
+    rp = adj.rowptr
+    starts = rp[lo]
+    lens = rp[lo + 1] - starts
+    total = int(lens.sum().item())
+    if total:
+        first = torch.cumsum(lens, 0) - lens
+        pos = torch.repeat_interleave(starts - first, lens) + torch.arange(total, device=ids.device)
+        hi = torch.cat([hi, adj.col[pos].to(torch.int64)])
+    return torch.unique(hi)
 
 
 def propagate_rows(adj: Adjacency, ego: torch.Tensor, n_layers: int, rows) -> torch.Tensor:

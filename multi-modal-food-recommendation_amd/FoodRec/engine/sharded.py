@@ -271,55 +271,87 @@ def _marks(g, key, n, dev):
     return m
 
 
+def _neighbour_items(g: ShardedGraph, loc: torch.Tensor) -> torch.Tensor:
+    """Item columns of this rank's batch users (rows ``loc`` >= 0 of A_ui), duplicates kept."""
+    own = loc[loc >= 0]
+    rp = g.A_ui.rowptr
+    starts, ends = rp[own], rp[own + 1]
+    lens = ends - starts
+    total = int(lens.sum().item())
+    if total == 0:
+        return torch.zeros(0, dtype=torch.int64, device=loc.device)
+    first = torch.cumsum(lens, 0) - lens
+    pos = torch.repeat_interleave(starts - first, lens) + torch.arange(total, device=loc.device)
+    return g.A_ui.col[pos].to(torch.int64)
+
+
 class _ShardedPropagateRows(torch.autograd.Function):
     """_ShardedPropagate (L = 2) for a loss that reads the propagated tables at the batch rows only
-    (the rows form of ops.propagate_rows, single-GPU config 4):
-      forward   layer 1 in full (item partial + all-reduce, user SpMM); layer 2 only at this rank's
-                batch users (row list; users owned elsewhere carry id -1) and at the batch items (row
-                list on the transpose slice, the 2B partial rows all-reduced: 2B x d instead of I x d);
+    (the rows form of ops.propagate_rows, single-GPU config 4).  The item table of layer 1 is needed
+    only at S = the items adjacent to the batch users (for their layer-2 rows) plus the batch items
+    (for theirs), and the first backward layer's item rows are non-zero only on the first part of S:
+      forward   S agreed on by every rank (an all-reduce of per-item flags, then the same nonzero
+                list everywhere); layer-1 item partial at S only (row list), its |S| rows all-reduced
+                (|S| x d instead of I x d); the user layer 1 in full (local); layer 2 at this rank's
+                batch users (row list, users owned elsewhere carry id -1) and at the batch items (row
+                list on the transpose slice, the 2B partial rows all-reduced);
       backward  the first layer from the sparse upstream gradients (users: A_ui at the batch items'
-                columns, items: A_iu at this rank's batch users' columns, then one full item
-                all-reduce), the second in full as before.
-    Collectives per step: 3 item all-reduces of I x d (was 4) + one of 2B x d.  Results are valid at
-    the batch rows only."""
+                columns; items: A_iu at this rank's batch users' columns, all-reduced at S only), the
+                second in full (item partial per item-row block, all-reduced as before).
+    Collectives per step: one all-reduce of I x d (the last backward layer, in blocks) + |S| x d
+    twice + 2B x d + the flags (I floats) + 2 owner gathers.  Results valid at the batch rows only."""
 
     @staticmethod
     def forward(ctx, ego_u, ego_i, g: ShardedGraph, group, loc, p, n):
         inv = 1.0 / 3.0
         ctx.g, ctx.group = g, group
-        pi1 = torch.empty_like(ego_i)
-        works = _item_partial(g, ego_u, pi1, group)               # E_i^1, reduce in flight
-        E1u = torch.empty_like(ego_u)
-        ops.spmm_launch(g.A_ui, ego_i, Y1=E1u)                   # E_u^1 (local)
-        _wait(works)
-        out_u = torch.empty_like(ego_u)                           # valid at this rank's batch users
-        ops.spmm_ex(g.A_ui, pi1, Y2=out_u, alpha=inv, A1=ego_u, beta1=inv, A2=E1u, beta2=inv, rows=[(loc, 0)],
-                    region="spmm_rows")
-        pi2 = torch.empty_like(ego_i)                             # valid at the batch items
-        ops.spmm_ex(g.A_iu, E1u, Y1=pi2, rows=[(p, 0), (n, 0)], region="spmm_rows")
+        dev = ego_u.device
         pn = torch.cat([p, n])
-        part = pi2.index_select(0, pn)
-        _all_reduce(part, group)
-        out_i = torch.empty_like(ego_i)                           # valid at the batch items
-        out_i.index_copy_(0, pn, (ego_i.index_select(0, pn) + pi1.index_select(0, pn) + part) * inv)
-        ctx.save_for_backward(loc, p, n)
+        # fp32 flags (the C-ABI communicator reduces fp32): every rank the same sums, the same list
+        flags = torch.zeros(g.n_items, dtype=torch.float32, device=dev)
+        flags[_neighbour_items(g, loc)] = 1.0
+        flags[pn] = 1.0
+        _all_reduce(flags, group)
+        S = torch.nonzero(flags > 0).reshape(-1)
+        del flags
+        pi1 = torch.empty_like(ego_i)                              # valid at S
+        ops.spmm_ex(g.A_iu, ego_u, Y1=pi1, rows=[(S, 0)], region="spmm_rows")
+        part1 = pi1.index_select(0, S)
+        work = _all_reduce(part1, group, async_op=True)
+        E1u = torch.empty_like(ego_u)
+        ops.spmm_launch(g.A_ui, ego_i, Y1=E1u)                    # E_u^1 (local, in flight beside the reduce)
+        _wait([work])
+        E1i = pi1
+        E1i.index_copy_(0, S, part1)                               # E_i^1, valid at S
+        out_u = torch.empty_like(ego_u)                            # valid at this rank's batch users
+        ops.spmm_ex(g.A_ui, E1i, Y2=out_u, alpha=inv, A1=ego_u, beta1=inv, A2=E1u, beta2=inv, rows=[(loc, 0)],
+                    region="spmm_rows")
+        pi2 = torch.empty_like(ego_i)                              # valid at the batch items
+        ops.spmm_ex(g.A_iu, E1u, Y1=pi2, rows=[(p, 0), (n, 0)], region="spmm_rows")
+        part2 = pi2.index_select(0, pn)
+        _all_reduce(part2, group)
+        out_i = torch.empty_like(ego_i)                            # valid at the batch items
+        out_i.index_copy_(0, pn, (ego_i.index_select(0, pn) + E1i.index_select(0, pn) + part2) * inv)
+        ctx.save_for_backward(loc, p, n, S)
         return out_u, out_i
 
     @staticmethod
     def backward(ctx, g_u, g_i):
         g, group = ctx.g, ctx.group
-        loc, p, n = ctx.saved_tensors
+        loc, p, n, S = ctx.saved_tensors
         inv = 1.0 / 3.0
         dev = loc.device
         g_u = g_u.contiguous() if g_u is not None else torch.zeros(g.n_local, 64, device=dev)
         g_i = g_i.contiguous() if g_i is not None else torch.zeros(g.n_items, 64, device=dev)
-        # items of the first backward layer: this rank's A_iu at its batch users, then the full reduce
+        # items of the first backward layer: A_iu at this rank's batch users (non-zero inside S only),
+        # all-reduced at S
         mu, bu = _marks(g, "users", g.n_local, dev)
         ops.rows_mark(mu, [(loc, 0)], 1, bits=bu)
         piH = torch.empty_like(g_i)
         ops.spmm_sparse_rect(g.A_iu, bu, g_u, piH, alpha=1.0)
         ops.rows_mark(mu, [(loc, 0)], 0, bits=bu)
-        work = _all_reduce(piH, group, async_op=True)
+        partH = piH.index_select(0, S)
+        work = _all_reduce(partH, group, async_op=True)
         # users of the first backward layer (local): A_ui at the batch items' columns
         mi, bi = _marks(g, "items", g.n_items, dev)
         ops.rows_mark(mi, [(p, 0), (n, 0)], 1, bits=bi)
@@ -327,9 +359,10 @@ class _ShardedPropagateRows(torch.autograd.Function):
         ops.spmm_sparse_rect(g.A_ui, bi, g_i, Hu, alpha=inv, A1=g_u, beta1=inv)
         ops.rows_mark(mi, [(p, 0), (n, 0)], 0, bits=bi)
         _wait([work])
-        Hi = piH.mul_(inv).add_(g_i, alpha=inv)
+        Hi = g_i * inv
+        Hi.index_copy_(0, S, partH.mul_(inv).add_(Hi.index_select(0, S)))
         # second layer in full
-        pi = torch.empty_like(g_i)
+        pi = piH
         works = _item_partial(g, Hu, pi, group)
         d_u = torch.empty_like(g_u)
         ops.spmm_launch(g.A_ui, Hi, Y2=d_u, alpha=1.0, A1=g_u, beta1=inv)

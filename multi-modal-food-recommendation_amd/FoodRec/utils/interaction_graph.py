@@ -53,6 +53,7 @@ class InteractionGraph:
         self.n_edges = int(rp[n_users].item())
         self.adj = Adjacency(rp, col, val, (n_users + n_items, n_users + n_items), device=dev, chunk=chunk,
                              symmetric=True)
+        self.adj.mark_bipartite(n_users)  # users connect to items only and items to users only
         self.device = dev
         self.seed = int(seed)
         self._perm = None

@@ -170,18 +170,28 @@ def test_propagate_lo_matches_full(cuda, L):
     assert torch.all(gb_hi[NS:] == 0)
 
 
-@pytest.mark.parametrize("N,L", [(3000, 2), (300_000, 2), (300_000, 1), (5000, 3)])
-def test_propagate_rows_matches_full(cuda, N, L):
+@pytest.mark.parametrize("N,L,bip", [(3000, 2, False), (300_000, 2, False), (300_000, 1, False), (5000, 3, False),
+                                     (6000, 2, True), (300_000, 2, True)])
+def test_propagate_rows_matches_full(cuda, N, L, bip):
     """ops.propagate_rows (LightGCN_ID's loss rows: last layer at the batch rows, backward from the
     sparse upstream gradient) vs propagate_mean: the listed rows' values and the ego gradient of a
     loss on those rows (duplicate ids included).  N > 262,144 exercises the sparse launch with its
     bitmask in L2 instead of LDS."""
     from FoodRec.engine import ops
     rng = np.random.default_rng(N + L)
-    r, c = _graph(N, N, 4, heavy=[(5, 3000)], seed=N)
-    adj = _adj(N, r, c, cuda, chunk=256)
-    ego0 = torch.randn(N, 64, device=cuda)
     U = N // 2
+    if bip:  # users [0, U) <-> items [U, N) (config 4's graph): layer 1's item block at the needed rows only
+        from FoodRec.utils.interaction_graph import InteractionGraph
+        uu = rng.integers(0, U, 4 * N)
+        uu[:3000] = 5  # a heavy user row
+        g = InteractionGraph(U, N - U, pairs=(torch.as_tensor(uu), torch.as_tensor(rng.integers(0, N - U, 4 * N))),
+                             device=cuda, chunk=256)
+        adj = g.adj
+        assert adj.bipartite_split == U
+    else:
+        r, c = _graph(N, N, 4, heavy=[(5, 3000)], seed=N)
+        adj = _adj(N, r, c, cuda, chunk=256)
+    ego0 = torch.randn(N, 64, device=cuda)
     u = torch.as_tensor(rng.integers(0, U, 200), device=cuda)
     p = torch.as_tensor(rng.integers(0, N - U, 200), device=cuda)
     n = torch.as_tensor(rng.integers(0, N - U, 200), device=cuda)
