@@ -16,6 +16,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
 
 
+@pytest.fixture(autouse=True)
+def _engine_mode_reset():
+    """A Trainer built with ``deterministic: True`` switches the engine-wide deterministic mode
+    (ops.set_deterministic); reset it after every test so the next test sees the default paths."""
+    yield
+    ops = sys.modules.get("FoodRec.engine.ops")
+    if ops is not None:
+        ops.set_deterministic(False)
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch
