@@ -610,7 +610,7 @@ int fr_io_candidates(const int64_t* neg, const int64_t* neg_off, const uint8_t* 
  * fr_spmm_sparse_upstream: Y2 = alpha * A X + beta1 * gate(X), d = 64, for an X that is non-zero
  *               only at the rows whose bit is set in d_bits (ceil(n_rows / 32) words): X is read
  *               only there, gate(X) = X at marked rows and 0 elsewhere.  One workgroup per 64 rows
- *               scans its edge range against the bitmask (staged in LDS up to 262,144 rows, read
+ *               scans its edge range against the bitmask (staged in LDS up to 32,768 rows, read
  *               from L2 beyond) and gathers only the marked columns; every row of Y2 (split at
  *               `split`) is written.
  *               The summation order of a row's hits is run-to-run variable (LDS float atomics):

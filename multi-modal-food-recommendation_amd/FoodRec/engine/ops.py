@@ -625,7 +625,7 @@ def rows_mark(mask: torch.Tensor, rows, value: int, zero: torch.Tensor | None = 
                                                 native.stream_of(mask)), "fr_rows_mark_zero")
 
 
-SPARSE_UPSTREAM_MAX_ROWS = 262144  # HealthRec's UI backward: bitmask in LDS up to here
+SPARSE_UPSTREAM_MAX_ROWS = 262144  # HealthRec's UI backward in the sparse-upstream form up to here
 
 
 def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, Y2_hi=None, split=0,

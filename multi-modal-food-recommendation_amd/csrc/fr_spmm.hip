@@ -305,10 +305,10 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ ma
 // column-masked gather).  d = 64.
 constexpr int kSpRows = 64;
 constexpr int kSpRound = 1024;
-constexpr int kSpMaxWords = 8192;  // bitmask in LDS (dynamic, ceil(n / 32) words): up to 262,144 rows
+constexpr int kSpStageWords = 1024;  // bitmask staged in LDS (dynamic, ceil(n / 32) words): up to 32,768 rows
 
 // GBITS: the bitmask is read from global memory (L2-resident: ceil(n / 32) words, 1.4 MB at 11M
-// rows) instead of being staged in LDS -- graphs beyond 262,144 rows (config 4).
+// rows) instead of being staged in LDS -- graphs beyond 32,768 rows (HealthRec UI, config 4).
 // UNGATED (a rectangular slice: the bitmask marks X's rows, i.e. columns, not output rows): A1 is
 // read at every output row.
 template <bool GBITS, bool UNGATED = false>
@@ -818,7 +818,10 @@ extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d
          split, nullptr};
   const int nwords = (int)fr::ceil_div(n_rows, 32);
   const dim3 grid((unsigned)fr::ceil_div(n_rows, kSpRows));
-  if (nwords <= kSpMaxWords)  // bitmask staged in LDS
+  // bitmask staged in LDS only while it is small next to a block's edge range: each of the
+  // ceil(n / 64) blocks would copy all of it (HealthRec's UI graph: 14.3 KB per block against ~6 KB
+  // of col / val; the L1-resident global lookups are 4.4 us faster per launch there)
+  if (nwords <= kSpStageWords)
     hipLaunchKernelGGL(spmm_sparse_kernel<false>, grid, dim3(256), (size_t)nwords * sizeof(uint32_t),
                        reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
                        reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
