@@ -92,6 +92,13 @@ def main():
     # multi-GPU runs use RCCL, one rank per GPU)
     backend = os.environ.get("FR_BENCH_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
+    # FR_BENCH_DP1=1: the data-parallel step (row exchange + dense all-reduce through RCCL, graphs A /
+    # B1 / B2 around the collectives) at world 1 -- the per-rank cost of the N > 1 path on one GPU
+    dp1 = world == 1 and os.environ.get("FR_BENCH_DP1") == "1"
+    if dp1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -107,8 +114,8 @@ def main():
 
     cfg, data, model = build(device, args.batch, extra=json.loads(args.config_json) if args.config_json else None)
     trainer = Trainer(cfg, model)
-    if world > 1:
-        trainer.grad_hook = GradAllReduce(model, world)
+    if world > 1 or dp1:
+        trainer.grad_hook = GradAllReduce(model, world, exchange_rows=True if dp1 else None)
     np.random.seed(1000 + rank)  # each replica draws its own triple stream
     sampler = TripleSampler(data, args.batch, device, replay_python_random=False)
     feats = trainer._features()
@@ -285,7 +292,7 @@ def main():
                 "config": {"workload": "healthrec_allrecipes", "model": "HealthRec (CIKM_Model)",
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                           "parallelism": f"dp{world}" if world > 1 else "single"},
+                           "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single")},
                 "roofline": roofline, "step_bytes": step_fig,
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
@@ -298,7 +305,7 @@ def main():
                 "spmm": spmm, "config1_bprmf_allrecipes": c1, "config3_clussl_foodcom": c3, "config4_10m": c4,
                 "config5_10m_bf16": c5, "kernels": kernels, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or dp1:
         dist.destroy_process_group()
 
 

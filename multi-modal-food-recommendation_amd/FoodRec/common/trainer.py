@@ -74,6 +74,12 @@ def book_step(parts, acc, nan_flag, accumulate=True):
                                            cptr, len(ctrs), native.stream_of(acc)), "fr_step_book")
 
 
+# Captures are thread-local: the process group's watchdog thread polls its collectives' events
+# (hipEventQuery) at any time, which a global-mode capture on another thread turns into a fatal
+# "operation not permitted when stream is capturing" (seen under rocprofv3 at world 1).
+_CAPTURE_MODE = "thread_local"
+
+
 class GraphedStep:
     """Trainer.train_step captured once in a HIP graph and replayed per batch.
 
@@ -155,7 +161,7 @@ class GraphedStep:
             self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
             self.tr.optimizer.zero_grad()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.static_loss = self._body(batch_idx, self.gstate, accumulate=True)
             self.graph = g
             if acc0 is not None:
@@ -289,18 +295,18 @@ class GraphedDPStep(GraphedStep):
             self.gstate["acc"] = torch.zeros(self.n_parts, dtype=torch.float64, device=self.u.device)
             tr.optimizer.zero_grad()
             ga = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
+            with torch.cuda.graph(ga, capture_error_mode=_CAPTURE_MODE):
                 self.static_loss = self._part_a(batch_idx, self.gstate, True)
             if self._split_b():
                 gb1, gb2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gb1, pool=ga.pool()):
+                with torch.cuda.graph(gb1, pool=ga.pool(), capture_error_mode=_CAPTURE_MODE):
                     self._part_b1(self.gstate)
-                with torch.cuda.graph(gb2, pool=ga.pool()):
+                with torch.cuda.graph(gb2, pool=ga.pool(), capture_error_mode=_CAPTURE_MODE):
                     self._part_b2(self.gstate)
                 self.graph_b = (gb1, gb2)
             else:
                 gb = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gb, pool=ga.pool()):
+                with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode=_CAPTURE_MODE):
                     self._part_b(self.gstate)
                 self.graph_b = (gb,)
             self.graph = ga

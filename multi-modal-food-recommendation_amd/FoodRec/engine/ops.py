@@ -759,6 +759,19 @@ def _persistent(adj, key, make):
     return t
 
 
+def grad_buffer(w: torch.Tensor) -> torch.Tensor:
+    """Where a backward writes parameter ``w``'s full gradient: the slot a data-parallel gradient
+    hook keeps for it in its flat all-reduce buffer (engine.dist.GradAllReduce sets
+    ``w._fr_grad_dest``; autograd adopts the returned view as ``w.grad``, so the hook's pack has
+    nothing to copy), else a new tensor."""
+    dest = w.__dict__.get("_fr_grad_dest")
+    if dest is not None:
+        v = dest()
+        if v is not None and v.shape == w.shape and v.dtype == w.dtype and v.device == w.device:
+            return v
+    return torch.empty_like(w)
+
+
 class _GraphBpr(torch.autograd.Function):
     """HealthRec's propagation + BPR + user/item EmbLoss (cikm_model.py:182-208, 255-279) as one
     autograd node:
@@ -806,6 +819,7 @@ class _GraphBpr(torch.autograd.Function):
                                          _f(gamma), out.data_ptr(), item_rows.data_ptr(), 64, ws.data_ptr(), ws.numel(),
                                          native.stream_of(user_w)), "fr_bpr_fwd_rows")
         ctx.save_for_backward(user_w, item_w, ui_all, u, p, n, pn)
+        ctx.ingre_w = ingre_w  # the parameter itself (grad_buffer looks up its gradient destination)
         ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
         return out[0], out[4:5], item_rows
 
@@ -891,14 +905,14 @@ class _GraphBpr(torch.autograd.Function):
                                            _f(gamma), _f(1.0), _f(0.0), g_mf.data_ptr(), dUI.data_ptr(),
                                            dUI[U:].data_ptr(), None, None, g_rows.data_ptr(), g_rows.stride(0),
                                            ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd_ex")
-        d_user = torch.empty_like(user_w)
+        d_user = grad_buffer(user_w)
         G_ri = _persistent(ri_adj, ("g_ri", str(dev)), lambda: torch.zeros(I + NI, 64, device=dev))
         if sparse:
             spmm_sparse_upstream(ui_adj, bits, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5)
         else:
             _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
-        d_item = torch.empty_like(item_w)
-        d_ingre = torch.empty(NI + 1, 64, dtype=torch.float32, device=dev)
+        d_item = grad_buffer(item_w)
+        d_ingre = grad_buffer(ctx.ingre_w)
         _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,

@@ -147,9 +147,8 @@ class HealthRec(GeneralRecommender):
         all_item = _pn(batch_data, "i_id")
         xg = self.__dict__.get("_fr_exchange")  # row-gradient exchange (FusedAdam / data parallel)
         # lazily updated image/text rows of this batch: caught up on a side stream (ALU-bound) while
-        # the propagation (memory-bound, other tables) runs.  Single process only: a data-parallel
-        # RowExchange has no prefetch_rows (a forked capture stream inside the DP graphs slowed the
-        # 2-rank rehearsal 16 -> 73 ms/step), its rows are caught up inline before the gather
+        # the propagation (memory-bound, other tables) runs (data parallel: RowExchange hands it to
+        # its sink, the same FusedAdam row state)
         join = xg.prefetch_rows([(t.weight, all_item) for t in self._row_tables()]) \
             if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) else (lambda: None)
         fused_graph = self._fused_graph(user)

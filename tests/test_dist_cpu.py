@@ -54,3 +54,60 @@ def test_grad_allreduce_gloo_world2(tmp_path):
             # replicas stay bit-identical: every rank holds the same averaged gradient
             assert torch.equal(res[0]["reduced"][name], res[1]["reduced"][name])
         assert res[0]["unused_grad"] is None
+
+
+class _Sink:
+    """Records what RowExchange.apply hands a FusedAdam row-gradient collector."""
+
+    def __init__(self):
+        self.calls = []
+
+    def stash_factored(self, w, pad, ids, dY, W):
+        self.calls.append((w, ids, dY.clone(), dY.data_ptr(), W))
+
+
+def _row_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from FoodRec.engine.dist import RowExchange, init_from_env
+    init_from_env(backend="gloo")
+    img, txt = torch.zeros(40, 32), torch.zeros(40, 16)  # two row tables gathered at the same ids
+    Wi, Wt = torch.randn(64, 32), torch.randn(64, 16)
+    xg = RowExchange(dist.group.WORLD, world)
+    xg.sink = _Sink()
+    out = []
+    for step in range(2):
+        g = torch.Generator().manual_seed(10 * step + rank)
+        ids = torch.randint(0, 40, (6,), generator=g)
+        dYi, dYt = torch.randn(6, 64, generator=g), torch.randn(6, 64, generator=g)
+        xg.stash_factored(img, None, ids, dYi, Wi)
+        xg.stash_factored(txt, None, ids, dYt, Wt)
+        xg.exchange()
+        xg.sink.calls.clear()
+        xg.apply()
+        out.append({"ids": ids, "dYi": dYi, "dYt": dYt,
+                    "calls": [(c[0] is img, c[1], c[2], c[3]) for c in xg.sink.calls],
+                    "same_ids": xg.sink.calls[0][1] is xg.sink.calls[1][1]})
+    torch.save(out, os.path.join(out_dir, f"rows_r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_row_exchange_gloo_world2_shared_ids(tmp_path):
+    """RowExchange over gloo, two factored tables stashed with one ids tensor (HealthRec's image /
+    text projections): one ids region on the wire; apply hands the sink ONE ids tensor (all ranks'
+    ids, rank-major) and the rows mean-scaled, as adjacent 64-column views of one buffer."""
+    world = 2
+    mp.start_processes(_row_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = [torch.load(tmp_path / f"rows_r{r}.pt", weights_only=False) for r in range(world)]
+    for step in range(2):
+        ids_all = torch.cat([res[r][step]["ids"] for r in range(world)])
+        for r in range(world):
+            st = res[r][step]
+            assert st["same_ids"]
+            (img_first, ids_i, dyi, pi), (_, ids_t, dyt, pt) = st["calls"]
+            assert img_first and torch.equal(ids_i, ids_all) and torch.equal(ids_t, ids_all)
+            assert pt == pi + 4 * 64  # adjacent column blocks of one buffer
+            torch.testing.assert_close(dyi, torch.cat([res[q][step]["dYi"] for q in range(world)]) / world)
+            torch.testing.assert_close(dyt, torch.cat([res[q][step]["dYt"] for q in range(world)]) / world)
