@@ -730,9 +730,9 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
     out = {"graph": "synthetic U=10M I=1M E=%d, row-sharded over %d ranks (built in %.1f s)"
                     % (g.n_edges, world, build_s),
            "model": "LightGCN_ID row-sharded (users in nnz-balanced blocks, items replicated), rows form",
-           "collectives_per_step": "3 all-reduces of I x d fp32 (256 MB; the forward's and the last backward "
-                                   "layer's cut into item-row blocks) + one of the 2B batch item rows + 2 B x d "
-                                   "owner gathers",
+           "collectives_per_step": "1 all-reduce of I x d fp32 (256 MB: the last backward layer's item partial, "
+                                   "cut into item-row blocks) + the item flags (I floats) + 2 of the |S| layer-1 "
+                                   "item rows + 1 of the 2B batch item rows + 2 B x d owner gathers",
            "byte_model": "config4_bytes_rows (the single-GPU step's algorithmic bytes)",
            "local_params_rank0": P_local, "local_nnz_per_rank": [int(x.item()) for x in nnz_all],
            "steps_timed": steps, "step": out_steps}
