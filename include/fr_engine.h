@@ -175,6 +175,21 @@ int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, float* d_out,
 int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g, const float* d_gscale,
                    float* d_dH, void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* InfoNCE over several view pairs in the same launches (CLUSSL's ssl_mode infonce:
+ * sum over pairs (a, b) of CL_loss(cat([views[a], views[b]])), pricai_modelx.py:263 / :354-378):
+ * views are n_views (<= 4) tables [b, d]; pairs[2k], pairs[2k+1] index them (n_pairs <= 16).  No
+ * concatenated copies; every view is normalised once; the backward sums each view's upstream over
+ * the pairs that hold it and writes d_dviews[v] (entries may be NULL).
+ * out[0] = the fp32 sum of the pair losses in pair order, out[1 + k] = pair k's loss.
+ * fr_infonce_fwd/_bwd are this with the two halves of H as views 0, 1 and one pair (d_dH written). */
+int64_t fr_infonce_multi_workspace(int n_views, int64_t b, int d, int n_pairs);
+int fr_infonce_multi_fwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
+                         int n_pairs, float tau, float* d_out, void* d_workspace, int64_t workspace_bytes,
+                         void* stream);
+int fr_infonce_multi_bwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
+                         int n_pairs, float tau, float g, const float* d_gscale, float* const* d_dviews,
+                         void* d_workspace, int64_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Multi-tensor Adam, following torch.optim.Adam (amsgrad=False, maximize=False) element order:
  *   g += wd*p;  m = m + (1-b1)(g-m);  v = v*b2 + ((1-b2)g)g;

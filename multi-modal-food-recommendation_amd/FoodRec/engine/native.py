@@ -115,6 +115,11 @@ _SIGS = {
     "fr_dcor_bwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
                             c_float, c_void_p, POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
     "fr_infonce_workspace": (c_int64, [c_int64]),
+    "fr_infonce_multi_workspace": (c_int64, [c_int, c_int64, c_int, c_int]),
+    "fr_infonce_multi_fwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int, c_float,
+                                     c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_infonce_multi_bwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int, c_float,
+                                     c_float, c_void_p, POINTER(c_void_p), c_void_p, c_int64, c_void_p]),
     "fr_infonce_fwd": (c_int, [c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_infonce_bwd": (c_int, [c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                                c_void_p, c_int64, c_void_p]),

@@ -1690,7 +1690,7 @@ class _InfoNCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (H,) = ctx.saved_tensors
-        dH = torch.zeros_like(H)
+        dH = torch.empty_like(H)  # written in full by fr_infonce_bwd
         gs = g.reshape(1).float().contiguous()
         native.check(native.lib().fr_infonce_bwd(H.data_ptr(), ctx.b, H.shape[1], _f(ctx.tau), _f(1.0),
                                                  gs.data_ptr(), dH.data_ptr(), ctx.ws.data_ptr(),
@@ -1700,6 +1700,49 @@ class _InfoNCE(torch.autograd.Function):
 
 def infonce_loss(H: torch.Tensor, tau: float = 0.5) -> torch.Tensor:
     return _InfoNCE.apply(H, float(tau))
+
+
+class _InfoNCEMulti(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pairs, tau, *views):
+        views = tuple(_rowmajor(v, f32_only=True) for v in views)
+        native.require_device(*views)
+        V = len(views)
+        b, d = views[0].shape
+        if any(v.shape != (b, d) for v in views):
+            raise native.EngineError("infonce_pairs: views of one shape [b, d] required")
+        lib = native.lib()
+        ws = native.workspace(lib.fr_infonce_multi_workspace(V, b, d, len(pairs)), views[0].device)
+        vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
+        pa = (ctypes.c_int32 * (2 * len(pairs)))(*[x for pr in pairs for x in pr])
+        out = torch.empty(1 + len(pairs), dtype=torch.float32, device=views[0].device)
+        native.check(lib.fr_infonce_multi_fwd(vp, V, b, d, pa, len(pairs), _f(tau), out.data_ptr(), ws.data_ptr(),
+                                              ws.numel(), native.stream_of(views[0])), "fr_infonce_multi_fwd")
+        ctx.save_for_backward(*views)
+        ctx.ws, ctx.pairs, ctx.tau = ws, pairs, tau
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        views = ctx.saved_tensors
+        V = len(views)
+        b, d = views[0].shape
+        grads = [torch.empty_like(v) if ctx.needs_input_grad[2 + i] else None for i, v in enumerate(views)]
+        vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
+        gp = (ctypes.c_void_p * V)(*[native.ptr(x) for x in grads])
+        pa = (ctypes.c_int32 * (2 * len(ctx.pairs)))(*[x for pr in ctx.pairs for x in pr])
+        gs = g.reshape(1).float().contiguous()
+        native.check(native.lib().fr_infonce_multi_bwd(vp, V, b, d, pa, len(ctx.pairs), _f(ctx.tau), _f(1.0),
+                                                       gs.data_ptr(), gp, ctx.ws.data_ptr(), ctx.ws.numel(),
+                                                       native.stream_of(views[0])), "fr_infonce_multi_bwd")
+        return (None, None, *grads)
+
+
+def infonce_pairs(views, pairs, tau: float = 0.5) -> torch.Tensor:
+    """sum over pairs (a, b) of infonce_loss(cat([views[a], views[b]]), tau) (CLUSSL's ssl_mode
+    infonce, pricai_modelx.py:263 with CL_loss :354-378) in one forward and one backward node: no
+    concatenation, each view normalised once, all pairs in the same launches.  0-dim result."""
+    return _InfoNCEMulti.apply(tuple(tuple(int(x) for x in p) for p in pairs), float(tau), *views)
 
 
 # ----------------------------------------------------------------------------- full-sort top-k

@@ -100,7 +100,8 @@ class CLUSSL(GeneralRecommender):
         mf_loss, emb = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                         user, pos_item, neg_item)
         if self.ssl_mode == "infonce":
-            cl = sum(ops.infonce_loss(torch.cat([views[a], views[b]], dim=0), 0.5) for a, b in _DCOR_PAIRS)
+            # sum over the pairs of CL_loss(cat([views[a], views[b]])): one fused node for all pairs
+            cl = ops.infonce_pairs(views, _DCOR_PAIRS, 0.5)
         else:
             cl = ops.dcor_loss(views, _DCOR_PAIRS)
         return mf_loss, self.loss_cl * cl, self.reg_weight * emb

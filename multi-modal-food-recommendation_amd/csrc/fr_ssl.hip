@@ -448,64 +448,108 @@ __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, 
 }
 
 // ============================ InfoNCE ==========================================================
-// workspace: Hn [2b][d] f32, norm [2b] f32, part (m,s) [JS][2b] f32x2, lse [2b] f32,
-//            P [JS][2b][d] f32 (bwd), out scratch
+// V views of b rows; pair p is H_p = [view pa[p] ; view pb[p]] (m = 2b rows).  All pairs of a step
+// run in the same launches (blockIdx.z / y = pair), the views are normalised once, and the backward
+// sums each view's upstream over the pairs it appears in before one normalize-backward per row
+// (linear in the upstream), so CLUSSL's three InfoNCE pairs are 6 launches instead of 18 + glue.
+// workspace: Hn [V][b][d] f32, nrm [V][b] f32, part (m,s) [P][JS][m] f32x2, lse [P][m] f32,
+//            P [P][JS][m][d] f32 (bwd), rowsum [P][ceil(m/4)] f64
 constexpr int NCE_JS = 8;
 
 struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; double* rowsum; };
 
-__host__ __device__ inline NceWS nce_ws(void* base, int64_t m, int d) {
+__host__ __device__ inline int64_t nce_nparts(int64_t m) { return (m + 3) / 4; }
+
+__host__ __device__ inline NceWS nce_ws(void* base, int V, int64_t b, int d, int P) {
   char* p = reinterpret_cast<char*>(base);
   auto take = [&](int64_t bytes) { char* r = p; p += (bytes + 255) / 256 * 256; return r; };
+  const int64_t m = 2 * b;
   NceWS w;
-  w.Hn = reinterpret_cast<float*>(take(m * d * 4));
-  w.nrm = reinterpret_cast<float*>(take(m * 4));
-  w.part = reinterpret_cast<float2*>(take((int64_t)NCE_JS * m * 8));
-  w.lse = reinterpret_cast<float*>(take(m * 4));
-  w.P = reinterpret_cast<float*>(take((int64_t)NCE_JS * m * d * 4));
-  w.rowsum = reinterpret_cast<double*>(take(((m + 3) / 4) * 8));
+  w.Hn = reinterpret_cast<float*>(take((int64_t)V * b * d * 4));
+  w.nrm = reinterpret_cast<float*>(take((int64_t)V * b * 4));
+  w.part = reinterpret_cast<float2*>(take((int64_t)P * NCE_JS * m * 8));
+  w.lse = reinterpret_cast<float*>(take((int64_t)P * m * 4));
+  w.P = reinterpret_cast<float*>(take((int64_t)P * NCE_JS * m * d * 4));
+  w.rowsum = reinterpret_cast<double*>(take((int64_t)P * nce_nparts(m) * 8));
   return w;
 }
 
-inline int64_t nce_ws_bytes(int64_t m, int d) {
-  auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
-  return r(m * d * 4) + r(m * 4) + r((int64_t)NCE_JS * m * 8) + r(m * 4) + r((int64_t)NCE_JS * m * d * 4) +
-         r(((m + 3) / 4) * 8);
+inline int64_t nce_ws_bytes(int V, int64_t b, int d, int P) {
+  auto r = [](int64_t x) { return (x + 255) / 256 * 256; };
+  const int64_t m = 2 * b;
+  return r((int64_t)V * b * d * 4) + r((int64_t)V * b * 4) + r((int64_t)P * NCE_JS * m * 8) + r((int64_t)P * m * 4) +
+         r((int64_t)P * NCE_JS * m * d * 4) + r((int64_t)P * nce_nparts(m) * 8);
 }
 
-// F.normalize(p=2, dim=-1): x / max(||x||, 1e-12); one wave per row
-__global__ __launch_bounds__(256) void nce_normalize_kernel(const float* __restrict__ H, int64_t m,
-                                                            int d, NceWS ws) {
+// normalised row r of pair p's H (rows [0, b) from view pa, [b, 2b) from view pb)
+__device__ __forceinline__ const float* nce_row(const NceWS& ws, const PairTab& pt, int p, int64_t b, int d,
+                                                int64_t r) {
+  const int v = r < b ? pt.pa[p] : pt.pb[p];
+  return ws.Hn + ((int64_t)v * b + (r < b ? r : r - b)) * d;
+}
+
+// rows [r0, r0+64) of pair p's H -> transposed LDS tile (0 beyond 2b)
+__device__ __forceinline__ void nce_tile_t(const NceWS& ws, const PairTab& pt, int p, int64_t b, int d, int64_t r0,
+                                           float* Xt) {
+  const int d4 = d >> 2;
+  for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
+    const int r = idx / d4, k4 = idx - r * d4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < 2 * b) v = reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, d, r0 + r))[k4];
+    Xt[(4 * k4 + 0) * PADT + r] = v.x;
+    Xt[(4 * k4 + 1) * PADT + r] = v.y;
+    Xt[(4 * k4 + 2) * PADT + r] = v.z;
+    Xt[(4 * k4 + 3) * PADT + r] = v.w;
+  }
+}
+
+// rows [r0, r0+64) of pair p's H -> row-major LDS tile Xr[r*(d+4) + k]
+__device__ __forceinline__ void nce_tile_r(const NceWS& ws, const PairTab& pt, int p, int64_t b, int d, int64_t r0,
+                                           float* Xr) {
+  const int d4 = d >> 2;
+  const int ld = d + 4;
+  for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
+    const int r = idx / d4, k4 = idx - r * d4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < 2 * b) v = reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, d, r0 + r))[k4];
+    *reinterpret_cast<float4*>(Xr + r * ld + 4 * k4) = v;
+  }
+}
+
+// F.normalize(p=2, dim=-1) of every view row: x / max(||x||, 1e-12); one wave per row
+__global__ __launch_bounds__(256) void nce_normalize_kernel(Views vw, int V, int64_t b, int d, NceWS ws) {
   const int lane = threadIdx.x & 63;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < m;
+  const int64_t rows = (int64_t)V * b;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < rows;
        r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const float* H = vw.x[r / b] + (r % b) * d;
     float s = 0.f;
-    for (int k = lane; k < d; k += 64) s = fmaf(H[r * d + k], H[r * d + k], s);
+    for (int k = lane; k < d; k += 64) s = fmaf(H[k], H[k], s);
     s = group_sum<64>(s);
     const float nr = sqrtf(s);
     const float den = fmaxf(nr, 1e-12f);
-    for (int k = lane; k < d; k += 64) ws.Hn[r * d + k] = H[r * d + k] / den;
+    for (int k = lane; k < d; k += 64) ws.Hn[r * d + k] = H[k] / den;
     if (lane == 0) ws.nrm[r] = nr;
   }
 }
 
 __device__ __forceinline__ int64_t nce_partner(int64_t i, int64_t b) { return i < b ? i + b : i - b; }
 
-// partial online log-sum-exp of row i over the column tiles of split js (self excluded)
-__global__ __launch_bounds__(256) void nce_lse_tiles_kernel(int64_t b, int d, float inv_tau, NceWS ws) {
+// partial online log-sum-exp of row i of pair blockIdx.z over the column tiles of split js (self excluded)
+__global__ __launch_bounds__(256) void nce_lse_tiles_kernel(int64_t b, int d, float inv_tau, PairTab pt, NceWS ws) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* At = smem;
   float* Bt = At + d * PADT;
   __shared__ float pm[T][17], ps[T][17];
   const int64_t m = 2 * b, nt = (m + T - 1) / T;
-  const int it = blockIdx.x, js = blockIdx.y;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
   const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
-  load_tile_t(ws.Hn, m, d, (int64_t)it * T, At);
+  nce_tile_t(ws, pt, p, b, d, (int64_t)it * T, At);
   float mx[4], sm[4];
   for (int x = 0; x < 4; ++x) { mx[x] = -INFINITY; sm[x] = 0.f; }
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
-    load_tile_t(ws.Hn, m, d, jt * T, Bt);
+    nce_tile_t(ws, pt, p, b, d, jt * T, Bt);
     __syncthreads();
     float g[4][4];
     gram4x4(At, Bt, d, ti, tj, g);
@@ -532,60 +576,73 @@ __global__ __launch_bounds__(256) void nce_lse_tiles_kernel(int64_t b, int d, fl
       else S += sk * expf(mk - M);
     }
     const int64_t gi = (int64_t)it * T + r;
-    if (gi < m) ws.part[(int64_t)js * m + gi] = make_float2(M, S);
+    if (gi < m) ws.part[((int64_t)p * NCE_JS + js) * m + gi] = make_float2(M, S);
   }
 }
 
-// merge splits -> lse; loss = sum_i (lse_i - l_i,p(i)) / b^2.  One wave per row (lanes over the
-// feature dim for the positive logit), 4 rows per block -> a per-block partial; nce_sum_kernel adds
-// the partials in a fixed order (deterministic)
-__global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, float inv_tau, int js_count,
+// merge splits -> lse; row terms (lse_i - l_i,p(i)) of pair blockIdx.y.  One wave per row (lanes over
+// the feature dim for the positive logit), 4 rows per block -> a per-block partial; nce_sum_kernel
+// adds the partials in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, float inv_tau, int js_count, PairTab pt,
                                                            NceWS ws) {
   __shared__ double red[4];
   const int64_t m = 2 * b;
+  const int p = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wv;
   double v = 0.0;
   if (i < m) {
     float M = -INFINITY, S = 0.f;
     for (int s = 0; s < js_count; ++s) {
-      const float2 p = ws.part[(int64_t)s * m + i];
-      if (p.y == 0.f) continue;
-      if (p.x > M) { S = S * expf(M - p.x) + p.y; M = p.x; }
-      else S += p.y * expf(p.x - M);
+      const float2 q = ws.part[((int64_t)p * NCE_JS + s) * m + i];
+      if (q.y == 0.f) continue;
+      if (q.x > M) { S = S * expf(M - q.x) + q.y; M = q.x; }
+      else S += q.y * expf(q.x - M);
     }
     const float lse = M + logf(S);
-    const int64_t j = nce_partner(i, b);
+    const float* hi = nce_row(ws, pt, p, b, d, i);
+    const float* hj = nce_row(ws, pt, p, b, d, nce_partner(i, b));
     double dp = 0.0;
-    for (int k = lane; k < d; k += 64) dp += (double)ws.Hn[i * d + k] * (double)ws.Hn[j * d + k];
+    for (int k = lane; k < d; k += 64) dp += (double)hi[k] * (double)hj[k];
     const float dot = (float)group_sum_d<64>(dp);
     if (lane == 0) {
-      ws.lse[i] = lse;
+      ws.lse[(int64_t)p * m + i] = lse;
       v = (double)lse - (double)(dot * inv_tau);
     }
   }
   if (lane == 0) red[wv] = v;
   __syncthreads();
-  if (threadIdx.x == 0) ws.rowsum[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) ws.rowsum[(int64_t)p * nce_nparts(m) + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int64_t nparts, NceWS ws, float* out) {
+// out_pairs[p] (optional) = pair p's loss (fp64 sum of its row terms in block order / b^2, rounded
+// once); out[0] = their fp32 sum in pair order (Python's sum() over the pairs' fp32 losses)
+__global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int n_pairs, NceWS ws, float* out,
+                                                      float* out_pairs) {
   __shared__ double red[16];
-  double loc = 0.0;
-  for (int64_t k = threadIdx.x; k < nparts; k += blockDim.x) loc += ws.rowsum[k];
-  loc = group_sum_d<64>(loc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
-    out[0] = (float)(s / ((double)b * (double)b));
+  const int64_t nparts = nce_nparts(2 * b);
+  float total = 0.f;
+  for (int p = 0; p < n_pairs; ++p) {
+    double loc = 0.0;
+    for (int64_t k = threadIdx.x; k < nparts; k += blockDim.x) loc += ws.rowsum[(int64_t)p * nparts + k];
+    loc = group_sum_d<64>(loc);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+      const float lp = (float)(s / ((double)b * (double)b));
+      if (out_pairs) out_pairs[p] = lp;
+      total = p == 0 ? lp : total + lp;
+    }
   }
+  if (threadIdx.x == 0) out[0] = total;
 }
 
-// dHn_i = (1/tau) sum_j W_ij Hn_j,  W_ij = dl_ij + dl_ji,  dl_ij = (P_ij - [j==p(i)]) * g / b^2
+// dHn_i = (1/tau) sum_j W_ij Hn_j,  W_ij = dl_ij + dl_ji,  dl_ij = (P_ij - [j==p(i)]) * g / b^2  (pair blockIdx.z)
 template <int KPER>
-__global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv_tau, NceWS ws) {
+__global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
   constexpr int d = 4 * KPER;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* At = smem;
@@ -594,25 +651,26 @@ __global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv
   float* Ws = Br + T * (d + 4);
   __shared__ float lse_i[T], lse_j[T];
   const int64_t m = 2 * b, nt = (m + T - 1) / T;
-  const int it = blockIdx.x, js = blockIdx.y;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
+  const float* lse = ws.lse + (int64_t)p * m;
   const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
   const int ar = threadIdx.x & 63, aslot = threadIdx.x >> 6;
   constexpr int kper = KPER;
-  load_tile_t(ws.Hn, m, d, (int64_t)it * T, At);
+  nce_tile_t(ws, pt, p, b, d, (int64_t)it * T, At);
   if (threadIdx.x < T) {
     const int64_t gi = (int64_t)it * T + threadIdx.x;
-    lse_i[threadIdx.x] = gi < m ? ws.lse[gi] : 0.f;
+    lse_i[threadIdx.x] = gi < m ? lse[gi] : 0.f;
   }
   float acc[KPER];
 #pragma unroll
   for (int k = 0; k < KPER; ++k) acc[k] = 0.f;
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
-    load_tile_t(ws.Hn, m, d, jt * T, Bt);
-    load_tile_r(ws.Hn, m, d, jt * T, Br);
+    nce_tile_t(ws, pt, p, b, d, jt * T, Bt);
+    nce_tile_r(ws, pt, p, b, d, jt * T, Br);
     if (threadIdx.x < T) {
       const int64_t gj = jt * T + threadIdx.x;
-      lse_j[threadIdx.x] = gj < m ? ws.lse[gj] : 0.f;
+      lse_j[threadIdx.x] = gj < m ? lse[gj] : 0.f;
     }
     __syncthreads();
     float g[4][4];
@@ -641,37 +699,45 @@ __global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv
   }
   const int64_t gi = (int64_t)it * T + ar;
   if (gi < m) {
-    float* P = ws.P + ((int64_t)js * m + gi) * d + aslot * kper;
+    float* P = ws.P + (((int64_t)p * NCE_JS + js) * m + gi) * d + aslot * kper;
 #pragma unroll
     for (int k = 0; k < kper; ++k) P[k] = acc[k];
   }
 }
 
-// dH_i += normalize_backward(dHn_i) with dHn_i = scale * sum_splits P / tau
-__global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(const float* __restrict__ H, int64_t b,
-                                                               int d, float inv_tau, int js_count,
-                                                               float g, const float* gscale,
-                                                               NceWS ws, float* dH) {
+// dview_v[r] = normalize_backward(gh) with gh = scale * (sum over the pairs holding view v, at the
+// row's position in that pair, of the split partials); written (views that no pair holds: zeros)
+__global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, int64_t b, int d, float inv_tau,
+                                                               int js_count, float g, const float* gscale, PairTab pt,
+                                                               NceWS ws) {
   const float scale = g * (gscale ? gscale[0] : 1.f) / ((float)b * (float)b) * inv_tau;
-  const int64_t m = 2 * b;
+  const int64_t m = 2 * b, rows = (int64_t)V * b;
   const int lane = threadIdx.x & 63;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < m;
-       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const float nr = ws.nrm[r];
+  for (int64_t vr = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; vr < rows;
+       vr += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int v = (int)(vr / b);
+    const int64_t r = vr % b;
+    float* dX = vw.dx[v];
+    if (dX == nullptr) continue;
+    const float nr = ws.nrm[vr];
+    const float* hn = ws.Hn + vr * d;
+    auto gsum = [&](int k) {
+      float q = 0.f;
+      for (int p = 0; p < pt.n_pairs; ++p) {
+        if (pt.pa[p] == v)
+          for (int s = 0; s < js_count; ++s) q += ws.P[(((int64_t)p * NCE_JS + s) * m + r) * d + k];
+        if (pt.pb[p] == v)
+          for (int s = 0; s < js_count; ++s) q += ws.P[(((int64_t)p * NCE_JS + s) * m + b + r) * d + k];
+      }
+      return q * scale;
+    };
     float dot = 0.f;
-    for (int k = lane; k < d; k += 64) {
-      float p = 0.f;
-      for (int s = 0; s < js_count; ++s) p += ws.P[((int64_t)s * m + r) * d + k];
-      dot = fmaf(p * scale, ws.Hn[r * d + k], dot);
-    }
+    for (int k = lane; k < d; k += 64) dot = fmaf(gsum(k), hn[k], dot);
     dot = group_sum<64>(dot);
     for (int k = lane; k < d; k += 64) {
-      float p = 0.f;
-      for (int s = 0; s < js_count; ++s) p += ws.P[((int64_t)s * m + r) * d + k];
-      const float gh = p * scale;
+      const float gh = gsum(k);
       // d/dx [x / max(|x|, eps)]
-      const float gx = nr > 1e-12f ? (gh - ws.Hn[r * d + k] * dot) / nr : gh / 1e-12f;
-      dH[r * d + k] += gx;
+      dX[r * d + k] = nr > 1e-12f ? (gh - hn[k] * dot) / nr : gh / 1e-12f;
     }
   }
 }
@@ -772,67 +838,123 @@ extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, 
   return FR_OK;
 }
 
-extern "C" int64_t fr_infonce_workspace(int64_t b) {
-  if (b <= 0) return 0;
-  return nce_ws_bytes(2 * b, 128);
-}
-
-extern "C" int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, float* d_out,
-                              void* d_workspace, int64_t workspace_bytes, void* stream) {
-  FR_REQUIRE(d_H && d_out && fr::aligned16(d_H), "H/out null or unaligned");
+static int nce_check(const float* const* views, int V, int64_t b, int d, const int32_t* pairs, int P, float tau,
+                     void* ws, int64_t wsb) {
+  FR_REQUIRE(views && V >= 1 && V <= MAXV, "1..4 views required");
   FR_REQUIRE(b >= 1, "b must be >= 1");
   FR_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "d must be 16, 32, 64 or 128");
   FR_REQUIRE(tau > 0.f, "tau must be > 0");
-  FR_REQUIRE(d_workspace && workspace_bytes >= nce_ws_bytes(2 * b, d) && fr::aligned16(d_workspace),
-             "workspace too small");
+  FR_REQUIRE(pairs && P >= 1 && P <= 16, "1..16 pairs required");
+  for (int k = 0; k < P; ++k)
+    FR_REQUIRE(pairs[2 * k] >= 0 && pairs[2 * k] < V && pairs[2 * k + 1] >= 0 && pairs[2 * k + 1] < V,
+               "pair view index out of range");
+  for (int a = 0; a < V; ++a) FR_REQUIRE(views[a] && fr::aligned16(views[a]), "view null/unaligned");
+  FR_REQUIRE(ws && wsb >= nce_ws_bytes(V, b, d, P) && fr::aligned16(ws), "workspace too small");
+  return FR_OK;
+}
+
+extern "C" int64_t fr_infonce_multi_workspace(int n_views, int64_t b, int d, int n_pairs) {
+  if (b <= 0 || n_views <= 0 || n_views > MAXV || n_pairs <= 0 || n_pairs > 16 || d <= 0 || d > 128) return 0;
+  return nce_ws_bytes(n_views, b, d, n_pairs);
+}
+
+static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs, int n_pairs,
+                        float tau, float* d_out, float* d_out_pairs, void* d_workspace, int64_t workspace_bytes,
+                        void* stream) {
+  int rc = nce_check(d_views, n_views, b, d, pairs, n_pairs, tau, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_out, "out null");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t m = 2 * b;
-  NceWS w = nce_ws(d_workspace, m, d);
+  NceWS w = nce_ws(d_workspace, n_views, b, d, n_pairs);
+  Views v{};
+  for (int a = 0; a < n_views; ++a) v.x[a] = d_views[a];
+  PairTab pt{};
+  pt.n_pairs = n_pairs;
+  for (int k = 0; k < n_pairs; ++k) { pt.pa[k] = pairs[2 * k]; pt.pb[k] = pairs[2 * k + 1]; }
   const float inv_tau = 1.f / tau;
-  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div(m, 4), 4096);
-  hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, d_H, m, d, w);
+  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div((int64_t)n_views * b, 4), 4096);
+  hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, v, n_views, b, d, w);
   FR_LAUNCH_CHECK();
   const int64_t nt = fr::ceil_div(m, T);
   const int js = (int)std::min<int64_t>(NCE_JS, nt);
   const size_t lds = (size_t)(2 * d * PADT) * 4;
-  hipLaunchKernelGGL(nce_lse_tiles_kernel, dim3((unsigned)nt, (unsigned)js), dim3(256), lds, s, b, d,
-                     inv_tau, w);
+  hipLaunchKernelGGL(nce_lse_tiles_kernel, dim3((unsigned)nt, (unsigned)js, (unsigned)n_pairs), dim3(256), lds, s, b,
+                     d, inv_tau, pt, w);
   FR_LAUNCH_CHECK();
-  const int64_t nparts = fr::ceil_div(m, 4);
-  hipLaunchKernelGGL(nce_finalize_kernel, dim3((unsigned)nparts), dim3(256), 0, s, b, d, inv_tau, js, w);
+  hipLaunchKernelGGL(nce_finalize_kernel, dim3((unsigned)nce_nparts(m), (unsigned)n_pairs), dim3(256), 0, s, b, d,
+                     inv_tau, js, pt, w);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nce_sum_kernel, dim3(1), dim3(1024), 0, s, b, nparts, w, d_out);
+  hipLaunchKernelGGL(nce_sum_kernel, dim3(1), dim3(1024), 0, s, b, n_pairs, w, d_out, d_out_pairs);
   FR_LAUNCH_CHECK();
   return FR_OK;
+}
+
+extern "C" int fr_infonce_multi_fwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
+                                    int n_pairs, float tau, float* d_out, void* d_workspace, int64_t workspace_bytes,
+                                    void* stream) {
+  return nce_fwd_impl(d_views, n_views, b, d, pairs, n_pairs, tau, d_out, d_out ? d_out + 1 : nullptr, d_workspace,
+                      workspace_bytes, stream);
+}
+
+extern "C" int fr_infonce_multi_bwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
+                                    int n_pairs, float tau, float g, const float* d_gscale, float* const* d_dviews,
+                                    void* d_workspace, int64_t workspace_bytes, void* stream) {
+  int rc = nce_check(d_views, n_views, b, d, pairs, n_pairs, tau, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  FR_REQUIRE(d_dviews, "dviews null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t m = 2 * b;
+  NceWS w = nce_ws(d_workspace, n_views, b, d, n_pairs);
+  Views v{};
+  for (int a = 0; a < n_views; ++a) {
+    v.x[a] = d_views[a];
+    v.dx[a] = d_dviews[a];
+    FR_REQUIRE(!v.dx[a] || fr::aligned16(v.dx[a]), "dview unaligned");
+  }
+  PairTab pt{};
+  pt.n_pairs = n_pairs;
+  for (int k = 0; k < n_pairs; ++k) { pt.pa[k] = pairs[2 * k]; pt.pb[k] = pairs[2 * k + 1]; }
+  const float inv_tau = 1.f / tau;
+  const int64_t nt = fr::ceil_div(m, T);
+  const int js = (int)std::min<int64_t>(NCE_JS, nt);
+  const size_t lds = (size_t)(2 * d * PADT + T * (d + 4) + T * 65) * 4;
+  const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
+  switch (d) {
+    case 16: hipLaunchKernelGGL(nce_bwd_tiles_kernel<4>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
+    case 32: hipLaunchKernelGGL(nce_bwd_tiles_kernel<8>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
+    case 64: hipLaunchKernelGGL(nce_bwd_tiles_kernel<16>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
+    default: hipLaunchKernelGGL(nce_bwd_tiles_kernel<32>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
+  }
+  FR_LAUNCH_CHECK();
+  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div((int64_t)n_views * b, 4), 4096);
+  hipLaunchKernelGGL(nce_bwd_finalize_kernel, dim3(nb), dim3(256), 0, s, v, n_views, b, d, inv_tau, js, g, d_gscale,
+                     pt, w);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+// one pair over a contiguous H [2b, d]: the two halves as views 0 and 1
+extern "C" int64_t fr_infonce_workspace(int64_t b) {
+  if (b <= 0) return 0;
+  return nce_ws_bytes(2, b, 128, 1);
+}
+
+extern "C" int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, float* d_out,
+                              void* d_workspace, int64_t workspace_bytes, void* stream) {
+  FR_REQUIRE(d_H && d_out && fr::aligned16(d_H) && b >= 1 && (b * d) % 4 == 0, "H/out null or unaligned");
+  const float* views[2] = {d_H, d_H + b * d};
+  const int32_t pair[2] = {0, 1};
+  return nce_fwd_impl(views, 2, b, d, pair, 1, tau, d_out, nullptr, d_workspace, workspace_bytes, stream);
 }
 
 extern "C" int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g,
                               const float* d_gscale, float* d_dH, void* d_workspace,
                               int64_t workspace_bytes, void* stream) {
-  FR_REQUIRE(d_H && d_dH && fr::aligned16(d_H), "H/dH null or unaligned");
-  FR_REQUIRE(b >= 1, "b must be >= 1");
-  FR_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128, "d must be 16, 32, 64 or 128");
-  FR_REQUIRE(tau > 0.f, "tau must be > 0");
-  FR_REQUIRE(d_workspace && workspace_bytes >= nce_ws_bytes(2 * b, d) && fr::aligned16(d_workspace),
-             "workspace too small");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t m = 2 * b;
-  NceWS w = nce_ws(d_workspace, m, d);
-  const float inv_tau = 1.f / tau;
-  const int64_t nt = fr::ceil_div(m, T);
-  const int js = (int)std::min<int64_t>(NCE_JS, nt);
-  const size_t lds = (size_t)(2 * d * PADT + T * (d + 4) + T * 65) * 4;
-  const dim3 grid((unsigned)nt, (unsigned)js);
-  switch (d) {
-    case 16: hipLaunchKernelGGL(nce_bwd_tiles_kernel<4>, grid, dim3(256), lds, s, b, inv_tau, w); break;
-    case 32: hipLaunchKernelGGL(nce_bwd_tiles_kernel<8>, grid, dim3(256), lds, s, b, inv_tau, w); break;
-    case 64: hipLaunchKernelGGL(nce_bwd_tiles_kernel<16>, grid, dim3(256), lds, s, b, inv_tau, w); break;
-    default: hipLaunchKernelGGL(nce_bwd_tiles_kernel<32>, grid, dim3(256), lds, s, b, inv_tau, w); break;
-  }
-  FR_LAUNCH_CHECK();
-  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div(m, 4), 4096);
-  hipLaunchKernelGGL(nce_bwd_finalize_kernel, dim3(nb), dim3(256), 0, s, d_H, b, d, inv_tau, js, g,
-                     d_gscale, w, d_dH);
-  FR_LAUNCH_CHECK();
-  return FR_OK;
+  FR_REQUIRE(d_H && d_dH && fr::aligned16(d_H) && fr::aligned16(d_dH) && b >= 1 && (b * d) % 4 == 0,
+             "H/dH null or unaligned");
+  const float* views[2] = {d_H, d_H + b * d};
+  float* dviews[2] = {d_dH, d_dH + b * d};
+  const int32_t pair[2] = {0, 1};
+  return fr_infonce_multi_bwd(views, 2, b, d, pair, 1, tau, g, d_gscale, dviews, d_workspace, workspace_bytes, stream);
 }
