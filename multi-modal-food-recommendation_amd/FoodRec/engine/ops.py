@@ -1668,6 +1668,49 @@ def dcor_loss(views, pairs) -> torch.Tensor:
     return _DCor.apply(tuple(tuple(p) for p in pairs), *views)
 
 
+class _ViewsSumGather(torch.autograd.Function):
+    """(v_0 + v_1 + ... , v_0[ids], v_1[ids], ...) for V equally shaped tables (CLUSSL: item_emb =
+    item_ingre + item_image + item_text and the SSL views gathered at the batch items,
+    pricai_modelx.py:227-263).  Backward: d v_k = g_sum + scatter_add(ids, g_k) for all k at once --
+    one broadcast copy and V atomic index_adds instead of, per view, a zero-filled scatter (the
+    deterministic counting sort: 4 launches) and autograd's accumulation add."""
+
+    @staticmethod
+    def forward(ctx, ids, *views):
+        ctx.save_for_backward(ids)
+        ctx.V, ctx.shape = len(views), views[0].shape
+        total = torch.add(views[0], views[1]) if len(views) > 1 else views[0].clone()
+        for v in views[2:]:
+            total.add_(v)
+        return (total, *[v.index_select(0, ids) for v in views])
+
+    @staticmethod
+    def backward(ctx, g_sum, *g_rows):
+        (ids,) = ctx.saved_tensors
+        V, (n, d) = ctx.V, ctx.shape
+        dev = ids.device
+        out = (g_sum.unsqueeze(0).expand(V, n, d).clone() if g_sum is not None
+               else torch.zeros(V, n, d, dtype=torch.float32, device=dev))
+        for k, g in enumerate(g_rows):
+            if g is not None:
+                out[k].index_add_(0, ids, g)
+        return (None, *out.unbind(0))
+
+
+def views_sum_gather(views, ids):
+    """(sum(views) in list order, [v[ids] for v in views]); see _ViewsSumGather.  Deterministic
+    mode keeps the separate sum and deterministic row gathers."""
+    ids = ids.reshape(-1).to(torch.int64)
+    if _DETERMINISTIC or not all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in views) \
+            or len({tuple(v.shape) for v in views}) != 1:
+        total = views[0]
+        for v in views[1:]:
+            total = total + v
+        return total, [embedding(ids, v) for v in views]
+    out = _ViewsSumGather.apply(ids, *views)
+    return out[0], list(out[1:])
+
+
 # ----------------------------------------------------------------------------- InfoNCE
 class _InfoNCE(torch.autograd.Function):
     @staticmethod

@@ -79,6 +79,11 @@ class CLUSSL(GeneralRecommender):
         return ops.propagate_lo(adj, self.item_embedding.weight, side_table[:n_side], self.n_ri_layers)
 
     def forward(self):
+        return self._forward()[:3]
+
+    def _forward(self, ssl_ids=None):
+        """forward(); with ``ssl_ids`` also the three views gathered there (image, text, ingre),
+        the sum and the gathers as one node (ops.views_sum_gather)."""
         item_ingre = self._view(self.ingre_norm_adj, self.ingre_embedding.weight[:-1, :], self.n_ingredients)
         img_side = self.image_trs(self.image_prototype_embedding.weight) if self.v_center is not None \
             else self.image_prototype_embedding.weight
@@ -86,17 +91,21 @@ class CLUSSL(GeneralRecommender):
         txt_side = self.text_trs(self.text_prototype_embedding.weight) if self.t_center is not None \
             else self.text_prototype_embedding.weight
         item_text = self._view(self.text_norm_adj, txt_side, self.n_cluster)
-        item_emb = item_ingre + item_image + item_text
+        gathered = None
+        if ssl_ids is not None:
+            item_emb, (g_ing, g_img, g_txt) = ops.views_sum_gather([item_ingre, item_image, item_text], ssl_ids)
+            gathered = [g_img, g_txt, g_ing]
+        else:
+            item_emb = item_ingre + item_image + item_text
         ui = ops.propagate_mean(self.norm_adj_matrix, torch.cat([self.user_embedding.weight, item_emb], dim=0),
                                 self.n_ui_layers)
         user_all, item_all = torch.split(ui, [self.n_users, self.n_items])
-        return user_all, item_all, (item_image, item_text, item_ingre)
+        return user_all, item_all, (item_image, item_text, item_ingre), gathered
 
     def calculate_loss(self, batch_data):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
         all_item = torch.cat([pos_item, neg_item], dim=0)
-        user_all, item_all, (v_img, v_txt, v_ing) = self.forward()
-        views = [ops.embedding(all_item, v) for v in (v_img, v_txt, v_ing)]
+        user_all, item_all, _, views = self._forward(all_item)  # views at the batch items: image, text, ingre
         mf_loss, emb = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
                                         user, pos_item, neg_item)
         if self.ssl_mode == "infonce":
