@@ -119,7 +119,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 //   coef [NP]                d(sum dcor)/d(centred pair sum), for unit upstream grad
 //   out-scalars scratch
 //   bwd partial P [JS][V][n][d] floats, rowm [JS][V][n] floats
-constexpr int DCOR_JS = 8;
+constexpr int DCOR_JS = 16;  // j-splits of the backward tiles: 16 x 16 = 256 workgroups at n = 1024 (1 per CU)
 
 struct DcorWS {
   double* S; float* row; double* mean; double* Abar; double* coef;
@@ -226,65 +226,69 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
     }
 }
 
-// one block: means, centred sums, dcor values, backward coefficients
+// one block: means, centred sums, dcor values, backward coefficients.  Two reduction rounds: (1) every
+// view's row means (fixed j-tile order; a thread's rows the same for all views) and their block sums
+// -> Abar; (2) every pair's sum of mean products and of per-tile pair sums, reduced together.
 __global__ __launch_bounds__(1024) void dcor_finalize_kernel(int V, int64_t n, PairTab pt,
                                                              DcorWS ws, float* out) {
-  __shared__ double red[16];
-  __shared__ double redS[16];
+  __shared__ double red[2 * MAXP][16];
   __shared__ double Sc[MAXP];
   __shared__ double Ab[MAXV];
   const int64_t nt = (n + T - 1) / T;
   const int NP = V * (V + 1) / 2;
-  // row means (fixed j-tile order)
-  for (int a = 0; a < V; ++a) {
-    double loc = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+  // round 1: row means of every view
+  double loc[MAXV] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
+    for (int a = 0; a < V; ++a) {
       double s = 0.0;
       for (int64_t jt = 0; jt < nt; ++jt) s += (double)ws.row[((int64_t)a * nt + jt) * n + i];
       const double m = s / (double)n;
       ws.mean[(int64_t)a * n + i] = m;
-      loc += m;
+      loc[a] += m;
     }
-    loc = group_sum_d<64>(loc);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double s = 0.0;
-      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
-      Ab[a] = s / (double)n;
-      ws.Abar[a] = Ab[a];
-    }
-    __syncthreads();
+  for (int a = 0; a < V; ++a) {
+    const double t = group_sum_d<64>(loc[a]);
+    if (lane == 0) red[a][wv] = t;
   }
-  // centred pair sums
-  for (int a = 0; a < V; ++a)
-    for (int b = a; b < V; ++b) {
-      const int pi = pair_index(a, b, V);
-      double loc = 0.0, locS = 0.0;
-      for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
-        loc += ws.mean[(int64_t)a * n + i] * ws.mean[(int64_t)b * n + i];
-      // per-tile pair sums: strided over the block, then a fixed-shape tree (deterministic)
-      for (int64_t blk = threadIdx.x; blk < nt * nt; blk += blockDim.x) locS += ws.S[blk * NP + pi];
-      loc = group_sum_d<64>(loc);
-      locS = group_sum_d<64>(locS);
-      __syncthreads();
-      if ((threadIdx.x & 63) == 0) {
-        red[threadIdx.x >> 6] = loc;
-        redS[threadIdx.x >> 6] = locS;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double ab = 0.0, S = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-          ab += red[w];
-          S += redS[w];
-        }
-        const double dn = (double)n;
-        Sc[pi] = S - 2.0 * dn * ab + dn * dn * Ab[a] * Ab[b];
-      }
-      __syncthreads();
-    }
+  __syncthreads();
+  if (threadIdx.x < V) {
+    double s = 0.0;
+    for (int w = 0; w < nw; ++w) s += red[threadIdx.x][w];
+    Ab[threadIdx.x] = s / (double)n;
+    ws.Abar[threadIdx.x] = Ab[threadIdx.x];
+  }
+  __syncthreads();  // (this thread's means were written by itself: read back below without a fence)
+  // round 2: centred pair sums
+  double lab[MAXP], lS[MAXP];
+  for (int k = 0; k < NP; ++k) { lab[k] = 0.0; lS[k] = 0.0; }
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    double mv[MAXV];
+    for (int a = 0; a < V; ++a) mv[a] = ws.mean[(int64_t)a * n + i];
+    for (int a = 0; a < V; ++a)
+      for (int b = a; b < V; ++b) lab[pair_index(a, b, V)] += mv[a] * mv[b];
+  }
+  // per-tile pair sums: strided over the block, then a fixed-shape tree (deterministic)
+  for (int64_t blk = threadIdx.x; blk < nt * nt; blk += blockDim.x)
+    for (int k = 0; k < NP; ++k) lS[k] += ws.S[blk * NP + k];
+  for (int k = 0; k < NP; ++k) {
+    const double ta = group_sum_d<64>(lab[k]);
+    const double tS = group_sum_d<64>(lS[k]);
+    if (lane == 0) { red[2 * k][wv] = ta; red[2 * k + 1][wv] = tS; }
+  }
+  __syncthreads();
+  if (threadIdx.x < NP) {
+    const int pi = threadIdx.x;
+    double ab = 0.0, S = 0.0;
+    for (int w = 0; w < nw; ++w) { ab += red[2 * pi][w]; S += red[2 * pi + 1][w]; }
+    int a = 0, b = 0;
+    for (int x = 0; x < V; ++x)
+      for (int y = x; y < V; ++y)
+        if (pair_index(x, y, V) == pi) { a = x; b = y; }
+    const double dn = (double)n;
+    Sc[pi] = S - 2.0 * dn * ab + dn * dn * Ab[a] * Ab[b];
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     const double dn2 = (double)n * (double)n;
     double coef[MAXP];
