@@ -709,54 +709,60 @@ extern "C" int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float
 // ---------------------------------------------------------------------------------------------
 // Atomic scatter-add (run-to-run order of float additions not fixed; the deterministic counting
 // sort above is the engine's `deterministic` mode).  dW must hold the values to add onto (zeros
-// for a plain embedding gradient).  One 16-lane group per position (d = 64: float4 per lane);
-// positions of the `hot` row (HealthRec's ingredient padding id: about half of the 2B x 20
-// positions) are summed in registers, then across the workgroup in LDS, and added with one atomic
-// row update per workgroup instead of one per position.  Two launches (zero fill + this) replace
-// the eight of the sort path.
+// for a plain embedding gradient).  d = 64: one wave per position, lane = column, so each
+// position is ONE atomic wave-instruction over 256 contiguous bytes of its row (the shape the
+// memory-side atomic units run at full rate; four float4 lanes-per-row groups per instruction,
+// 16-B strided, ran ~5x slower); a wave's 32 indices come in one load and are broadcast by
+// readlane, and four gradient rows are loaded before their atomics are issued.  Positions of the
+// `hot` row (HealthRec's ingredient padding id: about half of the 2B x 20 positions) are summed in
+// registers, then across the workgroup in LDS, and added with one atomic row update per workgroup.
+// Two launches (zero fill + this) replace the eight of the sort path.
 namespace {
 
-constexpr int kAtomGroups = 16;        // 16-lane groups per 256-thread block
-constexpr int kAtomPerGroup = 8;       // positions per group per block -> 128 positions per block
+constexpr int kAtomWaves = 4;          // 256 threads
+constexpr int kAtomPerWave = 32;       // positions per wave -> 128 positions per block
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int k) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, k);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), k);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
 
 __global__ __launch_bounds__(256) void emb_atomic_kernel(const int64_t* __restrict__ idx, int64_t n,
                                                          const float* __restrict__ G, int64_t ldg, int64_t R,
                                                          int64_t pad, int64_t hot, float* __restrict__ dW,
                                                          int64_t lddw) {
-  __shared__ float4 hot_part[kAtomGroups][16];
-  const int q = threadIdx.x & 15;
-  const int grp = threadIdx.x >> 4;
-  float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int64_t base = (int64_t)blockIdx.x * kAtomGroups * kAtomPerGroup;
-  for (int k = 0; k < kAtomPerGroup; ++k) {
-    const int64_t i = base + (int64_t)k * kAtomGroups + grp;
-    if (i >= n) break;
-    const int64_t r = idx[i];
-    if (r < 0 || r >= R || r == pad) continue;
-    const float4 g = reinterpret_cast<const float4*>(G + i * ldg)[q];
-    if (r == hot) {
-      h = f4_add(h, g);
-    } else {
-      float* p = dW + r * lddw + 4 * q;
-      atomicAdd(p + 0, g.x);
-      atomicAdd(p + 1, g.y);
-      atomicAdd(p + 2, g.z);
-      atomicAdd(p + 3, g.w);
+  __shared__ float hot_part[kAtomWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kAtomWaves * kAtomPerWave + wv;  // positions base + 4k
+  const int64_t my_i = base + (int64_t)kAtomWaves * (lane & 31);
+  const int64_t my_r = (lane < 32 && my_i < n) ? idx[my_i] : -1;
+  float h = 0.f;
+#pragma unroll 1
+  for (int k0 = 0; k0 < kAtomPerWave; k0 += 4) {
+    int64_t r[4];
+    float g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      r[u] = readlane64(my_r, k0 + u);  // wave-uniform; -1 past n
+      const bool live = r[u] >= 0 && r[u] < R && r[u] != pad;
+      g[u] = live ? G[(base + (int64_t)kAtomWaves * (k0 + u)) * ldg + lane] : 0.f;
+      if (!live) r[u] = -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (r[u] < 0) continue;
+      if (r[u] == hot) h += g[u];
+      else atomicAdd(dW + r[u] * lddw + lane, g[u]);
     }
   }
   if (hot < 0 || hot >= R) return;  // block-uniform
-  hot_part[grp][q] = h;
+  hot_part[wv][lane] = h;
   __syncthreads();
-  if (grp == 0) {
-    float4 t = hot_part[0][q];
-    for (int g2 = 1; g2 < kAtomGroups; ++g2) t = f4_add(t, hot_part[g2][q]);
-    if (t.x != 0.f || t.y != 0.f || t.z != 0.f || t.w != 0.f) {
-      float* p = dW + hot * lddw + 4 * q;
-      atomicAdd(p + 0, t.x);
-      atomicAdd(p + 1, t.y);
-      atomicAdd(p + 2, t.z);
-      atomicAdd(p + 3, t.w);
-    }
+  if (wv == 0) {
+    float t = hot_part[0][lane];
+    for (int w2 = 1; w2 < kAtomWaves; ++w2) t += hot_part[w2][lane];
+    if (__ballot(t != 0.f)) atomicAdd(dW + hot * lddw + lane, t);
   }
 }
 
@@ -771,7 +777,7 @@ extern "C" int fr_embedding_bwd_atomic(const int64_t* d_idx, int64_t n, const fl
   FR_REQUIRE(d_idx && d_grad && d_out, "null argument");
   FR_REQUIRE(ldg >= d && ldg % 4 == 0 && fr::aligned16(d_grad) && ldo >= d && ldo % 4 == 0 && fr::aligned16(d_out),
              "grad / out must be 16-B aligned with ld % 4 == 0");
-  const int64_t per_block = (int64_t)kAtomGroups * kAtomPerGroup;
+  const int64_t per_block = (int64_t)kAtomWaves * kAtomPerWave;
   const int64_t blocks = fr::ceil_div(n, per_block);
   FR_REQUIRE(blocks < (int64_t)INT32_MAX, "too many positions");
   hipLaunchKernelGGL(emb_atomic_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),

@@ -511,15 +511,16 @@ def test_feed_batch_one_launch_matches_gathers(cuda):
         np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep0/{key}"])
 
 
+@pytest.mark.parametrize("n", [1024 * 20, 1000])
 @pytest.mark.parametrize("hot", [None, 19987, 5])
-def test_embedding_bwd_atomic_matches_sorted(cuda, hot):
+def test_embedding_bwd_atomic_matches_sorted(cuda, hot, n):
     """fr_embedding_bwd_atomic (float atomics, the hot row pre-summed per workgroup) against the
     deterministic counting-sort scatter: equal to fp32 rounding (rel 1e-5 of the row scale), the
     padding_idx row skipped, out-of-range ids ignored; HealthRec's shape ([1024 x 20] positions,
-    about half of them the padding ingredient 19987, into 19988 rows)."""
+    about half of them the padding ingredient 19987, into 19988 rows), and a ragged position count."""
     from FoodRec.engine import ops
     g = torch.Generator().manual_seed(3)
-    R, n = 19988, 1024 * 20
+    R = 19988
     ids = torch.randint(0, R - 1, (n,), generator=g)
     ids[torch.rand(n, generator=g) < 0.5] = 19987
     ids[7] = R + 5  # out of range: skipped by both paths
