@@ -186,6 +186,44 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic_kernel(
   }
 }
 
+// d = 64: one wave per triple, lane = column -- every row update is ONE atomic wave-instruction over
+// 256 contiguous bytes (the full-rate shape of the memory-side atomic units; the float4-per-lane form
+// above issues four 16-B-strided instructions per four rows).  Same per-element arithmetic.
+__global__ __launch_bounds__(256) void bpr_bwd_atomic64_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
+    const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, float gamma, float gmf, float greg, const float* gscale, float* dU, int64_t lddu,
+    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws,
+    const float* __restrict__ extra, int64_t ldx) {
+  const int lane = threadIdx.x & 63;
+  if (gscale) { gmf *= gscale[0]; if (dUe || dIe) greg *= gscale[1]; }
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  for (int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; b < B; b += (int64_t)gridDim.x * 4) {
+    const int64_t u = uu[b], p = pp[b], n = nn[b];
+    const float g = bpr_coef(ws, b, B, gamma, gmf);
+    const float xu = U[u * ldu + lane], xp = I[p * ldi + lane], xn = I[n * ldi + lane];
+    if (dU) atomicAdd(dU + u * lddu + lane, fmaf(-g, xn, g * xp));
+    if (dI) {
+      float tp = g * xu, tn = -g * xu;
+      if (extra) {
+        tp += extra[b * ldx + lane];
+        tn += extra[(B + b) * ldx + lane];
+      }
+      atomicAdd(dI + p * lddi + lane, tp);
+      atomicAdd(dI + n * lddi + lane, tn);
+    }
+    if (Ue && dUe) atomicAdd(dUe + u * lddue + lane, ru * Ue[u * ldue + lane]);
+    if (Ie && dIe) {
+      atomicAdd(dIe + p * lddie + lane, rp * Ie[p * ldie + lane]);
+      atomicAdd(dIe + n * lddie + lane, rn * Ie[n * ldie + lane]);
+    }
+  }
+}
+
 // The tail of HealthRec's fused propagation backward (fr_graph_bpr_finish): clear the batch rows'
 // column-mask bytes (users at u, items at U + pos / U + neg), add the EmbLoss gradient of the ego
 // rows (the same per-row terms and float atomics as bpr_bwd_atomic_kernel's dUe / dIe branch, with
@@ -205,6 +243,26 @@ __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
   const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
   if (blockIdx.x == 0)
     for (int k = threadIdx.x; k < zero_n; k += 256) zero[k] = 0.f;
+  if (d4 == 16) {  // d = 64: one wave per triple, lane = column (one 256-B atomic instruction per row)
+    const int lane = threadIdx.x & 63;
+    for (int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; b < B; b += (int64_t)gridDim.x * 4) {
+      const int64_t u = uu[b], p = pp[b], n = nn[b];
+      if (mask && lane == 0) {
+        mask[u] = 0;
+        mask[U + p] = 0;
+        mask[U + n] = 0;
+      }
+      if (bits && lane == 0) {
+        atomicAnd(bits + (u >> 5), ~(1u << (u & 31)));
+        atomicAnd(bits + ((U + p) >> 5), ~(1u << ((U + p) & 31)));
+        atomicAnd(bits + ((U + n) >> 5), ~(1u << ((U + n) & 31)));
+      }
+      atomicAdd(dUe + u * lddue + lane, ru * Ue[u * ldue + lane]);
+      atomicAdd(dIe + p * lddie + lane, rp * Ie[p * ldie + lane]);
+      atomicAdd(dIe + n * lddie + lane, rn * Ie[n * ldie + lane]);
+    }
+    return;
+  }
   for (int64_t b = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; b < B; b += (int64_t)gridDim.x * GPB) {
     const int64_t u = uu[b], p = pp[b], n = nn[b];
     if (mask && q0 == 0) {
@@ -501,6 +559,11 @@ static int bpr_bwd_impl(const float* d_U, int64_t ldu, const float* d_I, int64_t
     hipLaunchKernelGGL(bpr_bwd_det_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
                        ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
                        ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
+  } else if (d == 64) {
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 4), 4096);
+    hipLaunchKernelGGL(bpr_bwd_atomic64_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
+                       ldue, d_Ie, ldie, d_u, d_p, d_n, B, gamma, g_mf, g_reg, d_gscale, d_dU,
+                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w, d_extra, ldx);
   } else {
     const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
     hipLaunchKernelGGL(bpr_bwd_atomic_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
@@ -545,7 +608,7 @@ extern "C" int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue
              "tables must be 16-B aligned with ld % 4 == 0");
   FR_REQUIRE(d_workspace && workspace_bytes >= bpr_ws_bytes(B) && fr::aligned16(d_workspace), "workspace too small");
   BprWS w = bpr_ws(d_workspace, B);
-  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, 256 / LPR), 4096);
+  const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(B, d == 64 ? 4 : 256 / LPR), 4096);
   hipLaunchKernelGGL(graph_bpr_finish_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_mask,
                      U, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, g_reg, d_greg, d_dUe, ldue, d_dIe, ldie, w,
                      d_zero, zero_n, d_bits);
