@@ -167,6 +167,11 @@ __device__ __forceinline__ void dist4x4(const float* At, const float* Bt, const 
     }
 }
 
+// D is symmetric, so only the tiles it <= jt are computed: an off-diagonal tile gives the row sums
+// of its it rows over column tile jt AND (as its column sums) the row sums of its jt rows over
+// column tile it, and counts twice in the pair sums; blocks below the diagonal only zero their
+// pair-sum slots.  (D_ij and D_ji differ in the last bits -- (r_i - 2g) + r_j vs (r_j - 2g) + r_i --
+// so this is a rounding-level change from evaluating both.)
 template <int V>
 __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int d, DcorWS ws) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -175,10 +180,16 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
   float* ra = Bt + d * PADT;        // [64]
   float* rb = ra + T;               // [64]
   double* red = reinterpret_cast<double*>(rb + T);  // [4]
+  __shared__ float colp[16][T];     // column partial sums (4 rows each) of an off-diagonal tile
   const int64_t nt = (n + T - 1) / T;
   const int it = blockIdx.x, jt = blockIdx.y;
   const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
   const int NP = V * (V + 1) / 2;
+  if (jt < it) {  // below the diagonal: the transposed tile carries it
+    if (threadIdx.x < NP) ws.S[((int64_t)it * nt + jt) * NP + threadIdx.x] = 0.0;
+    return;
+  }
+  const bool off = jt > it;
   float D[V][4][4];
 #pragma unroll
   for (int a = 0; a < V; ++a) {
@@ -209,6 +220,17 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
       const int64_t gi = (int64_t)it * T + 4 * ti + x;
       if (tj == 0 && gi < n) ws.row[((int64_t)a * nt + jt) * n + gi] = rs;
     }
+    if (off) {  // column sums = the jt rows' sums over column tile it (16 row groups, in order)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) colp[ti][4 * tj + y] = ((D[a][0][y] + D[a][1][y]) + D[a][2][y]) + D[a][3][y];
+      __syncthreads();
+      if (threadIdx.x < T) {
+        float cs = 0.f;
+        for (int k = 0; k < 16; ++k) cs += colp[k][threadIdx.x];
+        const int64_t gj = (int64_t)jt * T + threadIdx.x;
+        if (gj < n) ws.row[((int64_t)a * nt + it) * n + gj] = cs;
+      }
+    }
   }
   // all unordered pair sums from the same tiles
   const int64_t blk = (int64_t)it * nt + jt;
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
 #pragma unroll
         for (int y = 0; y < 4; ++y) s += (double)D[a][x][y] * (double)D[b][x][y];
       s = block_sum_d(s, red);
-      if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = s;
+      if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = off ? 2.0 * s : s;
     }
 }
 
