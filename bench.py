@@ -38,7 +38,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 def _args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); N > 1 without a torch.distributed environment starts "
+                         "the N ranks itself under torch.distributed.run (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="healthrec_allrecipes", choices=["healthrec_allrecipes"])
@@ -52,6 +54,9 @@ def _args():
                     help="eager steps of the per-kernel HIP-event timing pass (roofline)")
     ap.add_argument("--no-spmm-10m", action="store_true",  # also skips the config-4 training step
                     help="skip the SpMM measurement on the 10M x 1M x 200M synthetic graph")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launcher self-test: start the ranks, join the process group (gloo, CPU), assert "
+                         "the world size and print the n_gpus line -- no GPU work")
     ap.add_argument("--config-json", default=None, help="extra config keys for the HealthRec step (JSON)")
     ap.add_argument("--no-config3", action="store_true",
                     help="skip BASELINE config 3 (CLUSSL on Foodcom-shape data, dCor and InfoNCE SSL)")
@@ -79,19 +84,80 @@ def build(device, batch, seed=0, dataset_seed=0, extra=None):
     return cfg, data, model
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_command(gpus: int, argv, port: int):
+    """The child command that starts ``gpus`` ranks of this script (one process per GPU, rendezvous on
+    127.0.0.1): torch.distributed.run with the caller's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(gpus)}",
+            "--master-addr", "127.0.0.1", "--master-port", str(int(port)), os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """``--gpus N > 1`` run outside torch.distributed: start the N ranks as a CHILD process and return
+    its exit status.  This process imports nothing that touches HIP (the ranks own the GPUs); rank 0
+    prints the JSON line on the shared stdout."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL across processes)
+    return subprocess.run(launch_command(gpus, argv, _free_port()), env=env).returncode
+
+
+def resolve_world(gpus, environ) -> int:
+    """Ranks this process belongs to: WORLD_SIZE when launched by torch.distributed.run (it must equal
+    ``--gpus`` when both are given), else ``--gpus`` (default 1)."""
+    if "WORLD_SIZE" in environ:
+        world = int(environ["WORLD_SIZE"])
+        if gpus is not None and int(gpus) != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the launcher started a "
+                             f"different number of ranks")
+        return world
+    return 1 if gpus is None else int(gpus)
+
+
+def _check_launch(args, world, rank):
+    """--check-launch: the process-group half of a multi-rank run on the CPU (gloo)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+        got = dist.get_world_size()
+        dist.destroy_process_group()
+    else:
+        got = 1
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "n_gpus": got, "gpus_requested": args.gpus,
+                          "backend": "gloo" if world > 1 else None}), flush=True)
+    return 0
+
+
 def main():
     args = _args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    world = resolve_world(args.gpus, os.environ)
+    args.gpus = world
+    rank = int(os.environ.get("RANK", "0"))
+    if args.check_launch:
+        return _check_launch(args, world, rank)
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # FR_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks sharing one GPU (the driver's
     # multi-GPU runs use RCCL, one rank per GPU)
     backend = os.environ.get("FR_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())
+    if world > 1 and backend == "nccl" and ndev < world:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {ndev} visible "
+                         f"(FR_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
+    local = local % ndev
     # FR_BENCH_DP1=1: the data-parallel step (row exchange + dense all-reduce through RCCL, graphs A /
     # B1 / B2 around the collectives) at world 1 -- the per-rank cost of the N > 1 path on one GPU
     dp1 = world == 1 and os.environ.get("FR_BENCH_DP1") == "1"
@@ -105,7 +171,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        # the job really runs ``world`` ranks: checked against the process group itself
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
     device = torch.device("cuda", local)
+    ranks = _rank_report(world, backend, device) if world > 1 else None
 
     from FoodRec.common.trainer import Trainer
     from FoodRec.engine import profiling
@@ -284,16 +353,28 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
 
+    # the config-4 row-sharded step at a fixed global batch (strong scaling): the north star's
+    # "10M-user/1M-item" scaling figure, beside the HealthRec data-parallel `value` (weak scaling)
+    c4_scaling = None
+    if c4 is not None:
+        sh = c4.get("sharded_p1") if world == 1 else c4
+        c4_scaling = {"workload": "config4_10m LightGCN_ID row-sharded (U=10M, I=1M, E=200M, d=64)",
+                      "scaling": "strong", "ranks": world,
+                      "per_global_batch": {b: {"ms_per_step": v["ms_per_step"], "triples_per_s": v["triples_per_s"]}
+                                           for b, v in sh["step"].items()},
+                      "note": "every rank steps the same global batch B; triples_per_s = B / max-over-ranks "
+                              "step time; compare across n_gpus at equal B"}
+    n_pg = dist.get_world_size() if world > 1 else 1
     if rank == 0:
         line = {"metric": "BPR triples/sec + SpMM HBM GB/s, Allrecipes d=64, 1/2/4/8 MI355X",
-                "value": round(value, 1), "unit": "triples/s", "n_gpus": world, "steps": args.steps,
+                "value": round(value, 1), "unit": "triples/s", "n_gpus": n_pg, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
                 "config": {"workload": "healthrec_allrecipes", "model": "HealthRec (CIKM_Model)",
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single")},
-                "roofline": roofline, "step_bytes": step_fig,
+                "roofline": roofline, "ranks": ranks, "scaling_config4": c4_scaling, "step_bytes": step_fig,
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
                                    "ms_per_step_without": round(ms_steps, 4),
@@ -848,5 +929,28 @@ def config1(device, steps=50, warmup=5, cpu=True, cpu_steps=20):
     return out
 
 
+def _rank_report(world, backend, device):
+    """What the job runs on, from the process group: its size, backend, the distinct GPUs behind the
+    ranks (PCI bus ids), and -- over RCCL -- the rank count of an engine C-ABI communicator
+    (fr_comm_init) joined by every rank."""
+    import torch
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(device)
+    ident = f"{getattr(props, 'pci_bus_id', '?')}:{getattr(props, 'pci_device_id', '?')}:{device.index}"
+    allid = [None] * world
+    dist.all_gather_object(allid, ident)
+    rep = {"process_group_world_size": dist.get_world_size(), "backend": dist.get_backend(),
+           "distinct_gpus": len(set(allid)), "rccl_comm_ranks": None}
+    if backend == "nccl":
+        from FoodRec.engine.comm import RcclComm
+        comm = RcclComm.from_process_group()
+        one = torch.ones(1, device=device)
+        comm.all_reduce(one)  # every rank contributes 1: the communicator's rank count
+        rep["rccl_comm_ranks"] = int(one.item())
+        assert comm.world == world and rep["rccl_comm_ranks"] == world, rep
+        comm.close()
+    return rep
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -207,12 +207,16 @@ int fr_adam_step(float* const* params, const float* const* grads,
 /* Device-scalar variant (graph-capturable optimiser step): each tensor's step counter lives in
  * device memory (int64, incremented by the call before use) and the learning rate is read from
  * d_lr (device double; NULL -> lr), so a captured step replays with the current step and lr.
- * d_steps is a HOST array of device pointers, one per tensor. */
+ * d_steps is a HOST array of device pointers, one per tensor.  The launch's last workgroup bumps
+ * the counters; it finds out that it is last through d_ticket, FR_ADAM_TICKET_WORDS device uint32
+ * words owned by the caller (16-byte aligned, zero before first use; every launch leaves them zero).
+ * Launches that share ticket words must not overlap: give each optimiser its own. */
+#define FR_ADAM_TICKET_WORDS 32
 int fr_adam_step_dev(float* const* params, const float* const* grads,
                      float* const* exp_avg, float* const* exp_avg_sq,
                      int64_t* const* d_steps, const int64_t* numel, int n_tensors,
                      const double* d_lr, double lr, double beta1, double beta2, double eps,
-                     double weight_decay, const int32_t* d_skip, void* stream);
+                     double weight_decay, const int32_t* d_skip, uint32_t* d_ticket, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Negative sampler (host code): numpy legacy MT19937 stream, masked-rejection bounded ints,
@@ -341,7 +345,7 @@ int fr_adam_step_rows(float* const* params, const float* const* grads, float* co
                       float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                       const int32_t* const* d_rmaps, const int32_t* row_dims, int n_tensors, const double* d_lr,
                       double lr, double beta1, double beta2, double eps, double weight_decay,
-                      const int32_t* d_skip, void* stream);
+                      const int32_t* d_skip, uint32_t* d_ticket, void* stream);
 
 /* Row-gradient Adam with deferred zero-gradient steps (exact "lazy rows").  Same contract as
  * fr_adam_step_rows (torch.optim.Adam.step, common/trainer.py:224, over cikm_model.py:83-87's
@@ -696,20 +700,23 @@ int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t l
  *   out_health[j] = health[pn[j]] ([H] float, optional: H = 0 and NULLs), out_kpm[j][c] =
  *   -inf where out_codes[j][c] == pad, else 0 (optional: HealthRec's key-padding mask,
  *   cikm_model.py:231-232, in the additive float form the encoder layer consumes).
+ *   An item id outside [0, n_items) is replaced by 0 in every output (p / n included) and sets the
+ *   sticky device flag *d_err = 1 (optional: NULL) that the trainer checks at epoch end.
  * ------------------------------------------------------------------------------------------ */
 int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* d_items, const int64_t* d_negs,
                   const int64_t* d_cursor, int64_t B, int64_t* d_u, int64_t* d_p, int64_t* d_n,
                   const int64_t* d_codes, int L, const int64_t* d_nums, const float* d_health, int H,
                   int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes, int64_t* d_out_nums,
-                  float* d_out_health, float* d_out_kpm, void* stream);
+                  float* d_out_health, float* d_out_kpm, int32_t* d_err, void* stream);
 
 /* fr_step_book: the training loop's per-step loss bookkeeping (common/trainer.py:183-193) on the
  * device: acc[i] (+)= (double)*parts[i] for the n (<= 8) scalar loss components,
  * *nan |= isnan(sum of the parts in fp32, left to right), and each of the n_counters (<= 8) device
- * int64 step counters += 1 (dropout-hash step counters, the device feed's batch cursor).  One
- * launch, no host sync. */
+ * int64 step counters += 1 (dropout-hash step counters, the device feed's batch cursor), and, when
+ * d_loss_out is not NULL, *d_loss_out = that fp32 sum (the loss the step returns,
+ * common/trainer.py:225).  One launch, no host sync. */
 int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan,
-                 int64_t* const* d_counters, int n_counters, void* stream);
+                 int64_t* const* d_counters, int n_counters, float* d_loss_out, void* stream);
 
 /* fr_reg_combine_fwd / _bwd: HealthRec's weighted EmbLoss from its two fused pieces,
  * out = w * (a[0] + (b[0] + ... + b[nb-1]) / B)  (cikm_model.py:267-279); backward da = g w,

@@ -63,15 +63,18 @@ def metrics_by_user(doc_list, rel_list):
 
 def book_step(parts, acc, nan_flag, accumulate=True):
     """fr_step_book over the loss parts (device float scalars): acc (+)= parts, nan |= isnan(sum),
-    and the step's deferred device counters (ops.defer_increment) advanced in the same launch."""
+    and the step's deferred device counters (ops.defer_increment) advanced in the same launch.
+    Returns the step's loss (the fp32 sum of the parts, a fresh device scalar; no host sync)."""
     import ctypes
     from FoodRec.engine import native
     n = len(parts)
     ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in parts])
     ctrs = ops.take_pending_counters()
     cptr = (ctypes.c_void_p * max(1, len(ctrs)))(*[c.data_ptr() for c in ctrs])
+    loss = torch.empty((), dtype=torch.float32, device=acc.device)
     native.check(native.lib().fr_step_book(ptrs, n, acc.data_ptr(), int(bool(accumulate)), nan_flag.data_ptr(),
-                                           cptr, len(ctrs), native.stream_of(acc)), "fr_step_book")
+                                           cptr, len(ctrs), loss.data_ptr(), native.stream_of(acc)), "fr_step_book")
+    return loss
 
 
 # Captures are thread-local: the process group's watchdog thread polls its collectives' events
@@ -214,7 +217,7 @@ class GraphedDPStep(GraphedStep):
         try:
             losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
             parts = losses if isinstance(losses, tuple) else (losses,)
-            fused = tr._book_fused(state, parts, accumulate)
+            fused = tr._book_fused(state, parts, accumulate) is not None
         finally:
             ops.defer_counters(False)
         if fused:
@@ -400,8 +403,10 @@ class Trainer(AbstractTrainer):
         # host-side batch work (SCHGN's masked-ingredient SSL draws Python's random per batch) cannot
         # be captured: those configurations step eagerly
         # (and only the fused Adam reads the NaN flag on the device: other optimisers step eagerly)
+        # and a model whose step sizes launches from host reads (graph_capturable = False: the
+        # row-list propagation of LightGCN_ID / ShardedLightGCN) steps eagerly too
         self.use_graph = (bool(config["cuda_graph"]) and self._on_gpu() and not config["SCHGN_ssl"]
-                          and isinstance(self.optimizer, FusedAdam))
+                          and isinstance(self.optimizer, FusedAdam) and getattr(model, "graph_capturable", True))
         self._graphed = None
 
     @property
@@ -464,13 +469,15 @@ class Trainer(AbstractTrainer):
         try:
             losses = loss_func(interaction)
             parts = losses if isinstance(losses, tuple) else (losses,)
-            fused = second_inter is None and self._book_fused(state, parts, accumulate)
+            booked = self._book_fused(state, parts, accumulate) if second_inter is None else None
         finally:
             ops.defer_counters(False)  # (applies the increments eagerly when the step was not booked)
-        if fused:
-            # the loss sum is never materialised: each part back-propagates with a cached ones seed
+        if booked is not None:
+            # the loss sum is never materialised for autograd: each part back-propagates with a
+            # cached ones seed; the returned loss is fr_step_book's fp32 sum of the parts
             torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
-            return self._finish_step(state)
+            self._finish_step(state)
+            return booked
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
         if state.get("acc") is None:
@@ -506,21 +513,21 @@ class Trainer(AbstractTrainer):
         self._opt_step(state["nan"])
         return None
 
-    def _book_fused(self, state, parts, accumulate) -> bool:
+    def _book_fused(self, state, parts, accumulate):
         """Per-step loss bookkeeping in one HIP launch (fr_step_book): state['acc'] (float64 sums
-        of every loss part) and the sticky NaN flag of sum(parts).  False when it does not apply
-        (CPU, more than 8 parts, non-fp32 or non-scalar parts)."""
+        of every loss part) and the sticky NaN flag of sum(parts).  Returns the step's loss (the
+        fp32 sum, a device scalar), or None when it does not apply (CPU, more than 8 parts,
+        non-fp32 or non-scalar parts)."""
         if not (len(parts) <= 8 and all(torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
                                           and x.numel() == 1 and x.is_contiguous() and x.requires_grad
                                           for x in parts)):
-            return False
+            return None
         if state.get("acc") is None:
             state["acc"] = torch.zeros(len(parts), dtype=torch.float64, device=parts[0].device)
             accumulate = False
         elif state["acc"].numel() != len(parts):
-            return False
-        book_step(parts, state["acc"], state["nan"], accumulate)
-        return True
+            return None
+        return book_step(parts, state["acc"], state["nan"], accumulate)
 
     def _ones_like(self, parts):
         cache = self.__dict__.setdefault("_ones_cache", {})
@@ -569,6 +576,8 @@ class Trainer(AbstractTrainer):
             for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
                 loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
         self.flush_optimizer()
+        if hasattr(feats, "check_ids"):
+            feats.check_ids()
         if state["acc"] is None:
             return 0.0, loss_batches, None
         if int(state["nan"].item()):

@@ -76,7 +76,12 @@ class RowExchange:
             self.sink.join_background()
 
     def stash(self, weight, padding_idx, ids, G, W=None):
-        key = id(ids)  # tables stashed with the same ids tensor (HealthRec's image / text) share ids
+        # tables stashed with the same ids tensor (HealthRec's image / text) share one ids region.
+        # The key is the ids' memory, and the slot holds a reference to them until the exchange, so
+        # no other ids tensor can occupy that memory meanwhile (a Python id() of a freed temporary
+        # can be recycled within one backward)
+        key = (ids.data_ptr(), tuple(ids.shape), ids.dtype)
+        src = ids
         ids = ids.to(torch.int64)
         G = G.to(torch.float32)
         s = self.slots.get(id(weight))
@@ -88,6 +93,7 @@ class RowExchange:
             self.slots[id(weight)] = s
             self._send = self._recv = None  # layout changed: repack at the next exchange
         s["key"] = key
+        s["ids_src"] = src
         if not (s.get("shared") and key in self._ids_done):  # a shared ids region is written once
             s["ids"].copy_(ids)
             self._ids_done.add(key)
@@ -135,9 +141,19 @@ class RowExchange:
 
     def exchange(self):
         import torch.distributed as dist
+        if self._send is not None and any(len(slots) > 1 and len({s["key"] for s in slots}) > 1
+                                          for slots in self._groups):
+            # tables packed as sharing ids were stashed with different ids this step: every slot
+            # takes its own ids again and the buffers are repacked by this step's keys
+            for s in self.slots.values():
+                s["ids"] = s["ids_src"].to(torch.int64).clone()
+                s["G"] = s["G"].clone()
+            self._send = None
         if self._send is None:
             self._pack()
         self._ids_done.clear()
+        for s in self.slots.values():
+            s.pop("ids_src", None)
         # one collective for every table (views of these static buffers are what graph B reads)
         if dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(self._recv, self._send, group=self.group)

@@ -77,12 +77,12 @@ _SIGS = {
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "fr_step_book": (c_int, [POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p, POINTER(c_void_p), c_int,
-                             c_void_p]),
+                             c_void_p, c_void_p]),
     "fr_embedding_bwd_atomic": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_int64,
                                         c_void_p, c_int64, c_void_p]),
     "fr_feed_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int64, c_int64, c_void_p,
-                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_bpr_workspace": (c_int64, [c_int64]),
     "fr_embedding_bwd_workspace": (c_int64, [c_int64, c_int64, c_int]),
     "fr_embedding_bwd_status_offset": (c_int64, [c_int64]),
@@ -128,7 +128,7 @@ _SIGS = {
                              c_double, c_int64, c_void_p, c_void_p]),
     "fr_adam_step_dev": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                                  POINTER(c_void_p), POINTER(c_int64), c_int, c_void_p, c_double, c_double,
-                                 c_double, c_double, c_double, c_void_p, c_void_p]),
+                                 c_double, c_double, c_double, c_void_p, c_void_p, c_void_p]),
     "fr_spmm_bf16_workspace": (c_int64, [POINTER(FrSpmmPlan), c_int]),
     "fr_spmm_csr_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, POINTER(FrSpmmPlan),
                                  c_void_p, c_int64, c_int,
@@ -155,7 +155,8 @@ _SIGS = {
                                      c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_adam_step_rows": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                                   POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_int32), c_int,
-                                  c_void_p, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p]),
+                                  c_void_p, c_double, c_double, c_double, c_double, c_double, c_void_p, c_void_p,
+                                  c_void_p]),
     "fr_adam_step_rows_lazy": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                                        POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_void_p),
                                        POINTER(c_int64), POINTER(c_int32),

@@ -294,9 +294,12 @@ def propagate_rows(adj: Adjacency, ego: torch.Tensor, n_layers: int, rows) -> to
     """mean([ego, A ego, ..., A^L ego]) evaluated at the listed rows only ([(ids, offset), ...], up
     to three segments) -- the table is valid there and nowhere else; the gradient flowing back must
     be zero outside those rows (a BPR / EmbLoss on them).  fp32, d = 64 on the GPU, non-deterministic
-    mode; otherwise the full propagate_mean."""
+    mode; otherwise the full propagate_mean.  The row set is built with host reads (its size sets
+    the launch shapes), so inside a HIP-graph capture the full propagation runs instead (its
+    results agree at the listed rows)."""
     if (n_layers >= 1 and ego.is_cuda and ego.dtype == torch.float32 and ego.shape[1] == 64 and not _DETERMINISTIC
-            and adj.shape[0] == adj.shape[1] and 1 <= len(rows) <= 3):
+            and adj.shape[0] == adj.shape[1] and 1 <= len(rows) <= 3
+            and not torch.cuda.is_current_stream_capturing()):
         rows = [(ids.reshape(-1).to(torch.int64).contiguous(), int(off)) for ids, off in rows]
         return _PropagateRows.apply(adj, ego, int(n_layers), rows)
     return propagate_mean(adj, ego, n_layers)

@@ -329,6 +329,15 @@ class FusedAdam(torch.optim.Optimizer):
             dense = ops.scatter_rows(ids.reshape(-1), G.reshape(-1, w.shape[-1]), w.shape[0], pad)
             w.grad = dense if w.grad is None else w.grad.add_(dense)
 
+    def _ticket(self, device) -> int:
+        """This optimiser's arrival words for the device-scalar launches (fr_adam_step_dev's d_ticket):
+        its own, so two optimisers stepping concurrently never share them."""
+        tk = self.__dict__.setdefault("_tickets", {})
+        t = tk.get(device)
+        if t is None:
+            t = tk[device] = torch.zeros(32, dtype=torch.int32, device=device)  # FR_ADAM_TICKET_WORDS
+        return t.data_ptr()
+
     def _lr_tensor(self, gi, group, device):
         t, held = self._d_lr.get(gi, (None, None))
         if t is None:
@@ -450,7 +459,8 @@ class FusedAdam(torch.optim.Optimizer):
     def _launch_dense(self, lib, plist, hyper):
         grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in plist]
         P, G, M, V, S, N = self._arrays(plist, grads)
-        native.check(lib.fr_adam_step_dev(P, G, M, V, S, N, len(plist), *hyper), "fr_adam_step_dev")
+        native.check(lib.fr_adam_step_dev(P, G, M, V, S, N, len(plist), *hyper[:-1], self._ticket(plist[0].device),
+                                          hyper[-1]), "fr_adam_step_dev")
 
     def _prepare_factored(self, lib) -> dict:
         """Compact rows + row map of every factored entry: one fr_embedding_rowgrad over the entries'
@@ -552,7 +562,8 @@ class FusedAdam(torch.optim.Optimizer):
             return
         with profiling.region("adam_rows", sum(adam_rows_bytes(p.numel(), p.shape[0], c.numel())
                                               for p, c in zip(plist, compact))):
-            native.check(lib.fr_adam_step_rows(P, G, M, V, S, N, RM, RD, n, *hyper), "fr_adam_step_rows")
+            native.check(lib.fr_adam_step_rows(P, G, M, V, S, N, RM, RD, n, *hyper[:-1], self._ticket(plist[0].device),
+                                               hyper[-1]), "fr_adam_step_rows")
 
     def _step_bf16(self, p, group, lib, skip_flag, gi):
         """bf16 parameter: update the fp32 master with fp32 moments, re-round the parameter."""

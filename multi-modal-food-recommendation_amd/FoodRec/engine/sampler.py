@@ -264,7 +264,23 @@ class BatchFeatures:
             native.ptr(u), p.data_ptr(), n.data_ptr(), self.ingre_code.data_ptr(), self.ingre_code.shape[1],
             self.ingre_num.data_ptr(), native.ptr(h), H, self.ingre_code.shape[0], self.pad_id,
             out["pn_i_id"].data_ptr(), out["pn_ingre_code"].data_ptr(), out["pn_ingre_num"].data_ptr(),
-            native.ptr(out.get("pn_hl_mh")), out["pn_pad_kpm"].data_ptr(), native.stream_of(p)), "fr_feed_batch")
+            native.ptr(out.get("pn_hl_mh")), out["pn_pad_kpm"].data_ptr(), self.id_error_flag().data_ptr(),
+            native.stream_of(p)), "fr_feed_batch")
+
+    def id_error_flag(self):
+        """Sticky device flag fr_feed_batch sets when a batch carried an item id outside the item
+        table (replaced by item 0); the trainer checks it at epoch end (one host read)."""
+        f = self.__dict__.get("_id_err")
+        if f is None:
+            f = self._id_err = torch.zeros((), dtype=torch.int32, device=self.device)
+        return f
+
+    def check_ids(self):
+        f = self.__dict__.get("_id_err")
+        if f is not None and int(f.item()):
+            f.zero_()
+            raise RuntimeError("fr_feed_batch met item ids outside the item table (sampler or staging bug); "
+                               "they were replaced by item 0")
 
     def launch_feed(self, feed, u, p, n, out):
         self._launch(feed.perm, feed.users, feed.items, feed.negs, feed.cursor, feed.B, u, p, n, out)

@@ -397,6 +397,9 @@ class ShardedLightGCN(nn.Module):
     the replicated item table.  Initialised from the same seed as the single-GPU model (the full
     user table is drawn on every rank and sliced), so P ranks start from identical global tables."""
 
+    # the rows form sizes its launches from host reads (the agreed row set S): Trainer steps it eagerly
+    graph_capturable = False
+
     def __init__(self, graph: ShardedGraph, d=64, n_layers=2, reg_weight=0.1, group=None, seed=999):
         super().__init__()
         self.g, self.L, self.reg_weight, self.group, self.d = graph, int(n_layers), float(reg_weight), group, d
@@ -412,7 +415,8 @@ class ShardedLightGCN(nn.Module):
     def calculate_loss(self, batch):
         u, p, n = batch["u_id"], batch["pos_i_id"], batch["neg_i_id"]
         _, loc = self.g.owner_index(u)
-        if self.L == 2 and self.ego_u.is_cuda and self.d == 64 and not ops._DETERMINISTIC:
+        if (self.L == 2 and self.ego_u.is_cuda and self.d == 64 and not ops._DETERMINISTIC
+                and not torch.cuda.is_current_stream_capturing()):
             # the loss reads the propagated tables at the batch rows only (rows form)
             p, n = p.to(torch.int64).contiguous(), n.to(torch.int64).contiguous()
             out_u, out_i = _ShardedPropagateRows.apply(self.ego_u, self.ego_i, self.g, self.group,

@@ -34,6 +34,10 @@ class _TableView:
 
 
 class LightGCN_ID(GeneralRecommender):
+    # the row-list propagation (ops.propagate_rows) sizes its launches from host reads: Trainer steps
+    # this model eagerly (inside an explicit capture the full propagation runs instead)
+    graph_capturable = False
+
     def __init__(self, config, dataset):
         super().__init__(config, dataset)
         self.latent_dim = config["embedding_size"]

@@ -35,6 +35,7 @@ struct AdamArgs {
   // g[r] = rmap[r] >= 0 ? G[rmap[r]] : 0 (compact rows from fr_embedding_rowgrad)
   const int32_t* rmap[kMaxTensors];
   int32_t rshift[kMaxTensors];
+  unsigned* ticket;  // device-scalar mode: the caller's 9-word arrival counters (last_block)
   int n;
 };
 
@@ -85,9 +86,10 @@ __device__ __forceinline__ void adam4(float* P, const float* G, float* M, float*
 // read the counters) writes step + 1 back.  Arrival is two-level so that hundreds of blocks do not
 // serialise on one atomic word: block b takes a ticket on shard b % 8 (the blocks of one XCD), the
 // last arrival of a shard takes a ticket on the top word, the last of those is the grid's last.
-// Each last arrival resets its word for the next launch.  One ticket set per kernel kind: launches
-// of a kind run one at a time on the caller's stream.  (1-D grids.)
-__device__ unsigned g_adam_ticket[2][9];
+// Each last arrival resets its word for the next launch.  The words belong to the caller (one set
+// per optimiser and kernel kind, fr_adam_step_dev's d_ticket): launches that share a set must run
+// one at a time, which launches of one optimiser do on its stream; two optimisers stepping on two
+// streams (or concurrent branches of a captured graph) use their own sets.  (1-D grids.)
 
 __device__ __forceinline__ bool last_block(unsigned* ticket) {
   __shared__ bool last;
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
       for (int64_t k = base + threadIdx.x; k < end; k += blockDim.x) adam_elem(P[k], G[k], M[k], V[k], h);
     }
   }
-  if (a.step[0] && last_block(g_adam_ticket[ROWS ? 1 : 0]) && threadIdx.x < a.n && a.step[threadIdx.x])
+  if (a.step[0] && last_block(a.ticket) && threadIdx.x < a.n && a.step[threadIdx.x])
     a.step[threadIdx.x][0] += 1;
 }
 
@@ -694,8 +696,11 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
                      float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                      int n_tensors, double lr, const double* d_lr, double beta1, double beta2,
                      double eps, double weight_decay, int64_t step, const int32_t* d_skip,
-                     void* stream, const int32_t* const* rmaps = nullptr, const int32_t* row_dims = nullptr) {
+                     void* stream, const int32_t* const* rmaps = nullptr, const int32_t* row_dims = nullptr,
+                     uint32_t* d_ticket = nullptr) {
   FR_REQUIRE(n_tensors >= 0, "n_tensors < 0");
+  FR_REQUIRE(!d_steps || (d_ticket && fr::aligned16(d_ticket)),
+             "device-scalar mode needs the caller's 16-byte aligned ticket words (FR_ADAM_TICKET_WORDS)");
   if (n_tensors == 0) return FR_OK;
   FR_REQUIRE(params && grads && exp_avg && exp_avg_sq && numel, "null host array");
   FR_REQUIRE(d_steps || step >= 1, "step must be >= 1 (1-based, after increment)");
@@ -724,6 +729,7 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
     while (t < n_tensors) {
       AdamArgs a{};
       a.n = 0;
+      a.ticket = d_ticket ? reinterpret_cast<unsigned*>(d_ticket) + 16 * rows_pass : nullptr;
       int32_t blocks = 0;
       for (; t < n_tensors && a.n < kMaxTensors; ++t) {
         const bool is_rows = rmaps && rmaps[t];
@@ -784,20 +790,21 @@ extern "C" int fr_adam_step(float* const* params, const float* const* grads, flo
 extern "C" int fr_adam_step_dev(float* const* params, const float* const* grads, float* const* exp_avg,
                                 float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                                 int n_tensors, const double* d_lr, double lr, double beta1, double beta2,
-                                double eps, double weight_decay, const int32_t* d_skip, void* stream) {
+                                double eps, double weight_decay, const int32_t* d_skip, uint32_t* d_ticket,
+                                void* stream) {
   FR_REQUIRE(d_steps, "d_steps (device step counters) required");
   return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1,
-                   beta2, eps, weight_decay, 0, d_skip, stream);
+                   beta2, eps, weight_decay, 0, d_skip, stream, nullptr, nullptr, d_ticket);
 }
 
 extern "C" int fr_adam_step_rows(float* const* params, const float* const* grads, float* const* exp_avg,
                                  float* const* exp_avg_sq, int64_t* const* d_steps, const int64_t* numel,
                                  const int32_t* const* d_rmaps, const int32_t* row_dims, int n_tensors,
                                  const double* d_lr, double lr, double beta1, double beta2, double eps,
-                                 double weight_decay, const int32_t* d_skip, void* stream) {
+                                 double weight_decay, const int32_t* d_skip, uint32_t* d_ticket, void* stream) {
   FR_REQUIRE(d_steps && d_rmaps && row_dims, "d_steps, d_rmaps and row_dims required");
   return adam_impl(params, grads, exp_avg, exp_avg_sq, d_steps, numel, n_tensors, lr, d_lr, beta1, beta2, eps,
-                   weight_decay, 0, d_skip, stream, d_rmaps, row_dims);
+                   weight_decay, 0, d_skip, stream, d_rmaps, row_dims, d_ticket);
 }
 
 extern "C" int fr_adam_step_bf16(uint16_t* d_param, float* d_master, const uint16_t* d_grad, float* d_exp_avg,

@@ -40,6 +40,7 @@ struct FeedArgs {
   int64_t* out_nums;      // [2B]
   float* out_health;      // [2B, H] or null
   float* out_kpm;         // [2B, L] additive key mask (-inf at padding, 0 elsewhere) or null
+  int32_t* err;           // sticky flag: set to 1 when an item id was out of range (or null)
 };
 
 __global__ __launch_bounds__(256) void feed_batch_kernel(FeedArgs a, int64_t B) {
@@ -49,25 +50,34 @@ __global__ __launch_bounds__(256) void feed_batch_kernel(FeedArgs a, int64_t B) 
     const int c = (int)(t - j * a.W);
     const bool is_pos = j < B;
     const int64_t i = is_pos ? j : j - B;
-    int64_t item;
+    int64_t item, user = 0;
     if (a.perm) {
       const int64_t pos = a.cursor[0] * B + i;
       if (is_pos) {
         const int64_t k = a.perm[pos];
         item = a.items[k];
-        if (c == 0) {
-          a.u[i] = a.users[k];
-          a.p[i] = item;
-        }
+        user = a.users[k];
       } else {
         item = a.negs[pos];
-        if (c == 0) a.n[i] = item;
       }
     } else {
       item = is_pos ? a.p[i] : a.n[i];
     }
-    // ids come from the sampler (valid by construction); a corrupt id must not fault the GPU
-    if (item < 0 || item >= a.n_items) item = 0;
+    // ids come from the sampler (valid by construction); a corrupt id must not fault the GPU: it is
+    // replaced by item 0 in EVERY output (p / n included, so they agree with pn and the features)
+    // and reported through the sticky flag the trainer reads at epoch end
+    if (item < 0 || item >= a.n_items) {
+      item = 0;
+      if (c == 0 && a.err) atomicOr(a.err, 1);
+    }
+    if (a.perm && c == 0) {
+      if (is_pos) {
+        a.u[i] = user;
+        a.p[i] = item;
+      } else {
+        a.n[i] = item;
+      }
+    }
     if (c == 0) {
       a.pn[j] = item;
       a.out_nums[j] = a.nums[item];
@@ -87,7 +97,8 @@ extern "C" int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, cons
                              const int64_t* d_negs, const int64_t* d_cursor, int64_t B, int64_t* d_u, int64_t* d_p,
                              int64_t* d_n, const int64_t* d_codes, int L, const int64_t* d_nums, const float* d_health,
                              int H, int64_t n_items, int64_t pad, int64_t* d_pn, int64_t* d_out_codes,
-                             int64_t* d_out_nums, float* d_out_health, float* d_out_kpm, void* stream) {
+                             int64_t* d_out_nums, float* d_out_health, float* d_out_kpm, int32_t* d_err,
+                             void* stream) {
   FR_REQUIRE(B >= 1 && L >= 1 && L <= 1024 && H >= 0 && H <= 1024 && n_items >= 1, "bad sizes");
   FR_REQUIRE(d_p && d_n && d_codes && d_nums && d_pn && d_out_codes && d_out_nums, "null argument");
   FR_REQUIRE(!d_perm || (d_users && d_items && d_negs && d_cursor && d_u), "feed mode needs perm/users/items/negs/"
@@ -95,7 +106,7 @@ extern "C" int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, cons
   FR_REQUIRE((d_health == nullptr) == (d_out_health == nullptr) && (H == 0) == (d_health == nullptr),
              "health table and output go together (H > 0)");
   FeedArgs a{d_perm, d_users, d_items, d_negs, d_cursor, d_u, d_p, d_n, d_codes, d_nums, d_health, n_items, L, H,
-             L > H ? L : (H > 0 ? H : 1), pad, d_pn, d_out_codes, d_out_nums, d_out_health, d_out_kpm};
+             L > H ? L : (H > 0 ? H : 1), pad, d_pn, d_out_codes, d_out_nums, d_out_health, d_out_kpm, d_err};
   const int64_t total = 2 * B * a.W;
   const int64_t blocks = std::min<int64_t>(fr::ceil_div(total, (int64_t)256), (int64_t)fr::kNumCU * 8);
   hipLaunchKernelGGL(feed_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),

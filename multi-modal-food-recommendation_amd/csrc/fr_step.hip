@@ -23,7 +23,8 @@ struct Parts {
   int nc;
 };
 
-__global__ void step_book_kernel(Parts parts, double* __restrict__ acc, int accumulate, int32_t* __restrict__ nan_flag) {
+__global__ void step_book_kernel(Parts parts, double* __restrict__ acc, int accumulate, int32_t* __restrict__ nan_flag,
+                                 float* __restrict__ loss_out) {
   if (threadIdx.x != 0) return;
   for (int i = 0; i < parts.nc; ++i) parts.ctr[i][0] += 1;
   float s = 0.f;  // sum(losses) in fp32, left to right, as Python's sum over fp32 tensors
@@ -33,12 +34,13 @@ __global__ void step_book_kernel(Parts parts, double* __restrict__ acc, int accu
     s = i == 0 ? v : s + v;
   }
   if (s != s) nan_flag[0] |= 1;
+  if (loss_out) loss_out[0] = s;  // the step's loss value (what the reference's train step returns)
 }
 
 }  // namespace
 
 extern "C" int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan,
-                            int64_t* const* d_counters, int n_counters, void* stream) {
+                            int64_t* const* d_counters, int n_counters, float* d_loss_out, void* stream) {
   FR_REQUIRE(n >= 1 && n <= kMaxParts, "1..8 loss parts");
   FR_REQUIRE(n_counters >= 0 && n_counters <= kMaxCounters, "0..8 counters");
   FR_REQUIRE(d_parts && d_acc && d_nan && (n_counters == 0 || d_counters), "null argument");
@@ -54,7 +56,7 @@ extern "C" int fr_step_book(const float* const* d_parts, int n, double* d_acc, i
   }
   p.nc = n_counters;
   hipLaunchKernelGGL(step_book_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p, d_acc,
-                     accumulate, d_nan);
+                     accumulate, d_nan, d_loss_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -1,9 +1,10 @@
-"""GPU check of HealthRec data parallelism with the row-exchanged feature-table gradients
-(ops._EmbeddingExchanged + engine.dist.GradAllReduce), world_size ranks on ONE GPU (gloo over
-device tensors).  Launch:
+"""Rank worker of tests/test_multirank_gpu.py: HealthRec data parallelism with the row-exchanged
+feature-table gradients (ops._EmbeddingExchanged + engine.dist.GradAllReduce) and the graphed
+data-parallel step (engine.dist.GraphedDPStep), world_size ranks on ONE GPU (gloo over device
+tensors).  Launched by the test as
 
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-      --master-port 29512 tools/dp_check.py
+      --master-port P tests/mp/dp_worker.py
 
 Each rank trains its own batch.  Reference: the same step with every gradient all-reduced densely
 and averaged.  Checks: exchanged image/text table gradients equal the dense mean (|err| <= 1e-6 *
@@ -86,6 +87,9 @@ def main():
     tg, te = Trainer(cfg, mg), Trainer(cfg, me)
     tg.grad_hook, te.grad_hook = GradAllReduce(mg, world), GradAllReduce(me, world)
     graphed = tg.graphed_step(256, warmup=2)
+    from FoodRec.common.trainer import GraphedDPStep
+    if not isinstance(graphed, GraphedDPStep):
+        fails.append(f"graphed_step returned {type(graphed).__name__}, not GraphedDPStep")
     sg, se = tg.new_step_state(), te.new_step_state()
     def cycle():
         while True:

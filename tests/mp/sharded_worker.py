@@ -1,8 +1,12 @@
-"""GPU check of the row-sharded config-4 step (engine/sharded.py) with world_size ranks on ONE GPU
-(gloo over device tensors; the 8-GPU RCCL run is the driver's).  Launch:
+"""Rank worker of tests/test_multirank_gpu.py: the row-sharded config-4 step (engine/sharded.py) with
+world_size ranks on ONE GPU (gloo over device tensors; RCCL refuses two ranks on one device, the
+8-GPU RCCL run is the driver's).  Launched by the test as
 
-  python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-      --master-port 29511 tools/sharded_check.py
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node {2,4} --master-addr 127.0.0.1 \
+      --master-port P tests/mp/sharded_worker.py
+
+The step must run the rows form (_ShardedPropagateRows: item-flag all-reduce, the |S| layer-1 rows,
+the 2B batch item rows, the item-row blocks of the last backward layer) -- counted below.
 
 Every rank compares, on a 20k-user graph:
   * the sharded step (P ranks) with the same step unsharded (P=1, no collectives) and with the
@@ -26,7 +30,16 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import sharded
     from FoodRec.engine.sharded import ShardedGraph, ShardedLightGCN
+    rows_calls = [0]
+    _apply = sharded._ShardedPropagateRows.apply
+
+    def counted(*a):
+        rows_calls[0] += 1
+        return _apply(*a)
+
+    sharded._ShardedPropagateRows.apply = staticmethod(counted)
     from FoodRec.models.lightgcn_id import LightGCN_ID
     from FoodRec.utils.configurator import Config
     from FoodRec.utils.interaction_graph import InteractionGraph, synth_bipartite
@@ -78,6 +91,10 @@ def main():
     dist.all_gather(items, mP.ego_i.detach().contiguous())
     if not all(torch.equal(items[0], x) for x in items):
         fails.append("replicated item tables diverged across ranks after 3 Adam steps")
+    if rows_calls[0] < 4:  # 1 loss + 3 training steps of the sharded model
+        fails.append(f"rows form ran {rows_calls[0]} times (expected >= 4)")
+    if len(gP.iu_blocks) < 2:
+        fails.append("transpose slice not cut into item-row blocks")
     torch.cuda.synchronize()
     print(f"[rank {rank}/{world}] users [{gP.lo},{gP.hi}) nnz {gP.local_nnz}: "
           + ("PASS" if not fails else "FAIL " + "; ".join(fails)), flush=True)

@@ -94,3 +94,51 @@ def test_lightgcn_id_state_dict_uses_reference_keys(cuda):
     m2 = LightGCN_ID(_config(cuda), g)
     m2.load_state_dict(sd)
     assert torch.equal(m2.ego, m.ego)
+
+
+def test_lightgcn_id_steps_eagerly_and_captures_on_the_full_path(cuda):
+    """The row-list propagation reads sizes back to the host, so the Trainer steps LightGCN_ID
+    eagerly (use_graph False), and an explicit capture (graphed_step) falls back to the full
+    propagation inside the graph: its steps match the eager rows-form steps (losses rel 1e-5,
+    parameters 1e-5 * max after 4 Adam steps; float-atomic scatter order differs)."""
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.models.lightgcn_id import LightGCN_ID
+    g = _graph(cuda)
+    torch.manual_seed(0)
+    me = LightGCN_ID(_config(cuda), g)
+    mg = LightGCN_ID(_config(cuda), g)
+    mg.load_state_dict(me.state_dict())
+    te, tg = Trainer(_config(cuda), me), Trainer(_config(cuda), mg)
+    assert not te.use_graph
+    graphed = tg.graphed_step(512, warmup=1)
+    se, sg = te.new_step_state(), graphed.state
+    for k in range(4):
+        u, p, n = g.triples(512)
+        before = None if sg["acc"] is None else sg["acc"].clone()
+        graphed(u, p, n, k, sg)
+        ae = None if se["acc"] is None else se["acc"].clone()
+        te.train_step({"u_id": u, "pos_i_id": p, "neg_i_id": n}, k, se)
+        dg = sg["acc"] - (0 if before is None else before)
+        de = se["acc"] - (0 if ae is None else ae)
+        torch.testing.assert_close(dg, de, rtol=1e-5, atol=1e-7)
+    assert graphed.graph is not None
+    assert (mg.ego - me.ego).abs().max() <= 1e-5 * me.ego.abs().max()
+
+
+def test_fused_step_returns_its_loss(cuda):
+    """the fused-bookkeeping train_step returns the step's loss (a device fp32 scalar =
+    the sum of the loss parts, as the reference's step returns loss), not None."""
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.models.lightgcn_id import LightGCN_ID
+    g = _graph(cuda)
+    torch.manual_seed(0)
+    m = LightGCN_ID(_config(cuda), g)
+    tr = Trainer(_config(cuda), m)
+    st = tr.new_step_state()
+    u, p, n = g.triples(512)
+    with torch.no_grad():
+        mf, reg = m.calculate_loss({"u_id": u, "pos_i_id": p, "neg_i_id": n})
+    loss = tr.train_step({"u_id": u, "pos_i_id": p, "neg_i_id": n}, 0, st)
+    assert torch.is_tensor(loss) and loss.is_cuda and loss.dtype == torch.float32
+    assert float(loss) == pytest.approx(float(mf.reshape(-1)[0] + reg.reshape(-1)[0]), rel=1e-6)
+    assert float(loss) == pytest.approx(float(st["acc"].sum()), rel=1e-6)

@@ -111,3 +111,48 @@ def test_row_exchange_gloo_world2_shared_ids(tmp_path):
             assert pt == pi + 4 * 64  # adjacent column blocks of one buffer
             torch.testing.assert_close(dyi, torch.cat([res[q][step]["dYi"] for q in range(world)]) / world)
             torch.testing.assert_close(dyt, torch.cat([res[q][step]["dYt"] for q in range(world)]) / world)
+
+
+def _distinct_ids_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from FoodRec.engine.dist import RowExchange, init_from_env
+    init_from_env(backend="gloo")
+    a, b = torch.zeros(40, 32), torch.zeros(40, 16)
+    Wa, Wb = torch.randn(64, 32), torch.randn(64, 16)
+    xg = RowExchange(dist.group.WORLD, world)
+    xg.sink = _Sink()
+    out = []
+    for step in range(3):
+        g = torch.Generator().manual_seed(10 * step + rank)
+        # two tables with DIFFERENT ids of the same shape, each ids tensor a temporary freed right
+        # after its stash (the pattern under which a recycled Python id() grouped them as shared);
+        # at step 2 they share one ids tensor (the packed layout must change back)
+        ia = torch.randint(0, 40, (6,), generator=g)
+        ib = ia if step == 2 else torch.randint(0, 40, (6,), generator=g)
+        dYa, dYb = torch.randn(6, 64, generator=g), torch.randn(6, 64, generator=g)
+        xg.stash_factored(a, None, ia.reshape(-1).to(torch.int64) + 0, dYa, Wa)
+        xg.stash_factored(b, None, (ib.reshape(-1).to(torch.int64) + 0) if step != 2 else ia, dYb, Wb)
+        xg.exchange()
+        xg.sink.calls.clear()
+        xg.apply()
+        calls = {c[0] is a: c[1].clone() for c in xg.sink.calls}
+        out.append({"ia": ia, "ib": ib, "got_a": calls[True], "got_b": calls[False]})
+    torch.save(out, os.path.join(out_dir, f"distinct_r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_row_exchange_distinct_ids_same_shape(tmp_path):
+    """two tables stashed in one backward with different ids of equal shape are never
+    grouped as sharing ids; each gets every rank's own ids back."""
+    world = 2
+    mp.start_processes(_distinct_ids_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = [torch.load(tmp_path / f"distinct_r{r}.pt", weights_only=False) for r in range(world)]
+    for step in range(3):
+        ia = torch.cat([res[r][step]["ia"] for r in range(world)])
+        ib = torch.cat([res[r][step]["ib"] for r in range(world)])
+        for r in range(world):
+            assert torch.equal(res[r][step]["got_a"].reshape(-1), ia)
+            assert torch.equal(res[r][step]["got_b"].reshape(-1), ib)

@@ -375,6 +375,45 @@ def test_fused_adam_matches_torch(cuda):
     assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
 
 
+def test_fused_adam_two_optimisers_two_streams(cuda):
+    """Two FusedAdam instances stepping at the same time on two streams (many-block launches: the
+    device step counters are bumped by each launch's last workgroup through per-optimiser ticket
+    words): both step counters advance by one per step and both match torch.optim.Adam."""
+    from FoodRec.engine.optim import FusedAdam
+    g = torch.Generator().manual_seed(3)
+    shapes = [(4096, 64), (300_000,)]  # > 8 chunks per launch: many workgroups arrive
+    refs, devs, opts, orefs = [], [], [], []
+    for _ in range(2):
+        rp = [torch.randn(s, generator=g) for s in shapes]
+        dp = [p.clone().to(cuda).requires_grad_(True) for p in rp]
+        rp = [p.clone().requires_grad_(True) for p in rp]
+        refs.append(rp)
+        devs.append(dp)
+        opts.append(FusedAdam(dp, lr=1e-3))
+        orefs.append(torch.optim.Adam(rp, lr=1e-3, foreach=False))
+    streams = [torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)]
+    for step in range(5):
+        for k in range(2):
+            grads = [torch.randn(s, generator=g) for s in shapes]
+            for p, q, gr in zip(refs[k], devs[k], grads):
+                p.grad = gr.clone()
+                q.grad = gr.to(cuda)
+            orefs[k].step()
+        torch.cuda.synchronize()
+        for k in range(2):
+            streams[k].wait_stream(torch.cuda.current_stream(cuda))
+            with torch.cuda.stream(streams[k]):
+                opts[k].step()
+        torch.cuda.synchronize()
+    for k in range(2):
+        for p, q in zip(refs[k], devs[k]):
+            assert int(opts[k].state[q]["step"].item()) == 5
+            np.testing.assert_array_equal(opts[k].state[q]["exp_avg"].cpu().numpy(),
+                                          orefs[k].state[p]["exp_avg"].numpy())
+            a, b = q.detach().cpu().numpy(), p.detach().numpy()
+            assert np.all(np.abs(a - b) <= 4 * np.spacing(np.abs(b)) + 4 * np.spacing(np.float32(1e-3)))
+
+
 def test_adam_skip_flag(cuda):
     from FoodRec.engine.optim import FusedAdam
     p = torch.randn(100, device=cuda, requires_grad=True)

@@ -511,6 +511,36 @@ def test_feed_batch_one_launch_matches_gathers(cuda):
         np.testing.assert_array_equal(np.concatenate([b[k] for b in got]), g[f"ep0/{key}"])
 
 
+def test_feed_batch_bad_id_is_reported(cuda):
+    """fr_feed_batch replaces an out-of-range item id by item 0 in every output (in feed
+    mode p / n too, so they agree with pn and the features) and sets the sticky flag the trainer
+    reads at epoch end (BatchFeatures.check_ids raises)."""
+    from helpers import tiny_config, tiny_data
+    from FoodRec.engine.sampler import BatchFeatures, TripleSampler
+    cfg = tiny_config("CIKM_Model", False)
+    data = tiny_data(cfg)
+    B = 64
+    s = TripleSampler(data, B, cuda, replay_python_random=False)
+    feed = s.device_feed()
+    feats = BatchFeatures(data, cuda)
+    out = tuple(torch.zeros(B, dtype=torch.int64, device=cuda) for _ in range(3))
+    it = s.epoch(out=out, feed=feed)
+    next(it)
+    feed.negs[3] = feats.ingre_code.shape[0] + 7  # corrupt staged negative of batch 0, row 3
+    pre = feed.fill(*out, feats)
+    torch.cuda.synchronize()
+    assert int(out[2][3]) == 0 and int(pre["pn_i_id"][B + 3]) == 0
+    assert torch.equal(pre["pn_i_id"], torch.cat([out[1], out[2]]))
+    assert torch.equal(pre["pn_ingre_code"][B + 3], feats.ingre_code[0])
+    with pytest.raises(RuntimeError, match="outside the item table"):
+        feats.check_ids()
+    feats.check_ids()  # the flag was cleared by the report
+    lb = feats.batch(out[0].clone(), out[1].clone(), out[2].clone())  # a clean batch: no report
+    torch.cuda.synchronize()
+    assert torch.equal(lb["pn_i_id"], pre["pn_i_id"])
+    feats.check_ids()
+
+
 @pytest.mark.parametrize("n", [1024 * 20, 1000])
 @pytest.mark.parametrize("hot", [None, 19987, 5])
 def test_embedding_bwd_atomic_matches_sorted(cuda, hot, n):

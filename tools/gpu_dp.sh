@@ -8,5 +8,5 @@ TAG=${1:-dp}
 mkdir -p $OUT
 cd $R
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29531 tools/dp_check.py > $OUT/dp_check_$TAG.log 2>&1 || { echo dp_check failed; tail -30 $OUT/dp_check_$TAG.log; exit 1; }
+  --master-port 29531 tests/mp/dp_worker.py > $OUT/dp_check_$TAG.log 2>&1 || { echo dp_check failed; tail -30 $OUT/dp_check_$TAG.log; exit 1; }
 grep -E "PASS|FAIL" $OUT/dp_check_$TAG.log | head -5
