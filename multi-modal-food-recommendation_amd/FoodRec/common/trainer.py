@@ -446,8 +446,12 @@ class Trainer(AbstractTrainer):
     # ------------------------------------------------------------------------------ training
     def _features(self):
         if self._feats is None:
-            self._feats = BatchFeatures(self.model.dataset if hasattr(self.model, "dataset") else self._dataset,
-                                        self.device, ssl=bool(self.config["SCHGN_ssl"]))
+            ds = self.model.dataset if hasattr(self.model, "dataset") else getattr(self, "_dataset", None)
+            if ds is None or not hasattr(ds, "ingredientCodeDict"):
+                from FoodRec.engine.sampler import IdFeatures  # ids-only graph (InteractionGraph)
+                self._feats = IdFeatures(self.device)
+            else:
+                self._feats = BatchFeatures(ds, self.device, ssl=bool(self.config["SCHGN_ssl"]))
         return self._feats
 
     def _opt_step(self, skip_flag):

@@ -199,6 +199,22 @@ def ssl_sequences(codes: np.ndarray, nums: np.ndarray, n_ingredients: int, rnd=r
     return masked, codes.copy(), neg
 
 
+class IdFeatures:
+    """Batch assembly for an interaction graph without item side tables (LightGCN_ID on an
+    InteractionGraph): the batch is the (u, pos, neg) ids alone."""
+
+    ssl = False
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+
+    def native_ok(self) -> bool:
+        return False
+
+    def batch(self, u, p, n, pre=None):
+        return {"u_id": u, "pos_i_id": p, "neg_i_id": n}
+
+
 class BatchFeatures:
     """Device-resident per-item side tables used to assemble the reference's batch dict
     (dataloader.py:50-115): ingredient codes/counts, health multi-hot, image rows, calorie levels;
