@@ -718,6 +718,20 @@ int fr_feed_batch(const int64_t* d_perm, const int64_t* d_users, const int64_t* 
 int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumulate, int32_t* d_nan,
                  int64_t* const* d_counters, int n_counters, float* d_loss_out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * fr_rank_metrics: the per-user ranking of Trainer._valid_by_user_epoch (common/trainer.py:231-282;
+ * metrics_by_user / get_auc_fast :49-69) over EvalByUserDataloader's candidate lists
+ * (utils/dataloader.py:228-302).  User u's candidate scores are d_scores[d_offsets[u] ..
+ * d_offsets[u+1]), its first d_npos[u] candidates the positives.  Outputs per user:
+ *   d_hits[u]  bit t (t < k) = rank t of np.argsort(scores)[::-1] is a positive;
+ *   d_auc[u]   sum over positives p of #{negatives j: score[j] < score[p]} (strict);
+ *   d_flags[u] 0 = exact, 1 = the k+1 largest scores tie or a score is NaN (numpy's tie order
+ *              decides: rank on the host), 2 = more than fr_rank_capacity() candidates.
+ * k <= 31.  One launch, one wave per user, no host sync. */
+int fr_rank_metrics(const float* d_scores, const int64_t* d_offsets, const int32_t* d_npos, int64_t n_users,
+                    int k, uint32_t* d_hits, int64_t* d_auc, uint8_t* d_flags, void* stream);
+int fr_rank_capacity(void);
+
 /* fr_reg_combine_fwd / _bwd: HealthRec's weighted EmbLoss from its two fused pieces,
  * out = w * (a[0] + (b[0] + ... + b[nb-1]) / B)  (cikm_model.py:267-279); backward da = g w,
  * db[i] = g w / B.  One launch each. */

@@ -61,6 +61,48 @@ def metrics_by_user(doc_list, rel_list):
     return hits / len(rel_list), dcg / idcg
 
 
+# 1 / log2(i + 2): the DCG discount of rank i, the same Python float expression as metrics_by_user
+_DISCOUNT = [1 / (math.log(i + 2) / math.log(2)) for i in range(31)]
+
+
+def rank_user_host(pr, npo, neg_num, ks=(10, 20)):
+    """One user's (recall, ndcg, auc) per k by the reference's own code path (trainer.py:231-282):
+    numpy's argsort order, metrics_by_user, get_auc_fast."""
+    gt = range(npo)
+    order = np.argsort(pr)[::-1]
+    auc = get_auc_fast(gt, pr, neg_num)
+    out = np.zeros((3, len(ks)))
+    for j, topk in enumerate(ks):
+        r, nd = metrics_by_user(order[:topk], gt)
+        out[0, j], out[1, j], out[2, j] = r, nd, auc
+    return out
+
+
+def metrics_from_hits(hits, lens, npos, auc_cnt, neg_num, ks=(10, 20)):
+    """Per-user [recall, ndcg, auc] x ks from the device ranking (fr_rank_metrics: bit t of hits[u]
+    = rank t is a positive; auc_cnt[u] = the strict positive-over-negative count), evaluated with
+    metrics_by_user / get_auc_fast's float64 operations in their order (DCG summed over ranks in
+    increasing order, the other ranks adding 0.0), so every value equals the host loop's bit for bit."""
+    U = len(lens)
+    res = np.zeros((U, 3, len(ks)))
+    hits = np.asarray(hits).astype(np.int64)
+    lens = np.asarray(lens, np.int64)
+    npos = np.asarray(npos, np.int64)
+    auc = np.asarray(auc_cnt, np.int64) / (npos * int(neg_num))
+    for j, k in enumerate(ks):
+        dcg, hitn, idcg = np.zeros(U), np.zeros(U), np.zeros(U)
+        lim = np.minimum(np.minimum(lens, k), npos)  # min(len(order[:k]), len(gt))
+        for i in range(k):
+            b = ((hits >> i) & 1).astype(bool)
+            dcg = dcg + np.where(b, _DISCOUNT[i], 0.0)
+            hitn = hitn + b
+            idcg = idcg + np.where(i < lim, _DISCOUNT[i], 0.0)
+        res[:, 0, j] = hitn / npos
+        res[:, 1, j] = dcg / idcg
+        res[:, 2, j] = auc
+    return res
+
+
 def book_step(parts, acc, nan_flag, accumulate=True):
     """fr_step_book over the loss parts (device float scalars): acc (+)= parts, nan |= isnan(sum),
     and the step's deferred device counters (ops.defer_increment) advanced in the same launch.
@@ -605,22 +647,27 @@ class Trainer(AbstractTrainer):
     EVAL_CHUNK_ROWS = 1 << 18
 
     @torch.no_grad()
-    def _score(self, users, items):
+    def _score(self, users, items, on_device=False):
         """Scores of the (user, candidate) rows.  The fast graph path gathers from one forward; the
         per-row path (inference_by_user) runs over chunks of ``eval_chunk_rows`` rows (a model
-        attribute, else EVAL_CHUNK_ROWS), each an EvalBatch with the reference's side inputs."""
+        attribute, else EVAL_CHUNK_ROWS), each an EvalBatch with the reference's side inputs.
+        ``on_device``: return the fp32 scores as a device tensor (the device ranking's input)."""
         dev = torch.device(self.device)
+        fin = (lambda t: t.float().reshape(-1).contiguous()) if on_device else (lambda t: t.float().reshape(-1).cpu())
         if self.config["graph_inference_fast"]:
             batch = {"user_input": torch.from_numpy(users).to(dev), "item_input": torch.from_numpy(items).to(dev)}
             out = self.model.forward()
-            return self.model.inference_fast(batch, out[0], out[1]).float().cpu().numpy()
+            sc = fin(self.model.inference_fast(batch, out[0], out[1]))
+            return sc if on_device else sc.numpy()
         step = int(getattr(self.model, "eval_chunk_rows", None) or self.EVAL_CHUNK_ROWS)
         feats = self._features()
         parts = []
         for s in range(0, len(users), step):
             batch = EvalBatch(feats, torch.from_numpy(users[s:s + step]).to(dev),
                               torch.from_numpy(items[s:s + step]).to(dev))
-            parts.append(self.model.inference_by_user(batch).float().reshape(-1).cpu())
+            parts.append(fin(self.model.inference_by_user(batch)))
+        if on_device:
+            return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.float32, device=dev)
         return torch.cat(parts).numpy() if parts else np.zeros(0, np.float32)
 
     def flush_optimizer(self):
@@ -632,23 +679,38 @@ class Trainer(AbstractTrainer):
     def _valid_by_user_epoch(self, valid_data=None, is_test=False):
         self.flush_optimizer()
         users, items, lens, npos = self._candidates(is_test)
-        preds = self._score(users, items)
         neg_num = self.config["neg_sample_num"]
-        res = np.zeros((len(lens), 3, 2))
-        off = 0
-        for k, (ln, npo) in enumerate(zip(lens.tolist(), npos.tolist())):
-            pr = preds[off:off + ln].copy()
-            off += ln
-            gt = range(npo)
-            order = np.argsort(pr)[::-1]
-            auc = get_auc_fast(gt, pr, neg_num)
-            for j, topk in enumerate((10, 20)):
-                r, nd = metrics_by_user(order[:topk], gt)
-                res[k, 0, j], res[k, 1, j], res[k, 2, j] = r, nd, auc
+        if self._on_gpu():
+            res = self._rank_on_device(users, items, lens, npos, neg_num)
+        else:
+            preds = self._score(users, items)
+            res = np.zeros((len(lens), 3, 2))
+            off = 0
+            for k, (ln, npo) in enumerate(zip(lens.tolist(), npos.tolist())):
+                res[k] = rank_user_host(preds[off:off + ln].copy(), npo, neg_num)
+                off += ln
         recalls, ndcgs, aucs = res.mean(axis=0).tolist()
         metrics = {"AUC": aucs[0], "Recall@10": recalls[0], "Recall@20": recalls[1],
                    "NDCG@10": ndcgs[0], "NDCG@20": ndcgs[1]}
         return metrics["NDCG@20"], metrics
+
+    def _rank_on_device(self, users, items, lens, npos, neg_num):
+        """Scores stay on the device; fr_rank_metrics ranks every user (top-20 hit masks + the AUC
+        counts) and the host turns them into the reference's float64 metrics (metrics_from_hits).
+        Users whose top-21 scores tie (numpy's argsort tie order decides) are ranked by the host's
+        numpy path on their own scores."""
+        sc = self._score(users, items, on_device=True)
+        hits, aucc, flags = ops.rank_metrics(sc, lens, npos, 20)
+        res = metrics_from_hits(hits, lens, npos, aucc, neg_num)
+        redo = np.nonzero(flags)[0]
+        if len(redo):
+            off = np.zeros(len(lens) + 1, np.int64)
+            np.cumsum(lens, out=off[1:])
+            host = sc.cpu().numpy()
+            for k in redo.tolist():
+                res[k] = rank_user_host(host[off[k]:off[k + 1]].copy(), int(npos[k]), neg_num)
+        self.last_eval_host_users = int(len(redo))
+        return res
 
     # ------------------------------------------------------------------------------ fit
     def _generate_train_loss_output(self, epoch_idx, s_time, e_time, losses):

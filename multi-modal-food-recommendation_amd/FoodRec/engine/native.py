@@ -76,6 +76,9 @@ _SIGS = {
                                 c_void_p, c_int64, c_void_p]),
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "fr_rank_metrics": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p]),
+    "fr_rank_capacity": (c_int, []),
     "fr_step_book": (c_int, [POINTER(c_void_p), c_int, c_void_p, c_int, c_void_p, POINTER(c_void_p), c_int,
                              c_void_p, c_void_p]),
     "fr_embedding_bwd_atomic": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_int64,

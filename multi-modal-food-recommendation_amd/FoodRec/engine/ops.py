@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import native, profiling
@@ -1849,3 +1850,28 @@ def full_sort_topk(user_rows: torch.Tensor, item_table: torch.Tensor, k: int, us
             scores.data_ptr(), items.data_ptr(), native.ptr(hits), ws.data_ptr(), ws.numel(),
             native.stream_of(U)), "fr_topk_scores")
     return scores, items, hits
+
+
+# ----------------------------------------------------------------------------- evaluation ranking
+def rank_metrics(scores: torch.Tensor, lens, npos, k: int = 20):
+    """fr_rank_metrics over the per-user candidate scores (device fp32, users' lists back to back,
+    positives first): numpy (hits uint32, auc counts int64, flags uint8) per user.  Replaces the
+    per-user argsort / metrics_by_user / get_auc_fast loop (trainer.py:231-282, 49-69)."""
+    native.require_device(scores)
+    dev = scores.device
+    lens = np.asarray(lens, np.int64)
+    U = len(lens)
+    off = torch.zeros(U + 1, dtype=torch.int64)
+    torch.cumsum(torch.from_numpy(lens), 0, out=off[1:])
+    if int(off[-1]) != scores.numel():
+        raise ValueError("candidate lengths do not add up to the score count")
+    off_d = off.to(dev)
+    npos_d = torch.from_numpy(np.asarray(npos, np.int32)).to(dev)
+    hits = torch.empty(U, dtype=torch.int32, device=dev)
+    auc = torch.empty(U, dtype=torch.int64, device=dev)
+    flags = torch.empty(U, dtype=torch.uint8, device=dev)
+    sc = scores.float().contiguous()
+    native.check(native.lib().fr_rank_metrics(sc.data_ptr(), off_d.data_ptr(), npos_d.data_ptr(), U, int(k),
+                                              hits.data_ptr(), auc.data_ptr(), flags.data_ptr(),
+                                              native.stream_of(sc)), "fr_rank_metrics")
+    return hits.cpu().numpy().view(np.uint32), auc.cpu().numpy(), flags.cpu().numpy()

@@ -93,6 +93,15 @@ __device__ unsigned long long g_prof[2][32];
     if (prof && threadIdx.x == 0) g_prof[kind][n] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// the same stamp from inside a device function (prof: the kernel's flag, workgroup 0; thread 0)
+__device__ __forceinline__ void fr_mark(bool prof, int kind, int n) {
+  if (prof && threadIdx.x == 0) g_prof[kind][n] = __builtin_amdgcn_s_memtime();
+}
+
+// this thread's wave index as a scalar: the compiler cannot prove threadIdx.x >> 6 wave-uniform, and
+// branches on it (job tables) must be scalar branches, not exec-masked ones
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -133,16 +142,6 @@ __device__ __forceinline__ bool keep(uint32_t ks, uint32_t idx, uint32_t thr) {
   if (thr == 0u) return true;
   return half_keep(pair_hash(ks, idx >> 1), idx & 1u, thr);
 }
-
-// attention site: element base + j of a score row (base = task * L); for even L the row starts on
-// a pair boundary, so j and j + 1 (j even) share a hash the compiler computes once per unrolled pair
-template <int L>
-__device__ __forceinline__ bool keep_att_l(uint32_t ks, uint32_t base, int j, uint32_t thr) {
-  if (thr == 0u) return true;
-  if constexpr (L % 2 == 0) return half_keep(pair_hash(ks, (base >> 1) + (j >> 1)), j & 1, thr);
-  return keep(ks, base + j, thr);
-}
-#define keep_att(ks, base, j, thr) keep_att_l<L>(ks, base, j, thr)
 
 __device__ __forceinline__ uint32_t pair_swap_u(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
@@ -209,54 +208,6 @@ __device__ __forceinline__ int64_t dact_frag(int wg, int sg, int c, int r, int l
 
 // the partner lane's value (lanes 2k <-> 2k+1, DPP quad_perm [1,0,3,2])
 __device__ __forceinline__ float pair_swap(float v) { return dpp_mov<0xB1>(v); }
-
-// 16-dimension head slices as 8 packed pairs: dot products and axpys on v_pk_fma_f32 (two lanes of
-// arithmetic per instruction); a float4 LDS load lands in two aligned register pairs
-typedef f32x2 v16[8];
-
-__device__ __forceinline__ float dot16(const v16& q, const float* r) {
-  f32x2 d = {0.f, 0.f};
-#pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) {
-    const float4 v = lds4(r + 4 * e4);
-    d = __builtin_elementwise_fma(q[2 * e4], f32x2{v.x, v.y}, d);
-    d = __builtin_elementwise_fma(q[2 * e4 + 1], f32x2{v.z, v.w}, d);
-  }
-  return d.x + d.y;
-}
-
-__device__ __forceinline__ void axpy16(float s, const float* r, v16& c) {
-  const f32x2 s2 = {s, s};
-#pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) {
-    const float4 v = lds4(r + 4 * e4);
-    c[2 * e4] = __builtin_elementwise_fma(s2, f32x2{v.x, v.y}, c[2 * e4]);
-    c[2 * e4 + 1] = __builtin_elementwise_fma(s2, f32x2{v.z, v.w}, c[2 * e4 + 1]);
-  }
-}
-
-__device__ __forceinline__ void load16(const float* r, v16& v) {
-#pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) {
-    const float4 x = lds4(r + 4 * e4);
-    v[2 * e4] = f32x2{x.x, x.y};
-    v[2 * e4 + 1] = f32x2{x.z, x.w};
-  }
-}
-
-__device__ __forceinline__ void zero16(v16& v) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = f32x2{0.f, 0.f};
-}
-
-__device__ __forceinline__ float4 quad16(const v16& v, int e4) {
-  return make_float4(v[2 * e4].x, v[2 * e4].y, v[2 * e4 + 1].x, v[2 * e4 + 1].y);
-}
-
-__device__ __forceinline__ void store16(float* r, const v16& v) {
-#pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) *reinterpret_cast<float4*>(r + 4 * e4) = quad16(v, e4);
-}
 
 // acc[r][c] (+)= A[rows of tiles R0..R0+NR-1] (LDS, lda) . W^T, W [N x K] row-major in global; column
 // tiles c0..c0+NC-1; acc rows beyond NR are untouched.  The next chunk's W fragment is loaded before
@@ -527,17 +478,295 @@ __device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ 
   __syncthreads();
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// attention on MFMA (v_mfma_f32_16x16x4_f32)
+// ---------------------------------------------------------------------------------------------
+// A query tile R (token rows 16R .. 16R+15 of the workgroup) attends only to the keys of the
+// sequences its rows belong to: key tiles band_lo(R) .. band_hi(R) (at most 3; 13 of the 25
+// 16 x 16 tiles of the 80 x 80 score matrix for L = 20).  Scores are computed transposed,
+// S^T = K Q^T: lane (i = l & 15, g4 = l >> 4) holds S^T[key 16c + 4 g4 + q][query 16R + i], so each
+// lane owns one query column, the softmax over keys is lane-local over (c, q) plus the 4 lane rows
+// (permlane swaps), and the probabilities in registers are directly the A operand of the next
+// product over keys (ctx = P'V, dQ = dS K: k = key 4 g4 + q of each 16-key chunk).
+template <int L> constexpr int band_lo(int r) { return ((16 * r) / L) * L / 16; }
+template <int L> constexpr int band_hi(int r) {
+  const int e = ((16 * r + 15) / L + 1) * L - 1;
+  return (e > ROWS - 1 ? ROWS - 1 : e) / 16;
+}
+template <int L> constexpr int band_n(int r) { return band_hi<L>(r) - band_lo<L>(r) + 1; }
+template <int L> constexpr int band_slot(int r) {
+  int s = 0;
+  for (int k = 0; k < r; ++k) s += band_n<L>(k);
+  return s;
+}
+constexpr int TILE_LD = 20;               // scratch score tiles [16 keys][16 queries], rows padded to 20
+constexpr int TILE_SZ = 16 * TILE_LD;
+constexpr int MAX_SLOTS = 13;             // band tiles of the 5 query tiles, max over supported L
+constexpr int DQ_LD = HD + 4;
+
+// max / sum over the 4 lane rows (lanes l, l ^ 16, l ^ 32, l ^ 48), the same value in every lane
+__device__ __forceinline__ float rows4_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) { return swap32_sum(swap16_sum(v)); }
+
+// S^T tiles of query tile R, head hh: s[c] = K[key tile C0 + c] Q[tile R]^T (unscaled).  ``OFF``:
+// column offset of the left operand (E: K for scores; 2E: V for dP'^T = V dctx^T with Bsrc = dctx).
+// All operands are read first, then the NC independent accumulation chains are interleaved.
+template <int R, int C0, int NC>
+__device__ __forceinline__ void tiles_t(const float* RA, int off, const float* Bsrc, int ldb, int hh, f32x4 (&s)[NC]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, g4 = lane >> 4;
+  float4 a[NC][HD / 16], b[HD / 16];
+#pragma unroll
+  for (int kc = 0; kc < HD / 16; ++kc) {
+    b[kc] = lds4(Bsrc + (16 * R + i) * ldb + hh * HD + 16 * kc + 4 * g4);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) a[c][kc] = lds4(RA + (16 * (C0 + c) + i) * LD_QKV + off + hh * HD + 16 * kc + 4 * g4);
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) s[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < HD / 16; ++kc)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) s[c] = mfma4(comp(a[c][kc], m), comp(b[kc], m), s[c]);
+}
+
+// out[dt] = X^T-tiles (registers, A operand: k = key 4 g4 + m of each 16-key chunk) times the rows
+// of RA at column offset ``off`` (keys of the band, B operand as scalars), both column tiles of the head
+template <int C0, int NC>
+__device__ __forceinline__ void keys_product(const f32x4 (&x)[NC], const float* RA, int off, int hh,
+                                             f32x4 (&out)[HD / 16]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, g4 = lane >> 4;
+  float b[HD / 16][NC][4];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) b[dt][c][m] = RA[(16 * (C0 + c) + 4 * g4 + m) * LD_QKV + off + hh * HD + 16 * dt + i];
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) out[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) out[dt] = mfma4(x[c][m], b[dt][c][m], out[dt]);
+}
+
+// e^x as 2^(x log2 e) on v_exp_f32 (exact at -inf -> 0; relative error a few 1e-7 over the
+// softmax's range x in [-30, 0], far inside the layer's 2e-5 tolerance)
+__device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// scale + key masks (other sequences, key padding) and the softmax over keys, in place: s -> p
+template <int L, int C0, int NC>
+__device__ __forceinline__ void softmax_t(const float* MS, int qrow, f32x4 (&s)[NC]) {
+  const int g4 = (threadIdx.x & 63) >> 4, lo = (qrow / L) * L;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int key = 16 * (C0 + c) + 4 * g4 + q;
+      const float ms = MS[key];  // key < 80 always: an unconditional load, no branch
+      const float v = (unsigned)(key - lo) < (unsigned)L ? s[c][q] * kScale + ms : -INFINITY;
+      s[c][q] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = rows4_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e = exp_fast(s[c][q] - mx);
+      s[c][q] = e;
+      sum += e;
+    }
+  const float inv = 1.f / rows4_sum(sum);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) s[c] = s[c] * inv;
+}
+
+// keep bits of the attention dropout at this lane's (key, query) elements: bit 4c + q.  A lane's
+// four keys of a tile are consecutive elements of one score row; for even L a row starts on a pair
+// boundary, so q = 0, 1 and q = 2, 3 share one pair hash (keep()'s halves)
+template <int L, int C0, int NC>
+__device__ __forceinline__ uint32_t att_keep_bits(uint32_t ks, uint32_t thr, int64_t seq0, int hh, int qrow) {
+  if (thr == 0u) return 0xFFFFFFFFu;
+  const int g4 = (threadIdx.x & 63) >> 4, g = qrow / L;
+  const uint32_t base = (uint32_t)((((seq0 + g) * HEADS + hh) * L + (qrow - g * L)) * L);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    // keys of other sequences have p = 0: whatever their bit, they contribute nothing
+    const uint32_t e0 = base + (uint32_t)(16 * (C0 + c) + 4 * g4 - g * L);
+    if constexpr (L % 2 == 0) {
+      const uint32_t h0 = pair_hash(ks, e0 >> 1), h1 = pair_hash(ks, (e0 >> 1) + 1);
+      bits |= ((uint32_t)half_keep(h0, 0, thr) | ((uint32_t)half_keep(h0, 1, thr) << 1) |
+               ((uint32_t)half_keep(h1, 0, thr) << 2) | ((uint32_t)half_keep(h1, 1, thr) << 3)) << (4 * c);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bits |= (uint32_t)keep(ks, e0 + q, thr) << (4 * c + q);
+    }
+  }
+  return bits;
+}
+
+// forward: ctx rows of query tile R, head hh, written over the tile's q slots in RA
+template <int L, int R>
+__device__ __forceinline__ void attn_fwd_tile(float* RA, const float* MS, int hh, int64_t seq0, uint32_t ks,
+                                              const Weights& w, bool prof) {
+  constexpr int C0 = band_lo<L>(R), NC = band_n<L>(R);
+  const int lane = threadIdx.x & 63, i = lane & 15, g4 = lane >> 4;
+  const int qrow = 16 * R + i;
+  f32x4 s[NC];
+  tiles_t<R, C0, NC>(RA, E, RA, LD_QKV, hh, s);
+  fr_mark(prof, 0, 21);
+  softmax_t<L, C0, NC>(MS, qrow, s);
+  fr_mark(prof, 0, 22);
+  const uint32_t kb = att_keep_bits<L, C0, NC>(ks, w.thr[0], seq0, hh, qrow);
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[c][q] = ((kb >> (4 * c + q)) & 1u) ? s[c][q] * w.scale[0] : 0.f;
+  fr_mark(prof, 0, 23);
+  f32x4 ctx[HD / 16];
+  keys_product<C0, NC>(s, RA, 2 * E, hh, ctx);
+  // only this job reads the q slots of (tile R, head hh), and it is done with them
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) RA[(16 * R + 4 * g4 + q) * LD_QKV + hh * HD + 16 * dt + i] = ctx[dt][q];
+  fr_mark(prof, 0, 24);
+}
+
+// the 10 (query tile, head) jobs over 8 waves: tiles 1-3 (3 band tiles for L = 20, 10, 5) one per
+// wave, tiles 0 and 4 (2 band tiles) two per wave on waves 6 and 7
+template <int L>
+__device__ __forceinline__ void attn_fwd(float* RA, const float* MS, int64_t seq0, uint32_t ks, const Weights& w,
+                                         bool prof) {
+  static_assert(RT == 5 && HEADS == 2 && NT / 64 == 8, "job table");
+  const int wave = wave_id();
+  for (int j = wave; j < RT * HEADS; j += (wave >= 6 ? 2 : RT * HEADS)) {
+    const int R = j < 6 ? 1 + j % 3 : ((j - 6) % 2 ? 4 : 0), hh = j < 6 ? j / 3 : (j - 6) / 2;
+    switch (R) {
+      case 0: attn_fwd_tile<L, 0>(RA, MS, hh, seq0, ks, w, prof); break;
+      case 1: attn_fwd_tile<L, 1>(RA, MS, hh, seq0, ks, w, prof); break;
+      case 2: attn_fwd_tile<L, 2>(RA, MS, hh, seq0, ks, w, prof); break;
+      case 3: attn_fwd_tile<L, 3>(RA, MS, hh, seq0, ks, w, prof); break;
+      default: attn_fwd_tile<L, 4>(RA, MS, hh, seq0, ks, w, prof); break;
+    }
+  }
+}
+
+// backward, phase 1 (query tile R, head hh): recompute P, dP'^T = V dctx^T, dropout backward,
+// dS = P (dP - D) / sqrt(HD); P' and dS tiles to the scratch ([key][query], TILE_LD), dQ = dS K to DQ
+template <int L, int R>
+__device__ __forceinline__ void attn_bwd_rows(const float* RA, const float* RC, const float* MS, int hh, int64_t seq0,
+                                              uint32_t ks, const Weights& w, float* SP, float* SS, float* DQ,
+                                              bool prof) {
+  constexpr int C0 = band_lo<L>(R), NC = band_n<L>(R), S0 = band_slot<L>(R);
+  const int lane = threadIdx.x & 63, i = lane & 15, g4 = lane >> 4;
+  const int qrow = 16 * R + i;
+  f32x4 p[NC], d[NC];
+  tiles_t<R, C0, NC>(RA, E, RA, LD_QKV, hh, p);      // S^T = K Q^T
+  tiles_t<R, C0, NC>(RA, 2 * E, RC, LD_E, hh, d);    // dP'^T = V dctx^T
+  if (hh == 0) fr_mark(prof, 1, 13);
+  softmax_t<L, C0, NC>(MS, qrow, p);
+  const uint32_t kb = att_keep_bits<L, C0, NC>(ks, w.thr[0], seq0, hh, qrow);
+  if (hh == 0) fr_mark(prof, 1, 14);
+  float D = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dpj = ((kb >> (4 * c + q)) & 1u) ? d[c][q] * w.scale[0] : 0.f;  // dL/dp
+      d[c][q] = dpj;
+      D = fmaf(p[c][q], dpj, D);
+    }
+  D = rows4_sum(D);
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float pv = p[c][q];
+      const float ds = pv * (d[c][q] - D) * kScale;
+      d[c][q] = ds;
+      const int o = (S0 + c) * TILE_SZ + (4 * g4 + q) * TILE_LD + i;
+      SS[o] = ds;
+      SP[o] = ((kb >> (4 * c + q)) & 1u) ? pv * w.scale[0] : 0.f;  // p'
+    }
+  if (hh == 0) fr_mark(prof, 1, 15);
+  f32x4 dq[HD / 16];
+  keys_product<C0, NC>(d, RA, E, hh, dq);  // dQ = dS K
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) DQ[(16 * R + 4 * g4 + q) * DQ_LD + 16 * dt + i] = dq[dt][q];
+  if (hh == 0) fr_mark(prof, 1, 16);
+}
+
+// backward, phase 2 (key tile c, head hh, column tile dt): dK = dS^T Q (kind 0) or dV = P'^T dctx
+// (kind 1) over the query tiles whose band holds c, written over the key rows' k / v slots
+template <int L>
+__device__ __forceinline__ void attn_bwd_keys(float* RA, const float* RC, const float* SP, const float* SS, int hh,
+                                              int c, int kind, int dt) {
+  const int lane = threadIdx.x & 63, i = lane & 15, g4 = lane >> 4;
+  const float* T = kind ? SP : SS;
+  const float* Bm = kind ? RC : RA;
+  const int ldb = kind ? LD_E : LD_QKV;
+  float4 a[RT];
+  float b[RT][4];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {  // operands of every query tile first (tiles outside the band: zeros)
+    const bool in = c >= band_lo<L>(r) && c <= band_hi<L>(r);
+    const int slot = in ? band_slot<L>(r) + c - band_lo<L>(r) : 0;
+    a[r] = lds4(T + slot * TILE_SZ + i * TILE_LD + 4 * g4);
+    if (!in) a[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) b[r][m] = Bm[(16 * r + 4 * g4 + m) * ldb + hh * HD + 16 * dt + i];
+  }
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;  // two chains (even / odd query tiles), summed at the end
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      if (r % 2 == 0) acc0 = mfma4(comp(a[r], m), b[r][m], acc0);
+      else acc1 = mfma4(comp(a[r], m), b[r][m], acc1);
+    }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    RA[(16 * c + 4 * g4 + q) * LD_QKV + (kind ? 2 * E : E) + hh * HD + 16 * dt + i] = acc0[q] + acc1[q];
+}
+
+template <int L>
+__device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const float* RC, const float* MS, int hh,
+                                                  int64_t seq0, uint32_t ks, const Weights& w, float* SP, float* SS,
+                                                  float* DQ, bool prof) {
+  switch (R) {
+    case 0: attn_bwd_rows<L, 0>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    case 1: attn_bwd_rows<L, 1>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    case 2: attn_bwd_rows<L, 2>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    case 3: attn_bwd_rows<L, 3>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    default: attn_bwd_rows<L, 4>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
 template <int L>
 __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   constexpr int G = ROWS / L;
-  constexpr int NTASK = G * HEADS * L;
-  static_assert(2 * NTASK <= NT, "two lanes per attention task");
   __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];  // qkv (ctx in the q slots), then act
   __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];   // x -> y1 -> x1 -> y2
-  __shared__ float SB[L * NTASK];                                   // attention score rows
   __shared__ float MS[ROWS];                                        // key mask of the tile's tokens
   const Weights& w = a.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
@@ -579,48 +808,11 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();  // the copy has read every q slot before attention overwrites them with ctx
   FR_MARK(0, 20);
 
-  // attention: lanes 2t, 2t+1 own task t = (sequence, head, query row), dimensions [16 hl, 16 hl + 16);
-  // score rows in LDS as SB[j][task]
-  {
-    const int t = threadIdx.x >> 1, hl = threadIdx.x & 1;
-    const int g = t / (HEADS * L), hh = (t / L) % HEADS, qi = t % L;
-    if (t < NTASK && g < nseq) {  // both lanes of a pair take the same branch
-      const int rq = g * L + qi, dof = hh * HD + 16 * hl;
-      v16 q;
-      load16(RA + rq * LD_QKV + dof, q);
-      float* sr = SB + t;  // score row j at sr[j * NTASK] (both lanes write the same value)
-      float mx = -INFINITY;
-#pragma unroll 2
-      for (int j = 0; j < L; ++j) {
-        const float d = dot16(q, RA + (g * L + j) * LD_QKV + E + dof);
-        const float sj = (d + pair_swap(d)) * kScale + MS[g * L + j];
-        sr[j * NTASK] = sj;
-        mx = fmaxf(mx, sj);
-      }
-      float sum = 0.f;
-#pragma unroll 4
-      for (int j = 0; j < L; ++j) {
-        const float e = expf(sr[j * NTASK] - mx);
-        sr[j * NTASK] = e;
-        sum += e;
-      }
-      const float pin = w.scale[0] / sum;
-      const uint32_t base = (uint32_t)((((seq0 + g) * HEADS + hh) * L + qi) * L);
-      v16 c;
-      zero16(c);
-#pragma unroll 2
-      for (int j = 0; j < L; ++j) {
-        const float p = keep_att(ks.k[0], base, j, w.thr[0]) ? sr[j * NTASK] * pin : 0.f;
-        axpy16(p, RA + (g * L + j) * LD_QKV + 2 * E + dof, c);
-      }
-      store16(RA + rq * LD_QKV + dof, c);
-      float* go = a.ctx + (tok0 + rq) * E + dof;
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) *reinterpret_cast<float4*>(go + 4 * e4) = quad16(c, e4);
-    }
-  }
+  // attention on MFMA: 10 (query tile, head) jobs over the 8 waves; ctx over the q slots
+  attn_fwd<L>(RA, MS, seq0, ks.k[0], w, prof);
   __syncthreads();
   FR_MARK(0, 3);
+  lds_store<E>(RA, LD_QKV, a.ctx + tok0 * E, tv);  // ctx (saved for the backward): cols 0..63 of RA
 
   {  // y1 = x + dropout1(ctx W_o^T + b_o)   (column tile sg); ctx rows of padded sequences are stale
     f32x4 acc[RT0][1];
@@ -714,14 +906,21 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
 template <int L>
 __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   constexpr int G = ROWS / L;
-  constexpr int NTASK = G * HEADS * L;
-  static_assert(2 * NTASK <= NT, "two lanes per attention task");
-  __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];
-  __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];
-  __shared__ __attribute__((aligned(16))) float RC[ROWS * LD_E];
-  __shared__ __attribute__((aligned(16))) float RD[BUF_D];
-  static_assert(2 * G * HEADS * L * L <= BUF_D && ROWS * LD_E <= BUF_D && 2 * (NT / 16) * E <= BUF_D,
-                "attention / LayerNorm scratch");
+  // one LDS image: RA [80 x 260] | RC [80 x 68] | RB [80 x 68] | RD [BUF_D]; the attention backward's
+  // scratch (P' and dS tiles, dQ) overlays RB + RD (dY1 is held in registers across it)
+  constexpr int OFF_RC = ROWS * LD_FF, OFF_RB = OFF_RC + ROWS * LD_E, OFF_RD = OFF_RB + ROWS * LD_E;
+  constexpr int SCR_FLOATS = 2 * MAX_SLOTS * TILE_SZ + ROWS * DQ_LD;
+  static_assert(SCR_FLOATS <= ROWS * LD_E + BUF_D, "attention scratch fits RB + RD");
+  static_assert(ROWS * LD_E <= BUF_D && 2 * (NT / 16) * E <= BUF_D, "LayerNorm scratch / ctx in RD");
+  static_assert(band_slot<L>(RT) <= MAX_SLOTS, "band tiles");
+  __shared__ __attribute__((aligned(16))) float LDSB[OFF_RD + BUF_D];
+  float* const RA = LDSB;
+  float* const RC = LDSB + OFF_RC;
+  float* const RB = LDSB + OFF_RB;
+  float* const RD = LDSB + OFF_RD;
+  float* const SP = RB;                            // P' tiles   [MAX_SLOTS][16][TILE_LD]
+  float* const SS = RB + MAX_SLOTS * TILE_SZ;      // dS tiles
+  float* const DQ = RB + 2 * MAX_SLOTS * TILE_SZ;  // dQ of one head [80][DQ_LD]
   const Weights& w = a.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
   const int sg = wave & 3, hf = wave >> 2, r0 = hf ? RT0 : 0, nr = hf ? RT - RT0 : RT0;
@@ -840,6 +1039,13 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   wgrad_tiles<1, 2>(RC, LD_E, RD, LD_E, sg, 2 * hf, part + OFF_WO, E);
   colsum(RC, LD_E, E, part + OFF_BO);
 
+  // dY1 rows of this lane's final dX elements, held in registers: the attention scratch overlays RB
+  float dy1[RT0][4];
+#pragma unroll
+  for (int r = 0; r < RT0; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dy1[r][q] = r < nr ? RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + 16 * sg + i16] : 0.f;
+
   {  // 11. dctx = dO W_o -> RC;  qkv -> RA
     f32x4 acc[RT0][1];
     zero_acc(acc);
@@ -858,83 +1064,26 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   __syncthreads();
   FR_MARK(1, 9);
 
-  // 12. attention backward.  RD: P[j][task] (scores -> p -> p') and S[j][task] (dL/dp' -> ds * scale),
-  // task = (sequence, head, query row); lanes 2t, 2t+1 own task t's dimensions [16 hl, 16 hl + 16)
-  float* Pb = RD;
-  float* Sb = RD + NTASK * L;
-  const int tt = threadIdx.x >> 1, hl = threadIdx.x & 1;
-  const int tg = tt / (HEADS * L), thh = (tt / L) % HEADS, ti = tt % L;
-  const bool live = tt < NTASK && tg < nseq;  // the same for both lanes of a pair
-  const int dof = thh * HD + 16 * hl;
-  v16 dq;
-  if (live) {  // phase a: query row ti
-    const int rq = tg * L + ti;
-    v16 q, dc;
-    load16(RA + rq * LD_QKV + dof, q);
-    load16(RC + rq * LD_E + dof, dc);
-    float* pr = Pb + tt;  // both lanes of the pair write the same values
-    float* sr = Sb + tt;
-    float mx = -INFINITY;
-#pragma unroll 2
-    for (int j = 0; j < L; ++j) {
-      const float* kr = RA + (tg * L + j) * LD_QKV + E + dof;
-      const float d1 = dot16(q, kr), d2 = dot16(dc, kr + E);   // q . k_j,  dctx . v_j (= dL/dp')
-      const float sj = (d1 + pair_swap(d1)) * kScale + MS[tg * L + j];
-      pr[j * NTASK] = sj;
-      sr[j * NTASK] = d2 + pair_swap(d2);
-      mx = fmaxf(mx, sj);
+  // 12. attention backward on MFMA, one head at a time (the scratch holds one head's tiles):
+  //   phase 1: query tiles (5 waves): P, dP'^T, dS, the P' / dS tiles, dQ -> DQ
+  //   phase 2: (key tile, dK | dV, column tile) jobs: dK = dS^T Q, dV = P'^T dctx over the k / v slots
+  //   then dQ over the head's q slots (phase 2 has read them)
+  const int wv = wave_id();
+  for (int hh = 0; hh < HEADS; ++hh) {
+    if (wv < RT) attn_bwd_rows_any<L>(wv, RA, RC, MS, hh, seq0, ks.k[0], w, SP, SS, DQ, prof);
+    __syncthreads();
+    if (hh == 0) FR_MARK(1, 18);
+    for (int j = wv; j < RT * 2 * (HD / 16); j += NT / 64)
+      attn_bwd_keys<L>(RA, RC, SP, SS, hh, j % RT, (j / RT) % 2, j / (2 * RT));
+    __syncthreads();
+    if (hh == 0) FR_MARK(1, 19);
+    for (int e = threadIdx.x; e < ROWS * (HD / 4); e += NT) {
+      const int r = e / (HD / 4), c4 = e % (HD / 4);
+      *reinterpret_cast<float4*>(RA + r * LD_QKV + hh * HD + 4 * c4) = lds4(DQ + r * DQ_LD + 4 * c4);
     }
-    float sum = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < L; ++j) {
-      const float e = expf(pr[j * NTASK] - mx);
-      pr[j * NTASK] = e;
-      sum += e;
-    }
-    const float inv = 1.f / sum;
-    const uint32_t base = (uint32_t)((((seq0 + tg) * HEADS + thh) * L + ti) * L);
-    float D = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < L; ++j) {
-      const float p = pr[j * NTASK] * inv;
-      const bool kp = keep_att(ks.k[0], base, j, w.thr[0]);
-      const float dpj = kp ? sr[j * NTASK] * w.scale[0] : 0.f;  // dL/dp
-      pr[j * NTASK] = kp ? p : -p;                               // keep bit in the sign
-      sr[j * NTASK] = dpj;
-      D = fmaf(p, dpj, D);
-    }
-    zero16(dq);
-#pragma unroll 2
-    for (int j = 0; j < L; ++j) {
-      const float ps = pr[j * NTASK], p = fabsf(ps);
-      const float ds = p * (sr[j * NTASK] - D) * kScale;
-      axpy16(ds, RA + (tg * L + j) * LD_QKV + E + dof, dq);
-      sr[j * NTASK] = ds;
-      pr[j * NTASK] = ps > 0.f ? p * w.scale[0] : 0.f;  // p'
-    }
+    __syncthreads();
   }
-  __syncthreads();
   FR_MARK(1, 10);
-  if (live) {  // phase b: key row j = ti:  dk_j = sum_i ds_ij q_i,  dv_j = sum_i p'_ij dctx_i
-    const int rk = tg * L + ti;
-    v16 dk, dv;
-    zero16(dk);
-    zero16(dv);
-#pragma unroll 4
-    for (int qi = 0; qi < L; ++qi) {
-      const int qt = (tg * HEADS + thh) * L + qi;
-      const float ds = Sb[ti * NTASK + qt];
-      const float pp = Pb[ti * NTASK + qt];
-      axpy16(ds, RA + (tg * L + qi) * LD_QKV + dof, dk);
-      axpy16(pp, RC + (tg * L + qi) * LD_E + dof, dv);
-    }
-    // k / v slots of row rk are read by no one after phase a
-    store16(RA + rk * LD_QKV + E + dof, dk);
-    store16(RA + rk * LD_QKV + 2 * E + dof, dv);
-  }
-  __syncthreads();
-  FR_MARK(1, 11);
-  if (live) store16(RA + (tg * L + ti) * LD_QKV + dof, dq);
   if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
   lds_load<E>(RC, LD_E, a.x + tok0 * E, tv);
   __syncthreads();
@@ -955,40 +1104,42 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * (r0 + r) + 4 * h4 + q;
-        if (row < tv) a.dx[(tok0 + row) * E + col] = RB[row * LD_E + col] + acc[r][0][q];
+        if (row < tv) a.dx[(tok0 + row) * E + col] = dy1[r][q] + acc[r][0][q];
       }
     }
   }
   FR_MARK(1, 31);
 }
 
-// grad[j] = sum over workgroups of part[wg][j], in a fixed order (deterministic): a block owns 32
-// float4 columns; its 8 slices sum workgroups slice, slice+8, ... (8 loads in flight per thread),
-// then the slices are added in slice order.
+// grad[j] = sum over workgroups of part[wg][j], in a fixed order (deterministic).  A block owns 16
+// float4 columns and 16 slices; slice s sums workgroups s, s + 16, s + 32, ... in order (all of its
+// loads in flight at once: 16 per thread at 256 workgroups), then the slices are added in slice
+// order.  781 blocks for the 12,496 float4 columns: three per CU, every CU streaming.
+constexpr int RED_COLS = 16, RED_SL = 16, RED_UNR = 16;
 __global__ __launch_bounds__(256) void enc_reduce_kernel(const float4* __restrict__ part, int nwg,
                                                          float4* __restrict__ grad) {
-  constexpr int COLS = 32, SL = 8, UNR = 8, N4 = NPART / 4;
-  __shared__ float4 sl[SL][COLS];
-  const int c = blockIdx.x * COLS + (threadIdx.x % COLS), slice = threadIdx.x / COLS;
+  constexpr int N4 = NPART / 4;
+  __shared__ float4 sl[RED_SL][RED_COLS];
+  const int c = blockIdx.x * RED_COLS + (threadIdx.x % RED_COLS), slice = threadIdx.x / RED_COLS;
   const int cc = min(c, N4 - 1);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int g0 = slice; g0 < nwg; g0 += SL * UNR) {
-    float4 v[UNR];
+  for (int g0 = slice; g0 < nwg; g0 += RED_SL * RED_UNR) {
+    float4 v[RED_UNR];
 #pragma unroll
-    for (int k = 0; k < UNR; ++k) {
-      const int g = min(g0 + k * SL, nwg - 1);
+    for (int k = 0; k < RED_UNR; ++k) {
+      const int g = min(g0 + k * RED_SL, nwg - 1);
       v[k] = part[(int64_t)g * N4 + cc];
     }
 #pragma unroll
-    for (int k = 0; k < UNR; ++k)
-      if (g0 + k * SL < nwg) s = f4_add(s, v[k]);
+    for (int k = 0; k < RED_UNR; ++k)
+      if (g0 + k * RED_SL < nwg) s = f4_add(s, v[k]);
   }
-  sl[slice][threadIdx.x % COLS] = s;
+  sl[slice][threadIdx.x % RED_COLS] = s;
   __syncthreads();
   if (slice == 0 && c < N4) {
     float4 t = sl[0][threadIdx.x];
 #pragma unroll
-    for (int k = 1; k < SL; ++k) t = f4_add(t, sl[k][threadIdx.x]);
+    for (int k = 1; k < RED_SL; ++k) t = f4_add(t, sl[k][threadIdx.x]);
     grad[c] = t;
   }
 }
@@ -1006,7 +1157,7 @@ int launch_bwd(const BwdArgs& a, float* grad, hipStream_t s) {
   const int64_t nwg = fr::ceil_div(a.ns, ROWS / L);
   hipLaunchKernelGGL(enc_bwd_kernel<L>, dim3((unsigned)nwg), dim3(NT), 0, s, a);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, 32)), dim3(256), 0, s,
+  hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(a.part), (int)nwg, reinterpret_cast<float4*>(grad));
   FR_LAUNCH_CHECK();
   return FR_OK;

@@ -80,7 +80,7 @@ def main():
         phases = {}
         for kind, name in ((0, "fwd"), (1, "bwd")):
             m = marks[kind].astype(np.int64)
-            idx = [k for k in range(32) if m[k] != 0]
+            idx = sorted((k for k in range(32) if m[k] != 0), key=lambda k: m[k])  # in time order
             phases[name] = {f"{a}->{b}": int(m[b] - m[a]) for a, b in zip(idx, idx[1:])}
             phases[name]["total"] = int(m[idx[-1]] - m[idx[0]])
     print(json.dumps({"ns": args.ns, "L": args.L, "p": args.p, "fused_fwd_ms": round(t_fwd, 4),
