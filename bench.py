@@ -390,15 +390,27 @@ def main():
         dist.destroy_process_group()
 
 
+# the kernels each engine timing region launches on HEAD (tools/pmc_regions.py REGION_KERNELS): a
+# committed PMC file sampled from other kernels is stale and is not used
+REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel", "enc_reduce_kernel"], "encoder_fwd": ["enc_fwd_kernel"],
+                  "spmm": ["spmm_plain16_kernel"], "spmm_masked": ["spmm_sparse_kernel"],
+                  "spmm_rows": ["spmm_rows_kernel"], "adam": ["adam_kernel<false>"],
+                  "adam_rows": ["adam_lazy_rows_kernel<false>"]}
+
+
 def pmc_traffic(kernel):
-    """HBM bytes per launch of ``kernel`` measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, the
-    gfx950 calibration) in a separate profiling run, committed under profiles/ (newest round)."""
+    """HBM bytes per launch of region ``kernel`` measured by rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE,
+    the gfx950 calibration) in separate profiling passes, committed under profiles/ (newest round),
+    or None when that file's region was sampled from other kernels than the region launches today."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
     if not files or kernel is None:
         return None
     with open(files[-1]) as f:
-        return json.load(f).get("per_region_bytes", {}).get(kernel)
+        d = json.load(f)
+    if d.get("region_kernels", {}).get(kernel) != REGION_KERNELS.get(kernel):
+        return None
+    return d.get("per_region_bytes", {}).get(kernel)
 
 
 def config4_bytes_per_step(N, nnz, P, B, L=2, d=64, s=4, adam=28):

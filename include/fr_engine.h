@@ -454,7 +454,7 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * caller advances the counter; graph replays draw fresh masks).
  * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), fact [T,256] (dropout(act(FF1))),
  * y2 [T,64] (LN2 input), st1/st2 [T,2] (mean, rstd), T = n_seq * L, and dact (keep/(1-p) *
- * act'(FF1)) as ceil(n_seq / (80 / L)) * 80 * 256 floats in the kernels' MFMA fragment layout
+ * act'(FF1)) as fr_encoder_dact_numel(n_seq, L) floats in the kernels' MFMA fragment layout
  * (opaque to the caller; only fr_encoder_bwd reads it).
  * Backward writes dx and the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
  * gradients concatenated in d_params order); d_partials [fr_encoder_partials(n_seq, L)] floats of
@@ -462,6 +462,7 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_encoder_partials(int64_t n_seq, int L);
 int64_t fr_encoder_grad_numel(void);
+int64_t fr_encoder_dact_numel(int64_t n_seq, int L);
 /* Diagnostics: enable (1) / disable (0) / keep (-1) per-phase s_memtime stamps of workgroup 0 and
  * copy the stamp table (uint64 [2][32]: forward, backward; shader clock) to host_marks if non-NULL. */
 int fr_encoder_profile(int enable, uint64_t* host_marks);
@@ -663,6 +664,14 @@ int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
                       uint32_t* d_bits, void* stream);
+/* fr_spmm_scatter_upstream: fr_spmm_sparse_upstream's result for a SYMMETRIC adjacency (HealthRec's UI
+ * graph, cikm_model.py:136-180) by scattering from the listed rows' own CSR rows: Y2 = alpha A X +
+ * beta1 gate(X), X non-zero only at the rows of `rows` (mask[r] != 0 and bit r set in d_bits).
+ * Work proportional to the listed rows' degrees; the first occurrence of each row claims it by
+ * clearing its bit (d_bits is clear for the listed rows on return).  Float-atomic summation order. */
+int fr_spmm_scatter_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                             const uint8_t* d_mask, uint32_t* d_bits, const fr_rowlist* rows, const float* d_X,
+                             int64_t ldx, int64_t split, const fr_tab* Y2, float alpha, float beta1, void* stream);
 /* fr_spmm_sparse_upstream over a rectangular slice [n_rows x n_cols] (the row-sharded config-4
  * step's A_ui / A_iu, engine/sharded.py): the bitmask (ceil(n_cols / 32) words, read from L2) marks
  * the non-zero rows of X (the slice's columns); A1 is read at every output row (no gate). */

@@ -12,8 +12,9 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native",
-                         "libfr_engine.so")
+# FR_ENGINE_LIB: another build of the same ABI (A/B comparisons of kernel versions); no fallback either
+_LIB_PATH = os.environ.get("FR_ENGINE_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "libfr_engine.so")
 
 FR_OK = 0
 _STATUS = {1: "FR_EINVAL", 2: "FR_EHIP", 3: "FR_ENOTSUP", 4: "FR_ERANGE", 5: "FR_EIO", 6: "FR_EPARSE"}
@@ -66,6 +67,9 @@ _SIGS = {
     "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
     "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p,
                                   c_void_p]),
+    "fr_spmm_scatter_upstream": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                         POINTER(FrRowList), c_void_p, c_int64, c_int64, POINTER(FrTab), c_float,
+                                         c_float, c_void_p]),
     "fr_spmm_sparse_upstream": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64,
                                         POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p]),
     "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
@@ -187,6 +191,7 @@ _SIGS = {
                                     c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_encoder_partials": (c_int64, [c_int64, c_int]),
     "fr_encoder_grad_numel": (c_int64, []),
+    "fr_encoder_dact_numel": (c_int64, [c_int64, c_int]),
     "fr_encoder_profile": (c_int, [c_int, c_void_p]),
     "fr_encoder_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p), POINTER(c_float),
                                POINTER(c_float), c_uint64, c_int, c_void_p, c_void_p, c_void_p,

@@ -14,6 +14,7 @@ infonce_loss(H, tau)     CL_loss                           pricai_modelx.py:354-
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -651,6 +652,26 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
             native.stream_of(X)), "fr_spmm_sparse_upstream")
 
 
+def spmm_scatter_upstream(adj: Adjacency, mask: torch.Tensor, bits: torch.Tensor, rows, X: torch.Tensor, Y2,
+                          Y2_hi=None, split=0, alpha=1.0, beta1=0.0, region="spmm_masked"):
+    """fr_spmm_scatter_upstream: spmm_sparse_upstream's Y2 = alpha A X + beta1 gate(X) for a symmetric
+    adjacency, scattered from the listed rows' own CSR rows (work proportional to their degrees, not
+    to the edge count); ``mask`` / ``bits`` mark the listed rows (rows_mark) and the listed rows' bits
+    are clear on return.  d = 64; float-atomic summation order (non-deterministic mode only)."""
+    native.require_device(X, bits, mask)
+    N = adj.shape[0]
+    if adj.shape[1] != N or not adj.symmetric or X.shape[1] != 64 or X.shape[0] < N:
+        raise native.EngineError("spmm_scatter_upstream: symmetric square adjacency, X [rows, 64]")
+    if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32 or mask.numel() < N:
+        raise native.EngineError("spmm_scatter_upstream: uint8 mask and int32 bits over the rows")
+    _check_tab("Y2", Y2, Y2_hi, split, N, 64)
+    with profiling.region(region, 0):
+        native.check(native.lib().fr_spmm_scatter_upstream(
+            adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, mask.data_ptr(), bits.data_ptr(),
+            ctypes.byref(_rowlist(rows)), X.data_ptr(), X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)),
+            _f(alpha), _f(beta1), native.stream_of(X)), "fr_spmm_scatter_upstream")
+
+
 def spmm_sparse_rect(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, alpha=1.0, A1=None, beta1=0.0,
                      region="spmm_masked"):
     """fr_spmm_sparse_upstream_rect: Y2 = alpha A X + beta1 A1 over a rectangular [rows x cols]
@@ -911,7 +932,10 @@ class _GraphBpr(torch.autograd.Function):
                                            ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd_ex")
         d_user = grad_buffer(user_w)
         G_ri = _persistent(ri_adj, ("g_ri", str(dev)), lambda: torch.zeros(I + NI, 64, device=dev))
-        if sparse:
+        if sparse and ui_adj.symmetric and os.environ.get("FR_UI_SCATTER", "1") != "0":
+            # scatter from the batch rows' own adjacency rows (A symmetric): work ~ their degrees
+            spmm_scatter_upstream(ui_adj, mask, bits, rows, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5)
+        elif sparse:
             spmm_sparse_upstream(ui_adj, bits, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5)
         else:
             _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
@@ -1260,12 +1284,15 @@ ENCODER_LENGTHS = (4, 5, 8, 10, 16, 20)
 
 
 def encoder_flops(n_seq: int, L: int, backward: bool) -> int:
-    """MFMA flops of one fused encoder-layer launch (d=64, FF=256): the four GEMMs per token
-    (qkv 2*64*192, out-proj 2*64*64, FF1 2*64*256, FF2 2*256*64 = 98,304 flops); the backward runs
-    both the input- and the weight-gradient GEMMs (2x).  The 20x20 attention is VALU work, not
-    counted."""
+    """Algorithmic flops of one fused encoder-layer launch (d=64, 2 heads of 32, FF=256), all on
+    the matrix cores: the four GEMMs per token (qkv 2*64*192, out-proj 2*64*64, FF1 2*64*256, FF2
+    2*256*64 = 98,304 flops), twice in the backward (input and weight gradients); and attention's
+    matrix products per (sequence, head): Q K^T and P' V (2 * 2 L L 32) forward, dP' = dctx V^T,
+    dV = P'^T dctx, dQ = dS K, dK = dS^T Q (4 * 2 L L 32) backward.  The backward's recomputation of
+    the scores is not counted (it is not algorithmic work)."""
     per_tok = 2 * 64 * 192 + 2 * 64 * 64 + 2 * 64 * 256 + 2 * 256 * 64
-    return n_seq * L * per_tok * (2 if backward else 1)
+    att = n_seq * 2 * (4 if backward else 2) * 2 * L * L * 32
+    return n_seq * L * per_tok * (2 if backward else 1) + att
 
 
 def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
@@ -1292,7 +1319,7 @@ class _EncoderLayer(torch.autograd.Function):
         cx = torch.empty(T, 64, **f32)
         y1 = torch.empty(T, 64, **f32)
         fact = torch.empty(T, 256, **f32)
-        dact = torch.empty(-(-NS // (80 // L)) * 80 * 256, **f32)  # per-workgroup MFMA fragment layout
+        dact = torch.empty(int(native.lib().fr_encoder_dact_numel(NS, L)), **f32)  # per-workgroup fragment layout
         y2 = torch.empty(T, 64, **f32)
         st1 = torch.empty(T, 2, **f32)
         st2 = torch.empty(T, 2, **f32)

@@ -24,7 +24,18 @@ constexpr int LPR = 16;  // lanes per triple
 struct BprWS {
   float* spos; float* sneg; float* squ; float* sqp; float* sqn;  // [B] each
   float* norms;                                                   // [4]: |U|,|P|,|N|, pad
+  uint64_t* keys_u;  // deterministic scatter: (row << 20 | slot) of the user slots, sorted [pow2(B)]
+  uint64_t* keys_i;  //   ... of the item slots (pos t -> t, neg t -> B + t), sorted [pow2(2B)]
 };
+
+// the deterministic scatter sorts the slot keys of a table in one workgroup's LDS when the larger
+// table (2B item slots) fits: 16,384 keys = 128 KB
+constexpr int64_t kDetSortMax = 16384;
+__host__ __device__ inline int64_t pow2_at_least(int64_t n) {
+  int64_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
 
 __host__ __device__ inline BprWS bpr_ws(void* base, int64_t B) {
   char* p = reinterpret_cast<char*>(base);
@@ -36,12 +47,16 @@ __host__ __device__ inline BprWS bpr_ws(void* base, int64_t B) {
   w.sqp = reinterpret_cast<float*>(take(B * 4));
   w.sqn = reinterpret_cast<float*>(take(B * 4));
   w.norms = reinterpret_cast<float*>(take(16));
+  const bool sortable = 2 * B <= kDetSortMax;
+  w.keys_u = sortable ? reinterpret_cast<uint64_t*>(take(pow2_at_least(B) * 8)) : nullptr;
+  w.keys_i = sortable ? reinterpret_cast<uint64_t*>(take(pow2_at_least(2 * B) * 8)) : nullptr;
   return w;
 }
 
 inline int64_t bpr_ws_bytes(int64_t B) {
   auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
-  return 5 * r(B * 4) + r(16);
+  const int64_t keys = 2 * B <= kDetSortMax ? r(pow2_at_least(B) * 8) + r(pow2_at_least(2 * B) * 8) : 0;
+  return 5 * r(B * 4) + r(16) + keys;
 }
 
 __device__ __forceinline__ float4 ld4(const float* base, int64_t row, int64_t ld, int q) {
@@ -354,6 +369,104 @@ __global__ __launch_bounds__(256) void bpr_bwd_det_kernel(
 }
 
 
+// Deterministic scatter, sorted form (2B <= kDetSortMax): the owner-slot kernel above scans every
+// earlier slot and, per owner, every triple -- O(B^2), 19 ms at B = 8192.  Here each table's slot keys
+// (row << 20 | slot) are sorted once in LDS (block 0: users, block 1: items; bitonic, 1024 threads),
+// then the first slot of each row's run owns the row and sums the run in slot order -- the same
+// contributions in the same order as bpr_bwd_det_kernel (bit-identical results), O(B log B).
+__global__ __launch_bounds__(1024) void bpr_det_sort_kernel(const int64_t* __restrict__ uu,
+                                                            const int64_t* __restrict__ pp,
+                                                            const int64_t* __restrict__ nn, int64_t B, BprWS ws) {
+  __shared__ uint64_t K[kDetSortMax];
+  const bool items = blockIdx.x == 1;
+  const int64_t cnt = items ? 2 * B : B;
+  const int64_t N = pow2_at_least(cnt);
+  for (int64_t k = threadIdx.x; k < N; k += 1024) {
+    uint64_t key = ~0ull;  // padding sorts last
+    if (k < cnt) {
+      const int64_t row = items ? (k < B ? pp[k] : nn[k - B]) : uu[k];
+      key = ((uint64_t)row << 20) | (uint64_t)k;
+    }
+    K[k] = key;
+  }
+  __syncthreads();
+  for (int64_t len = 2; len <= N; len <<= 1) {
+    for (int64_t j = len >> 1; j > 0; j >>= 1) {
+      for (int64_t k = threadIdx.x; k < N; k += 1024) {
+        const int64_t x = k ^ j;
+        if (x > k) {
+          const uint64_t a = K[k], b = K[x];
+          const bool up = (k & len) == 0;
+          if ((a > b) == up) {
+            K[k] = b;
+            K[x] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  uint64_t* out = items ? ws.keys_i : ws.keys_u;
+  for (int64_t k = threadIdx.x; k < cnt; k += 1024) out[k] = K[k];
+}
+
+__global__ __launch_bounds__(256) void bpr_bwd_det_sorted_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi,
+    const float* __restrict__ Ue, int64_t ldue, const float* __restrict__ Ie, int64_t ldie,
+    const int64_t* __restrict__ uu, const int64_t* __restrict__ pp, const int64_t* __restrict__ nn,
+    int64_t B, int d4, float gamma, float gmf, float greg, const float* gscale, float* dU, int64_t lddu,
+    float* dI, int64_t lddi, float* dUe, int64_t lddue, float* dIe, int64_t lddie, BprWS ws) {
+  constexpr int GPB = 256 / LPR;
+  constexpr uint64_t SLOT = (1ull << 20) - 1;
+  const int q0 = threadIdx.x % LPR;
+  if (gscale) { gmf *= gscale[0]; if (dUe || dIe) greg *= gscale[1]; }
+  const float inv_b = 1.f / (float)B;
+  const float ru = ws.norms[0] > 0.f ? greg * inv_b / ws.norms[0] : 0.f;
+  const float rp = ws.norms[1] > 0.f ? greg * inv_b / ws.norms[1] : 0.f;
+  const float rn = ws.norms[2] > 0.f ? greg * inv_b / ws.norms[2] : 0.f;
+  for (int64_t s = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; s < 3 * B; s += (int64_t)gridDim.x * GPB) {
+    const bool is_user = s < B;
+    const uint64_t* keys = is_user ? ws.keys_u : ws.keys_i;
+    const int64_t k = is_user ? s : s - B, cnt = is_user ? B : 2 * B;
+    const uint64_t row = keys[k] >> 20;
+    if (k > 0 && (keys[k - 1] >> 20) == row) continue;  // not the first slot of its row's run
+    for (int q = q0; q < d4; q += LPR) {
+      if (is_user) {
+        float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), r4 = g4;
+        for (int64_t j = k; j < cnt && (keys[j] >> 20) == row; ++j) {
+          const int64_t t = (int64_t)(keys[j] & SLOT);
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          g4 = f4_add(g4, f4_add(f4_scale(g, ld4(I, pp[t], ldi, q)), f4_scale(-g, ld4(I, nn[t], ldi, q))));
+          if (Ue) r4 = f4_add(r4, f4_scale(ru, ld4(Ue, (int64_t)row, ldue, q)));
+        }
+        if (dU) { float4* o = reinterpret_cast<float4*>(dU + (int64_t)row * lddu) + q; *o = f4_add(*o, g4); }
+        if (Ue && dUe) { float4* o = reinterpret_cast<float4*>(dUe + (int64_t)row * lddue) + q; *o = f4_add(*o, r4); }
+      } else {
+        float4 gp = make_float4(0.f, 0.f, 0.f, 0.f), gn = gp, rp4 = gp, rn4 = gp;
+        for (int64_t j = k; j < cnt && (keys[j] >> 20) == row; ++j) {
+          const int64_t sl = (int64_t)(keys[j] & SLOT);
+          const bool mp = sl < B;
+          const int64_t t = mp ? sl : sl - B;
+          const float g = bpr_coef(ws, t, B, gamma, gmf);
+          const float4 xu = ld4(U, uu[t], ldu, q);
+          if (mp) {
+            gp = f4_add(gp, f4_scale(g, xu));
+            if (Ie) rp4 = f4_add(rp4, f4_scale(rp, ld4(Ie, (int64_t)row, ldie, q)));
+          } else {
+            gn = f4_add(gn, f4_scale(-g, xu));
+            if (Ie) rn4 = f4_add(rn4, f4_scale(rn, ld4(Ie, (int64_t)row, ldie, q)));
+          }
+        }
+        if (dI) { float4* o = reinterpret_cast<float4*>(dI + (int64_t)row * lddi) + q; *o = f4_add(*o, f4_add(gp, gn)); }
+        if (Ie && dIe) {
+          float4* o = reinterpret_cast<float4*>(dIe + (int64_t)row * lddie) + q;
+          *o = f4_add(*o, f4_add(rp4, rn4));
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // bf16 tables (BASELINE config 5): rows of d bf16, LPR = d/8 lanes x 16 B; fp32 arithmetic.
 // Same workspace / reduce kernel / coefficients as the fp32 path.
@@ -554,7 +667,14 @@ static int bpr_bwd_impl(const float* d_U, int64_t ldu, const float* d_I, int64_t
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   BprWS w = bpr_ws(d_workspace, B);
   // gradient tables share the leading dimension of their forward tables
-  if (deterministic) {
+  if (deterministic && w.keys_u) {
+    hipLaunchKernelGGL(bpr_det_sort_kernel, dim3(2), dim3(1024), 0, s, d_u, d_p, d_n, B, w);
+    FR_LAUNCH_CHECK();
+    const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(3 * B, 256 / LPR), 4096);
+    hipLaunchKernelGGL(bpr_bwd_det_sorted_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
+                       ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,
+                       ldu, d_dI, ldi, d_dUe, ldue, d_dIe, ldie, w);
+  } else if (deterministic) {
     const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(3 * B, 256 / LPR), 4096);
     hipLaunchKernelGGL(bpr_bwd_det_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue,
                        ldue, d_Ie, ldie, d_u, d_p, d_n, B, d / 4, gamma, g_mf, g_reg, d_gscale, d_dU,

@@ -101,10 +101,11 @@ __global__ __launch_bounds__(256) void rank_metrics_kernel(const float* __restri
     tie |= !(m < prev);  // equal to the previous round's value (or a NaN): tie order matters
     prev = m;
   }
+  const bool any_nan = __ballot(nan) != 0;  // every lane votes (a ballot under lane == 0 sees lane 0 only)
   if (lane == 0) {
     hits[u] = hit;
     auc[u] = auc_u;
-    flags[u] = (uint8_t)((tie || __ballot(nan) != 0) ? 1 : 0);
+    flags[u] = (uint8_t)((tie || any_nan) ? 1 : 0);
   }
 }
 

@@ -781,6 +781,92 @@ extern "C" int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_
   return FR_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Scatter form of the sparse upstream (fr_spmm_scatter_upstream), for a SYMMETRIC adjacency:
+// Y2 = alpha A X + beta1 gate(X) with X non-zero only at the listed rows.  Since A[c][r] = A[r][c],
+// row r's contribution to every output row c is on r's own CSR row, so the work is proportional to
+// the listed rows' degrees instead of a scan of every edge:
+//   1. every row of Y2 = beta1 X[r] where mask[r] != 0, else 0 (the dense write the output needs);
+//   2. one wave per listed occurrence; the first occurrence of a row claims it by clearing its bit
+//      in the bitmask, then adds alpha A[r][c] X[r] to Y2[c] for each edge of row r, lane = column
+//      (one 256-B float-atomic wave instruction per edge).
+// Run-to-run variable summation order (float atomics): the non-deterministic mode's UI backward.
+__global__ __launch_bounds__(256) void scatter_init_kernel(int64_t n_rows, const uint8_t* __restrict__ mask,
+                                                           const float4* __restrict__ X, int64_t ldx4, Tab Y,
+                                                           int64_t split, float beta1) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_rows * 16; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i >> 4;
+    const int q = (int)(i & 15);
+    const float4 v = mask[r] ? f4_scale(beta1, X[r * ldx4 + q]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<float4*>(const_cast<float*>(tab_row(Y, r, split)))[q] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_edges_kernel(const int64_t* __restrict__ rowptr,
+                                                            const int32_t* __restrict__ col,
+                                                            const float* __restrict__ val, RowList rl, int64_t total,
+                                                            uint32_t* __restrict__ bits, const float* __restrict__ X,
+                                                            int64_t ldx, Tab Y, int64_t split, float alpha) {
+  const int lane = threadIdx.x & 63;
+  const int64_t idx0 = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (idx0 >= total) return;
+  int64_t idx = idx0;
+  int seg = 0;
+  while (idx >= rl.n[seg]) idx -= rl.n[seg++];
+  if (rl.ids[seg][idx] < 0) return;
+  const int64_t row = rl.ids[seg][idx] + rl.off[seg];
+  uint32_t old = 0;
+  if (lane == 0) old = atomicAnd(bits + (row >> 5), ~(1u << (row & 31)));
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (!((old >> (row & 31)) & 1u)) return;  // an earlier occurrence owns the row
+  const float x = alpha * X[row * ldx + lane];
+  const int64_t rs = rowptr[row], re = rowptr[row + 1];
+  for (int64_t e = rs; e < re; e += 4) {
+    int c[4];
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = e + k < re ? col[e + k] : -1;
+      v[k] = e + k < re ? val[e + k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c[k] >= 0) atomicAdd(const_cast<float*>(tab_row(Y, c[k], split)) + lane, v[k] * x);
+  }
+}
+
+extern "C" int fr_spmm_scatter_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                        int64_t n_rows, const uint8_t* d_mask, uint32_t* d_bits,
+                                        const fr_rowlist* rows, const float* d_X, int64_t ldx, int64_t split,
+                                        const fr_tab* Y2, float alpha, float beta1, void* stream) {
+  FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX, "n_rows out of range");
+  if (n_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && d_col && d_val && d_mask && d_bits && rows && d_X && Y2 && Y2->lo, "null operand");
+  FR_REQUIRE(ldx >= 64 && ldx % 4 == 0 && fr::aligned16(d_X) && tab_ok(Y2, 64),
+             "X / Y2 must be 16-B aligned fp32 [*, 64] tables");
+  FR_REQUIRE(!(tab_touches(Y2, d_X)), "Y2 must not alias X");
+  RowList rl{};
+  int64_t total = 0;
+  for (int k = 0; k < 3; ++k) {
+    FR_REQUIRE(rows->n[k] >= 0 && (rows->n[k] == 0 || rows->ids[k]), "bad row segment");
+    rl.ids[k] = rows->ids[k];
+    rl.n[k] = rows->n[k];
+    rl.off[k] = rows->off[k];
+    total += rows->n[k];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Tab Y = host_tab(Y2);
+  const int64_t blocks = std::min<int64_t>(fr::ceil_div(n_rows * 16, (int64_t)256), (int64_t)fr::kNumCU * 8);
+  hipLaunchKernelGGL(scatter_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_rows, d_mask,
+                     reinterpret_cast<const float4*>(d_X), ldx / 4, Y, split, beta1);
+  FR_LAUNCH_CHECK();
+  if (total == 0) return FR_OK;
+  hipLaunchKernelGGL(scatter_edges_kernel, dim3((unsigned)fr::ceil_div(total, (int64_t)4)), dim3(256), 0, s,
+                     d_rowptr, d_col, d_val, rl, total, d_bits, d_X, ldx, Y, split, alpha);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
 extern "C" int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
                                             int64_t n_rows, int64_t n_cols, const uint32_t* d_bits, const float* d_X,
                                             int64_t ldx, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,

@@ -13,6 +13,10 @@ Fixtures (all on the seeded synthetic 'tiny' dataset of FoodRec/utils/synthetic.
   train_<M>.npz     per-epoch loss trace + final valid/test metrics of Trainer.fit
   ops.npz           correlation_distance / CL_loss / BPRLoss / EmbLoss values + grads
   metrics.npz       metrics_by_user / get_auc_fast on fixed rankings
+  train_CIKM_Model_spread.npz  HealthRec's train trace + test metrics under torch CPU thread counts
+                    1, 2, 3, 8, under 1-ulp random perturbations of the encoder layers' outputs and
+                    under +-4e-7*max noise there (the reference's own spread over equally valid fp32
+                    roundings)
   train_mg_LightGCN.npz  the same, trained by the reference's mirror-gradient trainer (--mg,
                     trainer.py:195-212; mg.yaml resolved to alpha1=1, alpha2=0.1, beta=3)
 
@@ -24,7 +28,7 @@ the reference's format and read by the reference's own loader; only small slices
     parameters, sampled rows of the large ones; init and after K Adam steps: sampled parameter rows
 
 Re-generate a subset:  python oracle/gen_golden.py --only train=CIKM_Model,mg,wide
-(sections: model, stream, train[=M1+M2], mg, ops, metrics, wide[=M1+M2])
+(sections: model, stream, train[=M1+M2], spread, mg, ops, metrics, wide[=M1+M2])
 """
 from __future__ import annotations
 
@@ -180,6 +184,9 @@ def main(argv=None):
     for name in (want["train"] or ("LightGCN", "BPRMF", "PRICAI_ModelX", "CIKM_Model")) if "train" in want else ():
         train_golden(f"train_{name}.npz", make_config(name, models[name]), name, FoodData, init_seed, get_model,
                      Trainer)
+    if "spread" in want:
+        train_spread("train_CIKM_Model_spread.npz", make_config("CIKM_Model", models["CIKM_Model"]), "CIKM_Model",
+                     FoodData, init_seed, get_model, Trainer)
     if "mg" in want:
         # the reference's --mg cascade (configurator.py:64-86 adds configs/mg.yaml; quick_start.py:54-88
         # takes the first value of each hyper-parameter list) and Trainer(config, model, mg=True)
@@ -217,6 +224,62 @@ def stream_golden(make_config, FoodData, init_seed, get_model, TrainDataLoader, 
     np.savez_compressed(os.path.join(OUT, "stream.npz"), **st)
     print("stream", st["ep0/u"][:8], st["ep0/n"][:8])
 
+
+
+def train_spread(fname, cfg, name, FoodData, init_seed, get_model, Trainer, threads=(1, 2, 3, 8),
+                 ulp_seeds=(1, 2, 3, 4, 5, 6), noise_seeds=tuple(range(1, 13))):
+    """The reference's own sensitivity to fp32 rounding: the same Trainer.fit (same seed, data and
+    batches) (a) under several torch CPU thread counts, whose reductions order their partial sums
+    differently, and (b) with every Transformer encoder layer's output moved by ONE ulp, up or down
+    at random (a seeded generator of its own; gradients unchanged) -- the size of the difference
+    between any two correct fp32 implementations of the layer -- and (c) by uniform noise of
+    +-4e-7 * max|output|, the fused MI355X layer's measured distance from float64 (tools/diag_enc.py).
+    Stores every run's loss trace and final test metrics."""
+    import torch
+    traces, tests, kinds = [], [], []
+    layer_cls = torch.nn.TransformerEncoderLayer
+    orig_forward = layer_cls.forward
+
+    def ulp_forward(gen):
+        def fwd(self, *a, **kw):
+            out = orig_forward(self, *a, **kw)
+            with torch.no_grad():  # every output element moved by one ulp up or down (own generator)
+                up = torch.rand(out.shape, generator=gen) < 0.5
+                to = torch.where(up, torch.full_like(out, float("inf")), torch.full_like(out, float("-inf")))
+                delta = torch.nextafter(out, to) - out
+            return out + delta
+        return fwd
+
+    def noise_forward(gen):
+        def fwd(self, *a, **kw):
+            out = orig_forward(self, *a, **kw)
+            with torch.no_grad():  # uniform +-4e-7 * max|out|: the fused kernel's measured error vs float64
+                eps = 4e-7 * float(out.abs().max())
+                delta = (torch.rand(out.shape, generator=gen) * 2 - 1) * eps
+            return out + delta
+        return fwd
+
+    runs = ([("threads", t) for t in threads] + [("ulp", k) for k in ulp_seeds] +
+            [("noise", k) for k in noise_seeds])
+    for kind, t in runs:
+        torch.set_num_threads(t if kind == "threads" else 4)
+        if kind == "ulp":
+            layer_cls.forward = ulp_forward(torch.Generator().manual_seed(int(t)))
+        elif kind == "noise":
+            layer_cls.forward = noise_forward(torch.Generator().manual_seed(1000 + int(t)))
+        data = FoodData(cfg)
+        init_seed(cfg["seed"])
+        model = get_model(name)(cfg, data)
+        tr = Trainer(cfg, model)
+        bv, bvr, btr = tr.fit(data, hyper_tuple=(999,), saved=True, verbose=False)
+        layer_cls.forward = orig_forward
+        traces.append([tr.train_loss_dict[e] for e in sorted(tr.train_loss_dict)])
+        tests.append(list(btr.values()))
+        kinds.append(f"{kind}={t}")
+        print("spread", name, kind, t, traces[-1], list(btr.values()))
+    torch.set_num_threads(4)
+    np.savez_compressed(os.path.join(OUT, fname), runs=np.array(kinds), train_loss=np.array(traces),
+                        test_keys=np.array(list(btr.keys())), test=np.array(tests))
 
 
 def train_golden(fname, cfg, name, FoodData, init_seed, get_model, Trainer, mg=False):

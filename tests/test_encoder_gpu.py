@@ -130,3 +130,70 @@ def test_encoder_deterministic(cuda):
     assert torch.equal(a[0], b[0])
     for pa, pb in zip([a[1]] + a[2], [b[1]] + b[2]):
         assert torch.equal(pa.grad, pb.grad)
+
+
+@pytest.mark.parametrize("NS,L", [(474, 20), (1027, 20), (7, 20), (333, 16), (101, 8), (50, 5), (33, 10), (9, 4)])
+def test_encoder_writes_stay_in_bounds(cuda, NS, L):
+    """Every buffer of fr_encoder_fwd / fr_encoder_bwd sits between guard zones of a sentinel value:
+    the kernels write only inside their outputs (no row of a partial workgroup or padding tile lands
+    past an output's end or in front of it) and never write their inputs or the saved tensors."""
+    import ctypes
+
+    from FoodRec.engine import native, ops
+    lib = native.lib()
+    G = 4096
+    SENT = 12345.0
+    T = NS * L
+    gen = torch.Generator().manual_seed(NS + L)
+
+    def guarded(n, fill=None):
+        buf = torch.full((n + 2 * G,), SENT, dtype=torch.float32, device=cuda)
+        if fill is not None:
+            buf[G:G + n] = fill.reshape(-1).to(cuda)
+        return buf, buf[G:G + n]
+
+    def intact(buf, n):
+        return bool((buf[:G] == SENT).all()) and bool((buf[G + n:] == SENT).all())
+
+    x_b, x = guarded(T * 64, torch.randn(T * 64, generator=gen))
+    pad = torch.rand(NS, L, generator=gen) < 0.3
+    pad[:, 0] = False
+    m_b, m = guarded(T, torch.zeros(NS, L).masked_fill(pad, float("-inf")))
+    params = [p.float() for p in _params(gen)]
+    pbufs = [guarded(p.numel(), p) for p in params]
+    pp = (ctypes.c_void_p * 12)(*[v.data_ptr() for _, v in pbufs])
+    eps = (ctypes.c_float * 2)(1e-5, 1e-5)
+    drop = (ctypes.c_float * 4)(0.1, 0.1, 0.1, 0.1)
+    counter = torch.zeros(1, dtype=torch.int64, device=cuda)
+    seed_used = torch.zeros(1, dtype=torch.int64, device=cuda)
+    sizes = {"out": T * 64, "qkv": T * 192, "ctx": T * 64, "y1": T * 64, "fact": T * 256,
+             "dact": int(lib.fr_encoder_dact_numel(NS, L)), "y2": T * 64, "st1": T * 2, "st2": T * 2}
+    outs = {k: guarded(n) for k, n in sizes.items()}
+    s = native.stream_of(x)
+    native.check(lib.fr_encoder_fwd(x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1, counter.data_ptr(),
+                                    seed_used.data_ptr(), *[outs[k][1].data_ptr() for k in sizes], s),
+                 "fr_encoder_fwd")
+    torch.cuda.synchronize()
+    for k, n in sizes.items():
+        assert intact(outs[k][0], n), f"forward wrote outside {k}"
+    snap = {k: v[0].clone() for k, v in outs.items()}
+    g_b, g = guarded(T * 64, torch.randn(T * 64, generator=gen))
+    g_snap = g_b.clone()
+    dx_b, dx = guarded(T * 64)
+    gr_b, gr = guarded(int(lib.fr_encoder_grad_numel()))
+    nparts = int(lib.fr_encoder_partials(NS, L))
+    pa_b, pa = guarded(nparts)
+    native.check(lib.fr_encoder_bwd(g.data_ptr(), x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1,
+                                    seed_used.data_ptr(), *[outs[k][1].data_ptr() for k in list(sizes)[1:]],
+                                    dx.data_ptr(), gr.data_ptr(), pa.data_ptr(), nparts, s), "fr_encoder_bwd")
+    torch.cuda.synchronize()
+    assert intact(dx_b, T * 64), "backward wrote outside dx"
+    assert intact(gr_b, int(lib.fr_encoder_grad_numel())), "backward wrote outside the gradient"
+    assert intact(pa_b, nparts), "backward wrote outside the partials"
+    assert torch.equal(g_b, g_snap), "backward wrote its upstream gradient"
+    for k in sizes:
+        assert torch.equal(outs[k][0], snap[k]), f"backward wrote the saved {k}"
+    for (b, v), p in zip(pbufs, params):
+        assert intact(b, p.numel()) and torch.equal(v.cpu(), p.reshape(-1)), "a parameter was written"
+    assert intact(x_b, T * 64) and intact(m_b, T)
+    assert torch.isfinite(dx).all() and torch.isfinite(gr).all()

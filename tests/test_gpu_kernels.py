@@ -3,7 +3,8 @@
 Tolerances (fp32 kernels vs fp64 or torch-CPU fp32 references):
   SpMM / propagation   : |err| <= 2e-5 * (|A||X| row scale) + 1e-6   (fp32 accumulate, reordered sum)
   BPR / EmbLoss values : rel 1e-5;  gradients rel 1e-4 (atomic scatter order)
-  dCor                 : rel 2e-4 on the value, 2e-3 on gradients (reference centres in fp32)
+  dCor                 : value and gradients no further from float64 than the reference's own fp32
+                         arithmetic is (the same restatement run in fp32), or within 1e-5 / 1e-4 * max
   InfoNCE              : rel 1e-5 value, 1e-4 gradients
   Adam                 : exp_avg/exp_avg_sq bit-identical to torch.optim.Adam (CPU); params
                          within 4 ulp after 3 steps (torch-CPU addcdiv rounding on ~0.1% of elements)
@@ -291,13 +292,22 @@ def test_dcor_three_views(cuda, n):
     pairs = [(0, 1), (0, 2), (2, 1)]  # (image,text), (image,ingre), (ingre,text) as pricai_modelx.py:263
     ref = sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
     (1.7 * ref.sum()).backward()
+    # the reference's own precision: the same restatement in fp32 (pricai_modelx.py:409-437 runs in
+    # fp32 on the CPU), measured against float64
+    v32 = [v.detach().float().requires_grad_(True) for v in views]
+    ref32 = sum(O.correlation_distance(v32[a], v32[b]) for a, b in pairs)
+    (1.7 * ref32.sum()).backward()
     dv = [v.detach().float().to(cuda).requires_grad_(True) for v in views]
     got = ops.dcor_loss(dv, pairs)
     (1.7 * got.sum()).backward()
-    assert abs(got.item() - ref.item()) <= 2e-4 * abs(ref.item())
-    for v, w in zip(views, dv):
-        gr, gg = v.grad.numpy(), w.grad.cpu().numpy()
-        assert np.abs(gg - gr).max() <= 2e-3 * np.abs(gr).max() + 1e-7
+    err_val, err32_val = abs(got.item() - ref.item()), abs(ref32.item() - ref.item())
+    # value: no further from float64 than the fp32 reference, or within 1e-5 relative
+    assert err_val <= max(err32_val, 1e-5 * abs(ref.item())), (err_val, err32_val)
+    for v, v3, w in zip(views, v32, dv):
+        gr, g3, gg = v.grad.numpy(), v3.grad.numpy(), w.grad.cpu().numpy()
+        err, err32 = np.abs(gg - gr).max(), np.abs(g3 - gr).max()
+        # gradients: no further from float64 than the fp32 reference is, or within 1e-4 * max
+        assert err <= max(err32, 1e-4 * np.abs(gr).max()) + 1e-9, (err, err32, np.abs(gr).max())
 
 
 @pytest.mark.parametrize("b", [512, 37])
@@ -724,6 +734,41 @@ def test_spmm_sparse_upstream(cuda, frac):
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
     ops.rows_mark(mask, [(marked, 0)], 0, bits=bits)
     assert int(mask.sum()) == 0 and int(bits.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("frac", [0.02, 0.3])
+def test_spmm_scatter_upstream(cuda, frac):
+    """fr_spmm_scatter_upstream (scatter from the listed rows' own CSR rows, symmetric A) against
+    fr_spmm_csr over the zero-filled upstream: listed rows with duplicates across three segments and
+    a negative id (no row), X garbage (NaN) outside them, heavy rows, split output; the listed rows'
+    bits are clear afterwards.  Float-atomic order: fp32 rounding."""
+    from FoodRec.engine import ops
+    n, d, split = 1500, 64, 600
+    r, c = _graph(n, n, 8, heavy=[(3, 1400), (700, 900), (11, 129)], seed=29)
+    adj = _adj(n, r, c, cuda, chunk=128)
+    assert adj.symmetric
+    g = torch.Generator().manual_seed(int(frac * 100) + 1)
+    a = torch.randint(0, split, (max(1, int(frac * n)),), generator=g).to(cuda)
+    b = torch.randint(0, n - split, (max(1, int(frac * n)),), generator=g).to(cuda)
+    # third segment: duplicates of the second, a negative id (no row) and the heavy row 700
+    rows = [(a, 0), (b, split), (torch.cat([b[:5], torch.tensor([-1, 700 - split], device=cuda)]), split)]
+    mask = torch.zeros(n, dtype=torch.uint8, device=cuda)
+    bits = torch.zeros((n + 31) // 32, dtype=torch.int32, device=cuda)
+    X = torch.full((n, d), float("nan"), device=cuda)
+    ops.rows_mark(mask, rows, 1, zero=X, bits=bits)
+    keep = mask.bool()
+    X[keep] = torch.randn(int(keep.sum()), d, device=cuda)
+    Xz = torch.where(keep.unsqueeze(1), X, torch.zeros_like(X))
+    ref = torch.empty(n, d, device=cuda)
+    ops.spmm_launch(adj, Xz, Y2=ref, alpha=0.5, A1=Xz, beta1=0.5)
+    lo, hi = torch.full((split, d), 7.0, device=cuda), torch.full((n - split, d), 7.0, device=cuda)
+    ops.spmm_scatter_upstream(adj, mask, bits, rows, X, lo, hi, split, alpha=0.5, beta1=0.5)
+    got = torch.cat([lo, hi])
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    assert int(bits.abs().sum()) == 0  # claimed rows cleared their bits
+    ops.rows_mark(mask, rows, 0, bits=bits)
+    assert int(mask.sum()) == 0
 
 
 def test_healthrec_graph_bpr_matches_unfused(cuda):
