@@ -64,6 +64,8 @@ def _args():
                     help="skip BASELINE config 5 (d=256 bf16 tables, full-sort top-k on MFMA)")
     ap.add_argument("--no-config1", action="store_true",
                     help="skip BASELINE config 1 (BPRMF on Allrecipes-shape data, GPU step + CPU oracle)")
+    ap.add_argument("--no-eval", action="store_true",
+                    help="skip the per-epoch evaluation leg (68,768 test users ranked on the device)")
     return ap.parse_args()
 
 
@@ -348,6 +350,9 @@ def main():
     c1 = None
     if world == 1 and not args.no_config1:
         c1 = config1(device, cpu=not args.no_cpu_baseline)
+    ev = None
+    if world == 1 and not args.no_eval:
+        ev = eval_leg(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -384,7 +389,7 @@ def main():
                                    "note": "value and ms_per_step include epoch_sampling.ms_per_epoch (the median "
                                            "of three epochs' sampling) / steps_per_epoch per step"},
                 "spmm": spmm, "config1_bprmf_allrecipes": c1, "config3_clussl_foodcom": c3, "config4_10m": c4,
-                "config5_10m_bf16": c5, "kernels": kernels, "cpu_baseline": cpu}
+                "config5_10m_bf16": c5, "eval_healthrec_allrecipes": ev, "kernels": kernels, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1 or dp1:
         dist.destroy_process_group()
@@ -938,6 +943,102 @@ def config1(device, steps=50, warmup=5, cpu=True, cpu_steps=20):
         out["cpu_baseline"] = {"value": round(B / cdt, 1), "unit": "triples/s", "cores": threads, "kind": "port",
                                "sample": f"{cpu_steps} BPRMF steps (B={B}) of the torch-CPU oracle after 1 warm-up",
                                "ms_per_step": round(cdt * 1e3, 2)}
+    return out
+
+
+def _fast_negatives(rng, user_ids, train_keys, I, neg=500, over=640):
+    """Bench-only evaluation candidates: ``neg`` distinct uniform item draws per user excluding its
+    train items (the synthetic generator's popularity^0.7 lists take ~1 min at Allrecipes shape; the
+    ranking's cost depends on the list lengths, not on which items they hold)."""
+    import numpy as np
+    out = np.empty((len(user_ids), neg), np.int64)
+    for c0 in range(0, len(user_ids), 8192):
+        uu = np.asarray(user_ids[c0:c0 + 8192], np.int64)
+        cand = np.sort(rng.integers(0, I, size=(len(uu), over)), axis=1)
+        key = uu[:, None] * I + cand
+        pos = np.searchsorted(train_keys, key)
+        ok = train_keys[np.minimum(pos, len(train_keys) - 1)] != key
+        ok[:, 1:] &= cand[:, 1:] != cand[:, :-1]
+        rank = np.cumsum(ok, axis=1)
+        assert np.all(rank[:, -1] >= neg), "increase `over`"
+        sel = ok & (rank <= neg)
+        rows = cand[sel].reshape(len(uu), neg)
+        out[c0:c0 + len(uu)] = rng.permuted(rows, axis=1)
+    return out
+
+
+def eval_leg(device, host_users=3000, reps=3):
+    """HealthRec's per-epoch evaluation at Allrecipes shape (EvalByUserDataloader + the trainer's
+    _valid_by_user_epoch, reference trainer.py:231-282,49-69, dataloader.py:228-302): all 68,768 test
+    users x (|test pos| + 500 negatives) scored on the device and ranked by fr_rank_metrics, beside
+    the reference-style per-user numpy loop (argsort / metrics_by_user / get_auc_fast) timed on a
+    sample of users and checked bit-equal to the device metrics on that sample."""
+    import numpy as np
+    import torch
+    from FoodRec.common.trainer import Trainer, metrics_from_hits, rank_user_host
+    from FoodRec.engine import ops
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.dataset import FoodData
+    from FoodRec.utils.synthetic import make_synthetic
+    from FoodRec.utils.utils import get_model, init_seed
+    ds = make_synthetic("allrecipes", 0, negatives=False)
+    I = ds.n_items
+    train_keys = np.unique(ds.train[:, 0] * I + ds.train[:, 1])
+    rng = np.random.default_rng(7)
+    ds.test_neg = _fast_negatives(rng, np.arange(ds.n_users), train_keys, I)
+    ds.valid_neg = _fast_negatives(rng, ds.valid_users, train_keys, I)
+    data = FoodData.from_synthetic(ds)
+    cfg = Config("CIKM_Model", "Allrecipes", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
+                                             "ckp_root": "/tmp/frckp/"})
+    cfg["device"] = device
+    data.args_config = cfg
+    init_seed(999)
+    model = get_model("CIKM_Model")(cfg, data).to(device)
+    tr = Trainer(cfg, model)
+    model.eval()
+    neg_num = cfg["neg_sample_num"]
+    out = {}
+    for name, is_test in (("test", True), ("valid", False)):
+        tr._valid_by_user_epoch(is_test=is_test)  # warm-up (allocations; the in-place positive removal)
+        torch.cuda.synchronize()
+        walls = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            tr._valid_by_user_epoch(is_test=is_test)
+            walls.append(time.perf_counter() - t0)
+        # the same call's parts
+        t0 = time.perf_counter()
+        users, items, lens, npos = tr._candidates(is_test)
+        t1 = time.perf_counter()
+        sc = tr._score(users, items, on_device=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        hits, aucc, flags = ops.rank_metrics(sc, lens, npos, 20)
+        res = metrics_from_hits(hits, lens, npos, aucc, neg_num)
+        t3 = time.perf_counter()
+        host = sc.cpu().numpy()
+        off = np.zeros(len(lens) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        nh = min(host_users, len(lens))
+        h0 = time.perf_counter()
+        ref = np.stack([rank_user_host(host[off[k]:off[k + 1]].copy(), int(npos[k]), neg_num) for k in range(nh)])
+        h1 = time.perf_counter()
+        ok = [k for k in range(nh) if not flags[k]]
+        host_loop_s = (h1 - h0) / nh * len(lens)
+        out[name] = {"users": int(len(lens)), "candidates": int(len(items)),
+                     "wall_s": round(sorted(walls)[len(walls) // 2], 4),
+                     "parts_s": {"candidates_host": round(t1 - t0, 4), "score_device": round(t2 - t1, 4),
+                                 "rank_device_and_metrics": round(t3 - t2, 4)},
+                     "tie_users_routed_to_host": int(flags.sum()),
+                     "reference_style_host_loop_s": round(host_loop_s, 3),
+                     "host_loop_sample_users": nh,
+                     "device_vs_host_loop_speedup_rank": round(host_loop_s / max(t3 - t2, 1e-9), 1),
+                     "metrics_bit_equal_on_sample": bool(np.array_equal(res[ok], ref[ok]))}
+    del tr, model
+    torch.cuda.empty_cache()
+    out["note"] = ("wall_s = Trainer._valid_by_user_epoch (median of %d): lazy-row flush + candidate lists + "
+                   "device scoring + fr_rank_metrics + float64 metrics; the reference-style loop is timed on "
+                   "%d users and scaled to all users" % (reps, host_users))
     return out
 
 
