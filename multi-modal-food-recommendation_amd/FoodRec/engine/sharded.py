@@ -285,21 +285,28 @@ def _neighbour_items(g: ShardedGraph, loc: torch.Tensor) -> torch.Tensor:
     return g.A_ui.col[pos].to(torch.int64)
 
 
-class _ShardedPropagateRows(torch.autograd.Function):
+class _ShardedRowsStep(torch.autograd.Function):
     """_ShardedPropagate (L = 2) for a loss that reads the propagated tables at the batch rows only
-    (the rows form of ops.propagate_rows, single-GPU config 4).  The item table of layer 1 is needed
-    only at S = the items adjacent to the batch users (for their layer-2 rows) plus the batch items
-    (for theirs), and the first backward layer's item rows are non-zero only on the first part of S:
+    (the rows form of ops.propagate_rows, single-GPU config 4), with the owner gathers of the batch
+    users' propagated and ego rows folded in.  The item table of layer 1 is needed only at S = the
+    items adjacent to the batch users (for their layer-2 rows) plus the batch items (for theirs),
+    and the first backward layer's item rows are non-zero only on the first part of S:
       forward   S agreed on by every rank (an all-reduce of per-item flags, then the same nonzero
                 list everywhere); layer-1 item partial at S only (row list), its |S| rows all-reduced
                 (|S| x d instead of I x d); the user layer 1 in full (local); layer 2 at this rank's
                 batch users (row list, users owned elsewhere carry id -1) and at the batch items (row
-                list on the transpose slice, the 2B partial rows all-reduced);
-      backward  the first layer from the sparse upstream gradients (users: A_ui at the batch items'
-                columns; items: A_iu at this rank's batch users' columns, all-reduced at S only), the
-                second in full (item partial per item-row block, all-reduced as before).
+                list on the transpose slice, the 2B partial rows all-reduced); the batch users'
+                propagated and ego rows gathered from their owners by ONE [2B x d] all-reduce;
+      backward  the batch users' upstream stays B rows: the first layer from the sparse upstream
+                gradients (users: A_ui at the batch items' columns; items: A_iu at this rank's batch
+                users' columns, all-reduced at S only), the second in full (item partial per item-row
+                block, all-reduced as before); the user rows' own terms (g / 3 and the ego rows'
+                gradient) are added at the batch rows after each user SpMM, so no dense
+                [n_local x d] upstream table is zero-filled, read as an epilogue addend, or summed
+                with a second dense ego gradient by autograd.
     Collectives per step: one all-reduce of I x d (the last backward layer, in blocks) + |S| x d
-    twice + 2B x d + the flags (I floats) + 2 owner gathers.  Results valid at the batch rows only."""
+    twice + 2B x d twice + the flags (I floats).  Returns (propagated user rows [B, d], ego user
+    rows [B, d], propagated item table valid at the batch items).  Float-atomic row additions."""
 
     @staticmethod
     def forward(ctx, ego_u, ego_i, g: ShardedGraph, group, loc, p, n):
@@ -330,42 +337,62 @@ class _ShardedPropagateRows(torch.autograd.Function):
         ops.spmm_ex(g.A_iu, E1u, Y1=pi2, rows=[(p, 0), (n, 0)], region="spmm_rows")
         part2 = pi2.index_select(0, pn)
         _all_reduce(part2, group)
+        del E1u
         out_i = torch.empty_like(ego_i)                            # valid at the batch items
         out_i.index_copy_(0, pn, (ego_i.index_select(0, pn) + E1i.index_select(0, pn) + part2) * inv)
+        # owner gathers: [out_u[loc] ; ego_u[loc]], rows owned elsewhere zero, one all-reduce
+        B = loc.numel()
+        safe = loc.clamp(min=0)
+        rows = torch.cat([out_u.index_select(0, safe), ego_u.index_select(0, safe)])
+        rows.mul_((loc >= 0).to(rows.dtype).repeat(2).unsqueeze(1))
+        _all_reduce(rows, group)
         ctx.save_for_backward(loc, p, n, S)
-        return out_u, out_i
+        ctx.n_local = ego_u.shape[0]
+        return rows[:B], rows[B:], out_i
 
     @staticmethod
-    def backward(ctx, g_u, g_i):
+    def backward(ctx, g_ub, g_eb, g_i):
         g, group = ctx.g, ctx.group
         loc, p, n, S = ctx.saved_tensors
         inv = 1.0 / 3.0
         dev = loc.device
-        g_u = g_u.contiguous() if g_u is not None else torch.zeros(g.n_local, 64, device=dev)
+        B = loc.numel()
+        own = (loc >= 0).to(torch.float32).unsqueeze(1)
+        safe = loc.clamp(min=0)
+        g_ub = g_ub.contiguous() * own if g_ub is not None else torch.zeros(B, 64, device=dev)
+        g_eb = g_eb.contiguous() * own if g_eb is not None else torch.zeros(B, 64, device=dev)
         g_i = g_i.contiguous() if g_i is not None else torch.zeros(g.n_items, 64, device=dev)
         # items of the first backward layer: A_iu at this rank's batch users (non-zero inside S only),
-        # all-reduced at S
+        # all-reduced at S.  The users' upstream rows go into a persistent table read only at the
+        # marked rows (those rows zeroed by the mark, then summed: a user may occur twice)
         mu, bu = _marks(g, "users", g.n_local, dev)
-        ops.rows_mark(mu, [(loc, 0)], 1, bits=bu)
+        Gu = g.__dict__.get("_g_rows")
+        if Gu is None or Gu.device != dev:
+            Gu = torch.empty(g.n_local, 64, device=dev)
+            g.__dict__["_g_rows"] = Gu
+        ops.rows_mark(mu, [(loc, 0)], 1, zero=Gu, bits=bu)
+        Gu.index_add_(0, safe, g_ub)                                 # rows owned elsewhere add 0 to an unread row
         piH = torch.empty_like(g_i)
-        ops.spmm_sparse_rect(g.A_iu, bu, g_u, piH, alpha=1.0)
+        ops.spmm_sparse_rect(g.A_iu, bu, Gu, piH, alpha=1.0)
         ops.rows_mark(mu, [(loc, 0)], 0, bits=bu)
         partH = piH.index_select(0, S)
         work = _all_reduce(partH, group, async_op=True)
-        # users of the first backward layer (local): A_ui at the batch items' columns
+        # users of the first backward layer (local): A_ui at the batch items' columns, + g / 3 at the rows
         mi, bi = _marks(g, "items", g.n_items, dev)
         ops.rows_mark(mi, [(p, 0), (n, 0)], 1, bits=bi)
-        Hu = torch.empty_like(g_u)
-        ops.spmm_sparse_rect(g.A_ui, bi, g_i, Hu, alpha=inv, A1=g_u, beta1=inv)
+        Hu = torch.empty(ctx.n_local, 64, device=dev)
+        ops.spmm_sparse_rect(g.A_ui, bi, g_i, Hu, alpha=inv)
         ops.rows_mark(mi, [(p, 0), (n, 0)], 0, bits=bi)
+        Hu.index_add_(0, safe, g_ub * inv)
         _wait([work])
         Hi = g_i * inv
         Hi.index_copy_(0, S, partH.mul_(inv).add_(Hi.index_select(0, S)))
-        # second layer in full
+        # second layer in full; the user rows' own terms (g / 3 + the ego rows' gradient) added after
         pi = piH
         works = _item_partial(g, Hu, pi, group)
-        d_u = torch.empty_like(g_u)
-        ops.spmm_launch(g.A_ui, Hi, Y2=d_u, alpha=1.0, A1=g_u, beta1=inv)
+        d_u = torch.empty(ctx.n_local, 64, device=dev)
+        ops.spmm_launch(g.A_ui, Hi, Y1=d_u)
+        d_u.index_add_(0, safe, g_ub * inv + g_eb)
         _wait(works)
         d_i = pi.add_(g_i, alpha=inv)
         return d_u, d_i, None, None, None, None, None
@@ -419,12 +446,12 @@ class ShardedLightGCN(nn.Module):
                 and not torch.cuda.is_current_stream_capturing()):
             # the loss reads the propagated tables at the batch rows only (rows form)
             p, n = p.to(torch.int64).contiguous(), n.to(torch.int64).contiguous()
-            out_u, out_i = _ShardedPropagateRows.apply(self.ego_u, self.ego_i, self.g, self.group,
-                                                       loc.contiguous(), p, n)
+            out_ub, ego_ub, out_i = _ShardedRowsStep.apply(self.ego_u, self.ego_i, self.g, self.group,
+                                                           loc.contiguous(), p, n)
         else:
             out_u, out_i = _ShardedPropagate.apply(self.ego_u, self.ego_i, self.g, self.L, self.group)
-        out_ub = _OwnerGather.apply(out_u, loc, self.group)
-        ego_ub = _OwnerGather.apply(self.ego_u, loc, self.group)
+            out_ub = _OwnerGather.apply(out_u, loc, self.group)
+            ego_ub = _OwnerGather.apply(self.ego_u, loc, self.group)
         B = u.numel()
         ar = torch.arange(B, device=u.device)
         # replicated item gradients must come out bit-identical on every rank: deterministic BPR

@@ -5,7 +5,7 @@ world_size ranks on ONE GPU (gloo over device tensors; RCCL refuses two ranks on
   python -m torch.distributed.run --nnodes=1 --nproc-per-node {2,4} --master-addr 127.0.0.1 \
       --master-port P tests/mp/sharded_worker.py
 
-The step must run the rows form (_ShardedPropagateRows: item-flag all-reduce, the |S| layer-1 rows,
+The step must run the rows form (_ShardedRowsStep: item-flag all-reduce, the |S| layer-1 rows,
 the 2B batch item rows, the item-row blocks of the last backward layer) -- counted below.
 
 Every rank compares, on a 20k-user graph:
@@ -33,13 +33,13 @@ def main():
     from FoodRec.engine import sharded
     from FoodRec.engine.sharded import ShardedGraph, ShardedLightGCN
     rows_calls = [0]
-    _apply = sharded._ShardedPropagateRows.apply
+    _apply = sharded._ShardedRowsStep.apply
 
     def counted(*a):
         rows_calls[0] += 1
         return _apply(*a)
 
-    sharded._ShardedPropagateRows.apply = staticmethod(counted)
+    sharded._ShardedRowsStep.apply = staticmethod(counted)
     from FoodRec.models.lightgcn_id import LightGCN_ID
     from FoodRec.utils.configurator import Config
     from FoodRec.utils.interaction_graph import InteractionGraph, synth_bipartite
