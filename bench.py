@@ -829,7 +829,7 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
            "model": "LightGCN_ID row-sharded (users in nnz-balanced blocks, items replicated), rows form",
            "collectives_per_step": "1 all-reduce of I x d fp32 (256 MB: the last backward layer's item partial, "
                                    "cut into item-row blocks) + the item flags (I floats) + 2 of the |S| layer-1 "
-                                   "item rows + 1 of the 2B batch item rows + 2 B x d owner gathers",
+                                   "item rows + 1 of the 2B batch item rows + 1 owner gather of the batch users' propagated and ego rows (2B x d)",
            "byte_model": "config4_bytes_rows (the single-GPU step's algorithmic bytes)",
            "local_params_rank0": P_local, "local_nnz_per_rank": [int(x.item()) for x in nnz_all],
            "steps_timed": steps, "step": out_steps}

@@ -33,16 +33,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int E = 64, HEADS = 2, HD = 32, FF = 256, QKV = 3 * E;
-constexpr int ROWS = 48;                            // token rows per workgroup (3 MFMA row tiles)
+constexpr int ROWS = 80;                            // token rows per workgroup (5 MFMA row tiles)
 constexpr int RT = ROWS / 16;
 constexpr int LD_E = E + 4, LD_QKV = QKV + 4, LD_FF = FF + 4;
-constexpr int FH = FF / 2, LD_FH = FH + 4;          // the backward's FF block, one column half at a time
-constexpr int NT = 256;                             // threads per workgroup: 4 waves, 1 per SIMD
-constexpr int NWAVE = NT / 64;
-// Two workgroups per CU (LDS <= 80 KB each): while one is in a VALU / LDS / memory phase (attention
-// softmax, LayerNorm, GELU, dropout hash, loads) the other's GEMM phase keeps the matrix pipes busy.
-// Wave w of a workgroup owns output column tiles by SIMD slot w and every row tile.
-constexpr int BUF_D = ROWS * LD_E;                  // LayerNorm scratch / ctx tile / attention scratch
+constexpr int NT = 512;                             // threads per workgroup: 8 waves, 2 per SIMD
+// Wave w owns output column tiles by its SIMD slot sg = w & 3 (as a 4-wave layout would) and, within
+// the SIMD, one of two row-tile ranges: hf = w >> 2 takes tiles [0, RT0) or [RT0, RT).  The two waves
+// of a SIMD share its MFMA pipe and hide each other's LDS / global / transcendental latency.
+constexpr int RT0 = (RT + 1) / 2;
+constexpr int BUF_D = 6400;                         // attention p'/ds buffers (2*G*H*L*L) and scratch
 
 // gradient partial layout (floats), identical to the flat gradient buffer fr_encoder_bwd writes
 constexpr int OFF_WIN = 0, OFF_BIN = OFF_WIN + QKV * E, OFF_WO = OFF_BIN + QKV, OFF_BO = OFF_WO + E * E,
@@ -287,12 +286,23 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[NA][NC]) {
     for (int c = 0; c < NC; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// weight-gradient partial  P[n][k] = sum_t Y[t][n] X[t][k] over the workgroup's rows: n-tiles
-// yc0.. of Y (LDS, ldy) and k-tiles xc0.. of X (LDS, ldx) -> partial rows pr0.., columns pc0.. (row
-// length K); NN x NK output tiles per wave.
+// this wave's row tiles: [0, RT0) for hf == 0, [RT0, RT) for hf == 1 (wave-uniform)
+#define FR_GEMM_XWT(NC, K, A, lda, W, c0, acc)                     \
+  do {                                                             \
+    if (hf == 0) gemm_xwt<NC, K, 0, RT0>(A, lda, W, c0, acc);      \
+    else gemm_xwt<NC, K, RT0, RT - RT0>(A, lda, W, c0, acc);       \
+  } while (0)
+#define FR_GEMM_YW(NC, N, KO, Y, ldy, W, c0, acc)                  \
+  do {                                                             \
+    if (hf == 0) gemm_yw<NC, N, KO, 0, RT0>(Y, ldy, W, c0, acc);   \
+    else gemm_yw<NC, N, KO, RT0, RT - RT0>(Y, ldy, W, c0, acc);    \
+  } while (0)
+
+// weight-gradient partial  P[n][k] = sum_t Y[t][n] X[t][k] over the 80 rows; this wave owns
+// n-tiles n0..n0+NN-1 x k-tiles k0..k0+NK-1; written to part (row length K).
 template <int NN, int NK>
-__device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, int yc0, const float* X, int ldx, int xc0,
-                                            float* __restrict__ part, int K, int pr0, int pc0) {
+__device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, const float* X, int ldx, int n0, int k0,
+                                            float* __restrict__ part, int K) {
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
   f32x4 acc[NN][NK];
 #pragma unroll
@@ -306,9 +316,9 @@ __device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, int yc0, co
       const int t = tc * 16 + 4 * h + m;
       float ya[NN], xb[NK];
 #pragma unroll
-      for (int a = 0; a < NN; ++a) ya[a] = Y[t * ldy + 16 * (yc0 + a) + i];
+      for (int a = 0; a < NN; ++a) ya[a] = Y[t * ldy + 16 * (n0 + a) + i];
 #pragma unroll
-      for (int b = 0; b < NK; ++b) xb[b] = X[t * ldx + 16 * (xc0 + b) + i];
+      for (int b = 0; b < NK; ++b) xb[b] = X[t * ldx + 16 * (k0 + b) + i];
 #pragma unroll
       for (int a = 0; a < NN; ++a)
 #pragma unroll
@@ -320,20 +330,19 @@ __device__ __forceinline__ void wgrad_tiles(const float* Y, int ldy, int yc0, co
 #pragma unroll
     for (int b = 0; b < NK; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) part[(16 * (pr0 + a) + 4 * h + q) * K + 16 * (pc0 + b) + i] = acc[a][b][q];
+      for (int q = 0; q < 4; ++q) part[(16 * (n0 + a) + 4 * h + q) * K + 16 * (k0 + b) + i] = acc[a][b][q];
 }
 
-// column sums of a [ROWS x n] LDS tile -> part[0..n): lanes 2c and 2c+1 sum the first and second
-// half of the rows of column c in order, then (first half) + (second half)
+// column sums of an [80 x n] LDS tile (n <= NT / 2) -> part[0..n): lanes 2c and 2c+1 sum rows
+// [0, 40) and [40, 80) of column c in order, then (first half) + (second half)
 __device__ __forceinline__ void colsum(const float* Y, int ldy, int n, float* __restrict__ part) {
-  const int hl = threadIdx.x & 1;
-  for (int c0 = 0; c0 < n; c0 += NT / 2) {  // wave-uniform trip count: pair_swap needs both lanes
-    const int c = c0 + (threadIdx.x >> 1), cc = min(c, n - 1);
+  const int c = threadIdx.x >> 1, hl = threadIdx.x & 1;
+  if (c < n) {
     float s = 0.f;
 #pragma unroll 8
-    for (int t = hl * (ROWS / 2); t < (hl + 1) * (ROWS / 2); ++t) s += Y[t * ldy + cc];
+    for (int t = hl * (ROWS / 2); t < (hl + 1) * (ROWS / 2); ++t) s += Y[t * ldy + c];
     const float o = pair_swap(s);
-    if (!hl && c < n) part[c] = s + o;
+    if (!hl) part[c] = s + o;
   }
 }
 
@@ -361,17 +370,17 @@ __device__ __forceinline__ void lds_zero(float* p, int ld, int rows, int cols) {
     *reinterpret_cast<float4*>(p + (e / per) * ld + 4 * (e % per)) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// load rows [0, tv) of COLS columns of a global tensor (row stride GLD) into LDS (ld), zero rows
-// [tv, ROWS).  All loads of a thread are issued before the first LDS store (unconditional addresses,
-// rows clamped), so the copy costs one memory latency, not one per row.
-template <int COLS, int GLD = COLS>
+// load rows [0, tv) of a [*, COLS] global tensor into LDS (ld), zero rows [tv, 80).  All loads of a
+// thread are issued before the first LDS store (unconditional addresses, rows clamped), so the
+// copy costs one memory latency, not one per row.
+template <int COLS>
 __device__ __forceinline__ void lds_load(float* p, int ld, const float* __restrict__ g, int tv) {
   constexpr int PER = COLS / 4, TOT = ROWS * PER, ITER = (TOT + NT - 1) / NT;
   float4 v[ITER];
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
     const int e = min((int)threadIdx.x + k * NT, TOT - 1), r = e / PER, c4 = e % PER;
-    v[k] = *reinterpret_cast<const float4*>(g + (int64_t)min(r, tv - 1) * GLD + 4 * c4);
+    v[k] = *reinterpret_cast<const float4*>(g + (int64_t)min(r, tv - 1) * COLS + 4 * c4);
   }
 #pragma unroll
   for (int k = 0; k < ITER; ++k) {
@@ -493,7 +502,7 @@ template <int L> constexpr int band_slot(int r) {
 }
 constexpr int TILE_LD = 20;               // scratch score tiles [16 keys][16 queries], rows padded to 20
 constexpr int TILE_SZ = 16 * TILE_LD;
-constexpr int MAX_SLOTS = 7;              // band tiles of the 3 query tiles, max over supported L
+constexpr int MAX_SLOTS = 13;             // band tiles of the 5 query tiles, max over supported L
 constexpr int DQ_LD = HD + 4;
 
 // max / sum over the 4 lane rows (lanes l, l ^ 16, l ^ 32, l ^ 48), the same value in every lane
@@ -638,20 +647,21 @@ __device__ __forceinline__ void attn_fwd_tile(float* RA, const float* MS, int hh
   fr_mark(prof, 0, 24);
 }
 
-// the 6 (query tile, head) jobs over 4 waves: tile 1 (3 band tiles for L = 20, 10, 5) one per wave on
-// waves 0 and 1, tiles 0 and 2 (2 band tiles) two per wave on waves 2 and 3
+// the 10 (query tile, head) jobs over 8 waves: tiles 1-3 (3 band tiles for L = 20, 10, 5) one per
+// wave, tiles 0 and 4 (2 band tiles) two per wave on waves 6 and 7
 template <int L>
 __device__ __forceinline__ void attn_fwd(float* RA, const float* MS, int64_t seq0, uint32_t ks, const Weights& w,
                                          bool prof) {
-  static_assert(RT == 3 && HEADS == 2 && NWAVE == 4, "job table");
+  static_assert(RT == 5 && HEADS == 2 && NT / 64 == 8, "job table");
   const int wave = wave_id();
-  for (int j = wave; j < RT * HEADS; j += (wave >= 2 ? 2 : RT * HEADS)) {
-    // j: 0, 1 -> (tile 1, head j); 2, 3 -> (tile 0, head j - 2); 4, 5 -> (tile 2, head j - 4)
-    const int R = j < 2 ? 1 : (j < 4 ? 0 : 2), hh = j & 1;
+  for (int j = wave; j < RT * HEADS; j += (wave >= 6 ? 2 : RT * HEADS)) {
+    const int R = j < 6 ? 1 + j % 3 : ((j - 6) % 2 ? 4 : 0), hh = j < 6 ? j / 3 : (j - 6) / 2;
     switch (R) {
       case 0: attn_fwd_tile<L, 0>(RA, MS, hh, seq0, ks, w, prof); break;
       case 1: attn_fwd_tile<L, 1>(RA, MS, hh, seq0, ks, w, prof); break;
-      default: attn_fwd_tile<L, 2>(RA, MS, hh, seq0, ks, w, prof); break;
+      case 2: attn_fwd_tile<L, 2>(RA, MS, hh, seq0, ks, w, prof); break;
+      case 3: attn_fwd_tile<L, 3>(RA, MS, hh, seq0, ks, w, prof); break;
+      default: attn_fwd_tile<L, 4>(RA, MS, hh, seq0, ks, w, prof); break;
     }
   }
 }
@@ -743,7 +753,9 @@ __device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const 
   switch (R) {
     case 0: attn_bwd_rows<L, 0>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
     case 1: attn_bwd_rows<L, 1>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
-    default: attn_bwd_rows<L, 2>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    case 2: attn_bwd_rows<L, 2>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    case 3: attn_bwd_rows<L, 3>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
+    default: attn_bwd_rows<L, 4>(RA, RC, MS, hh, seq0, ks, w, SP, SS, DQ, prof); break;
   }
 }
 
@@ -751,16 +763,17 @@ __device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const 
 // forward
 // ---------------------------------------------------------------------------------------------
 template <int L>
-__global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
-  constexpr int G = ROWS / L;                                       // whole sequences per workgroup
+__global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
+  constexpr int G = ROWS / L;
   __shared__ __attribute__((aligned(16))) float RA[ROWS * LD_FF];  // qkv (ctx in the q slots), then act
   __shared__ __attribute__((aligned(16))) float RB[ROWS * LD_E];   // x -> y1 -> x1 -> y2
   __shared__ float MS[ROWS];                                        // key mask of the tile's tokens
   const Weights& w = a.w;
-  const int sg = wave_id(), lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int sg = wave & 3, hf = wave >> 2, r0 = hf ? RT0 : 0, nr = hf ? RT - RT0 : RT0;
   const int64_t seq0 = (int64_t)blockIdx.x * G;
   const int nseq = (int)min<int64_t>(G, a.ns - seq0);
-  const int tv = nseq * L;                                          // valid rows; [tv, ROWS) are padding
+  const int tv = nseq * L;
   const int64_t tok0 = seq0 * L;
   const bool prof = g_prof_on && blockIdx.x == 0;
   FR_MARK(0, 0);
@@ -773,18 +786,20 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();
   FR_MARK(0, 1);
 
-  {  // qkv = x W_in^T + b_in  (wave sg: column tiles 3sg..3sg+2, every row tile)
-    f32x4 acc[RT][3];
+  {  // qkv = x W_in^T + b_in  (SIMD slot sg: column tiles 3sg..3sg+2)
+    f32x4 acc[RT0][3];
     zero_acc(acc);
-    gemm_xwt<3, E, 0, RT>(RB, LD_E, w.w_in, 3 * sg, acc);
+    FR_GEMM_XWT(3, E, RB, LD_E, w.w_in, 3 * sg, acc);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const int col = 16 * (3 * sg + c) + i16;
       const float bias = w.b_in[col];
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < RT0; ++r) {
+        if (r >= nr) break;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) RA[(16 * r + 4 * h4 + q) * LD_QKV + col] = acc[r][c][q] + bias;
+        for (int q = 0; q < 4; ++q) RA[(16 * (r0 + r) + 4 * h4 + q) * LD_QKV + col] = acc[r][c][q] + bias;
+      }
     }
   }
   __syncthreads();
@@ -793,21 +808,22 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();  // the copy has read every q slot before attention overwrites them with ctx
   FR_MARK(0, 20);
 
-  // attention on MFMA: 6 (query tile, head) jobs over the 4 waves; ctx over the q slots
+  // attention on MFMA: 10 (query tile, head) jobs over the 8 waves; ctx over the q slots
   attn_fwd<L>(RA, MS, seq0, ks.k[0], w, prof);
   __syncthreads();
   FR_MARK(0, 3);
   lds_store<E>(RA, LD_QKV, a.ctx + tok0 * E, tv);  // ctx (saved for the backward): cols 0..63 of RA
 
-  {  // y1 = x + dropout1(ctx W_o^T + b_o)   (column tile sg)
-    f32x4 acc[RT][1];
+  {  // y1 = x + dropout1(ctx W_o^T + b_o)   (column tile sg); ctx rows of padded sequences are stale
+    f32x4 acc[RT0][1];
     zero_acc(acc);
-    gemm_xwt<1, E, 0, RT>(RA, LD_QKV, w.w_o, sg, acc);
+    FR_GEMM_XWT(1, E, RA, LD_QKV, w.w_o, sg, acc);
     const int col = 16 * sg + i16;
     const float bias = w.b_o[col];
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int row0 = 16 * r + 4 * h4;
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
+      const int row0 = 16 * (r0 + r) + 4 * h4;
       const uint32_t kb = frag_keep4(ks.k[1], tok0 + row0, E, col, w.thr[1]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -822,12 +838,14 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
   __syncthreads();
   FR_MARK(0, 5);
 
-  {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA  (wave sg: column tiles 4sg..4sg+3)
-    f32x4 acc[RT][4];
+  {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA.  Column split (wave: tiles 4sg + 2hf, +1;
+     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue
+    f32x4 acc[RT][2];
     zero_acc(acc);
-    gemm_xwt<4, E, 0, RT>(RB, LD_E, w.w1, 4 * sg, acc);
+    gemm_xwt<2, E, 0, RT>(RB, LD_E, w.w1, 4 * sg + 2 * hf, acc);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int cc = 0; cc < 2; ++cc) {
+      const int c = 2 * hf + cc;  // column tile within the SIMD slot's four (dact fragment index)
       const int col = 16 * (4 * sg + c) + i16;
       const float bias = w.b1[col];
 #pragma unroll
@@ -838,7 +856,7 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int q2 = 0; q2 < 2; ++q2) {
           f32x2 av, gv;
-          act_fwd_grad2(f32x2{acc[r][c][2 * q2], acc[r][c][2 * q2 + 1]} + bias, w.gelu, av, gv);
+          act_fwd_grad2(f32x2{acc[r][cc][2 * q2], acc[r][cc][2 * q2 + 1]} + bias, w.gelu, av, gv);
           av = av * w.scale[2];
           gv = gv * w.scale[2];
 #pragma unroll
@@ -858,14 +876,15 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
   FR_MARK(0, 6);
 
   {  // y2 = x1 + dropout2(act' W2^T + b2)  (column tile sg, K = 256)
-    f32x4 acc[RT][1];
+    f32x4 acc[RT0][1];
     zero_acc(acc);
-    gemm_xwt<1, FF, 0, RT>(RA, LD_FF, w.w2, sg, acc);
+    FR_GEMM_XWT(1, FF, RA, LD_FF, w.w2, sg, acc);
     const int col = 16 * sg + i16;
     const float bias = w.b2[col];
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int row0 = 16 * r + 4 * h4;
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
+      const int row0 = 16 * (r0 + r) + 4 * h4;
       const uint32_t kb = frag_keep4(ks.k[3], tok0 + row0, E, col, w.thr[3]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -885,29 +904,26 @@ __global__ __launch_bounds__(NT, 2) void enc_fwd_kernel(FwdArgs a) {
 // backward
 // ---------------------------------------------------------------------------------------------
 template <int L>
-__global__ __launch_bounds__(NT, 2) void enc_bwd_kernel(BwdArgs a) {
+__global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   constexpr int G = ROWS / L;
-  // one LDS image (<= 80 KB: two workgroups per CU): RA [48 x 196] (the FF block's column half
-  // [48 x 132], then qkv / dqkv) | RC [48 x 68] | RB [48 x 68] | RD [48 x 68]; the attention
-  // backward's scratch (P' and dS tiles, dQ) overlays RB + RD (dY1 is held in registers across it)
-  constexpr int OFF_RC = ROWS * LD_QKV, OFF_RB = OFF_RC + ROWS * LD_E, OFF_RD = OFF_RB + ROWS * LD_E;
+  // one LDS image: RA [80 x 260] | RC [80 x 68] | RB [80 x 68] | RD [BUF_D]; the attention backward's
+  // scratch (P' and dS tiles, dQ) overlays RB + RD (dY1 is held in registers across it)
+  constexpr int OFF_RC = ROWS * LD_FF, OFF_RB = OFF_RC + ROWS * LD_E, OFF_RD = OFF_RB + ROWS * LD_E;
   constexpr int SCR_FLOATS = 2 * MAX_SLOTS * TILE_SZ + ROWS * DQ_LD;
-  static_assert(LD_FH <= LD_QKV, "FF half fits the qkv buffer");
   static_assert(SCR_FLOATS <= ROWS * LD_E + BUF_D, "attention scratch fits RB + RD");
-  static_assert(2 * (NT / 16) * E <= BUF_D, "LayerNorm scratch in RD");
+  static_assert(ROWS * LD_E <= BUF_D && 2 * (NT / 16) * E <= BUF_D, "LayerNorm scratch / ctx in RD");
   static_assert(band_slot<L>(RT) <= MAX_SLOTS, "band tiles");
-  static_assert((OFF_RD + BUF_D + ROWS) * 4 <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) float LDSB[OFF_RD + BUF_D];
-  __shared__ float MS[ROWS];
   float* const RA = LDSB;
   float* const RC = LDSB + OFF_RC;
   float* const RB = LDSB + OFF_RB;
   float* const RD = LDSB + OFF_RD;
   float* const SP = RB;                            // P' tiles   [MAX_SLOTS][16][TILE_LD]
   float* const SS = RB + MAX_SLOTS * TILE_SZ;      // dS tiles
-  float* const DQ = RB + 2 * MAX_SLOTS * TILE_SZ;  // dQ of one head [ROWS][DQ_LD]
+  float* const DQ = RB + 2 * MAX_SLOTS * TILE_SZ;  // dQ of one head [80][DQ_LD]
   const Weights& w = a.w;
-  const int sg = wave_id(), lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, h4 = lane >> 4;
+  const int sg = wave & 3, hf = wave >> 2, r0 = hf ? RT0 : 0, nr = hf ? RT - RT0 : RT0;
   const int64_t seq0 = (int64_t)blockIdx.x * G;
   const int nseq = (int)min<int64_t>(G, a.ns - seq0);
   const int tv = nseq * L;
@@ -916,16 +932,55 @@ __global__ __launch_bounds__(NT, 2) void enc_bwd_kernel(BwdArgs a) {
   FR_MARK(1, 0);
   const SiteKeys ks = site_keys(w.seed, *a.seed_in);
   float* part = a.part + (int64_t)blockIdx.x * NPART;
+  __shared__ float MS[ROWS];
   if (threadIdx.x < ROWS) MS[threadIdx.x] = (a.mask && threadIdx.x < tv) ? a.mask[tok0 + threadIdx.x] : 0.f;
 
-  // 1. LN2 backward: RB = dY2 (pad rows 0) -> dZ2
+  // 1. LN2 backward: RB = dY2 (pad rows 0)
   lds_load<E>(RB, LD_E, a.dout + tok0 * E, tv);
   __syncthreads();
   FR_MARK(1, 1);
   ln_rows_bwd(RB, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, tv, RD, part + OFF_G2, part + OFF_BE2);
 
-  // 2. dG = dropout2'(dZ2) -> RC;  x1 = LN1(y1) recomputed -> RD (read by dW1)
+  // 2. dG = dropout2'(dY2) -> RC;  act' (saved by the forward) -> RA
   drop_pairs(RB, RC, ks.k[3], tok0, w.thr[3], w.scale[3]);
+  lds_load<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);
+  __syncthreads();
+  FR_MARK(1, 2);
+
+  // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 2w, 2w+1);  db2
+  wgrad_tiles<4, 2>(RC, LD_E, RA, LD_FF, 0, 2 * wave, part + OFF_W2, FF);
+  colsum(RC, LD_E, E, part + OFF_B2);
+
+  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA  (wave: column tiles
+     // 4sg + 2hf, +1; every row tile)
+    f32x4 acc[RT][2];
+    zero_acc(acc);
+    gemm_yw<2, E, FF, 0, RT>(RC, LD_E, w.w2, 4 * sg + 2 * hf, acc);
+    float4 pv[2][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, sg, 2 * hf + cc, r, lane));
+    __syncthreads();  // every wave is done reading act' from RA
+    FR_MARK(1, 3);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int col = 16 * (4 * sg + 2 * hf + cc) + i16;
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * r + 4 * h4 + q;
+          RA[row * LD_FF + col] = row < tv ? acc[r][cc][q] * comp(pv[cc][r], q) : 0.f;
+        }
+    }
+  }
+  __syncthreads();
+  FR_MARK(1, 4);
+
+  // 5. db1; x1 = LN1(y1) recomputed -> RC
+  colsum(RA, LD_FF, FF, part + OFF_B1);
   {
     const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
     const float4 gg = *reinterpret_cast<const float4*>(w.g1 + 4 * l);
@@ -947,115 +1002,78 @@ __global__ __launch_bounds__(NT, 2) void enc_bwd_kernel(BwdArgs a) {
       const float mean = sv[k].x, rstd = sv[k].y;
       const float4 o = make_float4(fmaf((v.x - mean) * rstd, gg.x, bb.x), fmaf((v.y - mean) * rstd, gg.y, bb.y),
                                    fmaf((v.z - mean) * rstd, gg.z, bb.z), fmaf((v.w - mean) * rstd, gg.w, bb.w));
-      *reinterpret_cast<float4*>(RD + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(RC + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  lds_load<FH, FF>(RA, LD_FH, a.fact + tok0 * FF, tv);  // act', column half 0
   __syncthreads();
-  FR_MARK(1, 2);
-  colsum(RC, LD_E, E, part + OFF_B2);
+  FR_MARK(1, 5);
 
-  // 3. the FF block in two column halves of 128 (h): dW2[:, h] = dG^T act'_h, dpre_h = (dG W2[:, h]) *
-  //    dact_h, db1[h], dW1[h, :] = dpre_h^T x1, dX1 += dpre_h W1[h, :] (accumulated in registers)
-  f32x4 dx1[RT][1];
-  zero_acc(dx1);
-#pragma unroll 1
-  for (int h = 0; h < 2; ++h) {
-    // dW2 [64 x 256], this half's 128 columns: wave sg takes n-tile sg, k-tiles 0..7
-    wgrad_tiles<1, 8>(RC, LD_E, sg, RA, LD_FH, 0, part + OFF_W2, FF, sg, 8 * h);
-    {  // dact'_h = dG W2[:, h] (wave: column tiles 2sg, 2sg+1 of the half, every row tile)
-      f32x4 acc[RT][2];
-      zero_acc(acc);
-      gemm_yw<2, E, FF, 0, RT>(RC, LD_E, w.w2, 8 * h + 2 * sg, acc);
-      float4 pv[2][RT];  // dact at this lane's output elements (forward's fragment layout)
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const int ct = 8 * h + 2 * sg + cc;  // global FF column tile
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, ct >> 2, ct & 3, r, lane));
-      }
-      __syncthreads();  // every wave is done reading act'_h from RA
-      FR_MARK(1, 3 + 2 * h);
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const int col = 16 * (2 * sg + cc) + i16;
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int row = 16 * r + 4 * h4 + q;
-            RA[row * LD_FH + col] = row < tv ? acc[r][cc][q] * comp(pv[cc][r], q) : 0.f;
-          }
-      }
-    }
-    __syncthreads();
-    FR_MARK(1, 4 + 2 * h);
-    colsum(RA, LD_FH, FH, part + OFF_B1 + FH * h);
-    // dW1 [256 x 64], this half's 128 rows: wave sg takes n-tiles 2sg, 2sg+1, k-tiles 0..3
-    wgrad_tiles<2, 4>(RA, LD_FH, 2 * sg, RD, LD_E, 0, part + OFF_W1, E, 8 * h + 2 * sg, 0);
-    gemm_yw<1, FH, E, 0, RT>(RA, LD_FH, w.w1 + (int64_t)FH * h * E, sg, dx1);  // dX1 += dpre_h W1[h, :]
-    __syncthreads();  // dpre_h consumed: RA takes the next half's act'
-    if (h == 0) {
-      lds_load<FH, FF>(RA, LD_FH, a.fact + tok0 * FF + FH, tv);
-      __syncthreads();
-    }
-  }
-  FR_MARK(1, 7);
-  {  // dX1 = dZ2 + sum_h dpre_h W1[h, :]  -> RB
+  // 6. dW1 = dpre^T x1  [256 x 64] (wave: n-tiles 2w, 2w+1)
+  wgrad_tiles<2, 4>(RA, LD_FF, RC, LD_E, 2 * wave, 0, part + OFF_W1, E);
+
+  {  // 7. dX1 = dY2 + dpre W1  -> RB
+    f32x4 acc[RT0][1];
+    zero_acc(acc);
+    FR_GEMM_YW(1, FF, E, RA, LD_FF, w.w1, sg, acc);
     const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) RB[(16 * r + 4 * h4 + q) * LD_E + col] += dx1[r][0][q];
+      for (int q = 0; q < 4; ++q) RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
+    }
   }
   __syncthreads();
+  FR_MARK(1, 6);
 
-  // 4. LN1 backward: RB = dY1
+  // 8. LN1 backward: RB = dY1
   ln_rows_bwd(RB, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, tv, RD, part + OFF_G1, part + OFF_BE1);
 
-  // 5. dO = dropout1'(dY1) -> RC;  ctx -> RD
+  // 9. dO = dropout1'(dY1) -> RC;  ctx -> RD
   drop_pairs(RB, RC, ks.k[1], tok0, w.thr[1], w.scale[1]);
   lds_load<E>(RD, LD_E, a.ctx + tok0 * E, tv);
   __syncthreads();
-  FR_MARK(1, 8);
+  FR_MARK(1, 7);
 
-  // 6. dW_o = dO^T ctx [64 x 64] (wave: n-tile sg, k-tiles 0..3); db_o
-  wgrad_tiles<1, 4>(RC, LD_E, sg, RD, LD_E, 0, part + OFF_WO, E, sg, 0);
+  // 10. dW_o = dO^T ctx [64 x 64] (wave: n-tile sg, k-tiles 2hf, 2hf+1); db_o
+  wgrad_tiles<1, 2>(RC, LD_E, RD, LD_E, sg, 2 * hf, part + OFF_WO, E);
   colsum(RC, LD_E, E, part + OFF_BO);
 
-  // dY1 at this lane's final dX elements, held in registers: the attention scratch overlays RB
-  float dy1[RT][4];
+  // dY1 rows of this lane's final dX elements, held in registers: the attention scratch overlays RB
+  float dy1[RT0][4];
 #pragma unroll
-  for (int r = 0; r < RT; ++r)
+  for (int r = 0; r < RT0; ++r)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dy1[r][q] = RB[(16 * r + 4 * h4 + q) * LD_E + 16 * sg + i16];
+    for (int q = 0; q < 4; ++q) dy1[r][q] = r < nr ? RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + 16 * sg + i16] : 0.f;
 
-  {  // 7. dctx = dO W_o -> RC;  qkv -> RA
-    f32x4 acc[RT][1];
+  {  // 11. dctx = dO W_o -> RC;  qkv -> RA
+    f32x4 acc[RT0][1];
     zero_acc(acc);
-    gemm_yw<1, E, E, 0, RT>(RC, LD_E, w.w_o, sg, acc);
+    FR_GEMM_YW(1, E, E, RC, LD_E, w.w_o, sg, acc);
     lds_load<QKV>(RA, LD_QKV, a.qkv + tok0 * QKV, tv);
     __syncthreads();
-    FR_MARK(1, 9);
+    FR_MARK(1, 8);
     const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) RC[(16 * r + 4 * h4 + q) * LD_E + col] = acc[r][0][q];
+      for (int q = 0; q < 4; ++q) RC[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] = acc[r][0][q];
+    }
   }
   __syncthreads();
-  FR_MARK(1, 10);
+  FR_MARK(1, 9);
 
-  // 8. attention backward on MFMA, one head at a time (the scratch holds one head's tiles):
-  //   phase 1: query tiles (waves 0..2): P, dP'^T, dS, the P' / dS tiles, dQ -> DQ
+  // 12. attention backward on MFMA, one head at a time (the scratch holds one head's tiles):
+  //   phase 1: query tiles (5 waves): P, dP'^T, dS, the P' / dS tiles, dQ -> DQ
   //   phase 2: (key tile, dK | dV, column tile) jobs: dK = dS^T Q, dV = P'^T dctx over the k / v slots
   //   then dQ over the head's q slots (phase 2 has read them)
+  const int wv = wave_id();
   for (int hh = 0; hh < HEADS; ++hh) {
-    if (sg < RT) attn_bwd_rows_any<L>(sg, RA, RC, MS, hh, seq0, ks.k[0], w, SP, SS, DQ, prof);
+    if (wv < RT) attn_bwd_rows_any<L>(wv, RA, RC, MS, hh, seq0, ks.k[0], w, SP, SS, DQ, prof);
     __syncthreads();
     if (hh == 0) FR_MARK(1, 18);
-    for (int j = sg; j < RT * 2 * (HD / 16); j += NWAVE)
+    for (int j = wv; j < RT * 2 * (HD / 16); j += NT / 64)
       attn_bwd_keys<L>(RA, RC, SP, SS, hh, j % RT, (j / RT) % 2, j / (2 * RT));
     __syncthreads();
     if (hh == 0) FR_MARK(1, 19);
@@ -1065,28 +1083,30 @@ __global__ __launch_bounds__(NT, 2) void enc_bwd_kernel(BwdArgs a) {
     }
     __syncthreads();
   }
-  FR_MARK(1, 11);
+  FR_MARK(1, 10);
   if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
   lds_load<E>(RC, LD_E, a.x + tok0 * E, tv);
   __syncthreads();
   FR_MARK(1, 12);
 
-  // 9. db_in; dW_in = dqkv^T x [192 x 64] (wave: n-tiles 3sg..3sg+2, k-tiles 0..3)
+  // 13. db_in; dW_in = dqkv^T x [192 x 64] (wave: n-tiles 3sg..3sg+2, k-tiles 2hf, 2hf+1)
   colsum(RA, LD_QKV, QKV, part + OFF_BIN);
-  wgrad_tiles<3, 4>(RA, LD_QKV, 3 * sg, RC, LD_E, 0, part + OFF_WIN, E, 3 * sg, 0);
+  wgrad_tiles<3, 2>(RA, LD_QKV, RC, LD_E, 3 * sg, 2 * hf, part + OFF_WIN, E);
 
-  {  // 10. dX = dY1 + dqkv W_in
-    f32x4 acc[RT][1];
+  {  // 14. dX = dY1 + dqkv W_in
+    f32x4 acc[RT0][1];
     zero_acc(acc);
-    gemm_yw<1, QKV, E, 0, RT>(RA, LD_QKV, w.w_in, sg, acc);
+    FR_GEMM_YW(1, QKV, E, RA, LD_QKV, w.w_in, sg, acc);
     const int col = 16 * sg + i16;
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int r = 0; r < RT0; ++r) {
+      if (r >= nr) break;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int row = 16 * r + 4 * h4 + q;
+        const int row = 16 * (r0 + r) + 4 * h4 + q;
         if (row < tv) a.dx[(tok0 + row) * E + col] = dy1[r][q] + acc[r][0][q];
       }
+    }
   }
   FR_MARK(1, 31);
 }
