@@ -844,6 +844,7 @@ class _GraphBpr(torch.autograd.Function):
                                          native.stream_of(user_w)), "fr_bpr_fwd_rows")
         ctx.save_for_backward(user_w, item_w, ui_all, u, p, n, pn)
         ctx.ingre_w = ingre_w  # the parameter itself (grad_buffer looks up its gradient destination)
+        ctx.defer = ingre_w.__dict__.get("_fr_defer_rows")
         ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
         return out[0], out[4:5], item_rows
 
@@ -894,6 +895,8 @@ class _GraphBpr(torch.autograd.Function):
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_bpr_bwd(*common, None, None, d_user.data_ptr(), d_item.data_ptr(), det, ws.data_ptr(),
                                         ws.numel(), s), "fr_bpr_bwd")
+        if ctx.defer is not None:
+            ctx.defer.drain(d_ingre)
         return (d_user, d_item, d_ingre) + (None,) * 10
 
     @staticmethod
@@ -948,14 +951,46 @@ class _GraphBpr(torch.autograd.Function):
                                                  d_ingre[NI:].data_ptr(), 64, native.ptr(bits), ws.data_ptr(),
                                                  ws.numel(), s),
                          "fr_graph_bpr_finish")
+        if ctx.defer is not None:
+            ctx.defer.drain(d_ingre)  # the encoder input rows' gradient, atomically into d ingre
         return (d_user, d_item, d_ingre) + (None,) * 10
 
 
 def graph_bpr(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
     """HealthRec's propagation + BPR + EmbLoss(user, pos, neg) -> (BPRLoss, EmbLoss [1],
-    [ui_items[pos]; ui_items[neg]]); see _GraphBpr."""
+    [ui_items[pos]; ui_items[neg]]); see _GraphBpr.  Opens a deferred-rows slot on ``ingre_w``
+    (_DeferredRows) that the next embedding_norms over the same table takes."""
+    if torch.is_grad_enabled() and ingre_w.requires_grad and not _DETERMINISTIC:
+        ingre_w.__dict__["_fr_defer_rows"] = _DeferredRows()
     return _GraphBpr.apply(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma,
                            _DETERMINISTIC)
+
+
+class _DeferredRows:
+    """Row gradients of a table whose dense gradient another backward writes in full later: HealthRec's
+    ingredient table gets d ingre[:-1] from the RI propagation backward (graph_bpr, which runs last)
+    and the encoder input's rows W[ids] (embedding_norms, which runs first).  Instead of a zero-filled
+    dense scatter that autograd then adds to the propagation gradient (two PyTorch kernels over the
+    table), the embedding backward hands its rows over (``put``) and returns no gradient; graph_bpr's
+    backward scatters them atomically into the gradient it has just written (``drain``).  Either
+    order is safe: rows handed over after the drain (``open`` False) are refused and scattered the
+    usual way."""
+
+    def __init__(self):
+        self.open = True
+        self.rows = []
+
+    def put(self, idx, G, hot_row) -> bool:
+        if not self.open:
+            return False
+        self.rows.append((idx, G, hot_row))
+        return True
+
+    def drain(self, dW):
+        self.open = False
+        for idx, G, hot_row in self.rows:
+            scatter_rows_into(idx, G, dW, hot_row)
+        self.rows = []
 
 
 class _RegCombine(torch.autograd.Function):
@@ -1037,6 +1072,26 @@ def scatter_rows(ids: torch.Tensor, G: torch.Tensor, num_rows: int, padding_idx:
     return dW
 
 
+def scatter_rows_into(ids: torch.Tensor, G: torch.Tensor, dW: torch.Tensor, hot_row: int | None = None) -> None:
+    """``dW[ids[i]] += G[i]`` into an existing fp32 [rows, 64] table (fr_embedding_bwd_atomic without
+    the zero fill; float-atomic order, the non-deterministic mode's scatter)."""
+    G2 = G.reshape(-1, 64)
+    if G2.stride(1) != 1 or G2.stride(0) % 4 or G2.data_ptr() % 16:
+        G2 = G2.contiguous()
+    ids2 = ids.reshape(-1)
+    if ids2.dtype != torch.int64 or not ids2.is_contiguous():
+        ids2 = ids2.to(torch.int64).contiguous()
+    native.require_device(G2, ids2, dW)
+    if dW.dtype != torch.float32 or dW.shape[1] != 64 or dW.stride(1) != 1 or dW.stride(0) % 4 or dW.data_ptr() % 16:
+        raise native.EngineError("scatter_rows_into: fp32 [rows, 64] table with 16-B aligned rows required")
+    n = int(ids2.numel())
+    with profiling.region("embedding_bwd", embedding_bwd_bytes(n, int(dW.shape[0]), 64)):
+        native.check(native.lib().fr_embedding_bwd_atomic(
+            ids2.data_ptr(), n, G2.data_ptr(), G2.stride(0), 64, int(dW.shape[0]), -1,
+            -1 if hot_row is None else int(hot_row), dW.data_ptr(), dW.stride(0),
+            native.stream_of(G2)), "fr_embedding_bwd_atomic")
+
+
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, weight, padding_idx):
@@ -1099,7 +1154,9 @@ class _EmbeddingNorms(torch.autograd.Function):
                                                      native.stream_of(weight)), "fr_gather_norms_fwd")
             ctx.save_for_backward(idx_c, E, nrm)
             ctx.rows, ctx.pad, ctx.half, ctx.hp = weight.shape[0], pad, half, hp
+            ctx.defer = weight.__dict__.pop("_fr_defer_rows", None)
             return E, nrm
+        weight.__dict__.pop("_fr_defer_rows", None)  # this path scatters its own rows
         E = torch.nn.functional.embedding(idx, weight)
         Ef = E.reshape(2, -1)  # full-tensor norms of each half (a 2-output dim reduction is slow)
         nrm = torch.stack([torch.linalg.vector_norm(Ef[0]), torch.linalg.vector_norm(Ef[1])])
@@ -1120,6 +1177,8 @@ class _EmbeddingNorms(torch.autograd.Function):
                         E.data_ptr(), gn.data_ptr(), gn.stride(0), nrm.data_ptr(), out.data_ptr(),
                         native.stream_of(G)), "fr_norms_bwd_coef")
                 G = out
+            if ctx.defer is not None and ctx.defer.put(idx, G.reshape(-1, 64), ctx.pad):
+                return None, None, None, None  # scattered into graph_bpr's d ingre (_DeferredRows)
             return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None, hot_row=ctx.pad), None, None
         G = torch.zeros_like(E) if gE is None else gE
         if gn is not None:
