@@ -681,6 +681,19 @@ int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32_t* d_col, 
 int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
                             const uint32_t* d_bits, const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2,
                             float alpha, const fr_tab* A1, float beta1, void* stream);
+/* Either of the two above over an edge-balanced row-block plan (engine ops._sparse_plan, built once
+ * per adjacency): block b = (row_lo, row_hi, edge_lo, edge_hi) in d_blocks[4b .. 4b+3], at most 64
+ * rows of a bounded edge count, or one chunk of a heavy row (a Zipf item row of config 4's 10M x 1M
+ * graph has up to 434k edges; with uniform 64-row blocks its workgroup scans them alone).  Chunks add
+ * into their row atomically after the rows in d_split_rows got their own term (beta1 * gate(A1)).
+ * ungated = 1: the rectangular form (bitmask over n_cols, A1 at every row); 0: the square gated form
+ * (split tables at `split`).  The sparse-upstream backward of lightgcn.py:134-147's propagation
+ * (ops.propagate_rows) and of the row-sharded step (engine/sharded.py). */
+int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                                   int64_t n_cols, int ungated, const uint32_t* d_bits, const float* d_X, int64_t ldx,
+                                   int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
+                                   const int64_t* d_blocks, int64_t n_blocks, const int64_t* d_split_rows,
+                                   int64_t n_split_rows, void* stream);
 
 /* fr_graph_bpr_finish: the tail of HealthRec's fused propagation + BPR backward (engine
  * ops.graph_bpr), after both propagation backwards have written dUe (user_embedding's gradient)

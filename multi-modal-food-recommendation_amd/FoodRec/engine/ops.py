@@ -644,11 +644,77 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
     if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32:
         raise native.EngineError("spmm_sparse_upstream: bits must be int32 with ceil(rows / 32) words")
     _check_tab("Y2", Y2, Y2_hi, split, N, 64)
+    plan = _sparse_plan(adj)
     with profiling.region(region, 0):
+        if plan is not None:  # heavy rows (config 4's Zipf items): edge-balanced blocks
+            _sparse_blocks(adj, False, bits, X, Y2, Y2_hi, split, alpha, X, beta1, plan)
+            return
         native.check(native.lib().fr_spmm_sparse_upstream(
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, bits.data_ptr(), X.data_ptr(),
             X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha), ctypes.byref(_tab(X)), _f(beta1),
             native.stream_of(X)), "fr_spmm_sparse_upstream")
+
+
+SPARSE_BLOCK_ROWS = 64        # rows per block of the sparse-upstream kernel (kSpRows)
+SPARSE_BLOCK_EDGES = 2048     # edge budget of a plan block (two 1024-edge scan rounds)
+SPARSE_PLAN_TRIGGER = 8192    # use a plan when some uniform 64-row block would scan more edges
+
+
+def sparse_block_plan(rowptr: np.ndarray, rows_per_block=SPARSE_BLOCK_ROWS, edges=SPARSE_BLOCK_EDGES):
+    """Edge-balanced row blocks for the sparse-upstream kernel: (blocks [n, 4] = (row_lo, row_hi,
+    edge_lo, edge_hi), split_rows).  Cuts fall every ``rows_per_block`` rows, wherever the running
+    edge count crosses a multiple of ``edges``, and around every row of more than ``edges`` edges;
+    such a heavy row becomes ceil(deg / edges) chunks (listed in split_rows).  A block of light rows
+    scans at most 2 * edges edges."""
+    rp = np.asarray(rowptr, dtype=np.int64)
+    n = rp.shape[0] - 1
+    if n <= 0:
+        return np.zeros((0, 4), np.int64), np.zeros(0, np.int64)
+    deg = np.diff(rp)
+    heavy = np.nonzero(deg > edges)[0]
+    band = rp // edges
+    cuts = np.concatenate([np.arange(0, n + 1, rows_per_block), np.nonzero(band[1:] != band[:-1])[0] + 1,
+                           heavy, heavy + 1, [0, n]])
+    cuts = np.unique(cuts[(cuts >= 0) & (cuts <= n)])
+    lo, hi = cuts[:-1], cuts[1:]
+    single_heavy = (hi - lo == 1) & (deg[lo] > edges)
+    light = np.stack([lo, hi, rp[lo], rp[hi]], 1)[~single_heavy]
+    hr = lo[single_heavy]
+    nch = (deg[hr] + edges - 1) // edges
+    rows = np.repeat(hr, nch)
+    k = np.arange(rows.shape[0]) - np.repeat(np.cumsum(nch) - nch, nch)
+    e_lo = rp[rows] + k * edges
+    e_hi = np.minimum(e_lo + edges, rp[rows + 1])
+    chunks = np.stack([rows, rows + 1, e_lo, e_hi], 1)
+    blocks = np.concatenate([light, chunks])
+    return blocks[np.argsort(blocks[:, 2], kind="stable")], hr.astype(np.int64)
+
+
+def _sparse_plan(adj: Adjacency):
+    """The adjacency's sparse-upstream block plan on its device, or None when uniform 64-row blocks
+    are balanced enough (no block over SPARSE_PLAN_TRIGGER edges).  Built once per adjacency."""
+    def make():
+        rp = adj.rowptr.cpu().numpy()
+        ends = rp[np.minimum(np.arange(SPARSE_BLOCK_ROWS, rp.shape[0] - 1 + SPARSE_BLOCK_ROWS, SPARSE_BLOCK_ROWS),
+                             rp.shape[0] - 1)]
+        starts = rp[np.arange(0, rp.shape[0] - 1, SPARSE_BLOCK_ROWS)]
+        if ends.shape[0] == 0 or int((ends - starts).max()) <= SPARSE_PLAN_TRIGGER:
+            return False
+        blocks, split_rows = sparse_block_plan(rp, SPARSE_BLOCK_ROWS, SPARSE_BLOCK_EDGES)
+        dev = adj.rowptr.device
+        return (torch.from_numpy(np.ascontiguousarray(blocks)).to(dev), torch.from_numpy(split_rows).to(dev))
+    plan = _persistent(adj, "sparse_plan", make)
+    return plan if plan is not False else None
+
+
+def _sparse_blocks(adj, ungated, bits, X, Y2, Y2_hi, split, alpha, A1, beta1, plan):
+    blocks, split_rows = plan
+    R, C = adj.shape
+    native.check(native.lib().fr_spmm_sparse_upstream_blocks(
+        adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), R, C, int(ungated), bits.data_ptr(),
+        X.data_ptr(), X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha), ctypes.byref(_tab(A1)),
+        _f(beta1), blocks.data_ptr(), blocks.shape[0], split_rows.data_ptr(), split_rows.numel(),
+        native.stream_of(X)), "fr_spmm_sparse_upstream_blocks")
 
 
 def spmm_scatter_upstream(adj: Adjacency, mask: torch.Tensor, bits: torch.Tensor, rows, X: torch.Tensor, Y2,
@@ -682,7 +748,11 @@ def spmm_sparse_rect(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, al
         raise native.EngineError("spmm_sparse_rect: X [cols, 64] and int32 bits over the columns required")
     _check_tab("Y2", Y2, None, 0, R, 64)
     _check_tab("A1", A1, None, 0, R, 64)
+    plan = _sparse_plan(adj)
     with profiling.region(region, 0):
+        if plan is not None:  # heavy rows (the transpose slice's Zipf items): edge-balanced blocks
+            _sparse_blocks(adj, True, bits, X, Y2, None, 0, alpha, A1, beta1, plan)
+            return
         native.check(native.lib().fr_spmm_sparse_upstream_rect(
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), R, C, bits.data_ptr(), X.data_ptr(),
             X.stride(0), ctypes.byref(_tab(Y2)), _f(alpha), ctypes.byref(_tab(A1)), _f(beta1),

@@ -311,12 +311,18 @@ constexpr int kSpStageWords = 1024;  // bitmask staged in LDS (dynamic, ceil(n /
 // rows) instead of being staged in LDS -- graphs beyond 32,768 rows (HealthRec UI, config 4).
 // UNGATED (a rectangular slice: the bitmask marks X's rows, i.e. columns, not output rows): A1 is
 // read at every output row.
+// BLOCKS (a row-block plan, fr_spmm_sparse_upstream*_blocks): block b covers rows
+// [blocks[4b], blocks[4b+1]) and edges [blocks[4b+2], blocks[4b+3]) -- at most 64 rows of a bounded
+// edge count, or one CHUNK of a heavy row (Zipf item rows: up to 434k edges at config 4, which a
+// 64-row block would scan alone in hundreds of rounds).  A chunk adds alpha * its partial into the
+// row atomically; the row's own term (beta1 * A1 or 0) is written first by sparse_split_init_kernel.
 template <bool GBITS, bool UNGATED = false>
 __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int64_t n_rows,
                                                           const uint32_t* __restrict__ bits, int nwords,
-                                                          const float4* __restrict__ X, int64_t ldx4, Epi ep) {
+                                                          const float4* __restrict__ X, int64_t ldx4, Epi ep,
+                                                          const int64_t* __restrict__ blocks = nullptr) {
   constexpr int KS = kSpRound / 256;  // edges per thread per round
   extern __shared__ uint32_t sbits_dyn[];
   const uint32_t* sbits = GBITS ? bits : sbits_dyn;
@@ -327,8 +333,8 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   __shared__ float hit_v[kSpRound];  // its value
   __shared__ int cnt[KS * 4];        // hits per (k, wave) slice of the round
   const int t = threadIdx.x, q = t & 15, lane = t & 63, wave = t >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
-  const int nr = (int)min<int64_t>(kSpRows, n_rows - r0);
+  const int64_t r0 = blocks ? blocks[4 * (int64_t)blockIdx.x] : (int64_t)blockIdx.x * kSpRows;
+  const int nr = blocks ? (int)(blocks[4 * (int64_t)blockIdx.x + 1] - r0) : (int)min<int64_t>(kSpRows, n_rows - r0);
   if constexpr (!GBITS) {  // stage the bitmask: 16-B loads, all in flight before the LDS stores
     const int n4 = nwords >> 2;
     const uint4* b4 = reinterpret_cast<const uint4*>(bits);
@@ -339,7 +345,9 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   for (int i = t; i < kSpRows * 16; i += 256) acc[i >> 4][i & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i = t; i <= nr; i += 256) srp[i] = rowptr[r0 + i];
   __syncthreads();
-  const int64_t e0 = srp[0], e1 = srp[nr];
+  const int64_t e0 = blocks ? blocks[4 * (int64_t)blockIdx.x + 2] : srp[0];
+  const int64_t e1 = blocks ? blocks[4 * (int64_t)blockIdx.x + 3] : srp[nr];
+  const bool chunk = e0 != srp[0] || e1 != srp[nr];  // part of one heavy row (block-uniform)
   for (int64_t base = e0; base < e1; base += kSpRound) {
     // scan: coalesced column and value loads (edge base + k * 256 + t), hit flags by wave ballot
     int cs[KS];
@@ -430,6 +438,17 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
       atomicAdd(a + 3, sum.w);
     }
     __syncthreads();
+  }
+  if (chunk) {  // the row's own term is already in Y2 (sparse_split_init_kernel)
+    if (t < 16) {
+      float* y = const_cast<float*>(tab_row(ep.Y2, r0, ep.split)) + 4 * q;
+      const float4 o = f4_scale(ep.alpha, acc[0][q]);
+      atomicAdd(y + 0, o.x);
+      atomicAdd(y + 1, o.y);
+      atomicAdd(y + 2, o.z);
+      atomicAdd(y + 3, o.w);
+    }
+    return;
   }
   // write every row: Y2 = alpha * acc + beta1 * A1 (A1 read only at marked rows)
   for (int i = t; i < nr * 16; i += 256) {
@@ -864,6 +883,65 @@ extern "C" int fr_spmm_scatter_upstream(const int64_t* d_rowptr, const int32_t* 
   hipLaunchKernelGGL(scatter_edges_kernel, dim3((unsigned)fr::ceil_div(total, (int64_t)4)), dim3(256), 0, s,
                      d_rowptr, d_col, d_val, rl, total, d_bits, d_X, ldx, Y, split, alpha);
   FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+// the rows split into chunks by a block plan: Y2[r] = beta1 * A1[r] (A1 read where r is marked, or
+// always for a rectangular slice), else 0 -- the term the chunks then add onto
+__global__ __launch_bounds__(256) void sparse_split_init_kernel(const int64_t* __restrict__ rows, int64_t n,
+                                                                const uint32_t* __restrict__ bits, bool ungated,
+                                                                Epi ep) {
+  const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int q = threadIdx.x & 15;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ep.A1.lo && (ungated || ((bits[r >> 5] >> (r & 31)) & 1u)))
+    o = f4_scale(ep.beta1, reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q]);
+  reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
+}
+
+static hipError_t sparse_blocks_launch(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                       int64_t n_rows, const uint32_t* d_bits, int nwords, const float* d_X,
+                                       int64_t ldx, const Epi& ep, bool ungated, const int64_t* d_blocks,
+                                       int64_t n_blocks, const int64_t* d_split_rows, int64_t n_split_rows,
+                                       hipStream_t s) {
+  if (n_split_rows > 0)
+    hipLaunchKernelGGL(sparse_split_init_kernel, dim3((unsigned)fr::ceil_div(n_split_rows, (int64_t)16)), dim3(256),
+                       0, s, d_split_rows, n_split_rows, d_bits, ungated, ep);
+  if (ungated)
+    hipLaunchKernelGGL((spmm_sparse_kernel<true, true>), dim3((unsigned)n_blocks), dim3(256), 0, s, d_rowptr, d_col,
+                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks);
+  else
+    hipLaunchKernelGGL((spmm_sparse_kernel<true, false>), dim3((unsigned)n_blocks), dim3(256), 0, s, d_rowptr, d_col,
+                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks);
+  return hipGetLastError();
+}
+
+extern "C" int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                              int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
+                                              const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2,
+                                              float alpha, const fr_tab* A1, float beta1, const int64_t* d_blocks,
+                                              int64_t n_blocks, const int64_t* d_split_rows, int64_t n_split_rows,
+                                              void* stream) {
+  FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX && n_cols >= 0 && n_cols < (int64_t)INT32_MAX,
+             "n_rows / n_cols out of range");
+  if (n_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && d_col && d_val && d_bits && d_X && Y2 && Y2->lo, "null operand");
+  FR_REQUIRE(d_blocks && n_blocks > 0 && n_blocks < (int64_t)INT32_MAX, "block plan required");
+  FR_REQUIRE(n_split_rows == 0 || d_split_rows, "split-row list missing");
+  FR_REQUIRE(ungated || n_cols == n_rows, "the gated form needs a square adjacency");
+  FR_REQUIRE(fr::aligned16(d_bits), "bits must be 16-B aligned");
+  FR_REQUIRE(ldx >= 64 && ldx % 4 == 0 && fr::aligned16(d_X) && tab_ok(Y2, 64) && tab_ok(A1, 64),
+             "X / Y2 / A1 must be 16-B aligned fp32 [*, 64] tables");
+  FR_REQUIRE(!(tab_touches(Y2, d_X)), "Y2 must not alias X");
+  Epi ep{Tab{nullptr, 0, nullptr, 0}, host_tab(Y2), alpha, host_tab(A1), beta1, Tab{nullptr, 0, nullptr, 0}, 0.f,
+         ungated ? 0 : split, nullptr};
+  const int nwords = (int)fr::ceil_div(std::max<int64_t>(n_cols, 1), 32);
+  const hipError_t e = sparse_blocks_launch(d_rowptr, d_col, d_val, n_rows, d_bits, nwords, d_X, ldx, ep, ungated != 0,
+                                            d_blocks, n_blocks, d_split_rows, n_split_rows,
+                                            reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_spmm_sparse_upstream_blocks: ") + hipGetErrorString(e));
   return FR_OK;
 }
 

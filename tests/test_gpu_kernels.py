@@ -703,12 +703,19 @@ def test_spmm_ex_split_rows_mask_bitwise(cuda):
     assert int(mask.sum()) == 0
 
 
+@pytest.mark.parametrize("planned", [False, True])
 @pytest.mark.parametrize("frac", [0.01, 0.6])
-def test_spmm_sparse_upstream(cuda, frac):
+def test_spmm_sparse_upstream(cuda, frac, planned, monkeypatch):
     """fr_spmm_sparse_upstream against fr_spmm_csr over the zero-filled upstream: X is garbage (NaN)
     outside the marked rows and never read there; heavy rows span several 1024-edge scan rounds;
-    split output; bitmask set and cleared by fr_rows_mark_zero.  Float-atomic order: fp32 rounding."""
+    split output; bitmask set and cleared by fr_rows_mark_zero.  ``planned``: the edge-balanced
+    block plan (fr_spmm_sparse_upstream_blocks) with a 256-edge budget, so the heavy rows (1400 and
+    900 edges) run as chunks added atomically onto their initialised rows.  Float-atomic order:
+    fp32 rounding."""
     from FoodRec.engine import ops
+    if planned:
+        monkeypatch.setattr(ops, "SPARSE_PLAN_TRIGGER", 0)
+        monkeypatch.setattr(ops, "SPARSE_BLOCK_EDGES", 256)
     n, d, split = 1500, 64, 600
     r, c = _graph(n, n, 8, heavy=[(3, 1400), (700, 900), (11, 129)], seed=23)
     adj = _adj(n, r, c, cuda, chunk=128)
@@ -732,8 +739,46 @@ def test_spmm_sparse_upstream(cuda, frac):
     got = torch.cat([lo, hi])
     assert torch.isfinite(got).all()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    assert (ops._sparse_plan(adj) is not None) == planned
     ops.rows_mark(mask, [(marked, 0)], 0, bits=bits)
     assert int(mask.sum()) == 0 and int(bits.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("planned", [False, True])
+def test_spmm_sparse_rect(cuda, planned, monkeypatch):
+    """fr_spmm_sparse_upstream_rect (a rectangular [rows x cols] slice, X marked by column, A1 read
+    at every row) against fr_spmm_csr over the zero-filled X, uniform 64-row blocks and the
+    edge-balanced plan with heavy rows chunked (fr_spmm_sparse_upstream_blocks, ungated).  The
+    row-sharded config-4 step's first backward layer (engine/sharded.py)."""
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency
+    if planned:
+        monkeypatch.setattr(ops, "SPARSE_PLAN_TRIGGER", 0)
+        monkeypatch.setattr(ops, "SPARSE_BLOCK_EDGES", 200)
+    R, C, d = 900, 1300, 64
+    g = torch.Generator().manual_seed(41)
+    deg = torch.randint(0, 12, (R,), generator=g)
+    deg[[5, 400, 899]] = torch.tensor([1100, 700, 450])
+    rp = torch.zeros(R + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(deg, 0)
+    col = torch.cat([torch.sort(torch.randperm(C, generator=g)[:int(k)]).values for k in deg]).to(torch.int32)
+    val = torch.rand(int(rp[-1]), generator=g)
+    adj = Adjacency(rp.to(cuda), col.to(cuda), val.to(cuda), (R, C), device=cuda, symmetric=False)
+    marked = torch.unique(torch.randint(0, C, (200,), generator=g)).to(cuda)
+    bits = torch.zeros((C + 31) // 32, dtype=torch.int32, device=cuda)
+    cmask = torch.zeros(C, dtype=torch.uint8, device=cuda)
+    ops.rows_mark(cmask, [(marked, 0)], 1, bits=bits)
+    X = torch.full((C, d), float("nan"), device=cuda)
+    X[marked] = torch.randn(marked.numel(), d, device=cuda)
+    Xz = torch.where(cmask.bool().unsqueeze(1), X, torch.zeros_like(X))
+    A1 = torch.randn(R, d, device=cuda)
+    ref = torch.empty(R, d, device=cuda)
+    ops.spmm_launch(adj, Xz, Y2=ref, alpha=0.5, A1=A1, beta1=0.25)
+    got = torch.full((R, d), 7.0, device=cuda)
+    ops.spmm_sparse_rect(adj, bits, X, got, alpha=0.5, A1=A1, beta1=0.25)
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+    assert (ops._sparse_plan(adj) is not None) == planned
 
 
 @pytest.mark.parametrize("frac", [0.02, 0.3])
