@@ -14,6 +14,7 @@ infonce_loss(H, tau)     CL_loss                           pricai_modelx.py:354-
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -866,6 +867,46 @@ def grad_buffer(w: torch.Tensor) -> torch.Tensor:
     return torch.empty_like(w)
 
 
+class _GraphBprForward:
+    """The forward of _GraphBpr computed ahead of its autograd node (graph_bpr_begin), possibly on a
+    branch stream: the outputs and the tensors the backward reads."""
+    __slots__ = ("out", "item_rows", "ui_all", "u", "p", "n", "pn", "ws", "stream", "done", "args", "defer")
+
+
+@torch.no_grad()
+def _graph_bpr_forward(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma, stream=None):
+    U, I = user_w.shape[0], item_w.shape[0]
+    dev = user_w.device
+    native.require_device(user_w, item_w, ingre_w, u, p, n)
+    for t in (user_w, item_w, ingre_w):
+        if t.dtype != torch.float32 or t.shape[1] != 64 or not t.is_contiguous():
+            raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
+    u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
+    # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
+    ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
+    rows = [(u, 0), (p, U), (n, U)]
+    if L_ui == 1:
+        ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
+        spmm_ex(ui_adj, user_w, ir_all, U, Y2=ui_all, alpha=0.5, A1=user_w, A1_hi=ir_all, beta1=0.5,
+                rows=rows, region="spmm_rows")
+    else:
+        ui_all = _prop_fwd_split(ui_adj, user_w, ir_all, U, L_ui)
+    B = int(u.numel())
+    lib = native.lib()
+    ws = native.workspace(lib.fr_bpr_workspace(B), dev)
+    out = torch.empty(5, dtype=torch.float32, device=dev)
+    items = ui_all[U:]
+    item_rows = torch.empty(2 * B, 64, dtype=torch.float32, device=dev)  # [items[p] ; items[n]] (= items[pn])
+    native.check(lib.fr_bpr_fwd_rows(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
+                                     item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                     _f(gamma), out.data_ptr(), item_rows.data_ptr(), 64, ws.data_ptr(), ws.numel(),
+                                     native.stream_of(user_w)), "fr_bpr_fwd_rows")
+    f = _GraphBprForward()
+    f.out, f.item_rows, f.ui_all, f.u, f.p, f.n, f.pn, f.ws, f.stream = out, item_rows, ui_all, u, p, n, pn, ws, stream
+    f.defer = ingre_w.__dict__.get("_fr_defer_rows")
+    return f
+
+
 class _GraphBpr(torch.autograd.Function):
     """HealthRec's propagation + BPR + user/item EmbLoss (cikm_model.py:182-208, 255-279) as one
     autograd node:
@@ -884,47 +925,50 @@ class _GraphBpr(torch.autograd.Function):
     the graph) with the same split-table reads and writes."""
 
     @staticmethod
-    def forward(ctx, user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma, det):
-        U, I = user_w.shape[0], item_w.shape[0]
-        NI = ingre_w.shape[0] - 1
-        dev = user_w.device
-        native.require_device(user_w, item_w, ingre_w, u, p, n)
-        for t in (user_w, item_w, ingre_w):
-            if t.dtype != torch.float32 or t.shape[1] != 64 or not t.is_contiguous():
-                raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
-        u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
-        # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
-        ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
-        rows = [(u, 0), (p, U), (n, U)]
-        if L_ui == 1:
-            ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
-            spmm_ex(ui_adj, user_w, ir_all, U, Y2=ui_all, alpha=0.5, A1=user_w, A1_hi=ir_all, beta1=0.5,
-                    rows=rows, region="spmm_rows")
-        else:
-            ui_all = _prop_fwd_split(ui_adj, user_w, ir_all, U, L_ui)
-        B = int(u.numel())
-        lib = native.lib()
-        ws = native.workspace(lib.fr_bpr_workspace(B), dev)
-        out = torch.empty(5, dtype=torch.float32, device=dev)
-        items = ui_all[U:]
-        item_rows = torch.empty(2 * B, 64, dtype=torch.float32, device=dev)  # [items[p] ; items[n]] (= items[pn])
-        native.check(lib.fr_bpr_fwd_rows(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
-                                         item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
-                                         _f(gamma), out.data_ptr(), item_rows.data_ptr(), 64, ws.data_ptr(), ws.numel(),
-                                         native.stream_of(user_w)), "fr_bpr_fwd_rows")
+    def forward(ctx, user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma, det, pre=None):
+        if pre is None:
+            pre = _graph_bpr_forward(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma)
+        out, item_rows, ui_all, u, p, n, pn, ws = pre.out, pre.item_rows, pre.ui_all, pre.u, pre.p, pre.n, pre.pn, pre.ws
+        U, I, NI = user_w.shape[0], item_w.shape[0], ingre_w.shape[0] - 1
         ctx.save_for_backward(user_w, item_w, ui_all, u, p, n, pn)
         ctx.ingre_w = ingre_w  # the parameter itself (grad_buffer looks up its gradient destination)
-        ctx.defer = ingre_w.__dict__.get("_fr_defer_rows")
+        ctx.defer = pre.defer  # (taken at the forward's start: embedding_norms pops the slot meanwhile)
+        ctx.branch = pre.stream  # the branch stream the forward ran on (None: the current stream)
         ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
         return out[0], out[4:5], item_rows
 
     @staticmethod
     def backward(ctx, g_mf, g_emb, g_rows):
+        side = ctx.branch
+        if side is None:
+            return _GraphBpr._backward_here(ctx, g_mf, g_emb, g_rows)
+        # branch: the kernels go to the branch stream, which waits only for what the current stream
+        # has issued so far (the loss heads' backward); the rest of the backward (encoder, fusion,
+        # projections) proceeds on the current stream meanwhile.  The backward pass ends by joining
+        # (_join_branch, an autograd final callback): the current stream waits for the branch, then
+        # the deferred ingredient rows are added into its d ingre.
+        main = torch.cuda.current_stream(side.device)
+        side.wait_stream(main)
+        for g in (g_mf, g_emb, g_rows):
+            if g is not None:
+                g.record_stream(side)
+        with torch.cuda.stream(side):
+            grads = _GraphBpr._backward_here(ctx, g_mf, g_emb, g_rows, drain=False)
+            done = torch.cuda.Event()
+            done.record(side)
+        _BRANCH_PENDING.append((done, ctx.defer, ctx.ingre_w))  # (no reference to the returned grads:
+        # AccumulateGrad adopts them as .grad only when nothing else holds them)
+        if len(_BRANCH_PENDING) == 1:
+            torch.autograd.Variable._execution_engine.queue_callback(_join_branch)
+        return grads
+
+    @staticmethod
+    def _backward_here(ctx, g_mf, g_emb, g_rows, drain=True):
         user_w, item_w, ui_all, u, p, n, pn = ctx.saved_tensors
         ri_adj, ui_adj, L_ri, L_ui, gamma, det, ws, U, I, NI = ctx.meta
         dev = user_w.device
         if not det and L_ui == 1 and g_rows is not None and g_mf is not None and g_emb is not None:
-            return _GraphBpr._backward_fast(ctx, g_mf, g_emb, g_rows)
+            return _GraphBpr._backward_fast(ctx, g_mf, g_emb, g_rows, drain)
         g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
         g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
         gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
@@ -965,12 +1009,12 @@ class _GraphBpr(torch.autograd.Function):
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_bpr_bwd(*common, None, None, d_user.data_ptr(), d_item.data_ptr(), det, ws.data_ptr(),
                                         ws.numel(), s), "fr_bpr_bwd")
-        if ctx.defer is not None:
+        if ctx.defer is not None and drain:
             ctx.defer.drain(d_ingre)
-        return (d_user, d_item, d_ingre) + (None,) * 10
+        return (d_user, d_item, d_ingre) + (None,) * 11
 
     @staticmethod
-    def _backward_fast(ctx, g_mf, g_emb, g_rows):
+    def _backward_fast(ctx, g_mf, g_emb, g_rows, drain=True):
         """Float-atomic path for one UI layer: mark the batch rows in the column mask and its bitmask
         and zero them in the persistent UI upstream gradient (no full fill: its other rows are never
         read, the backward gates its residual read by the same mask); the BPR scatter (+ the KD rows'
@@ -1021,9 +1065,70 @@ class _GraphBpr(torch.autograd.Function):
                                                  d_ingre[NI:].data_ptr(), 64, native.ptr(bits), ws.data_ptr(),
                                                  ws.numel(), s),
                          "fr_graph_bpr_finish")
-        if ctx.defer is not None:
+        if ctx.defer is not None and drain:
             ctx.defer.drain(d_ingre)  # the encoder input rows' gradient, atomically into d ingre
-        return (d_user, d_item, d_ingre) + (None,) * 10
+        return (d_user, d_item, d_ingre) + (None,) * 11
+
+
+# graph_bpr_begin / _end on a branch stream (HealthRec's propagation beside its encoder); FR_BRANCH_STREAMS=0: off
+BRANCH_STREAMS = os.environ.get("FR_BRANCH_STREAMS", "1") != "0"
+_BRANCH_STREAM = {}
+_BRANCH_PENDING = []    # (event, deferred rows, ingredient table) of branch backwards not joined yet
+
+
+def _branch_stream(device):
+    s = _BRANCH_STREAM.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device)
+        _BRANCH_STREAM[device] = s
+    return s
+
+
+def _join_branch():
+    """End of a backward pass that ran graph_bpr's backward on the branch stream: the current stream
+    waits for it, then adds the deferred ingredient rows into d ingre (after both are complete)."""
+    pend = list(_BRANCH_PENDING)
+    _BRANCH_PENDING.clear()
+    for done, defer, ingre_w in pend:
+        torch.cuda.current_stream(ingre_w.device).wait_event(done)
+        if defer is not None and ingre_w.grad is not None:
+            defer.drain(ingre_w.grad)
+
+
+def graph_bpr_begin(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
+    """Start graph_bpr's forward (the RI + UI propagations and the fused BPR) on the branch stream,
+    so that the caller's next work (HealthRec: the ingredient encoder, projections, modal fusion,
+    which read none of its outputs) overlaps it; graph_bpr_end joins it and creates the autograd
+    node, whose backward then runs on the branch stream too, beside the encoder backward.  Without a
+    GPU, in the deterministic mode or with BRANCH_STREAMS off, the forward runs here."""
+    args = (user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma)
+    if torch.is_grad_enabled() and ingre_w.requires_grad and not _DETERMINISTIC:
+        ingre_w.__dict__["_fr_defer_rows"] = _DeferredRows()
+    if not (BRANCH_STREAMS and user_w.is_cuda):
+        f = _graph_bpr_forward(*args)
+        f.done, f.args = None, args
+        return f
+    main = torch.cuda.current_stream(user_w.device)
+    side = _branch_stream(user_w.device)
+    side.wait_stream(main)
+    for t in (u, p, n, pn):
+        t.record_stream(side)
+    with torch.cuda.stream(side):
+        f = _graph_bpr_forward(*args, stream=side)
+        f.done = torch.cuda.Event()
+        f.done.record(side)
+    f.args = args
+    return f
+
+
+def graph_bpr_end(f):
+    """(BPRLoss, EmbLoss [1], [ui_items[pos]; ui_items[neg]]) of a graph_bpr_begin; see _GraphBpr."""
+    if f.done is not None:
+        main = torch.cuda.current_stream(f.out.device)
+        main.wait_event(f.done)
+        f.out.record_stream(main)
+        f.item_rows.record_stream(main)
+    return _GraphBpr.apply(*f.args, _DETERMINISTIC, f)
 
 
 def graph_bpr(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
@@ -1033,7 +1138,7 @@ def graph_bpr(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, 
     if torch.is_grad_enabled() and ingre_w.requires_grad and not _DETERMINISTIC:
         ingre_w.__dict__["_fr_defer_rows"] = _DeferredRows()
     return _GraphBpr.apply(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma,
-                           _DETERMINISTIC)
+                           _DETERMINISTIC, None)
 
 
 class _DeferredRows:

@@ -154,11 +154,12 @@ class HealthRec(GeneralRecommender):
         fused_graph = self._fused_graph(user)
         if fused_graph:
             # both propagations + BPR + the user/item EmbLoss terms as one node: split-table reads and
-            # writes (no cat / split glue), the UI propagation evaluated at the batch rows only
-            mf_loss, emb3, item_rows = ops.graph_bpr(self.user_embedding.weight, self.item_embedding.weight,
-                                                     self.ingre_embedding.weight, user, pos_item, neg_item, all_item,
-                                                     self.ri_norm_adj, self.norm_adj_matrix, self.n_layers,
-                                                     self.ui_layers)
+            # writes (no cat / split glue), the UI propagation evaluated at the batch rows only.  Started
+            # on a branch stream: the encoder / projection / fusion work below overlaps it (and its
+            # backward overlaps theirs); joined before the KD head reads its item rows
+            branch = ops.graph_bpr_begin(self.user_embedding.weight, self.item_embedding.weight,
+                                         self.ingre_embedding.weight, user, pos_item, neg_item, all_item,
+                                         self.ri_norm_adj, self.norm_adj_matrix, self.n_layers, self.ui_layers)
         else:
             ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
@@ -199,7 +200,9 @@ class HealthRec(GeneralRecommender):
             health_in = F.normalize(item_health).mean(dim=1)
         # torch.cat([item_all[pos], item_all[neg]]) (cikm_model.py:256-257, 263): the BPR kernel's own
         # item rows; their KD gradient is added inside the BPR backward's scatter
-        if not fused_graph:
+        if fused_graph:
+            mf_loss, emb3, item_rows = ops.graph_bpr_end(branch)
+        else:
             mf_loss, emb3, item_rows = ops.bpr_emb_loss(ui_all, None, self.user_embedding.weight,
                                                         self.item_embedding.weight, user, pos_item, neg_item,
                                                         item_rows=True, item_offset=self.n_users)
