@@ -20,6 +20,7 @@ dense table's zero fill and gradient read (8 of 32 bytes per parameter).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -33,6 +34,11 @@ def adam_rows_bytes(numel: int, rows: int, compact: int) -> int:
     """Algorithmic HBM bytes of the row-gradient Adam on one table: p, m, v read + written (24 B per
     parameter), the row map (4 B per row) and the compact gradient rows (read once)."""
     return 24 * numel + 4 * rows + 4 * compact
+
+
+# FusedAdam.step: the factored row gradients and the row tables' update on a side stream (forked
+# at the projection backward); FR_ROWS_SIDE_STREAM=0: on the current stream after the backward
+ROWS_SIDE_STREAM = os.environ.get("FR_ROWS_SIDE_STREAM", "1") != "0"
 
 
 class RowGrads:
@@ -53,6 +59,7 @@ class RowGrads:
         # a (weight, pointer, numel) match below therefore names the same ids
         self._prefetched = []
         self._side = None
+        self.factored_event = None
 
     def stash_factored(self, weight, padding_idx, ids, dY, W):
         if id(weight) in self.pending or id(weight) in self.factored:  # repeated backward: explicit rows
@@ -62,6 +69,9 @@ class RowGrads:
             self.stash(weight, padding_idx, ids, dY @ W)
             return
         self.factored[id(weight)] = (weight, padding_idx, ids, dY, W)
+        if dY.is_cuda:  # where the backward stream stood when dY was written (FusedAdam.step forks here)
+            self.factored_event = torch.cuda.Event()
+            self.factored_event.record(torch.cuda.current_stream(dY.device))
 
     def stash(self, weight, padding_idx, ids, G):
         e = self.pending.get(id(weight))
@@ -75,6 +85,7 @@ class RowGrads:
         self.join_background()
         self.pending.clear()
         self.factored.clear()
+        self.factored_event = None
         self._prefetched.clear()
 
     def catch_up_rows(self, weight, ids):
@@ -373,8 +384,25 @@ class FusedAdam(torch.optim.Optimizer):
                 loss = closure()
         lib = native.lib()
         self.row_grads.join_background()
-        # factored row gradients read the projection weights: materialise them before any update
-        prepared = self._prepare_factored(lib) if (self.row_grads.factored and part != "dense") else {}
+        # factored row gradients read the projection weights: materialise them before any update.
+        # A full step runs them, and then the row tables' update, on a side stream that forks where
+        # the backward wrote dY (the projection backward, before the encoder backward): both leave
+        # the tail of the step and overlap the encoder backward and the dense update
+        side = self._rows_side() if (part == "all" and self.row_grads.factored) else None
+        w_read = None
+        if side is not None:
+            side.wait_event(self.row_grads.factored_event)
+            if self.row_grads._side is not None:  # the background slice replay (lazy state) first
+                side.wait_stream(self.row_grads._side)
+            for w, _, ids, dY, W in self.row_grads.factored.values():
+                ids.record_stream(side)
+                dY.record_stream(side)
+            with torch.cuda.stream(side):
+                prepared = self._prepare_factored(lib)
+                w_read = torch.cuda.Event()
+                w_read.record(side)
+        else:
+            prepared = self._prepare_factored(lib) if (self.row_grads.factored and part != "dense") else {}
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
             plist, rows = [], []
@@ -437,14 +465,34 @@ class FusedAdam(torch.optim.Optimizer):
             # slot this step never wrote
             self._flush_tables(group, lazy_dense)
             if plist:
+                if w_read is not None:
+                    torch.cuda.current_stream(dev).wait_event(w_read)  # (long done: forked early)
                 with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
                     self._launch_dense(lib, plist, hyper)
             for p in lazy_dense:
                 st = self.state[p]
                 st["lazy_last"].copy_(st["step"].to(torch.int32).expand(p.shape[0]))
             if rows:
-                self._launch_rows(lib, rows, hyper)
+                if side is not None:
+                    with torch.cuda.stream(side):
+                        self._launch_rows(lib, rows, hyper[:-1] + (side.cuda_stream,))
+                else:
+                    self._launch_rows(lib, rows, hyper)
+        if side is not None:
+            torch.cuda.current_stream(side.device).wait_stream(side)
         return loss
+
+    def _rows_side(self):
+        """The stream of the row tables' part of a full step (None: not on a GPU, or no fork point)."""
+        ev = self.row_grads.factored_event
+        if ev is None or not ROWS_SIDE_STREAM:
+            return None
+        dev = next(iter(self.row_grads.factored.values()))[3].device
+        if dev.type != "cuda":
+            return None
+        if getattr(self, "_rows_stream", None) is None or self._rows_stream.device != dev:
+            self._rows_stream = torch.cuda.Stream(dev)
+        return self._rows_stream
 
     def _arrays(self, plist, grads):
         n = len(plist)
