@@ -67,7 +67,7 @@ class RowExchange:
             return self.sink.prefetch_rows(pairs)
         for w, ids in pairs:
             self.catch_up_rows(w, ids)
-        return lambda: None
+        return lambda stream=None: None  # caught up inline on the current stream
 
     def join_background(self):
         """Join the sink's background slice replay (the end of a graphed step's part A: a captured

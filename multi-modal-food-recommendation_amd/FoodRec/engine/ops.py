@@ -1072,6 +1072,7 @@ class _GraphBpr(torch.autograd.Function):
 
 # graph_bpr_begin / _end on a branch stream (HealthRec's propagation beside its encoder); FR_BRANCH_STREAMS=0: off
 BRANCH_STREAMS = os.environ.get("FR_BRANCH_STREAMS", "1") != "0"
+AUX_STREAM = os.environ.get("FR_AUX_STREAM", "0") == "1"  # ops.aux_stream (FR_AUX_STREAM=1: on; measured no gain)
 _BRANCH_STREAM = {}
 _BRANCH_PENDING = []    # (event, deferred rows, ingredient table) of branch backwards not joined yet
 
@@ -1081,6 +1082,19 @@ def _branch_stream(device):
     if s is None:
         s = torch.cuda.Stream(device)
         _BRANCH_STREAM[device] = s
+    return s
+
+
+def aux_stream(device):
+    """A second branch stream (HealthRec's modal projections beside its encoder), or None when
+    branching is off."""
+    if not (BRANCH_STREAMS and AUX_STREAM):
+        return None
+    key = ("aux", str(device))
+    s = _BRANCH_STREAM.get(key)
+    if s is None:
+        s = torch.cuda.Stream(device)
+        _BRANCH_STREAM[key] = s
     return s
 
 

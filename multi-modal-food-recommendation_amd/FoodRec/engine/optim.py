@@ -100,10 +100,10 @@ class RowGrads:
     def prefetch_rows(self, pairs):
         """Catch up [(weight, ids), ...] on a side stream, overlapping whatever the caller runs next
         (HealthRec: the SpMM propagation, which reads none of these tables).  Returns a callable that
-        makes the current stream wait for it; call it before the gathers.  Graph-capturable (fork /
-        join of the capture stream)."""
+        makes a stream (default: the current one) wait for it; call it before the gathers.
+        Graph-capturable (fork / join of the capture stream)."""
         if self.catch_up is None or not pairs or not pairs[0][0].is_cuda:
-            return lambda: None
+            return lambda stream=None: None
         main = torch.cuda.current_stream(pairs[0][0].device)
         if self._side is None:
             self._side = torch.cuda.Stream(pairs[0][0].device)
@@ -126,7 +126,7 @@ class RowGrads:
                 # the step; joined before the optimiser touches any lazy state (join_background)
                 self.catch_up_slice([w for w, _ in pairs])
                 self._bg_join = lambda: main.wait_stream(side)
-        return lambda: main.wait_event(caught)
+        return lambda stream=None: (stream if stream is not None else main).wait_event(caught)
 
     def join_background(self):
         """Make the current stream wait for the background slice replay (before any optimiser

@@ -150,7 +150,8 @@ class HealthRec(GeneralRecommender):
         # the propagation (memory-bound, other tables) runs (data parallel: RowExchange hands it to
         # its sink, the same FusedAdam row state)
         join = xg.prefetch_rows([(t.weight, all_item) for t in self._row_tables()]) \
-            if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) else (lambda: None)
+            if xg is not None and hasattr(xg, "prefetch_rows") and self._fused_projection(all_item) \
+            else (lambda stream=None: None)
         fused_graph = self._fused_graph(user)
         if fused_graph:
             # both propagations + BPR + the user/item EmbLoss terms as one node: split-table reads and
@@ -162,6 +163,21 @@ class HealthRec(GeneralRecommender):
                                          self.ri_norm_adj, self.norm_adj_matrix, self.n_layers, self.ui_layers)
         else:
             ui_all, _ = self._propagate()  # one [users | items] table: one gradient buffer in the BPR backward
+        # the modal projections read only the (caught-up) image / text rows: on a second branch
+        # stream they overlap the encoder forward, and autograd runs their backward there too, beside
+        # the encoder backward; joined before the fusion reads mm_query
+        proj = self._fused_projection(all_item)
+        aux = ops.aux_stream(all_item.device) if proj else None
+        if aux is not None:
+            main = torch.cuda.current_stream(all_item.device)
+            aux.wait_stream(main)
+            join(aux)
+            all_item.record_stream(aux)
+            with torch.cuda.stream(aux):
+                mm_query = ops.modal_projection(all_item, [(self.image_embedding.weight, self.image_trs),
+                                                           (self.text_embedding.weight, self.text_trs)], exchange=xg)
+                projected = torch.cuda.Event()
+                projected.record(aux)
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
         health_level = _pn(batch_data, "hl_mh")
         ingredients = _pn(batch_data, "ingre_code")
@@ -177,9 +193,12 @@ class HealthRec(GeneralRecommender):
         encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
-        join()
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
-        if self._fused_projection(all_item):
+        if aux is not None:
+            main.wait_event(projected)
+            mm_query.record_stream(main)
+        elif proj:
+            join()
             # gathers folded into the projection GEMMs; the tables' gradient stays factored (dY, W)
             mm_query = ops.modal_projection(all_item, [(self.image_embedding.weight, self.image_trs),
                                                        (self.text_embedding.weight, self.text_trs)], exchange=xg)

@@ -8,7 +8,7 @@ cd $R
 for spec in "$@"; do
   tag=${spec%%:*}; rest=${spec#*:}; lib=${rest%%:*}; envs=${rest#*:}; [ "$envs" = "$rest" ] && envs=""
   if [ "$lib" = "head" ]; then L=""; else L="FR_ENGINE_LIB=$R/ab/libfr_engine_$lib.so"; fi
-  env $L $envs timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-spmm-10m --no-config3 --no-config5 \
+  env $L $envs timeout -k 10 300 python bench.py --steps ${AB_STEPS:-50} --warmup 10 --no-spmm-10m --no-config3 --no-config5 \
     --no-config1 --no-cpu-baseline --no-eval > $OUT/ab_$tag.json 2> $OUT/ab_$tag.err || { echo "$tag failed"; tail -5 $OUT/ab_$tag.err; exit 1; }
   python3 - "$OUT/ab_$tag.json" "$tag" <<'PY'
 import json, sys
