@@ -41,8 +41,8 @@ def _args():
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one process per GPU); N > 1 without a torch.distributed environment starts "
                          "the N ranks itself under torch.distributed.run (default: WORLD_SIZE, else 1)")
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="healthrec_allrecipes", choices=["healthrec_allrecipes"])
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
