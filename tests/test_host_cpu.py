@@ -246,3 +246,31 @@ def test_wide_goldens_match_generator(name, shape):
     from gen_golden import wide_digest
     from FoodRec.utils.synthetic import make_synthetic
     assert str(golden(f"wide_{name}_{shape}.npz")["digest"]) == wide_digest(make_synthetic(shape, 0, negatives=False))
+
+
+@pytest.mark.parametrize("edges", [64, 2048])
+def test_sparse_block_plan_covers_every_edge_once(edges):
+    """ops.sparse_block_plan (the sparse-upstream kernel's edge-balanced row blocks): every edge in
+    exactly one block, blocks of at most 64 whole rows and 2 x ``edges`` edges, heavy rows (more than
+    ``edges`` edges) cut into consecutive chunks of at most ``edges`` edges and listed once in
+    split_rows, empty rows and a trailing empty row covered."""
+    from FoodRec.engine.ops import sparse_block_plan
+    rng = np.random.default_rng(edges)
+    deg = np.concatenate([rng.integers(0, 30, 3000), [5 * edges + 3, 0, 0, edges, edges + 1],
+                          rng.zipf(1.6, 500).clip(max=40 * edges), [0]])
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    blocks, split_rows = sparse_block_plan(rp, 64, edges)
+    cover = np.zeros(rp[-1], np.int32)
+    rows_seen = np.zeros(len(deg), np.int32)
+    for r0, r1, e0, e1 in blocks:
+        cover[e0:e1] += 1
+        if e0 == rp[r0] and e1 == rp[r1]:  # whole rows
+            assert 0 < r1 - r0 <= 64 and e1 - e0 <= 2 * edges
+            rows_seen[r0:r1] += 1
+        else:  # a chunk of one heavy row
+            assert r1 - r0 == 1 and r0 in split_rows and 0 < e1 - e0 <= edges
+            assert rp[r0] <= e0 < e1 <= rp[r1]
+    assert (cover == 1).all()
+    assert np.array_equal(np.sort(split_rows), np.nonzero(deg > edges)[0])
+    assert (rows_seen[deg <= edges] == 1).all() and (rows_seen[deg > edges] == 0).all()
+    assert (np.diff(blocks[:, 2]) >= 0).all()  # in edge order
