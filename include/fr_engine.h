@@ -458,8 +458,7 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * (opaque to the caller; only fr_encoder_bwd reads it).
  * Backward writes dx and the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
  * gradients concatenated in d_params order); d_partials [fr_encoder_partials(n_seq, L)] floats of
- * per-workgroup partials, summed in workgroup order (deterministic).  d_grad = NULL: the partials
- * are left unreduced for fr_encoder_reduce (which a caller may run on another stream).
+ * per-workgroup partials, summed in workgroup order (deterministic).
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_encoder_partials(int64_t n_seq, int L);
 int64_t fr_encoder_grad_numel(void);
@@ -477,7 +476,6 @@ int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, i
                    const float* d_fact, const float* d_dact, const float* d_y2, const float* d_st1,
                    const float* d_st2, float* d_dx,
                    float* d_grad, float* d_partials, int64_t partial_floats, void* stream);
-int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_grad, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused modal fusion of HealthRec (models/cikm_model.py:245-249 with target_attention_layer,
@@ -492,8 +490,7 @@ int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_gr
  * d_ln: 4 device pointers {mm_target_atten.ln.weight, .bias, ingre_target_atten.ln.weight, .bias}
  * (both with the same eps).  L in {4, 5, 8, 10, 16, 20}.
  * Backward recomputes the forward and writes d_denc, d_dquery and d_dln (float [4][32]: the four
- * LayerNorm parameter gradients, block partials in d_partials summed in block order; d_dln = NULL:
- * left unreduced for fr_modal_fusion_reduce).
+ * LayerNorm parameter gradients, block partials in d_partials summed in block order).
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_modal_fusion_partials(int64_t n_items);
 int fr_modal_fusion_fwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
@@ -503,7 +500,6 @@ int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, const int64_t*
                         int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps,
                         const float* d_dknow, const float* d_dhin, float* d_denc, float* d_dquery, float* d_dln,
                         float* d_partials, int64_t partial_floats, void* stream);
-int fr_modal_fusion_reduce(const float* d_partials, int64_t n_items, float* d_dln, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused health / KD loss head of HealthRec (models/cikm_model.py:249-264,304-308), over n items:

@@ -75,8 +75,6 @@ _SIGS = {
     "fr_spmm_sparse_upstream_blocks": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p,
                                                c_void_p, c_int64, c_int64, POINTER(FrTab), c_float, POINTER(FrTab),
                                                c_float, c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
-    "fr_encoder_reduce": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p]),
-    "fr_modal_fusion_reduce": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_int64, c_void_p]),

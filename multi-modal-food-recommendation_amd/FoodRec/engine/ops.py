@@ -1109,52 +1109,6 @@ def _join_branch():
             defer.drain(ingre_w.grad)
 
 
-# parameter-gradient reductions (the encoder's and the modal fusion's ordered sums of per-workgroup
-# partials) on a side stream: nothing in the backward reads them, only the optimiser, so they leave
-# the critical path (encoder backward chain) and run beside it; joined at the end of the backward.
-# FR_DEFER_REDUCE=0: in line.
-DEFER_REDUCE = os.environ.get("FR_DEFER_REDUCE", "1") != "0"
-_REDUCE_PENDING = []
-
-
-def _join_reductions():
-    pend = list(_REDUCE_PENDING)
-    _REDUCE_PENDING.clear()
-    for done, dev in pend:
-        torch.cuda.current_stream(dev).wait_event(done)
-
-
-def _deferred_reduce(params, keep, launch) -> bool:
-    """Run ``launch(stream)`` (a reduction writing only ``params``' gradients) on the reduction side
-    stream when safe: a GPU backward, BRANCH_STREAMS on, and every parameter's .grad still None
-    (autograd then adopts the returned gradient tensors without reading them before the join).
-    ``keep``: tensors the launch reads (recorded for the side stream).  False: run it in line."""
-    if not (DEFER_REDUCE and BRANCH_STREAMS and all(p.is_cuda and p.grad is None for p in params)):
-        return False
-    dev = params[0].device
-    main = torch.cuda.current_stream(dev)
-    side = _branch_stream_k(dev, "reduce")
-    side.wait_stream(main)
-    for t in keep:
-        t.record_stream(side)
-    launch(side.cuda_stream)
-    done = torch.cuda.Event()
-    done.record(side)
-    _REDUCE_PENDING.append((done, dev))
-    if len(_REDUCE_PENDING) == 1:
-        torch.autograd.Variable._execution_engine.queue_callback(_join_reductions)
-    return True
-
-
-def _branch_stream_k(device, k):
-    key = ("branch", str(device), k)
-    s = _BRANCH_STREAM.get(key)
-    if s is None:
-        s = torch.cuda.Stream(device)
-        _BRANCH_STREAM[key] = s
-    return s
-
-
 def graph_bpr_begin(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
     """Start graph_bpr's forward (the RI + UI propagations and the fused BPR) on the branch stream,
     so that the caller's next work (HealthRec: the ingredient encoder, projections, modal fusion,
@@ -1628,7 +1582,6 @@ class _EncoderLayer(torch.autograd.Function):
         defer_increment(cfg.counter)  # advanced by the step's fr_step_book (or before its next read)
         ctx.cfg = cfg
         ctx.has_mask = mask is not None
-        ctx.params_ref = params  # the parameters themselves (a deferred reduction checks their .grad)
         ctx.save_for_backward(x, mask if mask is not None else seed_used, qkv, cx, y1, fact, dact, y2, st1,
                               st2, seed_used, *params)
         return out
@@ -1645,22 +1598,13 @@ class _EncoderLayer(torch.autograd.Function):
         nparts = lib.fr_encoder_partials(NS, L)
         part = torch.empty(nparts, dtype=torch.float32, device=x.device)
         pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
-        # the weight-gradient reduction runs beside the next layer's backward when it can
-        # (_deferred_reduce); the HIP-event timing region (bench's roofline) covers both launches
-        # only in line
-        defer = not profiling.active() and ctx.params_ref is not None and all(
-            q.grad is None for q in ctx.params_ref)
         with profiling.region("encoder_bwd", encoder_bytes(NS, L, True)):
             native.check(lib.fr_encoder_bwd(
                 g.data_ptr(), x.data_ptr(), mask.data_ptr() if ctx.has_mask else None, NS, L, pp, cfg.eps,
                 cfg.drop, cfg.seed, cfg.gelu, seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(),
                 fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
-                None if defer else grad.data_ptr(),
+                grad.data_ptr(),
                 part.data_ptr(), nparts, native.stream_of(g)), "fr_encoder_bwd")
-        if defer and not _deferred_reduce(list(ctx.params_ref), (part, grad), lambda s: native.check(
-                lib.fr_encoder_reduce(part.data_ptr(), NS, L, grad.data_ptr(), s), "fr_encoder_reduce")):
-            native.check(lib.fr_encoder_reduce(part.data_ptr(), NS, L, grad.data_ptr(), native.stream_of(g)),
-                         "fr_encoder_reduce")
         grads = torch.split(grad, [p.numel() for p in params])
         return (dx, None, None) + tuple(gr.view(p.shape) for gr, p in zip(grads, params))
 
@@ -1714,7 +1658,6 @@ class _ModalFusion(torch.autograd.Function):
                          "fr_modal_fusion_fwd")
         ctx.save_for_backward(enc, query, ids, num, ga, ba, gb, bb)
         ctx.pad_id, ctx.eps = int(pad_id), float(eps)
-        ctx.ln_ref = (ga, ba, gb, bb)  # the LayerNorm parameters themselves
         return know, hin
 
     @staticmethod
@@ -1730,17 +1673,11 @@ class _ModalFusion(torch.autograd.Function):
         nparts = lib.fr_modal_fusion_partials(n)
         part = torch.empty(nparts, dtype=torch.float32, device=enc.device)
         lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
-        defer = not profiling.active() and all(q.grad is None for q in ctx.ln_ref)
         with profiling.region("modal_fusion", fusion_bytes(n, L, True)):
             native.check(lib.fr_modal_fusion_bwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
                                                  ctx.pad_id, n, L, lnp, ctx.eps, dknow.data_ptr(), dhin.data_ptr(),
-                                                 denc.data_ptr(), dq.data_ptr(), None if defer else dln.data_ptr(),
-                                                 part.data_ptr(), nparts, native.stream_of(enc)), "fr_modal_fusion_bwd")
-        # the LayerNorm-parameter reduction beside the encoder backward when it can (_deferred_reduce)
-        if defer and not _deferred_reduce(list(ctx.ln_ref), (part, dln), lambda s: native.check(
-                lib.fr_modal_fusion_reduce(part.data_ptr(), n, dln.data_ptr(), s), "fr_modal_fusion_reduce")):
-            native.check(lib.fr_modal_fusion_reduce(part.data_ptr(), n, dln.data_ptr(), native.stream_of(enc)),
-                         "fr_modal_fusion_reduce")
+                                                 denc.data_ptr(), dq.data_ptr(), dln.data_ptr(), part.data_ptr(),
+                                                 nparts, native.stream_of(enc)), "fr_modal_fusion_bwd")
         return denc, dq, None, None, None, None, dln[0], dln[1], dln[2], dln[3]
 
 

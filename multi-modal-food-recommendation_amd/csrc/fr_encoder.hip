@@ -1157,7 +1157,6 @@ int launch_bwd(const BwdArgs& a, float* grad, hipStream_t s) {
   const int64_t nwg = fr::ceil_div(a.ns, ROWS / L);
   hipLaunchKernelGGL(enc_bwd_kernel<L>, dim3((unsigned)nwg), dim3(NT), 0, s, a);
   FR_LAUNCH_CHECK();
-  if (!grad) return FR_OK;  // the caller reduces the partials itself (fr_encoder_reduce)
   hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(a.part), (int)nwg, reinterpret_cast<float4*>(grad));
   FR_LAUNCH_CHECK();
@@ -1191,20 +1190,6 @@ extern "C" int64_t fr_encoder_partials(int64_t n_seq, int L) {
 }
 
 extern "C" int64_t fr_encoder_grad_numel(void) { return NPART; }
-
-// the ordered reduction of fr_encoder_bwd's per-workgroup weight-gradient partials into the flat
-// gradient, on its own (fr_encoder_bwd called with d_grad = NULL leaves them unreduced): lets a
-// caller run it on another stream, off the backward's critical path
-extern "C" int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_grad, void* stream) {
-  FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
-  FR_REQUIRE(d_partials && d_grad && fr::aligned16(d_partials) && fr::aligned16(d_grad), "null or unaligned operand");
-  const int64_t nwg = fr::ceil_div(n_seq, ROWS / L);
-  hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(d_partials), (int)nwg,
-                     reinterpret_cast<float4*>(d_grad));
-  FR_LAUNCH_CHECK();
-  return FR_OK;
-}
 
 // floats of the forward's dact buffer (per-workgroup MFMA fragment layout, ROWS x FF per workgroup)
 extern "C" int64_t fr_encoder_dact_numel(int64_t n_seq, int L) {
@@ -1260,7 +1245,8 @@ extern "C" int fr_encoder_bwd(const float* d_dout, const float* d_x, const float
                               int64_t partial_floats, void* stream) {
   FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
   FR_REQUIRE(d_dout && d_x && d_seed_in && d_qkv && d_ctx && d_y1 && d_fact && d_dact && d_y2 && d_st1 && d_st2 &&
-                 d_dx && d_partials,
+                 d_dx &&
+                 d_grad && d_partials,
              "null operand");
   FR_REQUIRE(fr::aligned16(d_dout) && fr::aligned16(d_x) && fr::aligned16(d_dx) && fr::aligned16(d_grad) &&
                  fr::aligned16(d_partials) && fr::aligned16(d_qkv) && fr::aligned16(d_ctx) && fr::aligned16(d_y1) &&

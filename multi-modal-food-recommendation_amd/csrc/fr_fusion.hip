@@ -353,24 +353,14 @@ extern "C" int fr_modal_fusion_bwd(const float* d_enc, const float* d_query, con
   FusionArgs a{};
   int rc = common_args(a, d_enc, d_query, d_ids, d_num, pad_id, n_items, L, d_ln, eps);
   if (rc) return rc;
-  FR_REQUIRE(d_dknow && d_dhin && d_denc && d_dquery && d_partials, "null operand");
+  FR_REQUIRE(d_dknow && d_dhin && d_denc && d_dquery && d_dln && d_partials, "null operand");
   FR_REQUIRE(partial_floats >= fr_modal_fusion_partials(n_items), "partial buffer too small");
   a.dknow = d_dknow; a.dhin = d_dhin; a.denc = d_denc; a.dquery = d_dquery; a.part = d_partials;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   rc = dispatch(a, L, true, s);
   if (rc) return rc;
-  if (!d_dln) return FR_OK;  // the caller reduces the partials itself (fr_modal_fusion_reduce)
   hipLaunchKernelGGL(fusion_reduce_kernel, dim3(1), dim3(1024), 0, s, d_partials, fr::ceil_div(n_items, WAVES),
                      d_dln);
-  FR_LAUNCH_CHECK();
-  return FR_OK;
-}
-
-// the LayerNorm-parameter gradients from fr_modal_fusion_bwd's partials (called with d_dln = NULL)
-extern "C" int fr_modal_fusion_reduce(const float* d_partials, int64_t n_items, float* d_dln, void* stream) {
-  FR_REQUIRE(n_items > 0 && d_partials && d_dln, "null operand or no items");
-  hipLaunchKernelGGL(fusion_reduce_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), d_partials,
-                     fr::ceil_div(n_items, WAVES), d_dln);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
