@@ -9,6 +9,7 @@ runs them over RCCL, one rank per GPU).
   identical on every rank; GraphedDPStep == the eager data-parallel step (losses rel 1e-4).
 """
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -32,9 +33,13 @@ def _ranks(script, world, timeout=240):
     env.setdefault("OMP_NUM_THREADS", "4")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     out = r.stdout + r.stderr
-    verdicts = [ln for ln in out.splitlines() if ln.startswith("[rank ")]
+    # one verdict per rank; the ranks share stdout, so two lines can land interleaved on one line:
+    # take every "[rank k/world] ... PASS|FAIL" span, not whole lines
+    verdicts = re.findall(r"\[rank \d+/\d+\].*?(?:PASS|FAIL)", out)
     assert r.returncode == 0, out[-4000:]
-    assert len(verdicts) == world and all("PASS" in v for v in verdicts), out[-4000:]
+    ranks = sorted(set(re.findall(r"\[rank (\d+)/\d+\]", " ".join(verdicts))))
+    assert len(verdicts) == world and len(ranks) == world and all(v.endswith("PASS") for v in verdicts), \
+        out[-4000:]
     return verdicts
 
 
