@@ -18,13 +18,16 @@ int32 {row, chunk} pairs (nnz-balanced units) + {row, first_partial, n_chunks} s
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
 
 from . import native
 
-DEFAULT_CHUNK = None  # None: auto_chunk(nnz)
+DEFAULT_CHUNK = None  # None: auto_chunk(nnz), widened by plain_chunk(rowptr)
+# widest chunk plain_chunk() widens to: rows up to this degree are walked whole by one 16-lane group
+PLAIN_MAX_DEGREE = 256 if os.environ.get("FR_PLAIN_CHUNK", "1") != "0" else 0
 
 
 def auto_chunk(nnz: int) -> int:
@@ -34,6 +37,21 @@ def auto_chunk(nnz: int) -> int:
     MI355X, tools/bench_spmm_small.py) while large graphs keep 1024-edge units (config 4)."""
     c = 32
     while c < 1024 and c * 16384 < nnz:
+        c *= 2
+    return c
+
+
+def plain_chunk(chunk: int, max_degree: int) -> int:
+    """Widen an auto chunk so that every row is one plain unit when no row is heavier than
+    PLAIN_MAX_DEGREE edges.  A graph with no split rows runs the pipelined row walk
+    (spmm_plain16_kernel) in one launch instead of the unit kernel plus the split-row fixup: the
+    CLUSSL item-cluster and recipe-ingredient graphs (Foodcom shape, rows up to ~125 edges) had
+    2,000-2,200 split rows at the auto chunk of 32/64.  Graphs with heavier rows keep the auto
+    chunk (a heavy row in one unit would bound the launch, auto_chunk's note)."""
+    if max_degree <= chunk or max_degree > PLAIN_MAX_DEGREE:
+        return chunk
+    c = chunk
+    while c < max_degree:
         c *= 2
     return c
 
@@ -134,7 +152,11 @@ class Adjacency:
         self.col = torch.as_tensor(col, dtype=torch.int32).to(device)
         self.val = torch.as_tensor(val, dtype=torch.float32).to(device)
         self.nnz = int(self.col.numel())
-        self.chunk = auto_chunk(self.nnz) if chunk is None else int(chunk)
+        if chunk is None:
+            max_deg = int((rp[1:] - rp[:-1]).max().item()) if rp.numel() > 1 else 0
+            self.chunk = plain_chunk(auto_chunk(self.nnz), max_deg)
+        else:
+            self.chunk = int(chunk)
         self._build_plan(rp.cpu())
         self._t = None
         self.bipartite_split = None  # see mark_bipartite
