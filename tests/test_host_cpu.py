@@ -274,3 +274,23 @@ def test_sparse_block_plan_covers_every_edge_once(edges):
     assert np.array_equal(np.sort(split_rows), np.nonzero(deg > edges)[0])
     assert (rows_seen[deg <= edges] == 1).all() and (rows_seen[deg > edges] == 0).all()
     assert (np.diff(blocks[:, 2]) >= 0).all()  # in edge order
+
+
+def test_plain_chunk_widens_light_graphs_only():
+    """graph.plain_chunk: a graph whose heaviest row fits PLAIN_MAX_DEGREE gets a chunk covering it
+    (no split rows: the single-launch row walk), a heavier graph keeps the auto chunk."""
+    from FoodRec.engine import graph
+    if graph.PLAIN_MAX_DEGREE == 0:
+        pytest.skip("FR_PLAIN_CHUNK=0")
+    assert graph.plain_chunk(32, 20) == 32
+    assert graph.plain_chunk(32, 125) == 128
+    assert graph.plain_chunk(64, 65) == 128
+    assert graph.plain_chunk(32, 256) == 256
+    assert graph.plain_chunk(32, 257) == 32
+    assert graph.plain_chunk(128, 2928) == 128
+    rng = np.random.default_rng(0)
+    rows = rng.integers(0, 300, 6000)
+    cols = 300 + rng.integers(0, 40, 6000)  # 40 side nodes of ~150 edges each
+    adj = graph.Adjacency.sym_normalized(340, torch.as_tensor(rows), torch.as_tensor(cols))
+    deg = np.diff(adj.rowptr.numpy())
+    assert 128 < deg.max() <= 256 and adj.chunk == 256 and adj.n_split == 0 and adj.n_plain == 340
