@@ -481,21 +481,25 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
                                                            const int32_t* __restrict__ col,
                                                            const float* __restrict__ val, int64_t row_lo,
                                                            int64_t n_rows, XSrc xs, Epi ep) {
-  // rows [row_lo, n_rows)
+  // rows [row_lo, n_rows), walked from the last row down: the bipartite item-side graphs keep
+  // their heavier side rows (ingredients, clusters) at the end, so these start first and the
+  // light item rows fill the tail
   constexpr int LPR = 16, GPB = 256 / LPR;
   const int q = threadIdx.x % LPR;
-  const int64_t G = (int64_t)gridDim.x * GPB;
-  int64_t r = row_lo + (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
-  if (r >= n_rows) return;
+  const int64_t G = (int64_t)gridDim.x * GPB, n = n_rows - row_lo;
+  int64_t j = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  if (j >= n) return;
+  int64_t r = n_rows - 1 - j;
   int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
   int c;
   float v;
   load_batch(col, val, e0, e1, q, c, v);
   const bool has_a1 = ep.Y2.lo && ep.A1.lo, has_a2 = ep.Y2.lo && ep.A2.lo;
   while (true) {
-    const int64_t rn = r + G;
+    const int64_t jn = j + G, rn = n_rows - 1 - jn;
+    const bool more = jn < n;
     int64_t ne0 = 0, ne1 = 0;
-    if (rn < n_rows) {
+    if (more) {
       ne0 = rowptr[rn];
       ne1 = rowptr[rn + 1];
     }
@@ -530,11 +534,11 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
 #undef FR_PG
       // the next batch of this row, else the next row's first batch, in flight during the gathers
       if (e + LPR < e1) load_batch(col, val, e + LPR, e1, q, c, v);
-      else if (rn < n_rows) load_batch(col, val, ne0, ne1, q, c, v);
+      else if (more) load_batch(col, val, ne0, ne1, q, c, v);
 #pragma unroll
       for (int k = 0; k < LPR; ++k) acc = f4_fma(w[k], x[k], acc);
     }
-    if (e0 == e1 && rn < n_rows) load_batch(col, val, ne0, ne1, q, c, v);  // empty row
+    if (e0 == e1 && more) load_batch(col, val, ne0, ne1, q, c, v);  // empty row
     if (ep.Y1.lo) reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y1, r, ep.split)))[q] = acc;
     if (ep.Y2.lo) {
       float4 o = f4_scale(ep.alpha, acc);
@@ -542,7 +546,8 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
       if (has_a2) o = f4_fma(ep.beta2, a2, o);
       reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
     }
-    if (rn >= n_rows) break;
+    if (!more) break;
+    j = jn;
     r = rn;
     e0 = ne0;
     e1 = ne1;
