@@ -159,7 +159,7 @@ def _propagate_mean_fwd(adj: Adjacency, ego: torch.Tensor, L: int) -> torch.Tens
     return out
 
 
-def _prop_bwd_bipartite2(adj, g, out_lo, out_hi, split):
+def _prop_bwd_bipartite2(adj, g, out_lo, out_hi, split, acc=None):
     """_prop_bwd_split for L = 2 on a bipartite adjacency split at ``split`` (adj.mark_bipartite)
     for an upstream gradient G = [g ; 0], zero at rows [split, n) (HealthRec's RI graph and CLUSSL's
     modality graphs: the side rows of the propagation are discarded).  ``g``: the rows [0, split)
@@ -170,14 +170,15 @@ def _prop_bwd_bipartite2(adj, g, out_lo, out_hi, split):
     (into out_hi) and the item rows read them there -- two half-graph launches instead of two full
     ones.  The item rows are the full form's sums in the same order (the skipped products are exact
     zeros); the side rows apply the 1/3 after the sum instead of to each term (a rounding-level
-    difference)."""
+    difference).  ``acc``: item-row gradients of other views added into out_lo in the same epilogue."""
     inv = 1.0 / 3.0
     N = adj.shape[0]
     # side rows gather item columns only: X = [g ; (never read)]
     pad = _persistent(adj, ("bwd_pad", str(g.device)), lambda: torch.zeros(N - split, g.shape[1], device=g.device))
     spmm_range(adj, g, split, N, X_hi=pad, split=split, Y2=out_lo, Y2_hi=out_hi, alpha=inv)
     # item rows gather side columns only: X = [(never read) ; out_hi]
-    spmm_range(adj, g, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=g, beta1=inv)
+    spmm_range(adj, g, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=g, beta1=inv,
+               A2=acc, beta2=0.0 if acc is None else 1.0)
 
 
 class _PropagateLo(torch.autograd.Function):
@@ -305,6 +306,59 @@ def propagate_rows(adj: Adjacency, ego: torch.Tensor, n_layers: int, rows) -> to
         rows = [(ids.reshape(-1).to(torch.int64).contiguous(), int(off)) for ids, off in rows]
         return _PropagateRows.apply(adj, ego, int(n_layers), rows)
     return propagate_mean(adj, ego, n_layers)
+
+
+class _PropagateLoViews(torch.autograd.Function):
+    """_PropagateLo over several bipartite graphs sharing the item table ``lo`` (CLUSSL's ingredient,
+    image-cluster and text-cluster views, pricai_modelx.py:183-226): one node, so the backward
+    chains the views' item-row gradients through the SpMM epilogue (A2 = the previous views' sum)
+    instead of leaving autograd a zero-initialised buffer and an add per view."""
+
+    @staticmethod
+    def forward(ctx, adjs, L, lo, *his):
+        native.require_device(lo, *his)
+        split = lo.shape[0]
+        ctx.adjs, ctx.L, ctx.split, ctx.hi_rows = adjs, L, split, [h.shape[0] for h in his]
+        return tuple(_prop_fwd_split(adj, lo, hi, split, L, lo_rows_only=True)[:split] for adj, hi in zip(adjs, his))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        split, L = ctx.split, ctx.L
+        d_lo, d_his = None, []
+        for adj, g, hi_rows in zip(ctx.adjs, gs, ctx.hi_rows):
+            N = adj.shape[0]
+            if g is None:  # a view nothing read
+                d_his.append(None)
+                continue
+            g = _rowmajor(g)
+            d = g.shape[1]
+            out = torch.empty(split, d, dtype=g.dtype, device=g.device)
+            d_hi = torch.empty(hi_rows, d, dtype=g.dtype, device=g.device)
+            if hi_rows > N - split:
+                d_hi[N - split:].zero_()  # rows past the graph (e.g. a padding row) get no gradient
+            if L == 2:
+                _prop_bwd_bipartite2(adj, g, out, d_hi, split, acc=d_lo)
+            else:
+                G = torch.zeros(N, d, dtype=g.dtype, device=g.device)
+                G[:split] = g
+                _prop_bwd_split(adj, G, L, out, d_hi, split)
+                if d_lo is not None:
+                    out.add_(d_lo)
+            d_lo = out
+            d_his.append(d_hi)
+        return (None, None, d_lo) + tuple(d_his)
+
+
+def propagate_lo_views(adjs, lo: torch.Tensor, his, n_layers: int):
+    """[propagate_lo(adj, lo, hi, n_layers) for adj, hi in zip(adjs, his)] as one autograd node
+    (_PropagateLoViews) when every view takes the bipartite path."""
+    his = list(his)
+    ok = (n_layers >= 1 and lo.is_cuda and lo.dtype == torch.float32 and lo.shape[1] == 64 and len(adjs) == len(his)
+          and all(getattr(a, "bipartite_split", None) == lo.shape[0] and h.dtype == torch.float32
+                  and h.shape[1] == 64 and h.shape[0] >= a.shape[0] - lo.shape[0] for a, h in zip(adjs, his)))
+    if not ok:
+        return [propagate_lo(a, lo, h, n_layers) for a, h in zip(adjs, his)]
+    return list(_PropagateLoViews.apply(tuple(adjs), int(n_layers), lo, *his))
 
 
 def propagate_lo(adj: Adjacency, lo: torch.Tensor, hi: torch.Tensor, n_layers: int) -> torch.Tensor:

@@ -9,6 +9,8 @@ dcor(image,text) + dcor(image,ingre) + dcor(ingre,text) (:263) share one set of 
 ``ssl_mode: infonce`` switches to the (in the reference commented-out) InfoNCE form over the same
 view pairs, run by the fused InfoNCE kernel (CL_loss, :354-378).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -73,10 +75,20 @@ class CLUSSL(GeneralRecommender):
             self.text_trs = nn.Linear(self.t_center.shape[1], d)
             nn.init.xavier_normal_(self.text_trs.weight)
 
-    def _view(self, adj, side_table, n_side):
+    def _view(self, adj, side_table):
         # split(propagate(cat(item, side)))[0] (pricai_modelx.py:183-226): on the GPU the item rows
-        # only, on the bipartite item-side graph (ops.propagate_lo: half-graph last layer and backward)
-        return ops.propagate_lo(adj, self.item_embedding.weight, side_table[:n_side], self.n_ri_layers)
+        # only, on the bipartite item-side graph (ops.propagate_lo: half-graph last layer and backward).
+        # The side table is passed whole: rows past the graph (the ingredient padding row the
+        # reference slices off, weight[:-1]) are never read and get a zero gradient, without the
+        # slice's zero-filled backward copy
+        return ops.propagate_lo(adj, self.item_embedding.weight, side_table, self.n_ri_layers)
+
+    def _views(self, adjs, side_tables):
+        # the three views as one node (ops.propagate_lo_views: the item-row gradients summed in the
+        # SpMM epilogue); FR_CLUSSL_VIEWS_NODE=0: one node per view
+        if os.environ.get("FR_CLUSSL_VIEWS_NODE", "1") == "0":
+            return [self._view(a, t) for a, t in zip(adjs, side_tables)]
+        return ops.propagate_lo_views(adjs, self.item_embedding.weight, side_tables, self.n_ri_layers)
 
     def forward(self):
         return self._forward()[:3]
@@ -84,13 +96,13 @@ class CLUSSL(GeneralRecommender):
     def _forward(self, ssl_ids=None):
         """forward(); with ``ssl_ids`` also the three views gathered there (image, text, ingre),
         the sum and the gathers as one node (ops.views_sum_gather)."""
-        item_ingre = self._view(self.ingre_norm_adj, self.ingre_embedding.weight[:-1, :], self.n_ingredients)
         img_side = self.image_trs(self.image_prototype_embedding.weight) if self.v_center is not None \
             else self.image_prototype_embedding.weight
-        item_image = self._view(self.image_norm_adj, img_side, self.n_cluster)
         txt_side = self.text_trs(self.text_prototype_embedding.weight) if self.t_center is not None \
             else self.text_prototype_embedding.weight
-        item_text = self._view(self.text_norm_adj, txt_side, self.n_cluster)
+        item_ingre, item_image, item_text = self._views(
+            (self.ingre_norm_adj, self.image_norm_adj, self.text_norm_adj),
+            (self.ingre_embedding.weight, img_side, txt_side))
         gathered = None
         if ssl_ids is not None:
             item_emb, (g_ing, g_img, g_txt) = ops.views_sum_gather([item_ingre, item_image, item_text], ssl_ids)

@@ -171,6 +171,39 @@ def test_propagate_lo_matches_full(cuda, L):
     assert torch.all(gb_hi[NS:] == 0)
 
 
+@pytest.mark.parametrize("L", [1, 2])
+def test_propagate_lo_views_matches_per_view(cuda, L):
+    """ops.propagate_lo_views (CLUSSL's three views as one node, the item-row gradients summed in the
+    SpMM epilogue) vs one propagate_lo per view: equal values; the item table's gradient to fp32
+    round-off of the different summation order; each side table's gradient (padding row included)."""
+    from FoodRec.engine import ops
+    from FoodRec.models._graphs import side_adjacency
+    rng = np.random.default_rng(10 + L)
+    I, sides = 2500, (400, 150, 150)
+    adjs = [side_adjacency(np.stack([rng.integers(0, I, 9000), rng.integers(0, ns, 9000)], 1), I, ns, cuda)
+            for ns in sides]
+    lo0 = torch.randn(I, 64, device=cuda)
+    his0 = [torch.randn(ns + (1 if k == 0 else 0), 64, device=cuda) for k, ns in enumerate(sides)]
+    gs = [torch.randn(I, 64, device=cuda) for _ in sides]
+    res = []
+    for fused in (False, True):
+        lo = lo0.clone().requires_grad_(True)
+        his = [h.clone().requires_grad_(True) for h in his0]
+        if fused:
+            outs = ops.propagate_lo_views(adjs, lo, his, L)
+        else:
+            outs = [ops.propagate_lo(a, lo, h, L) for a, h in zip(adjs, his)]
+        sum((o * g).sum() for o, g in zip(outs, gs)).backward()
+        res.append(([o.detach() for o in outs], lo.grad, [h.grad for h in his]))
+    (oa, la, ha), (ob, lb, hb) = res
+    for a, b in zip(oa, ob):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-6)
+    for a, b in zip(ha, hb):
+        torch.testing.assert_close(b, a, rtol=2e-6, atol=1e-7)
+    assert torch.all(hb[0][sides[0]:] == 0)
+
+
 @pytest.mark.parametrize("N,L,bip", [(3000, 2, False), (300_000, 2, False), (300_000, 1, False), (5000, 3, False),
                                      (6000, 2, True), (300_000, 2, True)])
 def test_propagate_rows_matches_full(cuda, N, L, bip):
