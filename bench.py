@@ -78,7 +78,9 @@ def build(device, batch, seed=0, dataset_seed=0, extra=None):
     data = FoodData.from_synthetic(ds)
     cfg = Config("CIKM_Model", "Allrecipes", {"use_gpu": device.type == "cuda", "seed": 999, "cuda_graph": True,
                                              "train_batch_size": batch, "log_root": "/tmp/frlog/",
-                                             "ckp_root": "/tmp/frckp/", **(extra or {})})
+                                             "ckp_root": "/tmp/frckp/", **(extra or {}),
+                                             # FR_BENCH_CFG: JSON config overrides for A/B runs
+                                             **json.loads(os.environ.get("FR_BENCH_CFG", "{}"))})
     cfg["device"] = device
     data.args_config = cfg
     init_seed(999 + seed)
