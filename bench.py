@@ -165,16 +165,14 @@ def main():
     # FR_BENCH_DP1=1: the data-parallel step (row exchange + dense all-reduce through RCCL, graphs A /
     # B1 / B2 around the collectives) at world 1 -- the per-rank cost of the N > 1 path on one GPU
     dp1 = world == 1 and os.environ.get("FR_BENCH_DP1") == "1"
+    from FoodRec.engine.dist import init_process_group  # explicit collective timeout (FR_PG_TIMEOUT_S)
     if dp1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        init_process_group("nccl", torch.device("cuda", local), rank=0, world_size=1)
     if world > 1:
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        init_process_group(backend, torch.device("cuda", local) if backend == "nccl" else None)
         # the job really runs ``world`` ranks: checked against the process group itself
         assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
     device = torch.device("cuda", local)

@@ -8,10 +8,29 @@ fused Adam update, so the replicas stay bit-identical.  (The row-sharded graph s
 """
 from __future__ import annotations
 
+import datetime
 import os
 
 import torch
 import torch.distributed as dist
+
+
+def pg_timeout() -> datetime.timedelta:
+    """Collective timeout of the engine's process groups: FR_PG_TIMEOUT_S seconds (default 300), so
+    a collective that one rank never joins ends the job with an error instead of hanging until
+    torch's default watchdog (10 minutes for RCCL, 30 for gloo)."""
+    return datetime.timedelta(seconds=float(os.environ.get("FR_PG_TIMEOUT_S", "300")))
+
+
+def init_process_group(backend, device=None, **kw):
+    """torch.distributed.init_process_group with the engine's timeout; for RCCL ("nccl") also the
+    asynchronous error handling that tears the process down when a collective times out or fails
+    (TORCH_NCCL_ASYNC_ERROR_HANDLING, unless the caller's environment sets it)."""
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        if device is not None:
+            kw["device_id"] = device
+    dist.init_process_group(backend, timeout=pg_timeout(), **kw)
 
 
 def init_from_env(backend=None):
@@ -24,9 +43,9 @@ def init_from_env(backend=None):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            init_process_group(backend, torch.device("cuda", local))
         else:
-            dist.init_process_group(backend)
+            init_process_group(backend)
     return rank, world, local
 
 

@@ -1010,10 +1010,16 @@ class _GraphBpr(torch.autograd.Function):
             grads = _GraphBpr._backward_here(ctx, g_mf, g_emb, g_rows, drain=False)
             done = torch.cuda.Event()
             done.record(side)
+        user_w, item_w = ctx.saved_tensors[:2]
+        if ctx.defer is None or any(w.grad is not None for w in (user_w, item_w, ctx.ingre_w)):
+            # autograd consumes the returned grads on the current stream right away when it has to
+            # sum them (another gradient of the same table, or an existing .grad): join here
+            main.wait_event(done)
         _BRANCH_PENDING.append((done, ctx.defer, ctx.ingre_w))  # (no reference to the returned grads:
         # AccumulateGrad adopts them as .grad only when nothing else holds them)
-        if len(_BRANCH_PENDING) == 1:
-            torch.autograd.Variable._execution_engine.queue_callback(_join_branch)
+        # queued by every branch backward (idempotent: the first callback joins every pending entry),
+        # so an entry left behind by a failed backward cannot keep later ones from being joined
+        torch.autograd.Variable._execution_engine.queue_callback(_join_branch)
         return grads
 
     @staticmethod
@@ -1159,8 +1165,24 @@ def _join_branch():
     _BRANCH_PENDING.clear()
     for done, defer, ingre_w in pend:
         torch.cuda.current_stream(ingre_w.device).wait_event(done)
-        if defer is not None and ingre_w.grad is not None:
-            defer.drain(ingre_w.grad)
+        if defer is not None:
+            if defer.rows and ingre_w.grad is None:  # (no propagation gradient was adopted: the rows alone)
+                ingre_w.grad = torch.zeros_like(ingre_w)
+            if ingre_w.grad is not None:
+                defer.drain(ingre_w.grad)
+            else:
+                defer.open = False
+
+
+def _drop_stale_branches():
+    """Entries of a backward that never reached its final callback (it raised): wait for their
+    kernels and forget them."""
+    pend = list(_BRANCH_PENDING)
+    _BRANCH_PENDING.clear()
+    for done, defer, ingre_w in pend:
+        torch.cuda.current_stream(ingre_w.device).wait_event(done)
+        if defer is not None:
+            defer.open, defer.rows = False, []
 
 
 def graph_bpr_begin(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, L_ui, gamma=1e-10):
@@ -1170,9 +1192,11 @@ def graph_bpr_begin(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, 
     node, whose backward then runs on the branch stream too, beside the encoder backward.  Without a
     GPU, in the deterministic mode or with BRANCH_STREAMS off, the forward runs here."""
     args = (user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma)
+    if _BRANCH_PENDING:
+        _drop_stale_branches()
     if torch.is_grad_enabled() and ingre_w.requires_grad and not _DETERMINISTIC:
         ingre_w.__dict__["_fr_defer_rows"] = _DeferredRows()
-    if not (BRANCH_STREAMS and user_w.is_cuda):
+    if not (BRANCH_STREAMS and user_w.is_cuda) or _DETERMINISTIC:
         f = _graph_bpr_forward(*args)
         f.done, f.args = None, args
         return f

@@ -350,14 +350,23 @@ class FusedAdam(torch.optim.Optimizer):
         return t.data_ptr()
 
     def _lr_tensor(self, gi, group, device):
+        """The group's device lr scalar and whether this call wrote it (on the current stream)."""
         t, held = self._d_lr.get(gi, (None, None))
         if t is None:
             t = torch.full((), float(group["lr"]), dtype=torch.float64, device=device)
             self._d_lr[gi] = (t, float(group["lr"]))
-        elif held != float(group["lr"]):
+            return t, True
+        if held != float(group["lr"]):
             t.fill_(float(group["lr"]))
             self._d_lr[gi] = (t, float(group["lr"]))
-        return t
+            return t, True
+        return t, False
+
+    def _ticket_created(self, device) -> bool:
+        """Create the ticket words for ``device`` now (on the current stream); True if created."""
+        new = device not in self.__dict__.get("_tickets", {})
+        self._ticket(device)
+        return new
 
     @torch.no_grad()
     def sync_lr(self):
@@ -403,17 +412,21 @@ class FusedAdam(torch.optim.Optimizer):
                 w_read.record(side)
         else:
             prepared = self._prepare_factored(lib) if (self.row_grads.factored and part != "dense") else {}
+        # pass 1, on the current stream: collect the tensors and create any state the launches read.
+        # When the row tables' update runs on the side stream, everything this pass writes on the
+        # current stream (zero-filled moments / step counters / lazy bookkeeping on a first step, the
+        # lr scalar, the ticket words, rows stashed after the fork event) must be ordered before it:
+        # ``dirty`` makes the side stream wait for the current one before the row launches
+        main = torch.cuda.current_stream(side.device) if side is not None else None
+        dirty = False
+        plans = []
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
             plist, rows = [], []
             for p in group["params"]:
                 if id(p) in prepared:
                     rows.append((p, prepared.pop(id(p))))
-                    st = self.state[p]
-                    if len(st) == 0:
-                        st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
-                        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    dirty |= self._init_state(p)
                     continue
                 if part == "dense" and (id(p) in self.row_grads.pending or id(p) in self.row_grads.factored):
                     continue
@@ -432,16 +445,9 @@ class FusedAdam(torch.optim.Optimizer):
                 native.require_device(p)
                 if not p.is_contiguous():
                     raise RuntimeError("FusedAdam needs contiguous parameters")
+                created = self._init_state(p)
                 st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
-                    # fp32 moments (and, for bf16 parameters, an fp32 master copy: config 5)
-                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32,
-                                                        memory_format=torch.preserve_format)
-                    if p.dtype == torch.bfloat16:
-                        st["master"] = p.detach().float()
-                elif st["step"].device != p.device or st["step"].dtype != torch.int64:
+                if not created and (st["step"].device != p.device or st["step"].dtype != torch.int64):
                     st["step"] = st["step"].to(device=p.device, dtype=torch.int64)
                 if p.dtype == torch.bfloat16:
                     self._step_bf16(p, group, lib, skip_flag, gi)
@@ -450,14 +456,27 @@ class FusedAdam(torch.optim.Optimizer):
                     raise RuntimeError(f"FusedAdam supports fp32 and bf16 parameters (got {p.dtype})")
                 if rg is not None:
                     rows.append((p, rg))
+                    dirty = True  # its rows were written by the backward, possibly after the fork event
+                    dirty |= created
                 else:
                     plist.append(p)
             if not plist and not rows:
                 continue
             dev = (plist or [rows[0][0]])[0].device
-            d_lr = self._lr_tensor(gi, group, dev)
+            d_lr, lr_written = self._lr_tensor(gi, group, dev)
+            dirty |= lr_written
+            if rows:
+                dirty |= self._ticket_created(dev)
+                if self.lazy_rows:
+                    for p, _ in rows:
+                        dirty |= self._init_lazy(p)
             hyper = (d_lr.data_ptr(), float(group["lr"]), float(beta1), float(beta2), float(group["eps"]),
                      float(group["weight_decay"]), native.ptr(skip_flag), torch.cuda.current_stream(dev).cuda_stream)
+            plans.append((group, plist, rows, hyper))
+        if side is not None and dirty:
+            side.wait_stream(main)
+        # pass 2: the launches
+        for group, plist, rows, hyper in plans:
             lazy_dense = [p for p in plist if "lazy_last" in self.state[p]]
             # a lazily updated table taking a dense step (a dense .grad: more ids than the row path
             # takes, a gradient hook, clipping): its deferred steps are replayed first and its rows
@@ -466,7 +485,7 @@ class FusedAdam(torch.optim.Optimizer):
             self._flush_tables(group, lazy_dense)
             if plist:
                 if w_read is not None:
-                    torch.cuda.current_stream(dev).wait_event(w_read)  # (long done: forked early)
+                    torch.cuda.current_stream(plist[0].device).wait_event(w_read)  # (long done: forked early)
                 with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
                     self._launch_dense(lib, plist, hyper)
             for p in lazy_dense:
@@ -481,6 +500,30 @@ class FusedAdam(torch.optim.Optimizer):
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
         return loss
+
+    def _init_state(self, p) -> bool:
+        """Create ``p``'s Adam state (on the current stream) if it has none; True if created."""
+        st = self.state[p]
+        if len(st):
+            return False
+        st["step"] = torch.zeros((), dtype=torch.int64, device=p.device)
+        # fp32 moments (and, for bf16 parameters, an fp32 master copy: config 5)
+        st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+        st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+        if p.dtype == torch.bfloat16:
+            st["master"] = p.detach().float()
+        return True
+
+    def _init_lazy(self, p) -> bool:
+        """The lazy-row bookkeeping of a row table (on the current stream); True if created."""
+        st = self.state[p]
+        if "lazy_last" in st:
+            return False
+        # every row is current through the table's present step (0, or the dense steps so far)
+        st["lazy_last"] = st["step"].to(torch.int32).expand(p.shape[0]).contiguous()
+        # per step: neg_step, bc2_sqrt (fp32) and RN64(1 / bc2_sqrt) (a double in floats 2-3)
+        st["lazy_hist"] = torch.zeros(self.hist_cap, 4, dtype=torch.float32, device=p.device)
+        return True
 
     def _rows_side(self):
         """The stream of the row tables' part of a full step (None: not on a GPU, or no fork point)."""
@@ -578,12 +621,7 @@ class FusedAdam(torch.optim.Optimizer):
         RD = (ctypes.c_int32 * n)(*dims)
         if self.lazy_rows:
             for p in plist:
-                st = self.state[p]
-                if "lazy_last" not in st:
-                    # every row is current through the table's present step (0, or the dense steps so far)
-                    st["lazy_last"] = st["step"].to(torch.int32).expand(p.shape[0]).contiguous()
-                    # per step: neg_step, bc2_sqrt (fp32) and RN64(1 / bc2_sqrt) (a double in floats 2-3)
-                    st["lazy_hist"] = torch.zeros(self.hist_cap, 4, dtype=torch.float32, device=p.device)
+                self._init_lazy(p)  # (created in step()'s first pass; kept for direct callers)
             idl = [i if i.is_contiguous() else i.contiguous() for i in idl]
             for k in range(0, n, 16):  # the kernel's argument block takes 16 tables per launch
                 m = min(16, n - k)
@@ -620,7 +658,7 @@ class FusedAdam(torch.optim.Optimizer):
         if g.dtype != torch.bfloat16:
             raise RuntimeError("a bf16 parameter needs a bf16 gradient")
         beta1, beta2 = group["betas"]
-        d_lr = self._lr_tensor(gi, group, p.device)
+        d_lr, _ = self._lr_tensor(gi, group, p.device)
         with profiling.region("adam", 30 * p.numel()):
             native.check(lib.fr_adam_step_bf16(
                 p.data_ptr(), st["master"].data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),

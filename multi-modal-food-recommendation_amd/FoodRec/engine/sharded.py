@@ -69,6 +69,31 @@ def _all_reduce(t, group, async_op=False):
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
+def _group_rank_world(group):
+    from .comm import RcclComm
+    if isinstance(group, RcclComm):
+        return group.rank, group.world
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def check_same_count(n: int, group, what: str, device):
+    """Fail fast when the ranks disagree on a row count the next collectives are sized by (the
+    rows form's |S|): one all-reduce of a P-slot vector, rank r's count in slot r, so every rank
+    sees every count exactly (fp32 is exact below 2^24).  A mismatch would otherwise make the
+    |S|-row all-reduces of different lengths hang or read past a buffer; here every rank raises."""
+    if group is None:
+        return
+    rank, world = _group_rank_world(group)
+    if world == 1 and not _FORCE[0]:
+        return
+    slots = torch.zeros(world, dtype=torch.float32, device=device)
+    slots[rank] = float(n)
+    _all_reduce(slots, group)
+    counts = [int(c) for c in slots.cpu().tolist()]
+    if any(c != counts[0] for c in counts):
+        raise RuntimeError(f"row-sharded step: ranks disagree on {what}: {counts} (rank {rank} has {n})")
+
+
 class ShardedGraph:
     """Rank ``rank``'s slice of the bipartite interaction graph (u, i) of n_users x n_items."""
 
@@ -321,6 +346,7 @@ class _ShardedRowsStep(torch.autograd.Function):
         _all_reduce(flags, group)
         S = torch.nonzero(flags > 0).reshape(-1)
         del flags
+        check_same_count(S.numel(), group, "|S| (layer-1 item rows)", dev)
         pi1 = torch.empty_like(ego_i)                              # valid at S
         ops.spmm_ex(g.A_iu, ego_u, Y1=pi1, rows=[(S, 0)], region="spmm_rows")
         part1 = pi1.index_select(0, S)
@@ -344,7 +370,9 @@ class _ShardedRowsStep(torch.autograd.Function):
         B = loc.numel()
         safe = loc.clamp(min=0)
         rows = torch.cat([out_u.index_select(0, safe), ego_u.index_select(0, safe)])
-        rows.mul_((loc >= 0).to(rows.dtype).repeat(2).unsqueeze(1))
+        # rows owned elsewhere read row 0 of a table valid only at this rank's batch users: select,
+        # not multiply (0 * a NaN / Inf bit pattern would reach every rank through the all-reduce)
+        rows.masked_fill_((loc < 0).repeat(2).unsqueeze(1), 0.0)
         _all_reduce(rows, group)
         ctx.save_for_backward(loc, p, n, S)
         ctx.n_local = ego_u.shape[0]

@@ -121,9 +121,10 @@ def test_sharded_step_through_rccl_world_one(cuda, nccl_group, kind):
             (mf0 + reg0.sum()).backward()
             # rows form (L = 2): forward the item flags, the layer-1 item rows at S and the 2B batch
             # item rows; backward the first layer's item rows at S + the second layer per item-row
-            # block; + the owner gather of the batch users' propagated and ego rows (one [2B, d])
+            # block; + the owner gather of the batch users' propagated and ego rows (one [2B, d]);
+            # + the |S| cross-check (check_same_count: one P-slot all-reduce)
             nb = len(g1.iu_blocks)
-            assert nb >= 2 and n_rccl == nb + 5, (nb, calls)
+            assert nb >= 2 and n_rccl == nb + 6, (nb, calls)
             _close(mfR.detach(), mf0.detach(), 1e-5)
             _close(regR.detach(), reg0.detach(), 1e-5)
             _close(mR.ego_i.grad, m0.ego_i.grad, 1e-4)

@@ -617,3 +617,46 @@ def test_rounding_shortcuts_bit_exact(cuda):
         native.check(native.lib().fr_adam_rounding_selftest(1 << 23, seed, bad.data_ptr(),
                                                             native.stream_of(bad)), "fr_adam_rounding_selftest")
     assert bad.tolist() == [0, 0, 0]
+
+
+def test_rows_side_stream_first_steps_equal_inline(cuda):
+    """FusedAdam.step's row-table update on the side stream (FR_ROWS_SIDE_STREAM=1, the default) vs
+    on the current stream, over the first two HealthRec steps (lazy rows, deterministic scatters).
+    Step 1 is the one that creates the Adam state, the lazy bookkeeping, the lr scalar and the ticket
+    words on the current stream: the side stream must be ordered after them (else it reads
+    uninitialised moments and the queued zero fills overwrite its update).  Every parameter and
+    moment agrees (rel 1e-6)."""
+    from helpers import golden, tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import optim
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("model_CIKM_Model.npz")
+    batch = {k[len("batch/"):]: torch.from_numpy(g[k]).to(cuda) for k in g.files if k.startswith("batch/")}
+    runs = []
+    det0 = torch.are_deterministic_algorithms_enabled()
+    side0 = optim.ROWS_SIDE_STREAM
+    torch.use_deterministic_algorithms(True)
+    try:
+        for side in (True, False):
+            optim.ROWS_SIDE_STREAM = side
+            cfg = tiny_config("CIKM_Model", True, cuda_graph=False, lazy_row_adam=True, deterministic=True)
+            data = tiny_data(cfg)
+            init_seed(999)
+            model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
+            tr = Trainer(cfg, model)
+            st = tr.new_step_state()
+            for k in range(2):
+                tr.train_step(batch, k, st)
+            tr.optimizer.flush()
+            torch.cuda.synchronize()
+            runs.append((model, tr.optimizer))
+    finally:
+        optim.ROWS_SIDE_STREAM = side0
+        torch.use_deterministic_algorithms(det0)
+    (ma, oa), (mb, ob) = runs
+    for (k, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9, msg=k)
+        if a in oa.state:
+            assert int(oa.state[a]["step"]) == int(ob.state[b]["step"]) == 2, k
+            for s_ in ("exp_avg", "exp_avg_sq"):
+                torch.testing.assert_close(oa.state[a][s_], ob.state[b][s_], rtol=1e-6, atol=1e-12, msg=(k, s_))
