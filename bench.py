@@ -294,8 +294,11 @@ def main():
             roofline = {**common, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
                         "flops_per_launch": fl, "bytes_per_launch": int(d["bytes_per_launch"]),
-                        "region_kernels": ("enc_bwd_kernel<20> + enc_reduce_kernel (the ordered weight-gradient "
-                                           "reduction): the two launches of one fr_encoder_bwd call"
+                        "region_kernels": ("enc_bwd_kernel<20> per layer + one enc_reduce_kernel (the ordered "
+                                           "weight-gradient reduction) per step: the top layer's reduction is "
+                                           "folded into the bottom layer's enc_bwd_kernel launch, the bottom "
+                                           "layer's own runs after it; avg_launch_ms = one fr_encoder_bwd call "
+                                           "averaged over the two layers"
                                            if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
@@ -331,14 +334,14 @@ def main():
     c3 = None
     if world == 1 and not args.no_config3:
         del graphed, state
-        c3 = config3(device)
+        c3 = config3(device, cpu=not args.no_cpu_baseline)
         graphed = state = None
     c4 = None
     if not args.no_spmm_10m:
         del trainer, model, sampler, state, graphed
         torch.cuda.empty_cache()
         if world == 1:
-            c4 = config4(device)
+            c4 = config4(device, cpu=not args.no_cpu_baseline)
             # the row-sharded step at P = 1 (no collectives): the denominator of the N-GPU runs'
             # config4_10m line (the driver's multi-GPU bench runs config4_sharded at P = N)
             c4["sharded_p1"] = config4_sharded(device, 1, 0)
@@ -543,7 +546,7 @@ def config5(device, batches=(512, 8192), steps=3, warmup=2, spmm_iters=5, topk_u
     return out
 
 
-def config3(device, steps=30, warmup=5, ssl_iters=20):
+def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
     """BASELINE config 3 on one GPU: CLUSSL (reference PRICAI_ModelX) on a Foodcom-shaped synthetic
     dataset (U=7,596, I=29,943, ~192k train pairs, 2,000 image / text k-means clusters, NI=4,963),
     d=64, B=512: the full graphed training step (3 item-side propagations with n_ri_layers=2, the
@@ -612,10 +615,125 @@ def config3(device, steps=30, warmup=5, ssl_iters=20):
         e1.record()
         torch.cuda.synchronize()
         out[name] = round(e0.elapsed_time(e1) / ssl_iters, 4)
+    if cpu:
+        out["cpu_baseline"] = config3_cpu(data, B, cpu_steps)
     return out
 
 
-def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
+def _cpu_threads():
+    """The CPU threads a baseline uses: the box's per-GPU share (OMP_NUM_THREADS=16 there), at most 16."""
+    return min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 16)
+
+
+def config3_cpu(data, B, steps):
+    """The config-3 step (CLUSSL, dCor SSL) of the torch-CPU oracle on this host's CPU share:
+    the engine model on oracle/cpu_backend (the reference's formulas in torch-CPU ops)."""
+    import numpy as np
+    import torch
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.configurator import Config
+    from FoodRec.utils.utils import get_model, init_seed
+    from oracle import cpu_backend
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
+    with cpu_backend.installed():
+        cfg = Config("PRICAI_ModelX", "Foodcom", {"use_gpu": False, "seed": 999, "train_batch_size": B,
+                                                  "ssl_mode": "dcor", "n_cluster": 2000, "log_root": "/tmp/frlog/",
+                                                  "ckp_root": "/tmp/frckp/"})
+        cfg["device"] = torch.device("cpu")
+        init_seed(999)
+        model = get_model("PRICAI_ModelX")(cfg, data)
+        tr = Trainer(cfg, model)
+        np.random.seed(2001)
+        sampler = TripleSampler(data, B, "cpu", replay_python_random=False)
+        feats = tr._features()
+        st = tr.new_step_state()
+        it = sampler.epoch()
+        u, p, n = next(it)
+        tr.train_step(feats.batch(u, p, n), 0, st)  # warm-up
+        c0 = time.perf_counter()
+        for i in range(steps):
+            u, p, n = next(it)
+            tr.train_step(feats.batch(u, p, n), 1 + i, st)
+        dt = (time.perf_counter() - c0) / steps
+    return {"value": round(B / dt, 1), "unit": "triples/s", "cores": threads, "kind": "port",
+            "host_cores_total": os.cpu_count(), "ms_per_step": round(dt * 1e3, 1),
+            "sample": f"{steps} CLUSSL dCor training steps (B={B}) of the torch-CPU oracle after 1 warm-up"}
+
+
+def config4_cpu(adj, n_users, P, batches, threads=None, sample_nnz=16_000_000):
+    """The reference's compute path for the config-4 step (lightgcn.py:134-177 with common/loss.py and
+    torch.optim.Adam) on this host's CPU share, as a bounded sample.  The reference multiplies by the
+    normalised adjacency as a coalesced COO tensor (torch.sparse.mm), ~0.3 us per non-zero on the
+    CPU here: one full product over the 400M non-zeros would take minutes.  So every s-th row of A
+    (s = nnz / sample_nnz: ~16M non-zeros, users and Zipf-heavy items alike) is multiplied with the
+    full [N, 64] table and the time is scaled by nnz / sampled non-zeros (the COO product is a loop
+    over the non-zeros).  The step is composed as 2L = 4 such products (forward; backward = the same
+    product, A symmetric) + Adam over the P parameters (a P/16 slice timed, scaled) + BPR / EmbLoss on
+    the B rows (timed).  Returns None when the host lacks the memory."""
+    import torch
+    threads = threads or _cpu_threads()
+    torch.set_num_threads(threads)
+    N, nnz = adj.shape[0], adj.nnz
+    try:
+        import psutil
+        if psutil.virtual_memory().available < 4 * N * 64 * 4 + 40 * sample_nnz:
+            return None
+    except ImportError:
+        pass
+    rp = adj.rowptr
+    stride = max(1, -(-nnz // sample_nnz))
+    sel = torch.arange(0, N, stride, device=rp.device)
+    lens = rp[sel + 1] - rp[sel]
+    tot = int(lens.sum().item())
+    first = torch.cumsum(lens, 0) - lens
+    pos = torch.repeat_interleave(rp[sel] - first, lens) + torch.arange(tot, device=rp.device)
+    rows = torch.repeat_interleave(torch.arange(sel.numel(), device=rp.device), lens)
+    idx = torch.stack([rows, adj.col[pos].to(torch.int64)]).cpu()
+    vals = adj.val[pos].cpu()
+    n_sel = int(sel.numel())
+    del pos, rows, lens, first, sel
+    A = torch.sparse_coo_tensor(idx, vals, (n_sel, N), is_coalesced=True)
+    del idx, vals
+    gen = torch.Generator().manual_seed(0)
+    X = torch.randn(N, 64, generator=gen)
+    t0 = time.perf_counter()
+    Y = torch.sparse.mm(A, X)
+    t_sample = time.perf_counter() - t0
+    t_spmm = t_sample * nnz / max(tot, 1)
+    del Y, A, X
+    # Adam on a slice of the parameters, scaled to P (the update is elementwise: linear in P)
+    m = max(1, P // 16)
+    w = torch.nn.Parameter(torch.randn(m, generator=gen))
+    w.grad = torch.randn(m, generator=gen)
+    opt = torch.optim.Adam([w], lr=1e-3)
+    opt.step()
+    t0 = time.perf_counter()
+    opt.step()
+    t_adam = (time.perf_counter() - t0) * (P / m)
+    del w, opt
+    out = {"spmm_s": round(t_spmm, 3), "adam_s": round(t_adam, 3), "cores": threads, "host_cores_total": os.cpu_count(),
+           "kind": "port", "step": {}}
+    E = torch.randn(n_users + 64, 64, generator=gen)
+    for B in batches:
+        ue, pe, ne = (E[torch.randint(0, E.shape[0], (B,), generator=gen)].requires_grad_(True) for _ in range(3))
+        t0 = time.perf_counter()
+        pos_s, neg_s = (ue * pe).sum(1), (ue * ne).sum(1)
+        mf = -torch.log(1e-10 + torch.sigmoid(pos_s - neg_s)).mean()
+        reg = (ue.norm(2).pow(2) + pe.norm(2).pow(2) + ne.norm(2).pow(2)) / B
+        (mf + 1e-4 * reg).backward()
+        t_loss = time.perf_counter() - t0
+        step_s = 4 * t_spmm + t_adam + t_loss
+        out["step"][str(B)] = {"value": round(B / step_s, 2), "unit": "triples/s", "ms_per_step": round(step_s * 1e3, 1)}
+    out["sample"] = ("torch.sparse.mm (coalesced COO, as the reference) over every %d-th row of A: %d of %d non-zeros "
+                     "x [%d, 64], %.2f s, scaled by non-zeros; x 4 (2 layers forward + backward) + torch.optim.Adam "
+                     "over %d params (a 1/16 slice timed, scaled) + BPRLoss / EmbLoss on B rows"
+                     % (stride, tot, nnz, N, t_sample, P))
+    return out
+
+
+def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10, cpu=True):
     """BASELINE config 4 on one GPU: the synthetic 10M users x 1M items x ~200M interactions graph.
     (1) fr_spmm_csr alone (the propagation kernel in its HBM-bound regime; the Allrecipes tables fit
     the Infinity Cache), (2) the full LightGCN-ID training step (device triple sampling, 2-layer
@@ -704,6 +822,8 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10):
                          "BPR/EmbLoss with a dense zero-filled gradient + sparse-upstream backward layer (col/val "
                          "scan, hits, H write) + full backward layer + 28*P Adam; survey_8d_dense_bytes = SURVEY "
                          "8(d)'s 2L*B_spmm + 2(L+1)*N*d*s + 28*P + B*(3*8+3*d*s)*2 (every layer over the full graph)"}
+    if cpu:
+        out["cpu_baseline"] = config4_cpu(adj, U, P, batches)
     del trainer, model, g, adj
     torch.cuda.empty_cache()
     out["spmm_beyond_mall"] = spmm_beyond_mall(device)
@@ -844,7 +964,7 @@ def cpu_baseline(args):
     from oracle import cpu_backend
     # the GPU box gives one GPU's job a 16-CPU share of the host (OMP_NUM_THREADS=16 there); the
     # host's total core count is reported beside it
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1, 16)
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     with cpu_backend.installed():
         from FoodRec.common.trainer import Trainer

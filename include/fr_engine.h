@@ -452,30 +452,59 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * dropout2.  Masks come from a counter-based hash of (seed, *d_counter, site, element); the
  * forward stores the counter value it used in *d_seed_out and the backward reads it back (the
  * caller advances the counter; graph replays draw fresh masks).
- * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), fact [T,256] (dropout(act(FF1))),
- * y2 [T,64] (LN2 input), st1/st2 [T,2] (mean, rstd), T = n_seq * L, and dact (keep/(1-p) *
- * act'(FF1)) as fr_encoder_dact_numel(n_seq, L) floats in the kernels' MFMA fragment layout
- * (opaque to the caller; only fr_encoder_bwd reads it).
- * Backward writes dx and the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
- * gradients concatenated in d_params order); d_partials [fr_encoder_partials(n_seq, L)] floats of
- * per-workgroup partials, summed in workgroup order (deterministic).
+ * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), y2 [T,64] (LN2 input), st1/st2
+ * [T,2] (mean, rstd), T = n_seq * L: 452 floats per token.  The FF activation is not saved: the
+ * backward recomputes it (x1 = LN1(y1), one more GEMM, the same GELU / dropout epilogue, bit-identical
+ * to the forward's).
+ * Backward writes dx and its per-workgroup weight-gradient partials d_partials
+ * [fr_encoder_partials(n_seq, L)]; with d_grad non-NULL it also sums them in workgroup order
+ * (deterministic) into the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
+ * gradients concatenated in d_params order), with d_grad NULL it leaves them for a later
+ * fr_encoder_reduce or for the next backward call: d_prev_partials / d_prev_grad (both or neither)
+ * name another call's partials (same n_seq and L) that this launch reduces into d_prev_grad -- a
+ * stacked encoder's layer-(k+1) reduction folded into layer k's launch.
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_encoder_partials(int64_t n_seq, int L);
 int64_t fr_encoder_grad_numel(void);
-int64_t fr_encoder_dact_numel(int64_t n_seq, int L);
 /* Diagnostics: enable (1) / disable (0) / keep (-1) per-phase s_memtime stamps of workgroup 0 and
  * copy the stamp table (uint64 [2][32]: forward, backward; shader clock) to host_marks if non-NULL. */
 int fr_encoder_profile(int enable, uint64_t* host_marks);
 int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_seq, int L, const float* const* d_params,
                    const float* eps, const float* drop, uint64_t seed, int gelu, const int64_t* d_counter,
-                   int64_t* d_seed_out, float* d_out, float* d_qkv, float* d_ctx, float* d_y1, float* d_fact,
-                   float* d_dact, float* d_y2, float* d_st1, float* d_st2, void* stream);
+                   int64_t* d_seed_out, float* d_out, float* d_qkv, float* d_ctx, float* d_y1, float* d_y2,
+                   float* d_st1, float* d_st2, void* stream);
 int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, int64_t n_seq, int L,
                    const float* const* d_params, const float* eps, const float* drop, uint64_t seed, int gelu,
                    const int64_t* d_seed_in, const float* d_qkv, const float* d_ctx, const float* d_y1,
-                   const float* d_fact, const float* d_dact, const float* d_y2, const float* d_st1,
-                   const float* d_st2, float* d_dx,
-                   float* d_grad, float* d_partials, int64_t partial_floats, void* stream);
+                   const float* d_y2, const float* d_st1, const float* d_st2, float* d_dx, float* d_grad,
+                   float* d_partials, int64_t partial_floats, const float* d_prev_partials, float* d_prev_grad,
+                   void* stream);
+int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_grad, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * HealthRec's loss head after the encoder as one op (models/cikm_model.py:245-264, 304-308,
+ * 311-369): fr_modal_fusion's know / hin per item (see below) feeding fr_health_kd's terms,
+ *   d_out[0] = w_health * sum(BCE(sigmoid(mlp(hin)), labels)),
+ *   d_out[1] = w_kd * max(0, 1 - mean_i cos(know_i, rows_i) - kd_threshold),  d_out[2] = the gate,
+ * with know / hin and their gradients kept in registers.  Forward: 2 launches (per-item kernel +
+ * fixed-order finalize).  Backward: 1 launch writing d_denc [n, L, 64], d_dquery [n, 2, 64], d_drows
+ * [n, 64] and one partial row per block; fr_modal_head_reduce sums them in block order into d_grad
+ * [fr_modal_head_grad_numel()] = dW1 [64x64] | db1 [64] | dW2 [16x64, rows >= H zero] | db2 [16] |
+ * d ln_a.weight [32] | d ln_a.bias | d ln_b.weight | d ln_b.bias.  d_ln / d_mlp as in
+ * fr_modal_fusion_* / fr_health_kd_*.  Replaces 7 launches of the separate ops.
+ * ------------------------------------------------------------------------------------------ */
+int64_t fr_modal_head_partials(int64_t n_items, int backward);
+int64_t fr_modal_head_grad_numel(void);
+int fr_modal_head_fwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
+                      int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, const float* d_rows,
+                      const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,
+                      float w_kd, float* d_out, float* d_partials, int64_t partial_floats, void* stream);
+int fr_modal_head_bwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
+                      int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, const float* d_rows,
+                      const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,
+                      float w_kd, const float* d_out, const float* d_gh, const float* d_gk, float* d_denc,
+                      float* d_dquery, float* d_drows, float* d_partials, int64_t partial_floats, void* stream);
+int fr_modal_head_reduce(const float* d_partials, int64_t n_items, float* d_grad, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused modal fusion of HealthRec (models/cikm_model.py:245-249 with target_attention_layer,

@@ -114,3 +114,20 @@ class TransformerEncoderLayer(nn.TransformerEncoderLayer):
         y = ops.linear(self.dropout(self.activation(ops.linear(x, self.linear1.weight, self.linear1.bias))),
                        self.linear2.weight, self.linear2.bias)
         return self.dropout2(y)
+
+
+def run_encoder(encoder: nn.TransformerEncoder, src, src_key_padding_mask=None):
+    """``encoder(src, src_key_padding_mask=...)`` for an nn.TransformerEncoder of engine layers
+    (cikm_model.py:232): when every layer takes the fused path, the whole stack is ONE autograd node
+    (ops.encoder_stack: each layer's weight-gradient reduction folded into the next backward launch);
+    otherwise the module runs as is."""
+    layers_ = list(encoder.layers)
+    if (encoder.norm is None and layers_ and all(isinstance(m, TransformerEncoderLayer) for m in layers_)
+            and all(m._engine_path(src, None, False) for m in layers_)):
+        kpm = F._canonical_mask(mask=src_key_padding_mask, mask_name="src_key_padding_mask", other_type=None,
+                                other_name="", target_type=src.dtype)
+        if all(m._fused_ok(src, kpm) for m in layers_):
+            out = ops.encoder_stack(src.transpose(0, 1), kpm, [m._fused_cfg(src.device) for m in layers_],
+                                    [m._fused_params() for m in layers_])
+            return out.transpose(0, 1)
+    return encoder(src, src_key_padding_mask=src_key_padding_mask)

@@ -1622,69 +1622,108 @@ def encoder_flops(n_seq: int, L: int, backward: bool) -> int:
 
 def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
     """Algorithmic HBM bytes of one fused encoder-layer launch: the saved activations (qkv 192 +
-    ctx 64 + y1 64 + fact 256 + dact 256 + y2 64 + 4 stats floats per token) written by the
-    forward and read back by the backward, plus x/out (forward) or dout/x/dx (backward); weights are
-    L2-resident."""
+    ctx 64 + y1 64 + y2 64 + 4 stats floats per token: the FF activation is recomputed, not saved)
+    written by the forward and read back by the backward, plus x / out (forward) or dout / x / dx
+    (backward); weights are L2-resident.  The backward's weight-gradient partials are not counted
+    (an implementation choice for the deterministic order, not algorithmic traffic)."""
     T = n_seq * L
-    saved = 4 * T * (192 + 64 + 64 + 256 + 256 + 64 + 4)
+    saved = 4 * T * (192 + 64 + 64 + 64 + 4)
     return (saved + 4 * T * 64 * 3) if backward else (saved + 4 * T * 64 * 2)
 
 
-class _EncoderLayer(torch.autograd.Function):
-    """Fused nn.TransformerEncoderLayer training step (fr_encoder_fwd / fr_encoder_bwd)."""
+class _EncoderStack(torch.autograd.Function):
+    """A stack of fused nn.TransformerEncoderLayer training steps (fr_encoder_fwd / fr_encoder_bwd),
+    one autograd node: forward layer by layer; backward from the top layer down, each layer's
+    ordered weight-gradient reduction folded into the next backward launch (d_prev_partials), the
+    bottom layer's by fr_encoder_reduce."""
 
     @staticmethod
-    def forward(ctx, x, mask, cfg, *params):
+    def forward(ctx, x, mask, cfgs, *flat):
+        nl = len(cfgs)
         NS, L, E = x.shape
         T = NS * L
         dev = x.device
         f32 = dict(dtype=torch.float32, device=dev)
-        out = torch.empty(NS, L, E, **f32)
-        qkv = torch.empty(T, 192, **f32)
-        cx = torch.empty(T, 64, **f32)
-        y1 = torch.empty(T, 64, **f32)
-        fact = torch.empty(T, 256, **f32)
-        dact = torch.empty(int(native.lib().fr_encoder_dact_numel(NS, L)), **f32)  # per-workgroup fragment layout
-        y2 = torch.empty(T, 64, **f32)
-        st1 = torch.empty(T, 2, **f32)
-        st2 = torch.empty(T, 2, **f32)
-        seed_used = torch.empty(1, dtype=torch.int64, device=dev)
-        pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
-        settle_counter(cfg.counter)  # a previous forward's increment not yet applied by a booked step
-        with profiling.region("encoder_fwd", encoder_bytes(NS, L, False)):
-            native.check(native.lib().fr_encoder_fwd(
-                x.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
-                cfg.counter.data_ptr(), seed_used.data_ptr(), out.data_ptr(), qkv.data_ptr(), cx.data_ptr(),
-                y1.data_ptr(), fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(),
-                native.stream_of(x)), "fr_encoder_fwd")
-        defer_increment(cfg.counter)  # advanced by the step's fr_step_book (or before its next read)
-        ctx.cfg = cfg
-        ctx.has_mask = mask is not None
-        ctx.save_for_backward(x, mask if mask is not None else seed_used, qkv, cx, y1, fact, dact, y2, st1,
-                              st2, seed_used, *params)
-        return out
+        lib = native.lib()
+        saved = []
+        h = x
+        for k, cfg in enumerate(cfgs):
+            params = flat[12 * k:12 * (k + 1)]
+            out = torch.empty(NS, L, E, **f32)
+            qkv = torch.empty(T, 192, **f32)
+            cx = torch.empty(T, 64, **f32)
+            y1 = torch.empty(T, 64, **f32)
+            y2 = torch.empty(T, 64, **f32)
+            st1 = torch.empty(T, 2, **f32)
+            st2 = torch.empty(T, 2, **f32)
+            seed_used = torch.empty(1, dtype=torch.int64, device=dev)
+            pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+            settle_counter(cfg.counter)  # a previous forward's increment not yet applied by a booked step
+            with profiling.region("encoder_fwd", encoder_bytes(NS, L, False)):
+                native.check(lib.fr_encoder_fwd(
+                    h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
+                    cfg.counter.data_ptr(), seed_used.data_ptr(), out.data_ptr(), qkv.data_ptr(), cx.data_ptr(),
+                    y1.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), native.stream_of(h)),
+                    "fr_encoder_fwd")
+            defer_increment(cfg.counter)  # advanced by the step's fr_step_book (or before its next read)
+            saved.append((h, qkv, cx, y1, y2, st1, st2, seed_used))
+            h = out
+        ctx.cfgs, ctx.saved, ctx.mask = cfgs, saved, mask
+        ctx.save_for_backward(*flat)
+        return h
 
     @staticmethod
     def backward(ctx, g):
-        x, mask, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used, *params = ctx.saved_tensors
-        cfg = ctx.cfg
-        NS, L, _ = x.shape
+        flat = ctx.saved_tensors
+        cfgs, mask = ctx.cfgs, ctx.mask
+        nl = len(cfgs)
         g = g.contiguous()
+        NS, L, _ = g.shape
         lib = native.lib()
-        dx = torch.empty_like(x)
-        grad = torch.empty(lib.fr_encoder_grad_numel(), dtype=torch.float32, device=x.device)
+        dev = g.device
         nparts = lib.fr_encoder_partials(NS, L)
-        part = torch.empty(nparts, dtype=torch.float32, device=x.device)
-        pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
-        with profiling.region("encoder_bwd", encoder_bytes(NS, L, True)):
-            native.check(lib.fr_encoder_bwd(
-                g.data_ptr(), x.data_ptr(), mask.data_ptr() if ctx.has_mask else None, NS, L, pp, cfg.eps,
-                cfg.drop, cfg.seed, cfg.gelu, seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(),
-                fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
-                grad.data_ptr(),
-                part.data_ptr(), nparts, native.stream_of(g)), "fr_encoder_bwd")
-        grads = torch.split(grad, [p.numel() for p in params])
-        return (dx, None, None) + tuple(gr.view(p.shape) for gr, p in zip(grads, params))
+        grads = [None] * nl
+        prev = None  # (partials, gradient) of the layer above, reduced by this layer's launch
+        for k in range(nl - 1, -1, -1):
+            h, qkv, cx, y1, y2, st1, st2, seed_used = ctx.saved[k]
+            cfg = cfgs[k]
+            params = flat[12 * k:12 * (k + 1)]
+            dx = torch.empty_like(h)
+            grad = torch.empty(lib.fr_encoder_grad_numel(), dtype=torch.float32, device=dev)
+            part = torch.empty(nparts, dtype=torch.float32, device=dev)
+            pp = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+            with profiling.region("encoder_bwd", encoder_bytes(NS, L, True)):
+                native.check(lib.fr_encoder_bwd(
+                    g.data_ptr(), h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
+                    seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(), y2.data_ptr(),
+                    st1.data_ptr(), st2.data_ptr(), dx.data_ptr(), grad.data_ptr() if k == 0 else None,
+                    part.data_ptr(), nparts, prev[0].data_ptr() if prev else None,
+                    prev[1].data_ptr() if prev else None, native.stream_of(g)), "fr_encoder_bwd")
+            grads[k] = grad
+            prev = (part, grad)
+            g = dx
+        out = []
+        for k in range(nl):
+            params = flat[12 * k:12 * (k + 1)]
+            out += [gr.view(p.shape) for gr, p in zip(torch.split(grads[k], [p.numel() for p in params]), params)]
+        ctx.saved = None
+        return (g, None, None) + tuple(out)
+
+
+def encoder_stack(x: torch.Tensor, mask, cfgs, params_list) -> torch.Tensor:
+    """Fused post-norm encoder layers applied in order over batch-first x [n_seq, L, 64] (fp32);
+    ``mask``: [n_seq, L] additive float key mask or None; ``cfgs`` / ``params_list``: one
+    EncoderConfig and the 12 layer tensors (torch order, include/fr_engine.h) per layer."""
+    native.require_device(x)
+    if x.dim() != 3 or x.shape[2] != 64 or x.shape[1] not in ENCODER_LENGTHS or x.dtype != torch.float32:
+        raise native.EngineError(f"fused encoder layer: unsupported input {tuple(x.shape)} {x.dtype}")
+    if len(cfgs) != len(params_list) or not cfgs:
+        raise native.EngineError("encoder_stack: one config per layer")
+    x = x.contiguous()
+    if mask is not None:
+        mask = mask.to(torch.float32).contiguous()
+    flat = [p for ps in params_list for p in ps]
+    return _EncoderStack.apply(x, mask, tuple(cfgs), *flat)
 
 
 class EncoderConfig:
@@ -1703,13 +1742,7 @@ def encoder_layer(x: torch.Tensor, mask, cfg: EncoderConfig, params) -> torch.Te
     """One fused post-norm encoder layer over batch-first x [n_seq, L, 64] (fp32, contiguous);
     ``mask``: [n_seq, L] additive float key mask or None; ``params``: the 12 layer tensors in
     torch order (see include/fr_engine.h)."""
-    native.require_device(x)
-    if x.dim() != 3 or x.shape[2] != 64 or x.shape[1] not in ENCODER_LENGTHS or x.dtype != torch.float32:
-        raise native.EngineError(f"fused encoder layer: unsupported input {tuple(x.shape)} {x.dtype}")
-    x = x.contiguous()
-    if mask is not None:
-        mask = mask.to(torch.float32).contiguous()
-    return _EncoderLayer.apply(x, mask, cfg, *params)
+    return encoder_stack(x, mask, [cfg], [params])
 
 
 # ----------------------------------------------------------------------------- modal fusion
@@ -1982,6 +2015,81 @@ def health_kd_loss(hin, know, rows, labels, mlp, kd_threshold, w_health, w_kd):
     return _HealthKD.apply(hin.contiguous(), know.contiguous(), rows.contiguous(),
                            labels.to(torch.float32).contiguous(), l1.weight, l1.bias, l2.weight, l2.bias,
                            kd_threshold, w_health, w_kd)
+
+
+# ----------------------------------------------------------------------------- fused loss head
+class _ModalHead(torch.autograd.Function):
+    """fr_modal_head_fwd / _bwd: HealthRec's target attentions + normalize heads feeding the health
+    MLP / BCE and KD cosine terms, one node (see include/fr_engine.h)."""
+
+    @staticmethod
+    def forward(ctx, enc, query, ids, num, rows, labels, pad_id, eps, thr, w_h, w_k, ga, ba, gb, bb, w1, b1, w2, b2):
+        n, L, _ = enc.shape
+        H = labels.shape[1]
+        dev = enc.device
+        lib = native.lib()
+        part = torch.empty(lib.fr_modal_head_partials(n, 0), dtype=torch.float32, device=dev)
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
+        mlp = (ctypes.c_void_p * 4)(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr())
+        with profiling.region("modal_head", fusion_bytes(n, L, False) + health_kd_bytes(n, H, False)):
+            native.check(lib.fr_modal_head_fwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
+                                               int(pad_id), n, L, lnp, float(eps), rows.data_ptr(), labels.data_ptr(), H,
+                                               mlp, float(thr), float(w_h), float(w_k), out.data_ptr(), part.data_ptr(),
+                                               part.numel(), native.stream_of(enc)), "fr_modal_head_fwd")
+        ctx.save_for_backward(enc, query, ids, num, rows, labels, ga, ba, gb, bb, w1, b1, w2, b2)
+        ctx.out, ctx.cfg = out, (int(pad_id), float(eps), float(thr), float(w_h), float(w_k))
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, gh, gk):
+        enc, query, ids, num, rows, labels, ga, ba, gb, bb, w1, b1, w2, b2 = ctx.saved_tensors
+        pad_id, eps, thr, w_h, w_k = ctx.cfg
+        n, L, _ = enc.shape
+        H = labels.shape[1]
+        dev = enc.device
+        zero = None
+        if gh is None or gk is None:
+            zero = torch.zeros((), dtype=torch.float32, device=dev)
+        gh = zero if gh is None else gh.to(torch.float32).contiguous()
+        gk = zero if gk is None else gk.to(torch.float32).contiguous()
+        lib = native.lib()
+        denc, dq, drows = torch.empty_like(enc), torch.empty_like(query), torch.empty_like(rows)
+        part = torch.empty(lib.fr_modal_head_partials(n, 1), dtype=torch.float32, device=dev)
+        grad = torch.empty(lib.fr_modal_head_grad_numel(), dtype=torch.float32, device=dev)
+        lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
+        mlp = (ctypes.c_void_p * 4)(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr())
+        with profiling.region("modal_head", fusion_bytes(n, L, True) + health_kd_bytes(n, H, True)):
+            native.check(lib.fr_modal_head_bwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(), pad_id, n,
+                                               L, lnp, eps, rows.data_ptr(), labels.data_ptr(), H, mlp, thr, w_h, w_k,
+                                               ctx.out.data_ptr(), gh.data_ptr(), gk.data_ptr(), denc.data_ptr(),
+                                               dq.data_ptr(), drows.data_ptr(), part.data_ptr(), part.numel(),
+                                               native.stream_of(enc)), "fr_modal_head_bwd")
+            native.check(lib.fr_modal_head_reduce(part.data_ptr(), n, grad.data_ptr(), native.stream_of(enc)),
+                         "fr_modal_head_reduce")
+        D, HM = 64, 16
+        o = 0
+        dw1 = grad[o:o + D * D].view(D, D); o += D * D
+        db1 = grad[o:o + D]; o += D
+        dw2 = grad[o:o + H * D].view(H, D); o += HM * D
+        db2 = grad[o:o + H]; o += HM
+        dln = grad[o:o + 128].view(4, 32)
+        return (denc, dq, None, None, drows, None, None, None, None, None, None, dln[0], dln[1], dln[2], dln[3],
+                dw1, db1, dw2, db2)
+
+
+def modal_head(enc, query, ids, num, pad_id, rows, labels, ln_a, ln_b, mlp, kd_threshold, w_health, w_kd):
+    """modal_fusion + health_kd_loss as one node (cikm_model.py:245-264): returns (w_health * BCE sum,
+    w_kd * max(0, 1 - mean cos(know, rows) - kd_threshold)).  ``mlp``: Linear(64, 64), ReLU,
+    Linear(64, H <= 16); ``ln_a`` / ``ln_b``: the target attentions' LayerNorm(32) modules."""
+    native.require_device(enc, query, ids, rows, labels)
+    if ln_a.eps != ln_b.eps:
+        raise native.EngineError("modal_head: both target-attention LayerNorms must share eps")
+    l1, l2 = mlp[0], mlp[2]
+    return _ModalHead.apply(enc.contiguous(), query.contiguous(), ids.contiguous(), num.contiguous(), rows.contiguous(),
+                            labels.to(torch.float32).contiguous(), int(pad_id), ln_a.eps,
+                            kd_threshold, w_health, w_kd, ln_a.weight, ln_a.bias, ln_b.weight, ln_b.bias,
+                            l1.weight, l1.bias, l2.weight, l2.bias)
 
 
 # ----------------------------------------------------------------------------- dCor

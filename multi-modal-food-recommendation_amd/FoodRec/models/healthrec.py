@@ -34,6 +34,10 @@ FUSED_FUSION = os.environ.get("FR_FUSED_FUSION", "1") != "0"
 FUSED_HEAD = os.environ.get("FR_FUSED_HEAD", "1") != "0"
 # FR_FUSED_PROJECTION=0 keeps gather + ops.linear for the image / text projections
 FUSED_PROJECTION = os.environ.get("FR_FUSED_PROJECTION", "1") != "0"
+# FR_FUSED_LOSS_HEAD=0 keeps the modal fusion and the health / KD head as two nodes (four kernels)
+FUSED_LOSS_HEAD = os.environ.get("FR_FUSED_LOSS_HEAD", "1") != "0"
+# FR_PROJECTION_FIRST=1: the modal projections before the encoder (their backward after the encoder's)
+PROJECTION_FIRST = os.environ.get("FR_PROJECTION_FIRST", "0") == "1"
 # FR_FUSED_GRAPH=0 keeps the concatenated-ego propagation + separate BPR op (full UI propagation)
 FUSED_GRAPH = os.environ.get("FR_FUSED_GRAPH", "1") != "0"
 
@@ -178,6 +182,13 @@ class HealthRec(GeneralRecommender):
                                                            (self.text_embedding.weight, self.text_trs)], exchange=xg)
                 projected = torch.cuda.Event()
                 projected.record(aux)
+        elif proj and PROJECTION_FIRST:
+            # projected before the encoder: its autograd node is then older than the encoder's, and the
+            # engine runs the younger of two ready nodes first -- the encoder's backward, then the
+            # projection backward (dW + the factored table rows, read only by the optimiser)
+            join()
+            mm_query = ops.modal_projection(all_item, [(self.image_embedding.weight, self.image_trs),
+                                                       (self.text_embedding.weight, self.text_trs)], exchange=xg)
         ingr_all = self.ingre_embedding.weight  # the reference discards the propagated ingredients
         health_level = _pn(batch_data, "hl_mh")
         ingredients = _pn(batch_data, "ingre_code")
@@ -190,13 +201,15 @@ class HealthRec(GeneralRecommender):
         mask = batch_data.get("pn_pad_kpm")  # additive key mask gathered with the codes (engine batch), else computed
         if mask is None:
             mask = ingredients == self.n_ingredients
-        encoded = self.ingr_encoder(ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
+        encoded = layers.run_encoder(self.ingr_encoder, ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
 
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
         if aux is not None:
             main.wait_event(projected)
             mm_query.record_stream(main)
+        elif proj and PROJECTION_FIRST:
+            pass
         elif proj:
             join()
             # gathers folded into the projection GEMMs; the tables' gradient stays factored (dY, W)
@@ -208,6 +221,20 @@ class HealthRec(GeneralRecommender):
             txt_q = ops.linear(ops.embedding(all_item, self.text_embedding.weight, exchange=xg),
                                self.text_trs.weight, self.text_trs.bias).unsqueeze(1)
             mm_query = torch.cat([img_q, txt_q], dim=1)
+        if FUSED_LOSS_HEAD and self._fused_fusion(encoded, mm_query) and self._fused_head(encoded, health_level):
+            # the target attentions, normalize heads, health MLP / BCE and KD cosine as ONE node
+            # (fr_modal_head_*: 2 launches forward, 2 backward; know / hin never leave the registers)
+            if fused_graph:
+                mf_loss, emb3, item_rows = ops.graph_bpr_end(branch)
+            else:
+                mf_loss, emb3, item_rows = ops.bpr_emb_loss(ui_all, None, self.user_embedding.weight,
+                                                            self.item_embedding.weight, user, pos_item, neg_item,
+                                                            item_rows=True, item_offset=self.n_users)
+            health_term, kd_term = ops.modal_head(encoded, mm_query, ingredients, ingre_num, self.n_ingredients,
+                                                  item_rows, health_level, self.mm_target_atten.ln,
+                                                  self.ingre_target_atten.ln, self.health_mlp, self.kd_threshold,
+                                                  self.loss_health, self.loss_kd)
+            return self._losses(mf_loss, health_term, kd_term, emb3, ing_norms, B)
         if self._fused_fusion(encoded, mm_query):
             # both target attentions + the normalize heads in one HIP kernel pair (fr_modal_fusion_*)
             item_know, health_in = ops.modal_fusion(encoded, mm_query, ingredients, ingre_num, self.n_ingredients,
@@ -235,6 +262,9 @@ class HealthRec(GeneralRecommender):
             kd = 1 - cosine_similarity(item_know, item_rows, dim=-1).mean()
             kd_term = self.loss_kd * self.norm_loss(kd, self.kd_threshold)
 
+        return self._losses(mf_loss, health_term, kd_term, emb3, ing_norms, B)
+
+    def _losses(self, mf_loss, health_term, kd_term, emb3, ing_norms, B):
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         if emb3.is_cuda and ing_norms.is_cuda and emb3.dtype == torch.float32 and ing_norms.dtype == torch.float32:
             return mf_loss, health_term, kd_term, ops.reg_combine(emb3, ing_norms, B, self.reg_weight)

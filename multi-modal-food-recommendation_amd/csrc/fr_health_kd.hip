@@ -17,20 +17,16 @@
 // Loss sums are per-block partials summed by a one-wave finalize launch (fixed-order wave sum);
 // parameter gradients are per-block partials summed in a fixed order by a reduce kernel.
 // Forward item inputs are loaded one item ahead; every load loop has a compile-time trip count.
-#include "fr_common.h"
+#include "fr_head_math.h"
 
 namespace {
 
 constexpr int D = 64;
-constexpr int HMAX = 16;
 constexpr int WAVES = 8;          // forward: waves per block (2 per SIMD), up to 128 blocks
 constexpr int BWAVES = 4;         // backward: 4 waves per block (its 64 dW1 accumulators per lane need the
                                   // full register file), up to 256 blocks
 constexpr int MAX_BLOCKS = 128;   // forward grid cap (1024 items: one per wave)
 constexpr int MAX_BLOCKS_BWD = 256;  // backward grid cap: bounds the parameter-gradient partials
-constexpr int W1S = D + 1;        // padded LDS row stride of W1
-constexpr float kCosEps = 1e-8f;  // cosine_similarity eps
-constexpr int NPART_BWD = D * D + D + HMAX * D + HMAX;  // dW1, db1, dW2 (HMAX rows), db2
 
 struct HeadArgs {
   const float* hin;     // [n, 64]
@@ -50,36 +46,9 @@ struct HeadArgs {
   float *dw1, *db1, *dw2, *db2;
 };
 
-__device__ __forceinline__ float wsum(float v) { return group_sum<64>(v); }
-
-__device__ __forceinline__ float bcast(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-
-// W1 (padded), b1, W2, b2 into LDS
-// (compile-time trip counts: every thread's loads are in flight together)
 template <int NW>
 __device__ __forceinline__ void stage_weights(const HeadArgs& a, float* sw1, float* sw2, float* sb) {
-  constexpr int T = 64 * NW;
-  float v1[D * D / T], v2[HMAX * D / T];
-#pragma unroll
-  for (int u = 0; u < D * D / T; ++u) v1[u] = a.w1[threadIdx.x + u * T];
-#pragma unroll
-  for (int u = 0; u < HMAX * D / T; ++u) {
-    const int e = threadIdx.x + u * T;
-    v2[u] = e < a.H * D ? a.w2[e] : 0.f;
-  }
-  const int e = threadIdx.x;
-  const float vb = e < D ? a.b1[e] : (e < D + a.H ? a.b2[e - D] : 0.f);
-#pragma unroll
-  for (int u = 0; u < D * D / T; ++u) {
-    const int f = threadIdx.x + u * T;
-    sw1[(f >> 6) * W1S + (f & 63)] = v1[u];
-  }
-#pragma unroll
-  for (int u = 0; u < HMAX * D / T; ++u) sw2[threadIdx.x + u * T] = v2[u];
-  if (e < D + HMAX) sb[e] = vb;
-  __syncthreads();
+  head_stage_weights<64 * NW>(a.w1, a.b1, a.w2, a.b2, a.H, sw1, sw2, sb);
 }
 
 // one item's inputs for lane j (loaded one item ahead of use)
@@ -98,20 +67,8 @@ __device__ __forceinline__ ItemIn load_item(const HeadArgs& a, int64_t i, int j)
   return x;
 }
 
-// z1 = W1 h + b1 for lane j (row j of W1), h broadcast by readlane; four interleaved partial sums
-// (k mod 4) keep the dependent FMA chain 16 long instead of 64
 __device__ __forceinline__ float layer1(const float* sw1, const float* sb, float h, int j) {
-  float z[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < D; ++k) z[k & 3] = fmaf(sw1[j * W1S + k], bcast(h, k), z[k & 3]);
-  return ((z[0] + z[1]) + (z[2] + z[3])) + sb[j];
-}
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
-
-__device__ __forceinline__ float bce(float p, float y) {
-  const float lp = fmaxf(logf(p), -100.f), l1p = fmaxf(log1pf(-p), -100.f);
-  return (y - 1.f) * l1p - y * lp;
+  return head_layer1(sw1, sb, h, j);
 }
 
 __global__ __launch_bounds__(64 * WAVES) void head_fwd_kernel(HeadArgs a) {

@@ -24,6 +24,8 @@ Fixtures at BASELINE widths (seeded synthetic data at the Allrecipes / Foodcom s
 the reference's format and read by the reference's own loader; only small slices are stored):
   wide_CIKM_Model_allrecipes.npz   HealthRec (p=0): first K training steps of Trainer.fit's stream
   wide_PRICAI_ModelX_foodcom.npz   CLUSSL, 2,000 clusters: first K training steps
+  wide_PRICAI_ModelX_infonce_foodcom.npz   the same with the InfoNCE SSL term of the commented
+                                   pricai_modelx.py:259 (CL_loss over the three view pairs)
     per step: the batch ids and every loss component; step 0: every gradient of the small
     parameters, sampled rows of the large ones; init and after K Adam steps: sampled parameter rows
 
@@ -193,7 +195,7 @@ def main(argv=None):
         train_golden("train_mg_LightGCN.npz", make_config("LightGCN", models["LightGCN"], mg=True), "LightGCN",
                      FoodData, init_seed, get_model, Trainer, mg=True)
     if "wide" in want:
-        for name in want["wide"] or ("CIKM_Model", "PRICAI_ModelX"):
+        for name in want["wide"] or tuple(WIDE):
             wide_golden(name, make_synthetic, write_reference_format, make_config, FoodData, init_seed, get_model,
                         Trainer, TrainDataLoader, DataLoader, RandomSampler)
     if "ops" in want:
@@ -298,10 +300,32 @@ def train_golden(fname, cfg, name, FoodData, init_seed, get_model, Trainer, mg=F
     print("train", fname, out["train_loss"], btr)
 
 
-WIDE = {  # model -> (synthetic shape, dataset name, training steps, config overrides)
-    "CIKM_Model": ("allrecipes", "Allrecipes", 3, {"attention_probs_dropout_prob": 0.0}),
-    "PRICAI_ModelX": ("foodcom", "Foodcom", 4, {}),
+WIDE = {  # case -> (model, synthetic shape, dataset name, training steps, config overrides, loss)
+    "CIKM_Model": ("CIKM_Model", "allrecipes", "Allrecipes", 3, {"attention_probs_dropout_prob": 0.0}, None),
+    "PRICAI_ModelX": ("PRICAI_ModelX", "foodcom", "Foodcom", 4, {}, None),
+    # the InfoNCE SSL variant: the reference's commented line pricai_modelx.py:259 (CL_loss over the
+    # three view pairs), computed by the harness with the reference model's own methods
+    "PRICAI_ModelX_infonce": ("PRICAI_ModelX", "foodcom", "Foodcom", 3, {}, "infonce"),
 }
+
+
+def clussl_infonce_losses(model, batch):
+    """PRICAI_ModelX.calculate_loss (pricai_modelx.py:234-276) with its SSL term replaced by the
+    commented InfoNCE line (:259): CL_loss(cat([image, text])) + CL_loss(cat([image, ingre])) +
+    CL_loss(cat([ingre, text])) over the batch items' views.  The BPR and EmbLoss terms are the
+    reference's own calculate_loss outputs; the views come from a second reference forward()
+    (deterministic: the same values, and the gradients of both graphs sum into the parameters)."""
+    import torch
+    mf, _, reg = model.calculate_loss(batch)
+    all_item = torch.cat([batch["pos_i_id"], batch["neg_i_id"]], dim=0)
+    _, _, (image, text, ingre) = model.forward()
+    a, b, c = image[all_item], text[all_item], ingre[all_item]
+    cl = model.CL_loss(torch.cat([a, b], dim=0)) + model.CL_loss(torch.cat([a, c], dim=0)) + \
+        model.CL_loss(torch.cat([c, b], dim=0))
+    return mf, model.loss_cl * cl, reg
+
+
+WIDE_LOSS = {None: lambda model, batch: model.calculate_loss(batch), "infonce": clussl_infonce_losses}
 WIDE_ROWS = 48          # sampled rows per large parameter
 WIDE_BIG = 1 << 16      # parameters with more elements than this are stored as sampled rows
 
@@ -331,7 +355,9 @@ def wide_golden(name, make_synthetic, write_reference_format, make_config, FoodD
     Trainer.fit's order (init_seed -> model -> Trainer -> two TrainDataLoaders -> RandomSampler),
     then the step loop of trainer.py:177-224 (zero_grad, calculate_loss, sum, backward, Adam)."""
     import torch
-    shape, dsname, steps, extra = WIDE[name]
+    case = name
+    name, shape, dsname, steps, extra, loss_kind = WIDE[case]
+    loss_fn = WIDE_LOSS[loss_kind]
     ds = make_synthetic(shape, 0, negatives=False)
     digest = wide_digest(ds)
     # the reference's .negative reader needs >= 1 candidate per line (dataset.py:245-256); the
@@ -367,9 +393,9 @@ def wide_golden(name, make_synthetic, write_reference_format, make_config, FoodD
             for pn, v in model.state_dict().items():
                 out[f"sd0/{pn}"] = (v[torch.from_numpy(rows[pn])] if pn in rows else v).numpy().copy()
         if k == 0:
-            _wide_f64_step(model, batch, rows, out)
+            _wide_f64_step(model, batch, rows, out, loss_fn)
         trainer.optimizer.zero_grad()
-        losses = model.calculate_loss(batch)
+        losses = loss_fn(model, batch)
         losses = losses if isinstance(losses, tuple) else (losses,)
         out[f"step{k}/loss"] = np.array([float(l.detach().reshape(-1)[0]) for l in losses])
         sum(losses).backward()
@@ -379,14 +405,14 @@ def wide_golden(name, make_synthetic, write_reference_format, make_config, FoodD
                     g = p.grad
                     out[f"grad0/{pn}"] = (g[torch.from_numpy(rows[pn])] if pn in rows else g).numpy().copy()
         trainer.optimizer.step()
-        print("wide", name, "step", k, out[f"step{k}/loss"], flush=True)
+        print("wide", case, "step", k, out[f"step{k}/loss"], flush=True)
     for pn, p in model.named_parameters():
         v = p.detach()
         out[f"final/{pn}"] = (v[torch.from_numpy(rows[pn])] if pn in rows else v).numpy().copy()
-    np.savez_compressed(os.path.join(OUT, f"wide_{name}_{shape}.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, f"wide_{case}_{shape}.npz"), **out)
 
 
-def _wide_f64_step(model, batch, rows, out):
+def _wide_f64_step(model, batch, rows, out, loss_fn):
     """The same first step of the reference model evaluated in float64 (a deep copy: parameters,
     feature tensors and adjacencies cast): ``step0/loss_f64`` and ``grad0_f64/*``.  At these widths
     the reference's own fp32 CPU gradients carry ~1e-4 - 4e-4 relative error upstream of the health
@@ -400,7 +426,7 @@ def _wide_f64_step(model, batch, rows, out):
             setattr(m64, k, v.double())
     b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in batch.items()}
     m64.train()
-    losses = m64.calculate_loss(b64)
+    losses = loss_fn(m64, b64)
     losses = losses if isinstance(losses, tuple) else (losses,)
     out["step0/loss_f64"] = np.array([float(l.detach().reshape(-1)[0]) for l in losses])
     sum(losses).backward()

@@ -166,8 +166,7 @@ def test_encoder_writes_stay_in_bounds(cuda, NS, L):
     drop = (ctypes.c_float * 4)(0.1, 0.1, 0.1, 0.1)
     counter = torch.zeros(1, dtype=torch.int64, device=cuda)
     seed_used = torch.zeros(1, dtype=torch.int64, device=cuda)
-    sizes = {"out": T * 64, "qkv": T * 192, "ctx": T * 64, "y1": T * 64, "fact": T * 256,
-             "dact": int(lib.fr_encoder_dact_numel(NS, L)), "y2": T * 64, "st1": T * 2, "st2": T * 2}
+    sizes = {"out": T * 64, "qkv": T * 192, "ctx": T * 64, "y1": T * 64, "y2": T * 64, "st1": T * 2, "st2": T * 2}
     outs = {k: guarded(n) for k, n in sizes.items()}
     s = native.stream_of(x)
     native.check(lib.fr_encoder_fwd(x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1, counter.data_ptr(),
@@ -185,11 +184,28 @@ def test_encoder_writes_stay_in_bounds(cuda, NS, L):
     pa_b, pa = guarded(nparts)
     native.check(lib.fr_encoder_bwd(g.data_ptr(), x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1,
                                     seed_used.data_ptr(), *[outs[k][1].data_ptr() for k in list(sizes)[1:]],
-                                    dx.data_ptr(), gr.data_ptr(), pa.data_ptr(), nparts, s), "fr_encoder_bwd")
+                                    dx.data_ptr(), gr.data_ptr(), pa.data_ptr(), nparts, None, None, s),
+                 "fr_encoder_bwd")
     torch.cuda.synchronize()
     assert intact(dx_b, T * 64), "backward wrote outside dx"
     assert intact(gr_b, int(lib.fr_encoder_grad_numel())), "backward wrote outside the gradient"
     assert intact(pa_b, nparts), "backward wrote outside the partials"
+    # the same backward again, reducing the first call's partials in its own launch (a stacked
+    # encoder's folded reduction) and leaving its own unreduced: the folded sum stays inside its
+    # output, equals fr_encoder_reduce's to fp32 reassociation, and the first partials are not written
+    pa_snap = pa_b.clone()
+    pb_b, pb = guarded(nparts)
+    gf_b, gf = guarded(int(lib.fr_encoder_grad_numel()))
+    dx2_b, dx2 = guarded(T * 64)
+    native.check(lib.fr_encoder_bwd(g.data_ptr(), x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1,
+                                    seed_used.data_ptr(), *[outs[k][1].data_ptr() for k in list(sizes)[1:]],
+                                    dx2.data_ptr(), None, pb.data_ptr(), nparts, pa.data_ptr(), gf.data_ptr(), s),
+                 "fr_encoder_bwd (folded reduction)")
+    torch.cuda.synchronize()
+    assert intact(gf_b, int(lib.fr_encoder_grad_numel())) and intact(pb_b, nparts) and intact(dx2_b, T * 64)
+    assert torch.equal(pa_b, pa_snap), "the folded reduction wrote the partials it reads"
+    assert torch.equal(dx2, dx) and torch.equal(pb, pa), "the backward itself must not change"
+    torch.testing.assert_close(gf, gr, rtol=1e-5, atol=1e-6 * float(gr.abs().max()))
     assert torch.equal(g_b, g_snap), "backward wrote its upstream gradient"
     for k in sizes:
         assert torch.equal(outs[k][0], snap[k]), f"backward wrote the saved {k}"
@@ -197,3 +213,37 @@ def test_encoder_writes_stay_in_bounds(cuda, NS, L):
         assert intact(b, p.numel()) and torch.equal(v.cpu(), p.reshape(-1)), "a parameter was written"
     assert intact(x_b, T * 64) and intact(m_b, T)
     assert torch.isfinite(dx).all() and torch.isfinite(gr).all()
+
+
+@pytest.mark.parametrize("NS,L,drop", [(1024, 20, (0.5, 0.5, 0.5, 0.5)), (257, 20, (0.0,) * 4), (101, 8, (0.1, 0.2, 0.3, 0.4))])
+def test_encoder_stack_two_layers(cuda, NS, L, drop):
+    """ops.encoder_stack (HealthRec's 2-layer ingredient encoder as ONE autograd node, layer 2's
+    weight-gradient reduction folded into layer 1's backward launch) vs two float64 layers with the
+    kernels' own masks: output 2e-5 * max, dx and all 24 parameter gradients 1e-4 * max."""
+    from FoodRec.engine import ops
+    gen = torch.Generator().manual_seed(NS + 7 * L)
+    x = torch.randn(NS, L, 64, generator=gen, dtype=torch.float64)
+    pad = torch.rand(NS, L, generator=gen) < 0.4
+    pad[:, 0] = False
+    mask = torch.zeros(NS, L, dtype=torch.float64).masked_fill(pad, float("-inf"))
+    params = [_params(gen), _params(gen)]
+    gout = torch.randn(NS, L, 64, generator=gen, dtype=torch.float64)
+    cfgs = [ops.EncoderConfig((1e-5, 1e-5), drop, True, 100 + k, cuda) for k in range(2)]
+    for k, c in enumerate(cfgs):
+        c.counter.fill_(3 + k)
+    xg = x.float().to(cuda).requires_grad_(True)
+    pg = [[p.float().to(cuda).requires_grad_(True) for p in ps] for ps in params]
+    out = ops.encoder_stack(xg, mask.float().to(cuda), cfgs, pg)
+    out.backward(gout.float().to(cuda))
+    xr = x.clone().requires_grad_(True)
+    pr = [[p.clone().requires_grad_(True) for p in ps] for ps in params]
+    h = xr
+    for k in range(2):
+        masks = O.encoder_keep_masks(100 + k, 3 + k, NS, L, drop)
+        h = O.encoder_layer_f64(h, mask, pr[k], masks, drop, gelu=True)
+    h.backward(gout)
+    o = out.detach().double().cpu()
+    assert (o - h.detach()).abs().max() <= 2e-5 * h.abs().max() + 2e-6
+    for a, b in zip([xg] + pg[0] + pg[1], [xr] + pr[0] + pr[1]):
+        ga, gb = a.grad.double().cpu(), b.grad
+        assert (ga - gb).abs().max() <= 1e-4 * gb.abs().max() + 1e-6

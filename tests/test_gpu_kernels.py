@@ -359,7 +359,7 @@ def test_infonce(cuda, b):
                                atol=1e-4 * float(H.grad.abs().max()))
 
 
-@pytest.mark.parametrize("b", [512, 37])
+@pytest.mark.parametrize("b", [1024, 512, 37])
 def test_infonce_pairs(cuda, b):
     """ops.infonce_pairs (all pairs in the same launches, views normalised once, no concatenation)
     against the float64 oracle sum of CL_loss(cat([views[a], views[b]])) over CLUSSL's three pairs:

@@ -4,7 +4,9 @@ The fixtures hold the reference's own first K training steps (Trainer.fit's orde
 model -> Trainer -> two TrainDataLoaders -> RandomSampler; then trainer.py:177-224) on seeded
 synthetic data at the Allrecipes shape (HealthRec = CIKM_Model, 2048-d image / 512-d text tables,
 NI = 19,987, attention dropout 0) and the Foodcom shape (CLUSSL = PRICAI_ModelX, 2,000 clusters per
-modality graph), d = 64, B = 512 -- the configurations bench.py measures (BASELINE configs 2, 3).
+modality graph; with the reference's dCor SSL term and with the InfoNCE term of its commented
+pricai_modelx.py:259, b = 1024 rows per view), d = 64, B = 512 -- the configurations bench.py
+measures (BASELINE configs 2, 3).
 
 Checked here on the MI355X, eagerly and through the graphed step bench.py times (DeviceFeed batch
 gather inside the graph, lazy row Adam with the side-stream catch-up of HealthRec's image/text rows):
@@ -40,8 +42,13 @@ from helpers import golden
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = {"CIKM_Model": ("allrecipes", "Allrecipes", {"attention_probs_dropout_prob": 0.0}),
-         "PRICAI_ModelX": ("foodcom", "Foodcom", {})}
+CASES = {  # fixture case -> (model, shape, dataset name, config overrides)
+    "CIKM_Model": ("CIKM_Model", "allrecipes", "Allrecipes", {"attention_probs_dropout_prob": 0.0}),
+    "PRICAI_ModelX": ("PRICAI_ModelX", "foodcom", "Foodcom", {}),
+    # CLUSSL with the InfoNCE SSL term (ssl_mode infonce) vs the reference's commented
+    # pricai_modelx.py:259 (CL_loss over the three [2B = 1024]-row view pairs), harness-computed
+    "PRICAI_ModelX_infonce": ("PRICAI_ModelX", "foodcom", "Foodcom", {"ssl_mode": "infonce"}),
+}
 _DATA = {}
 
 
@@ -61,17 +68,17 @@ def _setup(cuda, name, graph):
     from FoodRec.engine.sampler import TripleSampler
     from FoodRec.utils.configurator import Config
     from FoodRec.utils.utils import get_model, init_seed
-    shape, dsname, extra = CASES[name]
+    model_name, shape, dsname, extra = CASES[name]
     g = golden(f"wide_{name}_{shape}.npz")
     digest, data, n_cluster = _dataset(shape)
     assert digest == str(g["digest"]), "synthetic generator changed: regenerate the wide goldens"
-    cfg = Config(name, dsname, {"use_gpu": True, "seed": 999, "n_cluster": n_cluster, "cuda_graph": graph,
+    cfg = Config(model_name, dsname, {"use_gpu": True, "seed": 999, "n_cluster": n_cluster, "cuda_graph": graph,
                                 "cuda_graph_warmup": 1, "log_root": "/tmp/frlog/", "ckp_root": "/tmp/frckp/",
                                 **extra})
     cfg["device"] = cuda
     data.args_config = cfg
     init_seed(999)
-    model = get_model(name)(cfg, data).to(cuda)
+    model = get_model(model_name)(cfg, data).to(cuda)
     tr = Trainer(cfg, model)
     sampler = TripleSampler(data, int(g["batch_size"]), cuda)  # = the two TrainDataLoader constructions
     return g, cfg, model, tr, sampler
