@@ -152,6 +152,9 @@ int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
  * The backward takes d(out[P]) (the summed loss) scaled by g (or device d_gscale[0]) and
  * ACCUMULATES into dviews[v] (any may be NULL).
  * ------------------------------------------------------------------------------------------ */
+/* SSL kernel choice: mfma = 1 (default) runs the dCor / InfoNCE Gram tiles on v_mfma_f32_16x16x4_f32,
+ * 0 on the VALU 4x4-per-thread tiles (A/B measurements), -1 keeps it; returns the previous choice. */
+int fr_ssl_kernels(int mfma);
 int64_t fr_dcor_workspace(int64_t n, int n_views);
 
 int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, int d,
@@ -779,6 +782,13 @@ int fr_step_book(const float* const* d_parts, int n, double* d_acc, int accumula
  *   d_flags[u] 0 = exact, 1 = the k+1 largest scores tie or a score is NaN (numpy's tie order
  *              decides: rank on the host), 2 = more than fr_rank_capacity() candidates.
  * k <= 31.  One launch, one wave per user, no host sync. */
+/* fr_score_segments: the evaluation's candidate scores without materialised gathers --
+ * d_out[e] = dot(d_user[d_uid[s]], d_item[d_items[e]]) for e in [d_offsets[s], d_offsets[s + 1]),
+ * s < n_seg (HealthRec / CLUSSL / LightGCN inference_fast, cikm_model.py:294-302, over
+ * EvalByUserDataloader's per-user lists, dataloader.py:228-302).  d = 64; row strides in floats. */
+int fr_score_segments(const float* d_user, int64_t ld_user, const float* d_item, int64_t ld_item,
+                      const int64_t* d_uid, const int64_t* d_offsets, int64_t n_seg, const int64_t* d_items, int d,
+                      float* d_out, void* stream);
 int fr_rank_metrics(const float* d_scores, const int64_t* d_offsets, const int32_t* d_npos, int64_t n_users,
                     int k, uint32_t* d_hits, int64_t* d_auc, uint8_t* d_flags, void* stream);
 int fr_rank_capacity(void);

@@ -676,10 +676,52 @@ class Trainer(AbstractTrainer):
         if isinstance(self.optimizer, FusedAdam):
             self.optimizer.flush()
 
+    def _device_candidates(self, is_test):
+        """The evaluation lists on the device (uid / offsets / items per user segment, plus the host
+        lens / npos), built once per split and kept: after the first pass removed the positives from
+        the negatives in place, every later EvalByUserDataloader pass yields the same lists."""
+        ds = self.model.dataset
+        neg = ds.testNegatives if is_test else ds.validNegatives
+        cache = self.__dict__.setdefault("_dev_candidates", {})
+        ent = cache.get(bool(is_test))
+        if ent is None or ent["neg"] is not neg:
+            users, items, lens, npos = self._candidates(is_test)
+            dev = torch.device(self.device)
+            off = np.zeros(len(lens) + 1, np.int64)
+            np.cumsum(lens, out=off[1:])
+            uid = users[off[:-1][lens > 0]] if (lens > 0).all() else None
+            ent = {"neg": neg, "lens": lens, "npos": npos, "n": int(off[-1]),
+                   "uid": None if uid is None else torch.from_numpy(np.ascontiguousarray(uid)).to(dev),
+                   "off": torch.from_numpy(off).to(dev), "items": torch.from_numpy(items).to(dev),
+                   "users": users, "items_host": items}
+            cache[bool(is_test)] = ent
+        return ent
+
+    def _fused_scoring(self) -> bool:
+        """The model's inference_fast is the plain gather-dot of its forward() tables (engine models
+        declare it: ``fused_scores``) and the evaluation runs on the device: fr_score_segments."""
+        return (self._on_gpu() and bool(self.config["graph_inference_fast"])
+                and getattr(type(self.model), "fused_scores", False))
+
+    @torch.no_grad()
+    def _score_fused(self, dc):
+        """Device scores of the cached evaluation lists (fr_score_segments over forward()'s tables)."""
+        out = self.model.forward()
+        return ops.score_segments(out[0], out[1], dc["uid"], dc["off"], dc["items"])
+
     def _valid_by_user_epoch(self, valid_data=None, is_test=False):
         self.flush_optimizer()
-        users, items, lens, npos = self._candidates(is_test)
         neg_num = self.config["neg_sample_num"]
+        if self._fused_scoring():
+            dc = self._device_candidates(is_test)
+            if dc["uid"] is not None:
+                sc = self._score_fused(dc)
+                res = self._rank_scores(sc, dc["lens"], dc["npos"], neg_num)
+                recalls, ndcgs, aucs = res.mean(axis=0).tolist()
+                metrics = {"AUC": aucs[0], "Recall@10": recalls[0], "Recall@20": recalls[1],
+                           "NDCG@10": ndcgs[0], "NDCG@20": ndcgs[1]}
+                return metrics["NDCG@20"], metrics
+        users, items, lens, npos = self._candidates(is_test)
         if self._on_gpu():
             res = self._rank_on_device(users, items, lens, npos, neg_num)
         else:
@@ -699,7 +741,11 @@ class Trainer(AbstractTrainer):
         counts) and the host turns them into the reference's float64 metrics (metrics_from_hits).
         Users whose top-21 scores tie (numpy's argsort tie order decides) are ranked by the host's
         numpy path on their own scores."""
-        sc = self._score(users, items, on_device=True)
+        return self._rank_scores(self._score(users, items, on_device=True), lens, npos, neg_num)
+
+    def _rank_scores(self, sc, lens, npos, neg_num):
+        """fr_rank_metrics over device scores + the reference's float64 metric assembly; users whose
+        top-21 scores tie go to the host's numpy path on their own scores."""
         hits, aucc, flags = ops.rank_metrics(sc, lens, npos, 20)
         res = metrics_from_hits(hits, lens, npos, aucc, neg_num)
         redo = np.nonzero(flags)[0]

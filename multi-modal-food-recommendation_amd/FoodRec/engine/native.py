@@ -83,6 +83,8 @@ _SIGS = {
                                 c_void_p, c_int64, c_void_p]),
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "fr_score_segments": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                                  c_int, c_void_p, c_void_p]),
     "fr_rank_metrics": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p]),
     "fr_rank_capacity": (c_int, []),
@@ -119,6 +121,7 @@ _SIGS = {
                               c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                               c_void_p, c_int64, c_void_p]),
+    "fr_ssl_kernels": (c_int, [c_int]),
     "fr_dcor_workspace": (c_int64, [c_int64, c_int]),
     "fr_dcor_fwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
                             c_void_p, c_void_p, c_int64, c_void_p]),

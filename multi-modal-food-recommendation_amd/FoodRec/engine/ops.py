@@ -2313,6 +2313,24 @@ def full_sort_topk(user_rows: torch.Tensor, item_table: torch.Tensor, k: int, us
 
 
 # ----------------------------------------------------------------------------- evaluation ranking
+def score_segments(user_table: torch.Tensor, item_table: torch.Tensor, uid: torch.Tensor, offsets: torch.Tensor,
+                   items: torch.Tensor) -> torch.Tensor:
+    """``(user_table[u] * item_table[items[e]]).sum()`` for every candidate e of every user segment
+    (fr_score_segments): uid [S] user ids, offsets [S + 1] segment bounds, items [n] (int64 device
+    tensors).  The graph models' inference_fast over the evaluation lists without the [n, 64] gathers."""
+    native.require_device(user_table, item_table, uid, offsets, items)
+    d = user_table.shape[1]
+    if d != 64 or item_table.shape[1] != d or user_table.dtype != torch.float32 or item_table.dtype != torch.float32 \
+            or user_table.stride(1) != 1 or item_table.stride(1) != 1:
+        raise native.EngineError("score_segments: fp32 [*, 64] row-major tables required")
+    out = torch.empty(items.numel(), dtype=torch.float32, device=items.device)
+    native.check(native.lib().fr_score_segments(user_table.data_ptr(), user_table.stride(0), item_table.data_ptr(),
+                                                item_table.stride(0), uid.data_ptr(), offsets.data_ptr(), uid.numel(),
+                                                items.data_ptr(), d, out.data_ptr(), native.stream_of(items)),
+                 "fr_score_segments")
+    return out
+
+
 def rank_metrics(scores: torch.Tensor, lens, npos, k: int = 20):
     """fr_rank_metrics over the per-user candidate scores (device fp32, users' lists back to back,
     positives first): numpy (hits uint32, auc counts int64, flags uint8) per user.  Replaces the

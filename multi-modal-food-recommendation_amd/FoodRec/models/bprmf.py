@@ -33,6 +33,10 @@ class BPRMF(GeneralRecommender):
         mf, emb = ops.bpr_emb_loss(U, I, U, I, batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"])
         return mf, self.reg_weight * emb
 
+    # inference_fast below is the plain gather-dot of forward()'s tables: the trainer may score the
+    # evaluation lists with fr_score_segments instead (no [n, 64] gathers)
+    fused_scores = True
+
     def inference_fast(self, batch_data, user_emb, item_emb):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
 

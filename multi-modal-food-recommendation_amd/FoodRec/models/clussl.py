@@ -127,6 +127,10 @@ class CLUSSL(GeneralRecommender):
             cl = ops.dcor_loss(views, _DCOR_PAIRS)
         return mf_loss, self.loss_cl * cl, self.reg_weight * emb
 
+    # inference_fast below is the plain gather-dot of forward()'s tables: the trainer may score the
+    # evaluation lists with fr_score_segments instead (no [n, 64] gathers)
+    fused_scores = True
+
     def inference_fast(self, batch_data, user_emb, item_emb):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
 

@@ -338,6 +338,10 @@ class HealthRec(GeneralRecommender):
         user_all, item_all, _ = self.forward()
         return self.inference_fast(batch_data, user_all, item_all)
 
+    # inference_fast below is the plain gather-dot of forward()'s tables: the trainer may score the
+    # evaluation lists with fr_score_segments instead (no [n, 64] gathers)
+    fused_scores = True
+
     def inference_fast(self, batch_data, user_emb, item_emb):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
 

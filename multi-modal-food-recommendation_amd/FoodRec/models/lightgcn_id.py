@@ -100,6 +100,10 @@ class LightGCN_ID(GeneralRecommender):
             ex = (adj.rowptr, adj.col, self.n_users)  # user rows of the adjacency hold U + item
         return ops.full_sort_topk(user_all[users], item_all, k, user_ids=users, exclude=ex, held_out=held_out)
 
+    # inference_fast below is the plain gather-dot of forward()'s tables: the trainer may score the
+    # evaluation lists with fr_score_segments instead (no [n, 64] gathers)
+    fused_scores = True
+
     def inference_fast(self, batch_data, user_emb, item_emb):
         return torch.mul(user_emb[batch_data["user_input"]], item_emb[batch_data["item_input"]]).sum(dim=1)
 

@@ -109,7 +109,54 @@ __global__ __launch_bounds__(256) void rank_metrics_kernel(const float* __restri
   }
 }
 
+// Candidate scores of the evaluation, fused: score[e] = <U[uid[s]], I[items[e]]> for e in segment s
+// = [off[s], off[s + 1]) (the graph models' inference_fast, torch.mul(user[u], item[i]).sum(1), over
+// EvalByUserDataloader's back-to-back per-user lists).  One wave per segment: 16-lane groups hold
+// the user row as one float4 per lane (d = 64) and take 4 candidates per round, each group loading
+// its candidate's item row as 16 float4 (256 contiguous bytes) and reducing by DPP; two rounds in
+// flight.  No [n, 64] gathers are materialised (torch: two gathers, a product, a reduction).
+constexpr int SC_WAVES = 4;
+__global__ __launch_bounds__(64 * SC_WAVES) void score_segments_kernel(
+    const float* __restrict__ U, int64_t ldu, const float* __restrict__ I, int64_t ldi, const int64_t* __restrict__ uid,
+    const int64_t* __restrict__ off, int64_t nseg, const int64_t* __restrict__ items, float* __restrict__ out) {
+  const int64_t s = (int64_t)blockIdx.x * SC_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (s >= nseg) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const float4 u4 = *reinterpret_cast<const float4*>(U + uid[s] * ldu + 4 * j);
+  const int64_t e0 = off[s], e1 = off[s + 1];
+  for (int64_t e = e0 + g; e < e1; e += 8) {
+    const int64_t ea = e, eb = e + 4;
+    const bool hb = eb < e1;
+    const int64_t ia = items[ea], ib = hb ? items[eb] : ia;
+    const float4 a4 = *reinterpret_cast<const float4*>(I + ia * ldi + 4 * j);
+    const float4 b4 = *reinterpret_cast<const float4*>(I + ib * ldi + 4 * j);
+    const float sa = group_sum<16>(fmaf(u4.w, a4.w, fmaf(u4.z, a4.z, fmaf(u4.y, a4.y, u4.x * a4.x))));
+    const float sb = group_sum<16>(fmaf(u4.w, b4.w, fmaf(u4.z, b4.z, fmaf(u4.y, b4.y, u4.x * b4.x))));
+    if (j == 0) {
+      out[ea] = sa;
+      if (hb) out[eb] = sb;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int fr_score_segments(const float* d_user, int64_t ld_user, const float* d_item, int64_t ld_item,
+                                 const int64_t* d_uid, const int64_t* d_offsets, int64_t n_seg, const int64_t* d_items,
+                                 int d, float* d_out, void* stream) {
+  FR_REQUIRE(d == 64, "d = 64 (16 lanes x float4 per row)");
+  FR_REQUIRE(n_seg >= 0 && ld_user >= d && ld_item >= d && ld_user % 4 == 0 && ld_item % 4 == 0,
+             "n_seg >= 0, row strides >= d and multiples of 4");
+  if (n_seg == 0) return FR_OK;
+  FR_REQUIRE(d_user && d_item && d_uid && d_offsets && d_items && d_out && fr::aligned16(d_user) &&
+                 fr::aligned16(d_item),
+             "null or unaligned operand");
+  hipLaunchKernelGGL(score_segments_kernel, dim3((unsigned)fr::ceil_div(n_seg, SC_WAVES)), dim3(64 * SC_WAVES), 0,
+                     reinterpret_cast<hipStream_t>(stream), d_user, ld_user, d_item, ld_item, d_uid, d_offsets, n_seg,
+                     d_items, d_out);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
 
 extern "C" int fr_rank_metrics(const float* d_scores, const int64_t* d_offsets, const int32_t* d_npos, int64_t n_users,
                                int k, uint32_t* d_hits, int64_t* d_auc, uint8_t* d_flags, void* stream) {

@@ -110,6 +110,81 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return s;
 }
 
+// ============================ MFMA Gram tiles ==================================================
+// The n x n Gram products of both losses on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32
+// accumulation; the 16-wide k chunks permuted so a lane feeds four MFMAs from one float4 of each
+// operand, as in fr_encoder.hip).  Tiles are row-major in LDS ([64][d + 4]); wave w owns rows
+// [16w, 16w + 16) of the 64-row tile and all four 16-column tiles: acc[c][q] = C[16w + 4h + q][16c + i]
+// for lane (i = lane & 15, h = lane >> 4).  fr_ssl_kernels selects them (default) or the VALU
+// 4x4-per-thread tiles (A/B measurements).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+int g_ssl_mfma = 1;  // host-side kernel choice
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float comp4(const float4& v, int m) {
+  return m == 0 ? v.x : (m == 1 ? v.y : (m == 2 ? v.z : v.w));
+}
+
+// acc[c] = A[rows 16 rw..16 rw + 15] . B[rows 16 (c0 + c)..+15]^T over k < D, c < NC (A, B row-major,
+// ld = D + 4)
+template <int D, int NC = 4>
+__device__ __forceinline__ void gram_mfma(const float* A, const float* B, f32x4 (&acc)[NC], int rw = -1, int c0 = 0) {
+  constexpr int LD = D + 4;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+  if (rw < 0) rw = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < D / 16; ++kc) {
+    const float4 a = *reinterpret_cast<const float4*>(A + (16 * rw + i) * LD + 16 * kc + 4 * h);
+    float4 b[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) b[c] = *reinterpret_cast<const float4*>(B + (16 * (c0 + c) + i) * LD + 16 * kc + 4 * h);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = mfma4(comp4(a, m), comp4(b[c], m), acc[c]);
+  }
+}
+
+// acc[c] += W[rows 16 rw..16 rw + 15][0..64) . X[0..64)[cols 16 (c0 + c)..+15], c < NC (W row-major ld
+// 65, X row-major ld D + 4): the backward's "sum_j w_ij x_j" over one 64-row tile of X
+template <int D, int NC = D / 16>
+__device__ __forceinline__ void wx_mfma(const float* W, const float* X, f32x4 (&acc)[NC], int rw = -1, int c0 = 0) {
+  constexpr int LD = D + 4;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+  if (rw < 0) rw = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int jc = 0; jc < T / 16; ++jc) {
+    float a[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a[m] = W[(16 * rw + i) * 65 + 16 * jc + 4 * h + m];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float b[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) b[m] = X[(16 * jc + 4 * h + m) * LD + 16 * (c0 + c) + i];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[c] = mfma4(a[m], b[m], acc[c]);
+    }
+  }
+}
+
+// squared row norms (fp32, k order) of the 64 rows of a row-major tile (threads 0..63)
+template <int D>
+__device__ __forceinline__ void row_sq_r(const float* X, float* out) {
+  if (threadIdx.x < T) {
+    float s = 0.f;
+    for (int k = 0; k < D; ++k) {
+      const float v = X[threadIdx.x * (D + 4) + k];
+      s = fmaf(v, v, s);
+    }
+    out[threadIdx.x] = s;
+  }
+}
+
 // ============================ distance correlation ============================================
 // workspace layout (doubles unless noted):
 //   S    [nblk][NP]          per-tile pair sums      (nblk = nt*nt)
@@ -245,6 +320,85 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
         for (int y = 0; y < 4; ++y) s += (double)D[a][x][y] * (double)D[b][x][y];
       s = block_sum_d(s, red);
       if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = off ? 2.0 * s : s;
+    }
+}
+
+// MFMA form of dcor_tiles_kernel: the distance tiles' Gram products on the matrix cores (wave w: rows
+// [16w, 16w + 16), lane (i, h): columns 16c + i of rows 16w + 4h + q); row sums over the 16 lanes of a
+// row, column sums of off-diagonal tiles through LDS in row-group order, pair sums as before
+template <int V, int D>
+__global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n, DcorWS ws) {
+  constexpr int LD = D + 4;
+  __shared__ __attribute__((aligned(16))) float At[T * LD];
+  __shared__ __attribute__((aligned(16))) float Bt[T * LD];
+  __shared__ float ra[T], rb[T];
+  __shared__ float colp[16][T];
+  __shared__ double red[4];
+  const int64_t nt = (n + T - 1) / T;
+  const int it = blockIdx.x, jt = blockIdx.y;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  constexpr int NP = V * (V + 1) / 2;
+  if (jt < it) {  // below the diagonal: the transposed tile carries it
+    if (threadIdx.x < NP) ws.S[((int64_t)it * nt + jt) * NP + threadIdx.x] = 0.0;
+    return;
+  }
+  const bool off = jt > it;
+  float Dv[V][4][4];  // [view][column tile c][row q]
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    __syncthreads();
+    load_tile_r(v.x[a], n, D, (int64_t)it * T, At);
+    load_tile_r(v.x[a], n, D, (int64_t)jt * T, Bt);
+    __syncthreads();
+    row_sq_r<D>(At, ra);
+    if (threadIdx.x >= T && threadIdx.x < 2 * T) {
+      float sq = 0.f;
+      for (int k = 0; k < D; ++k) { const float t = Bt[(threadIdx.x - T) * LD + k]; sq = fmaf(t, t, sq); }
+      rb[threadIdx.x - T] = sq;
+    }
+    __syncthreads();
+    f32x4 g[4];
+    gram_mfma<D>(At, Bt, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * w + 4 * h + q;
+      const int64_t gi = (int64_t)it * T + r;
+      float rs = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t gj = (int64_t)jt * T + 16 * c + i;
+        // (r - 2 X X^T) + r^T, exactly the reference's evaluation order
+        const float qv = (ra[r] - 2.f * g[c][q]) + rb[16 * c + i];
+        Dv[a][c][q] = (gi < n && gj < n) ? sqrtf(fmaxf(qv, 0.f) + 1e-8f) : 0.f;
+        rs += Dv[a][c][q];
+      }
+      rs = group_sum<16>(rs);
+      if (i == 0 && gi < n) ws.row[((int64_t)a * nt + jt) * n + gi] = rs;
+    }
+    if (off) {  // column sums = the jt rows' sums over column tile it (16 row groups, in order)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) colp[4 * w + h][16 * c + i] = ((Dv[a][c][0] + Dv[a][c][1]) + Dv[a][c][2]) + Dv[a][c][3];
+      __syncthreads();
+      if (threadIdx.x < T) {
+        float cs = 0.f;
+        for (int k = 0; k < 16; ++k) cs += colp[k][threadIdx.x];
+        const int64_t gj = (int64_t)jt * T + threadIdx.x;
+        if (gj < n) ws.row[((int64_t)a * nt + it) * n + gj] = cs;
+      }
+    }
+  }
+  const int64_t blk = (int64_t)it * nt + jt;
+#pragma unroll
+  for (int a = 0; a < V; ++a)
+#pragma unroll
+    for (int b = a; b < V; ++b) {
+      double sum = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum += (double)Dv[a][c][q] * (double)Dv[b][c][q];
+      sum = block_sum_d(sum, red);
+      if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = off ? 2.0 * sum : sum;
     }
 }
 
@@ -447,6 +601,132 @@ __global__ __launch_bounds__(256) void dcor_bwd_tiles_kernel(Views v, int64_t n,
 #pragma unroll
       for (int k = 0; k < kper; ++k) P[k] = acc[a][k];
       if (aslot == 0) ws.rowm[((int64_t)js * V + a) * n + gi] = rowm[a];
+    }
+  }
+}
+
+// MFMA form of dcor_bwd_tiles_kernel: per j-tile the V distance tiles on the matrix cores, the
+// centred tiles and m_ij = K_a(i,j) gate(q) / (2 D) on the VALU, m staged in LDS, then
+// P_a += m X_a[j-tile] on the matrix cores (the view's j-tile reloaded row-major) and rowm_a from the
+// fragments.  8 waves: wave w owns row block rw = w & 3 and the column half ch = w >> 2 (two 16-column
+// tiles) of every 64 x 64 tile, so each lane holds 8 elements per view (two waves per SIMD).
+// LDS: V i-tiles + one j-tile + m (D = 64, V <= 4).
+constexpr int DB_NT = 512;
+template <int V, int D>
+__global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n, DcorWS ws) {
+  constexpr int LD = D + 4;
+  constexpr int NC = D / 32;  // output column tiles per wave
+  __shared__ __attribute__((aligned(16))) float Ai[V][T * LD];
+  __shared__ __attribute__((aligned(16))) float Bt[T * LD];
+  __shared__ float Ms[T * 65];
+  __shared__ float ra[V][T], rb[T];
+  __shared__ double mi[V][T], mj[V][T];
+  __shared__ float rowp[2][V][T];
+  const int64_t nt = (n + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  const int rw = w & 3, ch = w >> 2;
+  constexpr int NP = V * (V + 1) / 2;
+  double coef[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) coef[k] = ws.coef[k];
+  for (int a = 0; a < V; ++a) load_tile_r(v.x[a], n, D, (int64_t)it * T, Ai[a]);
+  if (threadIdx.x < T) {
+    const int64_t gi = (int64_t)it * T + threadIdx.x;
+    for (int a = 0; a < V; ++a) mi[a][threadIdx.x] = gi < n ? ws.mean[(int64_t)a * n + gi] : 0.0;
+  }
+  __syncthreads();
+  for (int a = 0; a < V; ++a) row_sq_r<D>(Ai[a], ra[a]);
+  f32x4 acc[V][NC];
+  float rowm[V][4];
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rowm[a][q] = 0.f;
+  }
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    float Dd[V][2][4], Dc[V][2][4];  // [view][column tile 2 ch + c][row q]
+    if (threadIdx.x < T) {
+      const int64_t gj = jt * T + threadIdx.x;
+      for (int a = 0; a < V; ++a) mj[a][threadIdx.x] = gj < n ? ws.mean[(int64_t)a * n + gj] : 0.0;
+    }
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      __syncthreads();
+      load_tile_r(v.x[a], n, D, jt * T, Bt);
+      __syncthreads();
+      if (threadIdx.x < T) {
+        float sq = 0.f;
+        for (int k = 0; k < D; ++k) { const float t = Bt[threadIdx.x * LD + k]; sq = fmaf(t, t, sq); }
+        rb[threadIdx.x] = sq;
+      }
+      __syncthreads();
+      f32x4 g[2];
+      gram_mfma<D, 2>(Ai[a], Bt, g, rw, 2 * ch);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rw + 4 * h + q;
+        const int64_t gi = (int64_t)it * T + r;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int col = 16 * (2 * ch + c) + i;
+          const int64_t gj = jt * T + col;
+          const float qv = (ra[a][r] - 2.f * g[c][q]) + rb[col];
+          const float dd = sqrtf(fmaxf(qv, 0.f) + 1e-8f);
+          const float gt = qv > 0.f ? 1.f : (qv == 0.f ? 0.5f : 0.f);
+          const bool ok = gi < n && gj < n;
+          Dc[a][c][q] = ok ? (float)((double)dd - mi[a][r] - mj[a][col] + ws.Abar[a]) : 0.f;
+          Dd[a][c][q] = (ok && gi != gj) ? gt / (2.f * dd) : 0.f;  // gate(q) / (2 D), 0 off the tile / diagonal
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      if (!v.dx[a]) continue;
+      __syncthreads();  // every wave is done with Ms and Bt
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rw + 4 * h + q;
+        float rs = 0.f;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          double K = 2.0 * coef[pair_index(a, a, V)] * Dc[a][c][q];
+#pragma unroll
+          for (int b = 0; b < V; ++b)
+            if (b != a) K += coef[pair_index(a, b, V)] * Dc[b][c][q];
+          const float mv = (float)(K * (double)Dd[a][c][q]);
+          Ms[r * 65 + 16 * (2 * ch + c) + i] = mv;
+          rs += mv;
+        }
+        rowm[a][q] += group_sum<16>(rs);
+      }
+      load_tile_r(v.x[a], n, D, jt * T, Bt);
+      __syncthreads();
+      wx_mfma<D, NC>(Ms, Bt, acc[a], rw, NC * ch);
+    }
+  }
+  // row sums: the two column halves in order (ch 0, then 1)
+#pragma unroll
+  for (int a = 0; a < V; ++a)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i == 0) rowp[ch][a][16 * rw + 4 * h + q] = rowm[a][q];
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    if (!v.dx[a]) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * rw + 4 * h + q;
+      const int64_t gi = (int64_t)it * T + r;
+      if (gi < n) {
+        float* P = ws.P + (((int64_t)js * V + a) * n + gi) * D;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) P[16 * (NC * ch + c) + i] = acc[a][c][q];
+        if (i == 0 && ch == 0) ws.rowm[((int64_t)js * V + a) * n + gi] = rowp[0][a][r] + rowp[1][a][r];
+      }
     }
   }
 }
@@ -731,6 +1011,116 @@ __global__ __launch_bounds__(256) void nce_bwd_tiles_kernel(int64_t b, float inv
   }
 }
 
+// MFMA form of nce_lse_tiles_kernel: the logits tile on the matrix cores, each lane keeping the online
+// (max, sum) of its 4 rows over its columns; the 16 lanes of a row merged in a fixed order at the end
+template <int D>
+__global__ __launch_bounds__(256) void nce_lse_mfma_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
+  __shared__ __attribute__((aligned(16))) float At[T * (D + 4)];
+  __shared__ __attribute__((aligned(16))) float Bt[T * (D + 4)];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  nce_tile_r(ws, pt, p, b, D, (int64_t)it * T, At);
+  float mx[4], sm[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { mx[q] = -INFINITY; sm[q] = 0.f; }
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    nce_tile_r(ws, pt, p, b, D, jt * T, Bt);
+    __syncthreads();
+    f32x4 g[4];
+    gram_mfma<D>(At, Bt, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t gi = (int64_t)it * T + 16 * w + 4 * h + q;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t gj = jt * T + 16 * c + i;
+        if (gj >= m || gi == gj) continue;
+        const float l = g[c][q] * inv_tau;
+        if (l > mx[q]) { sm[q] = sm[q] * expf(mx[q] - l) + 1.f; mx[q] = l; }
+        else sm[q] += expf(l - mx[q]);
+      }
+    }
+  }
+  // merge the 16 lanes of each row: lane i takes its neighbours' (M, S) at distance 1, 2, 4, 8
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float M = mx[q], S = sm[q];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float Mo = __shfl_xor(M, o, 16), So = __shfl_xor(S, o, 16);
+      const float Mn = fmaxf(M, Mo);
+      S = (S == 0.f ? 0.f : S * expf(M - Mn)) + (So == 0.f ? 0.f : So * expf(Mo - Mn));
+      M = Mn;
+    }
+    const int64_t gi = (int64_t)it * T + 16 * w + 4 * h + q;
+    if (i == 0 && gi < m) ws.part[((int64_t)p * NCE_JS + js) * m + gi] = make_float2(M, S);
+  }
+}
+
+// MFMA form of nce_bwd_tiles_kernel: the logits tile and W = dl + dl^T on the matrix cores / VALU,
+// W staged in LDS, then sum_j W_ij Hn_j on the matrix cores into per-lane accumulators
+template <int D>
+__global__ __launch_bounds__(256) void nce_bwd_mfma_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
+  constexpr int LD = D + 4;
+  __shared__ __attribute__((aligned(16))) float At[T * LD];
+  __shared__ __attribute__((aligned(16))) float Bt[T * LD];
+  __shared__ float Ws[T * 65];
+  __shared__ float lse_i[T], lse_j[T];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
+  const float* lse = ws.lse + (int64_t)p * m;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  nce_tile_r(ws, pt, p, b, D, (int64_t)it * T, At);
+  if (threadIdx.x < T) {
+    const int64_t gi = (int64_t)it * T + threadIdx.x;
+    lse_i[threadIdx.x] = gi < m ? lse[gi] : 0.f;
+  }
+  f32x4 acc[D / 16];
+#pragma unroll
+  for (int c = 0; c < D / 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    nce_tile_r(ws, pt, p, b, D, jt * T, Bt);
+    if (threadIdx.x < T) {
+      const int64_t gj = jt * T + threadIdx.x;
+      lse_j[threadIdx.x] = gj < m ? lse[gj] : 0.f;
+    }
+    __syncthreads();
+    f32x4 g[4];
+    gram_mfma<D>(At, Bt, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * w + 4 * h + q;
+      const int64_t gi = (int64_t)it * T + r;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t gj = jt * T + 16 * c + i;
+        float wv = 0.f;
+        if (gi < m && gj < m && gi != gj) {
+          const float l = g[c][q] * inv_tau;
+          const float pij = expf(l - lse_i[r]) - (gj == nce_partner(gi, b) ? 1.f : 0.f);
+          const float pji = expf(l - lse_j[16 * c + i]) - (gi == nce_partner(gj, b) ? 1.f : 0.f);
+          wv = pij + pji;
+        }
+        Ws[r * 65 + 16 * c + i] = wv;
+      }
+    }
+    __syncthreads();
+    wx_mfma<D>(Ws, Bt, acc);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t gi = (int64_t)it * T + 16 * w + 4 * h + q;
+    if (gi < m) {
+      float* P = ws.P + (((int64_t)p * NCE_JS + js) * m + gi) * D;
+#pragma unroll
+      for (int c = 0; c < D / 16; ++c) P[16 * c + i] = acc[c][q];
+    }
+  }
+}
+
 // dview_v[r] = normalize_backward(gh) with gh = scale * (sum over the pairs holding view v, at the
 // row's position in that pair, of the split partials); written (views that no pair holds: zeros)
 __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, int64_t b, int d, float inv_tau,
@@ -771,6 +1161,12 @@ __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, 
 }  // namespace
 
 // ------------------------------------------------------------------------------------------ ABI
+extern "C" int fr_ssl_kernels(int mfma) {
+  const int prev = g_ssl_mfma;
+  if (mfma >= 0) g_ssl_mfma = mfma ? 1 : 0;
+  return prev;
+}
+
 extern "C" int64_t fr_dcor_workspace(int64_t n, int n_views) {
   if (n <= 0 || n_views <= 0 || n_views > MAXV) return 0;
   return dcor_ws_bytes(n, n_views);
@@ -806,7 +1202,14 @@ extern "C" int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, 
   const int64_t nt = fr::ceil_div(n, T);
   const size_t lds = (size_t)(2 * d * PADT + 2 * T) * 4 + 64;
   const dim3 grid((unsigned)nt, (unsigned)nt);
-  switch (n_views) {
+  if (g_ssl_mfma && d == 64) {
+    switch (n_views) {
+      case 1: hipLaunchKernelGGL((dcor_tiles_mfma_kernel<1, 64>), grid, dim3(256), 0, s, v, n, w); break;
+      case 2: hipLaunchKernelGGL((dcor_tiles_mfma_kernel<2, 64>), grid, dim3(256), 0, s, v, n, w); break;
+      case 3: hipLaunchKernelGGL((dcor_tiles_mfma_kernel<3, 64>), grid, dim3(256), 0, s, v, n, w); break;
+      default: hipLaunchKernelGGL((dcor_tiles_mfma_kernel<4, 64>), grid, dim3(256), 0, s, v, n, w); break;
+    }
+  } else switch (n_views) {
     case 1: hipLaunchKernelGGL(dcor_tiles_kernel<1>, grid, dim3(256), lds, s, v, n, d, w); break;
     case 2: hipLaunchKernelGGL(dcor_tiles_kernel<2>, grid, dim3(256), lds, s, v, n, d, w); break;
     case 3: hipLaunchKernelGGL(dcor_tiles_kernel<3>, grid, dim3(256), lds, s, v, n, d, w); break;
@@ -838,6 +1241,15 @@ extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, 
   const size_t lds = (size_t)(n_views * d * PADT + d * PADT + T * (d + 4) + T * 65 + MAXV * T + T) * 4;
   FR_REQUIRE(lds <= 160 * 1024, "LDS budget exceeded (reduce views or d)");
   const dim3 grid((unsigned)nt, (unsigned)js);
+  if (g_ssl_mfma && d == 64) {
+    switch (n_views) {
+      case 1: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<1, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      case 2: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<2, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      case 3: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<3, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      default: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<4, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+    }
+    FR_LAUNCH_CHECK();
+  } else {
 #define FR_DCOR_BWD(VV, KK) \
   hipLaunchKernelGGL((dcor_bwd_tiles_kernel<VV, KK>), grid, dim3(256), lds, s, v, n, w)
 #define FR_DCOR_BWD_V(KK)                          \
@@ -856,6 +1268,7 @@ extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, 
 #undef FR_DCOR_BWD_V
 #undef FR_DCOR_BWD
   FR_LAUNCH_CHECK();
+  }
   const int64_t total = (int64_t)n_views * n * d;
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(total, 256), 4096);
   hipLaunchKernelGGL(dcor_bwd_finalize_kernel, dim3(blocks), dim3(256), 0, s, v, n_views, n, d, js,
@@ -905,8 +1318,17 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
   const int64_t nt = fr::ceil_div(m, T);
   const int js = (int)std::min<int64_t>(NCE_JS, nt);
   const size_t lds = (size_t)(2 * d * PADT) * 4;
-  hipLaunchKernelGGL(nce_lse_tiles_kernel, dim3((unsigned)nt, (unsigned)js, (unsigned)n_pairs), dim3(256), lds, s, b,
-                     d, inv_tau, pt, w);
+  const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
+  if (g_ssl_mfma) {
+    switch (d) {
+      case 16: hipLaunchKernelGGL(nce_lse_mfma_kernel<16>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 32: hipLaunchKernelGGL(nce_lse_mfma_kernel<32>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 64: hipLaunchKernelGGL(nce_lse_mfma_kernel<64>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      default: hipLaunchKernelGGL(nce_lse_mfma_kernel<128>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+    }
+  } else {
+    hipLaunchKernelGGL(nce_lse_tiles_kernel, grid, dim3(256), lds, s, b, d, inv_tau, pt, w);
+  }
   FR_LAUNCH_CHECK();
   hipLaunchKernelGGL(nce_finalize_kernel, dim3((unsigned)nce_nparts(m), (unsigned)n_pairs), dim3(256), 0, s, b, d,
                      inv_tau, js, pt, w);
@@ -946,7 +1368,14 @@ extern "C" int fr_infonce_multi_bwd(const float* const* d_views, int n_views, in
   const int js = (int)std::min<int64_t>(NCE_JS, nt);
   const size_t lds = (size_t)(2 * d * PADT + T * (d + 4) + T * 65) * 4;
   const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
-  switch (d) {
+  if (g_ssl_mfma) {
+    switch (d) {
+      case 16: hipLaunchKernelGGL(nce_bwd_mfma_kernel<16>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 32: hipLaunchKernelGGL(nce_bwd_mfma_kernel<32>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 64: hipLaunchKernelGGL(nce_bwd_mfma_kernel<64>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      default: hipLaunchKernelGGL(nce_bwd_mfma_kernel<128>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+    }
+  } else switch (d) {
     case 16: hipLaunchKernelGGL(nce_bwd_tiles_kernel<4>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
     case 32: hipLaunchKernelGGL(nce_bwd_tiles_kernel<8>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;
     case 64: hipLaunchKernelGGL(nce_bwd_tiles_kernel<16>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;

@@ -316,8 +316,18 @@ def test_bpr_shared_tables(cuda):
     np.testing.assert_allclose(Id.grad.cpu().numpy(), I.grad.numpy(), rtol=1e-4, atol=1e-6)
 
 
+@pytest.fixture(params=["mfma", "valu"])
+def ssl_kernels(request, cuda):
+    """Both Gram-tile forms of the SSL kernels (fr_ssl_kernels): the MFMA default and the VALU tiles."""
+    from FoodRec.engine import native
+    lib = native.lib()
+    prev = lib.fr_ssl_kernels(1 if request.param == "mfma" else 0)
+    yield request.param
+    lib.fr_ssl_kernels(prev)
+
+
 @pytest.mark.parametrize("n", [1024, 200])
-def test_dcor_three_views(cuda, n):
+def test_dcor_three_views(cuda, n, ssl_kernels):
     from FoodRec.engine import ops
     d = 64
     g = torch.Generator().manual_seed(n)
@@ -344,7 +354,7 @@ def test_dcor_three_views(cuda, n):
 
 
 @pytest.mark.parametrize("b", [512, 37])
-def test_infonce(cuda, b):
+def test_infonce(cuda, b, ssl_kernels):
     from FoodRec.engine import ops
     d = 64
     g = torch.Generator().manual_seed(b)
@@ -360,7 +370,7 @@ def test_infonce(cuda, b):
 
 
 @pytest.mark.parametrize("b", [1024, 512, 37])
-def test_infonce_pairs(cuda, b):
+def test_infonce_pairs(cuda, b, ssl_kernels):
     """ops.infonce_pairs (all pairs in the same launches, views normalised once, no concatenation)
     against the float64 oracle sum of CL_loss(cat([views[a], views[b]])) over CLUSSL's three pairs:
     value rel 1e-5, gradients rel 1e-4; the value is bit-identical to summing the single-pair op in

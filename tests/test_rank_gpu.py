@@ -105,3 +105,50 @@ def test_rank_metrics_allrecipes_scale_timing(cuda):
     assert np.array_equal(res[:sample][ok], ref[ok])
     print(f"\nrank {U} users: device {t_dev * 1e3:.1f} ms (incl. host metric assembly), "
           f"reference-style host loop ~{t_host:.1f} s (from {sample} users)")
+
+
+@pytest.mark.parametrize("U,I,stride_pad", [(68_768, 45_630, 0), (300, 50, 8), (1, 7, 0)])
+def test_score_segments_matches_gather_dot(cuda, U, I, stride_pad):
+    """fr_score_segments (the evaluation's fused gather-dot, one wave per user segment) vs torch's
+    mul(user[u], item[i]).sum(1) (the models' inference_fast) on the same fp32 tables: rel 1e-6 of
+    the score scale (fp32 summation order only), including row strides wider than 64 (table views)."""
+    from FoodRec.engine import ops
+    g = torch.Generator().manual_seed(U + I)
+    Ut = torch.randn(U, 64 + stride_pad, generator=g).to(cuda)[:, :64]
+    It = torch.randn(I, 64 + stride_pad, generator=g).to(cuda)[:, :64]
+    n_seg = min(U, 4096)
+    lens = torch.randint(1, 600, (n_seg,), generator=g)
+    off = torch.zeros(n_seg + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=off[1:])
+    uid = torch.randint(0, U, (n_seg,), generator=g)
+    items = torch.randint(0, I, (int(off[-1]),), generator=g)
+    got = ops.score_segments(Ut, It, uid.to(cuda), off.to(cuda), items.to(cuda))
+    users = torch.repeat_interleave(uid, lens).to(cuda)
+    ref = torch.mul(Ut[users], It[items.to(cuda)]).sum(1)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-6 * float(ref.abs().max()) + 1e-7)
+
+
+def test_fused_scoring_evaluation_matches_torch_path(cuda):
+    """Trainer._valid_by_user_epoch with fused scoring (cached device lists + fr_score_segments) vs the
+    same trainer with the model's torch inference_fast path, on the tiny HealthRec fixture: equal
+    metrics (the scores differ only in fp32 summation order, far below any ranking gap here)."""
+    from helpers import tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    cfg = tiny_config("CIKM_Model", True, cuda_graph=False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
+    tr = Trainer(cfg, model)
+    model.eval()
+    assert tr._fused_scoring()
+    fused = [tr._valid_by_user_epoch(is_test=t)[1] for t in (False, True, True)]
+    type(model).fused_scores = False
+    try:
+        plain = [tr._valid_by_user_epoch(is_test=t)[1] for t in (False, True)]
+    finally:
+        type(model).fused_scores = True
+    for a, b in zip(fused, plain + [plain[1]]):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert abs(a[k] - b[k]) <= 1e-9, (k, a[k], b[k])
