@@ -166,6 +166,14 @@ int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, int d,
                 float* const* d_dviews,
                 void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* CLUSSL's view sum and SSL gathers (PRICAI_ModelX.forward + calculate_loss,
+ * models/pricai_modelx.py:227-263: item_emb = ingre + image + text, then each view at the batch
+ * items): d_total = ((views[0] + views[1]) + ...) [n, d] in that order, d_gathered[k] [m, d] =
+ * views[k][ids] (ids outside [0, n) gather zeros).  1 <= n_views <= 4, d % 4 == 0, 16-byte aligned. */
+int fr_views_sum_gather(const float* const* d_views, int n_views, int64_t n, int d,
+                        const int64_t* d_ids, int64_t m, float* d_total, float* const* d_gathered,
+                        void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fused InfoNCE / NT-Xent (PRICAI_ModelX.CL_loss, hidden_norm=True): H is [2b, d];
  * out[0] = (CE([h1 h2^T | h1 h1^T - 1e9 I]/tau) + CE([h2 h1^T | h2 h2^T - 1e9 I]/tau)) / b.

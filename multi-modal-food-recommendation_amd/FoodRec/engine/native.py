@@ -123,6 +123,8 @@ _SIGS = {
                               c_void_p, c_int64, c_void_p]),
     "fr_ssl_kernels": (c_int, [c_int]),
     "fr_dcor_workspace": (c_int64, [c_int64, c_int]),
+    "fr_views_sum_gather": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, c_void_p, c_int64, c_void_p,
+                                    POINTER(c_void_p), c_void_p]),
     "fr_dcor_fwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
                             c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_dcor_bwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,

@@ -2143,10 +2143,18 @@ class _ViewsSumGather(torch.autograd.Function):
     def forward(ctx, ids, *views):
         ctx.save_for_backward(ids)
         ctx.V, ctx.shape = len(views), views[0].shape
-        total = torch.add(views[0], views[1]) if len(views) > 1 else views[0].clone()
-        for v in views[2:]:
-            total.add_(v)
-        return (total, *[v.index_select(0, ids) for v in views])
+        views = [_rowmajor(v) for v in views]
+        native.require_device(ids, *views)
+        n, d = views[0].shape
+        m = ids.numel()
+        total = torch.empty_like(views[0])
+        gathered = [torch.empty(m, d, dtype=views[0].dtype, device=ids.device) for _ in views]
+        V = len(views)
+        # the sum (torch's add order) and the gathers in one launch (fr_views_sum_gather)
+        native.check(native.lib().fr_views_sum_gather(
+            (ctypes.c_void_p * V)(*[v.data_ptr() for v in views]), V, n, d, ids.data_ptr(), m, total.data_ptr(),
+            (ctypes.c_void_p * V)(*[g.data_ptr() for g in gathered]), native.stream_of(total)), "fr_views_sum_gather")
+        return (total, *gathered)
 
     @staticmethod
     def backward(ctx, g_sum, *g_rows):
@@ -2166,7 +2174,7 @@ def views_sum_gather(views, ids):
     mode keeps the separate sum and deterministic row gathers."""
     ids = ids.reshape(-1).to(torch.int64)
     if _DETERMINISTIC or not all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in views) \
-            or len({tuple(v.shape) for v in views}) != 1:
+            or len({tuple(v.shape) for v in views}) != 1 or len(views) > 4 or views[0].shape[1] % 4:
         total = views[0]
         for v in views[1:]:
             total = total + v

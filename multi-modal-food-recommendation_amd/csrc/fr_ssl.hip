@@ -1413,3 +1413,65 @@ extern "C" int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, flo
   const int32_t pair[2] = {0, 1};
   return fr_infonce_multi_bwd(views, 2, b, d, pair, 1, tau, g, d_gscale, dviews, d_workspace, workspace_bytes, stream);
 }
+
+// ------------------------------------------------------------------------------------------------
+// CLUSSL's view sum and SSL gathers in one launch (pricai_modelx.py:227-263: item_emb = ingre +
+// image + text, and the three views at the batch items): total = ((v0 + v1) + v2) in torch's add
+// order (bit-identical), g_k[j] = v_k[ids[j]].  HBM stream: V reads + 1 write of the tables plus the
+// gathered rows; one float4 per thread and iteration, grid-strided.  Ids outside [0, n) gather zeros.
+// ------------------------------------------------------------------------------------------------
+namespace {
+struct ViewsSG {
+  const float4* v[4];
+  float4* g[4];
+};
+
+__global__ __launch_bounds__(256) void views_sum_gather_kernel(ViewsSG a, int V, int64_t n, int d4,
+                                                               const int64_t* __restrict__ ids, int64_t m,
+                                                               float4* __restrict__ total) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = n * d4;
+  for (int64_t i = t0; i < n4; i += stride) {
+    float4 s = a.v[0][i];
+    for (int k = 1; k < V; ++k) {
+      const float4 x = a.v[k][i];
+      s.x += x.x;
+      s.y += x.y;
+      s.z += x.z;
+      s.w += x.w;
+    }
+    total[i] = s;
+  }
+  const int64_t m4 = m * d4;
+  for (int64_t i = t0; i < m4 * V; i += stride) {
+    const int k = (int)(i / m4);
+    const int64_t j = i - (int64_t)k * m4, row = j / d4, c = j - row * d4;
+    const int64_t r = ids[row];
+    a.g[k][j] = (r >= 0 && r < n) ? a.v[k][r * d4 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+}  // namespace
+
+extern "C" int fr_views_sum_gather(const float* const* d_views, int n_views, int64_t n, int d,
+                                   const int64_t* d_ids, int64_t m, float* d_total, float* const* d_gathered,
+                                   void* stream) {
+  FR_REQUIRE(d_views && d_gathered && d_total && n_views >= 1 && n_views <= 4 && n >= 1 && d >= 4 && d % 4 == 0 &&
+                 m >= 0 && (m == 0 || d_ids) && fr::aligned16(d_total),
+             "views_sum_gather: bad arguments");
+  ViewsSG a{};
+  for (int k = 0; k < n_views; ++k) {
+    FR_REQUIRE(d_views[k] && fr::aligned16(d_views[k]) && (m == 0 || (d_gathered[k] && fr::aligned16(d_gathered[k]))),
+               "views_sum_gather: view / gathered table null or unaligned");
+    a.v[k] = reinterpret_cast<const float4*>(d_views[k]);
+    a.g[k] = m ? reinterpret_cast<float4*>(d_gathered[k]) : nullptr;
+  }
+  const int d4 = d / 4;
+  const int64_t work = n * d4;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(work, 256), (int64_t)fr::kNumCU * 16));
+  hipLaunchKernelGGL(views_sum_gather_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a, n_views, n, d4, d_ids, m,
+                     reinterpret_cast<float4*>(d_total));
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}

@@ -171,6 +171,42 @@ def test_propagate_lo_matches_full(cuda, L):
     assert torch.all(gb_hi[NS:] == 0)
 
 
+@pytest.mark.parametrize("V", [1, 3, 4])
+def test_views_sum_gather(cuda, V):
+    """ops.views_sum_gather (fr_views_sum_gather: CLUSSL's view sum in torch's add order and the
+    views at the batch items, one launch) vs torch: bit-identical sum and gathers (duplicate ids
+    included); backward vs autograd through the torch form."""
+    from FoodRec.engine import ops
+    g = torch.Generator().manual_seed(V)
+    n, m = 29943, 1024
+    views0 = [torch.randn(n, 64, generator=g).to(cuda) for _ in range(V)]
+    ids = torch.randint(0, n, (m,), generator=g).to(cuda)
+    ids[:8] = ids[8]  # duplicates
+    res = []
+    for fused in (False, True):
+        views = [v.clone().requires_grad_(True) for v in views0]
+        if fused:
+            total, gathered = ops.views_sum_gather(views, ids)
+        else:
+            total = views[0] if V == 1 else torch.add(views[0], views[1])
+            for v in views[2:]:
+                total = total + v
+            gathered = [v.index_select(0, ids) for v in views]
+        gs = torch.randn(n, 64, generator=g).to(cuda)
+        loss = (total * gs).sum() + sum((x * (k + 1)).sum() for k, x in enumerate(gathered))
+        loss.backward()
+        res.append((total.detach(), [x.detach() for x in gathered], [v.grad for v in views]))
+        g = torch.Generator().manual_seed(V)  # same upstream for both runs
+        [torch.randn(n, 64, generator=g) for _ in range(V)]
+        torch.randint(0, n, (m,), generator=g)
+    (ta, ga, da), (tb, gb, db) = res
+    assert torch.equal(ta, tb)
+    for a, b in zip(ga, gb):
+        assert torch.equal(a, b)
+    for a, b in zip(da, db):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("L", [1, 2])
 def test_propagate_lo_views_matches_per_view(cuda, L):
     """ops.propagate_lo_views (CLUSSL's three views as one node, the item-row gradients summed in the
