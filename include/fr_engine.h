@@ -463,10 +463,12 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * dropout2.  Masks come from a counter-based hash of (seed, *d_counter, site, element); the
  * forward stores the counter value it used in *d_seed_out and the backward reads it back (the
  * caller advances the counter; graph replays draw fresh masks).
- * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), y2 [T,64] (LN2 input), st1/st2
- * [T,2] (mean, rstd), T = n_seq * L: 452 floats per token.  The FF activation is not saved: the
- * backward recomputes it (x1 = LN1(y1), one more GEMM, the same GELU / dropout epilogue, bit-identical
- * to the forward's).
+ * Forward saves qkv [T,192], ctx [T,64], y1 [T,64] (LN1 input), fact [T,256] (dropout(act(FF1))),
+ * y2 [T,64] (LN2 input), st1/st2 [T,2] (mean, rstd), T = n_seq * L, and dact (keep/(1-p) *
+ * act'(FF1)) as fr_encoder_dact_numel(n_seq, L) floats in the kernels' MFMA fragment layout
+ * (opaque to the caller; only fr_encoder_bwd reads it).  (Recomputing the FF activation in the
+ * backward instead -- one more GEMM and the GELU / GELU' epilogue -- measured 175k vs 147k cycles
+ * per backward launch: the VALU epilogue, not the 42 MB of saved activations, is the cost.)
  * Backward writes dx and its per-workgroup weight-gradient partials d_partials
  * [fr_encoder_partials(n_seq, L)]; with d_grad non-NULL it also sums them in workgroup order
  * (deterministic) into the flat parameter gradient d_grad [fr_encoder_grad_numel()] (the 12
@@ -477,19 +479,20 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_encoder_partials(int64_t n_seq, int L);
 int64_t fr_encoder_grad_numel(void);
+int64_t fr_encoder_dact_numel(int64_t n_seq, int L);
 /* Diagnostics: enable (1) / disable (0) / keep (-1) per-phase s_memtime stamps of workgroup 0 and
  * copy the stamp table (uint64 [2][32]: forward, backward; shader clock) to host_marks if non-NULL. */
 int fr_encoder_profile(int enable, uint64_t* host_marks);
 int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_seq, int L, const float* const* d_params,
                    const float* eps, const float* drop, uint64_t seed, int gelu, const int64_t* d_counter,
-                   int64_t* d_seed_out, float* d_out, float* d_qkv, float* d_ctx, float* d_y1, float* d_y2,
-                   float* d_st1, float* d_st2, void* stream);
+                   int64_t* d_seed_out, float* d_out, float* d_qkv, float* d_ctx, float* d_y1, float* d_fact,
+                   float* d_dact, float* d_y2, float* d_st1, float* d_st2, void* stream);
 int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, int64_t n_seq, int L,
                    const float* const* d_params, const float* eps, const float* drop, uint64_t seed, int gelu,
                    const int64_t* d_seed_in, const float* d_qkv, const float* d_ctx, const float* d_y1,
-                   const float* d_y2, const float* d_st1, const float* d_st2, float* d_dx, float* d_grad,
-                   float* d_partials, int64_t partial_floats, const float* d_prev_partials, float* d_prev_grad,
-                   void* stream);
+                   const float* d_fact, const float* d_dact, const float* d_y2, const float* d_st1,
+                   const float* d_st2, float* d_dx, float* d_grad, float* d_partials, int64_t partial_floats,
+                   const float* d_prev_partials, float* d_prev_grad, void* stream);
 int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_grad, void* stream);
 
 /* ------------------------------------------------------------------------------------------

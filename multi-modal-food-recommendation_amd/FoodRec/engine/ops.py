@@ -1622,13 +1622,19 @@ def encoder_flops(n_seq: int, L: int, backward: bool) -> int:
 
 def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
     """Algorithmic HBM bytes of one fused encoder-layer launch: the saved activations (qkv 192 +
-    ctx 64 + y1 64 + y2 64 + 4 stats floats per token: the FF activation is recomputed, not saved)
-    written by the forward and read back by the backward, plus x / out (forward) or dout / x / dx
-    (backward); weights are L2-resident.  The backward's weight-gradient partials are not counted
-    (an implementation choice for the deterministic order, not algorithmic traffic)."""
+    ctx 64 + y1 64 + fact 256 + dact 256 + y2 64 + 4 stats floats per token) written by the forward
+    and read back by the backward, plus x / out (forward) or dout / x / dx (backward); weights are
+    L2-resident.  The backward's weight-gradient partials are not counted (an implementation choice
+    for the deterministic order, not algorithmic traffic)."""
     T = n_seq * L
-    saved = 4 * T * (192 + 64 + 64 + 64 + 4)
+    saved = 4 * T * (192 + 64 + 64 + 256 + 256 + 64 + 4)
     return (saved + 4 * T * 64 * 3) if backward else (saved + 4 * T * 64 * 2)
+
+
+# FR_ENCODER_FOLD=1: layer k+1's ordered reduction folded into layer k's backward launch (measured 5-10 us
+# slower per step than a separate reduction: the 200 KB per workgroup of partial reads at the launch
+# start are not overlapped); default: every layer reduces its own partials
+ENCODER_FOLD = os.environ.get("FR_ENCODER_FOLD", "0") == "1"
 
 
 class _EncoderStack(torch.autograd.Function):
@@ -1653,6 +1659,8 @@ class _EncoderStack(torch.autograd.Function):
             qkv = torch.empty(T, 192, **f32)
             cx = torch.empty(T, 64, **f32)
             y1 = torch.empty(T, 64, **f32)
+            fact = torch.empty(T, 256, **f32)
+            dact = torch.empty(int(lib.fr_encoder_dact_numel(NS, L)), **f32)  # per-workgroup fragment layout
             y2 = torch.empty(T, 64, **f32)
             st1 = torch.empty(T, 2, **f32)
             st2 = torch.empty(T, 2, **f32)
@@ -1663,10 +1671,10 @@ class _EncoderStack(torch.autograd.Function):
                 native.check(lib.fr_encoder_fwd(
                     h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
                     cfg.counter.data_ptr(), seed_used.data_ptr(), out.data_ptr(), qkv.data_ptr(), cx.data_ptr(),
-                    y1.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), native.stream_of(h)),
-                    "fr_encoder_fwd")
+                    y1.data_ptr(), fact.data_ptr(), dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(),
+                    native.stream_of(h)), "fr_encoder_fwd")
             defer_increment(cfg.counter)  # advanced by the step's fr_step_book (or before its next read)
-            saved.append((h, qkv, cx, y1, y2, st1, st2, seed_used))
+            saved.append((h, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used))
             h = out
         ctx.cfgs, ctx.saved, ctx.mask = cfgs, saved, mask
         ctx.save_for_backward(*flat)
@@ -1685,7 +1693,7 @@ class _EncoderStack(torch.autograd.Function):
         grads = [None] * nl
         prev = None  # (partials, gradient) of the layer above, reduced by this layer's launch
         for k in range(nl - 1, -1, -1):
-            h, qkv, cx, y1, y2, st1, st2, seed_used = ctx.saved[k]
+            h, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used = ctx.saved[k]
             cfg = cfgs[k]
             params = flat[12 * k:12 * (k + 1)]
             dx = torch.empty_like(h)
@@ -1695,12 +1703,13 @@ class _EncoderStack(torch.autograd.Function):
             with profiling.region("encoder_bwd", encoder_bytes(NS, L, True)):
                 native.check(lib.fr_encoder_bwd(
                     g.data_ptr(), h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
-                    seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(), y2.data_ptr(),
-                    st1.data_ptr(), st2.data_ptr(), dx.data_ptr(), grad.data_ptr() if k == 0 else None,
+                    seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(), fact.data_ptr(),
+                    dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
+                    grad.data_ptr() if (k == 0 or not ENCODER_FOLD) else None,
                     part.data_ptr(), nparts, prev[0].data_ptr() if prev else None,
                     prev[1].data_ptr() if prev else None, native.stream_of(g)), "fr_encoder_bwd")
             grads[k] = grad
-            prev = (part, grad)
+            prev = (part, grad) if ENCODER_FOLD else None
             g = dx
         out = []
         for k in range(nl):

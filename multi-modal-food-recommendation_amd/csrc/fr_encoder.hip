@@ -67,9 +67,9 @@ struct FwdArgs {
   const int64_t* counter;
   int64_t* seed_out;   // counter value used (read back by the backward)
   float* out;          // [NS, L, 64]
-  // saved for the backward (st: (mean, rstd) per token).  The FF activation is not saved: the
-  // backward recomputes pre = LN1(y1) W1^T + b1 (one more GEMM) and its GELU / dropout from it
-  float *qkv, *ctx, *y1, *y2, *st1, *st2;
+  // saved for the backward: fact = dropout(act(pre)), dact = keep * scale * act'(pre)  [T, 256];
+  // st: (mean, rstd) per token
+  float *qkv, *ctx, *y1, *fact, *dact, *y2, *st1, *st2;
 };
 
 struct BwdArgs {
@@ -79,7 +79,7 @@ struct BwdArgs {
   const float* mask;
   int64_t ns;
   const int64_t* seed_in;
-  const float *qkv, *ctx, *y1, *y2, *st1, *st2;
+  const float *qkv, *ctx, *y1, *fact, *dact, *y2, *st1, *st2;
   float* dx;
   float* part;         // [n_wg, NPART]
   // optional: another backward call's partials ([n_wg, NPART], the same n_wg) summed into prev_grad
@@ -204,6 +204,12 @@ __device__ __forceinline__ float comp(const float4& v, int m) {
 
 constexpr float kScale = 0.17677669529663688f;  // 1 / sqrt(HD)
 
+
+// offset of lane's float4 (4 rows of one column) of FF1 column tile (SIMD slot sg, c), row tile r, in
+// the fragment-layout dact buffer [n_wg][ROWS * FF]
+__device__ __forceinline__ int64_t dact_frag(int wg, int sg, int c, int r, int lane) {
+  return (int64_t)wg * (ROWS * FF) + ((((sg * 4 + c) * RT + r) * 64 + lane) << 2);
+}
 
 // the partner lane's value (lanes 2k <-> 2k+1, DPP quad_perm [1,0,3,2])
 __device__ __forceinline__ float pair_swap(float v) { return dpp_mov<0xB1>(v); }
@@ -758,41 +764,13 @@ __device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const 
   }
 }
 
-// x1 = LN1(y1) from the saved LN input and (mean, rstd), the forward's arithmetic (bit-identical) ->
-// LDS [80 x 64] at ld LD_E; rows >= tv zero
-__device__ __forceinline__ void ln1_recompute(float* X, const float* __restrict__ y1, const float* __restrict__ st1,
-                                              const float* __restrict__ g, const float* __restrict__ b, int tv) {
-  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
-  const float4 gg = *reinterpret_cast<const float4*>(g + 4 * l);
-  const float4 bb = *reinterpret_cast<const float4*>(b + 4 * l);
-  constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
-  float4 yv[NR];
-  float2 sv[NR];
-#pragma unroll
-  for (int k = 0; k < NR; ++k) {
-    const int r = min(grp + k * NG, tv - 1);
-    yv[k] = *reinterpret_cast<const float4*>(y1 + (int64_t)r * E + 4 * l);
-    sv[k] = *reinterpret_cast<const float2*>(st1 + 2 * r);
-  }
-#pragma unroll
-  for (int k = 0; k < NR; ++k) {
-    const int r = grp + k * NG;
-    if (r >= ROWS) break;
-    const float4 v = yv[k];
-    const float mean = sv[k].x, rstd = sv[k].y;
-    const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
-    const float4 o = make_float4(fmaf(d.x * rstd, gg.x, bb.x), fmaf(d.y * rstd, gg.y, bb.y),
-                                 fmaf(d.z * rstd, gg.z, bb.z), fmaf(d.w * rstd, gg.w, bb.w));
-    *reinterpret_cast<float4*>(X + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
 // The ordered reduction of another backward call's partials, folded into this launch: workgroup b
-// owns float4 columns [b C, (b + 1) C) of the NPART / 4 (C = ceil(NPART / 4 / n_wg)); PR_SL slices of
-// its threads sum workgroups s, s + PR_SL, ... in order (PR_UNR loads in flight per thread), then the
-// slices are added in slice order through LDS (scratch: PR_SL x C float4).  The same column always
-// gets the same order of additions: deterministic, independent of placement and timing.
-constexpr int PR_SL = 8, PR_UNR = 8;
+// owns float4 columns [b C, (b + 1) C) of the NPART / 4 (C = ceil(NPART / 4 / n_wg)), taken in chunks
+// of PR_CH columns (what the scratch holds); PR_SL slices of its threads sum workgroups s, s + PR_SL,
+// ... in order (PR_UNR loads in flight per thread), then the slices are added in slice order through
+// LDS (scratch: PR_SL x PR_CH float4).  The same column always gets the same order of additions:
+// deterministic, independent of placement and timing.
+constexpr int PR_SL = 10, PR_UNR = 26, PR_CH = (BUF_D / 4) / PR_SL;  // (256 workgroups: one batch of loads)
 __device__ __forceinline__ void prev_reduce(const float* __restrict__ prev, int nwg, float* __restrict__ out,
                                             float* scratch) {
   constexpr int N4 = NPART / 4;
@@ -800,28 +778,31 @@ __device__ __forceinline__ void prev_reduce(const float* __restrict__ prev, int 
   const int c0 = blockIdx.x * C;
   const float4* p4 = reinterpret_cast<const float4*>(prev);
   float4* s4 = reinterpret_cast<float4*>(scratch);
-  for (int e = threadIdx.x; e < PR_SL * C; e += NT) {
-    const int cl = e % C, sl = e / C, c = min(c0 + cl, N4 - 1);
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g0 = sl; g0 < nwg; g0 += PR_SL * PR_UNR) {
-      float4 v[PR_UNR];
+  for (int cb = 0; cb < C; cb += PR_CH) {
+    const int cn = min(PR_CH, C - cb);
+    for (int e = threadIdx.x; e < PR_SL * cn; e += NT) {
+      const int cl = e % cn, sl = e / cn, c = min(c0 + cb + cl, N4 - 1);
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int g0 = sl; g0 < nwg; g0 += PR_SL * PR_UNR) {
+        float4 v[PR_UNR];
 #pragma unroll
-      for (int k = 0; k < PR_UNR; ++k) v[k] = p4[(int64_t)min(g0 + k * PR_SL, nwg - 1) * N4 + c];
+        for (int k = 0; k < PR_UNR; ++k) v[k] = p4[(int64_t)min(g0 + k * PR_SL, nwg - 1) * N4 + c];
 #pragma unroll
-      for (int k = 0; k < PR_UNR; ++k)
-        if (g0 + k * PR_SL < nwg) s = f4_add(s, v[k]);
+        for (int k = 0; k < PR_UNR; ++k)
+          if (g0 + k * PR_SL < nwg) s = f4_add(s, v[k]);
+      }
+      s4[sl * cn + cl] = s;
     }
-    s4[sl * C + cl] = s;
-  }
-  __syncthreads();
-  for (int cl = threadIdx.x; cl < C; cl += NT) {
-    if (c0 + cl >= N4) break;
-    float4 t = s4[cl];
+    __syncthreads();
+    for (int cl = threadIdx.x; cl < cn; cl += NT) {
+      if (c0 + cb + cl >= N4) break;
+      float4 t = s4[cl];
 #pragma unroll
-    for (int k = 1; k < PR_SL; ++k) t = f4_add(t, s4[k * C + cl]);
-    reinterpret_cast<float4*>(out)[c0 + cl] = t;
+      for (int k = 1; k < PR_SL; ++k) t = f4_add(t, s4[k * cn + cl]);
+      reinterpret_cast<float4*>(out)[c0 + cb + cl] = t;
+    }
+    __syncthreads();
   }
-  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -904,30 +885,36 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   FR_MARK(0, 5);
 
   {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA.  Column split (wave: tiles 4sg + 2hf, +1;
-     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue.
-     // The backward recomputes exactly this (ff1_act_bwd): same tiles, same order, same epilogue
+     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue
     f32x4 acc[RT][2];
     zero_acc(acc);
     gemm_xwt<2, E, 0, RT>(RB, LD_E, w.w1, 4 * sg + 2 * hf, acc);
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
-      const int col = 16 * (4 * sg + 2 * hf + cc) + i16;
+      const int c = 2 * hf + cc;  // column tile within the SIMD slot's four (dact fragment index)
+      const int col = 16 * (4 * sg + c) + i16;
       const float bias = w.b1[col];
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
         const int row0 = 16 * r + 4 * h4;
         const uint32_t kb = frag_keep4(ks.k[2], tok0 + row0, FF, col, w.thr[2]);
+        float d[4];
 #pragma unroll
         for (int q2 = 0; q2 < 2; ++q2) {
-          f32x2 av, gv;  // (gv unused here: the backward's recomputation takes it from the same call)
+          f32x2 av, gv;
           act_fwd_grad2(f32x2{acc[r][cc][2 * q2], acc[r][cc][2 * q2 + 1]} + bias, w.gelu, av, gv);
           av = av * w.scale[2];
+          gv = gv * w.scale[2];
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int q = 2 * q2 + u;
-            RA[(row0 + q) * LD_FF + col] = ((kb >> q) & 1u) ? av[u] : 0.f;
+            const bool kp = (kb >> q) & 1u;
+            RA[(row0 + q) * LD_FF + col] = kp ? av[u] : 0.f;
+            d[q] = kp ? gv[u] : 0.f;
           }
         }
+        // dact in the MFMA fragment layout: one coalesced float4 per lane, read back the same way
+        *reinterpret_cast<float4*>(a.dact + dact_frag(blockIdx.x, sg, c, r, lane)) = make_float4(d[0], d[1], d[2], d[3]);
       }
     }
   }
@@ -954,6 +941,7 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   }
   __syncthreads();
   FR_MARK(0, 7);
+  lds_store<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);  // act' (RA is final after the FF2 barrier)
   ln_rows_fwd(RB, w.g2, w.be2, w.eps2, tv, a.y2 + tok0 * E, a.st2 + 2 * tok0, a.out + tok0 * E);
   FR_MARK(0, 31);
 }
@@ -1003,57 +991,27 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   FR_MARK(1, 1);
   ln_rows_bwd(RB, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, tv, RD, part + OFF_G2, part + OFF_BE2);
 
-  // 2. dG = dropout2'(dY2) -> RC;  x1 = LN1(y1) recomputed -> RD (free after LN2's last barrier)
+  // 2. dG = dropout2'(dY2) -> RC;  act' (saved by the forward) -> RA
   drop_pairs(RB, RC, ks.k[3], tok0, w.thr[3], w.scale[3]);
-  ln1_recompute(RD, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, w.be1, tv);
+  lds_load<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);
   __syncthreads();
   FR_MARK(1, 2);
-
-  // 2b. the FF activation recomputed exactly as the forward made it: pre = x1 W1^T + b1 (same tiles,
-  //     same order), act' = dropout(act(pre)) -> RA; dact = keep * scale * act'(pre) stays in
-  //     registers (this lane's fragment elements) until step 4
-  float dg[2][RT][4];
-  {
-    f32x4 acc[RT][2];
-    zero_acc(acc);
-    gemm_xwt<2, E, 0, RT>(RD, LD_E, w.w1, 4 * sg + 2 * hf, acc);
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const int col = 16 * (4 * sg + 2 * hf + cc) + i16;
-      const float bias = w.b1[col];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const int row0 = 16 * r + 4 * h4;
-        const uint32_t kb = frag_keep4(ks.k[2], tok0 + row0, FF, col, w.thr[2]);
-#pragma unroll
-        for (int q2 = 0; q2 < 2; ++q2) {
-          f32x2 av, gv;
-          act_fwd_grad2(f32x2{acc[r][cc][2 * q2], acc[r][cc][2 * q2 + 1]} + bias, w.gelu, av, gv);
-          av = av * w.scale[2];
-          gv = gv * w.scale[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int q = 2 * q2 + u;
-            const bool kp = (kb >> q) & 1u;
-            RA[(row0 + q) * LD_FF + col] = kp ? av[u] : 0.f;
-            dg[cc][r][q] = kp ? gv[u] : 0.f;
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  FR_MARK(1, 20);
 
   // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 2w, 2w+1);  db2
   wgrad_tiles<4, 2>(RC, LD_E, RA, LD_FF, 0, 2 * wave, part + OFF_W2, FF);
   colsum(RC, LD_E, E, part + OFF_B2);
 
-  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * dact -> RA  (wave: column tiles 4sg + 2hf, +1; every
-     // row tile: the fragments of step 2b)
+  {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA  (wave: column tiles
+     // 4sg + 2hf, +1; every row tile)
     f32x4 acc[RT][2];
     zero_acc(acc);
     gemm_yw<2, E, FF, 0, RT>(RC, LD_E, w.w2, 4 * sg + 2 * hf, acc);
+    float4 pv[2][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, sg, 2 * hf + cc, r, lane));
     __syncthreads();  // every wave is done reading act' from RA
     FR_MARK(1, 3);
 #pragma unroll
@@ -1064,19 +1022,44 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = 16 * r + 4 * h4 + q;
-          RA[row * LD_FF + col] = row < tv ? acc[r][cc][q] * dg[cc][r][q] : 0.f;
+          RA[row * LD_FF + col] = row < tv ? acc[r][cc][q] * comp(pv[cc][r], q) : 0.f;
         }
     }
   }
   __syncthreads();
   FR_MARK(1, 4);
 
-  // 5. db1 (x1 is in RD since step 2)
+  // 5. db1; x1 = LN1(y1) recomputed -> RC
   colsum(RA, LD_FF, FF, part + OFF_B1);
+  {
+    const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const float4 gg = *reinterpret_cast<const float4*>(w.g1 + 4 * l);
+    const float4 bb = *reinterpret_cast<const float4*>(w.be1 + 4 * l);
+    constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
+    float4 yv[NR];
+    float2 sv[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int r = min(grp + k * NG, tv - 1);
+      yv[k] = *reinterpret_cast<const float4*>(a.y1 + (tok0 + r) * E + 4 * l);
+      sv[k] = *reinterpret_cast<const float2*>(a.st1 + 2 * (tok0 + r));
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int r = grp + k * NG;
+      if (r >= ROWS) break;
+      const float4 v = yv[k];
+      const float mean = sv[k].x, rstd = sv[k].y;
+      const float4 o = make_float4(fmaf((v.x - mean) * rstd, gg.x, bb.x), fmaf((v.y - mean) * rstd, gg.y, bb.y),
+                                   fmaf((v.z - mean) * rstd, gg.z, bb.z), fmaf((v.w - mean) * rstd, gg.w, bb.w));
+      *reinterpret_cast<float4*>(RC + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __syncthreads();
   FR_MARK(1, 5);
 
   // 6. dW1 = dpre^T x1  [256 x 64] (wave: n-tiles 2w, 2w+1)
-  wgrad_tiles<2, 4>(RA, LD_FF, RD, LD_E, 2 * wave, 0, part + OFF_W1, E);
+  wgrad_tiles<2, 4>(RA, LD_FF, RC, LD_E, 2 * wave, 0, part + OFF_W1, E);
 
   {  // 7. dX1 = dY2 + dpre W1  -> RB
     f32x4 acc[RT0][1];
@@ -1260,6 +1243,12 @@ extern "C" int64_t fr_encoder_partials(int64_t n_seq, int L) {
 
 extern "C" int64_t fr_encoder_grad_numel(void) { return NPART; }
 
+// floats of the forward's dact buffer (per-workgroup MFMA fragment layout, ROWS x FF per workgroup)
+extern "C" int64_t fr_encoder_dact_numel(int64_t n_seq, int L) {
+  if (n_seq <= 0 || !supported_len(L)) return 0;
+  return fr::ceil_div(n_seq, ROWS / L) * (int64_t)(ROWS * FF);
+}
+
 extern "C" int fr_encoder_profile(int enable, uint64_t* host_marks) {
   if (enable >= 0) {
     const int on = enable ? 1 : 0;
@@ -1272,21 +1261,22 @@ extern "C" int fr_encoder_profile(int enable, uint64_t* host_marks) {
 extern "C" int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_seq, int L,
                               const float* const* d_params, const float* eps, const float* drop, uint64_t seed,
                               int gelu, const int64_t* d_counter, int64_t* d_seed_out, float* d_out,
-                              float* d_qkv, float* d_ctx, float* d_y1, float* d_y2, float* d_st1, float* d_st2,
-                              void* stream) {
+                              float* d_qkv, float* d_ctx, float* d_y1, float* d_fact, float* d_dact, float* d_y2,
+                              float* d_st1, float* d_st2, void* stream) {
   FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
   FR_REQUIRE(n_seq * L * FF < (int64_t)1 << 32 && n_seq * HEADS * L * L < (int64_t)1 << 32,
              "too many tokens for the 32-bit dropout element index");
-  FR_REQUIRE(d_x && d_out && d_counter && d_seed_out && d_qkv && d_ctx && d_y1 && d_y2 && d_st1 && d_st2,
+  FR_REQUIRE(d_x && d_out && d_counter && d_seed_out && d_qkv && d_ctx && d_y1 && d_fact && d_dact && d_y2 &&
+                 d_st1 && d_st2,
              "null operand");
   FR_REQUIRE(fr::aligned16(d_x) && fr::aligned16(d_out) && fr::aligned16(d_qkv) && fr::aligned16(d_ctx) &&
-                 fr::aligned16(d_y1) && fr::aligned16(d_y2),
+                 fr::aligned16(d_y1) && fr::aligned16(d_fact) && fr::aligned16(d_dact) && fr::aligned16(d_y2),
              "tensors must be 16-byte aligned");
   FwdArgs a{};
   int rc = fill_weights(a.w, d_params, eps, drop, seed, gelu);
   if (rc) return rc;
   a.x = d_x; a.mask = d_mask; a.ns = n_seq; a.counter = d_counter; a.seed_out = d_seed_out; a.out = d_out;
-  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
+  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.fact = d_fact; a.dact = d_dact; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (L) {
     case 20: return launch_fwd<20>(a, s);
@@ -1301,11 +1291,13 @@ extern "C" int fr_encoder_fwd(const float* d_x, const float* d_mask, int64_t n_s
 extern "C" int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, int64_t n_seq, int L,
                               const float* const* d_params, const float* eps, const float* drop, uint64_t seed,
                               int gelu, const int64_t* d_seed_in, const float* d_qkv, const float* d_ctx,
-                              const float* d_y1, const float* d_y2, const float* d_st1, const float* d_st2,
-                              float* d_dx, float* d_grad, float* d_partials, int64_t partial_floats,
-                              const float* d_prev_partials, float* d_prev_grad, void* stream) {
+                              const float* d_y1, const float* d_fact, const float* d_dact, const float* d_y2,
+                              const float* d_st1, const float* d_st2, float* d_dx, float* d_grad, float* d_partials,
+                              int64_t partial_floats, const float* d_prev_partials, float* d_prev_grad,
+                              void* stream) {
   FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
-  FR_REQUIRE(d_dout && d_x && d_seed_in && d_qkv && d_ctx && d_y1 && d_y2 && d_st1 && d_st2 && d_dx && d_partials,
+  FR_REQUIRE(d_dout && d_x && d_seed_in && d_qkv && d_ctx && d_y1 && d_fact && d_dact && d_y2 && d_st1 && d_st2 &&
+                 d_dx && d_partials,
              "null operand");
   FR_REQUIRE(!d_prev_partials == !d_prev_grad, "d_prev_partials and d_prev_grad go together");
   FR_REQUIRE(fr::aligned16(d_dout) && fr::aligned16(d_x) && fr::aligned16(d_dx) && fr::aligned16(d_grad) &&
@@ -1317,7 +1309,7 @@ extern "C" int fr_encoder_bwd(const float* d_dout, const float* d_x, const float
   int rc = fill_weights(a.w, d_params, eps, drop, seed, gelu);
   if (rc) return rc;
   a.dout = d_dout; a.x = d_x; a.mask = d_mask; a.ns = n_seq; a.seed_in = d_seed_in;
-  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
+  a.qkv = d_qkv; a.ctx = d_ctx; a.y1 = d_y1; a.fact = d_fact; a.dact = d_dact; a.y2 = d_y2; a.st1 = d_st1; a.st2 = d_st2;
   a.dx = d_dx; a.part = d_partials; a.prev_part = d_prev_partials; a.prev_grad = d_prev_grad;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (L) {

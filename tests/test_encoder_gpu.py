@@ -166,7 +166,8 @@ def test_encoder_writes_stay_in_bounds(cuda, NS, L):
     drop = (ctypes.c_float * 4)(0.1, 0.1, 0.1, 0.1)
     counter = torch.zeros(1, dtype=torch.int64, device=cuda)
     seed_used = torch.zeros(1, dtype=torch.int64, device=cuda)
-    sizes = {"out": T * 64, "qkv": T * 192, "ctx": T * 64, "y1": T * 64, "y2": T * 64, "st1": T * 2, "st2": T * 2}
+    sizes = {"out": T * 64, "qkv": T * 192, "ctx": T * 64, "y1": T * 64, "fact": T * 256,
+             "dact": int(lib.fr_encoder_dact_numel(NS, L)), "y2": T * 64, "st1": T * 2, "st2": T * 2}
     outs = {k: guarded(n) for k, n in sizes.items()}
     s = native.stream_of(x)
     native.check(lib.fr_encoder_fwd(x.data_ptr(), m.data_ptr(), NS, L, pp, eps, drop, 5, 1, counter.data_ptr(),
