@@ -280,6 +280,9 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # FR_SSL_MFMA=0: the VALU forms of the dCor / InfoNCE Gram tiles (A/B of the two kernel sets)
+        if os.environ.get("FR_SSL_MFMA") is not None:
+            handle.fr_ssl_kernels(int(os.environ["FR_SSL_MFMA"] != "0"))
         _lib = handle
     return _lib
 

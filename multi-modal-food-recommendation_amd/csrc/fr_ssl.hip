@@ -196,9 +196,11 @@ __device__ __forceinline__ void row_sq_r(const float* X, float* out) {
 //   bwd partial P [JS][V][n][d] floats, rowm [JS][V][n] floats
 constexpr int DCOR_JS = 16;  // j-splits of the backward tiles: 16 x 16 = 256 workgroups at n = 1024 (1 per CU)
 
+constexpr int DCOR_BP = MAXV + 2 * MAXP;  // per means-block partials: sum mean, sum mean products, sum S
+
 struct DcorWS {
   double* S; float* row; double* mean; double* Abar; double* coef;
-  float* P; float* rowm;
+  float* P; float* rowm; double* bpart;
 };
 
 __host__ __device__ inline DcorWS dcor_ws(void* base, int64_t n, int V) {
@@ -214,6 +216,7 @@ __host__ __device__ inline DcorWS dcor_ws(void* base, int64_t n, int V) {
   w.coef = reinterpret_cast<double*>(take(MAXP * 8));
   w.P = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 128 * 4));
   w.rowm = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 4));
+  w.bpart = reinterpret_cast<double*>(take((n + 63) / 64 * DCOR_BP * 8));
   return w;
 }
 
@@ -222,7 +225,8 @@ inline int64_t dcor_ws_bytes(int64_t n, int V) {
   const int NP = V * (V + 1) / 2;
   auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
   return r(nt * nt * NP * 8) + r((int64_t)V * nt * n * 4) + r((int64_t)V * n * 8) + r(MAXV * 8) +
-         r(MAXP * 8) + r((int64_t)DCOR_JS * V * n * 128 * 4) + r((int64_t)DCOR_JS * V * n * 4);
+         r(MAXP * 8) + r((int64_t)DCOR_JS * V * n * 128 * 4) + r((int64_t)DCOR_JS * V * n * 4) +
+         r((n + 63) / 64 * DCOR_BP * 8);
 }
 
 // distance tile of one view: D[x][y] for the thread's 4x4 block
@@ -402,70 +406,88 @@ __global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n
     }
 }
 
-// one block: means, centred sums, dcor values, backward coefficients.  Two reduction rounds: (1) every
-// view's row means (fixed j-tile order; a thread's rows the same for all views) and their block sums
-// -> Abar; (2) every pair's sum of mean products and of per-tile pair sums, reduced together.
-__global__ __launch_bounds__(1024) void dcor_finalize_kernel(int V, int64_t n, PairTab pt,
-                                                             DcorWS ws, float* out) {
-  __shared__ double red[2 * MAXP][16];
+// the row means and the block partials of the centred sums: one wave per 64 rows (thread i: row i of
+// every view, the j-tile row sums in fixed order), then per wave the sums of the means, of the pair
+// products of the means and of a contiguous chunk of the per-tile pair sums -> ws.bpart[block]
+template <int V>
+__global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
+  constexpr int NP = V * (V + 1) / 2;
+  const int64_t nt = (n + T - 1) / T;
+  const int lane = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  double mv[V];
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    double s = 0.0;
+    if (i < n) {
+      const float* r = ws.row + (int64_t)a * nt * n + i;
+      int64_t jt = 0;
+      for (; jt + 8 <= nt; jt += 8) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = r[(jt + u) * n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += (double)x[u];
+      }
+      for (; jt < nt; ++jt) s += (double)r[jt * n];
+    }
+    mv[a] = i < n ? s / (double)n : 0.0;
+    if (i < n) ws.mean[(int64_t)a * n + i] = mv[a];
+  }
+  double* bp = ws.bpart + (int64_t)blockIdx.x * DCOR_BP;
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    const double t = group_sum_d<64>(mv[a]);
+    if (lane == 0) bp[a] = t;
+  }
+#pragma unroll
+  for (int a = 0; a < V; ++a)
+#pragma unroll
+    for (int b = a; b < V; ++b) {
+      const double t = group_sum_d<64>(mv[a] * mv[b]);
+      if (lane == 0) bp[MAXV + pair_index(a, b, V)] = t;
+    }
+  const int64_t nblk = nt * nt, per = (nblk + gridDim.x - 1) / gridDim.x;
+  const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    double lS = 0.0;
+    for (int64_t blk = b0 + lane; blk < b1; blk += 64) lS += ws.S[blk * NP + k];
+    const double t = group_sum_d<64>(lS);
+    if (lane == 0) bp[MAXV + MAXP + k] = t;
+  }
+}
+
+// one wave: the block partials in block order -> Abar, centred sums, dcor values, backward coefficients
+__global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int nb, PairTab pt, DcorWS ws,
+                                                           float* out) {
+  __shared__ double tot[DCOR_BP];
   __shared__ double Sc[MAXP];
   __shared__ double Ab[MAXV];
-  const int64_t nt = (n + T - 1) / T;
   const int NP = V * (V + 1) / 2;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
-  // round 1: row means of every view
-  double loc[MAXV] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
-    for (int a = 0; a < V; ++a) {
-      double s = 0.0;
-      for (int64_t jt = 0; jt < nt; ++jt) s += (double)ws.row[((int64_t)a * nt + jt) * n + i];
-      const double m = s / (double)n;
-      ws.mean[(int64_t)a * n + i] = m;
-      loc[a] += m;
-    }
-  for (int a = 0; a < V; ++a) {
-    const double t = group_sum_d<64>(loc[a]);
-    if (lane == 0) red[a][wv] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < V) {
+  const int t = threadIdx.x;
+  const bool used = t < DCOR_BP && (t < V || (t >= MAXV && t < MAXV + NP) || (t >= MAXV + MAXP && t < MAXV + MAXP + NP));
+  if (used) {
     double s = 0.0;
-    for (int w = 0; w < nw; ++w) s += red[threadIdx.x][w];
-    Ab[threadIdx.x] = s / (double)n;
-    ws.Abar[threadIdx.x] = Ab[threadIdx.x];
-  }
-  __syncthreads();  // (this thread's means were written by itself: read back below without a fence)
-  // round 2: centred pair sums
-  double lab[MAXP], lS[MAXP];
-  for (int k = 0; k < NP; ++k) { lab[k] = 0.0; lS[k] = 0.0; }
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    double mv[MAXV];
-    for (int a = 0; a < V; ++a) mv[a] = ws.mean[(int64_t)a * n + i];
-    for (int a = 0; a < V; ++a)
-      for (int b = a; b < V; ++b) lab[pair_index(a, b, V)] += mv[a] * mv[b];
-  }
-  // per-tile pair sums: strided over the block, then a fixed-shape tree (deterministic)
-  for (int64_t blk = threadIdx.x; blk < nt * nt; blk += blockDim.x)
-    for (int k = 0; k < NP; ++k) lS[k] += ws.S[blk * NP + k];
-  for (int k = 0; k < NP; ++k) {
-    const double ta = group_sum_d<64>(lab[k]);
-    const double tS = group_sum_d<64>(lS[k]);
-    if (lane == 0) { red[2 * k][wv] = ta; red[2 * k + 1][wv] = tS; }
+    for (int b = 0; b < nb; ++b) s += ws.bpart[(int64_t)b * DCOR_BP + t];
+    tot[t] = s;
   }
   __syncthreads();
-  if (threadIdx.x < NP) {
-    const int pi = threadIdx.x;
-    double ab = 0.0, S = 0.0;
-    for (int w = 0; w < nw; ++w) { ab += red[2 * pi][w]; S += red[2 * pi + 1][w]; }
+  if (t < V) {
+    Ab[t] = tot[t] / (double)n;
+    ws.Abar[t] = Ab[t];
+  }
+  __syncthreads();
+  if (t < NP) {
     int a = 0, b = 0;
     for (int x = 0; x < V; ++x)
       for (int y = x; y < V; ++y)
-        if (pair_index(x, y, V) == pi) { a = x; b = y; }
+        if (pair_index(x, y, V) == t) { a = x; b = y; }
     const double dn = (double)n;
-    Sc[pi] = S - 2.0 * dn * ab + dn * dn * Ab[a] * Ab[b];
+    Sc[t] = tot[MAXV + MAXP + t] - 2.0 * dn * tot[MAXV + t] + dn * dn * Ab[a] * Ab[b];
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     const double dn2 = (double)n * (double)n;
     double coef[MAXP];
     for (int k = 0; k < NP; ++k) coef[k] = 0.0;
@@ -1216,7 +1238,15 @@ extern "C" int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, 
     default: hipLaunchKernelGGL(dcor_tiles_kernel<4>, grid, dim3(256), lds, s, v, n, d, w); break;
   }
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(1024), 0, s, n_views, n, pt, w, d_out);
+  const int nb = (int)fr::ceil_div(n, 64);
+  switch (n_views) {
+    case 1: hipLaunchKernelGGL(dcor_means_kernel<1>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
+    case 2: hipLaunchKernelGGL(dcor_means_kernel<2>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
+    case 3: hipLaunchKernelGGL(dcor_means_kernel<3>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
+    default: hipLaunchKernelGGL(dcor_means_kernel<4>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
+  }
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(64), 0, s, n_views, n, nb, pt, w, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
