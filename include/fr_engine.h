@@ -122,6 +122,13 @@ int fr_bpr_fwd_rows(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi
                     const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
                     int64_t B, int d, float gamma, float* d_out, float* d_rows, int64_t ld_rows,
                     void* d_workspace, int64_t workspace_bytes, void* stream);
+/* fr_bpr_fwd_rows with out[4] = w_emb * EmbLoss in fp32 (the models' reg_weight * reg term,
+ * e.g. pricai_modelx.py:267, without a multiply launch; w_emb 1 is the EmbLoss itself). */
+int fr_bpr_fwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                  const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                  const int64_t* d_u, const int64_t* d_p, const int64_t* d_n,
+                  int64_t B, int d, float gamma, float w_emb, float* d_out, float* d_rows, int64_t ld_rows,
+                  void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* Backward.  g_mf scales d(out[0]); g_reg scales d(out[4]) (i.e. reg_weight * upstream grad).
  * d_gscale (optional, device float[2]) multiplies g_mf / g_reg on the device so no host
@@ -165,6 +172,16 @@ int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, int d,
                 const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
                 float* const* d_dviews,
                 void* d_workspace, int64_t workspace_bytes, void* stream);
+/* _ex forms: out[P] = weight * sum_k out[k] in fp32 (CLUSSL's loss_cl * SSL term, pricai_modelx.py:263-
+ * 267, without a separate multiply launch; weight 1 is the plain sum); the backward with overwrite != 0
+ * WRITES dviews (no zero-filled buffers needed) instead of accumulating. */
+int fr_dcor_fwd_ex(const float* const* d_views, int n_views, int64_t n, int d,
+                   const int32_t* pairs, int n_pairs, float weight, float* d_out,
+                   void* d_workspace, int64_t workspace_bytes, void* stream);
+int fr_dcor_bwd_ex(const float* const* d_views, int n_views, int64_t n, int d,
+                   const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
+                   float* const* d_dviews, int overwrite,
+                   void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* CLUSSL's view sum and SSL gathers (PRICAI_ModelX.forward + calculate_loss,
  * models/pricai_modelx.py:227-263: item_emb = ingre + image + text, then each view at the batch
@@ -173,6 +190,15 @@ int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, int d,
 int fr_views_sum_gather(const float* const* d_views, int n_views, int64_t n, int d,
                         const int64_t* d_ids, int64_t m, float* d_total, float* const* d_gathered,
                         void* stream);
+/* Its backward: d_dviews[k] = d_gsum (NULL: zeros) + sum over j with ids[j] = r of d_grows[k][j], written in
+ * full.  Default: a broadcast, then float atomics (one wave-instruction per row and view; duplicate ids
+ * add in hardware order, as torch's index_add_).  deterministic != 0: the (id, j) pairs are sorted (one
+ * workgroup, workspace m * 8 bytes) and the head of each id's run adds that row's terms in increasing j
+ * (no atomics; m <= 8192). */
+int64_t fr_views_sum_gather_bwd_workspace(int64_t m);
+int fr_views_sum_gather_bwd(const float* d_gsum, const float* const* d_grows, int n_views, int64_t n, int d,
+                            const int64_t* d_ids, int64_t m, float* const* d_dviews, int deterministic,
+                            void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused InfoNCE / NT-Xent (PRICAI_ModelX.CL_loss, hidden_norm=True): H is [2b, d];
@@ -200,6 +226,10 @@ int fr_infonce_multi_fwd(const float* const* d_views, int n_views, int64_t b, in
 int fr_infonce_multi_bwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
                          int n_pairs, float tau, float g, const float* d_gscale, float* const* d_dviews,
                          void* d_workspace, int64_t workspace_bytes, void* stream);
+/* out[0] = weight * (the fp32 pair sum) (CLUSSL's loss_cl * CL term without a multiply launch). */
+int fr_infonce_multi_fwd_ex(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
+                            int n_pairs, float tau, float weight, float* d_out, void* d_workspace,
+                            int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Multi-tensor Adam, following torch.optim.Adam (amsgrad=False, maximize=False) element order:

@@ -583,6 +583,7 @@ class Trainer(AbstractTrainer):
             t = cache.get(key)
             if t is None:
                 t = torch.ones(x.shape, dtype=x.dtype, device=x.device)
+                t._fr_unit = True  # exactly one, never written: engine backwards skip their device scale
                 cache[key] = t
             out.append(t)
         return out

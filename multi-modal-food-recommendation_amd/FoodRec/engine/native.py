@@ -81,6 +81,9 @@ _SIGS = {
     "fr_bpr_fwd_rows": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                                 c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_int64,
                                 c_void_p, c_int64, c_void_p]),
+    "fr_bpr_fwd_ex": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                              c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
+                              c_int64, c_void_p, c_int64, c_void_p]),
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "fr_score_segments": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
@@ -125,6 +128,15 @@ _SIGS = {
     "fr_dcor_workspace": (c_int64, [c_int64, c_int]),
     "fr_views_sum_gather": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, c_void_p, c_int64, c_void_p,
                                     POINTER(c_void_p), c_void_p]),
+    "fr_views_sum_gather_bwd_workspace": (c_int64, [c_int64]),
+    "fr_views_sum_gather_bwd": (c_int, [c_void_p, POINTER(c_void_p), c_int, c_int64, c_int, c_void_p, c_int64,
+                                        POINTER(c_void_p), c_int, c_void_p, c_int64, c_void_p]),
+    "fr_dcor_fwd_ex": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int, c_float,
+                               c_void_p, c_void_p, c_int64, c_void_p]),
+    "fr_dcor_bwd_ex": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
+                               c_float, c_void_p, POINTER(c_void_p), c_int, c_void_p, c_int64, c_void_p]),
+    "fr_infonce_multi_fwd_ex": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int, c_float,
+                                        c_float, c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_dcor_fwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,
                             c_void_p, c_void_p, c_int64, c_void_p]),
     "fr_dcor_bwd": (c_int, [POINTER(c_void_p), c_int, c_int64, c_int, POINTER(c_int32), c_int,

@@ -408,10 +408,41 @@ def propagate_mean(adj: Adjacency, ego: torch.Tensor, n_layers: int) -> torch.Te
     return _PropagateMean.apply(adj, ego, int(n_layers))
 
 
+class _PropagateMeanSplit(torch.autograd.Function):
+    """propagate_mean(adj, cat([lo, hi])) with the concatenation folded into the SpMM addressing
+    (split tables): no [N, d] copy forward, and the two gradients are written straight into their
+    own buffers backward (no split of a concatenated gradient)."""
+
+    @staticmethod
+    def forward(ctx, adj, lo, hi, L):
+        lo, hi = _rowmajor(lo), _rowmajor(hi)
+        native.require_device(lo, hi)
+        ctx.adj, ctx.L, ctx.split = adj, L, lo.shape[0]
+        ctx.shapes = (lo.shape, hi.shape)
+        return _prop_fwd_split(adj, lo, hi, lo.shape[0], L)
+
+    @staticmethod
+    def backward(ctx, G):
+        G = _rowmajor(G)
+        d_lo = torch.empty(ctx.shapes[0], dtype=G.dtype, device=G.device)
+        d_hi = torch.empty(ctx.shapes[1], dtype=G.dtype, device=G.device)
+        _prop_bwd_split(ctx.adj, G, ctx.L, d_lo, d_hi, ctx.split)
+        return None, d_lo, d_hi, None
+
+
+def propagate_mean_split(adj: Adjacency, lo: torch.Tensor, hi: torch.Tensor, n_layers: int) -> torch.Tensor:
+    """propagate_mean(adj, torch.cat([lo, hi]), n_layers) without the concatenation (fp32, d = 64
+    on the GPU, a symmetric adjacency of len(lo) + len(hi) rows); otherwise exactly that."""
+    if (n_layers >= 1 and getattr(adj, "symmetric", False) and lo.is_cuda and lo.dtype == torch.float32 == hi.dtype and lo.shape[1] == 64 == hi.shape[1]
+            and lo.shape[0] + hi.shape[0] == adj.shape[0]):
+        return _PropagateMeanSplit.apply(adj, lo, hi, int(n_layers))
+    return propagate_mean(adj, torch.cat([lo, hi], dim=0), n_layers)
+
+
 # ----------------------------------------------------------------------------- BPR + EmbLoss
 class _BprEmb(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic, item_rows=False, item_offset=None):
+    def forward(ctx, U, I, Ue, Ie, u, p, n, gamma, deterministic, item_rows=False, item_offset=None, w_emb=1.0):
         # item_offset: items are rows [item_offset:] of U (one propagated table, one gradient buffer,
         # item ids unchanged); the kernels just see the offset base pointers
         ctx.ioff = None if item_offset is None else int(item_offset)
@@ -431,29 +462,47 @@ class _BprEmb(torch.autograd.Function):
         ws = native.workspace(lib.fr_bpr_workspace(B), U.device)
         out = torch.empty(5, dtype=torch.float32, device=U.device)
         ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
-        fwd = lib.fr_bpr_fwd_bf16 if bf16 else lib.fr_bpr_fwd
-        native.check(fwd(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
-                         native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
-                         B, d, _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(),
-                         native.stream_of(U)), "fr_bpr_fwd")
+        rows = None
+        if bf16:
+            if w_emb != 1.0:
+                raise native.EngineError("bpr_emb_loss: w_emb needs fp32 tables")
+            native.check(lib.fr_bpr_fwd_bf16(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
+                                             native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                                             B, d, _f(gamma), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             native.stream_of(U)), "fr_bpr_fwd_bf16")
+        else:
+            # out[4] = w_emb * EmbLoss in the kernel (no multiply launch); [I[pos]; I[neg]] written by the
+            # same launch when asked for
+            if item_rows:
+                rows = torch.empty(2 * B, d, dtype=I.dtype, device=I.device)
+            native.check(lib.fr_bpr_fwd_ex(U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue),
+                                           native.ptr(Ie), ld(Ie), u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                                           B, d, _f(gamma), _f(w_emb), out.data_ptr(), native.ptr(rows),
+                                           d if rows is not None else 0, ws.data_ptr(), ws.numel(),
+                                           native.stream_of(U)), "fr_bpr_fwd_ex")
         ctx.save_for_backward(U, I, Ue, Ie, u, p, n)
-        ctx.ws, ctx.gamma, ctx.det = ws, gamma, int(deterministic)
+        ctx.ws, ctx.gamma, ctx.det, ctx.w_emb = ws, gamma, int(deterministic), float(w_emb)
         ctx.same_u, ctx.same_i = Ue is U, Ie is I
         ctx.alias_ui, ctx.alias_e = alias_ui, alias_e
         ctx.item_rows = bool(item_rows) and not deterministic and I.dtype == torch.float32
         if not item_rows:
             return out[0], out[4:5]
         # [I[pos]; I[neg]] for another consumer; its gradient joins the backward's own scatter
-        rows = torch.index_select(I, 0, torch.cat([p, n]))
+        if rows is None:
+            rows = torch.index_select(I, 0, torch.cat([p, n]))
         return out[0], out[4:5], rows
 
     @staticmethod
     def backward(ctx, g_mf, g_emb, g_rows=None):
         U, I, Ue, Ie, u, p, n = ctx.saved_tensors
         dev = U.device
-        g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
-        g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
-        gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
+        if _is_unit(g_mf) and _is_unit(g_emb):
+            gscale = None  # both upstream gradients are the trainer's ones seeds: no device scale needed
+        else:
+            g_mf = g_mf if g_mf is not None else torch.zeros((), device=dev)
+            g_emb = g_emb if g_emb is not None else torch.zeros(1, device=dev)
+            gscale = torch.cat([g_mf.reshape(1), g_emb.reshape(1)]).float().contiguous()
+        g_reg = _f(ctx.w_emb)
         need = ctx.needs_input_grad
         if ctx.ioff is not None:
             dU = _grad_like(U) if need[0] else None
@@ -472,23 +521,23 @@ class _BprEmb(torch.autograd.Function):
         if U.dtype == torch.bfloat16:
             native.check(native.lib().fr_bpr_bwd_bf16(
                 U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
-                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
-                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), g_reg,
+                native.ptr(gscale), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
                 ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd_bf16")
         elif g_rows is not None and dI is not None and ctx.item_rows:
             g_rows = g_rows.contiguous()
             native.check(native.lib().fr_bpr_bwd_ex(
                 U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
-                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
-                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), g_reg,
+                native.ptr(gscale), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
                 g_rows.data_ptr(), g_rows.stride(0), ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)),
                 "fr_bpr_bwd_ex")
             g_rows = None
         else:
             native.check(native.lib().fr_bpr_bwd(
                 U.data_ptr(), ld(U), I.data_ptr(), ld(I), native.ptr(Ue), ld(Ue), native.ptr(Ie), ld(Ie),
-                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), _f(1.0),
-                gscale.data_ptr(), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
+                u.data_ptr(), p.data_ptr(), n.data_ptr(), B, d, _f(ctx.gamma), _f(1.0), g_reg,
+                native.ptr(gscale), native.ptr(dU), native.ptr(dI), native.ptr(dUe), native.ptr(dIe),
                 ctx.det, ctx.ws.data_ptr(), ctx.ws.numel(), native.stream_of(U)), "fr_bpr_bwd")
         if ctx.same_u:
             dUe = None
@@ -498,7 +547,13 @@ class _BprEmb(torch.autograd.Function):
             dI.index_add_(0, torch.cat([p, n]), g_rows.to(dI.dtype))
         if ctx.alias_ui or ctx.ioff is not None:
             dI = None
-        return dU, dI, dUe, dIe, None, None, None, None, None, None, None
+        return dU, dI, dUe, dIe, None, None, None, None, None, None, None, None
+
+
+def _is_unit(g) -> bool:
+    """An upstream gradient known to be exactly one: the trainer's cached backward seeds
+    (Trainer._ones_like marks them ``_fr_unit``; they are never written)."""
+    return g is not None and getattr(g, "_fr_unit", False)
 
 
 _DETERMINISTIC = False
@@ -570,13 +625,14 @@ def set_deterministic(on: bool) -> None:
 
 
 def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma: float = 1e-10, deterministic: bool = False,
-                 item_rows: bool = False, item_offset: int | None = None):
+                 item_rows: bool = False, item_offset: int | None = None, w_emb: float = 1.0):
     """Returns (BPRLoss, EmbLoss-unweighted [1]) with gathers, dots and norms fused; with
     ``item_rows`` also the gathered [I[pos]; I[neg]] rows, whose gradient is added inside the fused
     backward's scatter (no separate gather backward).  ``item_offset`` (with I None): the item table
-    is U[item_offset:] -- one [users + items] gradient buffer instead of two plus a concatenation."""
+    is U[item_offset:] -- one [users + items] gradient buffer instead of two plus a concatenation.
+    ``w_emb``: the EmbLoss output is w_emb * EmbLoss (the models' reg_weight), applied in the kernels."""
     return _BprEmb.apply(U, I, Ue, Ie, user, pos, neg, gamma, deterministic or _DETERMINISTIC, item_rows,
-                         item_offset)
+                         item_offset, float(w_emb))
 
 
 # ----------------------------------------------------------------------------- split-table SpMM
@@ -2104,7 +2160,7 @@ def modal_head(enc, query, ids, num, pad_id, rows, labels, ln_a, ln_b, mlp, kd_t
 # ----------------------------------------------------------------------------- dCor
 class _DCor(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pairs, *views):
+    def forward(ctx, pairs, weight, *views):
         views = tuple(_rowmajor(v, f32_only=True) for v in views)
         native.require_device(*views)
         V = len(views)
@@ -2114,10 +2170,11 @@ class _DCor(torch.autograd.Function):
         vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
         pa = (ctypes.c_int32 * (2 * len(pairs)))(*[x for pr in pairs for x in pr])
         out = torch.empty(len(pairs) + 1, dtype=torch.float32, device=views[0].device)
-        native.check(lib.fr_dcor_fwd(vp, V, n, d, pa, len(pairs), out.data_ptr(), ws.data_ptr(),
-                                     ws.numel(), native.stream_of(views[0])), "fr_dcor_fwd")
+        # out[P] = weight * sum of the pairs (the model's loss_cl applied in the kernel)
+        native.check(lib.fr_dcor_fwd_ex(vp, V, n, d, pa, len(pairs), _f(weight), out.data_ptr(), ws.data_ptr(),
+                                        ws.numel(), native.stream_of(views[0])), "fr_dcor_fwd_ex")
         ctx.save_for_backward(*views)
-        ctx.ws, ctx.pairs = ws, pairs
+        ctx.ws, ctx.pairs, ctx.weight = ws, pairs, float(weight)
         return out[len(pairs):]
 
     @staticmethod
@@ -2125,28 +2182,30 @@ class _DCor(torch.autograd.Function):
         views = ctx.saved_tensors
         V = len(views)
         n, d = views[0].shape
-        grads = [torch.zeros_like(v) if ctx.needs_input_grad[1 + i] else None for i, v in enumerate(views)]
+        # written in full by the kernel (overwrite): no zero-filled buffers
+        grads = [torch.empty_like(v) if ctx.needs_input_grad[2 + i] else None for i, v in enumerate(views)]
         vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
         gp = (ctypes.c_void_p * V)(*[native.ptr(x) for x in grads])
         pa = (ctypes.c_int32 * (2 * len(ctx.pairs)))(*[x for pr in ctx.pairs for x in pr])
-        gs = g.reshape(1).float().contiguous()
-        native.check(native.lib().fr_dcor_bwd(vp, V, n, d, pa, len(ctx.pairs), _f(1.0), gs.data_ptr(), gp,
-                                              ctx.ws.data_ptr(), ctx.ws.numel(),
-                                              native.stream_of(views[0])), "fr_dcor_bwd")
-        return (None, *grads)
+        gs = None if _is_unit(g) else g.reshape(1).float().contiguous()
+        native.check(native.lib().fr_dcor_bwd_ex(vp, V, n, d, pa, len(ctx.pairs), _f(ctx.weight), native.ptr(gs),
+                                                 gp, 1, ctx.ws.data_ptr(), ctx.ws.numel(),
+                                                 native.stream_of(views[0])), "fr_dcor_bwd_ex")
+        return (None, None, *grads)
 
 
-def dcor_loss(views, pairs) -> torch.Tensor:
-    """sum over pairs (a,b) of correlation_distance(views[a], views[b]) -> shape [1]."""
-    return _DCor.apply(tuple(tuple(p) for p in pairs), *views)
+def dcor_loss(views, pairs, weight: float = 1.0) -> torch.Tensor:
+    """weight * sum over pairs (a,b) of correlation_distance(views[a], views[b]) -> shape [1]."""
+    return _DCor.apply(tuple(tuple(p) for p in pairs), float(weight), *views)
 
 
 class _ViewsSumGather(torch.autograd.Function):
     """(v_0 + v_1 + ... , v_0[ids], v_1[ids], ...) for V equally shaped tables (CLUSSL: item_emb =
     item_ingre + item_image + item_text and the SSL views gathered at the batch items,
     pricai_modelx.py:227-263).  Backward: d v_k = g_sum + scatter_add(ids, g_k) for all k at once --
-    one broadcast copy and V atomic index_adds instead of, per view, a zero-filled scatter (the
-    deterministic counting sort: 4 launches) and autograd's accumulation add."""
+    a broadcast and one float-atomic row add per id and view (deterministic mode: an id sort and an
+    ordered add per distinct id) instead of, per view, a
+    zero-filled scatter and autograd's accumulation add."""
 
     @staticmethod
     def forward(ctx, ids, *views):
@@ -2170,19 +2229,28 @@ class _ViewsSumGather(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         V, (n, d) = ctx.V, ctx.shape
         dev = ids.device
-        out = (g_sum.unsqueeze(0).expand(V, n, d).clone() if g_sum is not None
-               else torch.zeros(V, n, d, dtype=torch.float32, device=dev))
-        for k, g in enumerate(g_rows):
-            if g is not None:
-                out[k].index_add_(0, ids, g)
-        return (None, *out.unbind(0))
+        out = [torch.empty(n, d, dtype=torch.float32, device=dev) for _ in range(V)]
+        m = ids.numel()
+        g_rows = [(_rowmajor(g) if g is not None else torch.zeros(m, d, dtype=torch.float32, device=dev))
+                  for g in g_rows]
+        g_sum = _rowmajor(g_sum) if g_sum is not None else None
+        # d v_k = g_sum + the rows of g_k scattered at ids: a broadcast and one float-atomic row add per
+        # id and view (deterministic mode: an id sort and one ordered add per distinct id instead)
+        lib = native.lib()
+        det = int(_DETERMINISTIC)
+        ws = native.workspace(lib.fr_views_sum_gather_bwd_workspace(m) if det else 16, dev)
+        native.check(lib.fr_views_sum_gather_bwd(
+            native.ptr(g_sum), (ctypes.c_void_p * V)(*[g.data_ptr() for g in g_rows]), V, n, d, ids.data_ptr(), m,
+            (ctypes.c_void_p * V)(*[o.data_ptr() for o in out]), det, ws.data_ptr(), ws.numel(),
+            native.stream_of(out[0])), "fr_views_sum_gather_bwd")
+        return (None, *out)
 
 
 def views_sum_gather(views, ids):
-    """(sum(views) in list order, [v[ids] for v in views]); see _ViewsSumGather.  Deterministic
-    mode keeps the separate sum and deterministic row gathers."""
+    """(sum(views) in list order, [v[ids] for v in views]); see _ViewsSumGather.  More than 8,192 ids:
+    the separate sum and row gathers."""
     ids = ids.reshape(-1).to(torch.int64)
-    if _DETERMINISTIC or not all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in views) \
+    if not all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in views) or ids.numel() > 8192 \
             or len({tuple(v.shape) for v in views}) != 1 or len(views) > 4 or views[0].shape[1] % 4:
         total = views[0]
         for v in views[1:]:
@@ -2228,7 +2296,7 @@ def infonce_loss(H: torch.Tensor, tau: float = 0.5) -> torch.Tensor:
 
 class _InfoNCEMulti(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pairs, tau, *views):
+    def forward(ctx, pairs, tau, weight, *views):
         views = tuple(_rowmajor(v, f32_only=True) for v in views)
         native.require_device(*views)
         V = len(views)
@@ -2240,10 +2308,11 @@ class _InfoNCEMulti(torch.autograd.Function):
         vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
         pa = (ctypes.c_int32 * (2 * len(pairs)))(*[x for pr in pairs for x in pr])
         out = torch.empty(1 + len(pairs), dtype=torch.float32, device=views[0].device)
-        native.check(lib.fr_infonce_multi_fwd(vp, V, b, d, pa, len(pairs), _f(tau), out.data_ptr(), ws.data_ptr(),
-                                              ws.numel(), native.stream_of(views[0])), "fr_infonce_multi_fwd")
+        native.check(lib.fr_infonce_multi_fwd_ex(vp, V, b, d, pa, len(pairs), _f(tau), _f(weight), out.data_ptr(),
+                                                 ws.data_ptr(), ws.numel(), native.stream_of(views[0])),
+                     "fr_infonce_multi_fwd_ex")
         ctx.save_for_backward(*views)
-        ctx.ws, ctx.pairs, ctx.tau = ws, pairs, tau
+        ctx.ws, ctx.pairs, ctx.tau, ctx.weight = ws, pairs, tau, float(weight)
         return out[0]
 
     @staticmethod
@@ -2251,22 +2320,23 @@ class _InfoNCEMulti(torch.autograd.Function):
         views = ctx.saved_tensors
         V = len(views)
         b, d = views[0].shape
-        grads = [torch.empty_like(v) if ctx.needs_input_grad[2 + i] else None for i, v in enumerate(views)]
+        grads = [torch.empty_like(v) if ctx.needs_input_grad[3 + i] else None for i, v in enumerate(views)]
         vp = (ctypes.c_void_p * V)(*[v.data_ptr() for v in views])
         gp = (ctypes.c_void_p * V)(*[native.ptr(x) for x in grads])
         pa = (ctypes.c_int32 * (2 * len(ctx.pairs)))(*[x for pr in ctx.pairs for x in pr])
-        gs = g.reshape(1).float().contiguous()
-        native.check(native.lib().fr_infonce_multi_bwd(vp, V, b, d, pa, len(ctx.pairs), _f(ctx.tau), _f(1.0),
-                                                       gs.data_ptr(), gp, ctx.ws.data_ptr(), ctx.ws.numel(),
+        gs = None if _is_unit(g) else g.reshape(1).float().contiguous()
+        native.check(native.lib().fr_infonce_multi_bwd(vp, V, b, d, pa, len(ctx.pairs), _f(ctx.tau), _f(ctx.weight),
+                                                       native.ptr(gs), gp, ctx.ws.data_ptr(), ctx.ws.numel(),
                                                        native.stream_of(views[0])), "fr_infonce_multi_bwd")
-        return (None, None, *grads)
+        return (None, None, None, *grads)
 
 
-def infonce_pairs(views, pairs, tau: float = 0.5) -> torch.Tensor:
+def infonce_pairs(views, pairs, tau: float = 0.5, weight: float = 1.0) -> torch.Tensor:
     """sum over pairs (a, b) of infonce_loss(cat([views[a], views[b]]), tau) (CLUSSL's ssl_mode
     infonce, pricai_modelx.py:263 with CL_loss :354-378) in one forward and one backward node: no
-    concatenation, each view normalised once, all pairs in the same launches.  0-dim result."""
-    return _InfoNCEMulti.apply(tuple(tuple(int(x) for x in p) for p in pairs), float(tau), *views)
+    concatenation, each view normalised once, all pairs in the same launches.  0-dim result, times
+    ``weight`` (the model's loss_cl) in the kernel."""
+    return _InfoNCEMulti.apply(tuple(tuple(int(x) for x in p) for p in pairs), float(tau), float(weight), *views)
 
 
 # ----------------------------------------------------------------------------- full-sort top-k

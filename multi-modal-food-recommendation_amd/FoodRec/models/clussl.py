@@ -109,23 +109,29 @@ class CLUSSL(GeneralRecommender):
             gathered = [g_img, g_txt, g_ing]
         else:
             item_emb = item_ingre + item_image + item_text
-        ui = ops.propagate_mean(self.norm_adj_matrix, torch.cat([self.user_embedding.weight, item_emb], dim=0),
-                                self.n_ui_layers)
+        # propagate(cat([user, item_emb])) with the concatenation folded into the SpMM addressing
+        ui = ops.propagate_mean_split(self.norm_adj_matrix, self.user_embedding.weight, item_emb, self.n_ui_layers)
+        if ssl_ids is not None:  # the loss reads the one table (bpr_emb_loss item_offset): no split backward
+            return ui, None, (item_image, item_text, item_ingre), gathered
         user_all, item_all = torch.split(ui, [self.n_users, self.n_items])
         return user_all, item_all, (item_image, item_text, item_ingre), gathered
 
     def calculate_loss(self, batch_data):
         user, pos_item, neg_item = batch_data["u_id"], batch_data["pos_i_id"], batch_data["neg_i_id"]
-        all_item = torch.cat([pos_item, neg_item], dim=0)
-        user_all, item_all, _, views = self._forward(all_item)  # views at the batch items: image, text, ingre
-        mf_loss, emb = ops.bpr_emb_loss(user_all, item_all, self.user_embedding.weight, self.item_embedding.weight,
-                                        user, pos_item, neg_item)
+        # [pos; neg] as the engine feed laid it out (a graphed step's batch), else concatenated
+        all_item = dict.get(batch_data, "pn_i_id") if isinstance(batch_data, dict) else None
+        if all_item is None:
+            all_item = torch.cat([pos_item, neg_item], dim=0)
+        ui, _, _, views = self._forward(all_item)  # views at the batch items: image, text, ingre
+        # the loss weights (reg_weight, loss_cl) are applied inside the kernels: no multiply launches
+        mf_loss, reg = ops.bpr_emb_loss(ui, None, self.user_embedding.weight, self.item_embedding.weight,
+                                        user, pos_item, neg_item, item_offset=self.n_users, w_emb=self.reg_weight)
         if self.ssl_mode == "infonce":
             # sum over the pairs of CL_loss(cat([views[a], views[b]])): one fused node for all pairs
-            cl = ops.infonce_pairs(views, _DCOR_PAIRS, 0.5)
+            cl = ops.infonce_pairs(views, _DCOR_PAIRS, 0.5, weight=self.loss_cl)
         else:
-            cl = ops.dcor_loss(views, _DCOR_PAIRS)
-        return mf_loss, self.loss_cl * cl, self.reg_weight * emb
+            cl = ops.dcor_loss(views, _DCOR_PAIRS, weight=self.loss_cl)
+        return mf_loss, cl, reg
 
     # inference_fast below is the plain gather-dot of forward()'s tables: the trainer may score the
     # evaluation lists with fr_score_segments instead (no [n, 64] gathers)

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void bpr_scores_kernel(
 }
 
 // one block, fixed-order fp64 reduction -> out[0..4], ws.norms
-__global__ __launch_bounds__(1024) void bpr_reduce_kernel(int64_t B, float gamma, int has_emb,
+__global__ __launch_bounds__(1024) void bpr_reduce_kernel(int64_t B, float gamma, int has_emb, float w_emb,
                                                           BprWS ws, float* out) {
   __shared__ double red[4][16];
   double l = 0.0, a = 0.0, c = 0.0, e = 0.0;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(1024) void bpr_reduce_kernel(int64_t B, float gamma
     out[1] = nu;
     out[2] = np;
     out[3] = nn;
-    out[4] = ((nu + np) + nn) / (float)B;
+    out[4] = w_emb * (((nu + np) + nn) / (float)B);  // (w_emb = 1: the EmbLoss itself, exactly)
     ws.norms[0] = nu;
     ws.norms[1] = np;
     ws.norms[2] = nn;
@@ -638,6 +638,15 @@ extern "C" int fr_bpr_fwd_rows(const float* d_U, int64_t ldu, const float* d_I, 
                                const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
                                float gamma, float* d_out, float* d_rows, int64_t ld_rows, void* d_workspace,
                                int64_t workspace_bytes, void* stream) {
+  return fr_bpr_fwd_ex(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, gamma, 1.f, d_out, d_rows,
+                       ld_rows, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_bpr_fwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
+                             const float* d_Ue, int64_t ldue, const float* d_Ie, int64_t ldie,
+                             const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, int d,
+                             float gamma, float w_emb, float* d_out, float* d_rows, int64_t ld_rows,
+                             void* d_workspace, int64_t workspace_bytes, void* stream) {
   int rc = bpr_check(d_U, ldu, d_I, ldi, d_Ue, ldue, d_Ie, ldie, d_u, d_p, d_n, B, d, d_workspace,
                      workspace_bytes);
   if (rc) return rc;
@@ -649,7 +658,7 @@ extern "C" int fr_bpr_fwd_rows(const float* d_U, int64_t ldu, const float* d_I, 
   hipLaunchKernelGGL(bpr_scores_kernel, dim3(blocks), dim3(256), 0, s, d_U, ldu, d_I, ldi, d_Ue, ldue,
                      d_Ie, ldie, d_u, d_p, d_n, B, d / 4, w, d_rows, ld_rows);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w, d_out);
+  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w_emb, w, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
@@ -779,7 +788,7 @@ extern "C" int fr_bpr_fwd_bf16(const uint16_t* d_U, int64_t ldu, const uint16_t*
                        d_Ie, ldie, d_u, d_p, d_n, B, d / 8, w);
   });
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, w, d_out);
+  hipLaunchKernelGGL(bpr_reduce_kernel, dim3(1), dim3(1024), 0, s, B, gamma, d_Ue ? 1 : 0, 1.f, w, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
 
 // one wave: the block partials in block order -> Abar, centred sums, dcor values, backward coefficients
 __global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int nb, PairTab pt, DcorWS ws,
-                                                           float* out) {
+                                                           float weight, float* out) {
   __shared__ double tot[DCOR_BP];
   __shared__ double Sc[MAXP];
   __shared__ double Ab[MAXV];
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int
       coef[iaa] += d_c11 * gate(s11) / (2.0 * c11) / dn2;
       coef[ibb] += d_c22 * gate(s22) / (2.0 * c22) / dn2;
     }
-    out[pt.n_pairs] = total;
+    out[pt.n_pairs] = weight * total;  // (weight 1: the sum itself, exactly)
     for (int k = 0; k < NP; ++k) ws.coef[k] = coef[k];
   }
 }
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n
 // dX_a[i][k] += 4 g (x_i[k] * rowm_i - P_i[k])   (sum over j-splits in order)
 __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, int64_t n, int d,
                                                                 int js_count, float g,
-                                                                const float* gscale, DcorWS ws) {
+                                                                const float* gscale, int overwrite, DcorWS ws) {
   const float gg = 4.f * g * (gscale ? gscale[0] : 1.f);
   const int64_t total = (int64_t)V * n * d;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -771,7 +771,8 @@ __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, 
       rm += ws.rowm[((int64_t)s * V + a) * n + i];
       p += ws.P[(((int64_t)s * V + a) * n + i) * d + k];
     }
-    v.dx[a][i * d + k] += gg * (v.x[a][i * d + k] * rm - p);
+    const float val = gg * (v.x[a][i * d + k] * rm - p);
+    v.dx[a][i * d + k] = overwrite ? val : v.dx[a][i * d + k] + val;
   }
 }
 
@@ -945,7 +946,7 @@ __global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, flo
 
 // out_pairs[p] (optional) = pair p's loss (fp64 sum of its row terms in block order / b^2, rounded
 // once); out[0] = their fp32 sum in pair order (Python's sum() over the pairs' fp32 losses)
-__global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int n_pairs, NceWS ws, float* out,
+__global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int n_pairs, NceWS ws, float weight, float* out,
                                                       float* out_pairs) {
   __shared__ double red[16];
   const int64_t nparts = nce_nparts(2 * b);
@@ -965,7 +966,7 @@ __global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int n_pairs, N
       total = p == 0 ? lp : total + lp;
     }
   }
-  if (threadIdx.x == 0) out[0] = total;
+  if (threadIdx.x == 0) out[0] = weight * total;  // (weight 1: the sum itself, exactly)
 }
 
 // dHn_i = (1/tau) sum_j W_ij Hn_j,  W_ij = dl_ij + dl_ji,  dl_ij = (P_ij - [j==p(i)]) * g / b^2  (pair blockIdx.z)
@@ -1211,6 +1212,12 @@ static int dcor_check(const float* const* views, int V, int64_t n, int d, const 
 extern "C" int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, int d,
                            const int32_t* pairs, int n_pairs, float* d_out, void* d_workspace,
                            int64_t workspace_bytes, void* stream) {
+  return fr_dcor_fwd_ex(d_views, n_views, n, d, pairs, n_pairs, 1.f, d_out, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fr_dcor_fwd_ex(const float* const* d_views, int n_views, int64_t n, int d,
+                              const int32_t* pairs, int n_pairs, float weight, float* d_out, void* d_workspace,
+                              int64_t workspace_bytes, void* stream) {
   int rc = dcor_check(d_views, n_views, n, d, pairs, n_pairs, d_workspace, workspace_bytes);
   if (rc) return rc;
   FR_REQUIRE(d_out, "out null");
@@ -1246,7 +1253,7 @@ extern "C" int fr_dcor_fwd(const float* const* d_views, int n_views, int64_t n, 
     default: hipLaunchKernelGGL(dcor_means_kernel<4>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
   }
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(64), 0, s, n_views, n, nb, pt, w, d_out);
+  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(64), 0, s, n_views, n, nb, pt, w, weight, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
@@ -1255,6 +1262,14 @@ extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, 
                            const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
                            float* const* d_dviews, void* d_workspace, int64_t workspace_bytes,
                            void* stream) {
+  return fr_dcor_bwd_ex(d_views, n_views, n, d, pairs, n_pairs, g, d_gscale, d_dviews, 0, d_workspace,
+                        workspace_bytes, stream);
+}
+
+extern "C" int fr_dcor_bwd_ex(const float* const* d_views, int n_views, int64_t n, int d,
+                              const int32_t* pairs, int n_pairs, float g, const float* d_gscale,
+                              float* const* d_dviews, int overwrite, void* d_workspace, int64_t workspace_bytes,
+                              void* stream) {
   int rc = dcor_check(d_views, n_views, n, d, pairs, n_pairs, d_workspace, workspace_bytes);
   if (rc) return rc;
   FR_REQUIRE(d_dviews, "dviews null");
@@ -1302,7 +1317,7 @@ extern "C" int fr_dcor_bwd(const float* const* d_views, int n_views, int64_t n, 
   const int64_t total = (int64_t)n_views * n * d;
   const unsigned blocks = (unsigned)std::min<int64_t>(fr::ceil_div(total, 256), 4096);
   hipLaunchKernelGGL(dcor_bwd_finalize_kernel, dim3(blocks), dim3(256), 0, s, v, n_views, n, d, js,
-                     g, d_gscale, w);
+                     g, d_gscale, overwrite, w);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
@@ -1328,8 +1343,8 @@ extern "C" int64_t fr_infonce_multi_workspace(int n_views, int64_t b, int d, int
 }
 
 static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs, int n_pairs,
-                        float tau, float* d_out, float* d_out_pairs, void* d_workspace, int64_t workspace_bytes,
-                        void* stream) {
+                        float tau, float weight, float* d_out, float* d_out_pairs, void* d_workspace,
+                        int64_t workspace_bytes, void* stream) {
   int rc = nce_check(d_views, n_views, b, d, pairs, n_pairs, tau, d_workspace, workspace_bytes);
   if (rc) return rc;
   FR_REQUIRE(d_out, "out null");
@@ -1363,7 +1378,7 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
   hipLaunchKernelGGL(nce_finalize_kernel, dim3((unsigned)nce_nparts(m), (unsigned)n_pairs), dim3(256), 0, s, b, d,
                      inv_tau, js, pt, w);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nce_sum_kernel, dim3(1), dim3(1024), 0, s, b, n_pairs, w, d_out, d_out_pairs);
+  hipLaunchKernelGGL(nce_sum_kernel, dim3(1), dim3(1024), 0, s, b, n_pairs, w, weight, d_out, d_out_pairs);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
@@ -1371,8 +1386,15 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
 extern "C" int fr_infonce_multi_fwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
                                     int n_pairs, float tau, float* d_out, void* d_workspace, int64_t workspace_bytes,
                                     void* stream) {
-  return nce_fwd_impl(d_views, n_views, b, d, pairs, n_pairs, tau, d_out, d_out ? d_out + 1 : nullptr, d_workspace,
+  return nce_fwd_impl(d_views, n_views, b, d, pairs, n_pairs, tau, 1.f, d_out, d_out ? d_out + 1 : nullptr, d_workspace,
                       workspace_bytes, stream);
+}
+
+extern "C" int fr_infonce_multi_fwd_ex(const float* const* d_views, int n_views, int64_t b, int d,
+                                       const int32_t* pairs, int n_pairs, float tau, float weight, float* d_out,
+                                       void* d_workspace, int64_t workspace_bytes, void* stream) {
+  return nce_fwd_impl(d_views, n_views, b, d, pairs, n_pairs, tau, weight, d_out, d_out ? d_out + 1 : nullptr,
+                      d_workspace, workspace_bytes, stream);
 }
 
 extern "C" int fr_infonce_multi_bwd(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs,
@@ -1430,7 +1452,7 @@ extern "C" int fr_infonce_fwd(const float* d_H, int64_t b, int d, float tau, flo
   FR_REQUIRE(d_H && d_out && fr::aligned16(d_H) && b >= 1 && (b * d) % 4 == 0, "H/out null or unaligned");
   const float* views[2] = {d_H, d_H + b * d};
   const int32_t pair[2] = {0, 1};
-  return nce_fwd_impl(views, 2, b, d, pair, 1, tau, d_out, nullptr, d_workspace, workspace_bytes, stream);
+  return nce_fwd_impl(views, 2, b, d, pair, 1, tau, 1.f, d_out, nullptr, d_workspace, workspace_bytes, stream);
 }
 
 extern "C" int fr_infonce_bwd(const float* d_H, int64_t b, int d, float tau, float g,
@@ -1481,7 +1503,137 @@ __global__ __launch_bounds__(256) void views_sum_gather_kernel(ViewsSG a, int V,
     a.g[k][j] = (r >= 0 && r < n) ? a.v[k][r * d4 + c] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
+// backward, phase 1: dv_k = g_sum for every k (one read of g_sum, V writes)
+__global__ __launch_bounds__(256) void views_bcast_kernel(ViewsSG a, int V, int64_t n4, const float4* __restrict__ gs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 x = gs ? gs[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < V; ++k) a.g[k][i] = x;
+  }
+}
+
+// phase 2, default: one wave per id, lane = column, one float atomic wave-instruction per view over the
+// 256 contiguous bytes of the row (the memory-side atomic units' full-rate shape); duplicate ids add
+// in hardware order (as torch's index_add_)
+__global__ __launch_bounds__(256) void views_scatter_atomic_kernel(ViewsSG a, int V, int64_t n, int d,
+                                                                   const int64_t* __restrict__ ids, int64_t m) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= m) return;
+  const int64_t r = ids[j];
+  if (r < 0 || r >= n) return;
+  for (int c = lane; c < d; c += 64)
+    for (int k = 0; k < V; ++k)
+      atomicAdd(reinterpret_cast<float*>(a.g[k]) + r * d + c, reinterpret_cast<const float*>(a.v[k])[j * d + c]);
+}
+
+// deterministic mode, phase 0 (one workgroup, before phase 1 in stream order): the (id, j) keys of all ids sorted in LDS
+// (bitonic network) -> keys[m].  key = (row + 1) << jbits | j; ids outside the table get row -1.
+constexpr int VSG_MAX_IDS = 8192;
+
+__global__ __launch_bounds__(1024) void views_sort_ids_kernel(const int64_t* __restrict__ ids, int64_t m, int64_t n,
+                                                              int mp2, int jbits, uint64_t* __restrict__ keys) {
+  __shared__ uint64_t key[VSG_MAX_IDS];
+  for (int t = threadIdx.x; t < mp2; t += blockDim.x) {
+    uint64_t k = ~0ull;  // padding keys sort last
+    if (t < m) {
+      const int64_t r = ids[t];
+      k = (r >= 0 && r < n) ? ((uint64_t)(r + 1) << jbits) | (uint64_t)t : (uint64_t)t;
+    }
+    key[t] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= mp2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (mp2 >> 1); t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t x = key[lo], y = key[hi];
+        if ((x > y) == up) { key[lo] = y; key[hi] = x; }
+      }
+      __syncthreads();
+    }
+  for (int t = threadIdx.x; t < m; t += blockDim.x) keys[t] = key[t];
+}
+
+// phase 2: every distinct id adds, for every view k, the sum of g_k over its occurrences in increasing
+// j -- each touched row written by one 16-lane group (the head of its run in the sorted keys), in a
+// fixed order (deterministic, no atomics); one float4 column per lane
+__global__ __launch_bounds__(256) void views_scatter_owner_kernel(ViewsSG a, int V, int d4,
+                                                                  const uint64_t* __restrict__ keys, int64_t m,
+                                                                  int jbits) {
+  const uint64_t jmask = (1ull << jbits) - 1;
+  const int q = threadIdx.x & 15;
+  const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (i >= m) return;
+  const uint64_t rid = keys[i] >> jbits;
+  if (rid == 0) return;                              // id outside the table
+  if (i > 0 && (keys[i - 1] >> jbits) == rid) return;  // not the head of its run
+  const int64_t r = (int64_t)rid - 1;
+  int64_t e = i + 1;
+  while (e < m && (keys[e] >> jbits) == rid) ++e;
+  for (int c = q; c < d4; c += 16) {
+    float4 acc[4];
+    for (int k = 0; k < V; ++k) acc[k] = a.g[k][r * d4 + c];
+    for (int64_t t = i; t < e; ++t) {
+      const int64_t jj = (int64_t)(keys[t] & jmask);
+      for (int k = 0; k < V; ++k) {
+        const float4 x = a.v[k][jj * d4 + c];
+        acc[k].x += x.x;
+        acc[k].y += x.y;
+        acc[k].z += x.z;
+        acc[k].w += x.w;
+      }
+    }
+    for (int k = 0; k < V; ++k) a.g[k][r * d4 + c] = acc[k];
+  }
+}
 }  // namespace
+
+extern "C" int64_t fr_views_sum_gather_bwd_workspace(int64_t m) { return m > 0 ? (m * 8 + 255) / 256 * 256 : 0; }
+
+extern "C" int fr_views_sum_gather_bwd(const float* d_gsum, const float* const* d_grows, int n_views, int64_t n,
+                                       int d, const int64_t* d_ids, int64_t m, float* const* d_dviews,
+                                       int deterministic, void* d_workspace, int64_t workspace_bytes,
+                                       void* stream) {
+  FR_REQUIRE(d_dviews && n_views >= 1 && n_views <= 4 && n >= 1 && d >= 4 && d % 4 == 0 && m >= 0 &&
+                 m <= VSG_MAX_IDS && (m == 0 || (d_ids && d_grows)) && (!d_gsum || fr::aligned16(d_gsum)),
+             "views_sum_gather_bwd: bad arguments (m <= 8192)");
+  FR_REQUIRE(!deterministic || m == 0 || (d_workspace && workspace_bytes >= m * 8 && fr::aligned16(d_workspace)),
+             "views_sum_gather_bwd: workspace too small");
+  ViewsSG a{};
+  for (int k = 0; k < n_views; ++k) {
+    FR_REQUIRE(d_dviews[k] && fr::aligned16(d_dviews[k]) && (m == 0 || (d_grows[k] && fr::aligned16(d_grows[k]))),
+               "views_sum_gather_bwd: gradient table null or unaligned");
+    a.g[k] = reinterpret_cast<float4*>(d_dviews[k]);
+    a.v[k] = m ? reinterpret_cast<const float4*>(d_grows[k]) : nullptr;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int d4 = d / 4;
+  int mp2 = 2, jbits = 1;
+  while (mp2 < m) { mp2 <<= 1; ++jbits; }
+  FR_REQUIRE(n < (int64_t(1) << (62 - jbits)), "views_sum_gather_bwd: table too large for the sort keys");
+  uint64_t* keys = reinterpret_cast<uint64_t*>(d_workspace);
+  if (m > 0 && deterministic) {
+    hipLaunchKernelGGL(views_sort_ids_kernel, dim3(1), dim3(1024), 0, s, d_ids, m, n, mp2, jbits, keys);
+    FR_LAUNCH_CHECK();
+  }
+  const int64_t work = n * d4;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(work, 256), (int64_t)fr::kNumCU * 16));
+  hipLaunchKernelGGL(views_bcast_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, n_views, work,
+                     reinterpret_cast<const float4*>(d_gsum));
+  FR_LAUNCH_CHECK();
+  if (m > 0 && deterministic) {
+    hipLaunchKernelGGL(views_scatter_owner_kernel, dim3((unsigned)fr::ceil_div(m, 16)), dim3(256), 0, s, a, n_views,
+                       d4, keys, m, jbits);
+    FR_LAUNCH_CHECK();
+  } else if (m > 0) {
+    hipLaunchKernelGGL(views_scatter_atomic_kernel, dim3((unsigned)fr::ceil_div(m, 4)), dim3(256), 0, s, a, n_views, n,
+                       d, d_ids, m);
+    FR_LAUNCH_CHECK();
+  }
+  return FR_OK;
+}
 
 extern "C" int fr_views_sum_gather(const float* const* d_views, int n_views, int64_t n, int d,
                                    const int64_t* d_ids, int64_t m, float* d_total, float* const* d_gathered,

@@ -59,17 +59,25 @@ def propagate_mean(adj, ego, n_layers):
 
 
 def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False, item_rows=False,
-                 item_offset=None):
+                 item_offset=None, w_emb=1.0):
     if item_offset is not None:
         I = U[item_offset:]
     u, p, n = U[user], I[pos], I[neg]
     mf = O.bpr_loss((u * p).sum(1), (u * n).sum(1), gamma)
     emb = torch.zeros(1) if Ue is None else O.emb_loss(Ue[user], Ie[pos], Ie[neg])
+    if w_emb != 1.0:
+        emb = w_emb * emb  # the model's reg_weight * EmbLoss (pricai_modelx.py:267)
     return (mf, emb, torch.cat([p, n])) if item_rows else (mf, emb)
 
 
-def dcor_loss(views, pairs):
-    return sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
+def dcor_loss(views, pairs, weight=1.0):
+    s = sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
+    return s if weight == 1.0 else weight * s  # loss_cl * SSL term (pricai_modelx.py:263-267)
+
+
+def infonce_pairs(views, pairs, tau=0.5, weight=1.0):
+    s = sum(O.cl_loss(torch.cat([views[a], views[b]]), tau) for a, b in pairs)
+    return s if weight == 1.0 else weight * s
 
 
 def infonce_loss(H, tau=0.5):
@@ -96,7 +104,7 @@ def linear(x, W, b=None):
 
 
 _PATCH = {"embedding": embedding, "embedding_norms": embedding_norms, "linear": linear, "spmm_launch": spmm_launch, "scatter_rows": scatter_rows, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
-          "dcor_loss": dcor_loss, "infonce_loss": infonce_loss}
+          "dcor_loss": dcor_loss, "infonce_loss": infonce_loss, "infonce_pairs": infonce_pairs}
 
 
 @contextlib.contextmanager

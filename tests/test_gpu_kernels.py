@@ -928,3 +928,96 @@ def test_healthrec_graph_bpr_matches_unfused(cuda):
     for k in ga:
         err = (ga[k] - gb[k]).abs().max().item()
         assert err <= 1e-5 * gb[k].abs().max().item() + 1e-9, (k, err)
+
+
+@pytest.mark.parametrize("det", [False, True])
+def test_views_sum_gather_bwd_heavy_duplicates(cuda, det, monkeypatch):
+    """fr_views_sum_gather_bwd with ids drawn from 40 rows (every row hit ~25 times): vs a float64
+    scatter reference; deterministic mode bit-identical across runs (sorted, ordered adds)."""
+    from FoodRec.engine import ops
+    monkeypatch.setattr(ops, "_DETERMINISTIC", det)
+    g = torch.Generator().manual_seed(5)
+    n, m, V = 3001, 1000, 3
+    views = [torch.randn(n, 64, generator=g).to(cuda).requires_grad_(True) for _ in range(V)]
+    ids = torch.randint(0, 40, (m,), generator=g).to(cuda)
+    gs = torch.randn(n, 64, generator=g)
+    gr = [torch.randn(m, 64, generator=g) for _ in range(V)]
+    runs = []
+    for _ in range(2):
+        for v in views:
+            v.grad = None
+        total, gathered = ops.views_sum_gather(views, ids)
+        torch.autograd.backward([total] + gathered, [gs.to(cuda)] + [x.to(cuda) for x in gr])
+        runs.append([v.grad.clone() for v in views])
+    if det:
+        for a, b in zip(*runs):
+            assert torch.equal(a, b)
+    ic = ids.cpu()
+    for k in range(V):
+        ref = gs.double().clone().index_add_(0, ic, gr[k].double())
+        torch.testing.assert_close(runs[0][k].cpu().double(), ref, rtol=0, atol=2e-5)
+
+
+def test_ssl_and_bpr_weights_in_kernel(cuda):
+    """dcor_loss / infonce_pairs (weight) and bpr_emb_loss (w_emb): the weighted loss equals the fp32
+    product w * (unweighted loss) bit for bit, and the gradients equal those of the multiply form
+    (the same products in the same order: bit-identical; the BPR scatter in its deterministic mode)."""
+    from FoodRec.engine import ops
+    from FoodRec.models.clussl import _DCOR_PAIRS
+    g = torch.Generator().manual_seed(3)
+    w = 0.037
+    views0 = [torch.randn(1024, 64, generator=g).to(cuda) for _ in range(3)]
+    for fn in (lambda vs, wt: ops.dcor_loss(vs, _DCOR_PAIRS, weight=wt),
+               lambda vs, wt: ops.infonce_pairs(vs, _DCOR_PAIRS, 0.5, weight=wt)):
+        va = [v.clone().requires_grad_(True) for v in views0]
+        vb = [v.clone().requires_grad_(True) for v in views0]
+        la = fn(va, w)
+        lb = w * fn(vb, 1.0)
+        assert torch.equal(la.detach(), lb.detach())
+        la.sum().backward()
+        lb.sum().backward()
+        for a, b in zip(va, vb):
+            assert torch.equal(a.grad, b.grad)
+    U = torch.randn(500, 64, generator=g).to(cuda)
+    E = [torch.randn(300, 64, generator=g).to(cuda) for _ in range(2)]
+    u = torch.randint(0, 200, (256,), generator=g).to(cuda)
+    p, n = (torch.randint(0, 300, (256,), generator=g).to(cuda) for _ in range(2))
+    res = []
+    for weighted in (True, False):
+        Ug = U.clone().requires_grad_(True)
+        Eg = [e.clone().requires_grad_(True) for e in E]
+        if weighted:
+            mf, reg = ops.bpr_emb_loss(Ug, None, Eg[0], Eg[1], u, p, n, item_offset=200, w_emb=w, deterministic=True)
+        else:
+            mf, reg = ops.bpr_emb_loss(Ug, None, Eg[0], Eg[1], u, p, n, item_offset=200, deterministic=True)
+            reg = w * reg
+        (mf + reg.sum()).backward()
+        res.append((mf.detach(), reg.detach(), Ug.grad, Eg[0].grad, Eg[1].grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_propagate_mean_split_matches_cat(cuda):
+    """ops.propagate_mean_split(adj, lo, hi) vs propagate_mean(adj, cat([lo, hi])): bit-identical
+    output and gradients (the same SpMM launches, split addressing)."""
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency
+    g = torch.Generator().manual_seed(11)
+    nu, ni, e = 700, 900, 9000
+    r = torch.randint(0, nu, (e,), generator=g)
+    c = torch.randint(0, ni, (e,), generator=g) + nu
+    rows, cols = torch.cat([r, c]), torch.cat([c, r])
+    deg = torch.bincount(rows, minlength=nu + ni).clamp(min=1).float()
+    vals = deg[rows].rsqrt() * deg[cols].rsqrt()
+    adj = Adjacency.from_coo(rows, cols, vals, (nu + ni, nu + ni), device=cuda)
+    lo0, hi0 = torch.randn(nu, 64, generator=g).to(cuda), torch.randn(ni, 64, generator=g).to(cuda)
+    G = torch.randn(nu + ni, 64, generator=g).to(cuda)
+    for L in (1, 2, 3):
+        la, ha = lo0.clone().requires_grad_(True), hi0.clone().requires_grad_(True)
+        lb, hb = lo0.clone().requires_grad_(True), hi0.clone().requires_grad_(True)
+        ya = ops.propagate_mean_split(adj, la, ha, L)
+        yb = ops.propagate_mean(adj, torch.cat([lb, hb]), L)
+        assert torch.equal(ya, yb), L
+        (ya * G).sum().backward()
+        (yb * G).sum().backward()
+        assert torch.equal(la.grad, lb.grad) and torch.equal(ha.grad, hb.grad), L
