@@ -234,6 +234,8 @@ def main():
 
     for i in range(max(args.warmup, 5 if use_graph else 0)):
         do_step(i)
+    if graphed is not None:
+        graphed.flush()  # no warm-up step left pending for the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -241,6 +243,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         do_step(args.warmup + i)
+    if graphed is not None:
+        graphed.flush()  # steps of an unrolled graph not yet replayed run inside the timed region
     t_submit = time.perf_counter() - t0  # host time to issue the steps (graph replays): < elapsed when GPU-bound
     torch.cuda.synchronize()
     t_steps = time.perf_counter() - t0
@@ -381,7 +385,9 @@ def main():
                 "config": {"workload": "healthrec_allrecipes", "model": "HealthRec (CIKM_Model)",
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                           "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single")},
+                           "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single"),
+                           "graph_steps_per_replay": (graphed.unroll if graphed is not None and world == 1 and not dp1
+                                                      else (1 if graphed is not None else 0))},
                 "roofline": roofline, "ranks": ranks, "scaling_config4": c4_scaling, "step_bytes": step_fig,
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
@@ -591,10 +597,12 @@ def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
         it = batches()
         for i in range(warmup):
             g(*next(it), i, state)
+        g.flush()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             g(*next(it), warmup + i, state)
+        g.flush()
         tr.flush_optimizer()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
@@ -1031,10 +1039,12 @@ def config1(device, steps=50, warmup=5, cpu=True, cpu_steps=20):
     it = batches()
     for i in range(warmup):
         g(*next(it), i, state)
+    g.flush()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         g(*next(it), warmup + i, state)
+    g.flush()
     tr.flush_optimizer()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps

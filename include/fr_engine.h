@@ -530,8 +530,9 @@ int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_gr
  * 311-369): fr_modal_fusion's know / hin per item (see below) feeding fr_health_kd's terms,
  *   d_out[0] = w_health * sum(BCE(sigmoid(mlp(hin)), labels)),
  *   d_out[1] = w_kd * max(0, 1 - mean_i cos(know_i, rows_i) - kd_threshold),  d_out[2] = the gate,
- * with know / hin and their gradients kept in registers.  Forward: 2 launches (per-item kernel +
- * fixed-order finalize).  Backward: 1 launch writing d_denc [n, L, 64], d_dquery [n, 2, 64], d_drows
+ * with know / hin and their gradients kept in registers.  Forward: 1 launch when d_ticket (a zero-
+ * initialised int32, reset to 0 by the launch) is given -- the last block to arrive runs the fixed-
+ * order finalize -- else 2 (per-item kernel + finalize kernel).  Backward: 1 launch writing d_denc [n, L, 64], d_dquery [n, 2, 64], d_drows
  * [n, 64] and one partial row per block; fr_modal_head_reduce sums them in block order into d_grad
  * [fr_modal_head_grad_numel()] = dW1 [64x64] | db1 [64] | dW2 [16x64, rows >= H zero] | db2 [16] |
  * d ln_a.weight [32] | d ln_a.bias | d ln_b.weight | d ln_b.bias.  d_ln / d_mlp as in
@@ -542,7 +543,8 @@ int64_t fr_modal_head_grad_numel(void);
 int fr_modal_head_fwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
                       int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, const float* d_rows,
                       const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,
-                      float w_kd, float* d_out, float* d_partials, int64_t partial_floats, void* stream);
+                      float w_kd, float* d_out, float* d_partials, int64_t partial_floats, int32_t* d_ticket,
+                      void* stream);
 int fr_modal_head_bwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
                       int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, const float* d_rows,
                       const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,

@@ -133,12 +133,21 @@ class GraphedStep:
     BPR/EmbLoss, backward, and the fused Adam update (device-side step counters and lr).  The
     first ``warmup`` calls run eagerly on a side stream (lazy workspaces, BLAS handles), the next
     call captures and replays.  Batches of another size (the epoch's last) run eagerly.
+
+    ``unroll`` > 1 (with a device feed and the graph's own state): a second graph holds ``unroll``
+    consecutive steps and is replayed once per ``unroll`` calls, so the per-replay launch gap
+    (~25 us between graphs on MI355X) is paid once per ``unroll`` steps.  Calls in between only count
+    the step; ``flush`` (run by the feed before it stages the next epoch, before a ragged batch, and
+    by the trainer at the epoch's end) replays the one-step graph for the steps still pending.
     """
 
-    def __init__(self, trainer, batch_size, warmup=3):
+    def __init__(self, trainer, batch_size, warmup=3, unroll=1):
         self.tr = trainer
         self.B = int(batch_size)
         self.warmup = max(1, int(warmup))
+        self.unroll = max(1, int(unroll))
+        self.graph_n = None   # the unrolled graph (unroll steps)
+        self.pending = 0      # steps called but not yet replayed (unroll > 1)
         dev = torch.device(trainer.device)
         self.u = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.p = torch.zeros_like(self.u)
@@ -160,7 +169,15 @@ class GraphedStep:
         if sampler.batch_size != self.B:
             raise ValueError("sampler batch size differs from the graphed step's")
         self.feed = sampler.device_feed()
+        self.feed.on_stage = self.flush  # pending steps read the epoch being replaced
         return self.feed
+
+    def flush(self):
+        """Replay the one-step graph for the steps an unrolled graph has not run yet."""
+        while self.pending:
+            self.pending -= 1
+            self.graph.replay()
+            self._note()
 
     @property
     def state(self):
@@ -187,6 +204,7 @@ class GraphedStep:
 
     def __call__(self, u, p, n, batch_idx, state):
         if u.numel() != self.B:
+            self.flush()
             return self.tr.train_step(self.tr._features().batch(u, p, n), batch_idx, state)
         for src, dst in ((u, self.u), (p, self.p), (n, self.n)):
             if src is not dst:
@@ -211,10 +229,29 @@ class GraphedStep:
             self.graph = g
             if acc0 is not None:
                 self.gstate["acc"].copy_(acc0)
+        if own and self.unroll > 1 and self.feed is not None:
+            self.pending += 1
+            if self.pending < self.unroll:
+                return self.static_loss
+            if self.graph_n is None:
+                # the same body unroll times in one capture, sharing the one-step graph's memory pool
+                # (the two graphs replay in stream order)
+                gn = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gn, pool=self.graph.pool(), capture_error_mode=_CAPTURE_MODE):
+                    for k in range(self.unroll):
+                        self.static_loss_n = self._body(batch_idx + k, self.gstate, accumulate=True)
+                self.graph_n = gn
+            self.pending = 0
+            self.graph_n.replay()
+            for _ in range(self.unroll):
+                self._note()
+            return self.static_loss_n
         if own:
+            self.flush()
             self.graph.replay()
             self._note()
             return self.static_loss
+        self.flush()
         self.gstate["nan"].copy_(state["nan"])
         self.gstate["acc"].zero_()
         self.graph.replay()
@@ -264,8 +301,10 @@ class GraphedDPStep(GraphedStep):
             ops.defer_counters(False)
         if fused:
             torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
+            ops.loss_side_join()
             tr.grad_hook.pack()
             return None
+        ops.loss_side_join()
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
         if state.get("acc") is None:
@@ -365,6 +404,7 @@ class GraphedDPStep(GraphedStep):
             self._comm_and_b(*replay_b)
             self._note()
             return self.static_loss
+        self.flush()
         self.gstate["nan"].copy_(state["nan"])
         self.gstate["acc"].zero_()
         self.graph.replay()
@@ -522,8 +562,10 @@ class Trainer(AbstractTrainer):
             # the loss sum is never materialised for autograd: each part back-propagates with a
             # cached ones seed; the returned loss is fr_step_book's fp32 sum of the parts
             torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
+            ops.loss_side_join()
             self._finish_step(state)
             return booked
+        ops.loss_side_join()
         loss = sum(parts)
         vec = torch.stack([x.detach().reshape(-1)[0].double() for x in parts])
         if state.get("acc") is None:
@@ -573,7 +615,14 @@ class Trainer(AbstractTrainer):
             accumulate = False
         elif state["acc"].numel() != len(parts):
             return None
-        return book_step(parts, state["acc"], state["nan"], accumulate)
+        side = ops.loss_side_stream()  # a loss op forked the side stream: book there too (joined after the backward)
+        if side is None:
+            return book_step(parts, state["acc"], state["nan"], accumulate)
+        side.wait_stream(torch.cuda.current_stream(parts[0].device))
+        for x in parts:
+            x.record_stream(side)
+        with torch.cuda.stream(side):
+            return book_step(parts, state["acc"], state["nan"], accumulate)
 
     def _ones_like(self, parts):
         cache = self.__dict__.setdefault("_ones_cache", {})
@@ -588,12 +637,15 @@ class Trainer(AbstractTrainer):
             out.append(t)
         return out
 
-    def graphed_step(self, batch_size: int, warmup: int = 3):
+    def graphed_step(self, batch_size: int, warmup: int = 3, unroll: int | None = None):
         """A callable (u, p, n, batch_idx, state) running train_step through captured HIP graphs
-        (data parallel: two graphs with the gradient collectives between them)."""
+        (data parallel: two graphs with the gradient collectives between them; single process:
+        ``unroll`` steps per replay, default config ``cuda_graph_unroll``)."""
         if self.grad_hook is not None and hasattr(self.grad_hook, "communicate"):
             return GraphedDPStep(self, batch_size, warmup)
-        return GraphedStep(self, batch_size, warmup)
+        if unroll is None:
+            unroll = int(self.config["cuda_graph_unroll"] or 1) if "cuda_graph_unroll" in self.config else 1
+        return GraphedStep(self, batch_size, warmup, unroll=unroll)
 
     def new_step_state(self):
         return {"acc": None, "nan": torch.zeros((), dtype=torch.int32, device=torch.device(self.device))}
@@ -619,6 +671,7 @@ class Trainer(AbstractTrainer):
                 step.attach_feed(train_data)
             for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs, feed=step.feed)):
                 loss_batches.append(step(u, p, n, batch_idx, state))
+            step.flush()
         else:
             for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
                 loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))

@@ -213,7 +213,7 @@ _SIGS = {
     "fr_modal_head_grad_numel": (c_int64, []),
     "fr_modal_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
                                   POINTER(c_void_p), c_float, c_void_p, c_void_p, c_int, POINTER(c_void_p),
-                                  c_float, c_float, c_float, c_void_p, c_void_p, c_int64, c_void_p]),
+                                  c_float, c_float, c_float, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "fr_modal_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
                                   POINTER(c_void_p), c_float, c_void_p, c_void_p, c_int, POINTER(c_void_p),
                                   c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -1330,17 +1330,70 @@ class _RegCombine(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         sa, sb, B, w = ctx.meta
+        key = (tuple(sa), tuple(sb), B, w, g.device)
+        if _is_unit(g):  # the trainer's ones seed: the gradients are constants, computed once
+            got = _REG_UNIT_GRADS.get(key)
+            if got is not None:
+                return got[0], got[1], None, None
         g = g.contiguous()
         da = torch.empty(sa, dtype=torch.float32, device=g.device)
         db = torch.empty(sb, dtype=torch.float32, device=g.device)
         native.check(native.lib().fr_reg_combine_bwd(g.data_ptr(), db.numel(), _f(B), _f(w), da.data_ptr(), db.data_ptr(),
                                                      native.stream_of(g)), "fr_reg_combine_bwd")
+        if _is_unit(g) and not torch.cuda.is_current_stream_capturing():
+            _REG_UNIT_GRADS[key] = (da, db)  # read-only from here on (consumers never write a grad input)
         return da, db, None, None
 
 
+_REG_UNIT_GRADS = {}
+
+# FR_LOSS_SIDE=1: the loss bookkeeping -- reg_combine's forward and the trainer's fr_step_book, which
+# only the optimiser's NaN gate and the next step read -- on a side stream forked after the loss terms
+# and joined after the backward, off the head -> backward chain.  Measured slower on MI355X (HealthRec
+# 0.79-0.81 vs 0.755 ms/step, profiles/r4/ab_hr1_*): one more stream than the hardware queues the
+# graph's branches map onto, so unrelated branches queue behind each other.  Default: main stream
+LOSS_SIDE = os.environ.get("FR_LOSS_SIDE", "0") == "1"
+_LOSS_STREAMS = {}
+_LOSS_PENDING = [None]  # (main stream, side stream) with work not yet joined
+
+
+def loss_side_stream(device=None, fork=False):
+    """The loss side stream of this step (``fork``: fork it off the current stream now, creating it
+    on first use); None when off, on the CPU, or outside a trainer step (which joins it: only the
+    trainer's booked steps, under defer_counters, fork it)."""
+    if not LOSS_SIDE or _DETERMINISTIC or not _DEFER[0]:
+        return None
+    if not fork:
+        p = _LOSS_PENDING[0]
+        return p[1] if p is not None else None
+    if device is None or device.type != "cuda":
+        return None
+    s = _LOSS_STREAMS.get(device.index)
+    if s is None:
+        s = _LOSS_STREAMS[device.index] = torch.cuda.Stream(device)
+    main = torch.cuda.current_stream(device)
+    s.wait_stream(main)
+    _LOSS_PENDING[0] = (main, s)
+    return s
+
+
+def loss_side_join() -> None:
+    """The main stream waits for the loss side stream's work (after the backward is issued)."""
+    p, _LOSS_PENDING[0] = _LOSS_PENDING[0], None
+    if p is not None:
+        p[0].wait_stream(p[1])
+
+
 def reg_combine(a, b, B, w):
-    """``w * (a + b.sum() / B)`` for a [1] and b [k] fp32 device tensors in one launch per direction."""
-    return _RegCombine.apply(a, b, B, w)
+    """``w * (a + b.sum() / B)`` for a [1] and b [k] fp32 device tensors in one launch per direction
+    (forward on the loss side stream when enabled: its value feeds only the step's bookkeeping)."""
+    s = loss_side_stream(a.device, fork=True) if a.is_cuda else None
+    if s is None:
+        return _RegCombine.apply(a, b, B, w)
+    a.record_stream(s)
+    b.record_stream(s)
+    with torch.cuda.stream(s):
+        return _RegCombine.apply(a, b, B, w)
 
 
 # ----------------------------------------------------------------------------- embedding
@@ -2083,6 +2136,22 @@ def health_kd_loss(hin, know, rows, labels, mlp, kd_threshold, w_health, w_kd):
 
 
 # ----------------------------------------------------------------------------- fused loss head
+_TICKETS = {}
+# FR_HEAD_TICKET=1: the modal head's finalize run by the forward's last-arriving block instead of its
+# own launch.  Measured ~5 us/step slower on MI355X (profiles/r4/ab_hr2_*: every block's fence +
+# arrival atomic and the serial finalize at the tail cost more than the launch they save): off
+HEAD_TICKET = os.environ.get("FR_HEAD_TICKET", "0") == "1"
+
+
+def _arrival_ticket(device) -> torch.Tensor:
+    """A zero int32 per device for kernels whose last-arriving block finalises (the kernel resets it
+    to 0): one allocation and fill, ever, not per step.  Launches sharing it must be stream-ordered."""
+    t = _TICKETS.get(device)
+    if t is None:
+        t = _TICKETS[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return t
+
+
 class _ModalHead(torch.autograd.Function):
     """fr_modal_head_fwd / _bwd: HealthRec's target attentions + normalize heads feeding the health
     MLP / BCE and KD cosine terms, one node (see include/fr_engine.h)."""
@@ -2101,7 +2170,8 @@ class _ModalHead(torch.autograd.Function):
             native.check(lib.fr_modal_head_fwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
                                                int(pad_id), n, L, lnp, float(eps), rows.data_ptr(), labels.data_ptr(), H,
                                                mlp, float(thr), float(w_h), float(w_k), out.data_ptr(), part.data_ptr(),
-                                               part.numel(), native.stream_of(enc)), "fr_modal_head_fwd")
+                                               part.numel(), _arrival_ticket(enc.device).data_ptr() if HEAD_TICKET else None,
+                                               native.stream_of(enc)), "fr_modal_head_fwd")
         ctx.save_for_backward(enc, query, ids, num, rows, labels, ga, ba, gb, bb, w1, b1, w2, b2)
         ctx.out, ctx.cfg = out, (int(pad_id), float(eps), float(thr), float(w_h), float(w_k))
         return out[0], out[1]

@@ -143,9 +143,12 @@ class DeviceFeed:
         self.offs = torch.arange(self.B, dtype=torch.int64, device=device)
         self._pos = torch.empty(self.B, dtype=torch.int64, device=device)
         self._idx = torch.empty(self.B, dtype=torch.int64, device=device)
+        self.on_stage = None  # called before a new epoch is staged (a graphed step's pending steps)
 
     def stage(self, perm_d, negs_d):
         from . import ops
+        if self.on_stage is not None:
+            self.on_stage()
         ops.drop_pending(self.cursor)
         self.perm.copy_(perm_d)
         self.negs.copy_(negs_d)

@@ -36,6 +36,7 @@ struct HeadArgs {
   float thr, wh, wk;
   float* out;                 // [3]: w_h * health, w_k * kd term, kd - thr (the gate)
   float* part;                // forward: [nblk, 2]; backward: [nblk, NPART_ROW]
+  int32_t* ticket;            // forward: zero-initialised arrival counter (the last block finalises; reset to 0)
   const float *gh, *gk;       // upstream gradients of out[0], out[1] (device scalars)
   float* drows;               // [n, 64]
 };
@@ -55,6 +56,8 @@ __device__ __forceinline__ float2 head_item_fwd(const HeadArgs& a, const float* 
   const float n1 = fmaxf(sqrtf(wsum(know * know)), kCosEps), n2 = fmaxf(sqrtf(wsum(r * r)), kCosEps);
   return make_float2(item_bce, wsum((know / n1) * (r / n2)));
 }
+
+__device__ __forceinline__ void head_final(const HeadArgs& a, int nblk, int j);
 
 template <int L>
 __global__ __launch_bounds__(NT) void modal_head_fwd_kernel(HeadArgs a) {
@@ -88,12 +91,24 @@ __global__ __launch_bounds__(NT) void modal_head_fwd_kernel(HeadArgs a) {
     a.part[2 * blockIdx.x] = sbce;
     a.part[2 * blockIdx.x + 1] = scos;
   }
+  if (a.ticket) {  // the last block to arrive sums every block's partials (the final kernel's work)
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+      __threadfence();  // this block's partials before its arrival
+      last = atomicAdd(a.ticket, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+      __threadfence();  // every block's partials visible to this one
+      if (threadIdx.x < 64) head_final(a, (int)gridDim.x, threadIdx.x);
+      if (threadIdx.x == 0) a.ticket[0] = 0;  // ready for the next launch (graph replays)
+    }
+  }
 }
 
 // the loss terms from the block partials (lane j: blocks j, j + 64, ... in that order), one
-// fixed-order wave sum each
-__global__ __launch_bounds__(64) void modal_head_final_kernel(HeadArgs a, int nblk) {
-  const int j = threadIdx.x;
+// fixed-order wave sum each (one wave)
+__device__ __forceinline__ void head_final(const HeadArgs& a, int nblk, int j) {
   float sbce = 0.f, scos = 0.f;
   for (int b = j; b < nblk; b += 64) {
     sbce += a.part[2 * b];
@@ -106,6 +121,8 @@ __global__ __launch_bounds__(64) void modal_head_final_kernel(HeadArgs a, int nb
   a.out[1] = a.wk * fmaxf(0.f, x);
   a.out[2] = x;
 }
+
+__global__ __launch_bounds__(64) void modal_head_final_kernel(HeadArgs a, int nblk) { head_final(a, nblk, threadIdx.x); }
 
 template <int L>
 __global__ __launch_bounds__(NT) void modal_head_bwd_kernel(HeadArgs a) {
@@ -290,18 +307,21 @@ extern "C" int fr_modal_head_fwd(const float* d_enc, const float* d_query, const
                                  int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps,
                                  const float* d_rows, const float* d_labels, int H, const float* const* d_mlp,
                                  float kd_threshold, float w_health, float w_kd, float* d_out, float* d_partials,
-                                 int64_t partial_floats, void* stream) {
+                                 int64_t partial_floats, int32_t* d_ticket, void* stream) {
   HeadArgs a{};
   int rc = fill(a, d_enc, d_query, d_ids, d_num, pad_id, n_items, L, d_ln, eps, d_rows, d_labels, H, d_mlp,
                 kd_threshold, w_health, w_kd, d_out);
   if (rc) return rc;
   FR_REQUIRE(d_partials && partial_floats >= fr_modal_head_partials(n_items, 0), "partial buffer too small");
   a.part = d_partials;
+  a.ticket = d_ticket;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   rc = dispatch(a, L, false, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(modal_head_final_kernel, dim3(1), dim3(64), 0, s, a, (int)fr::ceil_div(n_items, WAVES));
-  FR_LAUNCH_CHECK();
+  if (!d_ticket) {
+    hipLaunchKernelGGL(modal_head_final_kernel, dim3(1), dim3(64), 0, s, a, (int)fr::ceil_div(n_items, WAVES));
+    FR_LAUNCH_CHECK();
+  }
   return FR_OK;
 }
 

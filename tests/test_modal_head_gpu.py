@@ -109,6 +109,21 @@ def test_modal_head_equals_separate_ops(cuda):
         _close(ga, gb, 1e-5, name, 0)
 
 
+@pytest.mark.parametrize("ticket", [False, True])
+def test_modal_head_finalize_forms_equal(cuda, ticket, monkeypatch):
+    """The finalize as its own launch or run by the forward's last-arriving block (FR_HEAD_TICKET):
+    the same fixed-order sums, bit-identical losses; repeated launches (the ticket resets itself)."""
+    from FoodRec.engine import ops
+    pad_id = 211
+    x = _inputs(1021, 20, 7, pad_id, 3)
+    monkeypatch.setattr(ops, "HEAD_TICKET", False)
+    ref = _engine(x, pad_id, 0.25, 0.1, 0.05, 1.0, 1.0, cuda)
+    monkeypatch.setattr(ops, "HEAD_TICKET", ticket)
+    for _ in range(3):
+        got = _engine(x, pad_id, 0.25, 0.1, 0.05, 1.0, 1.0, cuda)
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
 def test_modal_head_deterministic(cuda):
     pad_id = 77
     x = _inputs(300, 20, 5, pad_id, 9)

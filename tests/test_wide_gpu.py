@@ -169,7 +169,7 @@ def test_wide_graphed_steps_match_reference(cuda, name):
     g, cfg, model, tr, sampler = _setup(cuda, name, graph=True)
     steps = int(g["steps"])
     model.train()
-    step = tr.graphed_step(int(g["batch_size"]), warmup=1)
+    step = tr.graphed_step(int(g["batch_size"]), warmup=1, unroll=1)
     feed = step.attach_feed(sampler)
     state = step.state
     prev = None
@@ -184,4 +184,29 @@ def test_wide_graphed_steps_match_reference(cuda, name):
         prev = acc
         np.testing.assert_allclose(got, g[f"step{k}/loss"], rtol=5e-5 if k == 0 else 3e-3, err_msg=str(k))
     assert step.graph is not None, "the step was never captured"
+    _check_final(g, cfg, model, steps)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_wide_unrolled_graph_steps_match_reference(cuda, name):
+    """GraphedStep(unroll=2): the captured graph holds two consecutive steps (each gathering its own
+    batch from the staged epoch); pending steps are flushed through the one-step graph.  The loss sums
+    over all steps and the final parameters match the reference's float64 run."""
+    g, cfg, model, tr, sampler = _setup(cuda, name, graph=True)
+    steps = int(g["steps"])
+    model.train()
+    step = tr.graphed_step(int(g["batch_size"]), warmup=1, unroll=2)
+    feed = step.attach_feed(sampler)
+    state = step.state
+    it = sampler.epoch(out=step.inputs, feed=feed)
+    for k in range(steps):
+        u, p, n = next(it)
+        step(u, p, n, k, state)
+    step.flush()
+    assert step.pending == 0
+    if steps >= 3:
+        assert step.graph_n is not None, "the unrolled graph was never captured"
+    got = state["acc"].cpu().numpy()
+    want = sum(np.asarray(g[f"step{k}/loss"], dtype=np.float64) for k in range(steps))
+    np.testing.assert_allclose(got, want, rtol=3e-3)
     _check_final(g, cfg, model, steps)
