@@ -298,12 +298,13 @@ def main():
             roofline = {**common, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
                         "flops_per_launch": fl, "bytes_per_launch": int(d["bytes_per_launch"]),
-                        "region_kernels": ("enc_bwd_kernel<20> per layer + one enc_reduce_kernel (the ordered "
-                                           "weight-gradient reduction) per step: the top layer's reduction is "
-                                           "folded into the bottom layer's enc_bwd_kernel launch, the bottom "
-                                           "layer's own runs after it; avg_launch_ms = one fr_encoder_bwd call "
-                                           "averaged over the two layers"
+                        "region_kernels": ("enc_bwd_kernel<20>, one launch per layer (avg over the two layers); "
+                                           "each layer's ordered weight-gradient reduction (enc_reduce_kernel) "
+                                           "is issued at the end of the backward (autograd final callback) and "
+                                           "timed as kernels.encoder_reduce"
                                            if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
+                        "reduce_ms_per_launch": (round(kern["encoder_reduce"]["avg_ms"], 4)
+                                                 if dom_name.endswith("bwd") and "encoder_reduce" in kern else None),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
         else:
@@ -331,6 +332,7 @@ def main():
                 "note": "Allrecipes-shape X tables (<=29 MB) are Infinity-Cache resident"}
     kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "per_step_ms": round(v["total_ms"] / ksteps, 4),
                    "gbps": round(v["gbps"], 1)} for k, v in kern.items()}
+    graph_unroll = (graphed.unroll if world == 1 and not dp1 else 1) if graphed is not None else 0
     kernels["_timing"] = {"step_execution": "hip_graph_replay" if use_graph else "eager",
                           "kernel_pass": f"{ksteps} eager steps, HIP events on the launch stream",
                           "eager_ms_per_step": round(eager_elapsed / ksteps * 1e3, 4)}
@@ -386,8 +388,7 @@ def main():
                            "dataset": "Allrecipes-shape synthetic (U=68768, I=45630, train=677054)",
                            "embedding_size": 64, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                            "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single"),
-                           "graph_steps_per_replay": (graphed.unroll if graphed is not None and world == 1 and not dp1
-                                                      else (1 if graphed is not None else 0))},
+                           "graph_steps_per_replay": graph_unroll},
                 "roofline": roofline, "ranks": ranks, "scaling_config4": c4_scaling, "step_bytes": step_fig,
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
@@ -406,7 +407,8 @@ def main():
 
 # the kernels each engine timing region launches on HEAD (tools/pmc_regions.py REGION_KERNELS): a
 # committed PMC file sampled from other kernels is stale and is not used
-REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel", "enc_reduce_kernel"], "encoder_fwd": ["enc_fwd_kernel"],
+REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel"], "encoder_reduce": ["enc_reduce_kernel"],
+                  "encoder_fwd": ["enc_fwd_kernel"],
                   "spmm": ["spmm_plain16_kernel"], "spmm_masked": ["spmm_sparse_kernel"],
                   "spmm_rows": ["spmm_rows_kernel"], "adam": ["adam_kernel<false>"],
                   "adam_rows": ["adam_lazy_rows_kernel<false>"]}

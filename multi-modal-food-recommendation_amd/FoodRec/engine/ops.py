@@ -1744,6 +1744,11 @@ def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
 # slower per step than a separate reduction: the 200 KB per workgroup of partial reads at the launch
 # start are not overlapped); default: every layer reduces its own partials
 ENCODER_FOLD = os.environ.get("FR_ENCODER_FOLD", "0") == "1"
+# FR_ENCODER_LATE_REDUCE=0: each layer's ordered weight-gradient reduction right after its backward
+# launch.  Default: the layers' backward launches back to back and their reductions issued by an
+# autograd final callback -- the weight gradients feed only the optimiser, so the reductions leave the
+# input-gradient chain (encoder -> ingredient gather backward) and run beside the step's tail
+ENCODER_LATE_REDUCE = os.environ.get("FR_ENCODER_LATE_REDUCE", "1") != "0"
 
 
 class _EncoderStack(torch.autograd.Function):
@@ -1801,6 +1806,11 @@ class _EncoderStack(torch.autograd.Function):
         nparts = lib.fr_encoder_partials(NS, L)
         grads = [None] * nl
         prev = None  # (partials, gradient) of the layer above, reduced by this layer's launch
+        # late reductions: only when the returned gradients become the parameters' .grad as they are
+        # (no accumulation reads them before the callback has written them)
+        late = (ENCODER_LATE_REDUCE and not ENCODER_FOLD and torch.is_grad_enabled() is False
+                and all(p.grad is None for p in flat))
+        pending = []
         for k in range(nl - 1, -1, -1):
             h, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used = ctx.saved[k]
             cfg = cfgs[k]
@@ -1814,12 +1824,24 @@ class _EncoderStack(torch.autograd.Function):
                     g.data_ptr(), h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
                     seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(), fact.data_ptr(),
                     dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
-                    grad.data_ptr() if (k == 0 or not ENCODER_FOLD) else None,
+                    None if late else (grad.data_ptr() if (k == 0 or not ENCODER_FOLD) else None),
                     part.data_ptr(), nparts, prev[0].data_ptr() if prev else None,
                     prev[1].data_ptr() if prev else None, native.stream_of(g)), "fr_encoder_bwd")
             grads[k] = grad
             prev = (part, grad) if ENCODER_FOLD else None
+            if late:
+                pending.append((part, grad))
             g = dx
+        if pending:
+            stream = native.stream_of(g)
+
+            def _reduce_late(pending=pending, NS=NS, L=L, stream=stream):
+                for part, grad in pending:
+                    with profiling.region("encoder_reduce", 4 * (part.numel() + grad.numel())):
+                        native.check(native.lib().fr_encoder_reduce(part.data_ptr(), NS, L, grad.data_ptr(), stream),
+                                     "fr_encoder_reduce")
+
+            torch.autograd.Variable._execution_engine.queue_callback(_reduce_late)
         out = []
         for k in range(nl):
             params = flat[12 * k:12 * (k + 1)]

@@ -125,33 +125,40 @@ __global__ __launch_bounds__(256) void wgrad_slab_multi_kernel(int64_t ldy, cons
              blockIdx.y);
 }
 
-// dW[n,k] = sum over slabs (in order, 4 interleaved slab lanes combined in fixed order)
+// dW[n,k] = sum over slabs (in order, 4 interleaved slab lanes combined in fixed order).  A thread owns
+// 4 consecutive outputs (one float4 per slab: 1 KiB per wave-load), a block 64 float4 columns; slab
+// group g sums slabs g, g + 4, ... with 4 loads in flight, the 4 groups added in fixed order
 __device__ __forceinline__ void wgrad_reduce(const float* __restrict__ part, int64_t slabs, int N, int K,
                                              float* __restrict__ dW, int64_t ldw, const float* __restrict__ pdb,
                                              float* __restrict__ db, int64_t bx) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   const int e_local = threadIdx.x % 64, g = threadIdx.x / 64;
-  const int64_t NK = (int64_t)N * K;
-  const int64_t total = NK + (db ? N : 0);
+  const int64_t NK4 = (int64_t)N * K / 4;  // K % 4 == 0: a float4 never straddles two rows of dW
+  const int64_t total4 = NK4 + (db ? N / 4 : 0);
   const int64_t e = bx * 64 + e_local;
-  float s = 0.f;
-  if (e < total) {
-    const float* src = e < NK ? part + e : pdb + (e - NK);
-    const int64_t stride = e < NK ? NK : N;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total4) {
+    const float4* src = e < NK4 ? reinterpret_cast<const float4*>(part) + e
+                                : reinterpret_cast<const float4*>(pdb) + (e - NK4);
+    const int64_t stride = e < NK4 ? NK4 : N / 4;
     int64_t sl = g;
     for (; sl + 12 < slabs; sl += 16) {  // four loads in flight per lane
-      const float v0 = src[sl * stride], v1 = src[(sl + 4) * stride];
-      const float v2 = src[(sl + 8) * stride], v3 = src[(sl + 12) * stride];
-      s += v0; s += v1; s += v2; s += v3;
+      const float4 v0 = src[sl * stride], v1 = src[(sl + 4) * stride];
+      const float4 v2 = src[(sl + 8) * stride], v3 = src[(sl + 12) * stride];
+      s = f4_add(s, v0); s = f4_add(s, v1); s = f4_add(s, v2); s = f4_add(s, v3);
     }
-    for (; sl < slabs; sl += 4) s += src[sl * stride];
+    for (; sl < slabs; sl += 4) s = f4_add(s, src[sl * stride]);
   }
   red[g][e_local] = s;
   __syncthreads();
-  if (g == 0 && e < total) {
-    const float r = ((red[0][e_local] + red[1][e_local]) + red[2][e_local]) + red[3][e_local];
-    if (e < NK) dW[(e / K) * ldw + (e % K)] = r;
-    else db[e - NK] = r;
+  if (g == 0 && e < total4) {
+    const float4 r = f4_add(f4_add(f4_add(red[0][e_local], red[1][e_local]), red[2][e_local]), red[3][e_local]);
+    if (e < NK4) {
+      const int64_t o = 4 * e;
+      *reinterpret_cast<float4*>(dW + (o / K) * ldw + (o % K)) = r;
+    } else {
+      *reinterpret_cast<float4*>(db + 4 * (e - NK4)) = r;
+    }
   }
 }
 
@@ -183,6 +190,8 @@ static int wgrad_impl(const float* d_dy, int64_t ldy, const int64_t* d_ids, cons
   FR_REQUIRE(d_dy && d_x && d_dw && ldy >= N && ldx >= K && ldw >= K && ldy % 4 == 0 && ldx % 4 == 0,
              "bad operands");
   FR_REQUIRE(fr::aligned16(d_dy) && fr::aligned16(d_x), "dY and X must be 16-byte aligned");
+  FR_REQUIRE(fr::aligned16(d_dw) && ldw % 4 == 0 && (!d_db || fr::aligned16(d_db)),
+             "dW (ld % 4 == 0) and db must be 16-byte aligned");
   FR_REQUIRE(d_workspace && fr::aligned16(d_workspace) && workspace_bytes >= fr_linear_wgrad_workspace(M, N, K),
              "workspace too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -194,8 +203,8 @@ static int wgrad_impl(const float* d_dy, int64_t ldy, const int64_t* d_ids, cons
   hipLaunchKernelGGL(wgrad_slab_kernel, dim3((unsigned)slabs, (unsigned)(ntiles * ktiles)), dim3(256), 0, s, d_dy,
                      ldy, d_x, ldx, d_ids, M, N, K, ktiles, part, d_db ? pdb : nullptr);
   FR_LAUNCH_CHECK();
-  const int64_t total = (int64_t)N * K + (d_db ? N : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)fr::ceil_div(total, 64)), dim3(256), 0, s, part, slabs, N,
+  const int64_t total4 = ((int64_t)N * K + (d_db ? N : 0)) / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)fr::ceil_div(total4, 64)), dim3(256), 0, s, part, slabs, N,
                      K, d_dw, ldw, pdb, d_db);
   FR_LAUNCH_CHECK();
   return FR_OK;
@@ -240,8 +249,9 @@ extern "C" int fr_linear_wgrad_gather_multi(const float* d_dy, int64_t ldy, cons
   int64_t blocks = 0;
   for (int t = 0; t < n_tab; ++t) {
     FR_REQUIRE(K[t] > 0 && K[t] % 4 == 0 && d_x[t] && d_dw[t] && ldx[t] >= K[t] && ldx[t] % 4 == 0 && ldw[t] >= K[t] &&
-                   fr::aligned16(d_x[t]),
-               "bad table operands");
+                   fr::aligned16(d_x[t]) && fr::aligned16(d_dw[t]) && ldw[t] % 4 == 0 &&
+                   (!d_db || !d_db[t] || fr::aligned16(d_db[t])),
+               "bad table operands (dW / db 16-byte aligned, ld % 4 == 0)");
     T.dy[t] = d_dy + (int64_t)t * N;
     T.X[t] = d_x[t];
     T.ldx[t] = ldx[t];
@@ -255,7 +265,7 @@ extern "C" int fr_linear_wgrad_gather_multi(const float* d_dy, int64_t ldy, cons
     T.ldw[t] = ldw[t];
     T.db[t] = d_db ? d_db[t] : nullptr;
     T.red_start[t] = blocks;
-    blocks += fr::ceil_div((int64_t)N * K[t] + (T.db[t] ? N : 0), 64);
+    blocks += fr::ceil_div(((int64_t)N * K[t] + (T.db[t] ? N : 0)) / 4, 64);
     max_tiles = std::max(max_tiles, T.tiles[t]);
   }
   T.red_start[n_tab] = blocks;
