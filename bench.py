@@ -298,13 +298,10 @@ def main():
             roofline = {**common, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
                         "flops_per_launch": fl, "bytes_per_launch": int(d["bytes_per_launch"]),
-                        "region_kernels": ("enc_bwd_kernel<20>, one launch per layer (avg over the two layers); "
-                                           "each layer's ordered weight-gradient reduction (enc_reduce_kernel) "
-                                           "is issued at the end of the backward (autograd final callback) and "
-                                           "timed as kernels.encoder_reduce"
+                        "region_kernels": ("enc_bwd_kernel<20> + its layer's ordered weight-gradient reduction "
+                                           "(enc_reduce_kernel), one fr_encoder_bwd call per layer; avg_launch_ms "
+                                           "averages the two layers' calls"
                                            if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
-                        "reduce_ms_per_launch": (round(kern["encoder_reduce"]["avg_ms"], 4)
-                                                 if dom_name.endswith("bwd") and "encoder_reduce" in kern else None),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
         else:
@@ -407,8 +404,7 @@ def main():
 
 # the kernels each engine timing region launches on HEAD (tools/pmc_regions.py REGION_KERNELS): a
 # committed PMC file sampled from other kernels is stale and is not used
-REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel"], "encoder_reduce": ["enc_reduce_kernel"],
-                  "encoder_fwd": ["enc_fwd_kernel"],
+REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel", "enc_reduce_kernel"], "encoder_fwd": ["enc_fwd_kernel"],
                   "spmm": ["spmm_plain16_kernel"], "spmm_masked": ["spmm_sparse_kernel"],
                   "spmm_rows": ["spmm_rows_kernel"], "adam": ["adam_kernel<false>"],
                   "adam_rows": ["adam_lazy_rows_kernel<false>"]}

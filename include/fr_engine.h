@@ -545,6 +545,24 @@ int fr_modal_head_fwd(const float* d_enc, const float* d_query, const int64_t* d
                       const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,
                       float w_kd, float* d_out, float* d_partials, int64_t partial_floats, int32_t* d_ticket,
                       void* stream);
+/* The forward's per-item kernel alone (block partials only; d_out untouched), and HealthRec's loss
+ * finalize as one launch: the head's finalize (d_out[0..2] as fr_modal_head_fwd writes them), the EmbLoss
+ * ingredient norms from fr_gather_norms_fwd's partials (d_nrm, as fr_reg_combine_norms_fwd), d_reg =
+ * w_reg * (d_emb3[0] + (nrm[0] + nrm[1]) / B), and, when d_acc is given, the step's bookkeeping over
+ * the parts [d_mf, d_out[0], d_out[1], d_reg] exactly as fr_step_book (counters advanced, fp32 sum to
+ * d_loss, NaN flag).  The loss chain after the encoder is then 4 launches: items, finalize, backward,
+ * reduce (models/cikm_model.py:245-279 + trainer.py:183-193).  d_head_partials NULL: no head finalize;
+ * d_norm_partials NULL: no norms / reg; the bookkeeping needs both. */
+int fr_modal_head_fwd_items(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
+                            int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps,
+                            const float* d_rows, const float* d_labels, int H, const float* const* d_mlp,
+                            float kd_threshold, float w_health, float w_kd, float* d_partials, int64_t partial_floats,
+                            void* stream);
+int fr_healthrec_loss_finalize(const float* d_head_partials, int64_t n_items, float kd_threshold, float w_health,
+                               float w_kd, float* d_out, const float* d_norm_partials, int64_t n_norm_rows,
+                               const float* d_emb3, float B, float w_reg, float* d_nrm, float* d_reg,
+                               const float* d_mf, double* d_acc, int accumulate, int32_t* d_nan,
+                               int64_t* const* d_counters, int n_counters, float* d_loss, void* stream);
 int fr_modal_head_bwd(const float* d_enc, const float* d_query, const int64_t* d_ids, const int64_t* d_num,
                       int64_t pad_id, int64_t n_items, int L, const float* const* d_ln, float eps, const float* d_rows,
                       const float* d_labels, int H, const float* const* d_mlp, float kd_threshold, float w_health,
@@ -641,12 +659,18 @@ int fr_linear_wgrad_gather_multi(const float* d_dy, int64_t ldy, const int64_t* 
  *   nrm[1] = ||E[half:]||_F (block partials from fr_gather_norms_partials, fixed-order sums).
  * fr_norms_bwd_coef: out[i] = G[i] + [ids[i] != pad] * (gn[h] / nrm[h]) * E[i], h = (i >= half),
  *   gn[1] read at d_gn + gn_stride (0 for a broadcast gradient); zero where a norm is zero.
+ * fr_gather_norms_fwd with d_nrm NULL leaves the norms' finalize to fr_reg_combine_norms_fwd: the same
+ *   fixed-order sums (bit-identical nrm) plus, when d_out is given, HealthRec's EmbLoss assembly
+ *   d_out[0] = w * (d_a[0] + (nrm[0] + nrm[1]) / B) (fr_reg_combine_fwd's arithmetic) in one launch,
+ *   issued where the loss needs it instead of before the encoder.  n = the gather's row count.
  * ------------------------------------------------------------------------------------------ */
 int64_t fr_gather_norms_partials(int64_t n);
 int fr_gather_norms_fwd(const int64_t* d_ids, int64_t n, int64_t half, const float* d_w, int64_t ldw, float* d_e,
                         float* d_partials, int64_t partial_floats, float* d_nrm, void* stream);
 int fr_norms_bwd_coef(const int64_t* d_ids, int64_t n, int64_t half, int64_t pad, const float* d_g, const float* d_e,
                       const float* d_gn, int64_t gn_stride, const float* d_nrm, float* d_out, void* stream);
+int fr_reg_combine_norms_fwd(const float* d_a, const float* d_partials, int64_t n, float B, float w, float* d_nrm,
+                             float* d_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Host-side readers of the reference's on-disk interaction formats (no GPU).

@@ -294,10 +294,13 @@ class GraphedDPStep(GraphedStep):
             pre = self.feed.fill(self.u, self.p, self.n, feats if not feats.ssl else None)
         tr.optimizer.zero_grad()
         try:
+            ops.book_request(state, accumulate)
             losses = tr.model.calculate_loss(feats.batch(self.u, self.p, self.n, pre=pre))
+            ops.finalize_pending()
             parts = losses if isinstance(losses, tuple) else (losses,)
             fused = tr._book_fused(state, parts, accumulate) is not None
         finally:
+            ops.book_taken()
             ops.defer_counters(False)
         if fused:
             torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
@@ -553,10 +556,14 @@ class Trainer(AbstractTrainer):
         second_inter = copy.copy(interaction) if (self.mg and batch_idx % self.beta == 0) else None
         ops.defer_counters(True)  # device step counters advance in the step's fr_step_book launch
         try:
+            if second_inter is None:
+                ops.book_request(state, accumulate)  # a fused loss op may book the step in its own launch
             losses = loss_func(interaction)
+            ops.finalize_pending()
             parts = losses if isinstance(losses, tuple) else (losses,)
             booked = self._book_fused(state, parts, accumulate) if second_inter is None else None
         finally:
+            ops.book_taken()  # (clears a request nothing answered)
             ops.defer_counters(False)  # (applies the increments eagerly when the step was not booked)
         if booked is not None:
             # the loss sum is never materialised for autograd: each part back-propagates with a
@@ -606,6 +613,11 @@ class Trainer(AbstractTrainer):
         of every loss part) and the sticky NaN flag of sum(parts).  Returns the step's loss (the
         fp32 sum, a device scalar), or None when it does not apply (CPU, more than 8 parts,
         non-fp32 or non-scalar parts)."""
+        done = ops.book_taken()
+        if done is not None:  # a fused loss op booked the step in its launch (ops.healthrec_loss_finalize)
+            if len(done[0]) != len(parts) or any(a is not b for a, b in zip(done[0], parts)):
+                raise RuntimeError("a loss op booked other loss parts than calculate_loss returned")
+            return done[1]
         if not (len(parts) <= 8 and all(torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32
                                           and x.numel() == 1 and x.is_contiguous() and x.requires_grad
                                           for x in parts)):

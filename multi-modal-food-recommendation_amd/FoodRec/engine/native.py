@@ -84,6 +84,7 @@ _SIGS = {
     "fr_bpr_fwd_ex": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                               c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                               c_int64, c_void_p, c_int64, c_void_p]),
+    "fr_reg_combine_norms_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "fr_reg_combine_fwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p]),
     "fr_reg_combine_bwd": (c_int, [c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "fr_score_segments": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
@@ -214,6 +215,12 @@ _SIGS = {
     "fr_modal_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
                                   POINTER(c_void_p), c_float, c_void_p, c_void_p, c_int, POINTER(c_void_p),
                                   c_float, c_float, c_float, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "fr_modal_head_fwd_items": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
+                                        POINTER(c_void_p), c_float, c_void_p, c_void_p, c_int, POINTER(c_void_p),
+                                        c_float, c_float, c_float, c_void_p, c_int64, c_void_p]),
+    "fr_healthrec_loss_finalize": (c_int, [c_void_p, c_int64, c_float, c_float, c_float, c_void_p, c_void_p, c_int64,
+                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                           c_void_p, POINTER(c_void_p), c_int, c_void_p, c_void_p]),
     "fr_modal_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
                                   POINTER(c_void_p), c_float, c_void_p, c_void_p, c_int, POINTER(c_void_p),
                                   c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

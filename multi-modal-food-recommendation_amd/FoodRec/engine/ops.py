@@ -1186,6 +1186,90 @@ class _GraphBpr(torch.autograd.Function):
         return (d_user, d_item, d_ingre) + (None,) * 11
 
 
+UI_BPR = os.environ.get("FR_UI_BPR", "1") != "0"  # FR_UI_BPR=0: CLUSSL's UI layer + BPR unfused
+
+
+class _UiBpr(torch.autograd.Function):
+    """One UI propagation layer + BPR + EmbLoss as one node (CLUSSL, pricai_modelx.py:226-267 with
+    n_ui_layers = 1): the propagation of [user ; item_hi] evaluated at the batch rows only (the loss
+    reads nothing else), BPR on them, EmbLoss on the ego rows (user_w, item_w) times w_emb.  Backward:
+    the batch rows marked and zeroed in a persistent upstream buffer, the BPR scatter into it, the UI
+    backward from those rows only (fr_spmm_sparse_upstream) straight into d user_w and d item_hi,
+    then fr_graph_bpr_finish (unmark, the ego rows' EmbLoss gradient).  Replaces the full-graph
+    propagation forward and backward, the dense zero-filled upstream and the split / accumulation
+    glue of propagate_mean + bpr_emb_loss."""
+
+    @staticmethod
+    def forward(ctx, user_w, item_hi, item_w, u, p, n, ui_adj, gamma, w_emb):
+        U, I = user_w.shape[0], item_hi.shape[0]
+        dev = user_w.device
+        u, p, n = (x.to(torch.int64).contiguous() for x in (u, p, n))
+        rows = [(u, 0), (p, U), (n, U)]
+        ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
+        spmm_ex(ui_adj, user_w, item_hi, U, Y2=ui_all, alpha=0.5, A1=user_w, A1_hi=item_hi, beta1=0.5, rows=rows,
+                region="spmm_rows")
+        B = int(u.numel())
+        lib = native.lib()
+        ws = native.workspace(lib.fr_bpr_workspace(B), dev)
+        out = torch.empty(5, dtype=torch.float32, device=dev)
+        items = ui_all[U:]
+        native.check(lib.fr_bpr_fwd_ex(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
+                                       item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                       _f(gamma), _f(w_emb), out.data_ptr(), None, 0, ws.data_ptr(), ws.numel(),
+                                       native.stream_of(user_w)), "fr_bpr_fwd_ex")
+        ctx.save_for_backward(user_w, item_w, ui_all, u, p, n)
+        ctx.meta = (ui_adj, float(gamma), float(w_emb), ws, U, I, tuple(item_hi.shape))
+        return out[0], out[4:5]
+
+    @staticmethod
+    def backward(ctx, g_mf, g_emb):
+        user_w, item_w, ui_all, u, p, n = ctx.saved_tensors
+        ui_adj, gamma, w_emb, ws, U, I, hi_shape = ctx.meta
+        dev = user_w.device
+        B = int(u.numel())
+        lib = native.lib()
+        s = native.stream_of(user_w)
+        gm = None if g_mf is None or _is_unit(g_mf) else g_mf.float().contiguous()
+        ge = None if g_emb is None or _is_unit(g_emb) else g_emb.float().contiguous()
+        dUI = _persistent(ui_adj, ("g_ui", str(dev)), lambda: torch.empty(U + I, 64, device=dev))
+        mask = _persistent(ui_adj, ("mask", str(dev)), lambda: torch.zeros(U + I, dtype=torch.uint8, device=dev))
+        bits = _persistent(ui_adj, ("bits", str(dev)),
+                           lambda: torch.zeros((U + I + 31) // 32, dtype=torch.int32, device=dev))
+        rows = [(u, 0), (p, U), (n, U)]
+        rows_mark(mask, rows, 1, zero=dUI, bits=bits)
+        with profiling.region("bpr_bwd", 0):
+            native.check(lib.fr_bpr_bwd(ui_all.data_ptr(), 64, ui_all[U:].data_ptr(), 64, user_w.data_ptr(), 64,
+                                        item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(gamma),
+                                        _f(0.0 if g_mf is None else 1.0), _f(0.0), native.ptr(gm), dUI.data_ptr(),
+                                        dUI[U:].data_ptr(), None, None, 0, ws.data_ptr(), ws.numel(), s), "fr_bpr_bwd")
+        d_user = grad_buffer(user_w)
+        d_hi = torch.empty(hi_shape, dtype=torch.float32, device=dev)
+        spmm_sparse_upstream(ui_adj, bits, dUI, d_user, d_hi, U, alpha=0.5, beta1=0.5)
+        d_item = torch.zeros_like(item_w)  # the ego item rows' EmbLoss gradient only
+        with profiling.region("bpr_bwd", 0):
+            native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
+                                                 u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
+                                                 _f(0.0 if g_emb is None else w_emb), native.ptr(ge), d_user.data_ptr(),
+                                                 d_item.data_ptr(), None, 0, bits.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                 s), "fr_graph_bpr_finish")
+        return d_user, d_hi, d_item, None, None, None, None, None, None
+
+
+def ui_bpr(ui_adj, user_w, item_hi, item_w, u, p, n, gamma: float = 1e-10, w_emb: float = 1.0):
+    """(BPRLoss, w_emb * EmbLoss) of ``propagate_mean(ui_adj, cat([user_w, item_hi]), 1)`` at
+    (u, U + p, U + n) with EmbLoss over the ego rows (user_w[u], item_w[p], item_w[n]) -- one node
+    (_UiBpr) when the sparse-upstream backward applies, else propagate_mean_split + bpr_emb_loss."""
+    U, I = user_w.shape[0], item_hi.shape[0]
+    ok = (UI_BPR and not _DETERMINISTIC and user_w.is_cuda and all(t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == 64
+                                                        and t.is_contiguous() for t in (user_w, item_hi, item_w))
+          and U + I == ui_adj.shape[0] and U + I <= SPARSE_UPSTREAM_MAX_ROWS and getattr(ui_adj, "symmetric", False)
+          and item_w.shape[0] == I)
+    if not ok:
+        ui = propagate_mean_split(ui_adj, user_w, item_hi, 1)
+        return bpr_emb_loss(ui, None, user_w, item_w, u, p, n, gamma=gamma, item_offset=U, w_emb=w_emb)
+    return _UiBpr.apply(user_w, item_hi, item_w, u, p, n, ui_adj, float(gamma), float(w_emb))
+
+
 # graph_bpr_begin / _end on a branch stream (HealthRec's propagation beside its encoder); FR_BRANCH_STREAMS=0: off
 BRANCH_STREAMS = os.environ.get("FR_BRANCH_STREAMS", "1") != "0"
 AUX_STREAM = os.environ.get("FR_AUX_STREAM", "0") == "1"  # ops.aux_stream (FR_AUX_STREAM=1: on; measured no gain)
@@ -1384,12 +1468,154 @@ def loss_side_join() -> None:
         p[0].wait_stream(p[1])
 
 
+NORMS_DEFER = os.environ.get("FR_NORMS_DEFER", "1") != "0"
+# FR_LOSS_FINALIZE=0: HealthRec's loss terms finalized by their own launches (head finalize, norms
+# finalize + reg, the trainer's fr_step_book).  Default: inside a booked trainer step, one
+# fr_healthrec_loss_finalize launch does all three (the loss chain after the encoder: 4 launches)
+LOSS_FINALIZE = os.environ.get("FR_LOSS_FINALIZE", "1") != "0"
+
+# outputs written by a later launch, keyed by their storage: a deferred norms finalize
+# (embedding_norms(defer_norms=True)) and a deferred head finalize (modal_head inside a booked step)
+_PENDING_NORMS = {}
+_PENDING_HEAD = {}
+
+
+def _storage(t) -> int:
+    return t.untyped_storage().data_ptr()
+
+
+def finalize_norms(nrm) -> None:
+    """Write the norms an embedding_norms(..., defer_norms=True) left pending (one launch); no-op
+    otherwise."""
+    got = _PENDING_NORMS.pop(_storage(nrm), None) if nrm.is_cuda else None
+    if got is not None:
+        part, n, t = got
+        native.check(native.lib().fr_reg_combine_norms_fwd(None, part.data_ptr(), n, _f(1.0), _f(1.0), t.data_ptr(),
+                                                           None, native.stream_of(t)), "fr_reg_combine_norms_fwd")
+
+
+def _finalize_head(out) -> None:
+    got = _PENDING_HEAD.pop(_storage(out), None) if out.is_cuda else None
+    if got is not None:
+        part, n, thr, wh, wk, t = got
+        native.check(native.lib().fr_healthrec_loss_finalize(
+            part.data_ptr(), n, _f(thr), _f(wh), _f(wk), t.data_ptr(), None, 0, None, _f(1.0), _f(1.0), None, None,
+            None, None, 0, None, None, 0, None, native.stream_of(t)), "fr_healthrec_loss_finalize")
+
+
+def finalize_pending() -> None:
+    """Run every deferred finalize not consumed by a loss op (the trainer calls this after the
+    model's calculate_loss, before anything reads the loss terms)."""
+    for _, (_, _, _, _, _, t) in list(_PENDING_HEAD.items()):
+        _finalize_head(t)
+    for _, (_, _, t) in list(_PENDING_NORMS.items()):
+        finalize_norms(t)
+
+
+# the trainer's request that a fused loss op book the step itself (fr_step_book's work in its launch)
+_BOOK = {"request": None, "done": None}
+
+
+def book_request(state, accumulate) -> None:
+    _BOOK["request"], _BOOK["done"] = (state, bool(accumulate)), None
+
+
+def book_taken():
+    """(parts, loss) when a loss op booked the step since book_request, else None; clears both."""
+    done = _BOOK["done"]
+    _BOOK["request"], _BOOK["done"] = None, None
+    return done
+
+
+class _RegCombineNorms(torch.autograd.Function):
+    """reg_combine over norms still pending (embedding_norms(defer_norms=True)): the norms' finalize
+    and the combination in one launch; the norms tensor is written in place (it is the embedding_norms
+    node's output, saved by it for its backward).  Backward as _RegCombine."""
+
+    @staticmethod
+    def forward(ctx, a, b, B, w):
+        part, n, _ = _PENDING_NORMS.pop(_storage(b))
+        a = a.contiguous()
+        out = torch.empty(1, dtype=torch.float32, device=a.device)
+        native.check(native.lib().fr_reg_combine_norms_fwd(a.data_ptr(), part.data_ptr(), n, _f(float(B)), _f(float(w)),
+                                                           b.data_ptr(), out.data_ptr(), native.stream_of(a)),
+                     "fr_reg_combine_norms_fwd")
+        ctx.meta = (a.shape, b.shape, float(B), float(w))
+        return out
+
+    backward = _RegCombine.backward
+
+
+class _HealthRecLossFinalize(torch.autograd.Function):
+    """HealthRec's loss finalize (fr_healthrec_loss_finalize): the head's loss terms and the ingredient
+    norms left pending, reg = w * (emb3 + sum(norms) / B), and the step's bookkeeping over
+    [mf, health, kd, reg] when the trainer asked for it -- one launch.  Output: reg; gradients only
+    to (emb3, norms), as reg_combine (the other inputs are read, not differentiated through)."""
+
+    @staticmethod
+    def forward(ctx, emb3, nrm, mf, health, kd, B, w, book):
+        hp, n, thr, wh, wk, out = _PENDING_HEAD.pop(_storage(health))
+        npart, nn, _ = _PENDING_NORMS.pop(_storage(nrm))
+        reg = torch.empty(1, dtype=torch.float32, device=emb3.device)
+        acc = nan = loss = None
+        ctrs = []
+        if book is not None:
+            acc, nan, accumulate, loss = book
+            ctrs = take_pending_counters()
+        cptr = (ctypes.c_void_p * max(1, len(ctrs)))(*[c.data_ptr() for c in ctrs])
+        native.check(native.lib().fr_healthrec_loss_finalize(
+            hp.data_ptr(), n, _f(thr), _f(wh), _f(wk), out.data_ptr(), npart.data_ptr(), nn, emb3.data_ptr(),
+            _f(float(B)), _f(float(w)), nrm.data_ptr(), reg.data_ptr(), native.ptr(mf) if book else None,
+            native.ptr(acc), int(accumulate) if book else 0, native.ptr(nan), cptr, len(ctrs), native.ptr(loss),
+            native.stream_of(emb3)), "fr_healthrec_loss_finalize")
+        ctx.meta = (emb3.shape, nrm.shape, float(B), float(w))
+        return reg
+
+    @staticmethod
+    def backward(ctx, g):
+        da, db, _, _ = _RegCombine.backward(ctx, g)
+        return da, db, None, None, None, None, None, None
+
+
+def healthrec_loss_finalize(mf, health, kd, emb3, nrm, B, w):
+    """``w * (emb3 + nrm.sum() / B)`` (HealthRec's EmbLoss assembly, cikm_model.py:267-279), finalizing
+    in the same launch the modal head's loss terms and the ingredient norms a booked trainer step left
+    pending, and booking the step ([mf, health, kd, reg]) when the trainer requested it."""
+    if not (health.is_cuda and _storage(health) in _PENDING_HEAD and _storage(nrm) in _PENDING_NORMS
+            and nrm.numel() == 2 and emb3.numel() == 1 and kd.untyped_storage().data_ptr() == _storage(health)):
+        if health.is_cuda:
+            _finalize_head(health)
+        return reg_combine(emb3, nrm, B, w)
+    book = None
+    req = _BOOK["request"]
+    if req is not None and mf.is_cuda and mf.dtype == torch.float32 and mf.numel() == 1:
+        state, accumulate = req
+        acc = state.get("acc")
+        if acc is None:
+            acc = state["acc"] = torch.zeros(4, dtype=torch.float64, device=mf.device)
+            accumulate = False
+        if acc.numel() == 4:
+            loss = torch.empty((), dtype=torch.float32, device=mf.device)
+            book = (acc, state["nan"], accumulate, loss)
+    reg = _HealthRecLossFinalize.apply(emb3, nrm, mf, health, kd, B, w, book)
+    if book is not None:
+        _BOOK["done"] = ((mf, health, kd, reg), book[3])
+    return reg
+
+
 def reg_combine(a, b, B, w):
     """``w * (a + b.sum() / B)`` for a [1] and b [k] fp32 device tensors in one launch per direction
-    (forward on the loss side stream when enabled: its value feeds only the step's bookkeeping)."""
+    (forward on the loss side stream when enabled: its value feeds only the step's bookkeeping).
+    ``b`` = norms an embedding_norms(defer_norms=True) left pending: finalized in the same launch."""
+    if not a.is_cuda:
+        return w * (a + b.sum() / B)
     s = loss_side_stream(a.device, fork=True) if a.is_cuda else None
     if s is None:
+        if _storage(b) in _PENDING_NORMS and b.numel() == 2:
+            return _RegCombineNorms.apply(a, b, B, w)
+        finalize_norms(b)
         return _RegCombine.apply(a, b, B, w)
+    finalize_norms(b)
     a.record_stream(s)
     b.record_stream(s)
     with torch.cuda.stream(s):
@@ -1511,7 +1737,7 @@ class _EmbeddingNorms(torch.autograd.Function):
     ONE deterministic scatter (fr_embedding_bwd)."""
 
     @staticmethod
-    def forward(ctx, idx, weight, pad, half):
+    def forward(ctx, idx, weight, pad, half, defer_norms=False):
         native.require_device(weight, idx)
         n = idx.numel()
         hp = half * idx.shape[-1]  # positions in the first half
@@ -1524,10 +1750,14 @@ class _EmbeddingNorms(torch.autograd.Function):
             nrm = torch.empty(2, dtype=torch.float32, device=weight.device)
             nparts = lib.fr_gather_norms_partials(n)
             part = torch.empty(nparts, dtype=torch.float32, device=weight.device)
+            defer = bool(defer_norms) and NORMS_DEFER
             with profiling.region("gather_norms", 8 * n + 2 * 4 * n * 64):
                 native.check(lib.fr_gather_norms_fwd(idx_c.data_ptr(), n, hp, weight.data_ptr(), weight.stride(0),
-                                                     E.data_ptr(), part.data_ptr(), nparts, nrm.data_ptr(),
+                                                     E.data_ptr(), part.data_ptr(), nparts,
+                                                     None if defer else nrm.data_ptr(),
                                                      native.stream_of(weight)), "fr_gather_norms_fwd")
+            if defer:  # finalized by the loss finalize / reg_combine (or finalize_pending) before any read
+                _PENDING_NORMS[_storage(nrm)] = (part, n, nrm)
             ctx.save_for_backward(idx_c, E, nrm)
             ctx.rows, ctx.pad, ctx.half, ctx.hp = weight.shape[0], pad, half, hp
             ctx.defer = weight.__dict__.pop("_fr_defer_rows", None)
@@ -1554,22 +1784,22 @@ class _EmbeddingNorms(torch.autograd.Function):
                         native.stream_of(G)), "fr_norms_bwd_coef")
                 G = out
             if ctx.defer is not None and ctx.defer.put(idx, G.reshape(-1, 64), ctx.pad):
-                return None, None, None, None  # scattered into graph_bpr's d ingre (_DeferredRows)
-            return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None, hot_row=ctx.pad), None, None
+                return None, None, None, None, None  # scattered into graph_bpr's d ingre (_DeferredRows)
+            return None, scatter_rows(idx, G.reshape(-1, 64), ctx.rows, None, hot_row=ctx.pad), None, None, None
         G = torch.zeros_like(E) if gE is None else gE
         if gn is not None:
             coef = (gn / nrm).view(2, 1).expand(2, ctx.half * idx.shape[-1]).reshape(idx.shape)
             coef = torch.where(idx != ctx.pad, coef, torch.zeros((), dtype=coef.dtype, device=coef.device))
             G = torch.addcmul(G, coef.unsqueeze(-1), E)
-        return None, scatter_rows(idx, G, ctx.rows, None), None, None
+        return None, scatter_rows(idx, G, ctx.rows, None), None, None, None
 
 
-def embedding_norms(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int, half: int):
+def embedding_norms(idx: torch.Tensor, weight: torch.Tensor, padding_idx: int, half: int, defer_norms: bool = False):
     """``(W[idx], stack(||Embedding(idx[:half], pad)||_F, ||Embedding(idx[half:], pad)||_F))`` with
     one gather and one scatter (see _EmbeddingNorms).  ``idx``: [2 * half, L]."""
     if idx.shape[0] != 2 * half:
         raise native.EngineError(f"embedding_norms: idx has {idx.shape[0]} rows, expected 2 x {half}")
-    return _EmbeddingNorms.apply(idx, weight, int(padding_idx), int(half))
+    return _EmbeddingNorms.apply(idx, weight, int(padding_idx), int(half), bool(defer_norms))
 
 
 _EMB_STATUS = None  # test hook: a list collecting each call's device status word (0 = consistent)
@@ -1744,11 +1974,6 @@ def encoder_bytes(n_seq: int, L: int, backward: bool) -> int:
 # slower per step than a separate reduction: the 200 KB per workgroup of partial reads at the launch
 # start are not overlapped); default: every layer reduces its own partials
 ENCODER_FOLD = os.environ.get("FR_ENCODER_FOLD", "0") == "1"
-# FR_ENCODER_LATE_REDUCE=0: each layer's ordered weight-gradient reduction right after its backward
-# launch.  Default: the layers' backward launches back to back and their reductions issued by an
-# autograd final callback -- the weight gradients feed only the optimiser, so the reductions leave the
-# input-gradient chain (encoder -> ingredient gather backward) and run beside the step's tail
-ENCODER_LATE_REDUCE = os.environ.get("FR_ENCODER_LATE_REDUCE", "1") != "0"
 
 
 class _EncoderStack(torch.autograd.Function):
@@ -1806,11 +2031,6 @@ class _EncoderStack(torch.autograd.Function):
         nparts = lib.fr_encoder_partials(NS, L)
         grads = [None] * nl
         prev = None  # (partials, gradient) of the layer above, reduced by this layer's launch
-        # late reductions: only when the returned gradients become the parameters' .grad as they are
-        # (no accumulation reads them before the callback has written them)
-        late = (ENCODER_LATE_REDUCE and not ENCODER_FOLD and torch.is_grad_enabled() is False
-                and all(p.grad is None for p in flat))
-        pending = []
         for k in range(nl - 1, -1, -1):
             h, qkv, cx, y1, fact, dact, y2, st1, st2, seed_used = ctx.saved[k]
             cfg = cfgs[k]
@@ -1824,24 +2044,12 @@ class _EncoderStack(torch.autograd.Function):
                     g.data_ptr(), h.data_ptr(), native.ptr(mask), NS, L, pp, cfg.eps, cfg.drop, cfg.seed, cfg.gelu,
                     seed_used.data_ptr(), qkv.data_ptr(), cx.data_ptr(), y1.data_ptr(), fact.data_ptr(),
                     dact.data_ptr(), y2.data_ptr(), st1.data_ptr(), st2.data_ptr(), dx.data_ptr(),
-                    None if late else (grad.data_ptr() if (k == 0 or not ENCODER_FOLD) else None),
+                    grad.data_ptr() if (k == 0 or not ENCODER_FOLD) else None,
                     part.data_ptr(), nparts, prev[0].data_ptr() if prev else None,
                     prev[1].data_ptr() if prev else None, native.stream_of(g)), "fr_encoder_bwd")
             grads[k] = grad
             prev = (part, grad) if ENCODER_FOLD else None
-            if late:
-                pending.append((part, grad))
             g = dx
-        if pending:
-            stream = native.stream_of(g)
-
-            def _reduce_late(pending=pending, NS=NS, L=L, stream=stream):
-                for part, grad in pending:
-                    with profiling.region("encoder_reduce", 4 * (part.numel() + grad.numel())):
-                        native.check(native.lib().fr_encoder_reduce(part.data_ptr(), NS, L, grad.data_ptr(), stream),
-                                     "fr_encoder_reduce")
-
-            torch.autograd.Variable._execution_engine.queue_callback(_reduce_late)
         out = []
         for k in range(nl):
             params = flat[12 * k:12 * (k + 1)]
@@ -2188,12 +2396,21 @@ class _ModalHead(torch.autograd.Function):
         out = torch.empty(3, dtype=torch.float32, device=dev)
         lnp = (ctypes.c_void_p * 4)(ga.data_ptr(), ba.data_ptr(), gb.data_ptr(), bb.data_ptr())
         mlp = (ctypes.c_void_p * 4)(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr())
+        defer = LOSS_FINALIZE and _DEFER[0] and not HEAD_TICKET
         with profiling.region("modal_head", fusion_bytes(n, L, False) + health_kd_bytes(n, H, False)):
-            native.check(lib.fr_modal_head_fwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
-                                               int(pad_id), n, L, lnp, float(eps), rows.data_ptr(), labels.data_ptr(), H,
-                                               mlp, float(thr), float(w_h), float(w_k), out.data_ptr(), part.data_ptr(),
-                                               part.numel(), _arrival_ticket(enc.device).data_ptr() if HEAD_TICKET else None,
-                                               native.stream_of(enc)), "fr_modal_head_fwd")
+            if defer:  # the finalize is left to healthrec_loss_finalize (or finalize_pending)
+                native.check(lib.fr_modal_head_fwd_items(
+                    enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(), int(pad_id), n, L, lnp, float(eps),
+                    rows.data_ptr(), labels.data_ptr(), H, mlp, float(thr), float(w_h), float(w_k), part.data_ptr(),
+                    part.numel(), native.stream_of(enc)), "fr_modal_head_fwd_items")
+                _PENDING_HEAD[_storage(out)] = (part, n, float(thr), float(w_h), float(w_k), out)
+            else:
+                native.check(lib.fr_modal_head_fwd(enc.data_ptr(), query.data_ptr(), ids.data_ptr(), num.data_ptr(),
+                                                   int(pad_id), n, L, lnp, float(eps), rows.data_ptr(), labels.data_ptr(),
+                                                   H, mlp, float(thr), float(w_h), float(w_k), out.data_ptr(),
+                                                   part.data_ptr(), part.numel(),
+                                                   _arrival_ticket(enc.device).data_ptr() if HEAD_TICKET else None,
+                                                   native.stream_of(enc)), "fr_modal_head_fwd")
         ctx.save_for_backward(enc, query, ids, num, rows, labels, ga, ba, gb, bb, w1, b1, w2, b2)
         ctx.out, ctx.cfg = out, (int(pad_id), float(eps), float(thr), float(w_h), float(w_k))
         return out[0], out[1]

@@ -109,6 +109,9 @@ class CLUSSL(GeneralRecommender):
             gathered = [g_img, g_txt, g_ing]
         else:
             item_emb = item_ingre + item_image + item_text
+        if ssl_ids is not None and self.n_ui_layers == 1:
+            # the loss evaluates the UI layer at its batch rows only (ops.ui_bpr): item_emb is its input
+            return None, item_emb, (item_image, item_text, item_ingre), gathered
         # propagate(cat([user, item_emb])) with the concatenation folded into the SpMM addressing
         ui = ops.propagate_mean_split(self.norm_adj_matrix, self.user_embedding.weight, item_emb, self.n_ui_layers)
         if ssl_ids is not None:  # the loss reads the one table (bpr_emb_loss item_offset): no split backward
@@ -122,10 +125,14 @@ class CLUSSL(GeneralRecommender):
         all_item = dict.get(batch_data, "pn_i_id") if isinstance(batch_data, dict) else None
         if all_item is None:
             all_item = torch.cat([pos_item, neg_item], dim=0)
-        ui, _, _, views = self._forward(all_item)  # views at the batch items: image, text, ingre
+        ui, item_emb, _, views = self._forward(all_item)  # views at the batch items: image, text, ingre
         # the loss weights (reg_weight, loss_cl) are applied inside the kernels: no multiply launches
-        mf_loss, reg = ops.bpr_emb_loss(ui, None, self.user_embedding.weight, self.item_embedding.weight,
-                                        user, pos_item, neg_item, item_offset=self.n_users, w_emb=self.reg_weight)
+        if ui is None:  # one UI layer: propagation at the batch rows + BPR + EmbLoss as one node
+            mf_loss, reg = ops.ui_bpr(self.norm_adj_matrix, self.user_embedding.weight, item_emb,
+                                      self.item_embedding.weight, user, pos_item, neg_item, w_emb=self.reg_weight)
+        else:
+            mf_loss, reg = ops.bpr_emb_loss(ui, None, self.user_embedding.weight, self.item_embedding.weight,
+                                            user, pos_item, neg_item, item_offset=self.n_users, w_emb=self.reg_weight)
         if self.ssl_mode == "infonce":
             # sum over the pairs of CL_loss(cat([views[a], views[b]])): one fused node for all pairs
             cl = ops.infonce_pairs(views, _DCOR_PAIRS, 0.5, weight=self.loss_cl)

@@ -197,7 +197,8 @@ class HealthRec(GeneralRecommender):
         # ingr_all[ingredients] (grad reaches the pad row too, cikm_model.py:230) and the EmbLoss
         # norms of ingre_embedding(pos / neg ingredients) with padding_idx (:270-279): the same
         # gather, so one gather and one combined deterministic scatter (fr_embedding_bwd)
-        ingr_emb, ing_norms = ops.embedding_norms(ingredients, ingr_all, self.n_ingredients, B)
+        # (the norms' finalize is left to the loss's reg_combine launch: they feed nothing before it)
+        ingr_emb, ing_norms = ops.embedding_norms(ingredients, ingr_all, self.n_ingredients, B, defer_norms=True)
         mask = batch_data.get("pn_pad_kpm")  # additive key mask gathered with the codes (engine batch), else computed
         if mask is None:
             mask = ingredients == self.n_ingredients
@@ -267,7 +268,11 @@ class HealthRec(GeneralRecommender):
     def _losses(self, mf_loss, health_term, kd_term, emb3, ing_norms, B):
         # EmbLoss over 5 blocks, / rows of the last block (= B): fused part carries 3 of them
         if emb3.is_cuda and ing_norms.is_cuda and emb3.dtype == torch.float32 and ing_norms.dtype == torch.float32:
-            return mf_loss, health_term, kd_term, ops.reg_combine(emb3, ing_norms, B, self.reg_weight)
+            # the head's and the norms' deferred finalizes, the EmbLoss assembly and (in a trainer step)
+            # the step's bookkeeping in one launch (ops.healthrec_loss_finalize)
+            return mf_loss, health_term, kd_term, ops.healthrec_loss_finalize(mf_loss, health_term, kd_term, emb3,
+                                                                              ing_norms, B, self.reg_weight)
+        ops.finalize_norms(ing_norms)
         reg = emb3 + ing_norms.sum() / B  # (= ing_norms[0] + ing_norms[1]; sum's backward is a view, no fills)
         return mf_loss, health_term, kd_term, self.reg_weight * reg
 

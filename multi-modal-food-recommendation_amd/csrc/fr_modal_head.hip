@@ -295,6 +295,57 @@ int dispatch(const HeadArgs& a, int L, bool backward, hipStream_t s) {
 
 }  // namespace
 
+// HealthRec's loss finalize in one launch (one 256-thread block): the head's finalize (the loss
+// terms from fr_modal_head_fwd_items' block partials: head_final), the EmbLoss ingredient norms from
+// fr_gather_norms_fwd's partials (norms_final's fixed-order sums), reg = w * (a + (n0 + n1) / B)
+// (fr_reg_combine_fwd's arithmetic) and, when acc is given, the step's bookkeeping over the parts
+// [mf, health, kd, reg] (fr_step_book's arithmetic and counter advance).
+struct LossFin {
+  const float* npart; int nnblk;
+  const float* emb3; float B, w;
+  float *nrm, *reg;
+  const float* mf;
+  double* acc; int accumulate; int32_t* nan; float* loss;
+  int64_t* ctr[8]; int nc;
+};
+
+__global__ __launch_bounds__(256) void loss_finalize_kernel(HeadArgs a, int nblk, LossFin f) {
+  __shared__ float red[2][256];
+  if (a.part && threadIdx.x < 64) head_final(a, nblk, threadIdx.x);  // out[0..2], written by thread 0
+  if (!f.npart) return;
+  float s0 = 0.f, s1 = 0.f;
+  for (int b = threadIdx.x; b < f.nnblk; b += 256) {
+    s0 += f.npart[2 * b];
+    s1 += f.npart[2 * b + 1];
+  }
+  red[0][threadIdx.x] = s0;
+  red[1][threadIdx.x] = s1;
+  __syncthreads();
+  for (int q = 128; q > 0; q >>= 1) {
+    if (threadIdx.x < q) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + q];
+      red[1][threadIdx.x] += red[1][threadIdx.x + q];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const float n0 = sqrtf(red[0][0]), n1 = sqrtf(red[1][0]);
+  f.nrm[0] = n0;
+  f.nrm[1] = n1;
+  const float reg = f.w * (f.emb3[0] + (n0 + n1) / f.B);
+  f.reg[0] = reg;
+  if (!f.acc) return;
+  for (int i = 0; i < f.nc; ++i) f.ctr[i][0] += 1;
+  const float v[4] = {f.mf[0], a.out[0], a.out[1], reg};  // this thread wrote out[0..1] above
+  float s = 0.f;
+  for (int i = 0; i < 4; ++i) {
+    f.acc[i] = f.accumulate ? f.acc[i] + (double)v[i] : (double)v[i];
+    s = i == 0 ? v[i] : s + v[i];
+  }
+  if (s != s) f.nan[0] |= 1;
+  if (f.loss) f.loss[0] = s;
+}
+
 extern "C" int64_t fr_modal_head_partials(int64_t n_items, int backward) {
   if (n_items <= 0) return 0;
   const int64_t nb = fr::ceil_div(n_items, WAVES);
@@ -322,6 +373,52 @@ extern "C" int fr_modal_head_fwd(const float* d_enc, const float* d_query, const
     hipLaunchKernelGGL(modal_head_final_kernel, dim3(1), dim3(64), 0, s, a, (int)fr::ceil_div(n_items, WAVES));
     FR_LAUNCH_CHECK();
   }
+  return FR_OK;
+}
+
+extern "C" int fr_modal_head_fwd_items(const float* d_enc, const float* d_query, const int64_t* d_ids,
+                                       const int64_t* d_num, int64_t pad_id, int64_t n_items, int L,
+                                       const float* const* d_ln, float eps, const float* d_rows, const float* d_labels,
+                                       int H, const float* const* d_mlp, float kd_threshold, float w_health, float w_kd,
+                                       float* d_partials, int64_t partial_floats, void* stream) {
+  HeadArgs a{};
+  float dummy_out[1];
+  int rc = fill(a, d_enc, d_query, d_ids, d_num, pad_id, n_items, L, d_ln, eps, d_rows, d_labels, H, d_mlp,
+                kd_threshold, w_health, w_kd, dummy_out);
+  if (rc) return rc;
+  a.out = nullptr;  // the per-item kernel writes only the block partials
+  FR_REQUIRE(d_partials && partial_floats >= fr_modal_head_partials(n_items, 0), "partial buffer too small");
+  a.part = d_partials;
+  return dispatch(a, L, false, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int fr_healthrec_loss_finalize(const float* d_head_partials, int64_t n_items, float kd_threshold,
+                                          float w_health, float w_kd, float* d_out, const float* d_norm_partials,
+                                          int64_t n_norm_rows, const float* d_emb3, float B, float w_reg,
+                                          float* d_nrm, float* d_reg, const float* d_mf, double* d_acc, int accumulate,
+                                          int32_t* d_nan, int64_t* const* d_counters, int n_counters, float* d_loss,
+                                          void* stream) {
+  FR_REQUIRE(!d_head_partials || (n_items > 0 && d_out), "head finalize needs n_items and out");
+  FR_REQUIRE(!d_norm_partials || (n_norm_rows > 0 && d_emb3 && B > 0.f && d_nrm && d_reg), "norms / reg operands");
+  FR_REQUIRE(!d_acc || (d_head_partials && d_norm_partials && d_mf && d_nan), "bookkeeping needs every part");
+  FR_REQUIRE(n_counters >= 0 && n_counters <= 8 && (n_counters == 0 || d_counters), "0..8 counters");
+  HeadArgs a{};
+  a.part = const_cast<float*>(d_head_partials);
+  a.f.n_items = n_items;
+  a.thr = kd_threshold; a.wh = w_health; a.wk = w_kd; a.out = d_out;
+  LossFin f{};
+  f.npart = d_norm_partials;
+  f.nnblk = d_norm_partials ? (int)(fr_gather_norms_partials(n_norm_rows) / 2) : 0;
+  f.emb3 = d_emb3; f.B = B; f.w = w_reg; f.nrm = d_nrm; f.reg = d_reg; f.mf = d_mf;
+  f.acc = d_acc; f.accumulate = accumulate; f.nan = d_nan; f.loss = d_loss;
+  for (int i = 0; i < n_counters; ++i) {
+    FR_REQUIRE(d_counters[i] != nullptr, "null counter");
+    f.ctr[i] = d_counters[i];
+  }
+  f.nc = n_counters;
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a,
+                     d_head_partials ? (int)fr::ceil_div(n_items, WAVES) : 0, f);
+  FR_LAUNCH_CHECK();
   return FR_OK;
 }
 

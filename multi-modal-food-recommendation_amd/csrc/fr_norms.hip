@@ -100,7 +100,7 @@ extern "C" int fr_gather_norms_fwd(const int64_t* d_ids, int64_t n, int64_t half
                                    float* d_e, float* d_partials, int64_t partial_floats, float* d_nrm,
                                    void* stream) {
   FR_REQUIRE(n > 0 && half >= 0 && half <= n, "n > 0 and 0 <= half <= n required");
-  FR_REQUIRE(d_ids && d_w && d_e && d_partials && d_nrm, "null operand");
+  FR_REQUIRE(d_ids && d_w && d_e && d_partials, "null operand");
   FR_REQUIRE(ldw >= 64 && ldw % 4 == 0 && fr::aligned16(d_w) && fr::aligned16(d_e), "64-wide 16-B aligned rows");
   FR_REQUIRE(partial_floats >= fr_gather_norms_partials(n), "partial buffer too small");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -108,7 +108,49 @@ extern "C" int fr_gather_norms_fwd(const int64_t* d_ids, int64_t n, int64_t half
   hipLaunchKernelGGL(gather_norms_kernel, dim3(nb), dim3(256), 0, s, d_ids, n, half,
                      reinterpret_cast<const float4*>(d_w), ldw / 4, reinterpret_cast<float4*>(d_e), d_partials);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(norms_final_kernel, dim3(1), dim3(256), 0, s, d_partials, nb, d_nrm);
+  if (d_nrm) {  // NULL: the finalize is left to fr_reg_combine_norms_fwd (the norms' only reader)
+    hipLaunchKernelGGL(norms_final_kernel, dim3(1), dim3(256), 0, s, d_partials, nb, d_nrm);
+    FR_LAUNCH_CHECK();
+  }
+  return FR_OK;
+}
+
+// the norms finalize (the same fixed-order sums as norms_final_kernel: bit-identical) with HealthRec's
+// EmbLoss assembly in the same launch: reg = w * (a + (nrm0 + nrm1) / B) as fr_reg_combine_fwd
+namespace {
+__global__ __launch_bounds__(256) void reg_norms_kernel(const float* __restrict__ part, int nblk,
+                                                        float* __restrict__ nrm, const float* __restrict__ a,
+                                                        float B, float w, float* __restrict__ out) {
+  __shared__ float red[2][256];
+  float s0 = 0.f, s1 = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 256) {
+    s0 += part[2 * b];
+    s1 += part[2 * b + 1];
+  }
+  red[0][threadIdx.x] = s0;
+  red[1][threadIdx.x] = s1;
+  __syncthreads();
+  for (int q = 128; q > 0; q >>= 1) {
+    if (threadIdx.x < q) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + q];
+      red[1][threadIdx.x] += red[1][threadIdx.x + q];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float n0 = sqrtf(red[0][0]), n1 = sqrtf(red[1][0]);
+    nrm[0] = n0;
+    nrm[1] = n1;
+    if (out) out[0] = w * (a[0] + (n0 + n1) / B);
+  }
+}
+}  // namespace
+
+extern "C" int fr_reg_combine_norms_fwd(const float* d_a, const float* d_partials, int64_t n, float B, float w,
+                                        float* d_nrm, float* d_out, void* stream) {
+  FR_REQUIRE(n > 0 && d_partials && d_nrm && (!d_out || (d_a && B > 0.f)), "bad argument");
+  hipLaunchKernelGGL(reg_norms_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_partials,
+                     blocks_for(n), d_nrm, d_a, B, w, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

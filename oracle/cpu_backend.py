@@ -70,6 +70,12 @@ def bpr_emb_loss(U, I, Ue, Ie, user, pos, neg, gamma=1e-10, deterministic=False,
     return (mf, emb, torch.cat([p, n])) if item_rows else (mf, emb)
 
 
+def ui_bpr(ui_adj, user_w, item_hi, item_w, u, p, n, gamma=1e-10, w_emb=1.0):
+    # the UI layer (pricai_modelx.py:226-232) and BPR + EmbLoss (:252-267) as the reference computes them
+    ui = propagate_mean(ui_adj, torch.cat([user_w, item_hi], dim=0), 1)
+    return bpr_emb_loss(ui, None, user_w, item_w, u, p, n, gamma=gamma, item_offset=user_w.shape[0], w_emb=w_emb)
+
+
 def dcor_loss(views, pairs, weight=1.0):
     s = sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
     return s if weight == 1.0 else weight * s  # loss_cl * SSL term (pricai_modelx.py:263-267)
@@ -91,7 +97,7 @@ def embedding(idx, weight, padding_idx=None, exchange=None):
     return torch.nn.functional.embedding(idx, weight, padding_idx=padding_idx)
 
 
-def embedding_norms(idx, weight, padding_idx, half):
+def embedding_norms(idx, weight, padding_idx, half, defer_norms=False):
     # ingr_all[ingredients] (cikm_model.py:230) and the EmbLoss norms of ingre_embedding(pos / neg)
     # with padding_idx (cikm_model.py:270-279), as the reference computes them
     E = torch.nn.functional.embedding(idx, weight)
@@ -104,7 +110,8 @@ def linear(x, W, b=None):
 
 
 _PATCH = {"embedding": embedding, "embedding_norms": embedding_norms, "linear": linear, "spmm_launch": spmm_launch, "scatter_rows": scatter_rows, "spmm": spmm, "propagate_mean": propagate_mean, "bpr_emb_loss": bpr_emb_loss,
-          "dcor_loss": dcor_loss, "infonce_loss": infonce_loss, "infonce_pairs": infonce_pairs}
+          "dcor_loss": dcor_loss, "infonce_loss": infonce_loss, "infonce_pairs": infonce_pairs,
+          "ui_bpr": ui_bpr}
 
 
 @contextlib.contextmanager

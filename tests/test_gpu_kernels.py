@@ -1021,3 +1021,36 @@ def test_propagate_mean_split_matches_cat(cuda):
         (ya * G).sum().backward()
         (yb * G).sum().backward()
         assert torch.equal(la.grad, lb.grad) and torch.equal(ha.grad, hb.grad), L
+
+
+def test_ui_bpr_matches_unfused(cuda):
+    """ops.ui_bpr (UI layer at the batch rows + BPR + EmbLoss, sparse-upstream backward) vs
+    propagate_mean_split + bpr_emb_loss on the same inputs: losses rel 1e-6, every gradient within
+    1e-5 of its max (float-atomic summation orders differ)."""
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency
+    g = torch.Generator().manual_seed(21)
+    U, I, e = 600, 900, 8000
+    r = torch.randint(0, U, (e,), generator=g)
+    c = torch.randint(0, I, (e,), generator=g) + U
+    rows, cols = torch.cat([r, c]), torch.cat([c, r])
+    deg = torch.bincount(rows, minlength=U + I).clamp(min=1).float()
+    adj = Adjacency.from_coo(rows, cols, deg[rows].rsqrt() * deg[cols].rsqrt(), (U + I, U + I), device=cuda)
+    t0 = [torch.randn(U, 64, generator=g), torch.randn(I, 64, generator=g), torch.randn(I, 64, generator=g)]
+    u = torch.randint(0, U, (256,), generator=g).to(cuda)
+    p, n = (torch.randint(0, I, (256,), generator=g).to(cuda) for _ in range(2))
+    res = []
+    for fused in (True, False):
+        uw, hi, iw = (x.clone().to(cuda).requires_grad_(True) for x in t0)
+        if fused:
+            mf, reg = ops.ui_bpr(adj, uw, hi, iw, u, p, n, w_emb=0.01)
+        else:
+            ui = ops.propagate_mean_split(adj, uw, hi, 1)
+            mf, reg = ops.bpr_emb_loss(ui, None, uw, iw, u, p, n, item_offset=U, w_emb=0.01)
+        (mf + reg.sum()).backward()
+        res.append((mf.detach(), reg.detach(), uw.grad, hi.grad, iw.grad))
+    (ma, ra, *ga), (mb, rb, *gb) = res
+    torch.testing.assert_close(ma, mb, rtol=1e-6, atol=0)
+    torch.testing.assert_close(ra, rb, rtol=1e-6, atol=0)
+    for a, b in zip(ga, gb):
+        assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-9

@@ -132,3 +132,49 @@ def test_modal_head_deterministic(cuda):
     assert torch.equal(first[0], again[0]) and torch.equal(first[1], again[1])
     for ga, gb in zip(first[2], again[2]):
         assert torch.equal(ga, gb)
+
+
+def test_healthrec_loss_finalize_step_equals_separate_launches(cuda, monkeypatch):
+    """A booked HealthRec trainer step with the loss terms finalized by one fr_healthrec_loss_finalize
+    launch (head finalize + ingredient norms + EmbLoss assembly + the step's bookkeeping) vs the
+    separate launches (FR_LOSS_FINALIZE=0: head finalize, reg_combine, fr_step_book): the same
+    arithmetic, so in deterministic mode the booked loss sums, the returned loss and every parameter
+    after three steps are bit-identical."""
+    import numpy as np
+    from helpers import tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import ops
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    det0 = torch.are_deterministic_algorithms_enabled()
+    runs = []
+    try:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        for fused in (True, False):
+            monkeypatch.setattr(ops, "LOSS_FINALIZE", fused)
+            cfg = tiny_config("CIKM_Model", True, train_batch_size=32, cuda_graph=False, deterministic=True)
+            data = tiny_data(cfg)
+            init_seed(999)
+            model = get_model("CIKM_Model")(cfg, data).to(cuda)
+            tr = Trainer(cfg, model)
+            np.random.seed(7)
+            sampler = TripleSampler(data, 32, cuda)
+            feats = tr._features()
+            state = tr.new_step_state()
+            model.train()
+            losses = []
+            for k, (u, p, n) in enumerate(sampler.epoch()):
+                if k == 3:
+                    break
+                losses.append(float(tr.train_step(feats.batch(u, p, n), k, state)))
+            tr.flush_optimizer()
+            runs.append((state["acc"].cpu().numpy().copy(), losses,
+                         {k: v.detach().clone() for k, v in model.state_dict().items()}))
+            assert not ops._PENDING_HEAD and not ops._PENDING_NORMS
+    finally:
+        torch.use_deterministic_algorithms(det0)
+    (aa, la, sa), (ab, lb, sb) = runs
+    np.testing.assert_array_equal(aa, ab)
+    assert la == lb
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k

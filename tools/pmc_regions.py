@@ -16,8 +16,7 @@ from collections import defaultdict
 
 # engine timing region -> the kernels (name substrings) one call of it launches on HEAD
 REGION_KERNELS = {
-    "encoder_bwd": ["enc_bwd_kernel"],
-    "encoder_reduce": ["enc_reduce_kernel"],
+    "encoder_bwd": ["enc_bwd_kernel", "enc_reduce_kernel"],
     "encoder_fwd": ["enc_fwd_kernel"],
     "spmm": ["spmm_plain16_kernel"],
     "spmm_masked": ["spmm_sparse_kernel"],
