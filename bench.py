@@ -274,6 +274,22 @@ def main():
         eager_elapsed = time.perf_counter() - tk0
     kern = timer.summary()
     ksteps = max(1, args.kernel_steps)
+    # the same eager pass with the propagation branch serialised (nothing runs beside the encoder):
+    # the kernels' own durations, next to the in-step ones above (stretched by the branch's SpMMs)
+    from FoodRec.engine import ops as _ops_mod
+    branch0 = _ops_mod.BRANCH_STREAMS
+    _ops_mod.BRANCH_STREAMS = False
+    try:
+        with profiling.timing() as timer_iso:
+            for i in range(args.kernel_steps):
+                u, p, n = next(it)
+                if feed is not None and u is graphed.inputs[0]:
+                    feed.fill(u, p, n)
+                trainer.train_step(feats.batch(u, p, n), i, state)
+            torch.cuda.synchronize()
+        kern_iso = timer_iso.summary()
+    finally:
+        _ops_mod.BRANCH_STREAMS = branch0
 
     ms_steps = elapsed / args.steps * 1e3
     ms_per_step = ms_steps + epoch_ms / steps_per_epoch
@@ -304,6 +320,13 @@ def main():
                                            if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
+            iso = kern_iso.get(dom_name)
+            if iso is not None:
+                tfi = fl / (iso["avg_ms"] * 1e-3) / 1e12
+                roofline["isolated"] = {"avg_launch_ms": round(iso["avg_ms"], 4), "achieved": round(tfi, 2),
+                                        "frac": round(tfi / MFMA_F32_PEAK_TFLOPS, 4),
+                                        "note": "same eager pass with the propagation branch serialised (FR_BRANCH_"
+                                                "STREAMS off): the launch without the RI / UI SpMMs beside it"}
         else:
             achieved = d["gbps"]
             roofline = {**common, "bound": "hbm", "achieved": round(achieved, 1),
