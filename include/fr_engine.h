@@ -760,6 +760,20 @@ int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float
                       const fr_spmm_plan* plan, int64_t split, const fr_tab* X, int d, const fr_tab* Y1,
                       const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
                       int64_t row_lo, int64_t row_hi, void* d_workspace, int64_t workspace_bytes, void* stream);
+/* Device-built row lists (HealthRec's RI forward evaluated at the item rows its UI layer reads):
+ * fr_rows_frontier marks, in d_mark [I] (zero on entry, left zero), the item columns (U + i) of the
+ *   batch users' rows of a [users | items] CSR and the batch items p, n, then writes them to d_list and
+ *   their number to d_count (order arbitrary).  Two launches.
+ * fr_spmm_csr_list: fr_spmm_csr_ex's epilogue (split tables, Y1 / Y2 / A1 / A2) for the rows
+ *   d_list[0 .. *d_count) only (the count read on the device; max_rows bounds it for the grid), d = 64,
+ *   rows bit-identical to the full launch's. */
+int fr_rows_frontier(const int64_t* d_rowptr, const int32_t* d_col, int64_t U, int64_t I, const int64_t* d_u,
+                     const int64_t* d_p, const int64_t* d_n, int64_t B, uint8_t* d_mark, int32_t* d_list,
+                     int32_t* d_count, void* stream);
+int fr_spmm_csr_list(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows, int64_t split,
+                     const fr_tab* X, const fr_tab* Y1, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
+                     const fr_tab* A2, float beta2, const int32_t* d_list, const int32_t* d_count, int64_t max_rows,
+                     void* stream);
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
                       uint32_t* d_bits, void* stream);

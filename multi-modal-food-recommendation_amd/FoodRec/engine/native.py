@@ -64,6 +64,11 @@ _SIGS = {
                                   c_float, POINTER(FrTab), c_float, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     "fr_spmm_sparse_upstream_rect": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                              c_int64, POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p]),
+    "fr_rows_frontier": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                 c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fr_spmm_csr_list": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, POINTER(FrTab), POINTER(FrTab),
+                                 POINTER(FrTab), c_float, POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p,
+                                 c_void_p, c_int64, c_void_p]),
     "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
     "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p,
                                   c_void_p]),

@@ -977,6 +977,41 @@ def grad_buffer(w: torch.Tensor) -> torch.Tensor:
     return torch.empty_like(w)
 
 
+# FR_RI_FRONTIER=0: HealthRec's RI forward at every item row (full layer 1, item rows of layer 2)
+RI_FRONTIER = os.environ.get("FR_RI_FRONTIER", "1") != "0"
+
+
+def _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n):
+    """mean(E, A E, A^2 E) of the bipartite RI graph at the item rows the batch's UI layer reads:
+    layer 1 over every ingredient row (layer 2 reads them all) and at the listed item rows, layer 2
+    at the listed item rows.  Rows outside the list are left unwritten (nothing reads them)."""
+    dev = item_w.device
+    N = ri_adj.shape[0]
+    lib = native.lib()
+    s = native.stream_of(item_w)
+    mark = _persistent(ri_adj, ("front_mark", str(dev)), lambda: torch.zeros(I, dtype=torch.uint8, device=dev))
+    lst = _persistent(ri_adj, ("front_list", str(dev)), lambda: torch.empty(I, dtype=torch.int32, device=dev))
+    cnt = _persistent(ri_adj, ("front_cnt", str(dev)), lambda: torch.zeros(1, dtype=torch.int32, device=dev))
+    native.check(lib.fr_rows_frontier(ui_adj.rowptr.data_ptr(), ui_adj.col.data_ptr(), U, I, u.data_ptr(), p.data_ptr(),
+                                      n.data_ptr(), int(u.numel()), mark.data_ptr(), lst.data_ptr(), cnt.data_ptr(), s),
+                 "fr_rows_frontier")
+    inv = 1.0 / 3.0
+    out = torch.empty(N, 64, dtype=torch.float32, device=dev)
+    E1 = torch.empty_like(out)
+    spmm_range(ri_adj, item_w, I, N, X_hi=ingre_w, split=I, Y1=E1)  # layer 1, ingredient rows
+    args = (ri_adj.rowptr.data_ptr(), ri_adj.col.data_ptr(), ri_adj.val.data_ptr(), N, I)
+    with profiling.region("spmm_rows", 0):
+        native.check(lib.fr_spmm_csr_list(*args, ctypes.byref(_tab(item_w, ingre_w)), ctypes.byref(_tab(E1)),
+                                          ctypes.byref(_tab(None)), _f(1.0), ctypes.byref(_tab(None)), _f(0.0),
+                                          ctypes.byref(_tab(None)), _f(0.0), lst.data_ptr(), cnt.data_ptr(), I, s),
+                     "fr_spmm_csr_list")  # layer 1, listed item rows
+        native.check(lib.fr_spmm_csr_list(*args, ctypes.byref(_tab(E1)), ctypes.byref(_tab(None)),
+                                          ctypes.byref(_tab(out)), _f(inv), ctypes.byref(_tab(item_w, ingre_w)),
+                                          _f(inv), ctypes.byref(_tab(E1)), _f(inv), lst.data_ptr(), cnt.data_ptr(), I,
+                                          s), "fr_spmm_csr_list")  # layer 2, listed item rows
+    return out
+
+
 class _GraphBprForward:
     """The forward of _GraphBpr computed ahead of its autograd node (graph_bpr_begin), possibly on a
     branch stream: the outputs and the tensors the backward reads."""
@@ -992,9 +1027,14 @@ def _graph_bpr_forward(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_r
         if t.dtype != torch.float32 or t.shape[1] != 64 or not t.is_contiguous():
             raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
     u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
-    # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
-    ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
     rows = [(u, 0), (p, U), (n, U)]
+    if L_ui == 1 and L_ri == 2 and ri_adj.bipartite_split == I and RI_FRONTIER:
+        # the UI layer at the batch rows reads item_ir only at the batch users' items and the batch
+        # items: the RI propagation's item rows are evaluated there only (device-built row list)
+        ir_all = _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n)
+    else:
+        # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
+        ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
     if L_ui == 1:
         ui_all = torch.empty(U + I, 64, dtype=torch.float32, device=dev)  # valid at the batch rows
         spmm_ex(ui_adj, user_w, ir_all, U, Y2=ui_all, alpha=0.5, A1=user_w, A1_hi=ir_all, beta1=0.5,

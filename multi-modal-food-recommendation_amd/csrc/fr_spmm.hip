@@ -554,6 +554,109 @@ __global__ __launch_bounds__(256) void spmm_plain16_kernel(const int64_t* __rest
   }
 }
 
+// Row-list walk (fr_spmm_csr_list): the rows list[0 .. *count) only, the count read on the device (a
+// list built by an earlier launch, e.g. fr_rows_frontier).  Each 16-lane group takes rows j, j + G,
+// ...; per row the same 16-edge batches and FMA order as spmm_plain16_kernel (rows bit-identical).
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void spmm_list16_kernel(const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const float* __restrict__ val,
+                                                          const int32_t* __restrict__ list,
+                                                          const int32_t* __restrict__ d_count, XSrc xs, Epi ep) {
+  constexpr int LPR = 16, GPB = 256 / LPR;
+  const int q = threadIdx.x % LPR;
+  const int64_t n = d_count[0];
+  const int64_t G = (int64_t)gridDim.x * GPB;
+  const bool has_a1 = ep.Y2.lo && ep.A1.lo, has_a2 = ep.Y2.lo && ep.A2.lo;
+  for (int64_t j = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; j < n; j += G) {
+    const int64_t r = list[j];
+    const int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
+    int c;
+    float v;
+    load_batch(col, val, e0, e1, q, c, v);
+    float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1;
+    if (has_a1) a1 = reinterpret_cast<const float4*>(tab_row(ep.A1, r, ep.split))[q];
+    if (has_a2) a2 = reinterpret_cast<const float4*>(tab_row(ep.A2, r, ep.split))[q];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = e0; e < e1; e += LPR) {
+      float4 x[LPR];
+      float w[LPR];
+      int64_t off = 0;
+      if constexpr (SPLIT)
+        off = c >= xs.split ? (xs.hi - xs.lo) + ((int64_t)c - xs.split) * xs.ldh4 : (int64_t)c * xs.ld4;
+      const int off_lo = (int)(uint32_t)(uint64_t)off, off_hi = (int)(uint32_t)((uint64_t)off >> 32);
+#define FR_PG(K)                                                                           \
+      {                                                                                    \
+        w[(K)] = bcast_f<LPR, (K)>(v);                                                     \
+        if constexpr (SPLIT) {                                                             \
+          const uint64_t ok = (uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_lo) |              \
+                              ((uint64_t)(uint32_t)bcast_i<LPR, (K)>(off_hi) << 32);       \
+          x[(K)] = xs.lo[(int64_t)ok + q];                                                 \
+        } else {                                                                           \
+          const int ck = bcast_i<LPR, (K)>(c);                                             \
+          x[(K)] = xs.lo[(int64_t)ck * xs.ld4 + q];                                        \
+        }                                                                                  \
+      }
+      FR_PG(0) FR_PG(1) FR_PG(2) FR_PG(3) FR_PG(4) FR_PG(5) FR_PG(6) FR_PG(7)
+      FR_PG(8) FR_PG(9) FR_PG(10) FR_PG(11) FR_PG(12) FR_PG(13) FR_PG(14) FR_PG(15)
+#undef FR_PG
+      if (e + LPR < e1) load_batch(col, val, e + LPR, e1, q, c, v);
+#pragma unroll
+      for (int k = 0; k < LPR; ++k) acc = f4_fma(w[k], x[k], acc);
+    }
+    if (ep.Y1.lo) reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y1, r, ep.split)))[q] = acc;
+    if (ep.Y2.lo) {
+      float4 o = f4_scale(ep.alpha, acc);
+      if (has_a1) o = f4_fma(ep.beta1, a1, o);
+      if (has_a2) o = f4_fma(ep.beta2, a2, o);
+      reinterpret_cast<float4*>(const_cast<float*>(tab_row(ep.Y2, r, ep.split)))[q] = o;
+    }
+  }
+}
+
+// fr_rows_frontier: mark[i] = 1 for the item columns of the batch users' rows of a [users | items]
+// adjacency (columns U + i) and for the batch items; count reset for the compaction.  One wave per
+// batch triple.
+__global__ __launch_bounds__(256) void frontier_mark_kernel(const int64_t* __restrict__ rowptr,
+                                                            const int32_t* __restrict__ col, int64_t U, int64_t I,
+                                                            const int64_t* __restrict__ uu,
+                                                            const int64_t* __restrict__ pp,
+                                                            const int64_t* __restrict__ nn, int64_t B,
+                                                            uint8_t* __restrict__ mark, int32_t* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (blockIdx.x == 0 && threadIdx.x == 0) count[0] = 0;
+  if (b >= B) return;
+  const int64_t u = uu[b];
+  for (int64_t e = rowptr[u] + lane; e < rowptr[u + 1]; e += 64) {
+    const int64_t i = (int64_t)col[e] - U;
+    if (i >= 0 && i < I) mark[i] = 1;
+  }
+  if (lane == 0) {
+    if (pp[b] >= 0 && pp[b] < I) mark[pp[b]] = 1;
+    if (nn[b] >= 0 && nn[b] < I) mark[nn[b]] = 1;
+  }
+}
+
+// the marked items appended to list (order: arbitrary -- each listed row is computed on its own) and
+// unmarked for the next step; one atomic per wave
+__global__ __launch_bounds__(256) void frontier_compact_kernel(uint8_t* __restrict__ mark, int64_t I,
+                                                               int32_t* __restrict__ list, int32_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool on = i < I && mark[i] != 0;
+  const uint64_t bal = __ballot(on);
+  if (bal == 0) return;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(count, __popcll(bal));
+  base = __shfl(base, 0, 64);
+  if (on) {
+    const int k = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    list[base + k] = (int32_t)i;
+    mark[i] = 0;
+  }
+}
+
 template <int LPR, bool SPLIT, bool MASK>
 hipError_t launch_units(const int64_t* rowptr, const int32_t* col, const float* val,
                         const fr_spmm_plan* plan, const XSrc& xs, int d4, const Epi& ep,
@@ -997,6 +1100,48 @@ extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d
   else
     hipLaunchKernelGGL(spmm_sparse_kernel<true>, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_rowptr,
                        d_col, d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_rows_frontier(const int64_t* d_rowptr, const int32_t* d_col, int64_t U, int64_t I,
+                                const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B, uint8_t* d_mark,
+                                int32_t* d_list, int32_t* d_count, void* stream) {
+  FR_REQUIRE(U >= 0 && I > 0 && I < (int64_t)INT32_MAX && B >= 1, "bad sizes");
+  FR_REQUIRE(d_rowptr && d_col && d_u && d_p && d_n && d_mark && d_list && d_count, "null argument");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(frontier_mark_kernel, dim3((unsigned)fr::ceil_div(B, (int64_t)4)), dim3(256), 0, s, d_rowptr,
+                     d_col, U, I, d_u, d_p, d_n, B, d_mark, d_count);
+  FR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(frontier_compact_kernel, dim3((unsigned)fr::ceil_div(I, (int64_t)256)), dim3(256), 0, s, d_mark,
+                     I, d_list, d_count);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_spmm_csr_list(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                                int64_t split, const fr_tab* X, const fr_tab* Y1, const fr_tab* Y2, float alpha,
+                                const fr_tab* A1, float beta1, const fr_tab* A2, float beta2, const int32_t* d_list,
+                                const int32_t* d_count, int64_t max_rows, void* stream) {
+  FR_REQUIRE(n_rows >= 0 && max_rows >= 0 && max_rows <= n_rows, "bad sizes");
+  if (max_rows == 0) return FR_OK;
+  FR_REQUIRE(d_rowptr && d_col && d_val && X && X->lo && d_list && d_count, "null argument");
+  FR_REQUIRE((Y1 && Y1->lo) || (Y2 && Y2->lo), "no output requested");
+  FR_REQUIRE(tab_ok(X, 64) && tab_ok(Y1, 64) && tab_ok(Y2, 64) && tab_ok(A1, 64) && tab_ok(A2, 64),
+             "tables must be 16-B aligned fp32 [*, 64] (d = 64)");
+  for (const fr_tab* y : {Y1, Y2})
+    FR_REQUIRE(!(y && (tab_touches(y, X->lo) || tab_touches(y, X->hi))), "outputs must not alias X");
+  Epi ep{host_tab(Y1), host_tab(Y2), alpha, host_tab(A1), beta1, host_tab(A2), beta2, split, nullptr};
+  XSrc xs{reinterpret_cast<const float4*>(X->lo), X->ld_lo >> 2, reinterpret_cast<const float4*>(X->hi),
+          X->hi ? (X->ld_hi >> 2) : 0, X->hi ? split : INT64_MAX, nullptr};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(max_rows, 16), (int64_t)fr::kNumCU * 8));
+  if (xs.hi)
+    hipLaunchKernelGGL(spmm_list16_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, d_rowptr, d_col, d_val,
+                       d_list, d_count, xs, ep);
+  else
+    hipLaunchKernelGGL(spmm_list16_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, d_rowptr, d_col, d_val,
+                       d_list, d_count, xs, ep);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
