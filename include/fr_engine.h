@@ -774,6 +774,17 @@ int fr_spmm_csr_list(const int64_t* d_rowptr, const int32_t* d_col, const float*
                      const fr_tab* X, const fr_tab* Y1, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
                      const fr_tab* A2, float beta2, const int32_t* d_list, const int32_t* d_count, int64_t max_rows,
                      void* stream);
+/* fr_spmm_list_scatter: Y[c - split] += alpha * A[r][c] * X[r] over the listed rows r (d_list[0 ..
+ *   *d_count), max_rows bounds it) and their columns c >= split; zero_first: Y's n_rows - split rows
+ *   set to 0 first (same stream).  For a SYMMETRIC adjacency and an X zero outside the list this is
+ *   Y = alpha * (A X)[split:], the side rows of a transpose product at cost proportional to the listed
+ *   rows' degrees (HealthRec's RI backward, first launch of the bipartite two-layer form,
+ *   cikm_model.py:185-208).  Float atomics: summation order unspecified.  X: fp32 [*, 64] (ldx),
+ *   Y: fp32 [n_rows - split, 64] (ldy), not aliasing X. */
+int fr_spmm_list_scatter(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                         int64_t split, const int32_t* d_list, const int32_t* d_count, int64_t max_rows,
+                         const float* d_X, int64_t ldx, float* d_Y, int64_t ldy, float alpha, int zero_first,
+                         void* stream);
 int fr_rows_mark(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, void* stream);
 int fr_rows_mark_zero(uint8_t* d_mask, const fr_rowlist* rows, uint8_t value, float* d_Z, int64_t ldz, int d,
                       uint32_t* d_bits, void* stream);

@@ -69,7 +69,9 @@ _SIGS = {
     "fr_spmm_csr_list": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, POINTER(FrTab), POINTER(FrTab),
                                  POINTER(FrTab), c_float, POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p,
                                  c_void_p, c_int64, c_void_p]),
-    "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
+    "fr_spmm_list_scatter": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                                     c_void_p, c_int64, c_void_p, c_int64, c_float, c_int, c_void_p]),
+    "fr_rows_mark":(c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
     "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p,
                                   c_void_p]),
     "fr_spmm_scatter_upstream": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

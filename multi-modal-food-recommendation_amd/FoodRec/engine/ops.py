@@ -943,10 +943,24 @@ def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None, gate=False)
     spmm_ex(adj, H, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=1.0, A1=G, beta1=inv)
 
 
-def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split):
+def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None):
     """The RI backward of graph_bpr (G zero at the ingredient rows): the half-graph form on a
-    bipartite adjacency with two layers, _prop_bwd_split otherwise."""
+    bipartite adjacency with two layers, _prop_bwd_split otherwise.  ``front``: the forward's
+    frontier list (lst, cnt) when G's item rows are zero outside it (the fast UI backward writes
+    them from the batch rows only) -- the ingredient rows R^T g / 3 are then the listed rows'
+    scatter (fr_spmm_list_scatter) instead of a gather over every ingredient row."""
     if L == 2 and adj.bipartite_split == split and not _RI_FULL_GRAPH:
+        if front is not None and adj.symmetric:
+            inv = 1.0 / 3.0
+            g = G[:split]
+            lst, cnt = front
+            with profiling.region("spmm_rows", 0):
+                native.check(native.lib().fr_spmm_list_scatter(
+                    adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], split,
+                    lst.data_ptr(), cnt.data_ptr(), split, g.data_ptr(), g.stride(0), out_hi.data_ptr(),
+                    out_hi.stride(0), _f(inv), 1, native.stream_of(g)), "fr_spmm_list_scatter")
+            spmm_range(adj, g, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=g, beta1=inv)
+            return
         _prop_bwd_bipartite2(adj, G[:split], out_lo, out_hi, split)
     else:
         _prop_bwd_split(adj, G, L, out_lo, out_hi, split)
@@ -979,19 +993,23 @@ def grad_buffer(w: torch.Tensor) -> torch.Tensor:
 
 # FR_RI_FRONTIER=0: HealthRec's RI forward at every item row (full layer 1, item rows of layer 2)
 RI_FRONTIER = os.environ.get("FR_RI_FRONTIER", "1") != "0"
+# FR_RI_FRONTIER_BWD=0: the RI backward's ingredient rows gathered over every ingredient row instead
+# of scattered from the frontier rows (the only item rows of its upstream gradient that are non-zero)
+RI_FRONTIER_BWD = os.environ.get("FR_RI_FRONTIER_BWD", "1") != "0"
 
 
 def _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n):
     """mean(E, A E, A^2 E) of the bipartite RI graph at the item rows the batch's UI layer reads:
     layer 1 over every ingredient row (layer 2 reads them all) and at the listed item rows, layer 2
-    at the listed item rows.  Rows outside the list are left unwritten (nothing reads them)."""
+    at the listed item rows.  Rows outside the list are left unwritten (nothing reads them).
+    Returns (rows, (list, count)); the list (this forward's own buffers) also serves the backward."""
     dev = item_w.device
     N = ri_adj.shape[0]
     lib = native.lib()
     s = native.stream_of(item_w)
     mark = _persistent(ri_adj, ("front_mark", str(dev)), lambda: torch.zeros(I, dtype=torch.uint8, device=dev))
-    lst = _persistent(ri_adj, ("front_list", str(dev)), lambda: torch.empty(I, dtype=torch.int32, device=dev))
-    cnt = _persistent(ri_adj, ("front_cnt", str(dev)), lambda: torch.zeros(1, dtype=torch.int32, device=dev))
+    lst = torch.empty(I, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)  # (reset by fr_rows_frontier)
     native.check(lib.fr_rows_frontier(ui_adj.rowptr.data_ptr(), ui_adj.col.data_ptr(), U, I, u.data_ptr(), p.data_ptr(),
                                       n.data_ptr(), int(u.numel()), mark.data_ptr(), lst.data_ptr(), cnt.data_ptr(), s),
                  "fr_rows_frontier")
@@ -1009,13 +1027,13 @@ def _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n):
                                           ctypes.byref(_tab(out)), _f(inv), ctypes.byref(_tab(item_w, ingre_w)),
                                           _f(inv), ctypes.byref(_tab(E1)), _f(inv), lst.data_ptr(), cnt.data_ptr(), I,
                                           s), "fr_spmm_csr_list")  # layer 2, listed item rows
-    return out
+    return out, (lst, cnt)
 
 
 class _GraphBprForward:
     """The forward of _GraphBpr computed ahead of its autograd node (graph_bpr_begin), possibly on a
     branch stream: the outputs and the tensors the backward reads."""
-    __slots__ = ("out", "item_rows", "ui_all", "u", "p", "n", "pn", "ws", "stream", "done", "args", "defer")
+    __slots__ = ("out", "item_rows", "ui_all", "u", "p", "n", "pn", "ws", "stream", "done", "args", "defer", "front")
 
 
 @torch.no_grad()
@@ -1028,11 +1046,12 @@ def _graph_bpr_forward(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_r
             raise native.EngineError("graph_bpr: contiguous fp32 [rows, 64] tables required")
     u, p, n, pn = (x.to(torch.int64).contiguous() for x in (u, p, n, pn))
     rows = [(u, 0), (p, U), (n, U)]
-    if L_ui == 1 and L_ri == 2 and ri_adj.bipartite_split == I and RI_FRONTIER:
+    if L_ui == 1 and L_ri == 2 and ri_adj.bipartite_split == I and ui_adj.bipartite_split == U and RI_FRONTIER:
         # the UI layer at the batch rows reads item_ir only at the batch users' items and the batch
         # items: the RI propagation's item rows are evaluated there only (device-built row list)
-        ir_all = _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n)
+        ir_all, front = _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n)
     else:
+        front = None
         # [I + NI, 64]; only the item rows are read (the reference discards the propagated ingredients)
         ir_all = _prop_fwd_split(ri_adj, item_w, ingre_w, I, L_ri, lo_rows_only=True)
     if L_ui == 1:
@@ -1054,6 +1073,7 @@ def _graph_bpr_forward(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_r
     f = _GraphBprForward()
     f.out, f.item_rows, f.ui_all, f.u, f.p, f.n, f.pn, f.ws, f.stream = out, item_rows, ui_all, u, p, n, pn, ws, stream
     f.defer = ingre_w.__dict__.get("_fr_defer_rows")
+    f.front = front if RI_FRONTIER_BWD else None
     return f
 
 
@@ -1084,6 +1104,7 @@ class _GraphBpr(torch.autograd.Function):
         ctx.ingre_w = ingre_w  # the parameter itself (grad_buffer looks up its gradient destination)
         ctx.defer = pre.defer  # (taken at the forward's start: embedding_norms pops the slot meanwhile)
         ctx.branch = pre.stream  # the branch stream the forward ran on (None: the current stream)
+        ctx.front = pre.front  # the RI frontier rows (list, count), or None
         ctx.meta = (ri_adj, ui_adj, L_ri, L_ui, gamma, int(bool(det)), ws, U, I, NI)
         return out[0], out[4:5], item_rows
 
@@ -1213,7 +1234,8 @@ class _GraphBpr(torch.autograd.Function):
             _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
         d_item = grad_buffer(item_w)
         d_ingre = grad_buffer(ctx.ingre_w)
-        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
+        # (the fast UI backward writes G_ri's item rows from the batch rows: non-zero at the frontier only)
+        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I, front=ctx.front)
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),

@@ -15,7 +15,10 @@ def ui_adjacency(dataset, n_users, n_items, device, chunk=DEFAULT_CHUNK) -> Adja
     coo = dataset.train_coo_matrix
     rows = np.asarray(coo.row, np.int64)
     cols = np.asarray(coo.col, np.int64) + n_users
-    return Adjacency.sym_normalized(n_users + n_items, rows, cols, device=device, chunk=chunk)
+    adj = Adjacency.sym_normalized(n_users + n_items, rows, cols, device=device, chunk=chunk)
+    # users connect only to items and items only to users
+    adj.mark_bipartite(n_users)
+    return adj
 
 
 def side_adjacency(triples, n_items, n_side, device, chunk=DEFAULT_CHUNK) -> Adjacency:

@@ -614,6 +614,39 @@ __global__ __launch_bounds__(256) void spmm_list16_kernel(const int64_t* __restr
   }
 }
 
+// fr_spmm_list_scatter: Y[c - split] += alpha * A[r][c] * X[r] for the listed rows r (count read on the
+// device) and their columns c >= split -- the transpose product A^T X restricted to the side rows, for
+// an X that is zero outside the list (A symmetric: the side rows' gather becomes the listed rows'
+// scatter, work proportional to the listed rows' degrees).  One wave per listed row, lane = column:
+// each edge is one 256-B float-atomic wave instruction; the row's edges are read 64 at a time
+// (coalesced) and broadcast from their lanes.
+__global__ __launch_bounds__(256) void list_scatter_kernel(const int64_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const float* __restrict__ val,
+                                                           const int32_t* __restrict__ list,
+                                                           const int32_t* __restrict__ d_count, int64_t split,
+                                                           const float* __restrict__ X, int64_t ldx,
+                                                           float* __restrict__ Y, int64_t ldy, float alpha) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = d_count[0];
+  const int64_t W = (int64_t)gridDim.x * 4;
+  for (int64_t j = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); j < n; j += W) {
+    const int64_t r = list[j];
+    const float x = alpha * X[r * ldx + lane];
+    const int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
+    for (int64_t e = e0; e < e1; e += 64) {
+      const int m = (int)min((int64_t)64, e1 - e);
+      const int cl = lane < m ? col[e + lane] : 0;
+      const float vl = lane < m ? val[e + lane] : 0.f;
+      for (int k = 0; k < m; ++k) {
+        const int64_t c = (int64_t)__builtin_amdgcn_readlane(cl, k);
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vl), k));
+        if (c >= split) atomicAdd(Y + (c - split) * ldy + lane, v * x);
+      }
+    }
+  }
+}
+
 // fr_rows_frontier: mark[i] = 1 for the item columns of the batch users' rows of a [users | items]
 // adjacency (columns U + i) and for the batch items; count reset for the compaction.  One wave per
 // batch triple.
@@ -1142,6 +1175,34 @@ extern "C" int fr_spmm_csr_list(const int64_t* d_rowptr, const int32_t* d_col, c
   else
     hipLaunchKernelGGL(spmm_list16_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, d_rowptr, d_col, d_val,
                        d_list, d_count, xs, ep);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_spmm_list_scatter(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                    int64_t n_rows, int64_t split, const int32_t* d_list, const int32_t* d_count,
+                                    int64_t max_rows, const float* d_X, int64_t ldx, float* d_Y, int64_t ldy,
+                                    float alpha, int zero_first, void* stream) {
+  FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX && split >= 0 && split <= n_rows && max_rows >= 0 &&
+                 max_rows <= n_rows,
+             "bad sizes");
+  FR_REQUIRE(d_rowptr && d_col && d_val && d_list && d_count && d_X && d_Y, "null argument");
+  FR_REQUIRE(ldx >= 64 && ldy >= 64, "X / Y must be fp32 [*, 64] tables");
+  const float* y_end = d_Y + (n_rows - split) * ldy;
+  FR_REQUIRE(!(d_X < y_end && d_Y < d_X + max_rows * ldx), "Y must not alias X");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (zero_first && n_rows > split) {
+    if (ldy == 64) {
+      FR_HIP_CHECK(hipMemsetAsync(d_Y, 0, (size_t)(n_rows - split) * 64 * sizeof(float), s));
+    } else {
+      FR_HIP_CHECK(hipMemset2DAsync(d_Y, (size_t)ldy * sizeof(float), 0, 64 * sizeof(float),
+                                    (size_t)(n_rows - split), s));
+    }
+  }
+  if (max_rows == 0) return FR_OK;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(fr::ceil_div(max_rows, 4), (int64_t)fr::kNumCU * 8));
+  hipLaunchKernelGGL(list_scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_rowptr, d_col, d_val, d_list,
+                     d_count, split, d_X, ldx, d_Y, ldy, alpha);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -895,14 +895,19 @@ def test_spmm_scatter_upstream(cuda, frac):
     assert int(mask.sum()) == 0
 
 
-def test_healthrec_graph_bpr_matches_unfused(cuda):
+@pytest.mark.parametrize("front", [(True, True), (True, False), (False, False)])
+def test_healthrec_graph_bpr_matches_unfused(cuda, front, monkeypatch):
     """ops.graph_bpr (split-table propagation, UI rows of the batch only, masked UI backward,
     gradients written into the parameters' buffers) against the concatenated full propagation +
-    fused BPR op it replaces: losses rel 1e-6, every gradient 1e-5 of its max."""
+    fused BPR op it replaces: losses rel 1e-6, every gradient 1e-5 of its max.  ``front``: the RI
+    forward at the frontier item rows only / the RI backward's ingredient rows scattered from them."""
     from helpers import golden, tiny_config, tiny_data
     from FoodRec.common.trainer import Trainer
+    from FoodRec.engine import ops
     from FoodRec.models import healthrec
     from FoodRec.utils.utils import get_model, init_seed
+    monkeypatch.setattr(ops, "RI_FRONTIER", front[0])
+    monkeypatch.setattr(ops, "RI_FRONTIER_BWD", front[1])
     g = golden("model_CIKM_Model.npz")
     batch = {k[len("batch/"):]: torch.from_numpy(g[k]).to(cuda) for k in g.files if k.startswith("batch/")}
     runs = []
