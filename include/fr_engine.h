@@ -761,7 +761,7 @@ int fr_spmm_csr_range(const int64_t* d_rowptr, const int32_t* d_col, const float
                       const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, const fr_tab* A2, float beta2,
                       int64_t row_lo, int64_t row_hi, void* d_workspace, int64_t workspace_bytes, void* stream);
 /* Device-built row lists (HealthRec's RI forward evaluated at the item rows its UI layer reads):
- * fr_rows_frontier marks, in d_mark [I] (zero on entry, left zero), the item columns (U + i) of the
+ * fr_rows_frontier marks, in d_mark [I] (4-B aligned; zero on entry, left zero), the item columns (U + i) of the
  *   batch users' rows of a [users | items] CSR and the batch items p, n, then writes them to d_list and
  *   their number to d_count (order arbitrary).  Two launches.
  * fr_spmm_csr_list: fr_spmm_csr_ex's epilogue (split tables, Y1 / Y2 / A1 / A2) for the rows

@@ -672,21 +672,47 @@ __global__ __launch_bounds__(256) void frontier_mark_kernel(const int64_t* __res
 }
 
 // the marked items appended to list (order: arbitrary -- each listed row is computed on its own) and
-// unmarked for the next step; one atomic per wave
+// unmarked for the next step.  Each thread takes 4 marks (one 32-bit load), the block scans its
+// counts (wave shuffles + LDS) and takes its list range with ONE atomic: a 1024-item block per
+// atomic instead of a wave per atomic (the counter is the serialisation point).
+constexpr int kCompactItems = 1024;
 __global__ __launch_bounds__(256) void frontier_compact_kernel(uint8_t* __restrict__ mark, int64_t I,
                                                                int32_t* __restrict__ list, int32_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool on = i < I && mark[i] != 0;
-  const uint64_t bal = __ballot(on);
-  if (bal == 0) return;
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (lane == 0) base = atomicAdd(count, __popcll(bal));
-  base = __shfl(base, 0, 64);
-  if (on) {
-    const int k = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-    list[base + k] = (int32_t)i;
-    mark[i] = 0;
+  __shared__ int wsum[4];
+  __shared__ int base_s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kCompactItems + 4 * t;
+  uint32_t m = 0;
+  if (i0 + 3 < I) {
+    m = *reinterpret_cast<const uint32_t*>(mark + i0);  // (mark 4-B aligned: host check)
+  } else {
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k < I && mark[i0 + k]) m |= 1u << (8 * k);
+  }
+  int c = 0;
+  for (int k = 0; k < 4; ++k) c += ((m >> (8 * k)) & 0xffu) != 0;
+  int x = c;  // inclusive wave scan
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    base_s = tot ? atomicAdd(count, tot) : 0;
+  }
+  __syncthreads();
+  int off = base_s + x - c;
+  for (int k = 0; k < w; ++k) off += wsum[k];
+  if (m == 0) return;
+  for (int k = 0; k < 4; ++k)
+    if ((m >> (8 * k)) & 0xffu) list[off++] = (int32_t)(i0 + k);
+  if (i0 + 3 < I) {
+    *reinterpret_cast<uint32_t*>(mark + i0) = 0u;
+  } else {
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k < I) mark[i0 + k] = 0;
   }
 }
 
@@ -1142,11 +1168,12 @@ extern "C" int fr_rows_frontier(const int64_t* d_rowptr, const int32_t* d_col, i
                                 int32_t* d_list, int32_t* d_count, void* stream) {
   FR_REQUIRE(U >= 0 && I > 0 && I < (int64_t)INT32_MAX && B >= 1, "bad sizes");
   FR_REQUIRE(d_rowptr && d_col && d_u && d_p && d_n && d_mark && d_list && d_count, "null argument");
+  FR_REQUIRE((reinterpret_cast<uintptr_t>(d_mark) & 3u) == 0, "mark must be 4-B aligned");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(frontier_mark_kernel, dim3((unsigned)fr::ceil_div(B, (int64_t)4)), dim3(256), 0, s, d_rowptr,
                      d_col, U, I, d_u, d_p, d_n, B, d_mark, d_count);
   FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(frontier_compact_kernel, dim3((unsigned)fr::ceil_div(I, (int64_t)256)), dim3(256), 0, s, d_mark,
+  hipLaunchKernelGGL(frontier_compact_kernel, dim3((unsigned)fr::ceil_div(I, (int64_t)kCompactItems)), dim3(256), 0, s, d_mark,
                      I, d_list, d_count);
   FR_LAUNCH_CHECK();
   return FR_OK;

@@ -1059,3 +1059,54 @@ def test_ui_bpr_matches_unfused(cuda):
     torch.testing.assert_close(ra, rb, rtol=1e-6, atol=0)
     for a, b in zip(ga, gb):
         assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-9
+
+
+@pytest.mark.parametrize("n_items", [2051, 4096])
+def test_rows_frontier_and_list_scatter(cuda, n_items):
+    """fr_rows_frontier: the list holds exactly the batch users' item columns and the batch items
+    (each once), the mark buffer is left zero, for item counts off and on the compaction's
+    4-item / 1024-item granules.  fr_spmm_list_scatter over that list on a bipartite RI graph:
+    (alpha A X)[split:] for an X zero outside the list, vs float64, with Y's garbage zeroed first."""
+    from FoodRec.engine import native
+    lib = native.lib()
+    s = native.stream_of(torch.empty(0, device=cuda))
+    U, I, B = 300, n_items, 128
+    r, c = _graph(U, I, 6.0, seed=11)
+    ui = _adj(U + I, r, c + U, cuda)
+    g = torch.Generator().manual_seed(2)
+    u = torch.randint(0, U, (B,), generator=g)
+    p, n = (torch.randint(0, I, (B,), generator=g) for _ in range(2))
+    mark = torch.zeros(I, dtype=torch.uint8, device=cuda)
+    lst = torch.full((I,), -7, dtype=torch.int32, device=cuda)
+    cnt = torch.full((1,), 99, dtype=torch.int32, device=cuda)
+    ud, pd, nd = (x.to(cuda) for x in (u, p, n))
+    for _ in range(2):  # the second call starts from the mark buffer the first left behind
+        native.check(lib.fr_rows_frontier(ui.rowptr.data_ptr(), ui.col.data_ptr(), U, I, ud.data_ptr(), pd.data_ptr(),
+                                          nd.data_ptr(), B, mark.data_ptr(), lst.data_ptr(), cnt.data_ptr(), s),
+                     "fr_rows_frontier")
+        torch.cuda.synchronize()
+        k = int(cnt.item())
+        rp, col = ui.rowptr.cpu(), ui.col.cpu()
+        want = set(p.tolist()) | set(n.tolist())
+        for x in u.tolist():
+            want |= {int(cc) - U for cc in col[int(rp[x]):int(rp[x + 1])].tolist() if cc >= U}
+        got = lst[:k].cpu().tolist()
+        assert len(got) == len(set(got)) and set(got) == want
+        assert int(mark.sum()) == 0
+    NI = 700
+    r2, c2 = _graph(I, NI, 5.0, seed=12)
+    ri = _adj(I + NI, r2, c2 + I, cuda)
+    X = torch.zeros(I, 64)
+    X[torch.tensor(got, dtype=torch.int64)] = torch.randn(len(got), 64, generator=g)
+    Y = torch.full((NI + 1, 64), 3.5, device=cuda)
+    alpha = 1.0 / 3.0
+    Xd = X.to(cuda)
+    native.check(lib.fr_spmm_list_scatter(ri.rowptr.data_ptr(), ri.col.data_ptr(), ri.val.data_ptr(), I + NI, I,
+                                          lst.data_ptr(), cnt.data_ptr(), I, Xd.data_ptr(), 64, Y.data_ptr(), 64,
+                                          alpha, 1, s), "fr_spmm_list_scatter")
+    torch.cuda.synchronize()
+    A = torch.sparse_csr_tensor(ri.rowptr.cpu(), ri.col.cpu().long(), ri.val.cpu().double(),
+                                (I + NI, I + NI)).to_dense()
+    ref = alpha * (A @ torch.cat([X.double(), torch.zeros(NI, 64, dtype=torch.float64)]))[I:]
+    torch.testing.assert_close(Y[:NI].cpu().double(), ref, rtol=0, atol=2e-6)
+    assert torch.equal(Y[NI:].cpu(), torch.full((1, 64), 3.5))  # rows past n_rows - split untouched
