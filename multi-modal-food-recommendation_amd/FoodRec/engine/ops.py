@@ -948,7 +948,9 @@ def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None):
     bipartite adjacency with two layers, _prop_bwd_split otherwise.  ``front``: the forward's
     frontier list (lst, cnt) when G's item rows are zero outside it (the fast UI backward writes
     them from the batch rows only) -- the ingredient rows R^T g / 3 are then the listed rows'
-    scatter (fr_spmm_list_scatter) instead of a gather over every ingredient row."""
+    scatter (fr_spmm_list_scatter, which zeroes them first) instead of a gather over every
+    ingredient row.  (Zeroing d ingre at the backward's start instead, ahead of the UI backward,
+    measured ~5 us/step slower.)"""
     if L == 2 and adj.bipartite_split == split and not _RI_FULL_GRAPH:
         if front is not None and adj.symmetric:
             inv = 1.0 / 3.0

@@ -11,8 +11,12 @@
 //
 // Forward: 16 x 16 output tiles on v_mfma_f32_16x16x4_f32 (exact f32).  Each lane group h of a wave
 // holds k = 4h..4h+3 of a 16-wide k chunk, so one float4 of the gathered row and one float4 of a W
-// row feed four MFMAs.  (A K split over workgroups with an in-kernel ticket reduction measured slower:
-// its device-scope fences cost more than the split saved.)
+// row feed four MFMAs.  KW = 16 waves split K: the problem is small (n = 2B = 1024 rows), so each
+// wave's share of K is loaded in one or two rounds of four chunks (15.8 us against 16.4 us with 4
+// waves over K at 1024 x (2048 + 512); one workgroup per 16 rows x all 64 columns, which reads each
+// gathered row once, measured 27 us: half the CUs idle).
+// (A K split over workgroups with an in-kernel ticket reduction measured slower: its device-scope
+// fences cost more than the split saved.)
 #include "fr_common.h"
 
 #include <algorithm>
@@ -23,27 +27,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int D = 64;            // output width (embedding size)
 constexpr int WAVES = 4;
+constexpr int KW = 16;           // waves over K per gathered-row tile (gather_linear_rows)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// One workgroup per (16-row tile, 16-column tile): its four waves take contiguous quarters of K
-// (loads of four 16-wide chunks issued before their sixteen MFMAs), then the four partial tiles are
-// added in wave order through LDS and the bias added: no cross-workgroup traffic, deterministic.
-__device__ __forceinline__ void gather_linear_tile(const int64_t* __restrict__ ids, int64_t n,
+// One workgroup per (16-row tile, 16-column tile): wave w takes chunks [C w / KW, C (w+1) / KW) of
+// the C = K / 16 k chunks; the KW partial tiles are added in wave order through LDS and the bias
+// added: no cross-workgroup traffic, deterministic.
+__device__ __forceinline__ void gather_linear_rows(const int64_t* __restrict__ ids, int64_t n,
                                                    const float* __restrict__ X, int64_t ldx, int K,
                                                    const float* __restrict__ W, const float* __restrict__ b,
-                                                   float* __restrict__ Y, int64_t ldy) {
-  __shared__ float red[WAVES][256];
+                                                   float* __restrict__ Y, int64_t ldy, int col0) {
+  __shared__ float red[KW][256];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = l & 15, h = l >> 4;
   const int64_t i = (int64_t)blockIdx.x * 16 + r;
-  const int col0 = blockIdx.y * 16;
   const float* __restrict__ xr = X + ids[i < n ? i : n - 1] * ldx;
   const float* __restrict__ wr = W + (int64_t)(col0 + r) * K;
   const int chunks = K / 16;
-  const int q0 = chunks * w / WAVES, q1 = chunks * (w + 1) / WAVES;
+  const int q0 = chunks * w / KW, q1 = chunks * (w + 1) / KW;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int c = q0; c < q1; c += 4) {
     float4 xa[4], wb[4];
@@ -70,18 +74,20 @@ __device__ __forceinline__ void gather_linear_tile(const int64_t* __restrict__ i
   __syncthreads();
   if (threadIdx.x < 256) {
     const int e = threadIdx.x, rr = e / 16, cc = e % 16;
-    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    float v = red[0][e];
+#pragma unroll
+    for (int k = 1; k < KW; ++k) v += red[k][e];
     const int64_t ii = (int64_t)blockIdx.x * 16 + rr;
     if (ii < n) Y[ii * ldy + col0 + cc] = v + (b ? b[col0 + cc] : 0.f);
   }
 }
 
-__global__ __launch_bounds__(64 * WAVES) void gather_linear_kernel(const int64_t* __restrict__ ids, int64_t n,
-                                                                   const float* __restrict__ X, int64_t ldx, int K,
-                                                                   const float* __restrict__ W,
-                                                                   const float* __restrict__ b, float* __restrict__ Y,
-                                                                   int64_t ldy) {
-  gather_linear_tile(ids, n, X, ldx, K, W, b, Y, ldy);
+__global__ __launch_bounds__(64 * KW) void gather_linear_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                const float* __restrict__ X, int64_t ldx, int K,
+                                                                const float* __restrict__ W,
+                                                                const float* __restrict__ b, float* __restrict__ Y,
+                                                                int64_t ldy) {
+  gather_linear_rows(ids, n, X, ldx, K, W, b, Y, ldy, blockIdx.y * 16);
 }
 
 // several tables at the same ids in one launch: blockIdx.z = table, its 64 output columns at 64 t
@@ -94,11 +100,10 @@ struct ProjTabs {
   const float* b[kMaxProj];
 };
 
-__global__ __launch_bounds__(64 * WAVES) void gather_linear_multi_kernel(const int64_t* __restrict__ ids, int64_t n,
-                                                                         ProjTabs P, float* __restrict__ Y,
-                                                                         int64_t ldy) {
+__global__ __launch_bounds__(64 * KW) void gather_linear_multi_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                                      ProjTabs P, float* __restrict__ Y, int64_t ldy) {
   const int t = blockIdx.z;
-  gather_linear_tile(ids, n, P.X[t], P.ldx[t], P.K[t], P.W[t], P.b[t], Y + (int64_t)t * D, ldy);
+  gather_linear_rows(ids, n, P.X[t], P.ldx[t], P.K[t], P.W[t], P.b[t], Y + (int64_t)t * D, ldy, blockIdx.y * 16);
 }
 
 // out[i, c] = sum_k S[i, k] W[k, c] for k < 64: 16 rows x 256 columns per workgroup, wave w the
@@ -175,7 +180,7 @@ extern "C" int fr_gather_linear_fwd(const int64_t* d_ids, int64_t n, const float
              "X rows and W must be 16-byte aligned, ldx >= K, ldy >= 64");
   const int64_t tiles = fr::ceil_div(n, 16);
   FR_REQUIRE(tiles < (1ll << 31), "too many rows");
-  hipLaunchKernelGGL(gather_linear_kernel, dim3((unsigned)tiles, D / 16), dim3(64 * WAVES), 0,
+  hipLaunchKernelGGL(gather_linear_kernel, dim3((unsigned)tiles, D / 16), dim3(64 * KW), 0,
                      reinterpret_cast<hipStream_t>(stream), d_ids, n, d_x, ldx, K, d_w, d_b, d_y, ldy);
   FR_LAUNCH_CHECK();
   return FR_OK;
@@ -209,7 +214,7 @@ extern "C" int fr_gather_linear_fwd_multi(const int64_t* d_ids, int64_t n, int n
   }
   const int64_t tiles = fr::ceil_div(n, 16);
   FR_REQUIRE(tiles < (1ll << 31), "too many rows");
-  hipLaunchKernelGGL(gather_linear_multi_kernel, dim3((unsigned)tiles, D / 16, (unsigned)n_tab), dim3(64 * WAVES), 0,
+  hipLaunchKernelGGL(gather_linear_multi_kernel, dim3((unsigned)tiles, D / 16, (unsigned)n_tab), dim3(64 * KW), 0,
                      reinterpret_cast<hipStream_t>(stream), d_ids, n, P, d_y, ldy);
   FR_LAUNCH_CHECK();
   return FR_OK;
