@@ -7,9 +7,11 @@
 // runs its four Linear layers over M = 2B x 20 = 20480 tokens: the weight gradients are
 // [<=256 x 20480] x [20480 x <=256] -- tiny outputs, a huge reduction.  A library GEMM tiles the
 // output and walks all 20480 rows in one workgroup per tile (~100 us each); here the rows are split
-// into slabs, one workgroup per (slab, 64x64 output tile), each thread holding a 4x4 register tile
-// fed from LDS-staged 16-row sub-tiles (double-buffered in registers), fp32 FMA (exact f32, the rate
-// f32 MFMA would give).  Slab partials are summed in slab order by a second kernel: deterministic.
+// into slabs, one workgroup per (slab, 64x64 output tile): the slab's 128 rows of both operands are
+// loaded into LDS in one round (every load in flight at once: the kernel is latency-bound at these
+// sizes), then each of the four waves runs a 16 x 64 strip of the tile on v_mfma_f32_16x16x4_f32
+// (exact f32 products), db as one more MFMA chain against a ones operand.  Slab partials are summed in
+// slab order by a second kernel: deterministic.
 #include "fr_common.h"
 
 #include <algorithm>
@@ -17,8 +19,11 @@
 namespace {
 
 constexpr int TN = 64, TK = 64;  // output tile
-constexpr int SUB = 16;          // rows per LDS sub-tile
 constexpr int kSlab = 128;       // rows per slab (split-K unit)
+constexpr int LDT = TN + 16;     // LDS row stride (floats): the four row groups of an MFMA fragment read
+                                 // land on disjoint banks
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float4 ld4_masked(const float* base, int64_t ld, int64_t m, int64_t M, int c, int C) {
   if (m < M && c < C) return *reinterpret_cast<const float4*>(base + m * ld + c);
@@ -37,57 +42,57 @@ __device__ __forceinline__ void wgrad_slab(const float* __restrict__ dY, int64_t
                                            int64_t ldx, const int64_t* __restrict__ ids, int64_t M, int N, int K,
                                            int ktiles, float* __restrict__ part, float* __restrict__ pdb,
                                            const int bx, const int by) {
-  __shared__ float4 As[SUB][TN / 4];
-  __shared__ float4 Bs[SUB][TK / 4];
+  __shared__ __attribute__((aligned(16))) float As[kSlab][LDT];  // dY rows of the slab, columns n0..n0+63
+  __shared__ __attribute__((aligned(16))) float Bs[kSlab][LDT];  // X rows of the slab, columns k0..k0+63
   const int t = threadIdx.x;
-  const int tn = t / 16, tk = t % 16;  // compute layout: 4 n x 4 k per thread
-  const int lr = t / 16, lc = t % 16;  // load layout: one float4 of one row per thread (A and B)
   const int n0 = (by / ktiles) * TN, k0 = (by % ktiles) * TK;
   const int64_t m0 = (int64_t)bx * kSlab;
   const int64_t m1 = min(M, m0 + kSlab);
   const bool want_db = pdb != nullptr && (by % ktiles) == 0;
-  float acc[4][4];
+  {  // 128 rows x 16 float4 per operand: 8 + 8 loads per thread, all issued before the LDS stores
+    constexpr int J = kSlab * (TN / 4) / 256;
+    const int r0 = t / 16, c4 = 4 * (t % 16);
+    float4 ra[J], rb[J];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 ra = ld4_masked(dY, ldy, m0 + lr, m1, n0 + lc * 4, N);
-  float4 rb = ldx4(X, ldx, ids, m0 + lr, m1, k0 + lc * 4, K);
-  for (int64_t ms = m0; ms < m1; ms += SUB) {
-    As[lr][lc] = ra;
-    Bs[lr][lc] = rb;
-    __syncthreads();
-    if (ms + SUB < m1) {  // prefetch the next sub-tile while this one is consumed
-      ra = ld4_masked(dY, ldy, ms + SUB + lr, m1, n0 + lc * 4, N);
-      rb = ldx4(X, ldx, ids, ms + SUB + lr, m1, k0 + lc * 4, K);
+    for (int j = 0; j < J; ++j) {
+      ra[j] = ld4_masked(dY, ldy, m0 + r0 + 16 * j, m1, n0 + c4, N);
+      rb[j] = ldx4(X, ldx, ids, m0 + r0 + 16 * j, m1, k0 + c4, K);
     }
 #pragma unroll
-    for (int r = 0; r < SUB; ++r) {
-      const float4 a = As[r][tn];
-      const float4 b = Bs[r][tk];
-      const float av[4] = {a.x, a.y, a.z, a.w};
-      const float bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
-      if (want_db && tk == 0) dbacc = f4_add(dbacc, a);
+    for (int j = 0; j < J; ++j) {
+      *reinterpret_cast<float4*>(&As[r0 + 16 * j][c4]) = ra[j];
+      *reinterpret_cast<float4*>(&Bs[r0 + 16 * j][c4]) = rb[j];
     }
-    __syncthreads();
   }
+  __syncthreads();
+  // wave w: output rows n0 + 16w .. +15, all four 16-column k tiles.  MFMA operands: A[i][kk] =
+  // dY[m][n0 + 16w + i], B[kk][j] = X[m][k0 + 16tt + j] at m = 4s + kk; lane (i16, h4) supplies row /
+  // column i16 at kk = h4
+  const int wave = t >> 6, lane = t & 63, i16 = lane & 15, h4 = lane >> 4;
+  f32x4 acc[4], accb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int st = 0; st < kSlab / 4; ++st) {
+    const int m = 4 * st + h4;
+    const float a = As[m][16 * wave + i16];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+      acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[m][16 * tt + i16], acc[tt], 0, 0, 0);
+    if (want_db) accb = __builtin_amdgcn_mfma_f32_16x16x4f32(a, 1.f, accb, 0, 0, 0);
+  }
+  // C layout: acc[tt][q] = dW[n0 + 16 wave + 4 h4 + q][k0 + 16 tt + i16]
   const int64_t slab = bx;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + tn * 4 + i;
-    const int k = k0 + tk * 4;
-    if (n < N && k < K)
-      *reinterpret_cast<float4*>(part + (slab * N + n) * K + k) =
-          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-  }
-  if (want_db && tk == 0) {
-    const int n = n0 + tn * 4;
-    if (n < N) *reinterpret_cast<float4*>(pdb + slab * N + n) = dbacc;
+  for (int q = 0; q < 4; ++q) {
+    const int n = n0 + 16 * wave + 4 * h4 + q;
+    if (n >= N) continue;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int k = k0 + 16 * tt + i16;
+      if (k < K) part[(slab * N + n) * K + k] = acc[tt][q];
+    }
+    if (want_db && i16 == 0) pdb[slab * N + n] = accb[q];
   }
 }
 
