@@ -127,8 +127,9 @@ def resolve_world(gpus, environ) -> int:
 def _check_launch(args, world, rank):
     """--check-launch: the process-group half of a multi-rank run on the CPU (gloo)."""
     import torch.distributed as dist
+    from FoodRec.engine.dist import init_process_group  # explicit collective timeout (FR_PG_TIMEOUT_S)
     if world > 1:
-        dist.init_process_group("gloo")
+        init_process_group("gloo")
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
         got = dist.get_world_size()
         dist.destroy_process_group()
