@@ -828,6 +828,8 @@ int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col
  *     with r_x = g_reg * d_greg[0] / B / ||.||_F of block x (the norms fr_bpr_fwd left in the
  *     workspace): EmbLoss(u_ego, pos_ego, neg_ego)'s gradient, cikm_model.py:273-279;
  *   d_zero[0 .. zero_n) = 0   (ingre_embedding's padding row, not a graph node).
+ * d_dUe / d_dIe may be NULL (that table's rows skipped: CLUSSL adds the item rows later, into the
+ * item views' gradient, with a second call that has d_dUe and d_mask NULL).
  * One launch instead of three (unmark, EmbLoss scatter, padding-row fill). */
 int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue, int64_t ldue, const float* d_Ie,
                         int64_t ldie, const int64_t* d_u, const int64_t* d_p, const int64_t* d_n, int64_t B,

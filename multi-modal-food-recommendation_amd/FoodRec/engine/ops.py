@@ -308,23 +308,50 @@ def propagate_rows(adj: Adjacency, ego: torch.Tensor, n_layers: int, rows) -> to
     return propagate_mean(adj, ego, n_layers)
 
 
+class _EmbRowsSink:
+    """EmbLoss ego-row gradients of an item table that a later backward node adds into its own
+    gradient of that table (CLUSSL: ui_bpr's item rows, added by the item views' node into its
+    d item): no dense zero-filled buffer for the rows and no autograd sum of the two gradients.
+    Opened by _PropagateLoViews.forward on the table, filled by _UiBpr.backward (which autograd runs
+    first: the views' backward needs its gradient), drained and closed by _PropagateLoViews.backward."""
+    __slots__ = ("open", "entries")
+
+    def __init__(self):
+        self.open, self.entries = True, []
+
+
+# FR_EMB_ROWS_INTO_VIEWS=0: ui_bpr returns its EmbLoss item rows as a dense zero-filled gradient
+EMB_ROWS_INTO_VIEWS = os.environ.get("FR_EMB_ROWS_INTO_VIEWS", "1") != "0"
+
+
 class _PropagateLoViews(torch.autograd.Function):
     """_PropagateLo over several bipartite graphs sharing the item table ``lo`` (CLUSSL's ingredient,
     image-cluster and text-cluster views, pricai_modelx.py:183-226): one node, so the backward
     chains the views' item-row gradients through the SpMM epilogue (A2 = the previous views' sum)
-    instead of leaving autograd a zero-initialised buffer and an add per view."""
+    instead of leaving autograd a zero-initialised buffer and an add per view; the EmbLoss ego rows a
+    ui_bpr node parked in the table's _EmbRowsSink are added into that gradient by one launch, which
+    also zeroes a side table's padding row."""
 
     @staticmethod
     def forward(ctx, adjs, L, lo, *his):
         native.require_device(lo, *his)
         split = lo.shape[0]
         ctx.adjs, ctx.L, ctx.split, ctx.hi_rows = adjs, L, split, [h.shape[0] for h in his]
+        ctx.sink = None
+        if EMB_ROWS_INTO_VIEWS and lo.requires_grad and not _DETERMINISTIC:
+            ctx.sink = lo.__dict__["_fr_emb_rows"] = _EmbRowsSink()
         return tuple(_prop_fwd_split(adj, lo, hi, split, L, lo_rows_only=True)[:split] for adj, hi in zip(adjs, his))
 
     @staticmethod
     def backward(ctx, *gs):
         split, L = ctx.split, ctx.L
         d_lo, d_his = None, []
+        sink = ctx.sink
+        rows = []
+        if sink is not None:
+            sink.open = False
+            rows, sink.entries = sink.entries, []
+        pad = None  # (the first padding block, zeroed by the EmbLoss rows' launch when there is one)
         for adj, g, hi_rows in zip(ctx.adjs, gs, ctx.hi_rows):
             N = adj.shape[0]
             if g is None:  # a view nothing read
@@ -334,8 +361,11 @@ class _PropagateLoViews(torch.autograd.Function):
             d = g.shape[1]
             out = torch.empty(split, d, dtype=g.dtype, device=g.device)
             d_hi = torch.empty(hi_rows, d, dtype=g.dtype, device=g.device)
-            if hi_rows > N - split:
-                d_hi[N - split:].zero_()  # rows past the graph (e.g. a padding row) get no gradient
+            if hi_rows > N - split:  # rows past the graph (e.g. a padding row) get no gradient
+                if rows and pad is None:
+                    pad = d_hi[N - split:]
+                else:
+                    d_hi[N - split:].zero_()
             if L == 2:
                 _prop_bwd_bipartite2(adj, g, out, d_hi, split, acc=d_lo)
             else:
@@ -346,6 +376,16 @@ class _PropagateLoViews(torch.autograd.Function):
                     out.add_(d_lo)
             d_lo = out
             d_his.append(d_hi)
+        for k, (user_w, item_w, u, p, n, ws, w_emb, ge) in enumerate(rows):
+            if d_lo is None:
+                d_lo = torch.zeros_like(item_w)  # (no view carried a gradient: the rows alone)
+            z = pad if k == 0 else None
+            with profiling.region("bpr_bwd", 0):
+                native.check(native.lib().fr_graph_bpr_finish(
+                    None, 0, user_w.data_ptr(), 64, item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                    int(u.numel()), 64, _f(w_emb), native.ptr(ge), None, d_lo.data_ptr(), native.ptr(z),
+                    0 if z is None else z.numel(), None, ws.data_ptr(), ws.numel(), native.stream_of(d_lo)),
+                    "fr_graph_bpr_finish")
         return (None, None, d_lo) + tuple(d_his)
 
 
@@ -1283,6 +1323,8 @@ class _UiBpr(torch.autograd.Function):
                                        native.stream_of(user_w)), "fr_bpr_fwd_ex")
         ctx.save_for_backward(user_w, item_w, ui_all, u, p, n)
         ctx.meta = (ui_adj, float(gamma), float(w_emb), ws, U, I, tuple(item_hi.shape))
+        sink = item_w.__dict__.get("_fr_emb_rows")
+        ctx.sink = sink if sink is not None and sink.open else None  # (opened by this pass's item views)
         return out[0], out[4:5]
 
     @staticmethod
@@ -1309,13 +1351,18 @@ class _UiBpr(torch.autograd.Function):
         d_user = grad_buffer(user_w)
         d_hi = torch.empty(hi_shape, dtype=torch.float32, device=dev)
         spmm_sparse_upstream(ui_adj, bits, dUI, d_user, d_hi, U, alpha=0.5, beta1=0.5)
-        d_item = torch.zeros_like(item_w)  # the ego item rows' EmbLoss gradient only
+        # the ego item rows' EmbLoss gradient: parked for the item views' backward (which adds it into
+        # its d item), else a dense zero-filled gradient of its own
+        sink = ctx.sink if ctx.sink is not None and ctx.sink.open and g_emb is not None else None
+        d_item = None if sink is not None else torch.zeros_like(item_w)
         with profiling.region("bpr_bwd", 0):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
                                                  _f(0.0 if g_emb is None else w_emb), native.ptr(ge), d_user.data_ptr(),
-                                                 d_item.data_ptr(), None, 0, bits.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                 native.ptr(d_item), None, 0, bits.data_ptr(), ws.data_ptr(), ws.numel(),
                                                  s), "fr_graph_bpr_finish")
+        if sink is not None:
+            sink.entries.append((user_w, item_w, u, p, n, ws, w_emb, ge))
         return d_user, d_hi, d_item, None, None, None, None, None, None
 
 

@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256) void bpr_bwd_atomic64_kernel(
 // The tail of HealthRec's fused propagation backward (fr_graph_bpr_finish): clear the batch rows'
 // column-mask bytes (users at u, items at U + pos / U + neg), add the EmbLoss gradient of the ego
 // rows (the same per-row terms and float atomics as bpr_bwd_atomic_kernel's dUe / dIe branch, with
-// g_reg scaled by d_greg[0]) and zero `zero_n` floats at `zero` (the padding row).
+// g_reg scaled by d_greg[0]; a null dUe / dIe skips that table) and zero `zero_n` floats at `zero`
+// (the padding row).
 __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
     uint8_t* __restrict__ mask, int64_t U, const float* __restrict__ Ue, int64_t ldue,
     const float* __restrict__ Ie, int64_t ldie, const int64_t* __restrict__ uu, const int64_t* __restrict__ pp,
@@ -272,9 +273,11 @@ __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
         atomicAnd(bits + ((U + p) >> 5), ~(1u << ((U + p) & 31)));
         atomicAnd(bits + ((U + n) >> 5), ~(1u << ((U + n) & 31)));
       }
-      atomicAdd(dUe + u * lddue + lane, ru * Ue[u * ldue + lane]);
-      atomicAdd(dIe + p * lddie + lane, rp * Ie[p * ldie + lane]);
-      atomicAdd(dIe + n * lddie + lane, rn * Ie[n * ldie + lane]);
+      if (dUe) atomicAdd(dUe + u * lddue + lane, ru * Ue[u * ldue + lane]);
+      if (dIe) {
+        atomicAdd(dIe + p * lddie + lane, rp * Ie[p * ldie + lane]);
+        atomicAdd(dIe + n * lddie + lane, rn * Ie[n * ldie + lane]);
+      }
     }
     return;
   }
@@ -291,9 +294,11 @@ __global__ __launch_bounds__(256) void graph_bpr_finish_kernel(
       atomicAnd(bits + ((U + n) >> 5), ~(1u << ((U + n) & 31)));
     }
     for (int q = q0; q < d4; q += LPR) {
-      atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
-      atomic_row_add(dIe, p, lddie, q, f4_scale(rp, ld4(Ie, p, ldie, q)));
-      atomic_row_add(dIe, n, lddie, q, f4_scale(rn, ld4(Ie, n, ldie, q)));
+      if (dUe) atomic_row_add(dUe, u, lddue, q, f4_scale(ru, ld4(Ue, u, ldue, q)));
+      if (dIe) {
+        atomic_row_add(dIe, p, lddie, q, f4_scale(rp, ld4(Ie, p, ldie, q)));
+        atomic_row_add(dIe, n, lddie, q, f4_scale(rn, ld4(Ie, n, ldie, q)));
+      }
     }
   }
 }
@@ -731,9 +736,9 @@ extern "C" int fr_graph_bpr_finish(uint8_t* d_mask, int64_t U, const float* d_Ue
                                    float* d_zero, int zero_n, uint32_t* d_bits, void* d_workspace,
                                    int64_t workspace_bytes, void* stream) {
   FR_REQUIRE(B >= 1 && d >= 4 && d % 4 == 0 && U >= 0 && zero_n >= 0, "bad sizes");
-  FR_REQUIRE(d_Ue && d_Ie && d_u && d_p && d_n && d_dUe && d_dIe && (zero_n == 0 || d_zero), "null argument");
-  FR_REQUIRE(fr::aligned16(d_Ue) && fr::aligned16(d_Ie) && fr::aligned16(d_dUe) && fr::aligned16(d_dIe) &&
-                 ldue % 4 == 0 && ldie % 4 == 0 && ldue >= d && ldie >= d,
+  FR_REQUIRE(d_Ue && d_Ie && d_u && d_p && d_n && (zero_n == 0 || d_zero), "null argument");
+  FR_REQUIRE(fr::aligned16(d_Ue) && fr::aligned16(d_Ie) && (!d_dUe || fr::aligned16(d_dUe)) &&
+                 (!d_dIe || fr::aligned16(d_dIe)) && ldue % 4 == 0 && ldie % 4 == 0 && ldue >= d && ldie >= d,
              "tables must be 16-B aligned with ld % 4 == 0");
   FR_REQUIRE(d_workspace && workspace_bytes >= bpr_ws_bytes(B) && fr::aligned16(d_workspace), "workspace too small");
   BprWS w = bpr_ws(d_workspace, B);
