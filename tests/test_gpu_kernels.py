@@ -1061,6 +1061,44 @@ def test_ui_bpr_matches_unfused(cuda):
         assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-9
 
 
+def test_emb_rows_into_views_matches_dense(cuda, monkeypatch):
+    """CLUSSL's step shape: item views (propagate_lo_views, one side table with a padding row) summed
+    into ui_bpr's item input.  The EmbLoss item rows parked by ui_bpr and added by the views' backward
+    (one launch that also zeroes the padding row) vs ui_bpr's dense zero-filled item gradient summed
+    by autograd: every gradient within 1e-5 of its max, the padding row exactly zero."""
+    from FoodRec.engine import ops
+    from FoodRec.engine.graph import Adjacency
+    g = torch.Generator().manual_seed(23)
+    U, I, S, e = 500, 700, 90, 6000
+    r = torch.randint(0, U, (e,), generator=g)
+    c = torch.randint(0, I, (e,), generator=g) + U
+    rows, cols = torch.cat([r, c]), torch.cat([c, r])
+    deg = torch.bincount(rows, minlength=U + I).clamp(min=1).float()
+    ui = Adjacency.from_coo(rows, cols, deg[rows].rsqrt() * deg[cols].rsqrt(), (U + I, U + I), device=cuda)
+    ui.mark_bipartite(U)
+    sides = []
+    for seed in (1, 2):
+        ri, si = _graph(I, S, 3.0, seed=seed)
+        a = _adj(I + S, ri, si + I, cuda)
+        a.mark_bipartite(I)
+        sides.append(a)
+    t0 = [torch.randn(U, 64, generator=g), torch.randn(I, 64, generator=g), torch.randn(S + 1, 64, generator=g),
+          torch.randn(S, 64, generator=g)]
+    u = torch.randint(0, U, (256,), generator=g).to(cuda)
+    p, n = (torch.randint(0, I, (256,), generator=g).to(cuda) for _ in range(2))
+    res = []
+    for into_views in (True, False):
+        monkeypatch.setattr(ops, "EMB_ROWS_INTO_VIEWS", into_views)
+        uw, iw, s1, s2 = (x.clone().to(cuda).requires_grad_(True) for x in t0)
+        v1, v2 = ops.propagate_lo_views(sides, iw, [s1, s2], 2)
+        mf, reg = ops.ui_bpr(ui, uw, v1 + v2, iw, u, p, n, w_emb=0.01)
+        (mf + reg.sum()).backward()
+        res.append((uw.grad, iw.grad, s1.grad, s2.grad))
+    for a, b in zip(*res):
+        assert (a - b).abs().max() <= 1e-5 * b.abs().max() + 1e-9
+    assert torch.equal(res[0][2][S:], torch.zeros(1, 64, device=cuda))
+
+
 @pytest.mark.parametrize("n_items", [2051, 4096])
 def test_rows_frontier_and_list_scatter(cuda, n_items):
     """fr_rows_frontier: the list holds exactly the batch users' item columns and the batch items
