@@ -542,6 +542,7 @@ class Trainer(AbstractTrainer):
     def _opt_step(self, skip_flag):
         if isinstance(self.optimizer, FusedAdam):
             self.optimizer.step(skip_flag=skip_flag)  # the kernels read the NaN flag on the device
+            ops.run_pending_drains()  # (no-op: the step ran them)
         elif not int(skip_flag.item()):
             # other optimisers: the reference returns before optimizer.step() at the first NaN batch
             # (trainer.py:191-193), so the flag is read on the host before stepping
@@ -568,7 +569,11 @@ class Trainer(AbstractTrainer):
         if booked is not None:
             # the loss sum is never materialised for autograd: each part back-propagates with a
             # cached ones seed; the returned loss is fr_step_book's fp32 sum of the parts
-            torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
+            ops.late_drain(self._late_drain_ok())
+            try:
+                torch.autograd.backward(list(parts), grad_tensors=self._ones_like(parts))
+            finally:
+                ops.late_drain(False)
             ops.loss_side_join()
             self._finish_step(state)
             return booked
@@ -592,9 +597,18 @@ class Trainer(AbstractTrainer):
             nan_flag |= torch.isnan(l2.detach().reshape(-1)[0]).to(torch.int32)
             (-1 * self.alpha2 * l2).backward()
         else:
-            loss.backward()
+            ops.late_drain(self._late_drain_ok())
+            try:
+                loss.backward()
+            finally:
+                ops.late_drain(False)
         self._finish_step(state)
         return loss.detach()
+
+    def _late_drain_ok(self) -> bool:
+        """Whether the step's gradients go straight to FusedAdam.step (no clipping, no gradient
+        hook): deferred gradient rows may then be added inside the step (ops.late_drain)."""
+        return not self.clip_grad_norm and self.grad_hook is None and isinstance(self.optimizer, FusedAdam)
 
     def _finish_step(self, state):
         """Gradient hook / clipping, then the optimiser step (common/trainer.py:215-224)."""

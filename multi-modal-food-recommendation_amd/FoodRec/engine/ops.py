@@ -1409,20 +1409,70 @@ def aux_stream(device):
     return s
 
 
+# FR_LATE_DRAIN=0: the deferred ingredient rows are always added at the end of the backward pass
+LATE_DRAIN = os.environ.get("FR_LATE_DRAIN", "1") != "0"
+_LATE_DRAIN = [False]   # set by the trainer around a backward whose gradients FusedAdam.step reads next
+_PENDING_DRAINS = []    # (fork event, deferred rows, table) left by _join_branch in late mode
+
+
+def late_drain(on: bool) -> None:
+    """The trainer's promise for the next backward pass: nothing but FusedAdam.step reads its
+    gradients.  The deferred ingredient rows are then not added at the end of the pass but by
+    run_pending_drains, which FusedAdam.step calls after launching the update of every other
+    tensor: the scatter runs on the branch stream beside that update instead of before it."""
+    _LATE_DRAIN[0] = bool(on) and LATE_DRAIN
+
+
+def pending_drain_params() -> set:
+    return {id(w) for _, _, w in _PENDING_DRAINS}
+
+
+def run_pending_drains() -> None:
+    """Add the rows _join_branch left (late mode) into their tables' gradients on the branch stream,
+    forked where the backward pass ended; the current stream waits for them (before the update of
+    those tables)."""
+    pend = list(_PENDING_DRAINS)
+    _PENDING_DRAINS.clear()
+    for fork, defer, ingre_w in pend:
+        main = torch.cuda.current_stream(ingre_w.device)
+        side = _branch_stream(ingre_w.device)
+        side.wait_event(fork)
+        for idx, G, _ in defer.rows:
+            idx.record_stream(side)
+            G.record_stream(side)
+        if ingre_w.grad is not None:
+            ingre_w.grad.record_stream(side)
+        with torch.cuda.stream(side):
+            _drain_into(defer, ingre_w)
+            done = torch.cuda.Event()
+            done.record(side)
+        main.wait_event(done)
+
+
+def _drain_into(defer, ingre_w):
+    if defer.rows and ingre_w.grad is None:  # (no propagation gradient was adopted: the rows alone)
+        ingre_w.grad = torch.zeros_like(ingre_w)
+    if ingre_w.grad is not None:
+        defer.drain(ingre_w.grad)
+    else:
+        defer.open = False
+
+
 def _join_branch():
     """End of a backward pass that ran graph_bpr's backward on the branch stream: the current stream
-    waits for it, then adds the deferred ingredient rows into d ingre (after both are complete)."""
+    waits for it, then adds the deferred ingredient rows into d ingre (after both are complete) --
+    or, in late mode (late_drain), leaves them to run_pending_drains."""
     pend = list(_BRANCH_PENDING)
     _BRANCH_PENDING.clear()
     for done, defer, ingre_w in pend:
         torch.cuda.current_stream(ingre_w.device).wait_event(done)
+        if defer is not None and _LATE_DRAIN[0] and ingre_w.is_cuda:
+            fork = torch.cuda.Event()
+            fork.record(torch.cuda.current_stream(ingre_w.device))
+            _PENDING_DRAINS.append((fork, defer, ingre_w))
+            continue
         if defer is not None:
-            if defer.rows and ingre_w.grad is None:  # (no propagation gradient was adopted: the rows alone)
-                ingre_w.grad = torch.zeros_like(ingre_w)
-            if ingre_w.grad is not None:
-                defer.drain(ingre_w.grad)
-            else:
-                defer.open = False
+            _drain_into(defer, ingre_w)
 
 
 def _drop_stale_branches():
@@ -1445,6 +1495,8 @@ def graph_bpr_begin(user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, L_ri, 
     args = (user_w, item_w, ingre_w, u, p, n, pn, ri_adj, ui_adj, int(L_ri), int(L_ui), gamma)
     if _BRANCH_PENDING:
         _drop_stale_branches()
+    if _PENDING_DRAINS:  # (a late-mode pass whose optimiser step never ran: its rows still belong in .grad)
+        run_pending_drains()
     if torch.is_grad_enabled() and ingre_w.requires_grad and not _DETERMINISTIC:
         ingre_w.__dict__["_fr_defer_rows"] = _DeferredRows()
     if not (BRANCH_STREAMS and user_w.is_cuda) or _DETERMINISTIC:

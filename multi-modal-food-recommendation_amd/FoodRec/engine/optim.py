@@ -393,6 +393,15 @@ class FusedAdam(torch.optim.Optimizer):
                 loss = closure()
         lib = native.lib()
         self.row_grads.join_background()
+        from . import ops
+        # tables whose gradient still waits for rows a late-mode backward left (ops.late_drain): the
+        # other tensors' update is launched first, then the rows are added (beside it, on the branch
+        # stream), then these tables' update
+        late = ops.pending_drain_params() if part != "rows" else set()
+        if late and any(p.grad is None for group in self.param_groups for p in group["params"] if id(p) in late):
+            ops.run_pending_drains()  # (a table whose whole gradient is the rows: added before collecting)
+            late = set()
+        late_plans = []
         # factored row gradients read the projection weights: materialise them before any update.
         # A full step runs them, and then the row tables' update, on a side stream that forks where
         # the backward wrote dY (the projection backward, before the encoder backward): both leave
@@ -483,6 +492,12 @@ class FusedAdam(torch.optim.Optimizer):
             # are marked current through the new step afterwards, so no later replay reads a history
             # slot this step never wrote
             self._flush_tables(group, lazy_dense)
+            if late:
+                lazy_ids = {id(p) for p in lazy_dense}
+                held = [p for p in plist if id(p) in late and id(p) not in lazy_ids]
+                if held:
+                    late_plans.append((held, hyper))
+                    plist = [p for p in plist if id(p) not in late or id(p) in lazy_ids]
             if plist:
                 if w_read is not None:
                     torch.cuda.current_stream(plist[0].device).wait_event(w_read)  # (long done: forked early)
@@ -497,6 +512,11 @@ class FusedAdam(torch.optim.Optimizer):
                         self._launch_rows(lib, rows, hyper[:-1] + (side.cuda_stream,))
                 else:
                     self._launch_rows(lib, rows, hyper)
+        if late or ops.pending_drain_params():
+            ops.run_pending_drains()
+        for held, hyper in late_plans:
+            with profiling.region("adam", 28 * sum(p.numel() for p in held)):
+                self._launch_dense(lib, held, hyper)
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
         return loss
