@@ -430,7 +430,7 @@ def main():
 # committed PMC file sampled from other kernels is stale and is not used
 REGION_KERNELS = {"encoder_bwd": ["enc_bwd_kernel", "enc_reduce_kernel"], "encoder_fwd": ["enc_fwd_kernel"],
                   "spmm": ["spmm_plain16_kernel"], "spmm_masked": ["spmm_sparse_kernel"],
-                  "spmm_rows": ["spmm_rows_kernel"], "adam": ["adam_kernel<false>"],
+                  "spmm_rows": ["spmm_rows_kernel"], "adam": ["adam_kernel<false, false>"],
                   "adam_rows": ["adam_lazy_rows_kernel<false>"]}
 
 

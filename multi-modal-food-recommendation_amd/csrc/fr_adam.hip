@@ -69,16 +69,33 @@ __device__ __forceinline__ void nt_store4(float* p, float4 v) {
   fv4 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<fv4*>(p));
 }
+// The fp32 update streams (adam_kernel) choose by launch size: ordinary loads / stores up to
+// kTemporalBytes of state -- at HealthRec's shape (8.9M parameters, 249 MB per launch, within the
+// 256 MB MALL) the launch measured 43.5 us against 52.5 us with the non-temporal hints
+// (tools/bench_adam.py; 0.708 / 0.713 -> 0.706 / 0.710 ms per step) -- and the non-temporal hints
+// beyond (config 4's 19.7 GB launch: 37.5 / 37.8 ms per step with them, 37.8 / 38.4 without).
+constexpr int64_t kTemporalBytes = 512ll << 20;
+template <bool NT>
+__device__ __forceinline__ float4 ld4t(const float* p) {
+  if constexpr (NT) return nt_load4(p);
+  else return *reinterpret_cast<const float4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st4t(float* p, float4 v) {
+  if constexpr (NT) nt_store4(p, v);
+  else *reinterpret_cast<float4*>(p) = v;
+}
 
+template <bool NT>
 __device__ __forceinline__ void adam4(float* P, const float* G, float* M, float* V, int64_t i, const AdamHyper& h,
                                       float4& p, float4& g, float4& m, float4& v) {
   adam_elem(p.x, g.x, m.x, v.x, h);
   adam_elem(p.y, g.y, m.y, v.y, h);
   adam_elem(p.z, g.z, m.z, v.z, h);
   adam_elem(p.w, g.w, m.w, v.w, h);
-  nt_store4(P + i, p);
-  nt_store4(M + i, m);
-  nt_store4(V + i, v);
+  st4t<NT>(P + i, p);
+  st4t<NT>(M + i, m);
+  st4t<NT>(V + i, v);
 }
 
 // Device-scalar mode bumps the step counters in the launch itself: every block derives its
@@ -108,7 +125,7 @@ __device__ __forceinline__ bool last_block(unsigned* ticket) {
 
 // Persistent grid over the launch's (tensor, chunk) list; the step-dependent scalars are derived
 // once per tensor a block meets.  Each thread keeps two float4 quartets (p, g, m, v) in flight.
-template <bool ROWS>
+template <bool ROWS, bool NT>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, const int32_t* skip) {
   if (skip && *skip) return;
   const int total = a.blk_start[a.n];
@@ -147,28 +164,28 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, AdamHyper h, cons
       int64_t i = base + 4 * threadIdx.x;
       for (; i + kStride < end; i += 2 * kStride) {  // two quartets in flight (end - base is a multiple of 4)
         const int64_t i1 = i + kStride;
-        float4 p0 = nt_load4(P + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i), g0 = grad4(i);
-        float4 p1 = nt_load4(P + i1), m1 = nt_load4(M + i1), v1 = nt_load4(V + i1), g1 = grad4(i1);
-        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
-        adam4(P, G, M, V, i1, h, p1, g1, m1, v1);
+        float4 p0 = ld4t<NT>(P + i), m0 = ld4t<NT>(M + i), v0 = ld4t<NT>(V + i), g0 = grad4(i);
+        float4 p1 = ld4t<NT>(P + i1), m1 = ld4t<NT>(M + i1), v1 = ld4t<NT>(V + i1), g1 = grad4(i1);
+        adam4<NT>(P, G, M, V, i, h, p0, g0, m0, v0);
+        adam4<NT>(P, G, M, V, i1, h, p1, g1, m1, v1);
       }
       for (; i < end; i += kStride) {
-        float4 p0 = nt_load4(P + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i), g0 = grad4(i);
-        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+        float4 p0 = ld4t<NT>(P + i), m0 = ld4t<NT>(M + i), v0 = ld4t<NT>(V + i), g0 = grad4(i);
+        adam4<NT>(P, G, M, V, i, h, p0, g0, m0, v0);
       }
     } else if (a.vec4[t]) {
       constexpr int64_t kStride = 4 * 256;
       int64_t i = base + 4 * threadIdx.x;
       for (; i + kStride + 3 < end; i += 2 * kStride) {
-        float4 p0 = nt_load4(P + i), g0 = nt_load4(G + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i);
+        float4 p0 = ld4t<NT>(P + i), g0 = ld4t<NT>(G + i), m0 = ld4t<NT>(M + i), v0 = ld4t<NT>(V + i);
         const int64_t i1 = i + kStride;
-        float4 p1 = nt_load4(P + i1), g1 = nt_load4(G + i1), m1 = nt_load4(M + i1), v1 = nt_load4(V + i1);
-        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
-        adam4(P, G, M, V, i1, h, p1, g1, m1, v1);
+        float4 p1 = ld4t<NT>(P + i1), g1 = ld4t<NT>(G + i1), m1 = ld4t<NT>(M + i1), v1 = ld4t<NT>(V + i1);
+        adam4<NT>(P, G, M, V, i, h, p0, g0, m0, v0);
+        adam4<NT>(P, G, M, V, i1, h, p1, g1, m1, v1);
       }
       for (; i + 3 < end; i += kStride) {
-        float4 p0 = nt_load4(P + i), g0 = nt_load4(G + i), m0 = nt_load4(M + i), v0 = nt_load4(V + i);
-        adam4(P, G, M, V, i, h, p0, g0, m0, v0);
+        float4 p0 = ld4t<NT>(P + i), g0 = ld4t<NT>(G + i), m0 = ld4t<NT>(M + i), v0 = ld4t<NT>(V + i);
+        adam4<NT>(P, G, M, V, i, h, p0, g0, m0, v0);
       }
       // scalar tail of the last chunk (numel % 4)
       const int64_t tail0 = base + ((end - base) / 4) * 4;
@@ -766,12 +783,18 @@ static int adam_impl(float* const* params, const float* const* grads, float* con
       if (a.n == 0) continue;
       (void)idx;
       // device-scalar mode: the kernel's last block advances the step counters
-      if (rows_pass)
-        hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0, s,
-                           a, h, d_skip);
+      int64_t state_bytes = 0;
+      for (int k = 0; k < a.n; ++k) state_bytes += 28 * a.numel[k];
+      const bool nt = state_bytes > kTemporalBytes;
+      const dim3 grid((unsigned)std::min<int32_t>(blocks, kAdamBlocks));
+      if (rows_pass && nt)
+        hipLaunchKernelGGL((adam_kernel<true, true>), grid, dim3(256), 0, s, a, h, d_skip);
+      else if (rows_pass)
+        hipLaunchKernelGGL((adam_kernel<true, false>), grid, dim3(256), 0, s, a, h, d_skip);
+      else if (nt)
+        hipLaunchKernelGGL((adam_kernel<false, true>), grid, dim3(256), 0, s, a, h, d_skip);
       else
-        hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)std::min<int32_t>(blocks, kAdamBlocks)), dim3(256), 0,
-                           s, a, h, d_skip);
+        hipLaunchKernelGGL((adam_kernel<false, false>), grid, dim3(256), 0, s, a, h, d_skip);
       FR_LAUNCH_CHECK();
     }
   }

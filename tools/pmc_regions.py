@@ -21,7 +21,7 @@ REGION_KERNELS = {
     "spmm": ["spmm_plain16_kernel"],
     "spmm_masked": ["spmm_sparse_kernel"],
     "spmm_rows": ["spmm_rows_kernel"],
-    "adam": ["adam_kernel<false>"],
+    "adam": ["adam_kernel<false, false>"],
     "adam_rows": ["adam_lazy_rows_kernel<false>"],
     "adam_rows_catch_up": ["adam_catch_up_multi_kernel"],
     "adam_rows_slice": ["adam_catch_up_slice_kernel"],

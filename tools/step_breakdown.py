@@ -14,7 +14,7 @@ rows = list(csv.DictReader(open(args[0])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # one optimiser launch per step marks the step: the row-gradient Adam when present, else the dense one
 adam = ([i for i, r in enumerate(rows) if "::adam_lazy_rows_kernel<false>" in r["Kernel_Name"]]
-        or [i for i, r in enumerate(rows) if "::adam_kernel<true>" in r["Kernel_Name"]]
+        or [i for i, r in enumerate(rows) if "::adam_kernel<true," in r["Kernel_Name"]]
         or [i for i, r in enumerate(rows) if "::adam_kernel" in r["Kernel_Name"]])
 # step groups: Adam launches of one step are back-to-back
 groups = [[adam[0]]]
