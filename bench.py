@@ -636,6 +636,8 @@ def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
     views = [torch.randn(2 * B, 64, device=device, requires_grad=True) for _ in range(3)]
     for name, fn in (("dcor_fwd_bwd_ms", lambda: ops.dcor_loss(views, _DCOR_PAIRS).backward()),
                      ("infonce_fwd_bwd_ms", lambda: ops.infonce_pairs(views, _DCOR_PAIRS, 0.5).backward())):
+        # eager (host-issued: Python + autograd per call) and the same call captured in a HIP graph
+        # and replayed (the kernels' GPU time, as the graphed training step runs them)
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -644,7 +646,30 @@ def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
             fn()
         e1.record()
         torch.cuda.synchronize()
+        out[name.replace("_ms", "_eager_ms")] = round(e0.elapsed_time(e1) / ssl_iters, 4)
+        for v in views:
+            v.grad = None  # (the capture adopts fresh .grad buffers: replays overwrite, no accumulate kernel)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            fn()
+            for v in views:
+                v.grad = None
+        torch.cuda.current_stream(device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fn()
+        graph.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(ssl_iters):
+            graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
         out[name] = round(e0.elapsed_time(e1) / ssl_iters, 4)
+        del graph
+        for v in views:
+            v.grad = None
     if cpu:
         out["cpu_baseline"] = config3_cpu(data, B, cpu_steps)
     return out
