@@ -1,0 +1,42 @@
+"""Config 3's SSL terms alone (CLUSSL's three views at 2B = 1,024 rows): dCor and InfoNCE forward +
+backward captured in HIP graphs and replayed, for rocprofv3 kernel traces of the SSL kernels."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "multi-modal-food-recommendation_amd"), ROOT]
+import torch  # noqa: E402
+
+from FoodRec.engine import ops  # noqa: E402
+from FoodRec.models.clussl import _DCOR_PAIRS  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+views = [torch.randn(1024, 64, device=dev, requires_grad=True) for _ in range(3)]
+res = {}
+for name, fn in (("dcor", lambda: ops.dcor_loss(views, _DCOR_PAIRS).backward()),
+                 ("infonce", lambda: ops.infonce_pairs(views, _DCOR_PAIRS, 0.5).backward())):
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        fn()
+        for v in views:
+            v.grad = None
+    torch.cuda.current_stream(dev).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(50):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    res[name + "_fwd_bwd_us"] = round(a.elapsed_time(b) / 50 * 1e3, 1)
+    for v in views:
+        v.grad = None
+print(json.dumps(res))
