@@ -123,7 +123,22 @@ extern "C" int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t n
   }
   MT mt{mt_key, mt_pos};
   const uint64_t rng = (uint64_t)(num_items - 1);
+  // the loop is bound by the cache misses of its exclusion-list lookups (users in permutation order):
+  // the row pointers are prefetched kPf2 users ahead and the lists' first lines kPf1 ahead (results
+  // unchanged: the draws and tests are the same, in the same order)
+  constexpr int64_t kPf1 = 8, kPf2 = 16;
   for (int64_t k = 0; k < n; ++k) {
+    if (k + kPf2 < n && users[k + kPf2] >= 0) {
+      __builtin_prefetch(excl_ptr + users[k + kPf2]);
+      if (excl2_ptr) __builtin_prefetch(excl2_ptr + users[k + kPf2]);
+    }
+    if (k + kPf1 < n && users[k + kPf1] >= 0) {
+      const int64_t v = users[k + kPf1];
+      const int64_t* ea = excl_items + excl_ptr[v];
+      __builtin_prefetch(ea);
+      __builtin_prefetch(ea + 8);
+      if (excl2_ptr) __builtin_prefetch(excl2_items + excl2_ptr[v]);
+    }
     const int64_t u = users[k];
     if (u < 0) {
       fr::set_error("fr_sampler_negatives: negative user id");
