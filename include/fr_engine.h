@@ -270,6 +270,13 @@ int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
                          const int64_t* excl_ptr, const int64_t* excl_items,
                          const int64_t* excl2_ptr, const int64_t* excl2_items,
                          int64_t* out_neg);
+/* the same draws for users[perm[k]], k < n (the epoch's permutation order: no permuted copy of the
+ * users); perm values must index users */
+int fr_sampler_negatives_perm(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
+                              const int64_t* users, const int64_t* perm, int64_t n,
+                              const int64_t* excl_ptr, const int64_t* excl_items,
+                              const int64_t* excl2_ptr, const int64_t* excl2_items,
+                              int64_t* out_neg);
 
 /* raw masked-rejection draws (test hook): out[i] = np.random.randint(high) for i < n */
 int fr_sampler_randint(uint32_t* mt_key, int32_t* mt_pos, int64_t high, int64_t n, int64_t* out);

@@ -71,7 +71,7 @@ _SIGS = {
                                  c_void_p, c_int64, c_void_p]),
     "fr_spmm_list_scatter": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                      c_void_p, c_int64, c_void_p, c_int64, c_float, c_int, c_void_p]),
-    "fr_rows_mark":(c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
+    "fr_rows_mark": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p]),
     "fr_rows_mark_zero": (c_int, [c_void_p, POINTER(FrRowList), ctypes.c_uint8, c_void_p, c_int64, c_int, c_void_p,
                                   c_void_p]),
     "fr_spmm_scatter_upstream": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
@@ -244,6 +244,8 @@ _SIGS = {
     "fr_encoder_reduce": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fr_sampler_negatives_perm": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_void_p, c_int64,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),
     "fr_health_kd_partials": (c_int64, [c_int64, c_int]),
     "fr_health_kd_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p),

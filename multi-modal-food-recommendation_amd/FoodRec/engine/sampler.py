@@ -33,20 +33,32 @@ def _np_state():
     return st, key, pos
 
 
-def draw_negatives(users: np.ndarray, num_items: int, excl_ptr, excl_items, excl2_ptr, excl2_items) -> np.ndarray:
-    """np.random-stream-exact rejection sampling for every user in ``users`` (in order)."""
+def draw_negatives(users: np.ndarray, num_items: int, excl_ptr, excl_items, excl2_ptr, excl2_items,
+                   perm: np.ndarray | None = None, out: np.ndarray | None = None) -> np.ndarray:
+    """np.random-stream-exact rejection sampling for every user in ``users`` (in order), or for
+    ``users[perm]`` with ``perm`` (no permuted copy); ``out``: a caller's int64 buffer (e.g. a pinned
+    staging tensor's numpy view) of the draws' length."""
     users = np.ascontiguousarray(users, dtype=np.int64)
-    out = np.empty(len(users), np.int64)
+    n = len(users) if perm is None else len(perm)
+    if perm is not None:
+        perm = np.ascontiguousarray(perm, dtype=np.int64)
+        if n and (int(perm.min()) < 0 or int(perm.max()) >= len(users)):
+            raise native.EngineError("draw_negatives: perm indexes outside users")
+    if out is None:
+        out = np.empty(n, np.int64)
+    elif out.dtype != np.int64 or out.shape != (n,) or not out.flags.c_contiguous:
+        raise native.EngineError("draw_negatives: out must be a contiguous int64 array of the draws' length")
     st, key, pos = _np_state()
     lib = native.lib()
-    rc = lib.fr_sampler_negatives(key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                                  pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(num_items),
-                                  users.ctypes.data, len(users),
-                                  np.ascontiguousarray(excl_ptr, np.int64).ctypes.data,
-                                  np.ascontiguousarray(excl_items, np.int64).ctypes.data,
-                                  None if excl2_ptr is None else np.ascontiguousarray(excl2_ptr, np.int64).ctypes.data,
-                                  None if excl2_items is None else np.ascontiguousarray(excl2_items, np.int64).ctypes.data,
-                                  out.ctypes.data)
+    tail = (np.ascontiguousarray(excl_ptr, np.int64).ctypes.data, np.ascontiguousarray(excl_items, np.int64).ctypes.data,
+            None if excl2_ptr is None else np.ascontiguousarray(excl2_ptr, np.int64).ctypes.data,
+            None if excl2_items is None else np.ascontiguousarray(excl2_items, np.int64).ctypes.data, out.ctypes.data)
+    kp = (key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+          int(num_items))
+    if perm is None:
+        rc = lib.fr_sampler_negatives(*kp, users.ctypes.data, n, *tail)
+    else:
+        rc = lib.fr_sampler_negatives_perm(*kp, users.ctypes.data, perm.ctypes.data, n, *tail)
     native.check(rc, "fr_sampler_negatives")
     np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
     return out
@@ -68,10 +80,10 @@ class TripleSampler:
         self._dev_users = torch.from_numpy(self.users).to(self.device)
         self._dev_items = torch.from_numpy(self.items).to(self.device)
 
-    def _negatives(self, users):
+    def _negatives(self, users, perm=None, out=None):
         d = self.ds
         return draw_negatives(users, d.num_items, d.excl_train_ptr, d.excl_train_items,
-                              d.excl_vt_ptr, d.excl_vt_items)
+                              d.excl_vt_ptr, d.excl_vt_items, perm=perm, out=out)
 
     def _init_neg_list(self, replay_python_random):
         negs = self._negatives(self.users)
@@ -106,11 +118,20 @@ class TripleSampler:
         perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
         # the whole epoch's negatives in one native call and one host->device copy: the same draws in
         # the same order as per-batch (or the reference's per-sample) drawing, since nothing else
-        # consumes np.random during an epoch; the steps then only index device arrays
-        negs_all = torch.from_numpy(self._negatives(self.users[perm]))
+        # consumes np.random during an epoch; the steps then only index device arrays.  On a GPU the
+        # draws land in a persistent pinned staging buffer (no pageable copy / pin per epoch)
         if self.device.type == "cuda":
-            negs_all = negs_all.pin_memory()
-        negs_d = negs_all.to(self.device, non_blocking=True)
+            if getattr(self, "_negs_pin", None) is None or self._negs_pin.numel() != self.n:
+                self._negs_pin = torch.empty(self.n, dtype=torch.int64, pin_memory=True)
+                self._negs_copied = None
+            if self._negs_copied is not None:
+                self._negs_copied.synchronize()  # the previous epoch's copy out of the buffer is done
+            self._negatives(self.users, perm=perm, out=self._negs_pin.numpy())
+            negs_d = self._negs_pin.to(self.device, non_blocking=True)
+            self._negs_copied = torch.cuda.Event()
+            self._negs_copied.record(torch.cuda.current_stream(self.device))
+        else:
+            negs_d = torch.from_numpy(self._negatives(self.users, perm=perm))
         if feed is not None and out is not None:
             feed.stage(perm_d, negs_d)
         for s in range(0, self.n, self.batch_size):

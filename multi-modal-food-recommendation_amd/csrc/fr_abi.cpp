@@ -112,15 +112,44 @@ extern "C" int fr_sampler_randint(uint32_t* mt_key, int32_t* mt_pos, int64_t hig
   return FR_OK;
 }
 
+static int sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items, const int64_t* users_all,
+                             const int64_t* perm, int64_t n, const int64_t* excl_ptr, const int64_t* excl_items,
+                             const int64_t* excl2_ptr, const int64_t* excl2_items, int64_t* out_neg);
+
 extern "C" int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
                                     const int64_t* users, int64_t n, const int64_t* excl_ptr,
                                     const int64_t* excl_items, const int64_t* excl2_ptr,
                                     const int64_t* excl2_items, int64_t* out_neg) {
-  if (!mt_key || !mt_pos || num_items <= 0 || n < 0 || (n > 0 && (!users || !out_neg)) ||
+  return sampler_negatives(mt_key, mt_pos, num_items, users, nullptr, n, excl_ptr, excl_items, excl2_ptr, excl2_items,
+                           out_neg);
+}
+
+extern "C" int fr_sampler_negatives_perm(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
+                                         const int64_t* users, const int64_t* perm, int64_t n,
+                                         const int64_t* excl_ptr, const int64_t* excl_items,
+                                         const int64_t* excl2_ptr, const int64_t* excl2_items, int64_t* out_neg) {
+  if (!perm && n > 0) {
+    fr::set_error("fr_sampler_negatives_perm: null perm");
+    return FR_EINVAL;
+  }
+  return sampler_negatives(mt_key, mt_pos, num_items, users, perm, n, excl_ptr, excl_items, excl2_ptr, excl2_items,
+                           out_neg);
+}
+
+static int sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items, const int64_t* users_all,
+                             const int64_t* perm, int64_t n, const int64_t* excl_ptr, const int64_t* excl_items,
+                             const int64_t* excl2_ptr, const int64_t* excl2_items, int64_t* out_neg) {
+  if (!mt_key || !mt_pos || num_items <= 0 || n < 0 || (n > 0 && (!users_all || !out_neg)) ||
       !excl_ptr || !excl_items) {
     fr::set_error("fr_sampler_negatives: bad argument");
     return FR_EINVAL;
   }
+  // users[k] = users_all[perm[k]] (the epoch's permutation order) or users_all[k]
+  struct Users {
+    const int64_t* a;
+    const int64_t* p;
+    int64_t operator[](int64_t k) const { return p ? a[p[k]] : a[k]; }
+  } users{users_all, perm};
   MT mt{mt_key, mt_pos};
   const uint64_t rng = (uint64_t)(num_items - 1);
   // the loop is bound by the cache misses of its exclusion-list lookups (users in permutation order):
@@ -128,6 +157,7 @@ extern "C" int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t n
   // unchanged: the draws and tests are the same, in the same order)
   constexpr int64_t kPf1 = 8, kPf2 = 16;
   for (int64_t k = 0; k < n; ++k) {
+    if (perm && k + kPf2 + 8 < n) __builtin_prefetch(users_all + perm[k + kPf2 + 8]);
     if (k + kPf2 < n && users[k + kPf2] >= 0) {
       __builtin_prefetch(excl_ptr + users[k + kPf2]);
       if (excl2_ptr) __builtin_prefetch(excl2_ptr + users[k + kPf2]);
