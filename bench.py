@@ -233,34 +233,46 @@ def main():
         else:
             trainer.train_step(feats.batch(u, p, n), i, state)
 
-    for i in range(max(args.warmup, 5 if use_graph else 0)):
-        do_step(i)
+    # every HIP graph the timed steps replay (the one-step graph and the unrolled graph) is captured
+    # and replayed once here, whatever --warmup says: no capture lands inside the timed region
+    prep_steps = graphed.prepare(lambda: next(it), state) if graphed is not None else 0
+    for i in range(args.warmup):
+        do_step(prep_steps + i)
     if graphed is not None:
         graphed.flush()  # no warm-up step left pending for the timed region
+    captures0 = graphed.captures if graphed is not None else 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        do_step(args.warmup + i)
+        do_step(prep_steps + args.warmup + i)
     if graphed is not None:
         graphed.flush()  # steps of an unrolled graph not yet replayed run inside the timed region
     t_submit = time.perf_counter() - t0  # host time to issue the steps (graph replays): < elapsed when GPU-bound
     torch.cuda.synchronize()
     t_steps = time.perf_counter() - t0
-    # the deferred zero-gradient row steps of the lazily updated tables (FusedAdam lazy rows) are
-    # applied inside the timed region: every parameter holds its dense-Adam value when it closes
+    captures_timed = (graphed.captures - captures0) if graphed is not None else 0
+    assert captures_timed == 0, f"{captures_timed} graph capture(s) inside the timed region"
+    # the deferred zero-gradient row steps of the lazily updated tables (FusedAdam lazy rows): the
+    # trainer applies them once per epoch (_train_epoch's flush_optimizer, before evaluation); here
+    # they run right after the steps, inside the bracket, and are timed on their own: `value`
+    # charges them per epoch like the epoch's sampling (every parameter holds its dense-Adam value
+    # when the bracket closes)
     trainer.flush_optimizer()
     torch.cuda.synchronize()
+    t_flushed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, t_steps, t_flushed - t_steps], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, t_steps, flush_s = (float(x) for x in t.tolist())
+    else:
+        flush_s = t_flushed - t_steps
     assert not int(state["nan"].item()), "NaN loss during bench"
     # per-kernel HIP-event timing (roofline): the same kernels, launched eagerly on the same
     # stream right after the timed region (events cannot bracket single kernels inside a replay)
@@ -292,8 +304,9 @@ def main():
     finally:
         _ops_mod.BRANCH_STREAMS = branch0
 
-    ms_steps = elapsed / args.steps * 1e3
-    ms_per_step = ms_steps + epoch_ms / steps_per_epoch
+    ms_steps = t_steps / args.steps * 1e3
+    flush_ms = flush_s * 1e3
+    ms_per_step = ms_steps + (epoch_ms + flush_ms) / steps_per_epoch
     triples = args.batch * args.steps * world
     value = triples / (ms_per_step * 1e-3 * args.steps)
 
@@ -411,14 +424,20 @@ def main():
                            "parallelism": f"dp{world}" if world > 1 else ("dp1 (forced exchange)" if dp1 else "single"),
                            "graph_steps_per_replay": graph_unroll},
                 "roofline": roofline, "ranks": ranks, "scaling_config4": c4_scaling, "step_bytes": step_fig,
+                "timed_region": {"graph_captures_in_timed_region": captures_timed,
+                                 "prepare_steps": prep_steps, "warmup_steps": args.warmup,
+                                 "elapsed_s": round(elapsed, 6), "steps_s": round(t_steps, 6),
+                                 "note": "GraphedStep.prepare() captured and replayed every graph before t0 "
+                                         "(prepare_steps untimed training steps, then --warmup steps)"},
                 "epoch_sampling": {"ms_per_epoch": round(epoch_ms, 2), "probes_ms": [round(x, 2) for x in probes],
                                    "steps_per_epoch": steps_per_epoch,
                                    "ms_per_step_without": round(ms_steps, 4),
                                    "host_submit_ms_per_step": round(t_submit / args.steps * 1e3, 4),
                                    "steps_ms_per_step": round(t_steps / args.steps * 1e3, 4),
-                                   "lazy_flush_ms_per_step": round((elapsed - t_steps) / args.steps * 1e3, 4),
-                                   "note": "value and ms_per_step include epoch_sampling.ms_per_epoch (the median "
-                                           "of three epochs' sampling) / steps_per_epoch per step"},
+                                   "lazy_flush_ms_per_epoch": round(flush_ms, 3),
+                                   "note": "value and ms_per_step = the timed steps + (epoch_sampling.ms_per_epoch, "
+                                           "the median of three epochs' sampling, + the once-per-epoch lazy-row "
+                                           "flush, timed inside the bracket after the steps) / steps_per_epoch"},
                 "spmm": spmm, "config1_bprmf_allrecipes": c1, "config3_clussl_foodcom": c3, "config4_10m": c4,
                 "config5_10m_bf16": c5, "eval_healthrec_allrecipes": ev, "kernels": kernels, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
@@ -617,19 +636,23 @@ def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
                     yield t
 
         it = batches()
+        prep = g.prepare(lambda: next(it), state)  # every graph captured and replayed before t0
         for i in range(warmup):
-            g(*next(it), i, state)
+            g(*next(it), prep + i, state)
         g.flush()
+        captures0 = g.captures
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            g(*next(it), warmup + i, state)
+            g(*next(it), prep + warmup + i, state)
         g.flush()
         tr.flush_optimizer()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
+        assert g.captures == captures0, "graph capture inside the config-3 timed region"
         assert not int(state["nan"].item()), "NaN loss in the config-3 step"
-        out[mode] = {"ms_per_step": round(dt * 1e3, 4), "triples_per_s": round(B / dt, 1)}
+        out[mode] = {"ms_per_step": round(dt * 1e3, 4), "triples_per_s": round(B / dt, 1),
+                     "graph_captures_in_timed_region": g.captures - captures0, "prepare_steps": prep}
         del tr, model, g, sampler, state, it
         torch.cuda.empty_cache()
     torch.manual_seed(0)
@@ -670,6 +693,25 @@ def config3(device, steps=30, warmup=5, ssl_iters=20, cpu=True, cpu_steps=5):
         del graph
         for v in views:
             v.grad = None
+    # MFMA roofline of the SSL kernels (fp32 v_mfma_f32_16x16x4_f32 Gram tiles): algorithmic FLOPs of
+    # one forward + backward over the three [2B, 64] views / the graph-replay GPU time
+    n_views, n_pairs = len(views), len(_DCOR_PAIRS)
+    for key, fl, name, kern in (
+            ("roofline", ops.infonce_flops(2 * B, 64, n_pairs), "infonce_fwd_bwd_ms",
+             "nce_lse_mfma + nce_bwd_mfma (+ their finalize launches): fr_infonce_multi_fwd_ex / _bwd"),
+            ("roofline_dcor", ops.dcor_flops(2 * B, 64, n_views), "dcor_fwd_bwd_ms",
+             "dcor tiles + means + finalize, dcor backward + finalize: fr_dcor_fwd_ex / fr_dcor_bwd_ex")):
+        tf = fl / (out[name] * 1e-3) / 1e12
+        out[key] = {"kernel": kern, "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                    "flops_per_call": fl, "avg_call_ms": out[name],
+                    "timing_source": f"HIP events around {ssl_iters} replays of one captured fwd+bwd call "
+                                     f"(config3_clussl_foodcom.{name})",
+                    "flop_model": ("per pair: the (2n)^2 logit Gram forward + dH = S H, S^T H backward, "
+                                   "2 (2n)^2 d each, n = 2B = 1024 rows per view, d = 64"
+                                   if key == "roofline" else
+                                   "per view: the n^2 distance Gram forward + the m X product backward, "
+                                   "2 n^2 d each, n = 2B = 1024, d = 64")}
     if cpu:
         out["cpu_baseline"] = config3_cpu(data, B, cpu_steps)
     return out

@@ -263,18 +263,22 @@ int fr_adam_step_dev(float* const* params, const float* const* grads,
  * Negative sampler (host code): numpy legacy MT19937 stream, masked-rejection bounded ints,
  * exactly the draws np.random.randint(num_items) makes in TrainDataLoader.get_random_neg.
  * state: 624 uint32 key + pos (as numpy.random.get_state()[1:3]); updated in place.
- * Exclusion sets are per-user sorted int64 lists in CSR form (train items, valid+test items).
+ * Exclusion sets are per-user sorted int64 lists in CSR form (train items, valid+test items):
+ * excl_ptr / excl2_ptr hold n_users + 1 entries, start at 0 and never decrease.  Every user id
+ * must lie in [0, n_users) (FR_ERANGE otherwise, checked before any lookup); a user whose two
+ * lists together contain every item of [0, num_items) returns FR_ERANGE (the reference's
+ * rejection loop would not end).  Unsorted lists give wrong draws, never an out-of-bounds read.
  * ------------------------------------------------------------------------------------------ */
 int fr_sampler_negatives(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
-                         const int64_t* users, int64_t n,
+                         const int64_t* users, int64_t n, int64_t n_users,
                          const int64_t* excl_ptr, const int64_t* excl_items,
                          const int64_t* excl2_ptr, const int64_t* excl2_items,
                          int64_t* out_neg);
 /* the same draws for users[perm[k]], k < n (the epoch's permutation order: no permuted copy of the
- * users); perm values must index users */
+ * users); users holds n_pairs ids and every perm value must index it (FR_ERANGE otherwise) */
 int fr_sampler_negatives_perm(uint32_t* mt_key, int32_t* mt_pos, int64_t num_items,
-                              const int64_t* users, const int64_t* perm, int64_t n,
-                              const int64_t* excl_ptr, const int64_t* excl_items,
+                              const int64_t* users, int64_t n_pairs, const int64_t* perm, int64_t n,
+                              int64_t n_users, const int64_t* excl_ptr, const int64_t* excl_items,
                               const int64_t* excl2_ptr, const int64_t* excl2_items,
                               int64_t* out_neg);
 

@@ -154,6 +154,7 @@ class GraphedStep:
         self.n = torch.zeros_like(self.u)
         self.graph = None
         self.calls = 0
+        self.captures = 0     # graph captures so far (a timed region must not contain one)
         self.static_loss = None
         # the graph's own state: each replay adds the step's loss vector to gstate["acc"] and ORs
         # the NaN flag into gstate["nan"].  Callers that pass this dict (``.state``) as their epoch
@@ -178,6 +179,27 @@ class GraphedStep:
             self.pending -= 1
             self.graph.replay()
             self._note()
+
+    def _unrolls(self, state) -> bool:
+        return state is self.gstate and self.unroll > 1 and self.feed is not None
+
+    def prepare(self, next_batch, state, first_idx=0) -> int:
+        """Run the eager warm-up calls and capture every graph later calls replay -- the one-step
+        graph and, when steps are unrolled, the ``unroll``-step graph -- replaying each at least
+        once, then flush.  ``next_batch()`` yields the (u, pos, neg) of one call (training steps:
+        the warm-up steps train).  Afterwards calls only replay (``captures`` does not move), so a
+        timed region that starts here measures the steady state whatever its length.  Returns the
+        number of steps taken."""
+        i = first_idx
+        while self.graph is None or (self._unrolls(state) and self.graph_n is None):
+            self(*next_batch(), i, state)
+            i += 1
+        if self._unrolls(state):
+            self.flush()
+            self(*next_batch(), i, state)  # pending 1: the one-step graph's first replay is the flush's
+            i += 1
+        self.flush()
+        return i - first_idx
 
     @property
     def state(self):
@@ -227,9 +249,10 @@ class GraphedStep:
             with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 self.static_loss = self._body(batch_idx, self.gstate, accumulate=True)
             self.graph = g
+            self.captures += 1
             if acc0 is not None:
                 self.gstate["acc"].copy_(acc0)
-        if own and self.unroll > 1 and self.feed is not None:
+        if self._unrolls(state):
             self.pending += 1
             if self.pending < self.unroll:
                 return self.static_loss
@@ -241,7 +264,12 @@ class GraphedStep:
                     for k in range(self.unroll):
                         self.static_loss_n = self._body(batch_idx + k, self.gstate, accumulate=True)
                 self.graph_n = gn
+                self.captures += 1
             self.pending = 0
+            if isinstance(self.tr.optimizer, FusedAdam):
+                # the replay runs ``unroll`` lazy steps before note_replay can flush: keep the
+                # history ring from wrapping inside it
+                self.tr.optimizer.reserve_replays(self.unroll)
             self.graph_n.replay()
             for _ in range(self.unroll):
                 self._note()
@@ -301,6 +329,7 @@ class GraphedDPStep(GraphedStep):
             fused = tr._book_fused(state, parts, accumulate) is not None
         finally:
             ops.book_taken()
+            ops.drop_pending()
             ops.defer_counters(False)
         if fused:
             torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
@@ -565,6 +594,7 @@ class Trainer(AbstractTrainer):
             booked = self._book_fused(state, parts, accumulate) if second_inter is None else None
         finally:
             ops.book_taken()  # (clears a request nothing answered)
+            ops.drop_pending()  # (partials a raising loss left behind)
             ops.defer_counters(False)  # (applies the increments eagerly when the step was not booked)
         if booked is not None:
             # the loss sum is never materialised for autograd: each part back-propagates with a
@@ -785,8 +815,12 @@ class Trainer(AbstractTrainer):
 
     @torch.no_grad()
     def _score_fused(self, dc):
-        """Device scores of the cached evaluation lists (fr_score_segments over forward()'s tables)."""
+        """Device scores of the cached evaluation lists (fr_score_segments over forward()'s tables),
+        or None when those tables are not the kernel's fp32 [*, 64] (another embedding_size, bf16
+        tables): the caller then scores through the model's inference_fast."""
         out = self.model.forward()
+        if not ops.score_segments_ok(out[0], out[1]):
+            return None
         return ops.score_segments(out[0], out[1], dc["uid"], dc["off"], dc["items"])
 
     def _valid_by_user_epoch(self, valid_data=None, is_test=False):
@@ -794,8 +828,8 @@ class Trainer(AbstractTrainer):
         neg_num = self.config["neg_sample_num"]
         if self._fused_scoring():
             dc = self._device_candidates(is_test)
-            if dc["uid"] is not None:
-                sc = self._score_fused(dc)
+            sc = self._score_fused(dc) if dc["uid"] is not None else None
+            if sc is not None:
                 res = self._rank_scores(sc, dc["lens"], dc["npos"], neg_num)
                 recalls, ndcgs, aucs = res.mean(axis=0).tolist()
                 metrics = {"AUC": aucs[0], "Recall@10": recalls[0], "Recall@20": recalls[1],

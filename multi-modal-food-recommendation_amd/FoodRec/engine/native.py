@@ -242,10 +242,10 @@ _SIGS = {
     "fr_encoder_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p), POINTER(c_float),
                                POINTER(c_float), c_uint64, c_int] + [c_void_p] * 12 + [c_int64] + [c_void_p] * 3),
     "fr_encoder_reduce": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p]),
-    "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64,
+    "fr_sampler_negatives": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "fr_sampler_negatives_perm": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_void_p, c_int64,
-                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fr_sampler_negatives_perm": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_void_p, c_int64, c_void_p,
+                                          c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fr_sampler_randint": (c_int, [POINTER(c_uint32), POINTER(c_int32), c_int64, c_int64, c_void_p]),
     "fr_health_kd_partials": (c_int64, [c_int64, c_int]),
     "fr_health_kd_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p),

@@ -1675,6 +1675,14 @@ def finalize_pending() -> None:
         finalize_norms(t)
 
 
+def drop_pending() -> None:
+    """Forget every deferred finalize (the trainer's ``finally`` after calculate_loss): a loss that
+    raised between a deferring op and its consumer must not leave partials keyed by an address a
+    later tensor may reuse.  On the success path finalize_pending / the loss ops consumed them."""
+    _PENDING_HEAD.clear()
+    _PENDING_NORMS.clear()
+
+
 # the trainer's request that a fused loss op book the step itself (fr_step_book's work in its launch)
 _BOOK = {"request": None, "done": None}
 
@@ -2811,6 +2819,24 @@ def infonce_pairs(views, pairs, tau: float = 0.5, weight: float = 1.0) -> torch.
     return _InfoNCEMulti.apply(tuple(tuple(int(x) for x in p) for p in pairs), float(tau), float(weight), *views)
 
 
+def infonce_flops(n: int, d: int, n_pairs: int, backward: bool = True) -> int:
+    """Algorithmic FLOPs of infonce_pairs over ``n_pairs`` pairs of [n, d] views (CL_loss,
+    pricai_modelx.py:354-378, hidden = [2n, d]): the logits aa / ab / ba / bb form one (2n)^2 Gram
+    (2 (2n)^2 d) forward; the backward's dH = S H and S^T H are two more.  Normalisation, exp and the
+    log-sum-exp are not counted."""
+    N = 2 * n
+    return n_pairs * 2 * N * N * d * (3 if backward else 1)
+
+
+def dcor_flops(n: int, d: int, n_views: int, backward: bool = True) -> int:
+    """Algorithmic FLOPs of dcor_loss over ``n_views`` [n, d] views (correlation_distance,
+    pricai_modelx.py:409-437): one X X^T Gram (2 n^2 d) per view forward -- every pair reuses the
+    views' distance matrices -- and the backward's m X product (2 n^2 d) per view.  The
+    centring sums and square roots are not counted; nor is the backward's recomputation of the
+    distances (not algorithmic work)."""
+    return n_views * 2 * n * n * d * (2 if backward else 1)
+
+
 # ----------------------------------------------------------------------------- full-sort top-k
 def topk_flops(n_users: int, n_items: int, d: int) -> int:
     """Algorithmic FLOPs of one fr_topk_scores call: the dense n_users x n_items x d score GEMM."""
@@ -2872,6 +2898,12 @@ def full_sort_topk(user_rows: torch.Tensor, item_table: torch.Tensor, k: int, us
 
 
 # ----------------------------------------------------------------------------- evaluation ranking
+def score_segments_ok(user_table, item_table) -> bool:
+    """The tables fr_score_segments takes: fp32, 2-D, 64 wide, unit column stride (any row stride)."""
+    return all(torch.is_tensor(t) and t.dim() == 2 and t.shape[1] == 64 and t.dtype == torch.float32
+               and t.stride(1) == 1 for t in (user_table, item_table))
+
+
 def score_segments(user_table: torch.Tensor, item_table: torch.Tensor, uid: torch.Tensor, offsets: torch.Tensor,
                    items: torch.Tensor) -> torch.Tensor:
     """``(user_table[u] * item_table[items[e]]).sum()`` for every candidate e of every user segment
@@ -2879,8 +2911,7 @@ def score_segments(user_table: torch.Tensor, item_table: torch.Tensor, uid: torc
     tensors).  The graph models' inference_fast over the evaluation lists without the [n, 64] gathers."""
     native.require_device(user_table, item_table, uid, offsets, items)
     d = user_table.shape[1]
-    if d != 64 or item_table.shape[1] != d or user_table.dtype != torch.float32 or item_table.dtype != torch.float32 \
-            or user_table.stride(1) != 1 or item_table.stride(1) != 1:
+    if not score_segments_ok(user_table, item_table):
         raise native.EngineError("score_segments: fp32 [*, 64] row-major tables required")
     out = torch.empty(items.numel(), dtype=torch.float32, device=items.device)
     native.check(native.lib().fr_score_segments(user_table.data_ptr(), user_table.stride(0), item_table.data_ptr(),

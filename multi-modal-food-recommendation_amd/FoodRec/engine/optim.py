@@ -319,6 +319,15 @@ class FusedAdam(torch.optim.Optimizer):
             if self._lazy_pending >= self.hist_cap - 2:
                 self.flush()
 
+    def reserve_replays(self, n: int):
+        """``n`` captured lazy steps are about to run in one replay (an unrolled graph) before
+        note_replay sees them: flush first when they would carry the pending count past the ring's
+        bound (hist_cap - 2), so no row ever replays from an overwritten history slot."""
+        if int(n) > self.hist_cap - 2:
+            raise ValueError(f"{n} steps per replay exceed the lazy history ring (hist_cap {self.hist_cap})")
+        if self._lazy_launched and self._lazy_pending + int(n) > self.hist_cap - 2:
+            self.flush()
+
     def state_dict(self):
         self.flush()
         return super().state_dict()
@@ -493,19 +502,18 @@ class FusedAdam(torch.optim.Optimizer):
             # slot this step never wrote
             self._flush_tables(group, lazy_dense)
             if late:
-                lazy_ids = {id(p) for p in lazy_dense}
-                held = [p for p in plist if id(p) in late and id(p) not in lazy_ids]
+                # a late table waits for its deferred gradient rows (ops.run_pending_drains below),
+                # also when it is a lazily updated table taking a dense step
+                held = [p for p in plist if id(p) in late]
                 if held:
                     late_plans.append((held, hyper))
-                    plist = [p for p in plist if id(p) not in late or id(p) in lazy_ids]
+                    plist = [p for p in plist if id(p) not in late]
             if plist:
                 if w_read is not None:
                     torch.cuda.current_stream(plist[0].device).wait_event(w_read)  # (long done: forked early)
                 with profiling.region("adam", 28 * sum(p.numel() for p in plist)):
                     self._launch_dense(lib, plist, hyper)
-            for p in lazy_dense:
-                st = self.state[p]
-                st["lazy_last"].copy_(st["step"].to(torch.int32).expand(p.shape[0]))
+            self._mark_current([p for p in lazy_dense if id(p) not in late])
             if rows:
                 if side is not None:
                     with torch.cuda.stream(side):
@@ -517,9 +525,16 @@ class FusedAdam(torch.optim.Optimizer):
         for held, hyper in late_plans:
             with profiling.region("adam", 28 * sum(p.numel() for p in held)):
                 self._launch_dense(lib, held, hyper)
+            self._mark_current([p for p in held if "lazy_last" in self.state[p]])
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
         return loss
+
+    def _mark_current(self, ps):
+        """Lazily updated tables that just took a dense step: every row is current through it."""
+        for p in ps:
+            st = self.state[p]
+            st["lazy_last"].copy_(st["step"].to(torch.int32).expand(p.shape[0]))
 
     def _init_state(self, p) -> bool:
         """Create ``p``'s Adam state (on the current stream) if it has none; True if created."""

@@ -41,16 +41,18 @@ def draw_negatives(users: np.ndarray, num_items: int, excl_ptr, excl_items, excl
     users = np.ascontiguousarray(users, dtype=np.int64)
     n = len(users) if perm is None else len(perm)
     if perm is not None:
-        perm = np.ascontiguousarray(perm, dtype=np.int64)
-        if n and (int(perm.min()) < 0 or int(perm.max()) >= len(users)):
-            raise native.EngineError("draw_negatives: perm indexes outside users")
+        perm = np.ascontiguousarray(perm, dtype=np.int64)  # (entries range-checked by the native loop)
     if out is None:
         out = np.empty(n, np.int64)
     elif out.dtype != np.int64 or out.shape != (n,) or not out.flags.c_contiguous:
         raise native.EngineError("draw_negatives: out must be a contiguous int64 array of the draws' length")
+    excl_ptr = np.ascontiguousarray(excl_ptr, np.int64)
+    n_users = len(excl_ptr) - 1
+    if n_users < 0 or (excl2_ptr is not None and len(excl2_ptr) != len(excl_ptr)):
+        raise native.EngineError("draw_negatives: the exclusion row pointers need n_users + 1 entries each")
     st, key, pos = _np_state()
     lib = native.lib()
-    tail = (np.ascontiguousarray(excl_ptr, np.int64).ctypes.data, np.ascontiguousarray(excl_items, np.int64).ctypes.data,
+    tail = (n_users, excl_ptr.ctypes.data, np.ascontiguousarray(excl_items, np.int64).ctypes.data,
             None if excl2_ptr is None else np.ascontiguousarray(excl2_ptr, np.int64).ctypes.data,
             None if excl2_items is None else np.ascontiguousarray(excl2_items, np.int64).ctypes.data, out.ctypes.data)
     kp = (key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
@@ -58,7 +60,7 @@ def draw_negatives(users: np.ndarray, num_items: int, excl_ptr, excl_items, excl
     if perm is None:
         rc = lib.fr_sampler_negatives(*kp, users.ctypes.data, n, *tail)
     else:
-        rc = lib.fr_sampler_negatives_perm(*kp, users.ctypes.data, perm.ctypes.data, n, *tail)
+        rc = lib.fr_sampler_negatives_perm(*kp, users.ctypes.data, len(users), perm.ctypes.data, n, *tail)
     native.check(rc, "fr_sampler_negatives")
     np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
     return out

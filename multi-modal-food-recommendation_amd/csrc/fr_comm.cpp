@@ -20,7 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include "fr_common.h"
+#include "fr_host.h"
 #include "fr_engine.h"
 
 namespace {

@@ -4,20 +4,9 @@
 #include <stdint.h>
 #include <string>
 #include "fr_engine.h"
+#include "fr_host.h"
 
 namespace fr {
-
-void set_error(const std::string& msg);
-
-inline int fail(int code, const std::string& msg) {
-  set_error(msg);
-  return code;
-}
-
-#define FR_REQUIRE(cond, msg)                                        \
-  do {                                                               \
-    if (!(cond)) return ::fr::fail(FR_EINVAL, std::string(__func__) + ": " + (msg)); \
-  } while (0)
 
 #define FR_HIP_CHECK(expr)                                                              \
   do {                                                                                  \

@@ -34,7 +34,7 @@
 #include "fr_engine.h"
 
 namespace fr {
-void set_error(const std::string& msg);  // fr_abi.cpp
+void set_error(const std::string& msg);  // fr_error.cpp
 }
 
 namespace {
@@ -71,11 +71,14 @@ bool parse_int(const char* b, const char* e, int64_t* out) {
     if (*b == '+' || *b == '-') { neg = *b == '-'; ++b; }
     if (b == e || *b < '0' || *b > '9') return false;
     uint64_t v = 0;
+    const uint64_t lim = neg ? uint64_t(INT64_MAX) + 1 : uint64_t(INT64_MAX);  // int64 range (the id arrays')
     bool prev_digit = false;
     for (; b < e; ++b) {
         char c = *b;
         if (c >= '0' && c <= '9') {
-            v = v * 10 + uint64_t(c - '0');
+            const uint64_t d = uint64_t(c - '0');
+            if (v > (lim - d) / 10) return false;  // outside int64: no wrapped id
+            v = v * 10 + d;
             prev_digit = true;
         } else if (c == '_' && prev_digit && b + 1 < e && b[1] >= '0' && b[1] <= '9') {
             prev_digit = false;
@@ -83,7 +86,7 @@ bool parse_int(const char* b, const char* e, int64_t* out) {
             return false;
         }
     }
-    *out = neg ? -int64_t(v) : int64_t(v);
+    *out = neg ? (v ? -int64_t(v - 1) - 1 : 0) : int64_t(v);
     return true;
 }
 

@@ -294,3 +294,24 @@ def test_plain_chunk_widens_light_graphs_only():
     adj = graph.Adjacency.sym_normalized(340, torch.as_tensor(rows), torch.as_tensor(cols))
     deg = np.diff(adj.rowptr.numpy())
     assert 128 < deg.max() <= 256 and adj.chunk == 256 and adj.n_split == 0 and adj.n_plain == 340
+
+
+def test_reserve_replays_flushes_before_the_ring_could_wrap():
+    """FusedAdam.reserve_replays: an unrolled graph runs ``n`` lazy steps before
+    note_replay sees them, so the optimiser flushes first when pending + n would pass hist_cap - 2."""
+    import torch
+    from FoodRec.engine.optim import FusedAdam
+    opt = FusedAdam([torch.nn.Parameter(torch.zeros(4, 4))], lazy_rows=True, hist_cap=8)
+    calls = []
+    opt.flush = lambda: (calls.append(opt._lazy_pending), setattr(opt, "_lazy_pending", 0))
+    opt.reserve_replays(4)  # nothing launched yet: nothing to flush
+    assert calls == []
+    opt._lazy_launched = True
+    opt._lazy_pending = 2
+    opt.reserve_replays(4)  # 2 + 4 = 6 = hist_cap - 2: within the bound
+    assert calls == []
+    opt._lazy_pending = 3
+    opt.reserve_replays(4)  # 3 + 4 = 7 > 6: flush first
+    assert calls == [3] and opt._lazy_pending == 0
+    with pytest.raises(ValueError):
+        opt.reserve_replays(7)  # more steps per replay than the ring can ever hold

@@ -152,3 +152,31 @@ def test_fused_scoring_evaluation_matches_torch_path(cuda):
         assert a.keys() == b.keys()
         for k in a:
             assert abs(a[k] - b[k]) <= 1e-9, (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("emb", [32, 128])
+def test_fused_scoring_falls_back_for_other_widths(cuda, emb):
+    """a model declaring ``fused_scores`` whose forward() tables are not fp32 [*, 64]
+    (here LightGCN at embedding_size 32 / 128) is evaluated through inference_fast instead of
+    fr_score_segments, with the same metrics as the non-fused path."""
+    from helpers import tiny_config, tiny_data
+    from FoodRec.common.trainer import Trainer
+    from FoodRec.utils.utils import get_model, init_seed
+    cfg = tiny_config("LightGCN", True, embedding_size=emb)
+    data = tiny_data(cfg)
+    init_seed(999)
+    model = get_model("LightGCN")(cfg, data).to(cfg["device"])
+    tr = Trainer(cfg, model)
+    assert tr._fused_scoring()
+    score, metrics = tr._valid_by_user_epoch(is_test=True)
+    cls = type(model)
+    saved = cls.__dict__.get("fused_scores", None)
+    cls.fused_scores = False
+    try:
+        score2, metrics2 = tr._valid_by_user_epoch(is_test=True)
+    finally:
+        if saved is None:
+            del cls.fused_scores
+        else:
+            cls.fused_scores = saved
+    assert metrics == metrics2
