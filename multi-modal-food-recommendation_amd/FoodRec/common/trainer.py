@@ -329,7 +329,7 @@ class GraphedDPStep(GraphedStep):
             fused = tr._book_fused(state, parts, accumulate) is not None
         finally:
             ops.book_taken()
-            ops.drop_pending()
+            ops.drop_pending_finalizes()
             ops.defer_counters(False)
         if fused:
             torch.autograd.backward(list(parts), grad_tensors=tr._ones_like(parts))
@@ -594,7 +594,7 @@ class Trainer(AbstractTrainer):
             booked = self._book_fused(state, parts, accumulate) if second_inter is None else None
         finally:
             ops.book_taken()  # (clears a request nothing answered)
-            ops.drop_pending()  # (partials a raising loss left behind)
+            ops.drop_pending_finalizes()  # (partials a raising loss left behind)
             ops.defer_counters(False)  # (applies the increments eagerly when the step was not booked)
         if booked is not None:
             # the loss sum is never materialised for autograd: each part back-propagates with a

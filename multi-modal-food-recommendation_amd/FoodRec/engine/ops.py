@@ -1675,7 +1675,7 @@ def finalize_pending() -> None:
         finalize_norms(t)
 
 
-def drop_pending() -> None:
+def drop_pending_finalizes() -> None:
     """Forget every deferred finalize (the trainer's ``finally`` after calculate_loss): a loss that
     raised between a deferring op and its consumer must not leave partials keyed by an address a
     later tensor may reuse.  On the success path finalize_pending / the loss ops consumed them."""
