@@ -26,6 +26,7 @@ the reference's format and read by the reference's own loader; only small slices
   wide_PRICAI_ModelX_foodcom.npz   CLUSSL, 2,000 clusters: first K training steps
   wide_PRICAI_ModelX_infonce_foodcom.npz   the same with the InfoNCE SSL term of the commented
                                    pricai_modelx.py:259 (CL_loss over the three view pairs)
+  wide_BPRMF_allrecipes.npz        BPRMF (the authored plugin, BASELINE config 1), B = 1024
     per step: the batch ids and every loss component; step 0: every gradient of the small
     parameters, sampled rows of the large ones; init and after K Adam steps: sampled parameter rows
 
@@ -306,6 +307,9 @@ WIDE = {  # case -> (model, synthetic shape, dataset name, training steps, confi
     # the InfoNCE SSL variant: the reference's commented line pricai_modelx.py:259 (CL_loss over the
     # three view pairs), computed by the harness with the reference model's own methods
     "PRICAI_ModelX_infonce": ("PRICAI_ModelX", "foodcom", "Foodcom", 3, {}, "infonce"),
+    # BASELINE config 1: the authored BPRMF plugin (oracle/ref_plugins) on the reference trainer at
+    # the Allrecipes shape, overall.yaml's batch (1024: the reference ships no BPRMF.yaml)
+    "BPRMF": ("BPRMF", "allrecipes", "Allrecipes", 4, {"reg_weight": 0.1}, None),
 }
 
 

@@ -237,7 +237,8 @@ def test_oracle_cpu_backend_covers_engine_models(model):
         assert torch.isfinite(state["acc"]).all() and int(state["nan"]) == 0
 
 
-@pytest.mark.parametrize("name,shape", [("CIKM_Model", "allrecipes"), ("PRICAI_ModelX", "foodcom")])
+@pytest.mark.parametrize("name,shape", [("CIKM_Model", "allrecipes"), ("PRICAI_ModelX", "foodcom"),
+                                        ("BPRMF", "allrecipes")])
 def test_wide_goldens_match_generator(name, shape):
     """The BASELINE-width reference fixtures (tests/golden/wide_*.npz) were produced on
     make_synthetic(shape, 0, negatives=False), the data bench.py trains on."""

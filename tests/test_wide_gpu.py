@@ -48,6 +48,9 @@ CASES = {  # fixture case -> (model, shape, dataset name, config overrides)
     # CLUSSL with the InfoNCE SSL term (ssl_mode infonce) vs the reference's commented
     # pricai_modelx.py:259 (CL_loss over the three [2B = 1024]-row view pairs), harness-computed
     "PRICAI_ModelX_infonce": ("PRICAI_ModelX", "foodcom", "Foodcom", {"ssl_mode": "infonce"}),
+    # BASELINE config 1: BPRMF vs the authored plugin on the reference trainer, B = 1024
+    # (overall.yaml's batch: the reference ships no BPRMF.yaml)
+    "BPRMF": ("BPRMF", "allrecipes", "Allrecipes", {"reg_weight": 0.1, "train_batch_size": 1024}),
 }
 _DATA = {}
 
