@@ -9,7 +9,7 @@ TAG=${1:-r5a}
 mkdir -p $OUT
 cd $R
 timeout -k 10 600 python -u -m pytest tests/test_graph_prepare_gpu.py tests/test_rank_gpu.py tests/test_late_drain_gpu.py \
-  tests/test_models_gpu.py tests/test_rowgrad_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  tests/test_models_gpu.py tests/test_rowgrad_gpu.py "tests/test_wide_gpu.py" -k "not (CIKM or PRICAI) or not wide" -m gpu -x -v --timeout 300 --timeout-method thread \
   > $OUT/gpu_tests_$TAG.log 2>&1 || { grep -E "FAILED|ERROR|Error" $OUT/gpu_tests_$TAG.log | head; tail -30 $OUT/gpu_tests_$TAG.log; exit 1; }
 tail -2 $OUT/gpu_tests_$TAG.log
 HR="--no-spmm-10m --no-config3 --no-config5 --no-config1 --no-cpu-baseline --no-eval"
