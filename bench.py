@@ -861,7 +861,8 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10, cpu=T
     ms = ev0.elapsed_time(ev1) / spmm_iters
     b = ops.spmm_bytes(adj, d, 1)
     spmm = {"avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
-            "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk}
+            "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), "chunk": adj.chunk,
+            **spmm_traffic("config4", ms)}
     del X, Y
     torch.cuda.empty_cache()
     cfg = Config("LightGCN_ID", "Synthetic10M", {"use_gpu": True, "seed": 999, "log_root": "/tmp/frlog/",
@@ -927,6 +928,24 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10, cpu=T
     return out
 
 
+def spmm_traffic(key, ms):
+    """PMC bytes per launch of the config-4 SpMM (``key``: config4 | beyond_mall) from the newest
+    profiles/r*/pmc_spmm10m.json (tools/pmc_spmm10m.py: FETCH_SIZE x 2 + WRITE_SIZE, bytes that left
+    the L2 -- DRAM plus Infinity Cache hits) and the rate they imply at this run's launch time
+    (``frac_dram``: that rate / the 8 TB/s peak; an upper bound on the DRAM-level fraction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_spmm10m.json")))
+    if not files:
+        return {"traffic": None}
+    with open(files[-1]) as f:
+        d = json.load(f).get(key)
+    if not d:
+        return {"traffic": None}
+    t = int(d["bytes_per_launch"])
+    return {"traffic": t, "traffic_gbps": round(t / ms / 1e6, 1), "frac_dram": round(t / ms / 1e6 / HBM_PEAK_GBPS, 4),
+            "traffic_source": os.path.relpath(files[-1], ROOT)}
+
+
 def spmm_beyond_mall(device, iters=5):
     """The config-4 SpMM with every gathered table far beyond the 256 MB Infinity Cache: 10M users x
     4M items (the item block of X is 1 GiB, the user block 2.56 GB), ~200M interactions, d=64 fp32 --
@@ -952,7 +971,7 @@ def spmm_beyond_mall(device, iters=5):
     b = ops.spmm_bytes(adj, d, 1)
     out = {"graph": "synthetic U=10M I=4M E=%d (nnz=%d)" % (g.n_edges, adj.nnz), "item_table_mb": I * d * 4 / 2**20,
            "avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
-           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4)}
+           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), **spmm_traffic("beyond_mall", ms)}
     del X, Y, g, adj
     torch.cuda.empty_cache()
     return out
