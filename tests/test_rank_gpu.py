@@ -162,7 +162,7 @@ def test_fused_scoring_falls_back_for_other_widths(cuda, emb):
     from helpers import tiny_config, tiny_data
     from FoodRec.common.trainer import Trainer
     from FoodRec.utils.utils import get_model, init_seed
-    cfg = tiny_config("LightGCN", True, embedding_size=emb)
+    cfg = tiny_config("LightGCN", True, embedding_size=emb, graph_inference_fast=True)
     data = tiny_data(cfg)
     init_seed(999)
     model = get_model("LightGCN")(cfg, data).to(cfg["device"])
