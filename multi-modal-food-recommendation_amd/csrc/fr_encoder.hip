@@ -407,6 +407,99 @@ __device__ __forceinline__ void lds_store(const float* p, int ld, float* __restr
   }
 }
 
+// A global -> LDS tile copy split in two: pf_issue puts this thread's loads in flight (rows [0, tv) of a
+// [*, COLS] tensor, rows clamped), pf_commit writes them to LDS (zero rows [tv, 80)).  Loads retire in
+// issue order (vmcnt), so a prefetch overlaps the work between the two calls only when no load issued
+// after it is waited for in between: the backward issues each phase's global operands (weight
+// fragments included) BEFORE the prefetch that must survive that phase.
+template <int COLS>
+struct TilePf {
+  static constexpr int PER = COLS / 4, TOT = ROWS * PER, ITER = (TOT + NT - 1) / NT;
+  float4 v[ITER];
+};
+
+template <int COLS>
+__device__ __forceinline__ void pf_issue(TilePf<COLS>& pf, const float* __restrict__ g, int tv) {
+  using P = TilePf<COLS>;
+#pragma unroll
+  for (int k = 0; k < P::ITER; ++k) {
+    const int e = min((int)threadIdx.x + k * NT, P::TOT - 1), r = e / P::PER, c4 = e % P::PER;
+    pf.v[k] = *reinterpret_cast<const float4*>(g + (int64_t)min(r, tv - 1) * COLS + 4 * c4);
+  }
+}
+
+template <int COLS>
+__device__ __forceinline__ void pf_commit(const TilePf<COLS>& pf, float* p, int ld, int tv) {
+  using P = TilePf<COLS>;
+#pragma unroll
+  for (int k = 0; k < P::ITER; ++k) {
+    const int e = threadIdx.x + k * NT, r = e / P::PER, c4 = e % P::PER;
+    if (P::TOT % NT == 0 || e < P::TOT)
+      *reinterpret_cast<float4*>(p + r * ld + 4 * c4) = r < tv ? pf.v[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// the per-row operands of a LayerNorm backward (or of the LN1 recompute) for this thread's rows
+// (16 lanes x float4 per row, rows grp, grp + 32, grp + 64): saved input rows, (mean, rstd), gamma
+// (and beta), issued ahead of their use
+struct LnPf {
+  static constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
+  float4 yv[NR];
+  float2 sv[NR];
+  float4 gg, bb;
+};
+
+__device__ __forceinline__ void ln_issue(LnPf& pf, const float* __restrict__ y, const float* __restrict__ st,
+                                         const float* __restrict__ g, const float* __restrict__ b, int tv) {
+  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+  pf.gg = *reinterpret_cast<const float4*>(g + 4 * l);
+  if (b) pf.bb = *reinterpret_cast<const float4*>(b + 4 * l);
+#pragma unroll
+  for (int k = 0; k < LnPf::NR; ++k) {
+    const int r = min(grp + k * LnPf::NG, tv - 1);
+    pf.yv[k] = *reinterpret_cast<const float4*>(y + (int64_t)r * E + 4 * l);
+    pf.sv[k] = *reinterpret_cast<const float2*>(st + 2 * r);
+  }
+}
+
+// the gemm_yw B operand (W [N x KO] row-major, output column tiles c0..c0+NC-1) for every N chunk,
+// loaded ahead of the GEMM (gemm_yw_pre)
+template <int NC, int N, int KO>
+struct YwFrags {
+  float b[N / 16][4][NC];
+};
+
+template <int NC, int N, int KO>
+__device__ __forceinline__ void yw_issue(YwFrags<NC, N, KO>& f, const float* __restrict__ W, int c0) {
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+#pragma unroll
+  for (int nc = 0; nc < N / 16; ++nc)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) f.b[nc][m][c] = W[(int64_t)(nc * 16 + 4 * h + m) * KO + 16 * (c0 + c) + i];
+}
+
+// gemm_yw with the B fragments already in registers (no global loads inside)
+template <int NC, int N, int KO, int R0, int NR, int NA>
+__device__ __forceinline__ void gemm_yw_pre(const float* Y, int ldy, const YwFrags<NC, N, KO>& f,
+                                            f32x4 (&acc)[NA][NC]) {
+  static_assert(NR <= NA, "accumulator rows");
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4;
+#pragma unroll
+  for (int nc = 0; nc < N / 16; ++nc) {
+    float4 a[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) a[r] = lds4(Y + (16 * (R0 + r) + i) * ldy + nc * 16 + 4 * h);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[r][c] = mfma4(comp(a[r], m), f.b[nc][m][c], acc[r][c]);
+  }
+}
+
 // LayerNorm forward over the 80 rows of an LDS [80 x 64] tile, in place; 16 lanes x float4 per row.
 // Saves y (the LN input) and (mean, rstd) for rows < tv.
 __device__ __forceinline__ void ln_rows_fwd(float* X, const float* __restrict__ g, const float* __restrict__ b,
@@ -438,28 +531,19 @@ __device__ __forceinline__ void ln_rows_fwd(float* X, const float* __restrict__ 
 // LayerNorm backward over the rows of an LDS [80 x 64] tile of upstream gradients, in place
 // (dY -> dX).  y: saved LN input rows (global), st: (mean, rstd).  dgamma / dbeta partials via the
 // scratch (NT / 16 row groups x 64, summed in group order) -> pg / pb.
-__device__ __forceinline__ void ln_rows_bwd(float* D, const float* __restrict__ y, const float* __restrict__ st,
-                                            const float* __restrict__ g, int tv, float* scratch,
+__device__ __forceinline__ void ln_rows_bwd(float* D, const LnPf& pf, int tv, float* scratch,
                                             float* __restrict__ pg, float* __restrict__ pb) {
   const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
-  constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
-  const float4 gg = *reinterpret_cast<const float4*>(g + 4 * l);
+  constexpr int NG = LnPf::NG, NR = LnPf::NR;
+  const float4 gg = pf.gg;
   float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
-  float4 yv[NR];
-  float2 sv[NR];
-#pragma unroll
-  for (int k = 0; k < NR; ++k) {  // issue every row's loads first (rows clamped to tv - 1)
-    const int r = min(grp + k * NG, tv - 1);
-    yv[k] = *reinterpret_cast<const float4*>(y + (int64_t)r * E + 4 * l);
-    sv[k] = *reinterpret_cast<const float2*>(st + 2 * r);
-  }
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     const int r = grp + k * NG;
     if (r >= tv) break;
     const float4 dy = lds4(D + r * LD_E + 4 * l);
-    const float4 v = yv[k];
-    const float mean = sv[k].x, rstd = sv[k].y;
+    const float4 v = pf.yv[k];
+    const float mean = pf.sv[k].x, rstd = pf.sv[k].y;
     const float4 xh = make_float4((v.x - mean) * rstd, (v.y - mean) * rstd, (v.z - mean) * rstd, (v.w - mean) * rstd);
     const float4 gd = make_float4(dy.x * gg.x, dy.y * gg.y, dy.z * gg.z, dy.w * gg.w);
     const float m1 = group_sum<16>(gd.x + gd.y + gd.z + gd.w) * (1.f / E);
@@ -985,33 +1069,49 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   //    the columns, summed over that call's workgroups in order (deterministic)
   if (a.prev_part) prev_reduce(a.prev_part, (int)gridDim.x, a.prev_grad, RD);
 
+  // Global operands are issued one phase ahead of their use, in the order they are waited for (loads
+  // retire in order): dY2, then LN2's rows, then act' (its ~80 KB per workgroup lands during LN2).
+  TilePf<E> pf_dout;
+  pf_issue(pf_dout, a.dout + tok0 * E, tv);
+  LnPf ln2;
+  ln_issue(ln2, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, nullptr, tv);
+  TilePf<FF> pf_fact;
+  pf_issue(pf_fact, a.fact + tok0 * FF, tv);
+
   // 1. LN2 backward: RB = dY2 (pad rows 0)
-  lds_load<E>(RB, LD_E, a.dout + tok0 * E, tv);
+  pf_commit(pf_dout, RB, LD_E, tv);
   __syncthreads();
   FR_MARK(1, 1);
-  ln_rows_bwd(RB, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, tv, RD, part + OFF_G2, part + OFF_BE2);
+  ln_rows_bwd(RB, ln2, tv, RD, part + OFF_G2, part + OFF_BE2);
 
   // 2. dG = dropout2'(dY2) -> RC;  act' (saved by the forward) -> RA
   drop_pairs(RB, RC, ks.k[3], tok0, w.thr[3], w.scale[3]);
-  lds_load<FF>(RA, LD_FF, a.fact + tok0 * FF, tv);
+  pf_commit(pf_fact, RA, LD_FF, tv);
   __syncthreads();
   FR_MARK(1, 2);
+
+  // the step-4 GEMM's W2 fragments, then dact at this lane's step-4 output elements (fragment
+  // layout): both in flight across the dW2 slab below
+  YwFrags<2, E, FF> w2f;
+  yw_issue(w2f, w.w2, 4 * sg + 2 * hf);
+  float4 pv[2][RT];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+      pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, sg, 2 * hf + cc, r, lane));
 
   // 3. dW2 = dG^T act'  [64 x 256] (wave: k-tiles 2w, 2w+1);  db2
   wgrad_tiles<4, 2>(RC, LD_E, RA, LD_FF, 0, 2 * wave, part + OFF_W2, FF);
   colsum(RC, LD_E, E, part + OFF_B2);
 
+  LnPf ln1;  // y1 rows / stats, gamma1 / beta1: the LN1 recompute (step 5) and the LN1 backward (step 8)
   {  // 4. dact' = dG W2 [80 x 256]; dpre = dact' * (keep * scale * act'(pre)) -> RA  (wave: column tiles
      // 4sg + 2hf, +1; every row tile)
     f32x4 acc[RT][2];
     zero_acc(acc);
-    gemm_yw<2, E, FF, 0, RT>(RC, LD_E, w.w2, 4 * sg + 2 * hf, acc);
-    float4 pv[2][RT];  // dact at this lane's output elements (fragment layout): in flight across the barrier
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-        pv[cc][r] = *reinterpret_cast<const float4*>(a.dact + dact_frag(blockIdx.x, sg, 2 * hf + cc, r, lane));
+    gemm_yw_pre<2, E, FF, 0, RT>(RC, LD_E, w2f, acc);
+    ln_issue(ln1, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, w.be1, tv);
     __syncthreads();  // every wave is done reading act' from RA
     FR_MARK(1, 3);
 #pragma unroll
@@ -1033,23 +1133,13 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   colsum(RA, LD_FF, FF, part + OFF_B1);
   {
     const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
-    const float4 gg = *reinterpret_cast<const float4*>(w.g1 + 4 * l);
-    const float4 bb = *reinterpret_cast<const float4*>(w.be1 + 4 * l);
-    constexpr int NG = NT / 16, NR = (ROWS + NG - 1) / NG;
-    float4 yv[NR];
-    float2 sv[NR];
+    const float4 gg = ln1.gg, bb = ln1.bb;
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      const int r = min(grp + k * NG, tv - 1);
-      yv[k] = *reinterpret_cast<const float4*>(a.y1 + (tok0 + r) * E + 4 * l);
-      sv[k] = *reinterpret_cast<const float2*>(a.st1 + 2 * (tok0 + r));
-    }
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      const int r = grp + k * NG;
+    for (int k = 0; k < LnPf::NR; ++k) {
+      const int r = grp + k * LnPf::NG;
       if (r >= ROWS) break;
-      const float4 v = yv[k];
-      const float mean = sv[k].x, rstd = sv[k].y;
+      const float4 v = ln1.yv[k];
+      const float mean = ln1.sv[k].x, rstd = ln1.sv[k].y;
       const float4 o = make_float4(fmaf((v.x - mean) * rstd, gg.x, bb.x), fmaf((v.y - mean) * rstd, gg.y, bb.y),
                                    fmaf((v.z - mean) * rstd, gg.z, bb.z), fmaf((v.w - mean) * rstd, gg.w, bb.w));
       *reinterpret_cast<float4*>(RC + r * LD_E + 4 * l) = r < tv ? o : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1073,15 +1163,22 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
       for (int q = 0; q < 4; ++q) RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
     }
   }
+  // ctx (step 9), the step-11 W_o fragments, then qkv (step 11): in flight across steps 8-10
+  TilePf<E> pf_ctx;
+  pf_issue(pf_ctx, a.ctx + tok0 * E, tv);
+  YwFrags<1, E, E> wof;
+  yw_issue(wof, w.w_o, sg);
+  TilePf<QKV> pf_qkv;
+  pf_issue(pf_qkv, a.qkv + tok0 * QKV, tv);
   __syncthreads();
   FR_MARK(1, 6);
 
   // 8. LN1 backward: RB = dY1
-  ln_rows_bwd(RB, a.y1 + tok0 * E, a.st1 + 2 * tok0, w.g1, tv, RD, part + OFF_G1, part + OFF_BE1);
+  ln_rows_bwd(RB, ln1, tv, RD, part + OFF_G1, part + OFF_BE1);
 
   // 9. dO = dropout1'(dY1) -> RC;  ctx -> RD
   drop_pairs(RB, RC, ks.k[1], tok0, w.thr[1], w.scale[1]);
-  lds_load<E>(RD, LD_E, a.ctx + tok0 * E, tv);
+  pf_commit(pf_ctx, RD, LD_E, tv);
   __syncthreads();
   FR_MARK(1, 7);
 
@@ -1099,8 +1196,9 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   {  // 11. dctx = dO W_o -> RC;  qkv -> RA
     f32x4 acc[RT0][1];
     zero_acc(acc);
-    FR_GEMM_YW(1, E, E, RC, LD_E, w.w_o, sg, acc);
-    lds_load<QKV>(RA, LD_QKV, a.qkv + tok0 * QKV, tv);
+    if (hf == 0) gemm_yw_pre<1, E, E, 0, RT0>(RC, LD_E, wof, acc);
+    else gemm_yw_pre<1, E, E, RT0, RT - RT0>(RC, LD_E, wof, acc);
+    pf_commit(pf_qkv, RA, LD_QKV, tv);
     __syncthreads();
     FR_MARK(1, 8);
     const int col = 16 * sg + i16;
@@ -1194,6 +1292,49 @@ __global__ __launch_bounds__(256) void enc_reduce_kernel(const float4* __restric
   }
 }
 
+// The same sum with every load a contiguous 1 KiB piece of one workgroup's partial row (round 5): a
+// block owns 64 float4 columns (lane = column) and RW_W waves; wave w sums workgroups w, w + RW_W,
+// w + 2 RW_W, ... in order (RW_UNR loads in flight), then the waves' sums are added in wave order
+// through LDS.  Deterministic like the kernel above (a different fixed order).  196 blocks of 16 waves
+// at NPART: every load streams whole 128-B lines of one partial row.
+constexpr int RW_W = 16, RW_UNR = 16;
+__global__ __launch_bounds__(64 * RW_W) void enc_reduce_rows_kernel(const float4* __restrict__ part, int nwg,
+                                                                   float4* __restrict__ grad) {
+  constexpr int N4 = NPART / 4;
+  __shared__ float4 sl[RW_W][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, cc = min(c, N4 - 1);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g0 = w; g0 < nwg; g0 += RW_W * RW_UNR) {
+    float4 v[RW_UNR];
+#pragma unroll
+    for (int k = 0; k < RW_UNR; ++k) v[k] = part[(int64_t)min(g0 + k * RW_W, nwg - 1) * N4 + cc];
+#pragma unroll
+    for (int k = 0; k < RW_UNR; ++k)
+      if (g0 + k * RW_W < nwg) s = f4_add(s, v[k]);
+  }
+  sl[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < N4) {
+    float4 t = sl[0][lane];
+#pragma unroll
+    for (int k = 1; k < RW_W; ++k) t = f4_add(t, sl[k][lane]);
+    grad[c] = t;
+  }
+}
+
+// 1: enc_reduce_rows_kernel (default), 0: enc_reduce_kernel (A/B: fr_encoder_options)
+int g_reduce_mode = 1;
+
+void launch_reduce(const float* part, int64_t nwg, float* grad, hipStream_t s) {
+  if (g_reduce_mode == 1)
+    hipLaunchKernelGGL(enc_reduce_rows_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, 64)), dim3(64 * RW_W), 0, s,
+                       reinterpret_cast<const float4*>(part), (int)nwg, reinterpret_cast<float4*>(grad));
+  else
+    hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(part), (int)nwg, reinterpret_cast<float4*>(grad));
+}
+
 template <int L>
 int launch_fwd(const FwdArgs& a, hipStream_t s) {
   const int64_t nwg = fr::ceil_div(a.ns, ROWS / L);
@@ -1208,8 +1349,7 @@ int launch_bwd(const BwdArgs& a, float* grad, hipStream_t s) {
   hipLaunchKernelGGL(enc_bwd_kernel<L>, dim3((unsigned)nwg), dim3(NT), 0, s, a);
   FR_LAUNCH_CHECK();
   if (grad) {
-    hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0, s,
-                       reinterpret_cast<const float4*>(a.part), (int)nwg, reinterpret_cast<float4*>(grad));
+    launch_reduce(a.part, nwg, grad, s);
     FR_LAUNCH_CHECK();
   }
   return FR_OK;
@@ -1326,9 +1466,15 @@ extern "C" int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, 
   FR_REQUIRE(n_seq > 0 && supported_len(L), "L must be one of 4, 5, 8, 10, 16, 20 and n_seq > 0");
   FR_REQUIRE(d_partials && d_grad && fr::aligned16(d_partials) && fr::aligned16(d_grad), "null or unaligned operand");
   const int64_t nwg = fr::ceil_div(n_seq, ROWS / L);
-  hipLaunchKernelGGL(enc_reduce_kernel, dim3((unsigned)fr::ceil_div(NPART / 4, RED_COLS)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(d_partials), (int)nwg,
-                     reinterpret_cast<float4*>(d_grad));
+  launch_reduce(d_partials, nwg, d_grad, reinterpret_cast<hipStream_t>(stream));
   FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+// A/B switches of the encoder's launches (host-side state of this library): reduce_mode 1 = the
+// row-streaming ordered reduction (default), 0 = the round-4 column-slice one; -1 leaves it.
+extern "C" int fr_encoder_options(int reduce_mode) {
+  FR_REQUIRE(reduce_mode >= -1 && reduce_mode <= 1, "reduce_mode must be -1, 0 or 1");
+  if (reduce_mode >= 0) g_reduce_mode = reduce_mode;
   return FR_OK;
 }

@@ -33,8 +33,12 @@ def main():
     ap.add_argument("--p", type=float, default=0.5)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--phases", action="store_true", help="per-phase s_memtime stamps of workgroup 0")
+    ap.add_argument("--reduce-mode", type=int, default=-1,
+                    help="fr_encoder_options: 1 row-streaming partial reduction, 0 round-4 column slices")
+    ap.add_argument("--no-torch", action="store_true", help="skip torch's own layer")
     args = ap.parse_args()
-    from FoodRec.engine import ops
+    from FoodRec.engine import native, ops
+    native.check(native.lib().fr_encoder_options(args.reduce_mode), "fr_encoder_options")
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     layer = torch.nn.TransformerEncoderLayer(64, 2, 256, dropout=args.p, activation="gelu").to(dev)
@@ -64,12 +68,11 @@ def main():
     with torch.no_grad():
         t_fwd = timed(fwd, args.iters)
     t_fb = timed(fwd_bwd, args.iters)
-    t_torch = timed(torch_fwd_bwd, args.iters)
+    t_torch = 0.0 if args.no_torch else timed(torch_fwd_bwd, args.iters)
     phases = None
     if args.phases:
         import ctypes
         import numpy as np
-        from FoodRec.engine import native
         lib = native.lib()
         native.check(lib.fr_encoder_profile(1, None), "fr_encoder_profile")
         for _ in range(3):
