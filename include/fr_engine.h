@@ -535,8 +535,8 @@ int fr_encoder_bwd(const float* d_dout, const float* d_x, const float* d_mask, i
                    const float* d_st2, float* d_dx, float* d_grad, float* d_partials, int64_t partial_floats,
                    const float* d_prev_partials, float* d_prev_grad, void* stream);
 int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, float* d_grad, void* stream);
-/* A/B switches (host-side library state): reduce_mode 1 = the ordered partial reduction streaming
- * whole 1 KiB pieces of each workgroup's partial row (default), 0 = the round-4 column-slice form;
+/* A/B switches (host-side library state): reduce_mode 0 = the column-slice ordered partial reduction
+ * (default), 1 = the form streaming whole 1 KiB pieces of each workgroup's partial row;
  * -1 leaves the setting.  Both are deterministic. */
 int fr_encoder_options(int reduce_mode);
 

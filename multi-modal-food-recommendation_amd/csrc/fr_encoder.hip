@@ -1071,15 +1071,17 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
 
   // Global operands are issued one phase ahead of their use, in the order they are waited for (loads
   // retire in order): dY2, then LN2's rows, then act' (its ~80 KB per workgroup lands during LN2).
+  // (act' is issued only once dY2 has landed: a burst issued ahead of it stalls the issuing waves for
+  // its whole transfer -- the loads are bandwidth-, not latency-bound -- and dY2 waits behind it)
   TilePf<E> pf_dout;
   pf_issue(pf_dout, a.dout + tok0 * E, tv);
   LnPf ln2;
   ln_issue(ln2, a.y2 + tok0 * E, a.st2 + 2 * tok0, w.g2, nullptr, tv);
-  TilePf<FF> pf_fact;
-  pf_issue(pf_fact, a.fact + tok0 * FF, tv);
 
   // 1. LN2 backward: RB = dY2 (pad rows 0)
   pf_commit(pf_dout, RB, LD_E, tv);
+  TilePf<FF> pf_fact;
+  pf_issue(pf_fact, a.fact + tok0 * FF, tv);
   __syncthreads();
   FR_MARK(1, 1);
   ln_rows_bwd(RB, ln2, tv, RD, part + OFF_G2, part + OFF_BE2);
@@ -1163,13 +1165,11 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
       for (int q = 0; q < 4; ++q) RB[(16 * (r0 + r) + 4 * h4 + q) * LD_E + col] += acc[r][0][q];
     }
   }
-  // ctx (step 9), the step-11 W_o fragments, then qkv (step 11): in flight across steps 8-10
+  // ctx (step 9) and the step-11 W_o fragments: in flight across the LN1 backward
   TilePf<E> pf_ctx;
   pf_issue(pf_ctx, a.ctx + tok0 * E, tv);
   YwFrags<1, E, E> wof;
   yw_issue(wof, w.w_o, sg);
-  TilePf<QKV> pf_qkv;
-  pf_issue(pf_qkv, a.qkv + tok0 * QKV, tv);
   __syncthreads();
   FR_MARK(1, 6);
 
@@ -1179,6 +1179,8 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   // 9. dO = dropout1'(dY1) -> RC;  ctx -> RD
   drop_pairs(RB, RC, ks.k[1], tok0, w.thr[1], w.scale[1]);
   pf_commit(pf_ctx, RD, LD_E, tv);
+  TilePf<QKV> pf_qkv;  // qkv (step 11): in flight across the dW_o slab and the dctx GEMM
+  pf_issue(pf_qkv, a.qkv + tok0 * QKV, tv);
   __syncthreads();
   FR_MARK(1, 7);
 
@@ -1323,8 +1325,9 @@ __global__ __launch_bounds__(64 * RW_W) void enc_reduce_rows_kernel(const float4
   }
 }
 
-// 1: enc_reduce_rows_kernel (default), 0: enc_reduce_kernel (A/B: fr_encoder_options)
-int g_reduce_mode = 1;
+// 0: enc_reduce_kernel (default), 1: enc_reduce_rows_kernel (A/B: fr_encoder_options; measured
+// 9.9 vs 9.7 us alone at HealthRec's shape, not kept as the default)
+int g_reduce_mode = 0;
 
 void launch_reduce(const float* part, int64_t nwg, float* grad, hipStream_t s) {
   if (g_reduce_mode == 1)
@@ -1471,8 +1474,8 @@ extern "C" int fr_encoder_reduce(const float* d_partials, int64_t n_seq, int L, 
   return FR_OK;
 }
 
-// A/B switches of the encoder's launches (host-side state of this library): reduce_mode 1 = the
-// row-streaming ordered reduction (default), 0 = the round-4 column-slice one; -1 leaves it.
+// A/B switches of the encoder's launches (host-side state of this library): reduce_mode 0 = the
+// column-slice ordered reduction (default), 1 = the row-streaming one; -1 leaves it.
 extern "C" int fr_encoder_options(int reduce_mode) {
   FR_REQUIRE(reduce_mode >= -1 && reduce_mode <= 1, "reduce_mode must be -1, 0 or 1");
   if (reduce_mode >= 0) g_reduce_mode = reduce_mode;

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--phases", action="store_true", help="per-phase s_memtime stamps of workgroup 0")
     ap.add_argument("--reduce-mode", type=int, default=-1,
-                    help="fr_encoder_options: 1 row-streaming partial reduction, 0 round-4 column slices")
+                    help="fr_encoder_options: 0 column-slice partial reduction (default), 1 row-streaming")
     ap.add_argument("--no-torch", action="store_true", help="skip torch's own layer")
     args = ap.parse_args()
     from FoodRec.engine import native, ops
