@@ -1427,13 +1427,14 @@ def pending_drain_params() -> set:
     return {id(w) for _, _, w in _PENDING_DRAINS}
 
 
-def run_pending_drains() -> None:
+def run_pending_drains(after=None) -> None:
     """Add the rows _join_branch left (late mode) into their tables' gradients on the branch stream,
     forked where the backward pass ended; the current stream waits for them (before the update of
-    those tables)."""
+    those tables).  ``after(stream)``: more work issued on the branch stream behind the last drain,
+    before the current stream's join (FusedAdam: the drained tables' own update)."""
     pend = list(_PENDING_DRAINS)
     _PENDING_DRAINS.clear()
-    for fork, defer, ingre_w in pend:
+    for k, (fork, defer, ingre_w) in enumerate(pend):
         main = torch.cuda.current_stream(ingre_w.device)
         side = _branch_stream(ingre_w.device)
         side.wait_event(fork)
@@ -1444,6 +1445,8 @@ def run_pending_drains() -> None:
             ingre_w.grad.record_stream(side)
         with torch.cuda.stream(side):
             _drain_into(defer, ingre_w)
+            if after is not None and k == len(pend) - 1:
+                after(side)
             done = torch.cuda.Event()
             done.record(side)
         main.wait_event(done)

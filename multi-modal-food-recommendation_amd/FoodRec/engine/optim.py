@@ -153,6 +153,11 @@ def _row_grad_ok(p, ids, G) -> bool:
             and ids.numel() <= ROW_GRAD_MAX and G.dtype == torch.float32 and p.data_ptr() % 16 == 0)
 
 
+# FR_HELD_ON_BRANCH=0: a late-drained table's update runs on the current stream after the join
+# (round 4); default: on the branch stream right behind the scatter of its deferred rows
+HELD_ON_BRANCH = os.environ.get("FR_HELD_ON_BRANCH", "1") != "0"
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, lazy_rows=False,
                  hist_cap=8192, lazy_slices=0):
@@ -493,7 +498,12 @@ class FusedAdam(torch.optim.Optimizer):
             plans.append((group, plist, rows, hyper))
         if side is not None and dirty:
             side.wait_stream(main)
-        # pass 2: the launches
+        # pass 2: the launches.  ``before_dense``: everything pass 1 wrote on the current stream, before
+        # the first update launch (a held table's update on the branch stream waits for it, not for them)
+        before_dense = None
+        if late and HELD_ON_BRANCH:
+            before_dense = torch.cuda.Event()
+            before_dense.record()
         for group, plist, rows, hyper in plans:
             lazy_dense = [p for p in plist if "lazy_last" in self.state[p]]
             # a lazily updated table taking a dense step (a dense .grad: more ids than the row path
@@ -520,12 +530,24 @@ class FusedAdam(torch.optim.Optimizer):
                         self._launch_rows(lib, rows, hyper[:-1] + (side.cuda_stream,))
                 else:
                     self._launch_rows(lib, rows, hyper)
+        def launch_held(stream=None):
+            for held, hyper in late_plans:
+                if stream is not None:
+                    stream.wait_event(before_dense)
+                    hyper = hyper[:-1] + (stream.cuda_stream,)
+                with profiling.region("adam", 28 * sum(p.numel() for p in held)):
+                    self._launch_dense(lib, held, hyper)
+                self._mark_current([p for p in held if "lazy_last" in self.state[p]])
+
         if late or ops.pending_drain_params():
-            ops.run_pending_drains()
-        for held, hyper in late_plans:
-            with profiling.region("adam", 28 * sum(p.numel() for p in held)):
-                self._launch_dense(lib, held, hyper)
-            self._mark_current([p for p in held if "lazy_last" in self.state[p]])
+            if late_plans and before_dense is not None:
+                # the held tables' update right behind their rows' scatter on the branch stream: no
+                # cross-queue hop between the scatter and the update; the current stream joins after
+                ops.run_pending_drains(after=launch_held)
+                late_plans = []
+            else:
+                ops.run_pending_drains()
+        launch_held()
         if side is not None:
             torch.cuda.current_stream(side.device).wait_stream(side)
         return loss
