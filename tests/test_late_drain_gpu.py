@@ -27,9 +27,9 @@ def _one_step(cuda, late, monkeypatch):
     seen = {}
     orig = ops.run_pending_drains
 
-    def spy():
+    def spy(**kw):
         seen["pending"] = seen.get("pending", 0) + len(ops._PENDING_DRAINS)
-        orig()
+        orig(**kw)
     monkeypatch.setattr(ops, "run_pending_drains", spy)
     tr.train_step(batch, 0, st)
     torch.cuda.synchronize()
