@@ -153,9 +153,10 @@ def _row_grad_ok(p, ids, G) -> bool:
             and ids.numel() <= ROW_GRAD_MAX and G.dtype == torch.float32 and p.data_ptr() % 16 == 0)
 
 
-# FR_HELD_ON_BRANCH=0: a late-drained table's update runs on the current stream after the join
-# (round 4); default: on the branch stream right behind the scatter of its deferred rows
-HELD_ON_BRANCH = os.environ.get("FR_HELD_ON_BRANCH", "1") != "0"
+# FR_HELD_ON_BRANCH=1: a late-drained table's update on the branch stream right behind the scatter of
+# its deferred rows (round-5 experiment: 0.694 / 0.691 vs 0.688 / 0.689 ms per step, slower, off);
+# default: on the current stream after the join (round 4)
+HELD_ON_BRANCH = os.environ.get("FR_HELD_ON_BRANCH", "0") == "1"
 
 
 class FusedAdam(torch.optim.Optimizer):
