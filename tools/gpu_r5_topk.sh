@@ -19,3 +19,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_topk_$TAG -o run -- python3 $R/tools/bench_topk.py \
   --only 20,0 --reps 3 --shape ${BEST:-3} > $OUT/topk_prof_$TAG.log 2>&1 || { tail -5 $OUT/topk_prof_$TAG.log; exit 1; }
 cut -d, -f1-4 $(find $OUT/prof_topk_$TAG -name "*kernel_stats.csv") | cut -c1-150 | head -8
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_ssl_$TAG -o run -- python3 $R/tools/profile_ssl.py \
+  > $OUT/ssl_prof_$TAG.log 2>&1 || { tail -5 $OUT/ssl_prof_$TAG.log; exit 1; }
+cut -d, -f1-4,6 $(find $OUT/prof_ssl_$TAG -name "*kernel_stats.csv") | cut -c1-150 | grep -E "nce|dcor|Name"
