@@ -456,6 +456,152 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   }
 }
 
+// APPEND pass, software-pipelined (bf16 tables): the threshold epilogue of tile t - 1 is issued
+// between the MFMAs of tile t, so its VALU work (compares, candidate extraction) fills the matrix
+// pipe's issue shadow instead of following it; the item tiles rotate through three LDS buffers (one
+// barrier per tile: a buffer is rewritten two tiles after its last read).  Same candidates, same
+// regions and counts as topk_score_kernel<.., kAppend, NB, 1, 8> (the merge sorts them).
+template <int D, int NB>
+__global__ __launch_bounds__(kThreads) void topk_append_pipe_kernel(ScoreArgs a) {
+  using T = uint16_t;
+  using C = Cfg<T, D, NB>;
+  constexpr int NBUF = 3;
+  constexpr int CH = (C::TILE * C::CPR + kThreads - 1) / kThreads;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * C::STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t n_users = a.d_nu ? (int64_t)*a.d_nu : a.n_users;
+  const int total = a.n_utiles * a.n_splits;
+  const int b = blockIdx.x, xcd = b & 7, q8 = total >> 3, r8 = total & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int ut = wg % a.n_utiles, sp = wg / a.n_utiles;
+  if ((int64_t)ut * kUsersPerWG >= n_users) return;
+  const int64_t slot = (int64_t)ut * kUsersPerWG + wave * 32 + r;
+  const bool uvalid = slot < n_users;
+  const int64_t urow = uvalid ? (a.urows ? (int64_t)a.urows[slot] : slot) : 0;
+  const int64_t i_lo = (int64_t)sp * a.span;
+  const int64_t i_hi = min(a.n_items, i_lo + a.span);
+  const int n_tiles = (int)((i_hi - i_lo + C::TILE - 1) / C::TILE);
+  const T* __restrict__ It = reinterpret_cast<const T*>(a.It);
+  const int64_t ldi = a.ldi;
+  bf16x8 bf[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s)
+    bf[s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(a.Uq) + urow * a.ldu + 16 * s + 8 * h);
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[s])));
+  const float thr = uvalid ? a.thr[slot] : INFINITY;
+  const int64_t region = (slot * a.n_splits + sp) * 2 + h;
+  int cnt = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  int srow[CH], sdst[CH];
+  const char* ssrc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int x = tid + c * kThreads;
+    const int row = x / C::CPR, cc = x % C::CPR;
+    srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;
+    sdst[c] = (row * C::CPR + swz<T, D>(row, cc)) * 16;
+    ssrc[c] = reinterpret_cast<const char*>(It) + ((i_lo + row) * ldi) * (int64_t)sizeof(T) + cc * 16;
+  }
+  const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
+  uint4 stg[CH];
+  auto load_tile = [&](int tt) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t item = i_lo + (int64_t)tt * C::TILE + srow[c];
+      stg[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)tt * tile_bytes) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + buf * C::STAGE + sdst[c]) = stg[c];
+  };
+  int aoff[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) aoff[s] = a_off<T, D>(r, h, s);
+
+  // candidates of one 32-item block: this lane's 16 scores (items ib + (j & 3) + 8 (j >> 2)) >= thr
+  auto epilogue = [&](const f32x16& av, int64_t ib) {
+    uint32_t mask = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mask |= av[j] >= thr ? (1u << j) : 0u;
+    if (ib + 28 >= i_hi) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
+    }
+    if (!uvalid) mask = 0u;
+    while (__ballot(mask != 0u)) {
+      const bool act = mask != 0u;
+      const int j = act ? __builtin_ctz(mask) : 0;
+      mask &= mask - 1u;
+      const float v0 = (j & 1) ? av[1] : av[0], v1 = (j & 1) ? av[3] : av[2];
+      const float v2 = (j & 1) ? av[5] : av[4], v3 = (j & 1) ? av[7] : av[6];
+      const float v4 = (j & 1) ? av[9] : av[8], v5 = (j & 1) ? av[11] : av[10];
+      const float v6 = (j & 1) ? av[13] : av[12], v7 = (j & 1) ? av[15] : av[14];
+      const float w0 = (j & 2) ? v1 : v0, w1 = (j & 2) ? v3 : v2, w2 = (j & 2) ? v5 : v4, w3 = (j & 2) ? v7 : v6;
+      const float x0 = (j & 4) ? w1 : w0, x1 = (j & 4) ? w3 : w2;
+      const float sc = (j & 8) ? x1 : x0;
+      if (act) {
+        if (cnt < a.cap) {
+          a.cs[region * a.cap + cnt] = sc;
+          a.ci[region * a.cap + cnt] = (int32_t)((ib + (j & 3) + 8 * (j >> 2)) * a.item_mul);
+        }
+        ++cnt;
+      }
+    }
+  };
+
+  // prologue: tiles 0 and 1 staged, tile 2 in registers
+  if (n_tiles > 0) { load_tile(0); store_tile(0); }
+  if (n_tiles > 1) { load_tile(1); store_tile(1); }
+  __syncthreads();
+  if (n_tiles > 2) load_tile(2);
+  f32x16 prev[NB];
+  for (int t = 0; t <= n_tiles; ++t) {
+    f32x16 acc[NB];
+    if (t < n_tiles) {
+      const char* abuf = smem + (t % NBUF) * C::STAGE;
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
+      bf16x8 af[2][NB];
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) af[0][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + aoff[0]);
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        if (s + 1 < C::KS) {
+#pragma unroll
+          for (int bb = 0; bb < NB; ++bb)
+            af[(s + 1) & 1][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + aoff[s + 1]);
+        }
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][bb], bf[s], acc[bb], 0, 0, 0);
+      }
+    }
+    // the previous tile's candidates, issued behind this tile's MFMAs
+    if (t > 0) {
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) epilogue(prev[bb], i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h);
+    }
+    if (t < n_tiles) {
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) prev[bb] = acc[bb];
+    }
+    // tile t + 2 into the buffer tile t - 1 used (every wave passed the last barrier after reading it)
+    if (t + 2 < n_tiles) store_tile((t + 2) % NBUF);
+    __syncthreads();
+    if (t + 3 < n_tiles) load_tile(t + 3);
+  }
+  if (uvalid) a.cc[region] = cnt;
+}
+
 struct MergeArgs {
   const float* ps; const int32_t* pi; const int32_t* cnt;   // regions (cnt null: every region holds k)
   int cap; int n_regions;
@@ -563,10 +709,10 @@ __global__ void topk_zero_kernel(int32_t* p) {
 // APPEND kernel shape (A/B: fr_topk_options): (waves per workgroup, 32-item blocks per staged tile,
 // 32-user sets per wave).  Several user sets apply to bf16 tables (fp32 tables take shape 0).
 int g_append_shape = 0;
-constexpr int kShapes = 6;
-constexpr int kAppendW[kShapes] = {8, 8, 8, 4, 4, 4};
-constexpr int kAppendNB[kShapes] = {2, 1, 4, 2, 4, 2};
-constexpr int kAppendUW[kShapes] = {1, 2, 1, 2, 2, 1};
+constexpr int kShapes = 7;  // 6: (8, 2, 1) software-pipelined (topk_append_pipe_kernel)
+constexpr int kAppendW[kShapes] = {8, 8, 8, 4, 4, 4, 8};
+constexpr int kAppendNB[kShapes] = {2, 1, 4, 2, 4, 2, 2};
+constexpr int kAppendUW[kShapes] = {1, 2, 1, 2, 2, 1, 1};
 
 int append_users_per_wg(int shape) { return kAppendW[shape] * 32 * kAppendUW[shape]; }
 
@@ -583,6 +729,7 @@ hipError_t launch_score_t(const ScoreArgs& a, hipStream_t s) {
         case 3: kern = topk_score_kernel<T, D, 1, kAppend, 2, 2, 4>; break;
         case 4: kern = topk_score_kernel<T, D, 1, kAppend, 4, 2, 4>; break;
         case 5: kern = topk_score_kernel<T, D, 1, kAppend, 2, 1, 4>; break;
+        case 6: kern = topk_append_pipe_kernel<D, 2>; break;
         default: kern = topk_score_kernel<T, D, 1, kAppend, 2, 1, 8>; break;
       }
     } else {
@@ -761,7 +908,7 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
 // A/B switch (host-side library state): the APPEND kernel's shape (see g_append_shape); -1 leaves it.
 // The workspace size depends on it: query fr_topk_workspace after setting it.
 extern "C" int fr_topk_options(int append_shape) {
-  FR_REQUIRE(append_shape >= -1 && append_shape < kShapes, "append_shape must be in [-1, 5]");
+  FR_REQUIRE(append_shape >= -1 && append_shape < kShapes, "append_shape must be in [-1, 6]");
   if (append_shape >= 0) g_append_shape = append_shape;
   return FR_OK;
 }

@@ -213,7 +213,7 @@ def test_full_sort_topk_sampled_path_every_append_shape(cuda, dtype, d, n_users,
     lib = native.lib()
     ref = None
     try:
-        for shape in range(6):
+        for shape in range(7):
             native.check(lib.fr_topk_options(shape), "fr_topk_options")
             s, i, _ = ops.full_sort_topk(Ud, Id, k, exclude=ex)
             s, i = s.cpu().numpy(), i.cpu().numpy()
