@@ -488,12 +488,6 @@ int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, const void* d_
                    const int64_t* d_test_ptr, const int32_t* d_test_col, int64_t test_base,
                    float* d_out_scores, int64_t* d_out_items, uint8_t* d_hits,
                    void* d_workspace, int64_t workspace_bytes, void* stream);
-/* A/B switch (host-side library state): the APPEND pass's kernel shape, (waves per workgroup, 32-item
- * blocks per staged tile, 32-user sets per wave) = 0: (8, 2, 1) default, 1: (8, 1, 2), 2: (8, 4, 1),
- * 3: (4, 2, 2), 4: (4, 4, 2), 5: (4, 2, 1), 6: (8, 2, 1) with the threshold epilogue software-pipelined
- * behind the next tile's MFMAs; -1 leaves it.  Results are identical; the workspace size
- * depends on it (query fr_topk_workspace after setting it). */
-int fr_topk_options(int append_shape);
 
 /* ------------------------------------------------------------------------------------------
  * Fused post-norm Transformer encoder layer, training forward + backward.

@@ -237,7 +237,6 @@ _SIGS = {
     "fr_encoder_grad_numel": (c_int64, []),
     "fr_encoder_profile": (c_int, [c_int, c_void_p]),
     "fr_encoder_options": (c_int, [c_int]),
-    "fr_topk_options": (c_int, [c_int]),
     "fr_encoder_dact_numel": (c_int64, [c_int64, c_int]),
     "fr_encoder_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_int, POINTER(c_void_p), POINTER(c_float),
                                POINTER(c_float), c_uint64, c_int] + [c_void_p] * 12),

@@ -147,16 +147,9 @@ struct ScoreArgs {
 
 enum { kList = 0, kAppend = 1 };
 
-// UW: user sets per wave (APPEND only): the wave holds UW x 32 users' B fragments and every A fragment
-// read from LDS feeds UW MFMAs, so a staged item tile (and its barrier) serves UW x 256 users.
-template <typename T, int D, int KC, int MODE, int NB, int UW = 1, int W = kWaves>
-__global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
+template <typename T, int D, int KC, int MODE, int NB>
+__global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   using C = Cfg<T, D, NB>;
-  static_assert(UW == 1 || (MODE == kAppend && C::BF), "several user sets per wave: the bf16 APPEND kernel");
-  static_assert(W == kWaves || MODE == kAppend, "the LIST kernel runs 8 waves");
-  constexpr int THR = W * 64;                              // threads per workgroup
-  constexpr int UPW = W * 32 * UW;                         // users per workgroup
-  constexpr int CH = (C::TILE * C::CPR + THR - 1) / THR;   // staged 16-B chunks per thread
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
 
   const int tid = threadIdx.x;
@@ -169,19 +162,11 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   const int b = blockIdx.x, xcd = b & 7, q8 = total >> 3, r8 = total & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int ut = wg % a.n_utiles, sp = wg / a.n_utiles;
-  if ((int64_t)ut * UPW >= n_users) return;  // whole workgroup idle (device-sized grids)
+  if ((int64_t)ut * kUsersPerWG >= n_users) return;  // whole workgroup idle (device-sized grids)
 
-  int64_t slot_u[UW], urow_u[UW];
-  bool uvalid_u[UW];
-#pragma unroll
-  for (int u = 0; u < UW; ++u) {
-    slot_u[u] = (int64_t)ut * UPW + (wave * UW + u) * 32 + r;
-    uvalid_u[u] = slot_u[u] < n_users;
-    urow_u[u] = uvalid_u[u] ? (a.urows ? (int64_t)a.urows[slot_u[u]] : slot_u[u]) : 0;
-  }
-  const int64_t slot = slot_u[0];
-  const bool uvalid = uvalid_u[0];
-  const int64_t urow = urow_u[0];
+  const int64_t slot = (int64_t)ut * kUsersPerWG + wave * 32 + r;
+  const bool uvalid = slot < n_users;
+  const int64_t urow = uvalid ? (a.urows ? (int64_t)a.urows[slot] : slot) : 0;
   const int64_t i_lo = (int64_t)sp * a.span;
   const int64_t i_hi = min(a.n_items, i_lo + a.span);
   const int n_tiles = (int)((i_hi - i_lo + C::TILE - 1) / C::TILE);
@@ -195,36 +180,23 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   // B operand: this lane's user, held for the whole kernel
   typedef typename std::conditional<C::BF, bf16x8, float4>::type BFrag;
   constexpr int NBF = C::BF ? C::KS : C::KS / 4;
-  BFrag bf[UW][NBF];
+  BFrag bf[NBF];
 #pragma unroll
-  for (int u = 0; u < UW; ++u)
-#pragma unroll
-    for (int s = 0; s < NBF; ++s) {
-      if constexpr (C::BF) {
-        bf[u][s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(a.Uq) + urow_u[u] * a.ldu +
-                                                    16 * s + 8 * h);
-      } else {
-        bf[u][s] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.Uq) + urow_u[u] * a.ldu +
-                                                   h * (D / 2) + 4 * s);
-      }
+  for (int s = 0; s < NBF; ++s) {
+    if constexpr (C::BF) {
+      bf[s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(a.Uq) + urow * a.ldu + 16 * s + 8 * h);
+    } else {
+      bf[s] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.Uq) + urow * a.ldu + h * (D / 2) + 4 * s);
     }
+  }
   // make the compiler itself retire these loads here (an asm that reads them), so its counted
   // waits inside the tile loop only ever cover the item-tile prefetch
 #pragma unroll
-  for (int u = 0; u < UW; ++u)
-#pragma unroll
-    for (int s = 0; s < NBF; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[u][s])));
-  // APPEND: each user set's threshold and this lane's region
-  float thr_u[UW];
-  int64_t region_u[UW];
-  int cnt_u[UW];
-#pragma unroll
-  for (int u = 0; u < UW; ++u) {
-    thr_u[u] = MODE == kAppend && uvalid_u[u] ? a.thr[slot_u[u]] : -INFINITY;
-    region_u[u] = (slot_u[u] * a.n_splits + sp) * 2 + h;
-    cnt_u[u] = 0;
-  }
-  const int64_t region = region_u[0];
+  for (int s = 0; s < NBF; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[s])));
+  // APPEND: this user's threshold and this lane's region
+  const float thr_u = MODE == kAppend && uvalid ? a.thr[slot] : -INFINITY;
+  const int64_t region = (slot * a.n_splits + sp) * 2 + h;
+  int cnt = 0;
 
   // the B-fragment / exclusion-row / threshold loads retire here, so the loop's counted waits
   // only ever cover the item-tile prefetch
@@ -241,12 +213,12 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   // item tiles: global -> registers (one tile ahead) -> LDS (double buffer, swizzled chunks).
   // APPEND keeps each staged chunk's row, LDS offset and global source (advanced one tile of rows
   // per step) in registers; the register-heavy LIST kernel recomputes them per tile.
-  constexpr int NSH = MODE == kAppend ? CH : 1;
+  constexpr int NSH = MODE == kAppend ? C::CH : 1;
   int srow[NSH], sdst[NSH];
   const char* ssrc[NSH];
 #pragma unroll
   for (int c = 0; c < NSH; ++c) {
-    const int x = tid + c * THR;
+    const int x = tid + c * kThreads;
     const int row = x / C::CPR, cc = x % C::CPR;
     srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;  // rows past the tile never load
     sdst[c] = (row * C::CPR + swz<T, D>(row, cc)) * 16;
@@ -254,13 +226,13 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   }
   const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
 #define FR_LOAD_TILE(T_)                                                                            \
-  _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                               \
+  _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
     if constexpr (MODE == kAppend) {                                                                \
       const int64_t item = i_lo + (int64_t)(T_) * C::TILE + srow[c];                                \
       stg[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)(T_) * tile_bytes)  \
                            : make_uint4(0, 0, 0, 0);                                                \
     } else {                                                                                        \
-      const int x = tid + c * THR;                                                             \
+      const int x = tid + c * kThreads;                                                             \
       stg[c] = make_uint4(0, 0, 0, 0);                                                              \
       if (x < C::TILE * C::CPR) {                                                                   \
         const int row = x / C::CPR, cc = x % C::CPR;                                                \
@@ -272,11 +244,11 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
     }                                                                                               \
   }
 #define FR_STORE_TILE(BUF_)                                                                         \
-  _Pragma("unroll") for (int c = 0; c < CH; ++c) {                                               \
+  _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
     if constexpr (MODE == kAppend) {                                                                \
       if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + sdst[c]) = stg[c]; \
     } else {                                                                                        \
-      const int x = tid + c * THR;                                                             \
+      const int x = tid + c * kThreads;                                                             \
       if (x < C::TILE * C::CPR) {                                                                   \
         const int row = x / C::CPR, cc = x % C::CPR;                                                \
         *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + (row * C::CPR + swz<T, D>(row, cc)) * 16) = stg[c]; \
@@ -292,7 +264,7 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   for (int s = 0; s < NAH; ++s) aoff[s] = a_off<T, D>(r, h, s);
 #define FR_AOFF(S_) (MODE == kAppend ? aoff[(MODE == kAppend) ? (S_) : 0] : a_off<T, D>(r, h, (S_)))
 
-  uint4 stg[CH];
+  uint4 stg[C::CH];
   if (n_tiles > 0) {
     FR_LOAD_TILE(0)
     FR_STORE_TILE(0)
@@ -300,16 +272,14 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
   __syncthreads();
   if (n_tiles > 1) { FR_LOAD_TILE(1) }
   for (int t = 0; t < n_tiles; ++t) {
-    // ---- scores of this tile on the matrix cores (NB independent 32-item blocks x UW user sets)
+    // ---- scores of this tile on the matrix cores (NB independent 32-item blocks)
     const char* abuf = smem + (t & 1) * C::STAGE;
-    f32x16 acc[NB][UW];
+    f32x16 acc[NB];
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
-      for (int u = 0; u < UW; ++u)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[bb][u][j] = 0.f;
-    if constexpr (C::BF && UW == 1) {
+      for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
+    if constexpr (C::BF) {
       // the tile's A fragments are read ahead of the MFMA chains that consume them in order
       bf16x8 af[NB][C::KS];
 #pragma unroll
@@ -321,7 +291,7 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
       for (int s = 0; s < C::KS; ++s)
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
-          acc[bb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[0][s], acc[bb][0], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[s], acc[bb], 0, 0, 0);
       // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight)
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
@@ -331,54 +301,31 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    } else if constexpr (C::BF) {
-      // several user sets: each A fragment feeds UW MFMAs; fragments read two k-steps ahead
-      bf16x8 af[3][NB];
-#pragma unroll
-      for (int s = 0; s < 2 && s < C::KS; ++s)
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb)
-          af[s][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + FR_AOFF(s));
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        if (s + 2 < C::KS) {
-#pragma unroll
-          for (int bb = 0; bb < NB; ++bb)
-            af[(s + 2) % 3][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + FR_AOFF(s + 2));
-        }
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-          for (int u = 0; u < UW; ++u)
-            acc[bb][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s % 3][bb], bf[u][s], acc[bb][u], 0, 0, 0);
-      }
     } else {
 #pragma unroll
       for (int sg = 0; sg < C::KS / 4; ++sg) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) {
           const float4 af = *reinterpret_cast<const float4*>(abuf + bb * 32 * C::RB + FR_AOFF(sg));
-          acc[bb][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, bf[0][sg].x, acc[bb][0], 0, 0, 0);
-          acc[bb][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, bf[0][sg].y, acc[bb][0], 0, 0, 0);
-          acc[bb][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, bf[0][sg].z, acc[bb][0], 0, 0, 0);
-          acc[bb][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[0][sg].w, acc[bb][0], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, bf[sg].x, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, bf[sg].y, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, bf[sg].z, acc[bb], 0, 0, 0);
+          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[sg].w, acc[bb], 0, 0, 0);
         }
       }
     }
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      // ---- this lane's 16 scores of block bb, user set u: user slot_u[u], items ib + (j&3) + 8(j>>2) + 4h
+    for (int bb = 0; bb < NB; ++bb) {
+      // ---- this lane's 16 scores of block bb: user `slot`, items ib + (j&3) + 8(j>>2) + 4h
       const int64_t ib = i_lo + (int64_t)t * C::TILE + bb * 32 + 4 * h;
       float wf;
       if constexpr (MODE == kList) {
         const uint32_t wsc = (uint32_t)(key[KC - 1] >> 32);
         wf = wsc < 0x00800000u ? -INFINITY : fr_unord(wsc);  // the list's worst score (empty: -inf)
       } else {
-        wf = thr_u[u];
+        wf = thr_u;
       }
-      const f32x16 av = acc[bb][u];
+      const f32x16 av = acc[bb];
       uint32_t mask = 0u;
 #pragma unroll
       for (int j = 0; j < 16; ++j) mask |= av[j] >= wf ? (1u << j) : 0u;
@@ -387,7 +334,7 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
         for (int j = 0; j < 16; ++j)
           if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
       }
-      if (!uvalid_u[u]) mask = 0u;
+      if (!uvalid) mask = 0u;
       // every lane handles its next candidate in the same pass
       while (__ballot(mask != 0u)) {
         const bool act = mask != 0u;
@@ -416,11 +363,11 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
           }
         } else {
           if (act) {
-            if (cnt_u[u] < a.cap) {
-              a.cs[region_u[u] * a.cap + cnt_u[u]] = sc;
-              a.ci[region_u[u] * a.cap + cnt_u[u]] = (int32_t)item;
+            if (cnt < a.cap) {
+              a.cs[region * a.cap + cnt] = sc;
+              a.ci[region * a.cap + cnt] = (int32_t)item;
             }
-            ++cnt_u[u];
+            ++cnt;
           }
         }
       }
@@ -434,12 +381,6 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
 #undef FR_STORE_TILE
 #undef FR_AOFF
 
-  if constexpr (MODE == kAppend) {
-#pragma unroll
-    for (int u = 0; u < UW; ++u)
-      if (uvalid_u[u]) a.cc[region_u[u]] = cnt_u[u];
-    return;
-  }
   if (!uvalid) return;
   if constexpr (MODE == kList) {
     // list (slot, split, half): k unsorted entries, decoded back to (score, item)
@@ -453,153 +394,9 @@ __global__ __launch_bounds__(W * 64) void topk_score_kernel(ScoreArgs a) {
         a.li[o + q] = empty ? INT32_MAX : (int32_t)(~(uint32_t)kk);
       }
     }
+  } else {
+    a.cc[region] = cnt;
   }
-}
-
-// APPEND pass, software-pipelined (bf16 tables): the threshold epilogue of tile t - 1 is issued
-// between the MFMAs of tile t, so its VALU work (compares, candidate extraction) fills the matrix
-// pipe's issue shadow instead of following it; the item tiles rotate through three LDS buffers (one
-// barrier per tile: a buffer is rewritten two tiles after its last read).  Same candidates, same
-// regions and counts as topk_score_kernel<.., kAppend, NB, 1, 8> (the merge sorts them).
-template <int D, int NB>
-__global__ __launch_bounds__(kThreads) void topk_append_pipe_kernel(ScoreArgs a) {
-  using T = uint16_t;
-  using C = Cfg<T, D, NB>;
-  constexpr int NBUF = 3;
-  constexpr int CH = (C::TILE * C::CPR + kThreads - 1) / kThreads;
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * C::STAGE];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int64_t n_users = a.d_nu ? (int64_t)*a.d_nu : a.n_users;
-  const int total = a.n_utiles * a.n_splits;
-  const int b = blockIdx.x, xcd = b & 7, q8 = total >> 3, r8 = total & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int ut = wg % a.n_utiles, sp = wg / a.n_utiles;
-  if ((int64_t)ut * kUsersPerWG >= n_users) return;
-  const int64_t slot = (int64_t)ut * kUsersPerWG + wave * 32 + r;
-  const bool uvalid = slot < n_users;
-  const int64_t urow = uvalid ? (a.urows ? (int64_t)a.urows[slot] : slot) : 0;
-  const int64_t i_lo = (int64_t)sp * a.span;
-  const int64_t i_hi = min(a.n_items, i_lo + a.span);
-  const int n_tiles = (int)((i_hi - i_lo + C::TILE - 1) / C::TILE);
-  const T* __restrict__ It = reinterpret_cast<const T*>(a.It);
-  const int64_t ldi = a.ldi;
-  bf16x8 bf[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s)
-    bf[s] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(a.Uq) + urow * a.ldu + 16 * s + 8 * h);
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[s])));
-  const float thr = uvalid ? a.thr[slot] : INFINITY;
-  const int64_t region = (slot * a.n_splits + sp) * 2 + h;
-  int cnt = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  int srow[CH], sdst[CH];
-  const char* ssrc[CH];
-#pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int x = tid + c * kThreads;
-    const int row = x / C::CPR, cc = x % C::CPR;
-    srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;
-    sdst[c] = (row * C::CPR + swz<T, D>(row, cc)) * 16;
-    ssrc[c] = reinterpret_cast<const char*>(It) + ((i_lo + row) * ldi) * (int64_t)sizeof(T) + cc * 16;
-  }
-  const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
-  uint4 stg[CH];
-  auto load_tile = [&](int tt) {
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int64_t item = i_lo + (int64_t)tt * C::TILE + srow[c];
-      stg[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)tt * tile_bytes) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-      if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + buf * C::STAGE + sdst[c]) = stg[c];
-  };
-  int aoff[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) aoff[s] = a_off<T, D>(r, h, s);
-
-  // candidates of one 32-item block: this lane's 16 scores (items ib + (j & 3) + 8 (j >> 2)) >= thr
-  auto epilogue = [&](const f32x16& av, int64_t ib) {
-    uint32_t mask = 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) mask |= av[j] >= thr ? (1u << j) : 0u;
-    if (ib + 28 >= i_hi) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
-    }
-    if (!uvalid) mask = 0u;
-    while (__ballot(mask != 0u)) {
-      const bool act = mask != 0u;
-      const int j = act ? __builtin_ctz(mask) : 0;
-      mask &= mask - 1u;
-      const float v0 = (j & 1) ? av[1] : av[0], v1 = (j & 1) ? av[3] : av[2];
-      const float v2 = (j & 1) ? av[5] : av[4], v3 = (j & 1) ? av[7] : av[6];
-      const float v4 = (j & 1) ? av[9] : av[8], v5 = (j & 1) ? av[11] : av[10];
-      const float v6 = (j & 1) ? av[13] : av[12], v7 = (j & 1) ? av[15] : av[14];
-      const float w0 = (j & 2) ? v1 : v0, w1 = (j & 2) ? v3 : v2, w2 = (j & 2) ? v5 : v4, w3 = (j & 2) ? v7 : v6;
-      const float x0 = (j & 4) ? w1 : w0, x1 = (j & 4) ? w3 : w2;
-      const float sc = (j & 8) ? x1 : x0;
-      if (act) {
-        if (cnt < a.cap) {
-          a.cs[region * a.cap + cnt] = sc;
-          a.ci[region * a.cap + cnt] = (int32_t)((ib + (j & 3) + 8 * (j >> 2)) * a.item_mul);
-        }
-        ++cnt;
-      }
-    }
-  };
-
-  // prologue: tiles 0 and 1 staged, tile 2 in registers
-  if (n_tiles > 0) { load_tile(0); store_tile(0); }
-  if (n_tiles > 1) { load_tile(1); store_tile(1); }
-  __syncthreads();
-  if (n_tiles > 2) load_tile(2);
-  f32x16 prev[NB];
-  for (int t = 0; t <= n_tiles; ++t) {
-    f32x16 acc[NB];
-    if (t < n_tiles) {
-      const char* abuf = smem + (t % NBUF) * C::STAGE;
-#pragma unroll
-      for (int bb = 0; bb < NB; ++bb)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
-      bf16x8 af[2][NB];
-#pragma unroll
-      for (int bb = 0; bb < NB; ++bb) af[0][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + aoff[0]);
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        if (s + 1 < C::KS) {
-#pragma unroll
-          for (int bb = 0; bb < NB; ++bb)
-            af[(s + 1) & 1][bb] = *reinterpret_cast<const bf16x8*>(abuf + bb * 32 * C::RB + aoff[s + 1]);
-        }
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb)
-          acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][bb], bf[s], acc[bb], 0, 0, 0);
-      }
-    }
-    // the previous tile's candidates, issued behind this tile's MFMAs
-    if (t > 0) {
-#pragma unroll
-      for (int bb = 0; bb < NB; ++bb) epilogue(prev[bb], i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h);
-    }
-    if (t < n_tiles) {
-#pragma unroll
-      for (int bb = 0; bb < NB; ++bb) prev[bb] = acc[bb];
-    }
-    // tile t + 2 into the buffer tile t - 1 used (every wave passed the last barrier after reading it)
-    if (t + 2 < n_tiles) store_tile((t + 2) % NBUF);
-    __syncthreads();
-    if (t + 3 < n_tiles) load_tile(t + 3);
-  }
-  if (uvalid) a.cc[region] = cnt;
 }
 
 struct MergeArgs {
@@ -706,44 +503,16 @@ __global__ void topk_zero_kernel(int32_t* p) {
   if (threadIdx.x == 0) p[0] = 0;
 }
 
-// APPEND kernel shape (A/B: fr_topk_options): (waves per workgroup, 32-item blocks per staged tile,
-// 32-user sets per wave).  Several user sets apply to bf16 tables (fp32 tables take shape 0).
-int g_append_shape = 0;
-constexpr int kShapes = 7;  // 6: (8, 2, 1) software-pipelined (topk_append_pipe_kernel)
-constexpr int kAppendW[kShapes] = {8, 8, 8, 4, 4, 4, 8};
-constexpr int kAppendNB[kShapes] = {2, 1, 4, 2, 4, 2, 2};
-constexpr int kAppendUW[kShapes] = {1, 2, 1, 2, 2, 1, 1};
-
-int append_users_per_wg(int shape) { return kAppendW[shape] * 32 * kAppendUW[shape]; }
-
 template <typename T, int D, int MODE>
 hipError_t launch_score_t(const ScoreArgs& a, hipStream_t s) {
   void (*kern)(ScoreArgs);
-  int users_per_wg = kUsersPerWG, threads = kThreads;
   if constexpr (MODE == kAppend) {
-    const int shape = sizeof(T) == 2 ? g_append_shape : 0;
-    if constexpr (sizeof(T) == 2) {
-      switch (shape) {
-        case 1: kern = topk_score_kernel<T, D, 1, kAppend, 1, 2, 8>; break;
-        case 2: kern = topk_score_kernel<T, D, 1, kAppend, 4, 1, 8>; break;
-        case 3: kern = topk_score_kernel<T, D, 1, kAppend, 2, 2, 4>; break;
-        case 4: kern = topk_score_kernel<T, D, 1, kAppend, 4, 2, 4>; break;
-        case 5: kern = topk_score_kernel<T, D, 1, kAppend, 2, 1, 4>; break;
-        case 6: kern = topk_append_pipe_kernel<D, 2>; break;
-        default: kern = topk_score_kernel<T, D, 1, kAppend, 2, 1, 8>; break;
-      }
-    } else {
-      kern = topk_score_kernel<T, D, 1, kAppend, 2, 1, 8>;
-    }
-    users_per_wg = append_users_per_wg(shape);
-    threads = kAppendW[shape] * 64;
+    kern = topk_score_kernel<T, D, 1, kAppend, 2>;
   } else {
     kern = a.k <= 10 ? topk_score_kernel<T, D, 10, kList, 1>
                      : (a.k <= 20 ? topk_score_kernel<T, D, 20, kList, 1> : topk_score_kernel<T, D, 32, kList, 1>);
   }
-  ScoreArgs b = a;
-  b.n_utiles = (int)fr::ceil_div(a.n_users, users_per_wg);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(b.n_utiles * b.n_splits)), dim3(threads), 0, s, b);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(a.n_utiles * a.n_splits)), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -758,8 +527,8 @@ hipError_t launch_score(int dtype, int d, const ScoreArgs& a, hipStream_t s) {
   return launch_score_t<float, 64, MODE>(a, s);
 }
 
-void split_plan(int64_t n_users, int64_t n_items, int* n_splits, int64_t* span, int users_per_wg = kUsersPerWG) {
-  const int64_t n_utiles = fr::ceil_div(n_users, users_per_wg);
+void split_plan(int64_t n_users, int64_t n_items, int* n_splits, int64_t* span) {
+  const int64_t n_utiles = fr::ceil_div(n_users, kUsersPerWG);
   int64_t ns = std::max<int64_t>(1, fr::ceil_div(2 * fr::kNumCU, n_utiles));
   ns = std::min<int64_t>(ns, 64);
   ns = std::min<int64_t>(ns, std::max<int64_t>(1, n_items / (8 * kTile)));  // >= 8 blocks per split
@@ -782,9 +551,7 @@ struct Plan {
 Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   Plan p{};
   p.sampled = n_items >= kSampledMinItems;
-  // the APPEND pass's splits (its workgroups hold kUsersPerWG x user sets); the exact LIST passes run on
-  // the same splits
-  split_plan(n_users, n_items, &p.ns2, &p.span2, p.sampled ? append_users_per_wg(g_append_shape) : kUsersPerWG);
+  split_plan(n_users, n_items, &p.ns2, &p.span2);
   auto take = [&](int64_t bytes) { const int64_t o = p.total; p.total += fr::align_up(bytes, 256); return o; };
   if (!p.sampled) {
     p.off_l1 = take(n_users * p.ns2 * 2 * (int64_t)k * 8);
@@ -902,13 +669,5 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   // 4. exact LIST pass + merge for the flagged users (grid sized for all; exits when none)
   e = list_pass(d_I, ldi, n_items, 1, p.ns2, p.span2, ws + p.off_l2, flag_list, flag_cnt, nullptr);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
-  return FR_OK;
-}
-
-// A/B switch (host-side library state): the APPEND kernel's shape (see g_append_shape); -1 leaves it.
-// The workspace size depends on it: query fr_topk_workspace after setting it.
-extern "C" int fr_topk_options(int append_shape) {
-  FR_REQUIRE(append_shape >= -1 && append_shape < kShapes, "append_shape must be in [-1, 6]");
-  if (append_shape >= 0) g_append_shape = append_shape;
   return FR_OK;
 }

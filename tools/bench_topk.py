@@ -18,11 +18,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--only", default=None, help="k,mask (e.g. 20,0) to run one variant")
-    ap.add_argument("--shape", type=int, default=-1, help="fr_topk_options APPEND shape (-1: library default)")
     args = ap.parse_args()
     import torch
-    from FoodRec.engine import native, ops
-    native.check(native.lib().fr_topk_options(args.shape), "fr_topk_options")
+    from FoodRec.engine import ops
     dev = torch.device("cuda:0")
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     g = torch.Generator(device=dev).manual_seed(0)
