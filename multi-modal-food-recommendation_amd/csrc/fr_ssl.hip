@@ -1086,6 +1086,61 @@ __global__ __launch_bounds__(256) void nce_lse_mfma_kernel(int64_t b, float inv_
   }
 }
 
+// Round 5 form of the InfoNCE log-sum-exp: the logits transposed per 16 x 16 sub-block (as
+// nce_bwd_mfma2_kernel), S^T = Hn_j Hn_b^T, so each lane owns ONE b row (its B fragments in registers
+// for the whole kernel: half the LDS reads of nce_lse_mfma_kernel) and keeps one online (max, sum)
+// over the j values it holds; the 4 lane groups of a row are merged at the end in a fixed order.
+template <int D>
+__global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
+  constexpr int LD = D + 4;
+  __shared__ __attribute__((aligned(16))) float Bt[T * LD];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  const int64_t gi = (int64_t)it * T + 16 * w + i;
+  const bool ivalid = gi < m;
+  float4 bfr[D / 16];
+  {
+    const float* row = ivalid ? nce_row(ws, pt, p, b, D, gi) : nullptr;
+#pragma unroll
+    for (int kc = 0; kc < D / 16; ++kc)
+      bfr[kc] = ivalid ? *reinterpret_cast<const float4*>(row + 16 * kc + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float mx = -INFINITY, sm = 0.f;
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    nce_tile_r(ws, pt, p, b, D, jt * T, Bt);
+    __syncthreads();
+#pragma unroll
+    for (int jc = 0; jc < T / 16; ++jc) {
+      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < D / 16; ++kc) {
+        const float4 a = *reinterpret_cast<const float4*>(Bt + (16 * jc + i) * LD + 16 * kc + 4 * h);
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) g = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t gj = jt * T + 16 * jc + 4 * h + q;
+        if (gj >= m || gi == gj) continue;
+        const float l = g[q] * inv_tau;
+        if (l > mx) { sm = sm * __expf(mx - l) + 1.f; mx = l; }
+        else sm += __expf(l - mx);
+      }
+    }
+  }
+  // merge the 4 lane groups of the row (lanes i, i + 16, i + 32, i + 48): distance 16, then 32
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    const float Mo = __shfl_xor(mx, o, 64), So = __shfl_xor(sm, o, 64);
+    const float Mn = fmaxf(mx, Mo);
+    sm = (sm == 0.f ? 0.f : sm * __expf(mx - Mn)) + (So == 0.f ? 0.f : So * __expf(Mo - Mn));
+    mx = Mn;
+  }
+  if (h == 0 && ivalid) ws.part[((int64_t)p * NCE_JS + js) * m + gi] = make_float2(mx, sm);
+}
+
 // MFMA form of nce_bwd_tiles_kernel: the logits tile and W = dl + dl^T on the matrix cores / VALU,
 // W staged in LDS, then sum_j W_ij Hn_j on the matrix cores into per-lane accumulators
 template <int D>
@@ -1148,6 +1203,100 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma_kernel(int64_t b, float inv_
   }
 }
 
+// Round 5 form of the InfoNCE backward: the logits are computed TRANSPOSED per 16 x 16 sub-block,
+// S^T = Hn_j Hn_b^T (lane (i, h) holds S[j = 16 jc + 4h + q][b = 16 w + i]), and because W is symmetric
+// those registers ARE the A operand of dHn_b = sum_j W_bj Hn_j (the k order of the 16-wide j chunk
+// permuted so that lane group h feeds k = 4h + q to MFMA q).  No W staging in LDS, one barrier per
+// column tile; the b-side rows' B fragments of the logits stay in registers for the whole kernel and
+// the j tile is staged twice (row-major for the logits, transposed for the product: one ds_read_b128
+// per B fragment).  Same partial layout as nce_bwd_mfma_kernel.
+template <int D>
+__global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
+  constexpr int LD = D + 4, LDT = T + 4;
+  __shared__ __attribute__((aligned(16))) float Bt[T * LD];    // j rows, row-major (logits' A operand)
+  __shared__ __attribute__((aligned(16))) float BtT[D * LDT];  // the same tile transposed (product's B operand)
+  __shared__ float lse_j[T];
+  const int64_t m = 2 * b, nt = (m + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
+  const float* lse = ws.lse + (int64_t)p * m;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  const int64_t gi = (int64_t)it * T + 16 * w + i;  // this lane's b row (the product's A row)
+  const bool ivalid = gi < m;
+  const float lse_i = ivalid ? lse[gi] : 0.f;
+  const int64_t part_i = ivalid ? nce_partner(gi, b) : -1;
+  // B operand of the logits: row gi of Hn, k-permuted float4 chunks
+  float4 bfr[D / 16];
+  {
+    const float* row = ivalid ? nce_row(ws, pt, p, b, D, gi) : nullptr;
+#pragma unroll
+    for (int kc = 0; kc < D / 16; ++kc)
+      bfr[kc] = ivalid ? *reinterpret_cast<const float4*>(row + 16 * kc + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  f32x4 acc[D / 16];
+#pragma unroll
+  for (int c = 0; c < D / 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t jt = js; jt < nt; jt += gridDim.y) {
+    __syncthreads();
+    {  // stage the j tile both ways, and its rows' lse
+      const int d4 = D / 4;
+      for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
+        const int r = idx / d4, k4 = idx - r * d4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (jt * T + r < m) v = reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4];
+        *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = v;
+        BtT[(4 * k4 + 0) * LDT + r] = v.x;
+        BtT[(4 * k4 + 1) * LDT + r] = v.y;
+        BtT[(4 * k4 + 2) * LDT + r] = v.z;
+        BtT[(4 * k4 + 3) * LDT + r] = v.w;
+      }
+      if (threadIdx.x < T) {
+        const int64_t gj = jt * T + threadIdx.x;
+        lse_j[threadIdx.x] = gj < m ? lse[gj] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jc = 0; jc < T / 16; ++jc) {
+      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < D / 16; ++kc) {
+        const float4 a = *reinterpret_cast<const float4*>(Bt + (16 * jc + i) * LD + 16 * kc + 4 * h);
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) g = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g);
+      }
+      float wv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int jl = 16 * jc + 4 * h + q;
+        const int64_t gj = jt * T + jl;
+        float x = 0.f;
+        if (ivalid && gj < m && gi != gj) {
+          const float l = g[q] * inv_tau;
+          const float pij = __expf(l - lse_i) - (gj == part_i ? 1.f : 0.f);
+          const float pji = __expf(l - lse_j[jl]) - (gi == nce_partner(gj, b) ? 1.f : 0.f);
+          x = pij + pji;
+        }
+        wv[q] = x;
+      }
+#pragma unroll
+      for (int c = 0; c < D / 16; ++c) {
+        const float4 bx = *reinterpret_cast<const float4*>(BtT + (16 * c + i) * LDT + 16 * jc + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[c] = mfma4(wv[q], comp4(bx, q), acc[c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t go = (int64_t)it * T + 16 * w + 4 * h + q;
+    if (go < m) {
+      float* P = ws.P + (((int64_t)p * NCE_JS + js) * m + go) * D;
+#pragma unroll
+      for (int c = 0; c < D / 16; ++c) P[16 * c + i] = acc[c][q];
+    }
+  }
+}
+
 // dview_v[r] = normalize_backward(gh) with gh = scale * (sum over the pairs holding view v, at the
 // row's position in that pair, of the split partials); written (views that no pair holds: zeros)
 __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, int64_t b, int d, float inv_tau,
@@ -1174,13 +1323,21 @@ __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, 
       }
       return q * scale;
     };
+    // this lane's columns k = lane, lane + 64 (d <= 128): the split partials are read once
+    float gk[2];
     float dot = 0.f;
-    for (int k = lane; k < d; k += 64) dot = fmaf(gsum(k), hn[k], dot);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = lane + 64 * t;
+      gk[t] = k < d ? gsum(k) : 0.f;
+      if (k < d) dot = fmaf(gk[t], hn[k], dot);
+    }
     dot = group_sum<64>(dot);
-    for (int k = lane; k < d; k += 64) {
-      const float gh = gsum(k);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = lane + 64 * t;
       // d/dx [x / max(|x|, eps)]
-      dX[r * d + k] = nr > 1e-12f ? (gh - hn[k] * dot) / nr : gh / 1e-12f;
+      if (k < d) dX[r * d + k] = nr > 1e-12f ? (gk[t] - hn[k] * dot) / nr : gk[t] / 1e-12f;
     }
   }
 }
@@ -1190,7 +1347,7 @@ __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, 
 // ------------------------------------------------------------------------------------------ ABI
 extern "C" int fr_ssl_kernels(int mfma) {
   const int prev = g_ssl_mfma;
-  if (mfma >= 0) g_ssl_mfma = mfma ? 1 : 0;
+  if (mfma >= 0) g_ssl_mfma = mfma > 2 ? 1 : mfma;
   return prev;
 }
 
@@ -1346,6 +1503,12 @@ extern "C" int64_t fr_infonce_multi_workspace(int n_views, int64_t b, int d, int
   return nce_ws_bytes(n_views, b, d, n_pairs);
 }
 
+// the log-sum-exp kernel of the MFMA forms: 1 = the round-5 transposed form, 2 = the round-4 one (A/B)
+template <int D>
+static auto lse_kern() -> void (*)(int64_t, float, PairTab, NceWS) {
+  return g_ssl_mfma == 2 ? nce_lse_mfma_kernel<D> : nce_lse_mfma2_kernel<D>;
+}
+
 static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs, int n_pairs,
                         float tau, float weight, float* d_out, float* d_out_pairs, void* d_workspace,
                         int64_t workspace_bytes, void* stream) {
@@ -1370,10 +1533,10 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
   const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
   if (g_ssl_mfma) {
     switch (d) {
-      case 16: hipLaunchKernelGGL(nce_lse_mfma_kernel<16>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      case 32: hipLaunchKernelGGL(nce_lse_mfma_kernel<32>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      case 64: hipLaunchKernelGGL(nce_lse_mfma_kernel<64>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      default: hipLaunchKernelGGL(nce_lse_mfma_kernel<128>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 16: hipLaunchKernelGGL(lse_kern<16>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 32: hipLaunchKernelGGL(lse_kern<32>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 64: hipLaunchKernelGGL(lse_kern<64>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      default: hipLaunchKernelGGL(lse_kern<128>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
     }
   } else {
     hipLaunchKernelGGL(nce_lse_tiles_kernel, grid, dim3(256), lds, s, b, d, inv_tau, pt, w);
@@ -1424,12 +1587,19 @@ extern "C" int fr_infonce_multi_bwd(const float* const* d_views, int n_views, in
   const int js = (int)std::min<int64_t>(NCE_JS, nt);
   const size_t lds = (size_t)(2 * d * PADT + T * (d + 4) + T * 65) * 4;
   const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
-  if (g_ssl_mfma) {
+  if (g_ssl_mfma == 2) {  // the round-4 MFMA backward (W staged in LDS), for A/B
     switch (d) {
       case 16: hipLaunchKernelGGL(nce_bwd_mfma_kernel<16>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
       case 32: hipLaunchKernelGGL(nce_bwd_mfma_kernel<32>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
       case 64: hipLaunchKernelGGL(nce_bwd_mfma_kernel<64>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
       default: hipLaunchKernelGGL(nce_bwd_mfma_kernel<128>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+    }
+  } else if (g_ssl_mfma) {
+    switch (d) {
+      case 16: hipLaunchKernelGGL(nce_bwd_mfma2_kernel<16>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 32: hipLaunchKernelGGL(nce_bwd_mfma2_kernel<32>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 64: hipLaunchKernelGGL(nce_bwd_mfma2_kernel<64>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      default: hipLaunchKernelGGL(nce_bwd_mfma2_kernel<128>, grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
     }
   } else switch (d) {
     case 16: hipLaunchKernelGGL(nce_bwd_tiles_kernel<4>, grid, dim3(256), lds, s, b, inv_tau, pt, w); break;

@@ -11,6 +11,9 @@ import torch  # noqa: E402
 from FoodRec.engine import ops  # noqa: E402
 from FoodRec.models.clussl import _DCOR_PAIRS  # noqa: E402
 
+if len(sys.argv) > 1:  # fr_ssl_kernels mode (1 MFMA default, 2 MFMA with the round-4 InfoNCE backward, 0 VALU)
+    from FoodRec.engine import native  # noqa: E402
+    native.lib().fr_ssl_kernels(int(sys.argv[1]))
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 views = [torch.randn(1024, 64, device=dev, requires_grad=True) for _ in range(3)]
