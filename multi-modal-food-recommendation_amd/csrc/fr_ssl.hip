@@ -1106,6 +1106,11 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
     for (int kc = 0; kc < D / 16; ++kc)
       bfr[kc] = ivalid ? *reinterpret_cast<const float4*>(row + 16 * kc + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // base-2 online log-sum-exp, four logits at a time (no divergent rescale branch):
+  // M' = max(M, max_q l2_q), S = S 2^(M - M') + sum_q 2^(l2_q - M')
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float s2 = inv_tau * kLog2e;
+  const int mi = (int)m, gi32 = (int)gi;
   float mx = -INFINITY, sm = 0.f;
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
@@ -1120,13 +1125,19 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm) g = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g);
       }
+      float l2[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t gj = jt * T + 16 * jc + 4 * h + q;
-        if (gj >= m || gi == gj) continue;
-        const float l = g[q] * inv_tau;
-        if (l > mx) { sm = sm * __expf(mx - l) + 1.f; mx = l; }
-        else sm += __expf(l - mx);
+        const int gj = (int)jt * T + 16 * jc + 4 * h + q;
+        l2[q] = (gj < mi && gj != gi32) ? g[q] * s2 : -INFINITY;
+      }
+      const float mn = fmaxf(mx, fmaxf(fmaxf(l2[0], l2[1]), fmaxf(l2[2], l2[3])));
+      if (mn != -INFINITY) {  // (lane-uniform only by accident: a select, not a branch, in practice)
+        float add = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) add += __builtin_amdgcn_exp2f(l2[q] - mn);
+        sm = (sm == 0.f ? 0.f : sm * __builtin_amdgcn_exp2f(mx - mn)) + add;
+        mx = mn;
       }
     }
   }
@@ -1135,10 +1146,11 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
   for (int o = 16; o < 64; o <<= 1) {
     const float Mo = __shfl_xor(mx, o, 64), So = __shfl_xor(sm, o, 64);
     const float Mn = fmaxf(mx, Mo);
-    sm = (sm == 0.f ? 0.f : sm * __expf(mx - Mn)) + (So == 0.f ? 0.f : So * __expf(Mo - Mn));
+    sm = (sm == 0.f ? 0.f : sm * __builtin_amdgcn_exp2f(mx - Mn)) + (So == 0.f ? 0.f : So * __builtin_amdgcn_exp2f(Mo - Mn));
     mx = Mn;
   }
-  if (h == 0 && ivalid) ws.part[((int64_t)p * NCE_JS + js) * m + gi] = make_float2(mx, sm);
+  // (max, sum) in natural-log units for nce_finalize_kernel: M = M2 ln 2, S unchanged
+  if (h == 0 && ivalid) ws.part[((int64_t)p * NCE_JS + js) * m + gi] = make_float2(mx * 0.69314718055994531f, sm);
 }
 
 // MFMA form of nce_bwd_tiles_kernel: the logits tile and W = dl + dl^T on the matrix cores / VALU,
@@ -1220,10 +1232,16 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
   const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
   const float* lse = ws.lse + (int64_t)p * m;
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
-  const int64_t gi = (int64_t)it * T + 16 * w + i;  // this lane's b row (the product's A row)
-  const bool ivalid = gi < m;
-  const float lse_i = ivalid ? lse[gi] : 0.f;
-  const int64_t part_i = ivalid ? nce_partner(gi, b) : -1;
+  // 32-bit row indices (m < 2^31, checked by the caller); base-2 logits: exp(l - lse) = exp2(l2 - lse2)
+  // with l2 = l log2(e).  The partner relation is an involution, so [i == partner(j)] = [j == partner(i)]:
+  // W_ij = exp(l - lse_i) + exp(l - lse_j) - 2 [j == partner(i)]
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float s2 = inv_tau * kLog2e;
+  const int mi = (int)m;
+  const int gi = it * T + 16 * w + i;  // this lane's b row (the product's A row)
+  const bool ivalid = gi < mi;
+  const float lse2_i = ivalid ? lse[gi] * kLog2e : 0.f;
+  const int part_i = ivalid ? (int)nce_partner(gi, b) : -1;
   // B operand of the logits: row gi of Hn, k-permuted float4 chunks
   float4 bfr[D / 16];
   {
@@ -1251,10 +1269,11 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
       }
       if (threadIdx.x < T) {
         const int64_t gj = jt * T + threadIdx.x;
-        lse_j[threadIdx.x] = gj < m ? lse[gj] : 0.f;
+        lse_j[threadIdx.x] = gj < m ? lse[gj] * kLog2e : 0.f;
       }
     }
     __syncthreads();
+    const int j0 = (int)jt * T;
 #pragma unroll
     for (int jc = 0; jc < T / 16; ++jc) {
       f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1268,15 +1287,11 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int jl = 16 * jc + 4 * h + q;
-        const int64_t gj = jt * T + jl;
-        float x = 0.f;
-        if (ivalid && gj < m && gi != gj) {
-          const float l = g[q] * inv_tau;
-          const float pij = __expf(l - lse_i) - (gj == part_i ? 1.f : 0.f);
-          const float pji = __expf(l - lse_j[jl]) - (gi == nce_partner(gj, b) ? 1.f : 0.f);
-          x = pij + pji;
-        }
-        wv[q] = x;
+        const int gj = j0 + jl;
+        const float l2 = g[q] * s2;
+        const float e = (__builtin_amdgcn_exp2f(l2 - lse2_i) + __builtin_amdgcn_exp2f(l2 - lse_j[jl])) -
+                        (gj == part_i ? 2.f : 0.f);
+        wv[q] = (ivalid && gj < mi && gi != gj) ? e : 0.f;
       }
 #pragma unroll
       for (int c = 0; c < D / 16; ++c) {
