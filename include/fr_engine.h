@@ -456,6 +456,13 @@ int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp
                            const int64_t* const* d_steps, const int64_t* rows, const int32_t* row_dims,
                            int32_t* const* d_last, const float* const* d_hist, int32_t n_slices, int32_t hist_cap,
                            double beta1, double beta2, double eps, double weight_decay, void* stream);
+/* the same slice in n_parts launches: part p replays the p-th of n_parts even row ranges of the step's
+ * slice (a step issues every part, at points of its choosing, before the optimiser's lazy kernels) */
+int fr_adam_catch_up_slice_part(int n_tables, float* const* params, float* const* exp_avg,
+                                float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
+                                const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
+                                int32_t n_slices, int32_t part, int32_t n_parts, int32_t hist_cap, double beta1,
+                                double beta2, double eps, double weight_decay, void* stream);
 
 /* Mixed-precision Adam for one bf16 parameter (torch.optim.Adam.step, common/trainer.py:224):
  * the update runs on the fp32 master copy with fp32 exp_avg / exp_avg_sq (same element order as

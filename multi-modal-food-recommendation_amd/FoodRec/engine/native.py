@@ -211,6 +211,10 @@ _SIGS = {
                                        POINTER(c_void_p), POINTER(c_int64), POINTER(c_int32), POINTER(c_void_p),
                                        POINTER(c_void_p), c_int32, c_int32, c_double, c_double, c_double, c_double,
                                        c_void_p]),
+    "fr_adam_catch_up_slice_part": (c_int, [c_int, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                                            POINTER(c_void_p), POINTER(c_int64), POINTER(c_int32), POINTER(c_void_p),
+                                            POINTER(c_void_p), c_int32, c_int32, c_int32, c_int32, c_double,
+                                            c_double, c_double, c_double, c_void_p]),
     "fr_modal_fusion_partials": (c_int64, [c_int64]),
     "fr_modal_fusion_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
                                     POINTER(c_void_p), c_float, c_void_p, c_void_p, c_void_p]),

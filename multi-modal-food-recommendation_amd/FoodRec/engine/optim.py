@@ -41,6 +41,11 @@ def adam_rows_bytes(numel: int, rows: int, compact: int) -> int:
 ROWS_SIDE_STREAM = os.environ.get("FR_ROWS_SIDE_STREAM", "1") != "0"
 
 
+# FR_SLICE_PARTS: the per-step background slice in this many launches -- the first beside the step's
+# start (as with 1), the others where the model calls RowGrads.background_rest
+SLICE_PARTS = max(1, int(os.environ.get("FR_SLICE_PARTS", "1")))
+
+
 class RowGrads:
     """Pending row gradients of row-gathered tables: ``stash`` is called from the backward of
     ``ops.embedding(..., exchange=self)``; several stashes of one table before a step (repeated
@@ -54,6 +59,7 @@ class RowGrads:
         self.catch_up = None  # set by a FusedAdam with lazy_rows
         self.catch_up_slice = None  # set by a FusedAdam with lazy_rows and lazy_slices > 0
         self._bg_join = None  # joins the background slice replay into the main stream
+        self._bg_rest = None  # issues the slice's remaining parts (background_rest)
         # (weight, ids) pairs caught up by prefetch_rows this step.  The ids tensors are held here, so
         # their memory cannot be handed to another tensor by the caching allocator before clear():
         # a (weight, pointer, numel) match below therefore names the same ids
@@ -123,14 +129,32 @@ class RowGrads:
             if self.catch_up_slice is not None and self._bg_join is None:
                 # then one row slice of the lazily updated tables replays its backlog behind the
                 # catch-up (the batch's rows are current by then and skip), overlapping the rest of
-                # the step; joined before the optimiser touches any lazy state (join_background)
-                self.catch_up_slice([w for w, _ in pairs])
+                # the step; joined before the optimiser touches any lazy state (join_background).
+                # With SLICE_PARTS > 1 only its first part here; background_rest issues the others
+                ws = [w for w, _ in pairs]
+                self.catch_up_slice(ws, 0, SLICE_PARTS)
                 self._bg_join = lambda: main.wait_stream(side)
+                if SLICE_PARTS > 1:
+                    def rest(ws=ws, side=side, main=main):
+                        side.wait_stream(main)
+                        with torch.cuda.stream(side):
+                            for part in range(1, SLICE_PARTS):
+                                self.catch_up_slice(ws, part, SLICE_PARTS)
+                    self._bg_rest = rest
         return lambda stream=None: (stream if stream is not None else main).wait_event(caught)
+
+    def background_rest(self):
+        """Issue the background slice's remaining parts behind everything the current stream has
+        issued so far (a model calls this where the step leaves the chip idle enough: HealthRec after
+        its encoder forward); join_background issues them if nobody did."""
+        if self._bg_rest is not None:
+            r, self._bg_rest = self._bg_rest, None
+            r()
 
     def join_background(self):
         """Make the current stream wait for the background slice replay (before any optimiser
         kernel reads or advances the lazy step counters / history)."""
+        self.background_rest()
         if self._bg_join is not None:
             j, self._bg_join = self._bg_join, None
             j()
@@ -215,10 +239,11 @@ class FusedAdam(torch.optim.Optimizer):
                 "fr_adam_catch_up_rows_multi")
 
     @torch.no_grad()
-    def catch_up_slice(self, ps):
-        """One background slice (fr_adam_catch_up_slice): rows [R s / K, R (s + 1) / K) of the lazily
-        updated tables ``ps``, s = device step counter mod K = ``lazy_slices``, replay their backlog
-        through the current step.  Tables without lazy state are skipped."""
+    def catch_up_slice(self, ps, part=0, n_parts=1):
+        """One background slice (fr_adam_catch_up_slice_part): rows [R s / K, R (s + 1) / K) of the
+        lazily updated tables ``ps``, s = device step counter mod K = ``lazy_slices``, replay their
+        backlog through the current step (``part`` of ``n_parts`` even row ranges of it).  Tables
+        without lazy state are skipped."""
         ps = [p for p in ps if "lazy_last" in self.state.get(p, {})]
         groups = {id(p): g for g in self.param_groups for p in g["params"]}
         by_group = {}
@@ -231,15 +256,15 @@ class FusedAdam(torch.optim.Optimizer):
                 n = len(chunk)
                 st = [self.state[p] for p in chunk]
                 arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
-                rows = sum(-(-p.shape[0] // self.lazy_slices) * p.shape[1] for p in chunk)
+                rows = sum(-(-p.shape[0] // self.lazy_slices) * p.shape[1] for p in chunk) // n_parts
                 with profiling.region("adam_rows_slice", 24 * rows):
-                    native.check(native.lib().fr_adam_catch_up_slice(
+                    native.check(native.lib().fr_adam_catch_up_slice_part(
                         n, arr(chunk), arr([s_["exp_avg"] for s_ in st]), arr([s_["exp_avg_sq"] for s_ in st]),
                         arr([s_["step"] for s_ in st]), (ctypes.c_int64 * n)(*[p.shape[0] for p in chunk]),
                         (ctypes.c_int32 * n)(*[p.shape[1] for p in chunk]), arr([s_["lazy_last"] for s_ in st]),
-                        arr([s_["lazy_hist"] for s_ in st]), self.lazy_slices, self.hist_cap, float(beta1),
-                        float(beta2), float(group["eps"]), float(group["weight_decay"]),
-                        native.stream_of(chunk[0])), "fr_adam_catch_up_slice")
+                        arr([s_["lazy_hist"] for s_ in st]), self.lazy_slices, int(part), int(n_parts), self.hist_cap,
+                        float(beta1), float(beta2), float(group["eps"]), float(group["weight_decay"]),
+                        native.stream_of(chunk[0])), "fr_adam_catch_up_slice_part")
 
     @torch.no_grad()
     def catch_up_rows(self, p, ids):

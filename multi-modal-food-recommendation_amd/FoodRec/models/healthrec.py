@@ -204,6 +204,8 @@ class HealthRec(GeneralRecommender):
             mask = ingredients == self.n_ingredients
         encoded = layers.run_encoder(self.ingr_encoder, ingr_emb.permute(1, 0, 2), src_key_padding_mask=mask)
         encoded = encoded.permute(1, 0, 2).contiguous()
+        if xg is not None and hasattr(xg, "background_rest"):
+            xg.background_rest()  # the rest of the lazy-Adam background slice beside the loss head
 
         # gather-then-project == project-then-gather for a row-wise Linear (module docstring)
         if aux is not None:

@@ -589,11 +589,14 @@ __device__ __forceinline__ void catch_up_row(float* __restrict__ P0, float* __re
 // claimed are current and skip).  Issued once per step, it bounds every row's backlog by K steps,
 // so the flush that a full-table read needs costs K / 2 steps per row instead of the whole run's;
 // the work is the same replay the flush would do, moved to a stream that overlaps the step.
-__global__ __launch_bounds__(256) void adam_catch_up_slice_kernel(CatchArgs a, int nslices, int cap, AdamHyper h) {
+// part ``part`` of ``nparts`` of the slice (rows split evenly; nparts 1: the whole slice)
+__global__ __launch_bounds__(256) void adam_catch_up_slice_kernel(CatchArgs a, int nslices, int cap, AdamHyper h,
+                                                                  int part, int nparts) {
   const int t = blockIdx.y;
   const int64_t st = a.step[t][0], R = a.rows[t];
   const int64_t s = st % nslices;
-  const int64_t lo = R * s / nslices, hi = R * (s + 1) / nslices;
+  const int64_t lo0 = R * s / nslices, hi0 = R * (s + 1) / nslices;
+  const int64_t lo = lo0 + (hi0 - lo0) * part / nparts, hi = lo0 + (hi0 - lo0) * (part + 1) / nparts;
   const int64_t r = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= hi) return;
   catch_up_at(a.p[t], a.m[t], a.v[t], st, r, a.rshift[t], a.last[t], a.hist[t], cap, h);
@@ -949,13 +952,14 @@ extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, f
   return FR_OK;
 }
 
-extern "C" int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp_avg,
-                                      float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
-                                      const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
-                                      int32_t n_slices, int32_t hist_cap, double beta1, double beta2, double eps,
-                                      double weight_decay, void* stream) {
+extern "C" int fr_adam_catch_up_slice_part(int n_tables, float* const* params, float* const* exp_avg,
+                                           float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
+                                           const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
+                                           int32_t n_slices, int32_t part, int32_t n_parts, int32_t hist_cap,
+                                           double beta1, double beta2, double eps, double weight_decay, void* stream) {
   FR_REQUIRE(n_tables >= 0 && n_tables <= kMaxCatch, "n_tables out of range [0, 4]");
   FR_REQUIRE(n_slices >= 1, "n_slices < 1");
+  FR_REQUIRE(n_parts >= 1 && part >= 0 && part < n_parts, "part out of range [0, n_parts)");
   if (n_tables == 0) return FR_OK;
   CatchArgs a;
   AdamHyper h;
@@ -963,13 +967,23 @@ extern "C" int fr_adam_catch_up_slice(int n_tables, float* const* params, float*
                             beta1, beta2, eps, weight_decay, a, h);
   if (rc != FR_OK) return rc;
   int64_t most = 0;
-  for (int t = 0; t < n_tables; ++t) most = std::max<int64_t>(most, fr::ceil_div(rows[t], (int64_t)n_slices));
+  for (int t = 0; t < n_tables; ++t)
+    most = std::max<int64_t>(most, fr::ceil_div(fr::ceil_div(rows[t], (int64_t)n_slices), (int64_t)n_parts));
   if (most == 0) return FR_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(adam_catch_up_slice_kernel, dim3((unsigned)fr::ceil_div(most, 4), (unsigned)n_tables), dim3(256),
-                     0, s, a, n_slices, hist_cap, h);
+  hipLaunchKernelGGL(adam_catch_up_slice_kernel, dim3((unsigned)fr::ceil_div(most + 1, 4), (unsigned)n_tables),
+                     dim3(256), 0, s, a, n_slices, hist_cap, h, part, n_parts);
   FR_LAUNCH_CHECK();
   return FR_OK;
+}
+
+extern "C" int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp_avg,
+                                      float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
+                                      const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
+                                      int32_t n_slices, int32_t hist_cap, double beta1, double beta2, double eps,
+                                      double weight_decay, void* stream) {
+  return fr_adam_catch_up_slice_part(n_tables, params, exp_avg, exp_avg_sq, d_steps, rows, row_dims, d_last, d_hist,
+                                     n_slices, 0, 1, hist_cap, beta1, beta2, eps, weight_decay, stream);
 }
 
 // ---- self-test of the rounding shortcuts (diagnostic; tests/test_rowgrad_gpu.py) ---------------
