@@ -11,7 +11,7 @@ cd $R
 timeout -k 10 400 python -u -m pytest tests/test_config5_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread \
   > $OUT/topk_tests_$TAG.log 2>&1 || { grep -E "FAILED|Error|assert" $OUT/topk_tests_$TAG.log | head; tail -20 $OUT/topk_tests_$TAG.log; exit 1; }
 tail -1 $OUT/topk_tests_$TAG.log
-for sh in 0; do
+for sh in 0 1; do
   timeout -k 10 120 python3 tools/bench_topk.py --only 20,0 --reps 5 > $OUT/topk_${TAG}_s$sh.log 2>&1 || { tail -5 $OUT/topk_${TAG}_s$sh.log; exit 1; }
   echo "shape $sh: $(grep TFLOP $OUT/topk_${TAG}_s$sh.log)"
 done
