@@ -326,28 +326,6 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
         wf = thr_u;
       }
       const f32x16 av = acc[bb];
-      if constexpr (MODE == kAppend) {
-        // per score j one compare and one wave-uniform branch on its ballot (~8% of them taken): no
-        // per-lane candidate mask and no dynamic extraction of the score (j is a compile-time index)
-        const float wv = uvalid ? wf : INFINITY;
-        const int64_t ib0 = i_lo + (int64_t)t * C::TILE + bb * 32;  // wave-uniform block start
-        const int lim = ib0 + 32 <= i_hi ? 32 : (int)(i_hi - ib0);   // the split's last block: items past its end drop
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int off = 4 * h + (j & 3) + 8 * (j >> 2);
-          const bool c = av[j] >= wv && off < lim;
-          if (__ballot(c)) {
-            if (c) {
-              if (cnt < a.cap) {
-                a.cs[region * a.cap + cnt] = av[j];
-                a.ci[region * a.cap + cnt] = (int32_t)((ib0 + off) * a.item_mul);
-              }
-              ++cnt;
-            }
-          }
-        }
-        continue;
-      }
       uint32_t mask = 0u;
 #pragma unroll
       for (int j = 0; j < 16; ++j) mask |= av[j] >= wf ? (1u << j) : 0u;
