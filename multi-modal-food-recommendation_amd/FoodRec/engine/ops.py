@@ -1388,10 +1388,22 @@ _BRANCH_STREAM = {}
 _BRANCH_PENDING = []    # (event, deferred rows, ingredient table) of branch backwards not joined yet
 
 
+# FR_STREAM_PRIO="branch=-1,loss=-1,...": HIP stream priorities of the engine's side streams (roles
+# branch, aux, loss, side, rows; lower = higher priority; default: torch's default priority)
+_STREAM_PRIO = {k: int(v) for k, v in (kv.split("=") for kv in os.environ.get("FR_STREAM_PRIO", "").split(",") if kv)}
+
+
+def new_stream(device, role: str):
+    """A side stream of the engine for ``role`` (its FR_STREAM_PRIO priority when set)."""
+    if role in _STREAM_PRIO:
+        return torch.cuda.Stream(device, priority=_STREAM_PRIO[role])
+    return torch.cuda.Stream(device)
+
+
 def _branch_stream(device):
     s = _BRANCH_STREAM.get(device)
     if s is None:
-        s = torch.cuda.Stream(device)
+        s = new_stream(device, "branch")
         _BRANCH_STREAM[device] = s
     return s
 
@@ -1404,7 +1416,7 @@ def aux_stream(device):
     key = ("aux", str(device))
     s = _BRANCH_STREAM.get(key)
     if s is None:
-        s = torch.cuda.Stream(device)
+        s = new_stream(device, "aux")
         _BRANCH_STREAM[key] = s
     return s
 
@@ -1620,7 +1632,7 @@ def loss_side_stream(device=None, fork=False):
         return None
     s = _LOSS_STREAMS.get(device.index)
     if s is None:
-        s = _LOSS_STREAMS[device.index] = torch.cuda.Stream(device)
+        s = _LOSS_STREAMS[device.index] = new_stream(device, "loss")
     main = torch.cuda.current_stream(device)
     s.wait_stream(main)
     _LOSS_PENDING[0] = (main, s)

@@ -112,7 +112,8 @@ class RowGrads:
             return lambda stream=None: None
         main = torch.cuda.current_stream(pairs[0][0].device)
         if self._side is None:
-            self._side = torch.cuda.Stream(pairs[0][0].device)
+            from . import ops
+            self._side = ops.new_stream(pairs[0][0].device, "side")
         side = self._side
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -617,7 +618,8 @@ class FusedAdam(torch.optim.Optimizer):
         if dev.type != "cuda":
             return None
         if getattr(self, "_rows_stream", None) is None or self._rows_stream.device != dev:
-            self._rows_stream = torch.cuda.Stream(dev)
+            from . import ops
+            self._rows_stream = ops.new_stream(dev, "rows")
         return self._rows_stream
 
     def _arrays(self, plist, grads):

@@ -720,7 +720,7 @@ extern "C" int fr_embedding_rowgrad(const int64_t* d_idx, int64_t n, const float
 namespace {
 
 constexpr int kAtomWaves = 4;          // 256 threads
-constexpr int kAtomPerWave = 32;       // positions per wave -> 128 positions per block
+constexpr int kAtomPerWave = 16;       // consecutive positions per wave -> 64 positions per block
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int k) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, k);
@@ -728,33 +728,37 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int k) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
 }
 
+// One wave per 16 consecutive positions: the ids in lanes 0-15, then all 16 gradient rows loaded
+// before the first atomic (one memory round trip per wave: the scatter runs in the step's tail,
+// where a chain of dependent load rounds is what made it slow), then one 256-B float-atomic wave
+// instruction per position.  Positions at ``hot`` (the padding row, most of the ids) are summed in
+// registers and added with one atomic per block.
 __global__ __launch_bounds__(256) void emb_atomic_kernel(const int64_t* __restrict__ idx, int64_t n,
                                                          const float* __restrict__ G, int64_t ldg, int64_t R,
                                                          int64_t pad, int64_t hot, float* __restrict__ dW,
                                                          int64_t lddw) {
   __shared__ float hot_part[kAtomWaves][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * kAtomWaves * kAtomPerWave + wv;  // positions base + 4k
-  const int64_t my_i = base + (int64_t)kAtomWaves * (lane & 31);
-  const int64_t my_r = (lane < 32 && my_i < n) ? idx[my_i] : -1;
+  const int64_t base = ((int64_t)blockIdx.x * kAtomWaves + wv) * kAtomPerWave;
+  const int64_t my_r = (lane < kAtomPerWave && base + lane < n) ? idx[base + lane] : -1;
+  int64_t r[kAtomPerWave];
+  float g[kAtomPerWave];
+#pragma unroll
+  for (int u = 0; u < kAtomPerWave; ++u) {
+    r[u] = readlane64(my_r, u);  // wave-uniform; -1 past n
+    if (!(r[u] >= 0 && r[u] < R && r[u] != pad)) r[u] = -1;
+    g[u] = r[u] >= 0 ? __builtin_nontemporal_load(G + (base + u) * ldg + lane) : 0.f;
+  }
+  // every row arrived before the first atomic: the waits the compiler would place inside the
+  // branchy atomic loop are vmcnt(0), which also waits for the atomics already issued
+#pragma unroll
+  for (int u = 0; u < kAtomPerWave; ++u) asm volatile("" : "+v"(g[u]));
   float h = 0.f;
-#pragma unroll 1
-  for (int k0 = 0; k0 < kAtomPerWave; k0 += 4) {
-    int64_t r[4];
-    float g[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      r[u] = readlane64(my_r, k0 + u);  // wave-uniform; -1 past n
-      const bool live = r[u] >= 0 && r[u] < R && r[u] != pad;
-      g[u] = live ? G[(base + (int64_t)kAtomWaves * (k0 + u)) * ldg + lane] : 0.f;
-      if (!live) r[u] = -1;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (r[u] < 0) continue;
-      if (r[u] == hot) h += g[u];
-      else atomicAdd(dW + r[u] * lddw + lane, g[u]);
-    }
+  for (int u = 0; u < kAtomPerWave; ++u) {
+    if (r[u] < 0) continue;
+    if (r[u] == hot) h += g[u];
+    else atomicAdd(dW + r[u] * lddw + lane, g[u]);
   }
   if (hot < 0 || hot >= R) return;  // block-uniform
   hot_part[wv][lane] = h;

@@ -541,7 +541,7 @@ def test_feed_batch_bad_id_is_reported(cuda):
     feats.check_ids()
 
 
-@pytest.mark.parametrize("n", [1024 * 20, 1000])
+@pytest.mark.parametrize("n", [1024 * 20, 1000, 17])
 @pytest.mark.parametrize("hot", [None, 19987, 5])
 def test_embedding_bwd_atomic_matches_sorted(cuda, hot, n):
     """fr_embedding_bwd_atomic (float atomics, the hot row pre-summed per workgroup) against the

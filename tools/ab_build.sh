@@ -8,7 +8,7 @@ T=/tmp/ab_$NAME/pkg/csrc
 rm -rf /tmp/ab_$NAME; mkdir -p /tmp/ab_$NAME; ln -s $R/include /tmp/ab_$NAME/include
 mkdir -p /tmp/ab_$NAME/pkg; cp -r $R/multi-modal-food-recommendation_amd/csrc $T; rm -rf $T/build
 git -C $R show $COMMIT:multi-modal-food-recommendation_amd/csrc/$FILE > $T/$FILE
-SRCS_CPP="fr_abi.cpp fr_io.cpp fr_comm.cpp"
+SRCS_CPP="fr_abi.cpp fr_io.cpp fr_comm.cpp fr_error.cpp fr_sampler.cpp"
 if [ -n "$EXTRA" ]; then cp $EXTRA $T/; SRCS_CPP="$SRCS_CPP $(basename $EXTRA)"; fi
 mkdir -p $R/ab
 make -s -j8 -C $T OUT_DIR=$R/ab OUT=$R/ab/libfr_engine_$NAME.so SRCS_CPP="$SRCS_CPP"
