@@ -160,8 +160,10 @@ int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
  * ACCUMULATES into dviews[v] (any may be NULL).
  * ------------------------------------------------------------------------------------------ */
 /* SSL kernel choice: mfma = 1 (default) runs the dCor / InfoNCE Gram tiles on v_mfma_f32_16x16x4_f32,
- * 2 the same with the round-4 InfoNCE kernels (row-layout logits, W staged in LDS), 0 the VALU 4x4-per-thread tiles (A/B
- * measurements), -1 keeps it; returns the previous choice. */
+ * 2 the same with the round-4 InfoNCE kernels (row-layout logits, W staged in LDS), 3 the round-5 transposed
+ * InfoNCE kernels with separate normalize / sum launches (mode 1 normalises inside the log-sum-exp
+ * kernel's tile staging and sums in the finalize's last workgroup), 0 the VALU 4x4-per-thread tiles
+ * (A/B measurements), -1 keeps it; returns the previous choice. */
 int fr_ssl_kernels(int mfma);
 int64_t fr_dcor_workspace(int64_t n, int n_views);
 
@@ -694,6 +696,13 @@ int fr_norms_bwd_coef(const int64_t* d_ids, int64_t n, int64_t half, int64_t pad
                       const float* d_gn, int64_t gn_stride, const float* d_nrm, float* d_out, void* stream);
 int fr_reg_combine_norms_fwd(const float* d_a, const float* d_partials, int64_t n, float B, float w, float* d_nrm,
                              float* d_out, void* stream);
+/* fr_norms_bwd_coef's rows scattered with fr_embedding_bwd_atomic's float atomics in one launch:
+ * d_out[ids[i]] += G[i] + [ids[i] != pad] (gn[h] / nrm[h]) E[i] for ids in [0, num_rows), the
+ * hot_row's positions pre-summed per workgroup (HealthRec's deferred ingredient rows, added into the
+ * RI backward's d ingre: cikm_model.py:230 + 270-279).  G, E: [n, 64] dense fp32. */
+int fr_norms_bwd_scatter(const int64_t* d_ids, int64_t n, int64_t half, int64_t pad, const float* d_g,
+                         const float* d_e, const float* d_gn, int64_t gn_stride, const float* d_nrm, int64_t num_rows,
+                         int64_t hot_row, float* d_out, int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Host-side readers of the reference's on-disk interaction formats (no GPU).

@@ -1450,9 +1450,8 @@ def run_pending_drains(after=None) -> None:
         main = torch.cuda.current_stream(ingre_w.device)
         side = _branch_stream(ingre_w.device)
         side.wait_event(fork)
-        for idx, G, _ in defer.rows:
-            idx.record_stream(side)
-            G.record_stream(side)
+        for t in defer.tensors():
+            t.record_stream(side)
         if ingre_w.grad is not None:
             ingre_w.grad.record_stream(side)
         with torch.cuda.stream(side):
@@ -1568,14 +1567,47 @@ class _DeferredRows:
     def put(self, idx, G, hot_row) -> bool:
         if not self.open:
             return False
-        self.rows.append((idx, G, hot_row))
+        self.rows.append(("rows", (idx, G), hot_row))
         return True
+
+    def put_norms(self, idx, G, E, gn, nrm, half, pad) -> bool:
+        """Rows G + coef E of embedding_norms' backward, formed by the drain's scatter itself
+        (fr_norms_bwd_scatter: no separate fr_norms_bwd_coef launch, no [n, 64] rows written)."""
+        if not self.open:
+            return False
+        self.rows.append(("norms", (idx, G, E, gn, nrm), (half, pad)))
+        return True
+
+    def tensors(self):
+        return [t for _, ts, _ in self.rows for t in ts]
 
     def drain(self, dW):
         self.open = False
-        for idx, G, hot_row in self.rows:
-            scatter_rows_into(idx, G, dW, hot_row)
+        for kind, ts, meta in self.rows:
+            if kind == "rows":
+                scatter_rows_into(ts[0], ts[1], dW, meta)
+            else:
+                norms_scatter_into(*ts, *meta, dW)
         self.rows = []
+
+
+# FR_NORMS_SCATTER=0: the deferred ingredient rows formed by fr_norms_bwd_coef at the end of the
+# encoder backward and scattered by the drain (two launches) instead of fr_norms_bwd_scatter there
+NORMS_SCATTER = os.environ.get("FR_NORMS_SCATTER", "1") != "0"
+
+
+def norms_scatter_into(idx, G, E, gn, nrm, half, pad, dW) -> None:
+    """``dW[idx[i]] += G[i] + [idx[i] != pad] (gn[h] / nrm[h]) E[i]`` (h: the position's half) with
+    float atomics, the pad row pre-summed per workgroup (fr_norms_bwd_scatter)."""
+    n = int(idx.numel())
+    native.require_device(G, E, dW)
+    if dW.dtype != torch.float32 or dW.shape[1] != 64 or dW.stride(1) != 1 or dW.stride(0) % 4 or dW.data_ptr() % 16:
+        raise native.EngineError("norms_scatter_into: fp32 [rows, 64] table with 16-B aligned rows required")
+    with profiling.region("embedding_bwd", embedding_bwd_bytes(n, int(dW.shape[0]), 64) + 4 * n * 64):
+        native.check(native.lib().fr_norms_bwd_scatter(
+            idx.data_ptr(), n, int(half), -1 if pad is None else int(pad), G.data_ptr(), E.data_ptr(), gn.data_ptr(),
+            gn.stride(0), nrm.data_ptr(), int(dW.shape[0]), -1 if pad is None else int(pad), dW.data_ptr(),
+            dW.stride(0), native.stream_of(G)), "fr_norms_bwd_scatter")
 
 
 class _RegCombine(torch.autograd.Function):
@@ -1961,6 +1993,10 @@ class _EmbeddingNorms(torch.autograd.Function):
         idx, E, nrm = ctx.saved_tensors
         if ctx.fused:
             G = torch.zeros_like(E) if gE is None else gE.contiguous()
+            if (gn is not None and NORMS_SCATTER and ctx.defer is not None and ctx.hp <= idx.numel()
+                    and ctx.defer.put_norms(idx.reshape(-1), G.reshape(-1, 64), E.reshape(-1, 64), gn, nrm, ctx.hp,
+                                            ctx.pad)):
+                return None, None, None, None, None  # formed and scattered by the drain (fr_norms_bwd_scatter)
             if gn is not None:
                 out = torch.empty_like(G)
                 with profiling.region("gather_norms", 8 * idx.numel() + 3 * 4 * G.numel()):

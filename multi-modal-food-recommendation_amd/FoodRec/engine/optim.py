@@ -178,10 +178,12 @@ def _row_grad_ok(p, ids, G) -> bool:
             and ids.numel() <= ROW_GRAD_MAX and G.dtype == torch.float32 and p.data_ptr() % 16 == 0)
 
 
-# FR_HELD_ON_BRANCH=1: a late-drained table's update on the branch stream right behind the scatter of
-# its deferred rows (round-5 experiment: 0.694 / 0.691 vs 0.688 / 0.689 ms per step, slower, off);
-# default: on the current stream after the join (round 4)
-HELD_ON_BRANCH = os.environ.get("FR_HELD_ON_BRANCH", "0") == "1"
+# a late-drained table's update on the branch stream right behind the scatter of its deferred rows
+# (no cross-queue hop between them).  Slower while that scatter was a chain of dependent load rounds
+# (0.694 / 0.691 vs 0.688 / 0.689 ms per step); with the one-round scatter formed from the norms'
+# backward in the same launch (fr_norms_bwd_scatter) 0.682 / 0.673 vs 0.685 / 0.684 ms, on.
+# FR_HELD_ON_BRANCH=0: the held update on the current stream after the join (round 4)
+HELD_ON_BRANCH = os.environ.get("FR_HELD_ON_BRANCH", "1") == "1"
 
 
 class FusedAdam(torch.optim.Optimizer):

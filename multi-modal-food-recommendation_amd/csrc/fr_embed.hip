@@ -770,6 +770,52 @@ __global__ __launch_bounds__(256) void emb_atomic_kernel(const int64_t* __restri
   }
 }
 
+// fr_norms_bwd_coef + fr_embedding_bwd_atomic in one launch (HealthRec's deferred ingredient rows):
+// the row of position i is G[i] + c_i E[i], c_i = [ids[i] != pad] gn[h] / nrm[h] with h the
+// position's half (vector_norm's backward, zero where the norm is zero), scattered as above
+__global__ __launch_bounds__(256) void norms_scatter_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t half,
+                                                            int64_t pad, const float* __restrict__ G,
+                                                            const float* __restrict__ E,
+                                                            const float* __restrict__ gn, int64_t gn_stride,
+                                                            const float* __restrict__ nrm, int64_t R, int64_t hot,
+                                                            float* __restrict__ dW, int64_t lddw) {
+  __shared__ float hot_part[kAtomWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float c0 = nrm[0] > 0.f ? gn[0] / nrm[0] : 0.f;
+  const float c1 = nrm[1] > 0.f ? gn[gn_stride] / nrm[1] : 0.f;
+  const int64_t base = ((int64_t)blockIdx.x * kAtomWaves + wv) * kAtomPerWave;
+  const int64_t my_i = (lane < kAtomPerWave && base + lane < n) ? idx[base + lane] : -1;
+  int64_t r[kAtomPerWave];
+  float g[kAtomPerWave], e[kAtomPerWave];
+#pragma unroll
+  for (int u = 0; u < kAtomPerWave; ++u) {
+    const int64_t id = readlane64(my_i, u);  // wave-uniform; -1 past n
+    r[u] = (id >= 0 && id < R) ? id : -1;
+    const int64_t off = (base + u) * 64 + lane;
+    g[u] = r[u] >= 0 ? __builtin_nontemporal_load(G + off) : 0.f;
+    e[u] = (r[u] >= 0 && id != pad) ? __builtin_nontemporal_load(E + off) : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kAtomPerWave; ++u) asm volatile("" : "+v"(g[u]), "+v"(e[u]));
+  float h = 0.f;
+#pragma unroll
+  for (int u = 0; u < kAtomPerWave; ++u) {
+    if (r[u] < 0) continue;
+    const float c = r[u] == pad ? 0.f : (base + u < half ? c0 : c1);
+    const float v = fmaf(c, e[u], g[u]);  // the bits norms_bwd_kernel writes
+    if (r[u] == hot) h += v;
+    else atomicAdd(dW + r[u] * lddw + lane, v);
+  }
+  if (hot < 0 || hot >= R) return;  // block-uniform
+  hot_part[wv][lane] = h;
+  __syncthreads();
+  if (wv == 0) {
+    float t = hot_part[0][lane];
+    for (int w2 = 1; w2 < kAtomWaves; ++w2) t += hot_part[w2][lane];
+    if (__ballot(t != 0.f)) atomicAdd(dW + hot * lddw + lane, t);
+  }
+}
+
 }  // namespace
 
 extern "C" int fr_embedding_bwd_atomic(const int64_t* d_idx, int64_t n, const float* d_grad, int64_t ldg, int d,
@@ -786,6 +832,22 @@ extern "C" int fr_embedding_bwd_atomic(const int64_t* d_idx, int64_t n, const fl
   FR_REQUIRE(blocks < (int64_t)INT32_MAX, "too many positions");
   hipLaunchKernelGGL(emb_atomic_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      d_idx, n, d_grad, ldg, num_rows, padding_idx, hot_row, d_out, ldo);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int fr_norms_bwd_scatter(const int64_t* d_ids, int64_t n, int64_t half, int64_t pad, const float* d_g,
+                                    const float* d_e, const float* d_gn, int64_t gn_stride, const float* d_nrm,
+                                    int64_t num_rows, int64_t hot_row, float* d_out, int64_t ldo, void* stream) {
+  FR_REQUIRE(n >= 0 && half >= 0 && half <= n && num_rows >= 1, "bad sizes");
+  if (n == 0) return FR_OK;
+  FR_REQUIRE(d_ids && d_g && d_e && d_gn && d_nrm && d_out, "null operand");
+  FR_REQUIRE(ldo >= 64 && ldo % 4 == 0 && fr::aligned16(d_out), "out: 64-wide rows, ld % 4 == 0, 16-B aligned");
+  const int64_t per_block = (int64_t)kAtomWaves * kAtomPerWave;
+  const int64_t blocks = fr::ceil_div(n, per_block);
+  FR_REQUIRE(blocks < (int64_t)INT32_MAX, "too many positions");
+  hipLaunchKernelGGL(norms_scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     d_ids, n, half, pad, d_g, d_e, d_gn, gn_stride, d_nrm, num_rows, hot_row, d_out, ldo);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

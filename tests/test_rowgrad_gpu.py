@@ -566,6 +566,34 @@ def test_embedding_bwd_atomic_matches_sorted(cuda, hot, n):
     assert torch.all((pad_got - pad_ref).abs() <= 1e-5 * scale + 1e-6)
 
 
+@pytest.mark.parametrize("n", [1024 * 20, 1000, 17])
+def test_norms_bwd_scatter_matches_two_launches(cuda, n):
+    """fr_norms_bwd_scatter (HealthRec's deferred ingredient rows formed inside the scatter) against
+    fr_norms_bwd_coef + the deterministic scatter: equal to fp32 rounding (rel 1e-5 of the row
+    scale); the padding positions take G only (pre-summed into the pad row), the two halves their
+    own coefficient, out-of-range ids skipped, a zero norm gives a zero coefficient."""
+    from FoodRec.engine import native, ops
+    g = torch.Generator().manual_seed(5)
+    R, pad = 19988, 19987
+    ids = torch.randint(0, R - 1, (n,), generator=g)
+    ids[torch.rand(n, generator=g) < 0.5] = pad
+    ids[min(7, n - 1)] = R + 5
+    G = torch.randn(n, 64, generator=g)
+    E = torch.randn(n, 64, generator=g)
+    half = n // 2
+    for nrm_h, gn_h in (([3.0, 2.0], [0.7, -1.3]), ([0.0, 2.0], [0.7, -1.3])):
+        idc, Gc, Ec = ids.to(cuda), G.to(cuda), E.to(cuda)
+        nrm, gn = torch.tensor(nrm_h, device=cuda), torch.tensor(gn_h, device=cuda)
+        rows = torch.empty_like(Gc)
+        native.check(native.lib().fr_norms_bwd_coef(idc.data_ptr(), n, half, pad, Gc.data_ptr(), Ec.data_ptr(),
+                                                    gn.data_ptr(), 1, nrm.data_ptr(), rows.data_ptr(), 0), "coef")
+        ref = ops.scatter_rows(idc, rows, R, None)
+        got = torch.zeros(R, 64, device=cuda)
+        ops.norms_scatter_into(idc, Gc, Ec, gn, nrm, half, pad, got)
+        scale = ops.scatter_rows(idc, rows.abs(), R, None) + ops.scatter_rows(idc, Ec.abs(), R, None)
+        assert torch.all((got - ref).abs() <= 1e-5 * scale + 1e-6)
+
+
 @pytest.mark.parametrize("slices", [1, 3, 8])
 def test_lazy_rows_background_slices(cuda, slices):
     """Background slice replay (fr_adam_catch_up_slice, issued by prefetch_rows behind the batch's

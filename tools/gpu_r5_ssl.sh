@@ -12,7 +12,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_wide_
   -k "infonce or dcor or nce or PRICAI" --timeout 200 --timeout-method thread > $OUT/ssl_tests_$TAG.log 2>&1 \
   || { grep -E "FAILED|Error|assert" $OUT/ssl_tests_$TAG.log | head; tail -20 $OUT/ssl_tests_$TAG.log; exit 1; }
 tail -1 $OUT/ssl_tests_$TAG.log
-for mode in 1 2 1 2; do
+for mode in ${SSL_MODES:-1 2 1 2}; do
   timeout -k 10 120 python3 tools/profile_ssl.py $mode > $OUT/ssl_${TAG}_m$mode.json 2>&1 || { tail -5 $OUT/ssl_${TAG}_m$mode.json; exit 1; }
   echo "mode $mode: $(tail -1 $OUT/ssl_${TAG}_m$mode.json)"
 done
