@@ -160,10 +160,8 @@ int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
  * ACCUMULATES into dviews[v] (any may be NULL).
  * ------------------------------------------------------------------------------------------ */
 /* SSL kernel choice: mfma = 1 (default) runs the dCor / InfoNCE Gram tiles on v_mfma_f32_16x16x4_f32,
- * 2 the same with the round-4 InfoNCE kernels (row-layout logits, W staged in LDS), 3 the round-5 transposed
- * InfoNCE kernels with separate normalize / sum launches (mode 1 normalises inside the log-sum-exp
- * kernel's tile staging and sums in the finalize's last workgroup), 0 the VALU 4x4-per-thread tiles
- * (A/B measurements), -1 keeps it; returns the previous choice. */
+ * 2 the same with the round-4 InfoNCE kernels (row-layout logits, W staged in LDS), 0 the VALU 4x4-per-thread tiles (A/B
+ * measurements), -1 keeps it; returns the previous choice. */
 int fr_ssl_kernels(int mfma);
 int64_t fr_dcor_workspace(int64_t n, int n_views);
 

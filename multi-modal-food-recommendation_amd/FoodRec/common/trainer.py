@@ -725,11 +725,12 @@ class Trainer(AbstractTrainer):
             state["nan"].zero_()
             if step.feed is None and hasattr(train_data, "device_feed"):
                 step.attach_feed(train_data)
-            for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs, feed=step.feed)):
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch(out=step.inputs, feed=step.feed,
+                                                                   prefetch=self._prefetch_ok(train_data, epoch_idx))):
                 loss_batches.append(step(u, p, n, batch_idx, state))
             step.flush()
         else:
-            for batch_idx, (u, p, n) in enumerate(train_data.epoch()):
+            for batch_idx, (u, p, n) in enumerate(train_data.epoch(prefetch=self._prefetch_ok(train_data, epoch_idx))):
                 loss_batches.append(self.train_step(feats.batch(u, p, n), batch_idx, state, loss_func))
         self.flush_optimizer()
         if hasattr(feats, "check_ids"):
@@ -741,6 +742,15 @@ class Trainer(AbstractTrainer):
             return torch.tensor(float("nan")), torch.tensor(0.0), None
         total = tuple(state["acc"].cpu().tolist())
         return (total if len(total) > 1 else total[0]), loss_batches, None
+
+    def _prefetch_ok(self, train_data, epoch_idx) -> bool:
+        """Draw the next epoch's permutation and negatives on a host thread during this epoch
+        (TripleSampler.prefetch): on a GPU, where nothing in a training epoch draws from the torch CPU
+        or np.random generators (dropout runs on the device), so the streams are the reference's;
+        not after the last epoch.  Config ``sampler_prefetch`` (default on) turns it off."""
+        on = self.config["sampler_prefetch"] if "sampler_prefetch" in self.config else None
+        return (hasattr(train_data, "prefetch") and self._on_gpu() and on is not False
+                and epoch_idx + 1 < self.epochs)
 
     # ------------------------------------------------------------------------------ evaluation
     def _candidates(self, is_test):

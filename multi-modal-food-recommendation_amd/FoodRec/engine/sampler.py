@@ -81,6 +81,12 @@ class TripleSampler:
         self.neg_list_post = self._init_neg_list(replay_python_random)
         self._dev_users = torch.from_numpy(self.users).to(self.device)
         self._dev_items = torch.from_numpy(self.items).to(self.device)
+        self._pending = None    # the next epoch's host draws, in flight on a host thread (prefetch)
+        self._pool = None
+        self._slot = 0          # pinned staging buffer of the next draw (two alternate)
+        self._pins = [None, None]
+        self._pin_copied = [None, None]
+        self.last_draw_ms = None
 
     def _negatives(self, users, perm=None, out=None):
         d = self.ds
@@ -111,31 +117,79 @@ class TripleSampler:
         batches: see DeviceFeed)."""
         return DeviceFeed(self._dev_users, self._dev_items, self.n, self.batch_size, self.device)
 
-    def epoch(self, out=None, feed=None):
+    def _draw_host(self, slot):
+        """One epoch's host draws: the permutation and every pair's negative, in the reference's
+        order; on a GPU into pinned staging buffer ``slot`` (after its previous copy has finished)."""
+        import time
+        t0 = time.perf_counter()
+        perm = self.epoch_order().numpy()
+        if self.device.type == "cuda":
+            if self._pins[slot] is None or self._pins[slot].numel() != self.n:
+                self._pins[slot] = torch.empty(self.n, dtype=torch.int64, pin_memory=True)
+                self._pin_copied[slot] = None
+            if self._pin_copied[slot] is not None:
+                self._pin_copied[slot].synchronize()  # this buffer's previous copy to the device is done
+            self._negatives(self.users, perm=perm, out=self._pins[slot].numpy())
+            negs = self._pins[slot]
+        else:
+            negs = torch.from_numpy(self._negatives(self.users, perm=perm))
+        self.last_draw_ms = (time.perf_counter() - t0) * 1e3
+        return perm, negs, slot
+
+    def prefetch(self):
+        """Start the next epoch's host draws (torch's permutation, np.random's negatives) on a host
+        thread, so they overlap this epoch's steps; the next ``epoch()`` takes them.  The streams are
+        those of drawing at the next epoch's start provided nothing else draws from the torch CPU or
+        np.random global generators meanwhile -- true of a GPU training epoch (device dropout), which is
+        where the trainer uses it.  The native sampler and randperm release the GIL."""
+        if self._pending is not None:
+            return
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fr-sampler")
+        slot, self._slot = self._slot, self._slot ^ 1
+        self._pending = self._pool.submit(self._draw_host, slot)
+
+    def wait_prefetch(self):
+        """Block until a prefetch in flight has finished (its draws stay queued for ``epoch()``)."""
+        if self._pending is not None:
+            self._pending.result()
+
+    def discard_prefetch(self):
+        """Wait for a prefetch in flight and drop its draws (the generators have advanced past them:
+        measurement use only)."""
+        if self._pending is not None:
+            self._pending.result()
+            self._pending = None
+
+    def epoch(self, out=None, feed=None, prefetch: bool = False):
         """Yield (u, pos, neg) int64 device tensors per batch for one epoch.  Negatives are drawn
         per batch (same stream as the reference's per-sample draws, in permutation order).  With
         ``out`` = three [batch_size] device buffers (a graphed step's static inputs), full batches
-        are written into them and the buffers are yielded."""
-        perm = self.epoch_order().numpy()
-        perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
+        are written into them and the buffers are yielded.  ``prefetch``: once this epoch is staged,
+        start the next epoch's host draws on a host thread (``prefetch()``)."""
         # the whole epoch's negatives in one native call and one host->device copy: the same draws in
         # the same order as per-batch (or the reference's per-sample) drawing, since nothing else
         # consumes np.random during an epoch; the steps then only index device arrays.  On a GPU the
-        # draws land in a persistent pinned staging buffer (no pageable copy / pin per epoch)
-        if self.device.type == "cuda":
-            if getattr(self, "_negs_pin", None) is None or self._negs_pin.numel() != self.n:
-                self._negs_pin = torch.empty(self.n, dtype=torch.int64, pin_memory=True)
-                self._negs_copied = None
-            if self._negs_copied is not None:
-                self._negs_copied.synchronize()  # the previous epoch's copy out of the buffer is done
-            self._negatives(self.users, perm=perm, out=self._negs_pin.numpy())
-            negs_d = self._negs_pin.to(self.device, non_blocking=True)
-            self._negs_copied = torch.cuda.Event()
-            self._negs_copied.record(torch.cuda.current_stream(self.device))
+        # draws land in one of two persistent pinned staging buffers (no pageable copy / pin per epoch)
+        if self._pending is not None:
+            perm, negs_h, slot = self._pending.result()
+            self._pending = None
         else:
-            negs_d = torch.from_numpy(self._negatives(self.users, perm=perm))
+            slot, self._slot = self._slot, self._slot ^ 1
+            perm, negs_h, slot = self._draw_host(slot)
+        perm_d = torch.from_numpy(perm).to(self.device, non_blocking=True)
+        if self.device.type == "cuda":
+            negs_d = negs_h.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._pin_copied[slot] = ev
+        else:
+            negs_d = negs_h
         if feed is not None and out is not None:
             feed.stage(perm_d, negs_d)
+        if prefetch:
+            self.prefetch()
         for s in range(0, self.n, self.batch_size):
             idx = perm_d[s:s + self.batch_size]
             negs = negs_d[s:s + self.batch_size]

@@ -76,6 +76,35 @@ def test_sampler_stream_bit_exact():
         np.testing.assert_array_equal(n, g[f"ep{ep}/n"])
 
 
+def test_sampler_prefetch_keeps_the_stream():
+    """TripleSampler.prefetch (the next epoch's permutation and negatives drawn on a host thread
+    while this epoch's batches are consumed) yields the reference stream: the golden epochs, and the
+    global RNG states after them, equal those of drawing at each epoch's start."""
+    from FoodRec.engine.sampler import TripleSampler
+    from FoodRec.utils.utils import get_model, init_seed
+    g = golden("stream.npz")
+    cfg = tiny_config("LightGCN", False)
+    data = tiny_data(cfg)
+    init_seed(999)
+    get_model("LightGCN")(cfg, data)
+    s = TripleSampler(data, int(g["batch_size"]))
+    for ep in range(2):
+        u, p, n = (np.concatenate(x) for x in zip(*[(a.numpy(), b.numpy(), c.numpy())
+                                                     for a, b, c in s.epoch(prefetch=ep == 0)]))
+        np.testing.assert_array_equal(u, g[f"ep{ep}/u"])
+        np.testing.assert_array_equal(p, g[f"ep{ep}/p"])
+        np.testing.assert_array_equal(n, g[f"ep{ep}/n"])
+    assert s._pending is None
+    after = (torch.get_rng_state(), np.random.get_state()[1].copy())
+    init_seed(999)
+    get_model("LightGCN")(cfg, data)
+    s2 = TripleSampler(data, int(g["batch_size"]))
+    for _ in range(2):
+        list(s2.epoch())
+    assert torch.equal(after[0], torch.get_rng_state())
+    np.testing.assert_array_equal(after[1], np.random.get_state()[1])
+
+
 def test_randint_stream_equals_numpy():
     from FoodRec.engine.sampler import draw_negatives
     import ctypes
