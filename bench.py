@@ -315,6 +315,12 @@ def main():
     finally:
         _ops_mod.BRANCH_STREAMS = branch0
 
+    # the same regions inside a graph replay: a one-step graph of the training step captured with
+    # device wall-clock stamps around every region (timing events cannot be recorded in a graph)
+    kern_graph = None
+    if graphed is not None and world == 1 and not dp1 and args.kernel_steps > 0:
+        kern_graph = graph_region_pass(trainer, args.batch, sampler, device, args.kernel_steps)
+
     ms_steps = t_steps / args.steps * 1e3
     flush_ms = flush_s * 1e3
     ms_per_step = ms_steps + (epoch_ms + flush_ms) / steps_per_epoch
@@ -326,11 +332,19 @@ def main():
     traffic = args.traffic if args.traffic is not None else pmc_traffic(dom_name)
     roofline = None
     if dom_name is not None:
-        d = kern[dom_name]
+        d = dict(kern[dom_name])
+        eager_d = dict(d)
+        src = ("HIP events per launch on the launch stream, eager pass of "
+               f"{ksteps} steps right after the timed region (kernels.{dom_name})")
+        if kern_graph is not None and dom_name in kern_graph:
+            gd = kern_graph[dom_name]
+            d.update(avg_ms=gd["avg_ms"], total_ms=gd["avg_ms"] * gd["launches_per_step"] * ksteps,
+                     launches=gd["launches_per_step"] * ksteps)
+            src = ("device wall-clock stamps (fr_stamp) around each call inside a graph replay: a one-step graph "
+                   f"of the training step captured with the stamps, {gd['replays']} replays (kernels_in_graph."
+                   f"{dom_name}; includes the stamps' launch gaps)")
         common = {"kernel": dom_name, "avg_launch_ms": round(d["avg_ms"], 4), "launches_per_step": d["launches"] / ksteps,
-                  "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3),
-                  "timing_source": "HIP events per launch on the launch stream, eager pass of "
-                                   f"{ksteps} steps right after the timed region (kernels.{dom_name})"}
+                  "share_of_step": round(d["total_ms"] / ksteps / ms_per_step, 3), "timing_source": src}
         if dom_name.startswith("encoder_"):
             # the fused Transformer layer: fp32 MFMA GEMMs (v_mfma_f32_16x16x4_f32) -> an MFMA roofline
             from FoodRec.engine import ops as _ops
@@ -345,6 +359,11 @@ def main():
                                            if dom_name.endswith("bwd") else "enc_fwd_kernel<20>"),
                         "note": "dense fp32 MFMA peak; the layer's 20x20 attention, LayerNorms, GELU and dropout "
                                 "hash run on the VALU between the GEMMs (latency-bound at 1 workgroup per CU)"}
+            tfe = fl / (eager_d["avg_ms"] * 1e-3) / 1e12
+            roofline["eager"] = {"avg_launch_ms": round(eager_d["avg_ms"], 4), "achieved": round(tfe, 2),
+                                 "frac": round(tfe / MFMA_F32_PEAK_TFLOPS, 4),
+                                 "note": "HIP events in the eager pass (other streams' kernels overlap it differently "
+                                         "than in the graph)"}
             iso = kern_iso.get(dom_name)
             if iso is not None:
                 tfi = fl / (iso["avg_ms"] * 1e-3) / 1e12
@@ -378,6 +397,8 @@ def main():
     kernels = {k: {"avg_ms": round(v["avg_ms"], 4), "per_step_ms": round(v["total_ms"] / ksteps, 4),
                    "gbps": round(v["gbps"], 1)} for k, v in kern.items()}
     graph_unroll = (graphed.unroll if world == 1 and not dp1 else 1) if graphed is not None else 0
+    if kern_graph is not None:
+        kernels["_in_graph"] = kern_graph
     kernels["_timing"] = {"step_execution": "hip_graph_replay" if use_graph else "eager",
                           "kernel_pass": f"{ksteps} eager steps, HIP events on the launch stream",
                           "eager_ms_per_step": round(eager_elapsed / ksteps * 1e3, 4)}
@@ -607,6 +628,40 @@ def config5(device, batches=(512, 8192), steps=3, warmup=2, spmm_iters=5, topk_u
            "byte_model": "SURVEY 8(d) with s=2: 2L*B_spmm + 2(L+1)*N*d*2 + 30*P + B*(3*8+3*d*2)*2"}
     del model, g, adj, tables
     torch.cuda.empty_cache()
+    return out
+
+
+def graph_region_pass(trainer, B, sampler, device, reps):
+    """Per-region durations INSIDE a graph replay: a one-step graph of the same training step (unroll
+    1, batches copied into its inputs) captured while profiling.StampTimer brackets every region with
+    device wall-clock stamps, then replayed ``reps`` times; {region: avg_ms, launches_per_step, ...}."""
+    from collections import defaultdict
+    from FoodRec.engine import profiling
+    g2 = trainer.graphed_step(B, warmup=3, unroll=1)
+    st2 = g2.state
+
+    def batches():
+        while True:
+            for t in sampler.epoch(out=g2.inputs):
+                yield t
+
+    it2 = batches()
+    with profiling.stamping(device) as stamps:
+        n0 = g2.prepare(lambda: next(it2), st2)
+    per = defaultdict(list)
+    for r in range(reps):
+        g2(*next(it2), n0 + r, st2)
+        step = defaultdict(list)
+        for name, us, _ in stamps.read():
+            step[name].append(us)
+        for name, v in step.items():
+            per[name].append(v)
+    out = {}
+    for name, steps in per.items():
+        flat = [x for v in steps for x in v]
+        out[name] = {"avg_ms": round(sum(flat) / len(flat) / 1e3, 4), "launches_per_step": len(steps[0]),
+                     "median_ms": round(sorted(flat)[len(flat) // 2] / 1e3, 4), "replays": len(steps)}
+    del g2, st2, it2
     return out
 
 

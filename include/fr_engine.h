@@ -162,6 +162,11 @@ int fr_bpr_bwd_ex(const float* d_U, int64_t ldu, const float* d_I, int64_t ldi,
 /* SSL kernel choice: mfma = 1 (default) runs the dCor / InfoNCE Gram tiles on v_mfma_f32_16x16x4_f32,
  * 2 the same with the round-4 InfoNCE kernels (row-layout logits, W staged in LDS), 0 the VALU 4x4-per-thread tiles (A/B
  * measurements), -1 keeps it; returns the previous choice. */
+/* Measurement: fr_stamp launches one single-lane kernel that writes the device's constant-rate wall
+ * clock (fr_stamp_hz ticks per second, 0 without a device) to *d_slot: two stamps on a stream bracket
+ * the kernels issued between them, also inside a captured HIP graph (no timing events there). */
+int fr_stamp(int64_t* d_slot, void* stream);
+int64_t fr_stamp_hz(void);
 int fr_ssl_kernels(int mfma);
 int64_t fr_dcor_workspace(int64_t n, int n_views);
 

@@ -277,6 +277,8 @@ _SIGS = {
                                     c_void_p, c_void_p]),
     "fr_norms_bwd_coef": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_void_p, c_void_p]),
+    "fr_stamp": (c_int, [c_void_p, c_void_p]),
+    "fr_stamp_hz": (c_int64, []),
     "fr_norms_bwd_scatter": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
                                      c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     "fr_comm_available": (c_int, []),

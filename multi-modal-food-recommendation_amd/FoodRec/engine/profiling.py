@@ -51,6 +51,42 @@ class KernelTimer:
                 for k, (n, t, b, v) in agg.items()}
 
 
+class StampTimer:
+    """Region timing inside a captured HIP graph (timing events cannot be recorded during capture):
+    each region is bracketed by two fr_stamp launches writing the device's constant-rate wall
+    clock into its own slot of a device buffer.  Capture one step with this active, replay the graph,
+    then ``read`` the per-region durations of that replay (the stamp kernels' own launch gaps, ~1-2
+    µs per region, are included: an upper bound on the kernels' time)."""
+
+    def __init__(self, device, capacity: int = 1024):
+        from . import native
+        self.lib = native.lib()
+        self.hz = int(self.lib.fr_stamp_hz())
+        self.buf = torch.zeros(capacity, 2, dtype=torch.int64, device=device)
+        self.names = []  # (name, algorithmic bytes) per slot, in issue order
+
+    @contextlib.contextmanager
+    def region(self, name: str, nbytes: int):
+        from . import native
+        i = len(self.names)
+        if i >= self.buf.shape[0]:
+            yield
+            return
+        self.names.append((name, int(nbytes), torch.cuda.is_current_stream_capturing()))
+        st = torch.cuda.current_stream(self.buf.device).cuda_stream
+        native.check(self.lib.fr_stamp(self.buf[i, 0].data_ptr(), st), "fr_stamp")
+        try:
+            yield
+        finally:
+            native.check(self.lib.fr_stamp(self.buf[i, 1].data_ptr(), st), "fr_stamp")
+
+    def read(self) -> list:
+        """[(name, microseconds, bytes)] of the captured regions' last replay, in issue order."""
+        torch.cuda.synchronize()
+        t = self.buf[:len(self.names)].cpu()
+        return [(n, float(t[i, 1] - t[i, 0]) * 1e6 / self.hz, b) for i, (n, b, cap) in enumerate(self.names) if cap]
+
+
 def active():
     return _ACTIVE
 
@@ -65,8 +101,23 @@ def timing():
         _ACTIVE = prev
 
 
+@contextlib.contextmanager
+def stamping(device):
+    """StampTimer active (for a capture): the regions issued meanwhile are stamped."""
+    global _ACTIVE
+    prev, _ACTIVE = _ACTIVE, StampTimer(device)
+    try:
+        yield _ACTIVE
+    finally:
+        _ACTIVE = prev
+
+
 def region(name: str, nbytes: int):
     t = _ACTIVE
-    if t is None or torch.cuda.is_current_stream_capturing():
+    if t is None:
+        return contextlib.nullcontext()
+    if isinstance(t, StampTimer):
+        return t.region(name, nbytes)
+    if torch.cuda.is_current_stream_capturing():
         return contextlib.nullcontext()
     return t.region(name, nbytes)

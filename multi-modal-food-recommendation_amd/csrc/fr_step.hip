@@ -103,3 +103,27 @@ extern "C" int fr_reg_combine_bwd(const float* d_g, int nb, float B, float w, fl
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
+
+// ---- device wall-clock stamps (measurement): one single-lane kernel writes the constant-rate
+// wall clock (s_memrealtime) with a vector store; stream order puts it after everything issued
+// before it and before everything after, so two stamps bracket the kernels between them -- also
+// inside a captured HIP graph, where timing events cannot be recorded (bench.py's roofline pass)
+namespace {
+__global__ void stamp_kernel(int64_t* out) {
+  if (threadIdx.x == 0) out[threadIdx.x] = (int64_t)wall_clock64();
+}
+}  // namespace
+
+extern "C" int fr_stamp(int64_t* d_slot, void* stream) {
+  FR_REQUIRE(d_slot, "null stamp slot");
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), d_slot);
+  FR_LAUNCH_CHECK();
+  return FR_OK;
+}
+
+extern "C" int64_t fr_stamp_hz() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+  return (int64_t)khz * 1000;
+}
