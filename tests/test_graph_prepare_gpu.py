@@ -85,3 +85,42 @@ def test_unrolled_replay_never_wraps_the_lazy_ring(cuda):
         torch.use_deterministic_algorithms(det0)
     for k in out[0]:
         np.testing.assert_allclose(out[1][k].numpy(), out[0][k].numpy(), rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_stamp_timer_inside_a_graph(cuda):
+    """profiling.StampTimer (fr_stamp wall-clock stamps around a region, the roofline pass's timing
+    inside a graph replay): a region captured in a graph reports a positive duration close to the
+    same kernel's event-timed duration outside the graph; regions issued outside the capture are not
+    reported."""
+    from FoodRec.engine import profiling
+    x = torch.randn(1 << 25, device=cuda)
+    y = torch.empty_like(x)
+    for _ in range(3):
+        torch.mul(x, 2.0, out=y)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        torch.mul(x, 2.0, out=y)
+    e1.record()
+    torch.cuda.synchronize()
+    eager_us = e0.elapsed_time(e1) / 10 * 1e3
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with profiling.stamping(cuda) as st:
+        with torch.cuda.stream(side):
+            with profiling.region("warm", 0):  # eager: stamped, not reported
+                torch.mul(x, 2.0, out=y)
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(g):
+            with profiling.region("mul", 8 * x.numel()):
+                torch.mul(x, 2.0, out=y)
+    assert st.hz > 0
+    durs = []
+    for _ in range(5):
+        g.replay()
+        got = st.read()
+        assert [n for n, _, _ in got] == ["mul"]
+        durs.append(got[0][1])
+    med = sorted(durs)[2]
+    assert 0.5 * eager_us < med < 2.0 * eager_us + 20.0, (med, eager_us)
