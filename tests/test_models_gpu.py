@@ -159,11 +159,13 @@ def test_mirror_gradient_training_matches_reference(cuda):
             assert abs(got[k] - v) <= 1e-3, ("mg", k, got[k], v)
 
 
-def test_healthrec_graphed_lazy_equals_eager_dense(cuda):
+@pytest.mark.parametrize("drop", [0.0, 0.5])
+def test_healthrec_graphed_lazy_equals_eager_dense(cuda, drop):
     """The HealthRec step bench.py times (captured graph, DeviceFeed batch gather, lazy row Adam with
     the side-stream catch-up, automatic flushes of a small history ring) against the eager step with
     the every-row Adam, over 2 epochs of 24 steps (B = 32: 23 graph replays + the ragged eager
-    batch per epoch), attention dropout 0.  Both runs are made run-to-run reproducible (config
+    batch per epoch), attention dropout 0 and the bench's 0.5 (the replayed graph must draw the
+    same per-step encoder keep-masks as the eager steps: device counters advance alike).  Both runs are made run-to-run reproducible (config
     ``deterministic``: owner-slot BPR scatter; torch's deterministic index_add_): Adam turns last-bit
     noise in near-zero gradients into +-lr steps, so atomics alone would make any two runs differ.
     Per-epoch loss sums and every parameter and Adam moment after the epochs (flushed) agree to
@@ -175,7 +177,7 @@ def test_healthrec_graphed_lazy_equals_eager_dense(cuda):
     det0 = torch.are_deterministic_algorithms_enabled()
     torch.use_deterministic_algorithms(True)
     try:
-        _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed)
+        _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed, drop)
     finally:
         torch.use_deterministic_algorithms(det0)
     (la, sa, oa, ma), (lb, sb, ob, mb) = runs
@@ -188,10 +190,10 @@ def test_healthrec_graphed_lazy_equals_eager_dense(cuda):
                 torch.testing.assert_close(ob.state[pb][s_], oa.state[pa][s_], rtol=1e-6, atol=1e-9, msg=(k, s_))
 
 
-def _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed):
+def _graphed_vs_eager_runs(runs, Trainer, TripleSampler, get_model, init_seed, drop=0.0):
     for graphed in (False, True):
         cfg = tiny_config("CIKM_Model", True, train_batch_size=32, cuda_graph=graphed, cuda_graph_warmup=2,
-                          lazy_row_adam=graphed, deterministic=True)
+                          lazy_row_adam=graphed, deterministic=True, attention_probs_dropout_prob=drop)
         data = tiny_data(cfg)
         init_seed(999)
         model = get_model("CIKM_Model")(cfg, data).to(cfg["device"])
