@@ -784,6 +784,10 @@ __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, 
 // workspace: Hn [V][b][d] f32, nrm [V][b] f32, part (m,s) [P][JS][m] f32x2, lse [P][m] f32,
 //            P [P][JS][m][d] f32 (bwd), rowsum [P][ceil(m/4)] f64
 constexpr int NCE_JS = 8;
+// the backward's product operand from a transposed copy of the j tile (true) or row-major dword reads
+constexpr bool kNceBwdT = false;
+// independent accumulator chains of the logits' MFMA products
+constexpr int kNceChains = 1;
 
 struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; double* rowsum; };
 
@@ -852,12 +856,16 @@ __global__ __launch_bounds__(256) void nce_normalize_kernel(Views vw, int V, int
   for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < rows;
        r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
     const float* H = vw.x[r / b] + (r % b) * d;
+    // d <= 128 (nce_check): this lane's columns lane, lane + 64 held in registers
+    const float h0 = lane < d ? H[lane] : 0.f, h1 = lane + 64 < d ? H[lane + 64] : 0.f;
     float s = 0.f;
-    for (int k = lane; k < d; k += 64) s = fmaf(H[k], H[k], s);
+    if (lane < d) s = fmaf(h0, h0, s);
+    if (lane + 64 < d) s = fmaf(h1, h1, s);
     s = group_sum<64>(s);
     const float nr = sqrtf(s);
     const float den = fmaxf(nr, 1e-12f);
-    for (int k = lane; k < d; k += 64) ws.Hn[r * d + k] = H[k] / den;
+    if (lane < d) ws.Hn[r * d + lane] = h0 / den;
+    if (lane + 64 < d) ws.Hn[r * d + lane + 64] = h1 / den;
     if (lane == 0) ws.nrm[r] = nr;
   }
 }
@@ -921,18 +929,27 @@ __global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, flo
   const int64_t i = (int64_t)blockIdx.x * 4 + wv;
   double v = 0.0;
   if (i < m) {
+    // every load of the row issued up front (the split partials and both rows of the positive logit)
+    const float* hi = nce_row(ws, pt, p, b, d, i);
+    const float* hj = nce_row(ws, pt, p, b, d, nce_partner(i, b));
+    const float h0 = lane < d ? hi[lane] : 0.f, j0 = lane < d ? hj[lane] : 0.f;
+    const float h1 = lane + 64 < d ? hi[lane + 64] : 0.f, j1 = lane + 64 < d ? hj[lane + 64] : 0.f;
+    float2 qs[NCE_JS];
+#pragma unroll
+    for (int s = 0; s < NCE_JS; ++s)
+      qs[s] = s < js_count ? ws.part[((int64_t)p * NCE_JS + s) * m + i] : make_float2(0.f, 0.f);
     float M = -INFINITY, S = 0.f;
-    for (int s = 0; s < js_count; ++s) {
-      const float2 q = ws.part[((int64_t)p * NCE_JS + s) * m + i];
-      if (q.y == 0.f) continue;
+#pragma unroll
+    for (int s = 0; s < NCE_JS; ++s) {
+      const float2 q = qs[s];
+      if (s >= js_count || q.y == 0.f) continue;
       if (q.x > M) { S = S * expf(M - q.x) + q.y; M = q.x; }
       else S += q.y * expf(q.x - M);
     }
     const float lse = M + logf(S);
-    const float* hi = nce_row(ws, pt, p, b, d, i);
-    const float* hj = nce_row(ws, pt, p, b, d, nce_partner(i, b));
     double dp = 0.0;
-    for (int k = lane; k < d; k += 64) dp += (double)hi[k] * (double)hj[k];
+    if (lane < d) dp += (double)h0 * (double)j0;
+    if (lane + 64 < d) dp += (double)h1 * (double)j1;
     const float dot = (float)group_sum_d<64>(dp);
     if (lane == 0) {
       ws.lse[(int64_t)p * m + i] = lse;
@@ -948,25 +965,40 @@ __global__ __launch_bounds__(256) void nce_finalize_kernel(int64_t b, int d, flo
 // once); out[0] = their fp32 sum in pair order (Python's sum() over the pairs' fp32 losses)
 __global__ __launch_bounds__(1024) void nce_sum_kernel(int64_t b, int n_pairs, NceWS ws, float weight, float* out,
                                                       float* out_pairs) {
-  __shared__ double red[16];
+  __shared__ double red[16 * 16];
   const int64_t nparts = nce_nparts(2 * b);
-  float total = 0.f;
-  for (int p = 0; p < n_pairs; ++p) {
-    double loc = 0.0;
-    for (int64_t k = threadIdx.x; k < nparts; k += blockDim.x) loc += ws.rowsum[(int64_t)p * nparts + k];
-    loc = group_sum_d<64>(loc);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = loc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
+  // every pair's strided partial sums first (their loads in flight together), then the per-pair
+  // reductions in the same order as before
+  double locs[16];
+  const bool first = (int64_t)threadIdx.x < nparts;
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+    locs[p] = 0.0 + (p < n_pairs && first ? ws.rowsum[(int64_t)p * nparts + threadIdx.x] : 0.0);
+  if (nparts > (int64_t)blockDim.x) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+      if (p < n_pairs)
+        for (int64_t k = threadIdx.x + blockDim.x; k < nparts; k += blockDim.x) locs[p] += ws.rowsum[(int64_t)p * nparts + k];
+  }
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    if (p < n_pairs) {  // (uniform)
+      const double loc = group_sum_d<64>(locs[p]);
+      if ((threadIdx.x & 63) == 0) red[16 * p + (threadIdx.x >> 6)] = loc;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float total = 0.f;
+    for (int p = 0; p < n_pairs; ++p) {
       double s = 0.0;
-      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[16 * p + w];
       const float lp = (float)(s / ((double)b * (double)b));
       if (out_pairs) out_pairs[p] = lp;
       total = p == 0 ? lp : total + lp;
     }
+    out[0] = weight * total;  // (weight 1: the sum itself, exactly)
   }
-  if (threadIdx.x == 0) out[0] = weight * total;  // (weight 1: the sum itself, exactly)
 }
 
 // dHn_i = (1/tau) sum_j W_ij Hn_j,  W_ij = dl_ij + dl_ji,  dl_ij = (P_ij - [j==p(i)]) * g / b^2  (pair blockIdx.z)
@@ -1086,6 +1118,25 @@ __global__ __launch_bounds__(256) void nce_lse_mfma_kernel(int64_t b, float inv_
   }
 }
 
+// the logits of a 16 x 16 sub-block: sum over k of the lane's A row (LDS, k-permuted float4 chunks)
+// times its B fragments (registers), on kNceChains independent accumulators (k chunks dealt round
+// robin) added at the end
+template <int D>
+__device__ __forceinline__ f32x4 nce_logits(const float* __restrict__ arow, const float4 (&bfr)[D / 16]) {
+  f32x4 g[kNceChains];
+#pragma unroll
+  for (int c = 0; c < kNceChains; ++c) g[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < D / 16; ++kc) {
+    const float4 a = *reinterpret_cast<const float4*>(arow + 16 * kc);
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) g[(4 * kc + mm) % kNceChains] = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g[(4 * kc + mm) % kNceChains]);
+  }
+#pragma unroll
+  for (int c = 1; c < kNceChains; ++c) g[0] = g[0] + g[c];
+  return g[0];
+}
+
 // Round 5 form of the InfoNCE log-sum-exp: the logits transposed per 16 x 16 sub-block (as
 // nce_bwd_mfma2_kernel), S^T = Hn_j Hn_b^T, so each lane owns ONE b row (its B fragments in registers
 // for the whole kernel: half the LDS reads of nce_lse_mfma_kernel) and keeps one online (max, sum)
@@ -1112,19 +1163,30 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
   const float s2 = inv_tau * kLog2e;
   const int mi = (int)m, gi32 = (int)gi;
   float mx = -INFINITY, sm = 0.f;
+  // the j tile's rows loaded into registers one tile ahead (in flight during the previous tile)
+  constexpr int D4 = D / 4, NPF = T * D4 / 256;
+  float4 pf[NPF];
+  auto load_tile = [&](int64_t jt) {
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+      pf[u] = jt * T + r < m ? reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4]
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  if (js < nt) load_tile(js);
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
-    nce_tile_r(ws, pt, p, b, D, jt * T, Bt);
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+      *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = pf[u];
+    }
     __syncthreads();
+    if (jt + gridDim.y < nt) load_tile(jt + gridDim.y);
 #pragma unroll
     for (int jc = 0; jc < T / 16; ++jc) {
-      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kc = 0; kc < D / 16; ++kc) {
-        const float4 a = *reinterpret_cast<const float4*>(Bt + (16 * jc + i) * LD + 16 * kc + 4 * h);
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) g = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g);
-      }
+      const f32x4 g = nce_logits<D>(Bt + (16 * jc + i) * LD + 4 * h, bfr);
       float l2[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1226,7 +1288,7 @@ template <int D>
 __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
   constexpr int LD = D + 4, LDT = T + 4;
   __shared__ __attribute__((aligned(16))) float Bt[T * LD];    // j rows, row-major (logits' A operand)
-  __shared__ __attribute__((aligned(16))) float BtT[D * LDT];  // the same tile transposed (product's B operand)
+  __shared__ __attribute__((aligned(16))) float BtT[kNceBwdT ? D * LDT : 4];  // the same tile transposed (product's B operand)
   __shared__ float lse_j[T];
   const int64_t m = 2 * b, nt = (m + T - 1) / T;
   const int it = blockIdx.x, js = blockIdx.y, p = blockIdx.z;
@@ -1262,10 +1324,12 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (jt * T + r < m) v = reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4];
         *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = v;
-        BtT[(4 * k4 + 0) * LDT + r] = v.x;
-        BtT[(4 * k4 + 1) * LDT + r] = v.y;
-        BtT[(4 * k4 + 2) * LDT + r] = v.z;
-        BtT[(4 * k4 + 3) * LDT + r] = v.w;
+        if constexpr (kNceBwdT) {
+          BtT[(4 * k4 + 0) * LDT + r] = v.x;
+          BtT[(4 * k4 + 1) * LDT + r] = v.y;
+          BtT[(4 * k4 + 2) * LDT + r] = v.z;
+          BtT[(4 * k4 + 3) * LDT + r] = v.w;
+        }
       }
       if (threadIdx.x < T) {
         const int64_t gj = jt * T + threadIdx.x;
@@ -1276,13 +1340,7 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
     const int j0 = (int)jt * T;
 #pragma unroll
     for (int jc = 0; jc < T / 16; ++jc) {
-      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kc = 0; kc < D / 16; ++kc) {
-        const float4 a = *reinterpret_cast<const float4*>(Bt + (16 * jc + i) * LD + 16 * kc + 4 * h);
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) g = mfma4(comp4(a, mm), comp4(bfr[kc], mm), g);
-      }
+      const f32x4 g = nce_logits<D>(Bt + (16 * jc + i) * LD + 4 * h, bfr);
       float wv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1295,7 +1353,13 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
       }
 #pragma unroll
       for (int c = 0; c < D / 16; ++c) {
-        const float4 bx = *reinterpret_cast<const float4*>(BtT + (16 * c + i) * LDT + 16 * jc + 4 * h);
+        float4 bx;
+        if constexpr (kNceBwdT) {
+          bx = *reinterpret_cast<const float4*>(BtT + (16 * c + i) * LDT + 16 * jc + 4 * h);
+        } else {  // four conflict-free dword reads of the row-major tile (banks i + 16 h + 4 q)
+          const float* bc = Bt + (16 * jc + 4 * h) * LD + 16 * c + i;
+          bx = make_float4(bc[0], bc[LD], bc[2 * LD], bc[3 * LD]);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[c] = mfma4(wv[q], comp4(bx, q), acc[c]);
       }
@@ -1331,10 +1395,17 @@ __global__ __launch_bounds__(256) void nce_bwd_finalize_kernel(Views vw, int V, 
     auto gsum = [&](int k) {
       float q = 0.f;
       for (int p = 0; p < pt.n_pairs; ++p) {
-        if (pt.pa[p] == v)
-          for (int s = 0; s < js_count; ++s) q += ws.P[(((int64_t)p * NCE_JS + s) * m + r) * d + k];
-        if (pt.pb[p] == v)
-          for (int s = 0; s < js_count; ++s) q += ws.P[(((int64_t)p * NCE_JS + s) * m + b + r) * d + k];
+        for (int side = 0; side < 2; ++side) {
+          if ((side ? pt.pb[p] : pt.pa[p]) != v) continue;
+          // the pair's split partials of this row: loads issued together, added in split order
+          const float* src = ws.P + ((int64_t)p * NCE_JS * m + (side ? b + r : r)) * d + k;
+          float x[NCE_JS];
+#pragma unroll
+          for (int s = 0; s < NCE_JS; ++s) x[s] = s < js_count ? src[(int64_t)s * m * d] : 0.f;
+#pragma unroll
+          for (int s = 0; s < NCE_JS; ++s)
+            if (s < js_count) q += x[s];
+        }
       }
       return q * scale;
     };
