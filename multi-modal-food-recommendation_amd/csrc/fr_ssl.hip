@@ -66,6 +66,30 @@ __device__ __forceinline__ void load_tile_r(const float* __restrict__ X, int64_t
   }
 }
 
+// load_tile_r for a compile-time d and block size: every thread's loads issued before its first LDS
+// store (one global round trip per tile instead of one per strided step); NTILES tiles at once
+template <int D, int NT, int NTILES = 1>
+__device__ __forceinline__ void load_tiles_rc(const float* const (&X)[NTILES], int64_t n, const int64_t (&r0)[NTILES],
+                                              float* const (&Xr)[NTILES]) {
+  constexpr int D4 = D / 4, NST = T * D4 / NT, LD = D + 4;
+  static_assert(T * D4 % NT == 0, "tile chunks must divide over the block");
+  float4 v[NTILES][NST];
+#pragma unroll
+  for (int t = 0; t < NTILES; ++t)
+#pragma unroll
+    for (int u = 0; u < NST; ++u) {
+      const int idx = threadIdx.x + NT * u, r = idx / D4, k4 = idx - r * D4;
+      v[t][u] = r0[t] + r < n ? reinterpret_cast<const float4*>(X[t] + (r0[t] + r) * D)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+  for (int t = 0; t < NTILES; ++t)
+#pragma unroll
+    for (int u = 0; u < NST; ++u) {
+      const int idx = threadIdx.x + NT * u, r = idx / D4, k4 = idx - r * D4;
+      *reinterpret_cast<float4*>(Xr[t] + r * LD + 4 * k4) = v[t][u];
+    }
+}
+
 // 4x4 Gram block of thread (ti,tj): g[x][y] = <row 4ti+x of A, row 4tj+y of B>
 __device__ __forceinline__ void gram4x4(const float* At, const float* Bt, int d, int ti, int tj,
                                         float g[4][4]) {
@@ -351,8 +375,7 @@ __global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n
 #pragma unroll
   for (int a = 0; a < V; ++a) {
     __syncthreads();
-    load_tile_r(v.x[a], n, D, (int64_t)it * T, At);
-    load_tile_r(v.x[a], n, D, (int64_t)jt * T, Bt);
+    load_tiles_rc<D, 256, 2>({v.x[a], v.x[a]}, n, {(int64_t)it * T, (int64_t)jt * T}, {At, Bt});
     __syncthreads();
     row_sq_r<D>(At, ra);
     if (threadIdx.x >= T && threadIdx.x < 2 * T) {
@@ -416,23 +439,32 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
   const int lane = threadIdx.x;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   double mv[V];
+  {  // every view's row sums: the loads of 8 j tiles of all views in flight together, added in j order
+    double sv[V];
 #pragma unroll
-  for (int a = 0; a < V; ++a) {
-    double s = 0.0;
+    for (int a = 0; a < V; ++a) sv[a] = 0.0;
     if (i < n) {
-      const float* r = ws.row + (int64_t)a * nt * n + i;
       int64_t jt = 0;
       for (; jt + 8 <= nt; jt += 8) {
-        float x[8];
+        float x[V][8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = r[(jt + u) * n];
+        for (int a = 0; a < V; ++a)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += (double)x[u];
+          for (int u = 0; u < 8; ++u) x[a][u] = ws.row[(int64_t)a * nt * n + i + (jt + u) * n];
+#pragma unroll
+        for (int a = 0; a < V; ++a)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sv[a] += (double)x[a][u];
       }
-      for (; jt < nt; ++jt) s += (double)r[jt * n];
+      for (; jt < nt; ++jt)
+#pragma unroll
+        for (int a = 0; a < V; ++a) sv[a] += (double)ws.row[(int64_t)a * nt * n + i + jt * n];
     }
-    mv[a] = i < n ? s / (double)n : 0.0;
-    if (i < n) ws.mean[(int64_t)a * n + i] = mv[a];
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      mv[a] = i < n ? sv[a] / (double)n : 0.0;
+      if (i < n) ws.mean[(int64_t)a * n + i] = mv[a];
+    }
   }
   double* bp = ws.bpart + (int64_t)blockIdx.x * DCOR_BP;
 #pragma unroll
@@ -449,11 +481,19 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
     }
   const int64_t nblk = nt * nt, per = (nblk + gridDim.x - 1) / gridDim.x;
   const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+  double lS[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) lS[k] = 0.0;
+  for (int64_t blk = b0 + lane; blk < b1; blk += 64) {
+    double x[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) x[k] = ws.S[blk * NP + k];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) lS[k] += x[k];
+  }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    double lS = 0.0;
-    for (int64_t blk = b0 + lane; blk < b1; blk += 64) lS += ws.S[blk * NP + k];
-    const double t = group_sum_d<64>(lS);
+    const double t = group_sum_d<64>(lS[k]);
     if (lane == 0) bp[MAXV + MAXP + k] = t;
   }
 }
@@ -469,7 +509,15 @@ __global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int
   const bool used = t < DCOR_BP && (t < V || (t >= MAXV && t < MAXV + NP) || (t >= MAXV + MAXP && t < MAXV + MAXP + NP));
   if (used) {
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += ws.bpart[(int64_t)b * DCOR_BP + t];
+    int b = 0;
+    for (; b + 8 <= nb; b += 8) {  // 8 loads in flight, added in block order
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = ws.bpart[(int64_t)(b + u) * DCOR_BP + t];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += x[u];
+    }
+    for (; b < nb; ++b) s += ws.bpart[(int64_t)b * DCOR_BP + t];
     tot[t] = s;
   }
   __syncthreads();
@@ -652,7 +700,7 @@ __global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n
   double coef[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) coef[k] = ws.coef[k];
-  for (int a = 0; a < V; ++a) load_tile_r(v.x[a], n, D, (int64_t)it * T, Ai[a]);
+  for (int a = 0; a < V; ++a) load_tiles_rc<D, DB_NT>({v.x[a]}, n, {(int64_t)it * T}, {Ai[a]});
   if (threadIdx.x < T) {
     const int64_t gi = (int64_t)it * T + threadIdx.x;
     for (int a = 0; a < V; ++a) mi[a][threadIdx.x] = gi < n ? ws.mean[(int64_t)a * n + gi] : 0.0;
@@ -677,7 +725,7 @@ __global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n
 #pragma unroll
     for (int a = 0; a < V; ++a) {
       __syncthreads();
-      load_tile_r(v.x[a], n, D, jt * T, Bt);
+      load_tiles_rc<D, DB_NT>({v.x[a]}, n, {jt * T}, {Bt});
       __syncthreads();
       if (threadIdx.x < T) {
         float sq = 0.f;
@@ -724,7 +772,7 @@ __global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n
         }
         rowm[a][q] += group_sum<16>(rs);
       }
-      load_tile_r(v.x[a], n, D, jt * T, Bt);
+      load_tiles_rc<D, DB_NT>({v.x[a]}, n, {jt * T}, {Bt});
       __syncthreads();
       wx_mfma<D, NC>(Ms, Bt, acc[a], rw, NC * ch);
     }
@@ -766,13 +814,24 @@ __global__ __launch_bounds__(256) void dcor_bwd_finalize_kernel(Views v, int V, 
     const int64_t rem = t - (int64_t)a * n * d;
     const int64_t i = rem / d;
     const int k = (int)(rem - i * d);
-    float rm = 0.f, p = 0.f;
-    for (int s = 0; s < js_count; ++s) {
-      rm += ws.rowm[((int64_t)s * V + a) * n + i];
-      p += ws.P[(((int64_t)s * V + a) * n + i) * d + k];
+    // every split's partials loaded before the sums (added in split order)
+    float rms[DCOR_JS], ps[DCOR_JS];
+#pragma unroll
+    for (int s = 0; s < DCOR_JS; ++s) {
+      rms[s] = s < js_count ? ws.rowm[((int64_t)s * V + a) * n + i] : 0.f;
+      ps[s] = s < js_count ? ws.P[(((int64_t)s * V + a) * n + i) * d + k] : 0.f;
     }
-    const float val = gg * (v.x[a][i * d + k] * rm - p);
-    v.dx[a][i * d + k] = overwrite ? val : v.dx[a][i * d + k] + val;
+    const float xv = v.x[a][i * d + k];
+    const float dv = overwrite ? 0.f : v.dx[a][i * d + k];
+    float rm = 0.f, p = 0.f;
+#pragma unroll
+    for (int s = 0; s < DCOR_JS; ++s)
+      if (s < js_count) {
+        rm += rms[s];
+        p += ps[s];
+      }
+    const float val = gg * (xv * rm - p);
+    v.dx[a][i * d + k] = overwrite ? val : dv + val;
   }
 }
 
@@ -1317,12 +1376,21 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
   for (int c = 0; c < D / 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
-    {  // stage the j tile both ways, and its rows' lse
-      const int d4 = D / 4;
-      for (int idx = threadIdx.x; idx < T * d4; idx += blockDim.x) {
-        const int r = idx / d4, k4 = idx - r * d4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (jt * T + r < m) v = reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4];
+    {  // stage the j tile (every thread's loads issued before its first store), and its rows' lse
+      constexpr int D4 = D / 4, NST = T * D4 / 256;
+      float4 vs[NST];
+#pragma unroll
+      for (int u = 0; u < NST; ++u) {
+        const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+        vs[u] = jt * T + r < m ? reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4]
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const int64_t gj = jt * T + threadIdx.x;
+      const float lj = threadIdx.x < T && gj < m ? lse[gj] * kLog2e : 0.f;
+#pragma unroll
+      for (int u = 0; u < NST; ++u) {
+        const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+        const float4 v = vs[u];
         *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = v;
         if constexpr (kNceBwdT) {
           BtT[(4 * k4 + 0) * LDT + r] = v.x;
@@ -1331,10 +1399,7 @@ __global__ __launch_bounds__(256) void nce_bwd_mfma2_kernel(int64_t b, float inv
           BtT[(4 * k4 + 3) * LDT + r] = v.w;
         }
       }
-      if (threadIdx.x < T) {
-        const int64_t gj = jt * T + threadIdx.x;
-        lse_j[threadIdx.x] = gj < m ? lse[gj] * kLog2e : 0.f;
-      }
+      if (threadIdx.x < T) lse_j[threadIdx.x] = lj;
     }
     __syncthreads();
     const int j0 = (int)jt * T;

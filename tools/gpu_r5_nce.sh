@@ -9,7 +9,7 @@ BASE=${BASE:-ncehead}
 mkdir -p $OUT
 cd $R
 timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_wide_gpu.py tests/test_models_gpu.py -m gpu -x -q \
-  -k "infonce or nce or PRICAI" --timeout 200 --timeout-method thread > $OUT/nce_tests_$TAG.log 2>&1 \
+  -k "infonce or nce or dcor or PRICAI" --timeout 200 --timeout-method thread > $OUT/nce_tests_$TAG.log 2>&1 \
   || { grep -E "FAILED|Error|assert" $OUT/nce_tests_$TAG.log | head; tail -20 $OUT/nce_tests_$TAG.log; exit 1; }
 tail -1 $OUT/nce_tests_$TAG.log
 for k in 1 2; do
