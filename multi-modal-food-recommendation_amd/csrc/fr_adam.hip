@@ -283,12 +283,19 @@ __device__ __forceinline__ float2 lazy_scalars(const AdamHyper& h, int64_t st) {
 }
 
 __global__ void adam_lazy_inc_kernel(LazyArgs a, AdamHyper h, const int32_t* skip) {
-  if (skip && *skip) return;
   const int t = threadIdx.x;
   if (t >= a.n) return;
+  // the skip flag, the step and the device lr loaded together (one memory round trip, not three)
+  const int32_t sk = skip ? *skip : 0;
   const int64_t st = a.step[t][0] + 1;
+  AdamHyper hh = h;
+  if (h.d_lr) {
+    hh.lr = h.d_lr[0];
+    hh.d_lr = nullptr;
+  }
+  if (sk) return;
   a.step[t][0] = st;
-  const float2 e = lazy_scalars(h, st);
+  const float2 e = lazy_scalars(hh, st);
   float* hp = a.hist[t] + 4 * (st % a.cap);  // kHist = 4: neg_step, bc2_sqrt, RN64(1 / bc2_sqrt)
   hp[0] = e.x;
   hp[1] = e.y;

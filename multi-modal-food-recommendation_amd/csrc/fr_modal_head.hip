@@ -110,9 +110,18 @@ __global__ __launch_bounds__(NT) void modal_head_fwd_kernel(HeadArgs a) {
 // fixed-order wave sum each (one wave)
 __device__ __forceinline__ void head_final(const HeadArgs& a, int nblk, int j) {
   float sbce = 0.f, scos = 0.f;
-  for (int b = j; b < nblk; b += 64) {
-    sbce += a.part[2 * b];
-    scos += a.part[2 * b + 1];
+  for (int b0 = j; b0 < nblk; b0 += 256) {  // four blocks' partials in flight, added in block order
+    float2 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = b0 + 64 * u < nblk ? make_float2(a.part[2 * (b0 + 64 * u)], a.part[2 * (b0 + 64 * u) + 1])
+                                : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (b0 + 64 * u < nblk) {
+        sbce += x[u].x;
+        scos += x[u].y;
+      }
   }
   const float tb = wsum(sbce), tc = wsum(scos);
   if (j != 0) return;
@@ -311,10 +320,27 @@ struct LossFin {
 
 __global__ __launch_bounds__(256) void loss_finalize_kernel(HeadArgs a, int nblk, LossFin f) {
   __shared__ float red[2][256];
+  // thread 0's bookkeeping operands (independent of the sums) and every thread's first norm partials
+  // are loaded before anything waits: the launch's memory round trips overlap instead of chaining
+  int64_t cv[8];
+  double av[4];
+  float mfv = 0.f;
+  const bool book = threadIdx.x == 0 && f.npart && f.acc;
+  if (book) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = i < f.nc ? f.ctr[i][0] : 0;
+    mfv = f.mf[0];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) av[i] = f.accumulate ? f.acc[i] : 0.0;
+  }
+  float s0 = 0.f, s1 = 0.f;
+  if (f.npart && (int)threadIdx.x < f.nnblk) {
+    s0 = f.npart[2 * threadIdx.x];
+    s1 = f.npart[2 * threadIdx.x + 1];
+  }
   if (a.part && threadIdx.x < 64) head_final(a, nblk, threadIdx.x);  // out[0..2], written by thread 0
   if (!f.npart) return;
-  float s0 = 0.f, s1 = 0.f;
-  for (int b = threadIdx.x; b < f.nnblk; b += 256) {
+  for (int b = threadIdx.x + 256; b < f.nnblk; b += 256) {
     s0 += f.npart[2 * b];
     s1 += f.npart[2 * b + 1];
   }
@@ -334,12 +360,15 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(HeadArgs a, int nblk
   f.nrm[1] = n1;
   const float reg = f.w * (f.emb3[0] + (n0 + n1) / f.B);
   f.reg[0] = reg;
-  if (!f.acc) return;
-  for (int i = 0; i < f.nc; ++i) f.ctr[i][0] += 1;
-  const float v[4] = {f.mf[0], a.out[0], a.out[1], reg};  // this thread wrote out[0..1] above
+  if (!book) return;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < f.nc) f.ctr[i][0] = cv[i] + 1;  // (distinct counters: checked by the host)
+  const float v[4] = {mfv, a.out[0], a.out[1], reg};  // this thread wrote out[0..1] above
   float s = 0.f;
+#pragma unroll
   for (int i = 0; i < 4; ++i) {
-    f.acc[i] = f.accumulate ? f.acc[i] + (double)v[i] : (double)v[i];
+    f.acc[i] = f.accumulate ? av[i] + (double)v[i] : (double)v[i];
     s = i == 0 ? v[i] : s + v[i];
   }
   if (s != s) f.nan[0] |= 1;
@@ -413,6 +442,7 @@ extern "C" int fr_healthrec_loss_finalize(const float* d_head_partials, int64_t 
   f.acc = d_acc; f.accumulate = accumulate; f.nan = d_nan; f.loss = d_loss;
   for (int i = 0; i < n_counters; ++i) {
     FR_REQUIRE(d_counters[i] != nullptr, "null counter");
+    for (int j = 0; j < i; ++j) FR_REQUIRE(d_counters[j] != d_counters[i], "counters must be distinct");
     f.ctr[i] = d_counters[i];
   }
   f.nc = n_counters;

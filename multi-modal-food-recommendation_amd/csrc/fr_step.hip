@@ -26,11 +26,27 @@ struct Parts {
 __global__ void step_book_kernel(Parts parts, double* __restrict__ acc, int accumulate, int32_t* __restrict__ nan_flag,
                                  float* __restrict__ loss_out) {
   if (threadIdx.x != 0) return;
-  for (int i = 0; i < parts.nc; ++i) parts.ctr[i][0] += 1;
+  // every operand loaded before the first store (the counters are distinct: checked by the host), so
+  // the launch is one memory round trip instead of a chain of read-modify-writes
+  int64_t cv[kMaxCounters];
+  float pv[kMaxParts];
+  double av[kMaxParts];
+#pragma unroll
+  for (int i = 0; i < kMaxCounters; ++i) cv[i] = i < parts.nc ? parts.ctr[i][0] : 0;
+#pragma unroll
+  for (int i = 0; i < kMaxParts; ++i) {
+    pv[i] = i < parts.n ? parts.p[i][0] : 0.f;
+    av[i] = i < parts.n && accumulate ? acc[i] : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxCounters; ++i)
+    if (i < parts.nc) parts.ctr[i][0] = cv[i] + 1;
   float s = 0.f;  // sum(losses) in fp32, left to right, as Python's sum over fp32 tensors
-  for (int i = 0; i < parts.n; ++i) {
-    const float v = parts.p[i][0];
-    acc[i] = accumulate ? acc[i] + (double)v : (double)v;
+#pragma unroll
+  for (int i = 0; i < kMaxParts; ++i) {
+    if (i >= parts.n) break;
+    const float v = pv[i];
+    acc[i] = accumulate ? av[i] + (double)v : (double)v;
     s = i == 0 ? v : s + v;
   }
   if (s != s) nan_flag[0] |= 1;
@@ -52,6 +68,7 @@ extern "C" int fr_step_book(const float* const* d_parts, int n, double* d_acc, i
   p.n = n;
   for (int i = 0; i < n_counters; ++i) {
     FR_REQUIRE(d_counters[i] != nullptr, "null counter");
+    for (int j = 0; j < i; ++j) FR_REQUIRE(d_counters[j] != d_counters[i], "counters must be distinct");
     p.ctr[i] = d_counters[i];
   }
   p.nc = n_counters;
