@@ -49,6 +49,7 @@ constexpr int kThreads = kWaves * 64;
 constexpr int kUsersPerWG = kWaves * 32;
 constexpr int kTile = 32;      // items per staged tile
 constexpr int kKMax = 32;      // largest k
+constexpr int kAppendDepth = 2;  // APPEND's register stages of item tiles (1 or 2)
 
 template <typename T, int D, int NB = 1>
 struct Cfg {
@@ -225,33 +226,33 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
     ssrc[c] = reinterpret_cast<const char*>(It) + ((i_lo + row) * ldi) * (int64_t)sizeof(T) + cc * 16;
   }
   const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
-#define FR_LOAD_TILE(T_)                                                                            \
+#define FR_LOAD_TILE(T_, S_)                                                                        \
   _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
     if constexpr (MODE == kAppend) {                                                                \
       const int64_t item = i_lo + (int64_t)(T_) * C::TILE + srow[c];                                \
-      stg[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)(T_) * tile_bytes)  \
+      S_[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)(T_) * tile_bytes)   \
                            : make_uint4(0, 0, 0, 0);                                                \
     } else {                                                                                        \
       const int x = tid + c * kThreads;                                                             \
-      stg[c] = make_uint4(0, 0, 0, 0);                                                              \
+      S_[c] = make_uint4(0, 0, 0, 0);                                                               \
       if (x < C::TILE * C::CPR) {                                                                   \
         const int row = x / C::CPR, cc = x % C::CPR;                                                \
         const int64_t item = i_lo + (int64_t)(T_) * C::TILE + row;                                  \
         if (item < i_hi)                                                                            \
-          stg[c] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(It) +              \
+          S_[c] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(It) +               \
                                                    (item * ldi) * (int64_t)sizeof(T) + cc * 16);    \
       }                                                                                             \
     }                                                                                               \
   }
-#define FR_STORE_TILE(BUF_)                                                                         \
+#define FR_STORE_TILE(BUF_, S_)                                                                     \
   _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
     if constexpr (MODE == kAppend) {                                                                \
-      if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + sdst[c]) = stg[c]; \
+      if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + sdst[c]) = S_[c];  \
     } else {                                                                                        \
       const int x = tid + c * kThreads;                                                             \
       if (x < C::TILE * C::CPR) {                                                                   \
         const int row = x / C::CPR, cc = x % C::CPR;                                                \
-        *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + (row * C::CPR + swz<T, D>(row, cc)) * 16) = stg[c]; \
+        *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + (row * C::CPR + swz<T, D>(row, cc)) * 16) = S_[c];  \
       }                                                                                             \
     }                                                                                               \
   }
@@ -264,14 +265,23 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   for (int s = 0; s < NAH; ++s) aoff[s] = a_off<T, D>(r, h, s);
 #define FR_AOFF(S_) (MODE == kAppend ? aoff[(MODE == kAppend) ? (S_) : 0] : a_off<T, D>(r, h, (S_)))
 
-  uint4 stg[C::CH];
+  // register stages of the item tiles: APPEND keeps two (the global loads of tile t + 3 are issued
+  // after tile t's barrier and have two tiles of MFMA work to land in), LIST one (its key lists
+  // hold the registers)
+  constexpr int DEPTH = MODE == kAppend ? kAppendDepth : 1;
+  uint4 stgA[C::CH], stgB[DEPTH == 2 ? C::CH : 1];
   if (n_tiles > 0) {
-    FR_LOAD_TILE(0)
-    FR_STORE_TILE(0)
+    FR_LOAD_TILE(0, stgA)
+    FR_STORE_TILE(0, stgA)
   }
   __syncthreads();
-  if (n_tiles > 1) { FR_LOAD_TILE(1) }
-  for (int t = 0; t < n_tiles; ++t) {
+  if (n_tiles > 1) { FR_LOAD_TILE(1, stgA) }
+  if constexpr (DEPTH == 2) {
+    if (n_tiles > 2) { FR_LOAD_TILE(2, stgB) }
+  }
+  // one tile: its scores and selection from LDS buffer t & 1, then the next tile (in `cur`) into the
+  // other buffer, and `cur` refilled DEPTH + 1 tiles ahead
+  auto tile_step = [&](const int t, uint4 (&cur)[C::CH]) {
     // ---- scores of this tile on the matrix cores (NB independent 32-item blocks)
     const char* abuf = smem + (t & 1) * C::STAGE;
     f32x16 acc[NB];
@@ -372,10 +382,18 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
         }
       }
     }
-    // ---- next tile into the other buffer; prefetch the one after
-    if (t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1) }
+    // ---- next tile into the other buffer; prefetch DEPTH + 1 tiles ahead into the freed stage
+    if (t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
     __syncthreads();
-    if (t + 2 < n_tiles) { FR_LOAD_TILE(t + 2) }
+    if (t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
+  };
+  if constexpr (DEPTH == 2) {
+    for (int t = 0; t < n_tiles; t += 2) {
+      tile_step(t, stgA);
+      if (t + 1 < n_tiles) tile_step(t + 1, stgB);
+    }
+  } else {
+    for (int t = 0; t < n_tiles; ++t) tile_step(t, stgA);
   }
 #undef FR_LOAD_TILE
 #undef FR_STORE_TILE
