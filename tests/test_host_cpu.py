@@ -345,3 +345,20 @@ def test_reserve_replays_flushes_before_the_ring_could_wrap():
     assert calls == [3] and opt._lazy_pending == 0
     with pytest.raises(ValueError):
         opt.reserve_replays(7)  # more steps per replay than the ring can ever hold
+
+
+def test_bookkeeping_launches_refuse_repeated_counters():
+    """fr_step_book / fr_healthrec_loss_finalize load every counter before advancing any (one
+    memory round trip), so a counter named twice would advance once: the ABI refuses it before
+    any launch (host-side check; no device needed)."""
+    import ctypes
+    from FoodRec.engine import native
+    lib = native.lib()
+    parts = (ctypes.c_void_p * 1)(0x1000)
+    twice = (ctypes.c_void_p * 2)(0x2000, 0x2000)
+    with pytest.raises(native.EngineError, match="distinct"):
+        native.check(lib.fr_step_book(parts, 1, 0x3000, 0, 0x4000, twice, 2, None, None), "fr_step_book")
+    with pytest.raises(native.EngineError, match="distinct"):
+        native.check(lib.fr_healthrec_loss_finalize(0x1000, 16, 0.5, 1.0, 1.0, 0x1100, 0x1200, 64, 0x1300, 512.0,
+                                                    1e-3, 0x1400, 0x1500, 0x1600, 0x1700, 0, 0x1800, twice, 2,
+                                                    None, None), "fr_healthrec_loss_finalize")
