@@ -29,7 +29,7 @@ def _one_step(cuda, late, monkeypatch):
 
     def spy(**kw):
         seen["pending"] = seen.get("pending", 0) + len(ops._PENDING_DRAINS)
-        orig(**kw)
+        return orig(**kw)
     monkeypatch.setattr(ops, "run_pending_drains", spy)
     tr.train_step(batch, 0, st)
     torch.cuda.synchronize()
