@@ -847,6 +847,8 @@ constexpr int NCE_JS = 8;
 constexpr bool kNceBwdT = false;
 // independent accumulator chains of the logits' MFMA products
 constexpr int kNceChains = 1;
+// the views normalised inside the log-sum-exp kernel's row staging (no normalize launch)
+constexpr bool kNceFusedNorm = true;
 
 struct NceWS { float* Hn; float* nrm; float2* part; float* lse; float* P; double* rowsum; };
 
@@ -1200,8 +1202,8 @@ __device__ __forceinline__ f32x4 nce_logits(const float* __restrict__ arow, cons
 // nce_bwd_mfma2_kernel), S^T = Hn_j Hn_b^T, so each lane owns ONE b row (its B fragments in registers
 // for the whole kernel: half the LDS reads of nce_lse_mfma_kernel) and keeps one online (max, sum)
 // over the j values it holds; the 4 lane groups of a row are merged at the end in a fixed order.
-template <int D>
-__global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws) {
+template <int D, bool FUSED>
+__global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv_tau, PairTab pt, NceWS ws, Views vw) {
   constexpr int LD = D + 4;
   __shared__ __attribute__((aligned(16))) float Bt[T * LD];
   const int64_t m = 2 * b, nt = (m + T - 1) / T;
@@ -1209,8 +1211,70 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
   const int64_t gi = (int64_t)it * T + 16 * w + i;
   const bool ivalid = gi < m;
+  constexpr int D4 = D / 4, NPF = T * D4 / 256;
+  // FUSED: the rows are read raw (the views) and normalised where they are staged.  Staging layout:
+  // a thread holds 4 adjacent float4 chunks of one row, a row spans LPR adjacent lanes; its sum of
+  // squares is the thread's fmaf chain then a DPP group sum (the same order in every workgroup),
+  // Hn = x * (1 / max(|x|, 1e-12)).  The j == 0 split's workgroups also write their i rows' Hn and
+  // norms for the finalize and the backward (no normalize launch)
+  constexpr int LPR = D4 / 4 >= 1 ? D4 / 4 : 1, RPP = 256 / LPR, NPASS = (T + RPP - 1) / RPP;
+  auto raw_row = [&](int64_t r) -> const float* {
+    const int v = r < b ? pt.pa[p] : pt.pb[p];
+    return vw.x[v] + (r < b ? r : r - b) * D;
+  };
+  auto fused_load = [&](int64_t r0, float4 (&fv)[NPASS][4]) {
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int r = ps * RPP + (int)threadIdx.x / LPR, c0 = ((int)threadIdx.x % LPR) * 4;
+      const bool ok = r < T && r0 + r < m;
+      const float4* src = ok ? reinterpret_cast<const float4*>(raw_row(r0 + r)) + c0 : nullptr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fv[ps][q] = ok && c0 + q < D4 ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // normalise and store to Bt; owner: also write Hn / norms of rows r0 + r (global row index of pair p)
+  auto fused_store = [&](int64_t r0, float4 (&fv)[NPASS][4], bool owner) {
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int r = ps * RPP + (int)threadIdx.x / LPR, c0 = ((int)threadIdx.x % LPR) * 4;
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ss = fmaf(fv[ps][q].x, fv[ps][q].x, fmaf(fv[ps][q].y, fv[ps][q].y, fmaf(fv[ps][q].z, fv[ps][q].z, fmaf(fv[ps][q].w, fv[ps][q].w, ss))));
+      ss = group_sum<LPR>(ss);
+      const float nr = sqrtf(ss);
+      const float inv = 1.f / fmaxf(nr, 1e-12f);
+      if (r < T) {
+        const int64_t gr = r0 + r;
+        float* hn_g = nullptr;
+        if (owner && gr < m) {
+          const int v = gr < b ? pt.pa[p] : pt.pb[p];
+          const int64_t vr = (int64_t)v * b + (gr < b ? gr : gr - b);
+          hn_g = ws.Hn + vr * D;
+          if (c0 == 0) ws.nrm[vr] = nr;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (c0 + q >= D4) continue;
+          const float4 x = fv[ps][q];
+          const float4 hn = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
+          *reinterpret_cast<float4*>(Bt + r * LD + 4 * (c0 + q)) = hn;
+          if (hn_g) reinterpret_cast<float4*>(hn_g)[c0 + q] = hn;
+        }
+      }
+    }
+  };
   float4 bfr[D / 16];
-  {
+  if constexpr (FUSED) {
+    // the i tile staged normalised in Bt first, the B fragments read back from it
+    float4 fi[NPASS][4];
+    fused_load((int64_t)it * T, fi);
+    fused_store((int64_t)it * T, fi, js == 0);
+    __syncthreads();
+#pragma unroll
+    for (int kc = 0; kc < D / 16; ++kc)
+      bfr[kc] = *reinterpret_cast<const float4*>(Bt + (16 * w + i) * LD + 16 * kc + 4 * h);
+  } else {
     const float* row = ivalid ? nce_row(ws, pt, p, b, D, gi) : nullptr;
 #pragma unroll
     for (int kc = 0; kc < D / 16; ++kc)
@@ -1223,23 +1287,31 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
   const int mi = (int)m, gi32 = (int)gi;
   float mx = -INFINITY, sm = 0.f;
   // the j tile's rows loaded into registers one tile ahead (in flight during the previous tile)
-  constexpr int D4 = D / 4, NPF = T * D4 / 256;
-  float4 pf[NPF];
+  float4 pf[FUSED ? 1 : NPF];
+  float4 fj[FUSED ? NPASS : 1][4];
   auto load_tile = [&](int64_t jt) {
+    if constexpr (FUSED) {
+      fused_load(jt * T, fj);
+    } else {
 #pragma unroll
-    for (int u = 0; u < NPF; ++u) {
-      const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
-      pf[u] = jt * T + r < m ? reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4]
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < NPF; ++u) {
+        const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+        pf[u] = jt * T + r < m ? reinterpret_cast<const float4*>(nce_row(ws, pt, p, b, D, jt * T + r))[k4]
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   };
   if (js < nt) load_tile(js);
   for (int64_t jt = js; jt < nt; jt += gridDim.y) {
     __syncthreads();
+    if constexpr (FUSED) {
+      fused_store(jt * T, fj, false);
+    } else {
 #pragma unroll
-    for (int u = 0; u < NPF; ++u) {
-      const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
-      *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = pf[u];
+      for (int u = 0; u < NPF; ++u) {
+        const int idx = threadIdx.x + 256 * u, r = idx / D4, k4 = idx - r * D4;
+        *reinterpret_cast<float4*>(Bt + r * LD + 4 * k4) = pf[u];
+      }
     }
     __syncthreads();
     if (jt + gridDim.y < nt) load_tile(jt + gridDim.y);
@@ -1656,8 +1728,14 @@ extern "C" int64_t fr_infonce_multi_workspace(int n_views, int64_t b, int d, int
 
 // the log-sum-exp kernel of the MFMA forms: 1 = the round-5 transposed form, 2 = the round-4 one (A/B)
 template <int D>
-static auto lse_kern() -> void (*)(int64_t, float, PairTab, NceWS) {
-  return g_ssl_mfma == 2 ? nce_lse_mfma_kernel<D> : nce_lse_mfma2_kernel<D>;
+static void launch_lse(dim3 grid, hipStream_t s, int64_t b, float inv_tau, const PairTab& pt, const NceWS& w,
+                       const Views& v, bool fused) {
+  if (g_ssl_mfma == 2)
+    hipLaunchKernelGGL(nce_lse_mfma_kernel<D>, grid, dim3(256), 0, s, b, inv_tau, pt, w);
+  else if (fused)
+    hipLaunchKernelGGL((nce_lse_mfma2_kernel<D, true>), grid, dim3(256), 0, s, b, inv_tau, pt, w, v);
+  else
+    hipLaunchKernelGGL((nce_lse_mfma2_kernel<D, false>), grid, dim3(256), 0, s, b, inv_tau, pt, w, v);
 }
 
 static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int d, const int32_t* pairs, int n_pairs,
@@ -1675,19 +1753,30 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
   pt.n_pairs = n_pairs;
   for (int k = 0; k < n_pairs; ++k) { pt.pa[k] = pairs[2 * k]; pt.pb[k] = pairs[2 * k + 1]; }
   const float inv_tau = 1.f / tau;
-  const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div((int64_t)n_views * b, 4), 4096);
-  hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, v, n_views, b, d, w);
-  FR_LAUNCH_CHECK();
+  // the round-5 MFMA kernels normalise the views in their staging when every view is in a pair
+  // (each view's rows are then some workgroup's i rows, whose Hn / norms it writes)
+  bool every_view_paired = true;
+  for (int a = 0; a < n_views; ++a) {
+    bool in = false;
+    for (int k = 0; k < n_pairs; ++k) in |= pt.pa[k] == a || pt.pb[k] == a;
+    every_view_paired &= in;
+  }
+  const bool fused = kNceFusedNorm && g_ssl_mfma == 1 && every_view_paired;
+  if (!fused) {
+    const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div((int64_t)n_views * b, 4), 4096);
+    hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, v, n_views, b, d, w);
+    FR_LAUNCH_CHECK();
+  }
   const int64_t nt = fr::ceil_div(m, T);
   const int js = (int)std::min<int64_t>(NCE_JS, nt);
   const size_t lds = (size_t)(2 * d * PADT) * 4;
   const dim3 grid((unsigned)nt, (unsigned)js, (unsigned)n_pairs);
   if (g_ssl_mfma) {
     switch (d) {
-      case 16: hipLaunchKernelGGL(lse_kern<16>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      case 32: hipLaunchKernelGGL(lse_kern<32>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      case 64: hipLaunchKernelGGL(lse_kern<64>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
-      default: hipLaunchKernelGGL(lse_kern<128>(), grid, dim3(256), 0, s, b, inv_tau, pt, w); break;
+      case 16: launch_lse<16>(grid, s, b, inv_tau, pt, w, v, fused); break;
+      case 32: launch_lse<32>(grid, s, b, inv_tau, pt, w, v, fused); break;
+      case 64: launch_lse<64>(grid, s, b, inv_tau, pt, w, v, fused); break;
+      default: launch_lse<128>(grid, s, b, inv_tau, pt, w, v, fused); break;
     }
   } else {
     hipLaunchKernelGGL(nce_lse_tiles_kernel, grid, dim3(256), lds, s, b, d, inv_tau, pt, w);

@@ -430,6 +430,26 @@ def test_infonce_pairs(cuda, b, ssl_kernels):
     assert torch.equal(single, got.detach())
 
 
+def test_infonce_pairs_unpaired_view(cuda, ssl_kernels):
+    """A view that no pair holds: the launches fall back to the separate normalize pass (the
+    round-5 log-sum-exp kernel normalises only the rows of paired views while staging them); the
+    loss matches the float64 oracle and the unpaired view's gradient is exactly zero."""
+    from FoodRec.engine import ops
+    b, d, pairs = 200, 64, ((0, 2),)
+    g = torch.Generator().manual_seed(7)
+    V = [torch.randn(b, d, generator=g, dtype=torch.float64, requires_grad=True) for _ in range(3)]
+    ref = sum(O.cl_loss(torch.cat([V[a], V[c]]), 0.5) for a, c in pairs)
+    ref.backward()
+    Vd = [v.detach().float().to(cuda).requires_grad_(True) for v in V]
+    got = ops.infonce_pairs(Vd, pairs, 0.5)
+    got.backward()
+    assert abs(got.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    for k in (0, 2):
+        np.testing.assert_allclose(Vd[k].grad.cpu().numpy(), V[k].grad.numpy(), rtol=1e-4,
+                                   atol=1e-4 * float(V[k].grad.abs().max()))
+    assert Vd[1].grad is None or not Vd[1].grad.any()
+
+
 def test_fused_adam_matches_torch(cuda):
     from FoodRec.engine.optim import FusedAdam
     g = torch.Generator().manual_seed(1)
