@@ -45,7 +45,7 @@ def _args():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="healthrec_allrecipes", choices=["healthrec_allrecipes"])
     ap.add_argument("--batch", type=int, default=512)
-    ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes/launch of the dominant kernel from rocprofv3 PMC (profiles/)")
@@ -996,25 +996,30 @@ def config4(device, batches=(512, 8192), steps=5, warmup=2, spmm_iters=10, cpu=T
         out["cpu_baseline"] = config4_cpu(adj, U, P, batches)
     del trainer, model, g, adj
     torch.cuda.empty_cache()
-    bm = out["spmm_beyond_mall"] = spmm_beyond_mall(device)
-    # the DRAM-honest figure leads: on the 1M-item graph the 256 MB item block of X is Infinity-Cache
-    # sized, so the no-reuse byte model (and even the PMC beyond-L2 bytes, which count cache hits)
-    # implies more than the ~6.3 TB/s HBM can deliver; on the 4M-item graph (1 GiB item block) the
-    # gathers miss the cache and the PMC bytes equal the model's -- that rate is the DRAM-level one
+    bm = out["spmm_dram_uniform"] = spmm_dram_uniform(device)
+    # the DRAM figure comes from a graph whose gathers miss the Infinity Cache: on config 4's 1M-item
+    # graph the 256 MB item block is MALL-sized, and even the PMC beyond-L2 bytes (FETCH_SIZE counts
+    # MALL hits, MI355X_MICROARCH.md) are partly cache hits -- so this graph's rate is reported as
+    # cache-assisted / beyond-L2, never as DRAM.  spmm_dram_uniform: 10M users x 16M uniformly popular
+    # items (4 GB item block, no hot rows): min(model, PMC) bytes / launch time is a DRAM rate.
     sp = out["spmm"]
     dram_bytes = min(bm["bytes_per_launch"], bm.get("traffic") or bm["bytes_per_launch"])
     dram_gbps = dram_bytes / bm["avg_launch_ms"] / 1e6
     sp.update({"achieved_gbps_cache_assisted": sp["achieved_gbps"], "frac_cache_assisted": sp["frac"],
                "achieved_gbps_dram": round(dram_gbps, 1), "frac_dram": round(dram_gbps / HBM_PEAK_GBPS, 4),
                "frac": round(dram_gbps / HBM_PEAK_GBPS, 4),
-               "frac_note": "frac = frac_dram: the same kernel on the 10M x 4M graph (spmm_beyond_mall), min(model, "
-                            "PMC) bytes / launch time; *_cache_assisted: this graph's no-reuse byte model, whose item "
-                            "block (256 MB) the Infinity Cache holds -- not a DRAM rate"})
+               "frac_note": "frac = frac_dram: the same kernel on a 10M x 16M uniform-popularity graph "
+                            "(spmm_dram_uniform: 4 GB item block, every gather beyond the Infinity Cache), "
+                            "min(model, PMC) bytes / launch time; *_cache_assisted: this graph's no-reuse byte "
+                            "model, whose Zipf-hot item rows the Infinity Cache holds; frac_beyond_l2: PMC bytes "
+                            "that left the L2 (DRAM + Infinity-Cache hits) -- neither is a DRAM rate"})
+    if sp["frac_dram"] * HBM_PEAK_GBPS > 6300:
+        sp["frac_note"] += "; WARNING: frac_dram above the guide's 6.29 TB/s streaming ceiling"
     return out
 
 
 def spmm_traffic(key, ms):
-    """PMC bytes per launch of the config-4 SpMM (``key``: config4 | beyond_mall) from the newest
+    """PMC bytes per launch of the config-4 SpMM (``key``: config4 | dram_uniform) from the newest
     profiles/r*/pmc_spmm10m.json (tools/pmc_spmm10m.py: FETCH_SIZE x 2 + WRITE_SIZE, bytes that left
     the L2 -- DRAM plus Infinity Cache hits) and the rate they imply at this run's launch time
     (``frac_beyond_l2``: that rate / the 8 TB/s peak -- DRAM plus Infinity-Cache hits)."""
@@ -1031,16 +1036,16 @@ def spmm_traffic(key, ms):
             "frac_beyond_l2": round(t / ms / 1e6 / HBM_PEAK_GBPS, 4), "traffic_source": os.path.relpath(files[-1], ROOT)}
 
 
-def spmm_beyond_mall(device, iters=5):
-    """The config-4 SpMM with every gathered table far beyond the 256 MB Infinity Cache: 10M users x
-    4M items (the item block of X is 1 GiB, the user block 2.56 GB), ~200M interactions, d=64 fp32 --
-    the byte model then counts DRAM traffic, not MALL hits (the 1M-item table of config 4 is the
-    MALL's size)."""
+def spmm_dram_uniform(device, iters=5):
+    """The config-4 SpMM with every gather beyond the 256 MB Infinity Cache: 10M users x 16M
+    uniformly popular items (uniform_bipartite: config 4's user degrees, ~200M interactions; the item
+    block of X is 4 GB, the user block 2.56 GB, no hot rows), d=64 fp32 -- the byte model then counts
+    DRAM traffic (checked against the PMC beyond-L2 bytes of tools/spmm10m.py --uniform)."""
     import torch
     from FoodRec.engine import ops
-    from FoodRec.utils.interaction_graph import InteractionGraph
-    U, I, d = 10_000_000, 4_000_000, 64
-    g = InteractionGraph(U, I, 20.0, seed=1, device=device)
+    from FoodRec.utils.interaction_graph import InteractionGraph, uniform_bipartite
+    U, I, d = 10_000_000, 16_000_000, 64
+    g = InteractionGraph(U, I, 20.0, seed=1, device=device, pairs=uniform_bipartite(U, I, 20.0, 1, device))
     adj = g.adj
     X = torch.randn(U + I, d, device=device)
     Y = torch.empty_like(X)
@@ -1054,9 +1059,10 @@ def spmm_beyond_mall(device, iters=5):
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / iters
     b = ops.spmm_bytes(adj, d, 1)
-    out = {"graph": "synthetic U=10M I=4M E=%d (nnz=%d)" % (g.n_edges, adj.nnz), "item_table_mb": I * d * 4 / 2**20,
-           "avg_launch_ms": round(ms, 3), "bytes_per_launch": b, "achieved_gbps": round(b / ms / 1e6, 1),
-           "peak": HBM_PEAK_GBPS, "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), **spmm_traffic("beyond_mall", ms)}
+    out = {"graph": "synthetic uniform U=10M I=16M E=%d (nnz=%d)" % (g.n_edges, adj.nnz),
+           "item_table_mb": I * d * 4 / 2**20, "avg_launch_ms": round(ms, 3), "bytes_per_launch": b,
+           "achieved_gbps": round(b / ms / 1e6, 1), "peak": HBM_PEAK_GBPS,
+           "frac": round(b / ms / 1e6 / HBM_PEAK_GBPS, 4), **spmm_traffic("dram_uniform", ms)}
     del X, Y, g, adj
     torch.cuda.empty_cache()
     return out
@@ -1160,13 +1166,14 @@ def config4_sharded(device, world, rank, batches=(512, 8192), steps=5, warmup=2)
 
 
 def cpu_baseline(args):
-    """Time the oracle's CPU restatement of the same step on this host (bounded sample)."""
+    """Time the oracle's CPU restatement of the same step on this host, as BASELINE.md section 3 states
+    it: every host core (torch.set_num_threads(os.cpu_count())), ``--cpu-baseline-steps`` (20) timed
+    steps after 3 warm-ups.  The per-GPU share of the host (the GPU box gives one GPU's job 16 CPUs,
+    OMP_NUM_THREADS=16) is timed beside it on a shorter sample (``per_gpu_share``)."""
     import torch
     from oracle import cpu_backend
-    # the GPU box gives one GPU's job a 16-CPU share of the host (OMP_NUM_THREADS=16 there); the
-    # host's total core count is reported beside it
-    threads = _cpu_threads()
-    torch.set_num_threads(threads)
+    all_cores = os.cpu_count() or 1
+    share = _cpu_threads()
     with cpu_backend.installed():
         from FoodRec.common.trainer import Trainer
         from FoodRec.engine.sampler import TripleSampler
@@ -1176,18 +1183,38 @@ def cpu_baseline(args):
         feats = trainer._features()
         state = trainer.new_step_state()
         it = sampler.epoch()
-        u, p, n = next(it)
-        trainer.train_step(feats.batch(u, p, n), 0, state)  # warm-up
-        t0 = time.perf_counter()
+        step = [0]
+
+        def run(threads, warm, k):
+            torch.set_num_threads(threads)
+            for _ in range(warm):
+                u, p, n = next(it)
+                trainer.train_step(feats.batch(u, p, n), step[0], state)
+                step[0] += 1
+            t0 = time.perf_counter()
+            for _ in range(k):
+                u, p, n = next(it)
+                trainer.train_step(feats.batch(u, p, n), step[0], state)
+                step[0] += 1
+            return time.perf_counter() - t0
+
         k = max(1, args.cpu_baseline_steps)
-        for i in range(k):
-            u, p, n = next(it)
-            trainer.train_step(feats.batch(u, p, n), 1 + i, state)
-        dt = time.perf_counter() - t0
-    return {"value": round(args.batch * k / dt, 2), "unit": "triples/s", "cores": threads, "kind": "port",
-            "host_cores_total": os.cpu_count(),
-            "sample": f"{k} HealthRec training steps (B={args.batch}) of the torch-CPU oracle after 1 warm-up",
-            "ms_per_step": round(dt / k * 1e3, 1)}
+        dt = run(all_cores, 3, k)
+        ks = 4
+        dts = run(share, 1, ks)
+    torch.set_num_threads(share)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"value": round(args.batch * k / dt, 2), "unit": "triples/s", "cores": all_cores, "kind": "port",
+            "host_cores_total": all_cores, "cores_in_affinity": affinity,
+            "sample": f"{k} HealthRec training steps (B={args.batch}) of the torch-CPU oracle after 3 warm-ups, "
+                      f"torch.set_num_threads({all_cores})",
+            "ms_per_step": round(dt / k * 1e3, 1),
+            "per_gpu_share": {"value": round(args.batch * ks / dts, 2), "cores": share,
+                              "ms_per_step": round(dts / ks * 1e3, 1),
+                              "sample": f"{ks} steps after 1 warm-up, torch.set_num_threads({share})"}}
 
 
 def config1(device, steps=50, warmup=5, cpu=True, cpu_steps=20):

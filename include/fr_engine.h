@@ -853,6 +853,15 @@ int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col
                                    int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
                                    const int64_t* d_blocks, int64_t n_blocks, const int64_t* d_split_rows,
                                    int64_t n_split_rows, void* stream);
+/* Rows per block of the sparse-upstream kernel (its LDS row accumulator): a plan block of more rows,
+ * rows outside [0, n_rows) or an edge range outside its rows is refused by the kernel (the block
+ * computes nothing) and flagged in the library's plan status. */
+int fr_spmm_sparse_block_rows(void);
+/* The plan status the sparse-upstream kernel sets (0: every block was valid; bit 0: a block of more
+ * than fr_spmm_sparse_block_rows() rows or outside the adjacency; bit 1: a block whose edge range
+ * leaves its rows), cleared when clear != 0.  Synchronous (a device symbol read): not inside graph
+ * capture. */
+int fr_spmm_plan_status(int clear);
 
 /* fr_graph_bpr_finish: the tail of HealthRec's fused propagation + BPR backward (engine
  * ops.graph_bpr), after both propagation backwards have written dUe (user_embedding's gradient)

@@ -900,45 +900,58 @@ class Trainer(AbstractTrainer):
         ckpt = os.path.join(ckroot, ckpt_name)
         sampler = TripleSampler(dataset, self.config["train_batch_size"], self.device)
         saved_once = False
-        for epoch_idx in range(self.start_epoch, self.epochs):
-            t0 = time()
-            self.model.pre_epoch_processing()
-            train_loss, _, _ = self._train_epoch(sampler, epoch_idx)
-            if torch.is_tensor(train_loss):
-                break
-            for group in self.optimizer.param_groups:
-                self.logger.info("======lr: %f" % group["lr"])
-            self.lr_scheduler.step()
-            if isinstance(self.optimizer, FusedAdam):
-                self.optimizer.sync_lr()
-            self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
-            t1 = time()
-            post = self.model.post_epoch_processing()
-            if verbose:
-                self.logger.info(self._generate_train_loss_output(epoch_idx, t0, t1, train_loss))
-                if post is not None:
-                    self.logger.info(post)
-            if (epoch_idx + 1) % self.eval_step == 0:
-                v0 = time()
-                valid_score, valid_result = self._valid_by_user_epoch(is_test=False)
-                self.best_valid_score, self.cur_step, stop_flag, update_flag = early_stopping(
-                    valid_score, self.best_valid_score, self.cur_step, max_step=self.stopping_step,
-                    bigger=self.valid_metric_bigger)
-                v1 = time()
-                if verbose:
-                    self.logger.info("epoch %d evaluating [time: %.2fs, valid_score: %f]" % (epoch_idx, v1 - v0, valid_score))
-                    self.logger.info("valid result: \n" + dict2str(valid_result))
-                if update_flag:
-                    torch.save(self.model.state_dict(), ckpt)
-                    saved_once = True
-                    if verbose:
-                        self.logger.info("██ " + str(self.config["model"]) + "--Best validation results updated!!!")
-                    self.best_valid_result = valid_result
-                if stop_flag:
-                    if verbose:
-                        self.logger.info("+++++Finished training, best eval result in epoch %d" %
-                                         (epoch_idx - self.cur_step * self.eval_step))
+        finished = False
+        try:
+            for epoch_idx in range(self.start_epoch, self.epochs):
+                t0 = time()
+                self.model.pre_epoch_processing()
+                train_loss, _, _ = self._train_epoch(sampler, epoch_idx)
+                if torch.is_tensor(train_loss):
                     break
+                for group in self.optimizer.param_groups:
+                    self.logger.info("======lr: %f" % group["lr"])
+                self.lr_scheduler.step()
+                if isinstance(self.optimizer, FusedAdam):
+                    self.optimizer.sync_lr()
+                self.train_loss_dict[epoch_idx] = sum(train_loss) if isinstance(train_loss, tuple) else train_loss
+                t1 = time()
+                post = self.model.post_epoch_processing()
+                if verbose:
+                    self.logger.info(self._generate_train_loss_output(epoch_idx, t0, t1, train_loss))
+                    if post is not None:
+                        self.logger.info(post)
+                if (epoch_idx + 1) % self.eval_step == 0:
+                    v0 = time()
+                    valid_score, valid_result = self._valid_by_user_epoch(is_test=False)
+                    self.best_valid_score, self.cur_step, stop_flag, update_flag = early_stopping(
+                        valid_score, self.best_valid_score, self.cur_step, max_step=self.stopping_step,
+                        bigger=self.valid_metric_bigger)
+                    v1 = time()
+                    if verbose:
+                        self.logger.info("epoch %d evaluating [time: %.2fs, valid_score: %f]" % (epoch_idx, v1 - v0, valid_score))
+                        self.logger.info("valid result: \n" + dict2str(valid_result))
+                    if update_flag:
+                        torch.save(self.model.state_dict(), ckpt)
+                        saved_once = True
+                        if verbose:
+                            self.logger.info("██ " + str(self.config["model"]) + "--Best validation results updated!!!")
+                        self.best_valid_result = valid_result
+                    if stop_flag:
+                        if verbose:
+                            self.logger.info("+++++Finished training, best eval result in epoch %d" %
+                                             (epoch_idx - self.cur_step * self.eval_step))
+                        break
+            finished = True
+        finally:
+            # early stop, the NaN break or an exception: the sampler's prefetch thread is joined here,
+            # so no host draw outlives fit() (a grid search reseeds before its next run)
+            if finished:
+                sampler.close()
+            else:
+                try:
+                    sampler.close()
+                except Exception:  # (the exception already raised is the one to report)
+                    pass
         if saved_once:
             self.model.load_state_dict(torch.load(ckpt, weights_only=True))
         _, test_result = self._valid_by_user_epoch(is_test=True)

@@ -91,6 +91,69 @@ def spmm_bytes(adj: Adjacency, d: int, n_rowio: int = 1, elem: int = 4) -> int:
     return 8 * (n + 1) + 8 * adj.nnz + elem * d * adj.nnz + elem * d * n * n_rowio
 
 
+def mean_degree(adj: Adjacency, row: int = 0) -> float:
+    """Mean edges per row of the side of ``row`` (a bipartite adjacency's two sides differ: users vs
+    items, items vs ingredients), else of the whole adjacency."""
+    n, split = adj.shape[0], adj.bipartite_split
+    if split is None or not 0 < split < n:
+        return adj.nnz / max(n, 1)
+    if row < split:
+        return adj.nnz_below_split / split
+    return (adj.nnz - adj.nnz_below_split) / (n - split)
+
+
+def rows_bytes(adj: Adjacency, rows, d: int = 64, n_rowio: int = 1, elem: int = 4) -> int:
+    """Expected HBM bytes of a row-list SpMM (only the listed rows computed): per listed row its rowptr
+    pair (16), its edges' col/val (8) and gathered rows (elem d) at the mean degree of its side
+    (the degrees of the listed rows are on the device), and elem d per output written / addend read.
+    ``rows``: [(ids, offset), ...] or a row count (at side 0)."""
+    if isinstance(rows, int):
+        segs = [(rows, 0)]
+    else:
+        segs = [(int(ids.numel()), int(off)) for ids, off in rows]
+    tot = 0.0
+    for n, off in segs:
+        deg = mean_degree(adj, off)
+        tot += n * (16 + deg * (8 + elem * d) + elem * d * n_rowio)
+    return int(tot)
+
+
+def frontier_rows(ui_adj: Adjacency, B: int, n_items: int) -> int:
+    """Expected size of the RI frontier (fr_rows_frontier: the items adjacent to B batch users plus the
+    2B batch items; the count is on the device): min(I, B * mean user degree + 2B)."""
+    return int(min(n_items, B * mean_degree(ui_adj, 0) + 2 * B))
+
+
+def sparse_upstream_bytes(adj: Adjacency, d: int = 64, elem: int = 4) -> int:
+    """Scan + write bytes of a sparse-upstream SpMM (spmm_sparse_upstream / _rect / _blocks): rowptr,
+    every edge's col/val, every output row written.  The gathers at marked columns (hits) are left
+    out: their count is on the device (a lower bound)."""
+    n = adj.shape[0]
+    return 8 * (n + 1) + 8 * adj.nnz + elem * d * n
+
+
+def scatter_upstream_bytes(adj: Adjacency, rows, d: int = 64, elem: int = 4) -> int:
+    """fr_spmm_scatter_upstream: per listed row its X row read, per edge col/val (8) and an atomic
+    read-modify-write of the target row (2 elem d), at the listed side's mean degree."""
+    tot = 0.0
+    for ids, off in rows:
+        n = int(ids.numel())
+        tot += n * (16 + elem * d + mean_degree(adj, int(off)) * (8 + 2 * elem * d))
+    return int(tot)
+
+
+def bpr_bwd_bytes(B: int, d: int = 64, elem: int = 4) -> int:
+    """fr_bpr_bwd(_ex): per triple row (3B: u, p, n) its id (8), the propagated and the ego rows read
+    (2 elem d) and the gradient row's read-modify-write (2 elem d)."""
+    return 3 * B * (8 + 4 * elem * d)
+
+
+def bpr_finish_bytes(B: int, d: int = 64, elem: int = 4) -> int:
+    """fr_graph_bpr_finish: per triple row its id and mask byte (9), the ego row read (elem d) and the
+    gradient row's read-modify-write (2 elem d)."""
+    return 3 * B * (9 + 3 * elem * d)
+
+
 def _spmm_call_bf16(adj, X, d, plan, ws, s, Y1, Y2, alpha, A1, beta1, A2, beta2, ld):
     rc = native.lib().fr_spmm_csr_bf16(
         adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], ctypes.byref(plan),
@@ -380,7 +443,7 @@ class _PropagateLoViews(torch.autograd.Function):
             if d_lo is None:
                 d_lo = torch.zeros_like(item_w)  # (no view carried a gradient: the rows alone)
             z = pad if k == 0 else None
-            with profiling.region("bpr_bwd", 0):
+            with profiling.region("bpr_bwd", bpr_finish_bytes(int(u.numel()))):
                 native.check(native.lib().fr_graph_bpr_finish(
                     None, 0, user_w.data_ptr(), 64, item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(),
                     int(u.numel()), 64, _f(w_emb), native.ptr(ge), None, d_lo.data_ptr(), native.ptr(z),
@@ -726,7 +789,8 @@ def spmm_ex(adj: Adjacency, X, X_hi=None, split=0, Y1=None, Y1_hi=None, Y2=None,
     ws = _ws_for(adj, d, X.device)
     rl = _rowlist(rows) if rows is not None else None
     if nbytes is None:
-        nbytes = spmm_bytes(adj, d, sum(x is not None for x in (Y1, Y2, A1, A2))) if rows is None else 0
+        nio = sum(x is not None for x in (Y1, Y2, A1, A2))
+        nbytes = spmm_bytes(adj, d, nio) if rows is None else rows_bytes(adj, rows, d, nio)
     with profiling.region(region, nbytes):
         native.check(native.lib().fr_spmm_csr_ex(
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, ctypes.byref(plan), int(split),
@@ -796,7 +860,7 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
         raise native.EngineError("spmm_sparse_upstream: bits must be int32 with ceil(rows / 32) words")
     _check_tab("Y2", Y2, Y2_hi, split, N, 64)
     plan = _sparse_plan(adj)
-    with profiling.region(region, 0):
+    with profiling.region(region, sparse_upstream_bytes(adj)):
         if plan is not None:  # heavy rows (config 4's Zipf items): edge-balanced blocks
             _sparse_blocks(adj, False, bits, X, Y2, Y2_hi, split, alpha, X, beta1, plan)
             return
@@ -806,17 +870,52 @@ def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2
             native.stream_of(X)), "fr_spmm_sparse_upstream")
 
 
-SPARSE_BLOCK_ROWS = 64        # rows per block of the sparse-upstream kernel (kSpRows)
+def sparse_block_rows() -> int:
+    """Rows per block of the sparse-upstream kernel: its LDS row accumulator (kSpRows), as the
+    library exports it (fr_spmm_sparse_block_rows) -- never restated by hand."""
+    return int(native.lib().fr_spmm_sparse_block_rows())
+
+
 SPARSE_BLOCK_EDGES = 2048     # edge budget of a plan block (two 1024-edge scan rounds)
 SPARSE_PLAN_TRIGGER = 8192    # use a plan when some uniform 64-row block would scan more edges
 
 
-def sparse_block_plan(rowptr: np.ndarray, rows_per_block=SPARSE_BLOCK_ROWS, edges=SPARSE_BLOCK_EDGES):
+def check_sparse_plan(blocks: np.ndarray, rowptr: np.ndarray, max_rows: int) -> None:
+    """Refuse a sparse-upstream block plan the kernel cannot run: a block of more than ``max_rows``
+    rows (its LDS accumulator), rows outside the adjacency, or an edge range outside the block's rows
+    (a multi-row block must cover its rows' edges exactly; a chunk is one row's sub-range)."""
+    b = np.asarray(blocks, dtype=np.int64).reshape(-1, 4)
+    rp = np.asarray(rowptr, dtype=np.int64)
+    n = rp.shape[0] - 1
+    lo, hi, e0, e1 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
+    bad = (lo < 0) | (hi < lo) | (hi - lo > max_rows) | (hi > n)
+    if bad.any():
+        k = int(np.nonzero(bad)[0][0])
+        raise native.EngineError(f"sparse block plan: block {k} rows [{lo[k]}, {hi[k]}) exceed the kernel's "
+                                 f"{max_rows}-row accumulator or the adjacency's {n} rows")
+    lo_c, hi_c = np.clip(lo, 0, n), np.clip(hi, 0, n)
+    inside = (e0 >= rp[lo_c]) & (e1 <= rp[hi_c]) & (e0 <= e1)
+    chunk = (e0 != rp[lo_c]) | (e1 != rp[hi_c])
+    bad = ~inside | (chunk & (hi - lo != 1))
+    if bad.any():
+        k = int(np.nonzero(bad)[0][0])
+        raise native.EngineError(f"sparse block plan: block {k} edges [{e0[k]}, {e1[k]}) leave rows "
+                                 f"[{lo[k]}, {hi[k]})")
+
+
+def sparse_block_plan(rowptr: np.ndarray, rows_per_block=None, edges=SPARSE_BLOCK_EDGES):
     """Edge-balanced row blocks for the sparse-upstream kernel: (blocks [n, 4] = (row_lo, row_hi,
     edge_lo, edge_hi), split_rows).  Cuts fall every ``rows_per_block`` rows, wherever the running
     edge count crosses a multiple of ``edges``, and around every row of more than ``edges`` edges;
     such a heavy row becomes ceil(deg / edges) chunks (listed in split_rows).  A block of light rows
-    scans at most 2 * edges edges."""
+    scans at most 2 * edges edges.  ``rows_per_block`` defaults to the kernel's exported limit and may
+    not exceed it (check_sparse_plan)."""
+    limit = sparse_block_rows()
+    if rows_per_block is None:
+        rows_per_block = limit
+    if not 0 < rows_per_block <= limit:
+        raise native.EngineError(f"sparse_block_plan: rows_per_block {rows_per_block} exceeds the kernel's "
+                                 f"{limit}-row accumulator")
     rp = np.asarray(rowptr, dtype=np.int64)
     n = rp.shape[0] - 1
     if n <= 0:
@@ -838,7 +937,9 @@ def sparse_block_plan(rowptr: np.ndarray, rows_per_block=SPARSE_BLOCK_ROWS, edge
     e_hi = np.minimum(e_lo + edges, rp[rows + 1])
     chunks = np.stack([rows, rows + 1, e_lo, e_hi], 1)
     blocks = np.concatenate([light, chunks])
-    return blocks[np.argsort(blocks[:, 2], kind="stable")], hr.astype(np.int64)
+    blocks = blocks[np.argsort(blocks[:, 2], kind="stable")]
+    check_sparse_plan(blocks, rp, limit)
+    return blocks, hr.astype(np.int64)
 
 
 def _sparse_plan(adj: Adjacency):
@@ -846,12 +947,12 @@ def _sparse_plan(adj: Adjacency):
     are balanced enough (no block over SPARSE_PLAN_TRIGGER edges).  Built once per adjacency."""
     def make():
         rp = adj.rowptr.cpu().numpy()
-        ends = rp[np.minimum(np.arange(SPARSE_BLOCK_ROWS, rp.shape[0] - 1 + SPARSE_BLOCK_ROWS, SPARSE_BLOCK_ROWS),
-                             rp.shape[0] - 1)]
-        starts = rp[np.arange(0, rp.shape[0] - 1, SPARSE_BLOCK_ROWS)]
+        nb = sparse_block_rows()
+        ends = rp[np.minimum(np.arange(nb, rp.shape[0] - 1 + nb, nb), rp.shape[0] - 1)]
+        starts = rp[np.arange(0, rp.shape[0] - 1, nb)]
         if ends.shape[0] == 0 or int((ends - starts).max()) <= SPARSE_PLAN_TRIGGER:
             return False
-        blocks, split_rows = sparse_block_plan(rp, SPARSE_BLOCK_ROWS, SPARSE_BLOCK_EDGES)
+        blocks, split_rows = sparse_block_plan(rp, nb, SPARSE_BLOCK_EDGES)
         dev = adj.rowptr.device
         return (torch.from_numpy(np.ascontiguousarray(blocks)).to(dev), torch.from_numpy(split_rows).to(dev))
     plan = _persistent(adj, "sparse_plan", make)
@@ -881,7 +982,7 @@ def spmm_scatter_upstream(adj: Adjacency, mask: torch.Tensor, bits: torch.Tensor
     if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32 or mask.numel() < N:
         raise native.EngineError("spmm_scatter_upstream: uint8 mask and int32 bits over the rows")
     _check_tab("Y2", Y2, Y2_hi, split, N, 64)
-    with profiling.region(region, 0):
+    with profiling.region(region, scatter_upstream_bytes(adj, rows)):
         native.check(native.lib().fr_spmm_scatter_upstream(
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, mask.data_ptr(), bits.data_ptr(),
             ctypes.byref(_rowlist(rows)), X.data_ptr(), X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)),
@@ -900,7 +1001,7 @@ def spmm_sparse_rect(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, al
     _check_tab("Y2", Y2, None, 0, R, 64)
     _check_tab("A1", A1, None, 0, R, 64)
     plan = _sparse_plan(adj)
-    with profiling.region(region, 0):
+    with profiling.region(region, sparse_upstream_bytes(adj) + (256 * R if A1 is not None else 0)):
         if plan is not None:  # heavy rows (the transpose slice's Zipf items): edge-balanced blocks
             _sparse_blocks(adj, True, bits, X, Y2, None, 0, alpha, A1, beta1, plan)
             return
@@ -995,8 +1096,11 @@ def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None):
         if front is not None and adj.symmetric:
             inv = 1.0 / 3.0
             g = G[:split]
-            lst, cnt = front
-            with profiling.region("spmm_rows", 0):
+            lst, cnt = front[0], front[1]
+            # the frontier's item rows (expected count: front[2], the count itself is on the device)
+            # scattered into the ingredient rows: X row read, per edge col/val + an atomic row update
+            nf = front[2] if len(front) > 2 else int(lst.numel())
+            with profiling.region("spmm_rows", int(nf * (16 + 256 + mean_degree(adj, 0) * (8 + 512)))):
                 native.check(native.lib().fr_spmm_list_scatter(
                     adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], split,
                     lst.data_ptr(), cnt.data_ptr(), split, g.data_ptr(), g.stride(0), out_hi.data_ptr(),
@@ -1060,7 +1164,10 @@ def _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n):
     E1 = torch.empty_like(out)
     spmm_range(ri_adj, item_w, I, N, X_hi=ingre_w, split=I, Y1=E1)  # layer 1, ingredient rows
     args = (ri_adj.rowptr.data_ptr(), ri_adj.col.data_ptr(), ri_adj.val.data_ptr(), N, I)
-    with profiling.region("spmm_rows", 0):
+    nf = frontier_rows(ui_adj, int(u.numel()), I)
+    # two row-list layers over the frontier's item rows: layer 1 writes E1, layer 2 writes out and
+    # reads the two addends (item_w / ingre_w and E1)
+    with profiling.region("spmm_rows", rows_bytes(ri_adj, nf, 64, 1) + rows_bytes(ri_adj, nf, 64, 3)):
         native.check(lib.fr_spmm_csr_list(*args, ctypes.byref(_tab(item_w, ingre_w)), ctypes.byref(_tab(E1)),
                                           ctypes.byref(_tab(None)), _f(1.0), ctypes.byref(_tab(None)), _f(0.0),
                                           ctypes.byref(_tab(None)), _f(0.0), lst.data_ptr(), cnt.data_ptr(), I, s),
@@ -1069,7 +1176,7 @@ def _ri_fwd_frontier(ri_adj, ui_adj, item_w, ingre_w, U, I, u, p, n):
                                           ctypes.byref(_tab(out)), _f(inv), ctypes.byref(_tab(item_w, ingre_w)),
                                           _f(inv), ctypes.byref(_tab(E1)), _f(inv), lst.data_ptr(), cnt.data_ptr(), I,
                                           s), "fr_spmm_csr_list")  # layer 2, listed item rows
-    return out, (lst, cnt)
+    return out, (lst, cnt, nf)
 
 
 class _GraphBprForward:
@@ -1199,7 +1306,7 @@ class _GraphBpr(torch.autograd.Function):
         dI = dUI[U:]
         common = (ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                   u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(gamma), _f(1.0), _f(1.0), gscale.data_ptr())
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_bwd_bytes(int(u.numel()))):
             if g_rows is not None and not det:
                 g_rows = g_rows.contiguous()
                 native.check(lib.fr_bpr_bwd_ex(*common, dUI.data_ptr(), dI.data_ptr(), None, None, g_rows.data_ptr(),
@@ -1225,7 +1332,7 @@ class _GraphBpr(torch.autograd.Function):
         _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I)
         d_ingre[NI:].zero_()  # the padding row is not a graph node
         # EmbLoss on the ego rows, accumulated into the propagation gradients
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_bwd_bytes(int(u.numel()))):
             native.check(lib.fr_bpr_bwd(*common, None, None, d_user.data_ptr(), d_item.data_ptr(), det, ws.data_ptr(),
                                         ws.numel(), s), "fr_bpr_bwd")
         if ctx.defer is not None and drain:
@@ -1259,7 +1366,7 @@ class _GraphBpr(torch.autograd.Function):
                             lambda: torch.zeros((U + I + 31) // 32, dtype=torch.int32, device=dev)) if sparse else None)
         rows = [(u, 0), (p, U), (n, U)]
         rows_mark(mask, rows, 1, zero=dUI, bits=bits)
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_bwd_bytes(int(u.numel()))):
             native.check(lib.fr_bpr_bwd_ex(ui_all.data_ptr(), 64, items.data_ptr(), 64, user_w.data_ptr(), 64,
                                            item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
                                            _f(gamma), _f(1.0), _f(0.0), g_mf.data_ptr(), dUI.data_ptr(),
@@ -1278,7 +1385,7 @@ class _GraphBpr(torch.autograd.Function):
         d_ingre = grad_buffer(ctx.ingre_w)
         # (the fast UI backward writes G_ri's item rows from the batch rows: non-zero at the frontier only)
         _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I, front=ctx.front)
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_finish_bytes(int(u.numel()))):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),
                                                  g_emb.data_ptr(), d_user.data_ptr(), d_item.data_ptr(),
@@ -1343,7 +1450,7 @@ class _UiBpr(torch.autograd.Function):
                            lambda: torch.zeros((U + I + 31) // 32, dtype=torch.int32, device=dev))
         rows = [(u, 0), (p, U), (n, U)]
         rows_mark(mask, rows, 1, zero=dUI, bits=bits)
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_bwd_bytes(int(u.numel()))):
             native.check(lib.fr_bpr_bwd(ui_all.data_ptr(), 64, ui_all[U:].data_ptr(), 64, user_w.data_ptr(), 64,
                                         item_w.data_ptr(), 64, u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(gamma),
                                         _f(0.0 if g_mf is None else 1.0), _f(0.0), native.ptr(gm), dUI.data_ptr(),
@@ -1355,7 +1462,7 @@ class _UiBpr(torch.autograd.Function):
         # its d item), else a dense zero-filled gradient of its own
         sink = ctx.sink if ctx.sink is not None and ctx.sink.open and g_emb is not None else None
         d_item = None if sink is not None else torch.zeros_like(item_w)
-        with profiling.region("bpr_bwd", 0):
+        with profiling.region("bpr_bwd", bpr_finish_bytes(int(u.numel()))):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64,
                                                  _f(0.0 if g_emb is None else w_emb), native.ptr(ge), d_user.data_ptr(),
@@ -1600,9 +1707,21 @@ def norms_scatter_into(idx, G, E, gn, nrm, half, pad, dW) -> None:
     """``dW[idx[i]] += G[i] + [idx[i] != pad] (gn[h] / nrm[h]) E[i]`` (h: the position's half) with
     float atomics, the pad row pre-summed per workgroup (fr_norms_bwd_scatter)."""
     n = int(idx.numel())
-    native.require_device(G, E, dW)
+    native.require_device(idx, G, E, gn, nrm, dW)
     if dW.dtype != torch.float32 or dW.shape[1] != 64 or dW.stride(1) != 1 or dW.stride(0) % 4 or dW.data_ptr() % 16:
         raise native.EngineError("norms_scatter_into: fp32 [rows, 64] table with 16-B aligned rows required")
+    # the kernel reads G / E as dense [n, 64] rows (row stride 64), idx as n int64, gn[h * stride] and
+    # nrm[h] for the two halves h = 0, 1
+    for name, t in (("G", G), ("E", E)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != (n, 64):
+            raise native.EngineError(f"norms_scatter_into: {name} must be a contiguous fp32 [{n}, 64] tensor")
+    if idx.dtype != torch.int64 or not idx.is_contiguous():
+        raise native.EngineError("norms_scatter_into: idx must be a contiguous int64 tensor")
+    if gn.dtype != torch.float32 or gn.dim() < 1 or gn.shape[0] < 2 or nrm.dtype != torch.float32 \
+            or not nrm.is_contiguous() or nrm.numel() < 2:
+        raise native.EngineError("norms_scatter_into: gn and nrm must be fp32 with an entry per half (2)")
+    if not 0 <= int(half) <= n:
+        raise native.EngineError("norms_scatter_into: half must be in [0, n]")
     with profiling.region("embedding_bwd", embedding_bwd_bytes(n, int(dW.shape[0]), 64) + 4 * n * 64):
         native.check(native.lib().fr_norms_bwd_scatter(
             idx.data_ptr(), n, int(half), -1 if pad is None else int(pad), G.data_ptr(), E.data_ptr(), gn.data_ptr(),

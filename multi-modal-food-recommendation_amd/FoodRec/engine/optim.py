@@ -545,7 +545,14 @@ class FusedAdam(torch.optim.Optimizer):
                 # also when it is a lazily updated table taking a dense step
                 held = [p for p in plist if id(p) in late]
                 if held:
-                    late_plans.append((held, hyper))
+                    # the branch stream's update of a held table must also follow its backlog flush
+                    # (_flush_tables above, on the current stream after ``before_dense``): such a
+                    # table's plan waits for an event recorded behind that flush instead
+                    ready = before_dense
+                    if before_dense is not None and any(id(p) in {id(q) for q in lazy_dense} for p in held):
+                        ready = torch.cuda.Event()
+                        ready.record()
+                    late_plans.append((held, hyper, ready))
                     plist = [p for p in plist if id(p) not in late]
             if plist:
                 if w_read is not None:
@@ -560,9 +567,9 @@ class FusedAdam(torch.optim.Optimizer):
                 else:
                     self._launch_rows(lib, rows, hyper)
         def launch_held(stream=None):
-            for held, hyper in late_plans:
+            for held, hyper, ready in late_plans:
                 if stream is not None:
-                    stream.wait_event(before_dense)
+                    stream.wait_event(ready)
                     hyper = hyper[:-1] + (stream.cuda_stream,)
                 with profiling.region("adam", 28 * sum(p.numel() for p in held)):
                     self._launch_dense(lib, held, hyper)

@@ -162,6 +162,19 @@ class TripleSampler:
             self._pending.result()
             self._pending = None
 
+    def close(self):
+        """Join a prefetch in flight (its draws are dropped; an exception the host thread raised is
+        re-raised here) and shut the thread down, so no draw outlives the caller's training run (a
+        later run's init_seed could otherwise be overwritten by a late np.random.set_state)."""
+        pend, self._pending = self._pending, None
+        try:
+            if pend is not None:
+                pend.result()
+        finally:
+            if self._pool is not None:
+                self._pool.shutdown(wait=True)
+                self._pool = None
+
     def epoch(self, out=None, feed=None, prefetch: bool = False):
         """Yield (u, pos, neg) int64 device tensors per batch for one epoch.  Negatives are drawn
         per batch (same stream as the reference's per-sample draws, in permutation order).  With

@@ -35,6 +35,17 @@ def synth_bipartite(n_users, n_items, mean_deg=20.0, seed=0, device="cuda"):
     return u, i
 
 
+def uniform_bipartite(n_users, n_items, mean_deg=20.0, seed=0, device="cuda"):
+    """(user, item) pairs with config 4's user degrees but uniformly popular items: no item row is
+    hot, so a gather over an item table far beyond the Infinity Cache misses it (a DRAM-level SpMM
+    measurement; duplicates removed later by the CSR build)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    deg = torch.poisson(torch.full((n_users,), mean_deg - 1.0, device=device), generator=g).to(torch.int64) + 1
+    u = torch.repeat_interleave(torch.arange(n_users, device=device), deg)
+    i = torch.randint(0, n_items, (u.numel(),), device=device, generator=g)
+    return u, i
+
+
 class InteractionGraph:
     """Dataset object for LightGCN_ID: n_users / n_items (what GeneralRecommender reads), the
     normalised adjacency ``adj`` and a device triple sampler."""

@@ -304,6 +304,9 @@ __global__ __launch_bounds__(256) void rows_mark_kernel(uint8_t* __restrict__ ma
 // or rounds gets several adds in a run-to-run variable order (the deterministic mode keeps the
 // column-masked gather).  d = 64.
 constexpr int kSpRows = 64;
+// bit 0: a plan block of more than kSpRows rows (or outside [0, n_rows)); bit 1: a block whose edge
+// range leaves its rows.  Set by spmm_sparse_kernel, read and cleared by fr_spmm_plan_status.
+__device__ unsigned int g_sparse_plan_status;
 constexpr int kSpRound = 1024;
 constexpr int kSpStageWords = 1024;  // bitmask staged in LDS (dynamic, ceil(n / 32) words): up to 32,768 rows
 
@@ -334,7 +337,15 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   __shared__ int cnt[KS * 4];        // hits per (k, wave) slice of the round
   const int t = threadIdx.x, q = t & 15, lane = t & 63, wave = t >> 6;
   const int64_t r0 = blocks ? blocks[4 * (int64_t)blockIdx.x] : (int64_t)blockIdx.x * kSpRows;
-  const int nr = blocks ? (int)(blocks[4 * (int64_t)blockIdx.x + 1] - r0) : (int)min<int64_t>(kSpRows, n_rows - r0);
+  const int64_t r1 = blocks ? blocks[4 * (int64_t)blockIdx.x + 1] : min<int64_t>(r0 + kSpRows, n_rows);
+  // a plan block must fit the LDS row accumulator (kSpRows rows) and the adjacency's rows: anything
+  // else is refused here (block-uniform, before any LDS index depends on it) and reported through
+  // g_sparse_plan_status (fr_spmm_plan_status), never computed into a wrong row
+  if (r0 < 0 || r1 < r0 || r1 - r0 > kSpRows || r1 > n_rows) {
+    if (t == 0) atomicOr(&g_sparse_plan_status, 1u);
+    return;
+  }
+  const int nr = (int)(r1 - r0);
   if constexpr (!GBITS) {  // stage the bitmask: 16-B loads, all in flight before the LDS stores
     const int n4 = nwords >> 2;
     const uint4* b4 = reinterpret_cast<const uint4*>(bits);
@@ -348,6 +359,10 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   const int64_t e0 = blocks ? blocks[4 * (int64_t)blockIdx.x + 2] : srp[0];
   const int64_t e1 = blocks ? blocks[4 * (int64_t)blockIdx.x + 3] : srp[nr];
   const bool chunk = e0 != srp[0] || e1 != srp[nr];  // part of one heavy row (block-uniform)
+  if (e0 < srp[0] || e1 > srp[nr] || e1 < e0 || (chunk && nr != 1)) {  // edges outside the block's rows
+    if (t == 0) atomicOr(&g_sparse_plan_status, 2u);
+    return;
+  }
   for (int64_t base = e0; base < e1; base += kSpRound) {
     // scan: coalesced column and value loads (edge base + k * 256 + t), hit flags by wave ballot
     int cs[KS];
@@ -1110,6 +1125,18 @@ extern "C" int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int
                                             reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_spmm_sparse_upstream_blocks: ") + hipGetErrorString(e));
   return FR_OK;
+}
+
+extern "C" int fr_spmm_sparse_block_rows(void) { return kSpRows; }
+
+extern "C" int fr_spmm_plan_status(int clear) {
+  unsigned int v = 0;
+  FR_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_sparse_plan_status), sizeof(v)));
+  if (clear && v) {
+    const unsigned int z = 0;
+    FR_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sparse_plan_status), &z, sizeof(z)));
+  }
+  return (int)v;
 }
 
 extern "C" int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,

@@ -911,24 +911,46 @@ __device__ __forceinline__ void nce_tile_r(const NceWS& ws, const PairTab& pt, i
 }
 
 // F.normalize(p=2, dim=-1) of every view row: x / max(||x||, 1e-12); one wave per row
-__global__ __launch_bounds__(256) void nce_normalize_kernel(Views vw, int V, int64_t b, int d, NceWS ws) {
-  const int lane = threadIdx.x & 63;
-  const int64_t rows = (int64_t)V * b;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < rows;
-       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const float* H = vw.x[r / b] + (r % b) * d;
-    // d <= 128 (nce_check): this lane's columns lane, lane + 64 held in registers
-    const float h0 = lane < d ? H[lane] : 0.f, h1 = lane + 64 < d ? H[lane + 64] : 0.f;
-    float s = 0.f;
-    if (lane < d) s = fmaf(h0, h0, s);
-    if (lane + 64 < d) s = fmaf(h1, h1, s);
-    s = group_sum<64>(s);
-    const float nr = sqrtf(s);
-    const float den = fmaxf(nr, 1e-12f);
-    if (lane < d) ws.Hn[r * d + lane] = h0 / den;
-    if (lane + 64 < d) ws.Hn[r * d + lane + 64] = h1 / den;
-    if (lane == 0) ws.nrm[r] = nr;
-  }
+// One row's squared norm the way the fused log-sum-exp staging computes it (nce_lse_mfma2_kernel<D,
+// true>): a thread holds 4 adjacent float4 chunks of the row (lanes of a row: LPR = max(D / 16, 1)),
+// each chunk folded w, z, y, x into one fmaf chain, then a DPP group sum over the row's lanes.  Both
+// the normalize pass and the fused staging use it, so Hn / norms are bit-identical either way.
+template <int D>
+struct NceRowLayout {
+  static constexpr int D4 = D / 4, LPR = D4 / 4 >= 1 ? D4 / 4 : 1;
+};
+
+template <int D>
+__device__ __forceinline__ float nce_row_sumsq(const float4 (&fv)[4]) {
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    ss = fmaf(fv[q].x, fv[q].x, fmaf(fv[q].y, fv[q].y, fmaf(fv[q].z, fv[q].z, fmaf(fv[q].w, fv[q].w, ss))));
+  return group_sum<NceRowLayout<D>::LPR>(ss);
+}
+
+// Hn = H / max(|H|, 1e-12) and the norms, rows of every view (the staging layout above: LPR lanes per
+// row, every lane of a wave active for the DPP sum; rows past the end read zeros and store nothing)
+template <int D>
+__global__ __launch_bounds__(256) void nce_normalize_kernel(Views vw, int V, int64_t b, NceWS ws) {
+  using Ly = NceRowLayout<D>;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = t / Ly::LPR, rows = (int64_t)V * b;
+  const int c0 = (int)(t % Ly::LPR) * 4;
+  const bool ok = r < rows;
+  const float4* src = ok ? reinterpret_cast<const float4*>(vw.x[r / b] + (r % b) * D) + c0 : nullptr;
+  float4 fv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) fv[q] = ok && c0 + q < Ly::D4 ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float nr = sqrtf(nce_row_sumsq<D>(fv));
+  const float den = fmaxf(nr, 1e-12f);
+  if (!ok) return;
+  if (c0 == 0) ws.nrm[r] = nr;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (c0 + q < Ly::D4)
+      reinterpret_cast<float4*>(ws.Hn + r * D)[c0 + q] =
+          make_float4(fv[q].x / den, fv[q].y / den, fv[q].z / den, fv[q].w / den);
 }
 
 __device__ __forceinline__ int64_t nce_partner(int64_t i, int64_t b) { return i < b ? i + b : i - b; }
@@ -1215,9 +1237,9 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
   // FUSED: the rows are read raw (the views) and normalised where they are staged.  Staging layout:
   // a thread holds 4 adjacent float4 chunks of one row, a row spans LPR adjacent lanes; its sum of
   // squares is the thread's fmaf chain then a DPP group sum (the same order in every workgroup),
-  // Hn = x * (1 / max(|x|, 1e-12)).  The j == 0 split's workgroups also write their i rows' Hn and
+  // Hn = x / max(|x|, 1e-12) (nce_row_sumsq: the normalize pass's arithmetic).  The j == 0 split's workgroups also write their i rows' Hn and
   // norms for the finalize and the backward (no normalize launch)
-  constexpr int LPR = D4 / 4 >= 1 ? D4 / 4 : 1, RPP = 256 / LPR, NPASS = (T + RPP - 1) / RPP;
+  constexpr int LPR = NceRowLayout<D>::LPR, RPP = 256 / LPR, NPASS = (T + RPP - 1) / RPP;
   auto raw_row = [&](int64_t r) -> const float* {
     const int v = r < b ? pt.pa[p] : pt.pb[p];
     return vw.x[v] + (r < b ? r : r - b) * D;
@@ -1237,13 +1259,8 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
 #pragma unroll
     for (int ps = 0; ps < NPASS; ++ps) {
       const int r = ps * RPP + (int)threadIdx.x / LPR, c0 = ((int)threadIdx.x % LPR) * 4;
-      float ss = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        ss = fmaf(fv[ps][q].x, fv[ps][q].x, fmaf(fv[ps][q].y, fv[ps][q].y, fmaf(fv[ps][q].z, fv[ps][q].z, fmaf(fv[ps][q].w, fv[ps][q].w, ss))));
-      ss = group_sum<LPR>(ss);
-      const float nr = sqrtf(ss);
-      const float inv = 1.f / fmaxf(nr, 1e-12f);
+      const float nr = sqrtf(nce_row_sumsq<D>(fv[ps]));
+      const float den = fmaxf(nr, 1e-12f);
       if (r < T) {
         const int64_t gr = r0 + r;
         float* hn_g = nullptr;
@@ -1257,7 +1274,7 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
         for (int q = 0; q < 4; ++q) {
           if (c0 + q >= D4) continue;
           const float4 x = fv[ps][q];
-          const float4 hn = make_float4(x.x * inv, x.y * inv, x.z * inv, x.w * inv);
+          const float4 hn = make_float4(x.x / den, x.y / den, x.z / den, x.w / den);
           *reinterpret_cast<float4*>(Bt + r * LD + 4 * (c0 + q)) = hn;
           if (hn_g) reinterpret_cast<float4*>(hn_g)[c0 + q] = hn;
         }
@@ -1763,8 +1780,14 @@ static int nce_fwd_impl(const float* const* d_views, int n_views, int64_t b, int
   }
   const bool fused = kNceFusedNorm && g_ssl_mfma == 1 && every_view_paired;
   if (!fused) {
-    const unsigned nb = (unsigned)std::min<int64_t>(fr::ceil_div((int64_t)n_views * b, 4), 4096);
-    hipLaunchKernelGGL(nce_normalize_kernel, dim3(nb), dim3(256), 0, s, v, n_views, b, d, w);
+    const int lpr = d / 16;  // NceRowLayout<d>::LPR
+    const unsigned nb = (unsigned)fr::ceil_div((int64_t)n_views * b * lpr, (int64_t)256);
+    switch (d) {
+      case 16: hipLaunchKernelGGL(nce_normalize_kernel<16>, dim3(nb), dim3(256), 0, s, v, n_views, b, w); break;
+      case 32: hipLaunchKernelGGL(nce_normalize_kernel<32>, dim3(nb), dim3(256), 0, s, v, n_views, b, w); break;
+      case 64: hipLaunchKernelGGL(nce_normalize_kernel<64>, dim3(nb), dim3(256), 0, s, v, n_views, b, w); break;
+      default: hipLaunchKernelGGL(nce_normalize_kernel<128>, dim3(nb), dim3(256), 0, s, v, n_views, b, w); break;
+    }
     FR_LAUNCH_CHECK();
   }
   const int64_t nt = fr::ceil_div(m, T);

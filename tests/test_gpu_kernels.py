@@ -389,10 +389,10 @@ def test_dcor_three_views(cuda, n, ssl_kernels):
         assert err <= max(err32, 1e-4 * np.abs(gr).max()) + 1e-9, (err, err32, np.abs(gr).max())
 
 
+@pytest.mark.parametrize("d", [16, 32, 64, 128])
 @pytest.mark.parametrize("b", [512, 37])
-def test_infonce(cuda, b, ssl_kernels):
+def test_infonce(cuda, b, d, ssl_kernels):
     from FoodRec.engine import ops
-    d = 64
     g = torch.Generator().manual_seed(b)
     H = torch.randn(2 * b, d, generator=g, dtype=torch.float64, requires_grad=True)
     ref = O.cl_loss(H, 0.5)
@@ -405,15 +405,17 @@ def test_infonce(cuda, b, ssl_kernels):
                                atol=1e-4 * float(H.grad.abs().max()))
 
 
+@pytest.mark.parametrize("d", [16, 32, 64, 128])
 @pytest.mark.parametrize("b", [1024, 512, 37])
-def test_infonce_pairs(cuda, b, ssl_kernels):
+def test_infonce_pairs(cuda, b, d, ssl_kernels):
     """ops.infonce_pairs (all pairs in the same launches, views normalised once, no concatenation)
     against the float64 oracle sum of CL_loss(cat([views[a], views[b]])) over CLUSSL's three pairs:
     value rel 1e-5, gradients rel 1e-4; the value is bit-identical to summing the single-pair op in
-    pair order (the same per-pair arithmetic, the same fp32 sum)."""
+    pair order (the same per-pair arithmetic, the same fp32 sum).  Every d the kernels accept: each
+    has its own row staging (1 / 2 / 4 / 8 lanes per row) and normalisation layout."""
     from FoodRec.engine import ops
-    d, pairs = 64, ((0, 1), (0, 2), (2, 1))
-    g = torch.Generator().manual_seed(100 + b)
+    pairs = ((0, 1), (0, 2), (2, 1))
+    g = torch.Generator().manual_seed(100 + b + d)
     V = [torch.randn(b, d, generator=g, dtype=torch.float64, requires_grad=True) for _ in range(3)]
     ref = sum(O.cl_loss(torch.cat([V[a], V[c]]), 0.5) for a, c in pairs)
     (2.5 * ref).backward()
@@ -448,6 +450,25 @@ def test_infonce_pairs_unpaired_view(cuda, ssl_kernels):
         np.testing.assert_allclose(Vd[k].grad.cpu().numpy(), V[k].grad.numpy(), rtol=1e-4,
                                    atol=1e-4 * float(V[k].grad.abs().max()))
     assert Vd[1].grad is None or not Vd[1].grad.any()
+
+
+@pytest.mark.parametrize("d", [16, 32, 64, 128])
+def test_infonce_fused_norm_matches_normalize_pass(cuda, d, ssl_kernels):
+    """The views normalised inside the log-sum-exp staging (every view in a pair) and by the separate
+    normalize pass (a view in no pair) share one arithmetic (nce_row_sumsq, Hn = x / max(|x|, 1e-12)):
+    the same pair gives a bit-identical loss and bit-identical gradients either way."""
+    from FoodRec.engine import ops
+    b = 300
+    g = torch.Generator().manual_seed(d)
+    V = [torch.randn(b, d, generator=g).to(cuda) for _ in range(3)]
+    a = [V[0].clone().requires_grad_(True), V[2].clone().requires_grad_(True)]
+    fused = ops.infonce_pairs(a, ((0, 1),), 0.5)          # every view paired: fused normalisation
+    fused.backward()
+    c = [v.clone().requires_grad_(True) for v in V]
+    sep = ops.infonce_pairs(c, ((0, 2),), 0.5)           # view 1 unpaired: the normalize pass
+    sep.backward()
+    assert torch.equal(fused.detach(), sep.detach())
+    assert torch.equal(a[0].grad, c[0].grad) and torch.equal(a[1].grad, c[2].grad)
 
 
 def test_fused_adam_matches_torch(cuda):
@@ -878,6 +899,55 @@ def test_spmm_sparse_rect(cuda, planned, monkeypatch):
     assert torch.isfinite(got).all()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
     assert (ops._sparse_plan(adj) is not None) == planned
+
+
+@pytest.mark.parametrize("bad", ["rows65", "edges"])
+def test_spmm_sparse_plan_guard(cuda, bad):
+    """A hand-made block plan the sparse-upstream kernel cannot run -- a 65-row block (its LDS row
+    accumulator holds fr_spmm_sparse_block_rows() = 64), or a block whose edge range leaves its rows --
+    is refused by the kernel: the block computes nothing (its rows keep their sentinel), the valid
+    blocks are exact, and fr_spmm_plan_status reports it (then reads 0 once cleared).  The host plan
+    builder refuses the same plan before it reaches the device."""
+    from FoodRec.engine import native, ops
+    lib = native.lib()
+    limit = ops.sparse_block_rows()
+    assert limit == 64
+    lib.fr_spmm_plan_status(1)
+    R, C, d = 300, 200, 64
+    g = torch.Generator().manual_seed(5)
+    deg = torch.randint(1, 6, (R,), generator=g)
+    rp = torch.zeros(R + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(deg, 0)
+    col = torch.cat([torch.sort(torch.randperm(C, generator=g)[:int(k)]).values for k in deg]).to(torch.int32)
+    val = torch.rand(int(rp[-1]), generator=g)
+    from FoodRec.engine.graph import Adjacency
+    adj = Adjacency(rp.to(cuda), col.to(cuda), val.to(cuda), (R, C), device=cuda, symmetric=False)
+    bits = torch.zeros((C + 31) // 32, dtype=torch.int32, device=cuda)
+    cmask = torch.zeros(C, dtype=torch.uint8, device=cuda)
+    ops.rows_mark(cmask, [(torch.arange(C, device=cuda), 0)], 1, bits=bits)
+    X = torch.randn(C, d, device=cuda)
+    ref = torch.empty(R, d, device=cuda)
+    ops.spmm_launch(adj, X, Y2=ref, alpha=1.0)
+    rpn = rp.numpy()
+    cuts = [0, 64, 128 + (bad == "rows65"), 192, 256, R]  # (rows65: the second block has 65 rows)
+    blocks = [(a, b, rpn[a], rpn[b]) for a, b in zip(cuts[:-1], cuts[1:])]
+    if bad == "edges":
+        blocks[1] = (64, 128, rpn[64], rpn[130])
+    bad_rows = slice(64, cuts[2])
+    plan_np = np.asarray(blocks, dtype=np.int64)
+    with pytest.raises(native.EngineError):
+        ops.check_sparse_plan(plan_np, rpn, limit)
+    plan = (torch.from_numpy(plan_np).to(cuda), torch.zeros(0, dtype=torch.int64, device=cuda))
+    got = torch.full((R, d), 7.0, device=cuda)
+    ops._sparse_blocks(adj, True, bits, X, got, None, 0, 1.0, None, 0.0, plan)
+    torch.cuda.synchronize()
+    status = lib.fr_spmm_plan_status(1)
+    assert status == (1 if bad == "rows65" else 2)
+    assert lib.fr_spmm_plan_status(0) == 0
+    keep = torch.ones(R, dtype=torch.bool)
+    keep[bad_rows] = False
+    assert bool((got[~keep.to(cuda)] == 7.0).all())
+    torch.testing.assert_close(got[keep.to(cuda)], ref[keep.to(cuda)], rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("frac", [0.02, 0.3])

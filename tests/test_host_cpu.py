@@ -76,6 +76,28 @@ def test_sampler_stream_bit_exact():
         np.testing.assert_array_equal(n, g[f"ep{ep}/n"])
 
 
+def test_sampler_close_joins_the_prefetch_thread(monkeypatch):
+    """TripleSampler.close (Trainer.fit's finally): a prefetch in flight is joined, its host thread
+    shut down, and an exception the thread raised reaches the caller instead of being dropped."""
+    import threading
+    from FoodRec.engine.sampler import TripleSampler
+    cfg = tiny_config("LightGCN", False)
+    data = tiny_data(cfg)
+    s = TripleSampler(data, 64)
+    s.prefetch()
+    s.close()
+    assert s._pending is None and s._pool is None
+    assert not [t for t in threading.enumerate() if t.name.startswith("fr-sampler")]
+
+    def boom(slot):
+        raise RuntimeError("draw failed")
+    monkeypatch.setattr(s, "_draw_host", boom)
+    s.prefetch()
+    with pytest.raises(RuntimeError, match="draw failed"):
+        s.close()
+    assert s._pool is None
+
+
 def test_sampler_prefetch_keeps_the_stream():
     """TripleSampler.prefetch (the next epoch's permutation and negatives drawn on a host thread
     while this epoch's batches are consumed) yields the reference stream: the golden epochs, and the
@@ -306,6 +328,25 @@ def test_sparse_block_plan_covers_every_edge_once(edges):
     assert (np.diff(blocks[:, 2]) >= 0).all()  # in edge order
 
 
+def test_sparse_block_rows_exported_and_plans_refused():
+    """The sparse-upstream kernel's row limit comes from the library (fr_spmm_sparse_block_rows, the
+    kernel's kSpRows = 64; no GPU call), sparse_block_plan refuses a wider block size, and
+    check_sparse_plan refuses a 65-row block, rows past the adjacency and an edge range outside its
+    rows -- the same conditions the kernel flags in fr_spmm_plan_status."""
+    from FoodRec.engine import native, ops
+    assert native.lib().fr_spmm_sparse_block_rows() == 64 == ops.sparse_block_rows()
+    rp = np.arange(0, 301 * 3, 3, dtype=np.int64)  # 300 rows of 3 edges
+    with pytest.raises(native.EngineError):
+        ops.sparse_block_plan(rp, 65, 2048)
+    blocks, _ = ops.sparse_block_plan(rp)
+    assert (blocks[:, 1] - blocks[:, 0]).max() == 64
+    ops.check_sparse_plan(blocks, rp, 64)
+    for bad in ([[0, 65, 0, 195]], [[290, 301, 870, 903]], [[0, 10, 0, 33]], [[5, 7, 16, 20]]):
+        with pytest.raises(native.EngineError):
+            ops.check_sparse_plan(np.asarray(bad), rp, 64)
+    ops.check_sparse_plan(np.asarray([[5, 6, 16, 17], [5, 6, 17, 18]]), rp, 64)  # chunks of one row
+
+
 def test_plain_chunk_widens_light_graphs_only():
     """graph.plain_chunk: a graph whose heaviest row fits PLAIN_MAX_DEGREE gets a chunk covering it
     (no split rows: the single-launch row walk), a heavier graph keeps the auto chunk."""
@@ -362,3 +403,26 @@ def test_bookkeeping_launches_refuse_repeated_counters():
         native.check(lib.fr_healthrec_loss_finalize(0x1000, 16, 0.5, 1.0, 1.0, 0x1100, 0x1200, 64, 0x1300, 512.0,
                                                     1e-3, 0x1400, 0x1500, 0x1600, 0x1700, 0, 0x1800, twice, 2,
                                                     None, None), "fr_healthrec_loss_finalize")
+
+
+def test_region_byte_models():
+    """The byte models of the regions that used to report none: row-list SpMM at
+    each side's mean degree, the RI frontier's expected size, the sparse-upstream scan + write, the
+    scatter-upstream, and the BPR backward / finish kernels -- pinned on a small bipartite shape."""
+    from types import SimpleNamespace
+    import torch
+    from FoodRec.engine import ops
+    adj = SimpleNamespace(shape=(100, 100), nnz=600, bipartite_split=40, nnz_below_split=300)
+    assert ops.mean_degree(adj, 0) == 7.5 and ops.mean_degree(adj, 40) == 5.0
+    flat = SimpleNamespace(shape=(100, 100), nnz=600, bipartite_split=None, nnz_below_split=0)
+    assert ops.mean_degree(flat, 77) == 6.0
+    ids = torch.zeros(10, dtype=torch.int64)
+    # users (side 0) and items (offset 40: side 1), one output written each
+    want = 10 * (16 + 7.5 * (8 + 256) + 256) + 10 * (16 + 5.0 * (8 + 256) + 256)
+    assert ops.rows_bytes(adj, [(ids, 0), (ids, 40)], 64, 1) == int(want)
+    assert ops.rows_bytes(adj, 10, 64, 3) == int(10 * (16 + 7.5 * 264 + 3 * 256))
+    assert ops.frontier_rows(adj, 4, 60) == 38 and ops.frontier_rows(adj, 40, 60) == 60
+    assert ops.sparse_upstream_bytes(adj) == 8 * 101 + 8 * 600 + 256 * 100
+    assert ops.scatter_upstream_bytes(adj, [(ids, 40)]) == int(10 * (16 + 256 + 5.0 * (8 + 512)))
+    assert ops.bpr_bwd_bytes(512) == 3 * 512 * (8 + 1024)
+    assert ops.bpr_finish_bytes(512) == 3 * 512 * (9 + 768)

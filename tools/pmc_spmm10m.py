@@ -6,7 +6,7 @@ MI355X_MICROARCH.md's HBM section) + WRITE_SIZE, summed over the kernels one spm
 unit kernel and, for split rows, the ordered fix-up), averaged over the launches.  These are bytes
 that left the L2: DRAM traffic plus Infinity Cache (MALL) hits -- an upper bound on DRAM bytes.
 
-usage: python tools/pmc_spmm10m.py FETCH_DIR WRITE_DIR OUT_JSON KEY [note]   (KEY: config4 | beyond_mall)
+usage: python tools/pmc_spmm10m.py FETCH_DIR WRITE_DIR OUT_JSON KEY [note]   (KEY: config4 | dram_uniform)
 """
 import csv
 import glob

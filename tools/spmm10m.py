@@ -1,4 +1,4 @@
-"""The config-4 SpMM launches exactly as bench.py's config4 / spmm_beyond_mall legs build them
+"""The config-4 SpMM launches exactly as bench.py's config4 / spmm_dram_uniform legs build them
 (InteractionGraph(10M, I, 20, seed), d = 64 fp32, ops.spmm_launch), for rocprofv3 PMC passes:
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -- python3 tools/spmm10m.py --items 1000000 --seed 0
@@ -23,11 +23,14 @@ def main():
     ap.add_argument("--items", type=int, default=1_000_000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--uniform", action="store_true", help="uniformly popular items (bench.py spmm_dram_uniform)")
     a = ap.parse_args()
     from FoodRec.engine import ops
-    from FoodRec.utils.interaction_graph import InteractionGraph
+    from FoodRec.utils.interaction_graph import InteractionGraph, uniform_bipartite
     dev = torch.device("cuda")
-    g = InteractionGraph(a.users, a.items, 20.0, seed=a.seed, device=dev)
+    pairs = uniform_bipartite(a.users, a.items, 20.0, a.seed, dev) if a.uniform else None
+    g = InteractionGraph(a.users, a.items, 20.0, seed=a.seed, device=dev, pairs=pairs)
+    del pairs
     adj = g.adj
     X = torch.randn(a.users + a.items, 64, device=dev)
     Y = torch.empty_like(X)
