@@ -896,6 +896,220 @@ __device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// attention per (sequence, head) on one wave, v_mfma_f32_32x32x2_f32 (L = 20: a sequence padded to
+// one 32 x 32 tile).  The workgroup's 4 sequences x 2 heads are exactly its 8 waves: no job table,
+// no barrier between the products, no scratch shared between waves.  Layout of a 32 x 32 output:
+// lane l holds column j = l & 31, register v row tile_row(v, hf = l >> 5).  Scores are computed
+// transposed, S^T = K Q^T (rows keys, lane = query): the softmax over keys is lane-local plus the
+// partner half (permlane32 swap), and register s is directly the A operand of a product over keys
+// (contraction index key(s, hf) = tile_row(s, hf): 12 steps cover keys 0..23).  Products over
+// queries (dK, dV) read dS / P' back transposed from a 20 x 24 slice of LDS private to the wave
+// (contraction index query 2s + hf: 10 steps).  Operand rows past the sequence (keys / queries
+// >= L) are read as zeros, so padded rows contribute nothing (0 x garbage never enters an MFMA).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int tile_row(int v, int hf) { return 8 * (v >> 2) + 4 * hf + (v & 3); }
+__device__ __forceinline__ float swap32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+constexpr int SEQ_TLD = 24;                       // private transposed dS / P' slices: [key][query]
+constexpr int SEQ_TSZ = 20 * SEQ_TLD;             // floats per slice (L = 20)
+
+// this wave's (sequence g, head hh) for L = 20
+struct SeqJob {
+  int g, hh, base, j, hf;
+  bool jv;
+};
+template <int L>
+__device__ __forceinline__ SeqJob seq_job() {
+  const int w = wave_id(), lane = threadIdx.x & 63;
+  SeqJob q;
+  q.g = w & 3;
+  q.hh = w >> 2;
+  q.base = q.g * L;
+  q.j = lane & 31;
+  q.hf = lane >> 5;
+  q.jv = q.j < L;
+  return q;
+}
+
+// S^T = K Q^T of the job (unscaled, rows keys, lane = query); optionally the same product with
+// V (A) and dctx (B) -> dP'^T
+template <int L>
+__device__ __forceinline__ f32x16 seq_scores(const float* RA, int offA, const float* Bsrc, int ldb, int offB,
+                                             const SeqJob& q) {
+  const int row = q.base + (q.jv ? q.j : 0);
+  const float* ar = RA + row * LD_QKV + offA + q.hh * HD + 16 * q.hf;
+  const float* br = Bsrc + row * ldb + offB + q.hh * HD + 16 * q.hf;
+  float4 av[4], bv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    av[k] = lds4(ar + 4 * k);
+    bv[k] = lds4(br + 4 * k);
+    if (!q.jv) av[k] = bv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 16; ++st) acc = mfma32(comp(av[st >> 2], st & 3), comp(bv[st >> 2], st & 3), acc);
+  return acc;
+}
+
+// scale + key masks + softmax over keys, in place (S^T -> P^T); keys >= L get p = 0
+template <int L>
+__device__ __forceinline__ void seq_softmax(f32x16& s, const float* MS, const SeqJob& q) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int key = tile_row(v, q.hf);
+    const float ms = MS[q.base + (key < L ? key : 0)];
+    const float x = key < L ? s[v] * kScale + ms : -INFINITY;
+    s[v] = x;
+    mx = fmaxf(mx, x);
+  }
+  mx = swap32_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const float e = exp_fast(s[v] - mx);
+    s[v] = e;
+    sum += e;
+  }
+  const float inv = 1.f / swap32_sum(sum);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) s[v] *= inv;
+}
+
+// attention-dropout keep bits of the lane's 16 (query j, key tile_row(v, hf)) elements, bit v; keys
+// come in aligned groups of 4, so pairs (k, k + 1) share one hash (keep()'s halves)
+template <int L>
+__device__ __forceinline__ uint32_t seq_keep_bits(uint32_t ks, uint32_t thr, int64_t seq0, const SeqJob& q) {
+  static_assert(L % 2 == 0, "pair hashes need even rows");
+  if (thr == 0u) return 0xFFFFu;
+  const uint32_t rowb = (uint32_t)((((seq0 + q.g) * HEADS + q.hh) * L + q.j) * L);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int grp = 0; grp < 4; ++grp) {
+    const int k0 = 8 * grp + 4 * q.hf;
+    const uint32_t p0 = (rowb + (uint32_t)k0) >> 1;
+    const uint32_t h0 = pair_hash(ks, p0), h1 = pair_hash(ks, p0 + 1);
+    bits |= ((uint32_t)half_keep(h0, 0, thr) | ((uint32_t)half_keep(h0, 1, thr) << 1) |
+             ((uint32_t)half_keep(h1, 0, thr) << 2) | ((uint32_t)half_keep(h1, 1, thr) << 3)) << (4 * grp);
+  }
+  return bits;
+}
+
+// out[query][d] (+)= sum over keys X^T[key][query] Bm[key][d]: X^T in registers (A operand, key(s, hf) =
+// tile_row(s, hf)), Bm rows of the sequence's keys at column offset off (head hh), zero past L
+template <int L>
+__device__ __forceinline__ f32x16 seq_keys_product(const f32x16& x, const float* Bm, int ldb, int off,
+                                                   const SeqJob& q) {
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  float b[12];
+#pragma unroll
+  for (int st = 0; st < 12; ++st) {
+    const int key = tile_row(st, q.hf);
+    b[st] = key < L ? Bm[(q.base + key) * ldb + off + q.hh * HD + q.j] : 0.f;
+  }
+#pragma unroll
+  for (int st = 0; st < 12; ++st) acc = mfma32(x[st], b[st], acc);
+  return acc;
+}
+
+// out[key][d] = sum over queries T[key][query] Bm[query][d]: T the wave's transposed slice (A
+// operand: lane = key, query 2s + hf), Bm the sequence's query rows (column offset off, head hh)
+template <int L>
+__device__ __forceinline__ f32x16 seq_queries_product(const float* T, const float* Bm, int ldb, int off,
+                                                      const SeqJob& q) {
+  static_assert(L == 20, "10 steps of 2 queries");
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  float a[10], b[10];
+#pragma unroll
+  for (int st = 0; st < 10; ++st) {
+    const int qr = 2 * st + q.hf;
+    a[st] = q.jv ? T[q.j * SEQ_TLD + qr] : 0.f;
+    b[st] = Bm[(q.base + qr) * ldb + off + q.hh * HD + q.j];
+  }
+#pragma unroll
+  for (int st = 0; st < 10; ++st) acc = mfma32(a[st], b[st], acc);
+  return acc;
+}
+
+// store the rows < L of a 32 x 32 output (rows tile_row(v, hf), column j = d) to LDS rows of the
+// sequence at column offset off (head hh)
+template <int L>
+__device__ __forceinline__ void seq_store(float* dst, int ld, int off, const f32x16& o, const SeqJob& q) {
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int r = tile_row(v, q.hf);
+    if (r < L) dst[(q.base + r) * ld + off + q.hh * HD + q.j] = o[v];
+  }
+}
+
+// forward: ctx = dropout(softmax(q k^T / sqrt(32) + mask)) v of the wave's (sequence, head), over the
+// q slots of RA
+template <int L>
+__device__ __forceinline__ void attn_fwd_seq(float* RA, const float* MS, int64_t seq0, uint32_t ks, const Weights& w) {
+  const SeqJob q = seq_job<L>();
+  f32x16 p = seq_scores<L>(RA, E, RA, LD_QKV, 0, q);  // S^T = K Q^T
+  seq_softmax<L>(p, MS, q);
+  const uint32_t kb = seq_keep_bits<L>(ks, w.thr[0], seq0, q);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) p[v] = ((kb >> v) & 1u) ? p[v] * w.scale[0] : 0.f;
+  const f32x16 ctx = seq_keys_product<L>(p, RA, LD_QKV, 2 * E, q);  // P' V
+  seq_store<L>(RA, LD_QKV, 0, ctx, q);  // only this wave reads the (sequence, head) q slots
+}
+
+// backward of the wave's (sequence, head): dQ, dK, dV over the q / k / v slots of RA (each wave owns
+// its slots: no other wave reads them).  RC: dctx.  TB: 2 x SEQ_TSZ floats private to the wave.
+template <int L>
+__device__ __forceinline__ void attn_bwd_seq(float* RA, const float* RC, const float* MS, int64_t seq0, uint32_t ks,
+                                             const Weights& w, float* TB) {
+  const SeqJob q = seq_job<L>();
+  f32x16 p = seq_scores<L>(RA, E, RA, LD_QKV, 0, q);        // S^T = K Q^T
+  f32x16 d = seq_scores<L>(RA, 2 * E, RC, LD_E, 0, q);      // dP'^T = V dctx^T
+  seq_softmax<L>(p, MS, q);
+  const uint32_t kb = seq_keep_bits<L>(ks, w.thr[0], seq0, q);
+  float D = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const float dpj = ((kb >> v) & 1u) ? d[v] * w.scale[0] : 0.f;  // dL/dp
+    d[v] = dpj;
+    D = fmaf(p[v], dpj, D);
+  }
+  D = swap32_sum(D);
+  float* TS = TB;            // dS^T as [key][query]
+  float* TP = TB + SEQ_TSZ;  // P'^T
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const float pv = p[v];
+    const float ds = pv * (d[v] - D) * kScale;
+    d[v] = ds;
+    const int key = tile_row(v, q.hf);
+    if (key < L && q.jv) {
+      TS[key * SEQ_TLD + q.j] = ds;
+      TP[key * SEQ_TLD + q.j] = ((kb >> v) & 1u) ? pv * w.scale[0] : 0.f;
+    }
+  }
+  const f32x16 dq = seq_keys_product<L>(d, RA, LD_QKV, E, q);          // dQ = dS K
+  const f32x16 dk = seq_queries_product<L>(TS, RA, LD_QKV, 0, q);       // dK = dS^T Q
+  const f32x16 dv = seq_queries_product<L>(TP, RC, LD_E, 0, q);         // dV = P'^T dctx
+  seq_store<L>(RA, LD_QKV, 0, dq, q);
+  seq_store<L>(RA, LD_QKV, E, dk, q);
+  seq_store<L>(RA, LD_QKV, 2 * E, dv, q);
+}
+
 // The ordered reduction of another backward call's partials, folded into this launch: workgroup b
 // owns float4 columns [b C, (b + 1) C) of the NPART / 4 (C = ceil(NPART / 4 / n_wg)), taken in chunks
 // of PR_CH columns (what the scratch holds); PR_SL slices of its threads sum workgroups s, s + PR_SL,
@@ -988,7 +1202,8 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   FR_MARK(0, 20);
 
   // attention on MFMA: 10 (query tile, head) jobs over the 8 waves; ctx over the q slots
-  attn_fwd<L>(RA, MS, seq0, ks.k[0], w, prof);
+  if constexpr (L == 20) attn_fwd_seq<L>(RA, MS, seq0, ks.k[0], w);
+  else attn_fwd<L>(RA, MS, seq0, ks.k[0], w, prof);
   __syncthreads();
   FR_MARK(0, 3);
   lds_store<E>(RA, LD_QKV, a.ctx + tok0 * E, tv);  // ctx (saved for the backward): cols 0..63 of RA
@@ -1090,6 +1305,7 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   constexpr int OFF_RC = ROWS * LD_FF, OFF_RB = OFF_RC + ROWS * LD_E, OFF_RD = OFF_RB + ROWS * LD_E;
   constexpr int SCR_FLOATS = 2 * MAX_SLOTS * TILE_SZ + ROWS * DQ_LD;
   static_assert(SCR_FLOATS <= ROWS * LD_E + BUF_D, "attention scratch fits RB + RD");
+  static_assert((NT / 64) * 2 * SEQ_TSZ <= ROWS * LD_E + BUF_D, "per-wave transposed slices fit RB + RD");
   static_assert(ROWS * LD_E <= BUF_D && 3 * (NT / 16) * E <= BUF_D, "LayerNorm scratch / ctx in RD");
   static_assert(band_slot<L>(RT) <= MAX_SLOTS, "band tiles");
   __shared__ __attribute__((aligned(16))) float LDSB[OFF_RD + BUF_D];
@@ -1276,6 +1492,10 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   //   phase 2: (key tile, dK | dV, column tile) jobs: dK = dS^T Q, dV = P'^T dctx over the k / v slots
   //   then dQ over the head's q slots (phase 2 has read them)
   const int wv = wave_id();
+  if constexpr (L == 20) {
+    attn_bwd_seq<L>(RA, RC, MS, seq0, ks.k[0], w, RB + wv * 2 * SEQ_TSZ);
+    __syncthreads();
+  } else
   for (int hh = 0; hh < HEADS; ++hh) {
     if (wv < RT) attn_bwd_rows_any<L>(wv, RA, RC, MS, hh, seq0, ks.k[0], w, SP, SS, DQ, prof);
     __syncthreads();
