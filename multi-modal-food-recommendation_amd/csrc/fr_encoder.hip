@@ -1233,13 +1233,16 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
   FR_MARK(0, 5);
 
   {  // pre = x1 W1^T + b1; act' = dropout(act(pre)) -> RA.  Column split (wave: tiles 4sg + 2hf, +1;
-     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue
-    f32x4 acc[RT][2];
-    zero_acc(acc);
-    gemm_xwt<2, E, 0, RT>(RB, LD_E, w.w1, 4 * sg + 2 * hf, acc);
+     // every row tile), so both waves of a SIMD get the same share of the GELU / dropout epilogue.
+     // One column tile at a time (GEMM, then its epilogue): 20 accumulator registers live instead of
+     // 40 keeps the kernel at <= 128 VGPRs, so a SIMD can hold two of its waves beside two waves of a
+     // 128-register kernel (the background Adam slice) in the training step's graph
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
+      f32x4 acc[RT][1];
+      zero_acc(acc);
       const int c = 2 * hf + cc;  // column tile within the SIMD slot's four (dact fragment index)
+      gemm_xwt<1, E, 0, RT>(RB, LD_E, w.w1, 4 * sg + c, acc);
       const int col = 16 * (4 * sg + c) + i16;
       const float bias = w.b1[col];
 #pragma unroll
@@ -1250,7 +1253,7 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int q2 = 0; q2 < 2; ++q2) {
           f32x2 av, gv;
-          act_fwd_grad2(f32x2{acc[r][cc][2 * q2], acc[r][cc][2 * q2 + 1]} + bias, w.gelu, av, gv);
+          act_fwd_grad2(f32x2{acc[r][0][2 * q2], acc[r][0][2 * q2 + 1]} + bias, w.gelu, av, gv);
           av = av * w.scale[2];
           gv = gv * w.scale[2];
 #pragma unroll
@@ -1264,6 +1267,7 @@ __global__ __launch_bounds__(NT) void enc_fwd_kernel(FwdArgs a) {
         // dact in the MFMA fragment layout: one coalesced float4 per lane, read back the same way
         *reinterpret_cast<float4*>(a.dact + dact_frag(blockIdx.x, sg, c, r, lane)) = make_float4(d[0], d[1], d[2], d[3]);
       }
+      FR_SCHED_FENCE();
     }
   }
   __syncthreads();
@@ -1511,9 +1515,15 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
     __syncthreads();
   }
   FR_MARK(1, 10);
-  if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
-  lds_load<E>(RC, LD_E, a.x + tok0 * E, tv);
+  // x (step 13), then the step-14 GEMM's W_in fragments (K = 192: 48 registers, in flight across the
+  // dW_in slab); x's commit waits only for its own loads (issued first: loads retire in order)
+  TilePf<E> pf_x;
+  pf_issue(pf_x, a.x + tok0 * E, tv);
+  YwFrags<1, QKV, E> winf;
+  yw_issue(winf, w.w_in, sg);
   FR_SCHED_FENCE();
+  if (tv < ROWS) lds_zero(RA + tv * LD_QKV, LD_QKV, ROWS - tv, QKV);
+  pf_commit(pf_x, RC, LD_E, tv);
   __syncthreads();
   FR_MARK(1, 12);
 
@@ -1523,7 +1533,8 @@ __global__ __launch_bounds__(NT) void enc_bwd_kernel(BwdArgs a) {
   {  // 14. dX = dY1 + dqkv W_in
     f32x4 acc[RT0][1];
     zero_acc(acc);
-    FR_GEMM_YW(1, QKV, E, RA, LD_QKV, w.w_in, sg, acc);
+    if (hf == 0) gemm_yw_pre<1, QKV, E, 0, RT0>(RA, LD_QKV, winf, acc);
+    else gemm_yw_pre<1, QKV, E, RT0, RT - RT0>(RA, LD_QKV, winf, acc);
     const int col = 16 * sg + i16;
 #pragma unroll
     for (int r = 0; r < RT0; ++r) {
