@@ -909,6 +909,12 @@ __device__ __forceinline__ void attn_bwd_rows_any(int R, const float* RA, const 
 // >= L) are read as zeros, so padded rows contribute nothing (0 x garbage never enters an MFMA).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// v & msk bitwise (msk all ones or zero): a branch-free zero of operands past the sequence
+__device__ __forceinline__ float mask1(float v, uint32_t msk) { return __uint_as_float(__float_as_uint(v) & msk); }
+__device__ __forceinline__ float4 mask4(float4 v, uint32_t msk) {
+  return make_float4(mask1(v.x, msk), mask1(v.y, msk), mask1(v.z, msk), mask1(v.w, msk));
+}
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -947,12 +953,19 @@ __device__ __forceinline__ f32x16 seq_scores(const float* RA, int offA, const fl
   const int row = q.base + (q.jv ? q.j : 0);
   const float* ar = RA + row * LD_QKV + offA + q.hh * HD + 16 * q.hf;
   const float* br = Bsrc + row * ldb + offB + q.hh * HD + 16 * q.hf;
+  // rows past L read the sequence's first row (finite) and are zeroed by a lane mask: no branch between
+  // the loads, all eight in flight at once
+  const uint32_t msk = q.jv ? 0xFFFFFFFFu : 0u;
   float4 av[4], bv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     av[k] = lds4(ar + 4 * k);
     bv[k] = lds4(br + 4 * k);
-    if (!q.jv) av[k] = bv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    av[k] = mask4(av[k], msk);
+    bv[k] = mask4(bv[k], msk);
   }
   f32x16 acc;
 #pragma unroll
@@ -1018,8 +1031,10 @@ __device__ __forceinline__ f32x16 seq_keys_product(const f32x16& x, const float*
 #pragma unroll
   for (int st = 0; st < 12; ++st) {
     const int key = tile_row(st, q.hf);
-    b[st] = key < L ? Bm[(q.base + key) * ldb + off + q.hh * HD + q.j] : 0.f;
+    b[st] = Bm[(q.base + (key < L ? key : 0)) * ldb + off + q.hh * HD + q.j];
   }
+#pragma unroll
+  for (int st = 0; st < 12; ++st) b[st] = mask1(b[st], tile_row(st, q.hf) < L ? 0xFFFFFFFFu : 0u);
 #pragma unroll
   for (int st = 0; st < 12; ++st) acc = mfma32(x[st], b[st], acc);
   return acc;
@@ -1035,12 +1050,16 @@ __device__ __forceinline__ f32x16 seq_queries_product(const float* T, const floa
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
   float a[10], b[10];
+  const int jr = q.jv ? q.j : 0;
+  const uint32_t msk = q.jv ? 0xFFFFFFFFu : 0u;
 #pragma unroll
   for (int st = 0; st < 10; ++st) {
     const int qr = 2 * st + q.hf;
-    a[st] = q.jv ? T[q.j * SEQ_TLD + qr] : 0.f;
+    a[st] = T[jr * SEQ_TLD + qr];
     b[st] = Bm[(q.base + qr) * ldb + off + q.hh * HD + q.j];
   }
+#pragma unroll
+  for (int st = 0; st < 10; ++st) a[st] = mask1(a[st], msk);
 #pragma unroll
   for (int st = 0; st < 10; ++st) acc = mfma32(a[st], b[st], acc);
   return acc;
