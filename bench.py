@@ -1207,11 +1207,19 @@ def cpu_baseline(args):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
+    quota = None
+    try:  # the cgroup's CPU quota (cpu.max "QUOTA PERIOD"): what the threads can actually run on
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"value": round(args.batch * k / dt, 2), "unit": "triples/s", "cores": all_cores, "kind": "port",
-            "host_cores_total": all_cores, "cores_in_affinity": affinity,
+            "host_cores_total": all_cores, "cores_in_affinity": affinity, "cgroup_cpu_quota": quota,
             "sample": f"{k} HealthRec training steps (B={args.batch}) of the torch-CPU oracle after 3 warm-ups, "
                       f"torch.set_num_threads({all_cores})",
             "ms_per_step": round(dt / k * 1e3, 1),
+            "note": "BASELINE.md section 3: every host core; where the cgroup quota is below the core count the "
+                    "threads oversubscribe it and per_gpu_share (threads = the quota) is the faster CPU figure",
             "per_gpu_share": {"value": round(args.batch * ks / dts, 2), "cores": share,
                               "ms_per_step": round(dts / ks * 1e3, 1),
                               "sample": f"{ks} steps after 1 warm-up, torch.set_num_threads({share})"}}
