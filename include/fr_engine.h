@@ -853,6 +853,20 @@ int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col
                                    int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
                                    const int64_t* d_blocks, int64_t n_blocks, const int64_t* d_split_rows,
                                    int64_t n_split_rows, void* stream);
+/* fr_spmm_sparse_upstream / fr_spmm_sparse_upstream_blocks with a side job: the launch also zeroes
+ * d_zero[0 .. zero_floats) (16-B aligned, a multiple of 4 floats) -- the region the next kernel on the
+ * stream accumulates into (HealthRec's d ingre rows before the RI backward's list scatter), folded
+ * into this launch instead of a memset node of its own. */
+int fr_spmm_sparse_upstream_zero(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val, int64_t n_rows,
+                                 const uint32_t* d_bits, const float* d_X, int64_t ldx, int64_t split,
+                                 const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1, float* d_zero,
+                                 int64_t zero_floats, void* stream);
+int fr_spmm_sparse_upstream_blocks_zero(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                        int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
+                                        const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2, float alpha,
+                                        const fr_tab* A1, float beta1, const int64_t* d_blocks, int64_t n_blocks,
+                                        const int64_t* d_split_rows, int64_t n_split_rows, float* d_zero,
+                                        int64_t zero_floats, void* stream);
 /* Rows per block of the sparse-upstream kernel (its LDS row accumulator): a plan block of more rows,
  * rows outside [0, n_rows) or an edge range outside its rows is refused by the kernel (the block
  * computes nothing) and flagged in the library's plan status. */

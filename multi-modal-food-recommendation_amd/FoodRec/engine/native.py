@@ -82,6 +82,13 @@ _SIGS = {
     "fr_spmm_sparse_upstream_blocks": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p,
                                                c_void_p, c_int64, c_int64, POINTER(FrTab), c_float, POINTER(FrTab),
                                                c_float, c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
+    "fr_spmm_sparse_upstream_zero": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                                             c_int64, POINTER(FrTab), c_float, POINTER(FrTab), c_float, c_void_p,
+                                             c_int64, c_void_p]),
+    "fr_spmm_sparse_upstream_blocks_zero": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                                                    c_void_p, c_int64, c_int64, POINTER(FrTab), c_float,
+                                                    POINTER(FrTab), c_float, c_void_p, c_int64, c_void_p, c_int64,
+                                                    c_void_p, c_int64, c_void_p]),
     "fr_spmm_sparse_block_rows": (c_int, []),
     "fr_spmm_plan_status": (c_int, [c_int]),
     "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,

@@ -848,26 +848,32 @@ SPARSE_UPSTREAM_MAX_ROWS = 262144  # HealthRec's UI backward in the sparse-upstr
 
 
 def spmm_sparse_upstream(adj: Adjacency, bits: torch.Tensor, X: torch.Tensor, Y2, Y2_hi=None, split=0,
-                         alpha=1.0, beta1=0.0, region="spmm_masked"):
+                         alpha=1.0, beta1=0.0, region="spmm_masked", zero=None):
     """fr_spmm_sparse_upstream: Y2 = alpha A X + beta1 gate(X) for an X that is non-zero only at the
     rows set in ``bits`` (int32 words); X is read only there.  d = 64; float-atomic summation order
-    (non-deterministic mode only)."""
+    (non-deterministic mode only).  ``zero``: a contiguous fp32 tensor the same launch zeroes (a side
+    job, fr_spmm_sparse_upstream_zero: the next kernel's accumulation target, no memset node)."""
     native.require_device(X, bits)
     N = adj.shape[0]
     if adj.shape[1] != N or X.shape[1] != 64 or X.shape[0] < N:
         raise native.EngineError("spmm_sparse_upstream: square adjacency, X [rows, 64]")
+    if zero is not None and (zero.dtype != torch.float32 or not zero.is_contiguous() or zero.numel() % 4
+                             or zero.data_ptr() % 16 or zero.device != X.device):
+        raise native.EngineError("spmm_sparse_upstream: zero must be a contiguous 16-B aligned fp32 tensor "
+                                 "(a multiple of 4 floats) on X's device")
+    zp, zn = (zero.data_ptr(), zero.numel()) if zero is not None else (None, 0)
     if bits.dtype != torch.int32 or bits.numel() < (N + 31) // 32:
         raise native.EngineError("spmm_sparse_upstream: bits must be int32 with ceil(rows / 32) words")
     _check_tab("Y2", Y2, Y2_hi, split, N, 64)
     plan = _sparse_plan(adj)
     with profiling.region(region, sparse_upstream_bytes(adj)):
         if plan is not None:  # heavy rows (config 4's Zipf items): edge-balanced blocks
-            _sparse_blocks(adj, False, bits, X, Y2, Y2_hi, split, alpha, X, beta1, plan)
+            _sparse_blocks(adj, False, bits, X, Y2, Y2_hi, split, alpha, X, beta1, plan, zero=zero)
             return
-        native.check(native.lib().fr_spmm_sparse_upstream(
+        native.check(native.lib().fr_spmm_sparse_upstream_zero(
             adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), N, bits.data_ptr(), X.data_ptr(),
             X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha), ctypes.byref(_tab(X)), _f(beta1),
-            native.stream_of(X)), "fr_spmm_sparse_upstream")
+            zp, zn, native.stream_of(X)), "fr_spmm_sparse_upstream_zero")
 
 
 def sparse_block_rows() -> int:
@@ -959,14 +965,15 @@ def _sparse_plan(adj: Adjacency):
     return plan if plan is not False else None
 
 
-def _sparse_blocks(adj, ungated, bits, X, Y2, Y2_hi, split, alpha, A1, beta1, plan):
+def _sparse_blocks(adj, ungated, bits, X, Y2, Y2_hi, split, alpha, A1, beta1, plan, zero=None):
     blocks, split_rows = plan
     R, C = adj.shape
-    native.check(native.lib().fr_spmm_sparse_upstream_blocks(
+    zp, zn = (zero.data_ptr(), zero.numel()) if zero is not None else (None, 0)
+    native.check(native.lib().fr_spmm_sparse_upstream_blocks_zero(
         adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), R, C, int(ungated), bits.data_ptr(),
         X.data_ptr(), X.stride(0), int(split), ctypes.byref(_tab(Y2, Y2_hi)), _f(alpha), ctypes.byref(_tab(A1)),
-        _f(beta1), blocks.data_ptr(), blocks.shape[0], split_rows.data_ptr(), split_rows.numel(),
-        native.stream_of(X)), "fr_spmm_sparse_upstream_blocks")
+        _f(beta1), blocks.data_ptr(), blocks.shape[0], split_rows.data_ptr(), split_rows.numel(), zp, zn,
+        native.stream_of(X)), "fr_spmm_sparse_upstream_blocks_zero")
 
 
 def spmm_scatter_upstream(adj: Adjacency, mask: torch.Tensor, bits: torch.Tensor, rows, X: torch.Tensor, Y2,
@@ -1084,7 +1091,7 @@ def _prop_bwd_split(adj, G, L, out_lo, out_hi, split, col_mask=None, gate=False)
     spmm_ex(adj, H, Y2=out_lo, Y2_hi=out_hi, split=split, alpha=1.0, A1=G, beta1=inv)
 
 
-def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None):
+def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None, zeroed=False):
     """The RI backward of graph_bpr (G zero at the ingredient rows): the half-graph form on a
     bipartite adjacency with two layers, _prop_bwd_split otherwise.  ``front``: the forward's
     frontier list (lst, cnt) when G's item rows are zero outside it (the fast UI backward writes
@@ -1104,7 +1111,7 @@ def _prop_bwd_ri(adj, G, L, out_lo, out_hi, split, front=None):
                 native.check(native.lib().fr_spmm_list_scatter(
                     adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.val.data_ptr(), adj.shape[0], split,
                     lst.data_ptr(), cnt.data_ptr(), split, g.data_ptr(), g.stride(0), out_hi.data_ptr(),
-                    out_hi.stride(0), _f(inv), 1, native.stream_of(g)), "fr_spmm_list_scatter")
+                    out_hi.stride(0), _f(inv), 0 if zeroed else 1, native.stream_of(g)), "fr_spmm_list_scatter")
             spmm_range(adj, g, 0, split, X_hi=out_hi, split=split, Y2=out_lo, alpha=1.0, A1=g, beta1=inv)
             return
         _prop_bwd_bipartite2(adj, G[:split], out_lo, out_hi, split)
@@ -1377,14 +1384,18 @@ class _GraphBpr(torch.autograd.Function):
         # (the scatter form, spmm_scatter_upstream, measured 362 us against this scan's 50 us at
         # Allrecipes shape: the batch items are popularity-drawn positives, so the marked rows' degree
         # sum is a large share of the edges and a heavy row serialises on one wave)
-        if sparse:
-            spmm_sparse_upstream(ui_adj, bits, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5)
-        else:
-            _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
         d_item = grad_buffer(item_w)
         d_ingre = grad_buffer(ctx.ingre_w)
+        # the RI backward's list scatter accumulates into d ingre's first NI rows: the UI backward's
+        # launch zeroes them on the side (no memset node between the two)
+        zero = d_ingre[:NI] if (SPARSE_ZERO_SIDE and sparse and ctx.front is not None and ri_adj.symmetric
+                                and L_ri == 2 and d_ingre.is_contiguous() and d_ingre.data_ptr() % 16 == 0) else None
+        if sparse:
+            spmm_sparse_upstream(ui_adj, bits, dUI, d_user, G_ri, U, alpha=0.5, beta1=0.5, zero=zero)
+        else:
+            _prop_bwd_split(ui_adj, dUI, 1, d_user, G_ri, U, col_mask=mask, gate=True)
         # (the fast UI backward writes G_ri's item rows from the batch rows: non-zero at the frontier only)
-        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I, front=ctx.front)
+        _prop_bwd_ri(ri_adj, G_ri, L_ri, d_item, d_ingre, I, front=ctx.front, zeroed=zero is not None)
         with profiling.region("bpr_bwd", bpr_finish_bytes(int(u.numel()))):
             native.check(lib.fr_graph_bpr_finish(mask.data_ptr(), U, user_w.data_ptr(), 64, item_w.data_ptr(), 64,
                                                  u.data_ptr(), p.data_ptr(), n.data_ptr(), B, 64, _f(1.0),
@@ -1397,6 +1408,9 @@ class _GraphBpr(torch.autograd.Function):
         return (d_user, d_item, d_ingre) + (None,) * 11
 
 
+# FR_SPARSE_ZERO=0: HealthRec's d ingre rows zeroed by the list scatter's own memset node instead of on
+# the side of the UI backward's launch
+SPARSE_ZERO_SIDE = os.environ.get("FR_SPARSE_ZERO", "1") != "0"
 UI_BPR = os.environ.get("FR_UI_BPR", "1") != "0"  # FR_UI_BPR=0: CLUSSL's UI layer + BPR unfused
 
 

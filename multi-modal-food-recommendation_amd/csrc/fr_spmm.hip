@@ -325,7 +325,8 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
                                                           const float* __restrict__ val, int64_t n_rows,
                                                           const uint32_t* __restrict__ bits, int nwords,
                                                           const float4* __restrict__ X, int64_t ldx4, Epi ep,
-                                                          const int64_t* __restrict__ blocks = nullptr) {
+                                                          const int64_t* __restrict__ blocks = nullptr,
+                                                          float4* __restrict__ zero4 = nullptr, int64_t zero_n4 = 0) {
   constexpr int KS = kSpRound / 256;  // edges per thread per round
   extern __shared__ uint32_t sbits_dyn[];
   const uint32_t* sbits = GBITS ? bits : sbits_dyn;
@@ -336,6 +337,11 @@ __global__ __launch_bounds__(256) void spmm_sparse_kernel(const int64_t* __restr
   __shared__ float hit_v[kSpRound];  // its value
   __shared__ int cnt[KS * 4];        // hits per (k, wave) slice of the round
   const int t = threadIdx.x, q = t & 15, lane = t & 63, wave = t >> 6;
+  // side job (fr_spmm_sparse_upstream_zero): zero a contiguous region for the next kernel on the
+  // stream -- HealthRec's d ingre rows, which the RI backward's list scatter then accumulates into --
+  // instead of a memset launch of its own between the two
+  for (int64_t k = (int64_t)blockIdx.x * 256 + t; k < zero_n4; k += (int64_t)gridDim.x * 256)
+    zero4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int64_t r0 = blocks ? blocks[4 * (int64_t)blockIdx.x] : (int64_t)blockIdx.x * kSpRows;
   const int64_t r1 = blocks ? blocks[4 * (int64_t)blockIdx.x + 1] : min<int64_t>(r0 + kSpRows, n_rows);
   // a plan block must fit the LDS row accumulator (kSpRows rows) and the adjacency's rows: anything
@@ -1087,18 +1093,33 @@ static hipError_t sparse_blocks_launch(const int64_t* d_rowptr, const int32_t* d
                                        int64_t n_rows, const uint32_t* d_bits, int nwords, const float* d_X,
                                        int64_t ldx, const Epi& ep, bool ungated, const int64_t* d_blocks,
                                        int64_t n_blocks, const int64_t* d_split_rows, int64_t n_split_rows,
-                                       hipStream_t s) {
+                                       hipStream_t s, float* d_zero = nullptr, int64_t zero_floats = 0) {
   if (n_split_rows > 0)
     hipLaunchKernelGGL(sparse_split_init_kernel, dim3((unsigned)fr::ceil_div(n_split_rows, (int64_t)16)), dim3(256),
                        0, s, d_split_rows, n_split_rows, d_bits, ungated, ep);
   if (ungated)
     hipLaunchKernelGGL((spmm_sparse_kernel<true, true>), dim3((unsigned)n_blocks), dim3(256), 0, s, d_rowptr, d_col,
-                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks);
+                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks,
+                       reinterpret_cast<float4*>(d_zero), zero_floats / 4);
   else
     hipLaunchKernelGGL((spmm_sparse_kernel<true, false>), dim3((unsigned)n_blocks), dim3(256), 0, s, d_rowptr, d_col,
-                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks);
+                       d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, d_blocks,
+                       reinterpret_cast<float4*>(d_zero), zero_floats / 4);
   return hipGetLastError();
 }
+
+static int sparse_zero_check(const float* d_zero, int64_t zero_floats) {
+  FR_REQUIRE(zero_floats >= 0 && zero_floats % 4 == 0 && (zero_floats == 0 || (d_zero && fr::aligned16(d_zero))),
+             "zero region: 16-B aligned, a multiple of 4 floats");
+  return FR_OK;
+}
+
+static int sparse_upstream_blocks_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                       int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
+                                       const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2, float alpha,
+                                       const fr_tab* A1, float beta1, const int64_t* d_blocks, int64_t n_blocks,
+                                       const int64_t* d_split_rows, int64_t n_split_rows, float* d_zero,
+                                       int64_t zero_floats, void* stream);
 
 extern "C" int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
                                               int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
@@ -1106,6 +1127,29 @@ extern "C" int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int
                                               float alpha, const fr_tab* A1, float beta1, const int64_t* d_blocks,
                                               int64_t n_blocks, const int64_t* d_split_rows, int64_t n_split_rows,
                                               void* stream) {
+  return sparse_upstream_blocks_impl(d_rowptr, d_col, d_val, n_rows, n_cols, ungated, d_bits, d_X, ldx, split, Y2,
+                                     alpha, A1, beta1, d_blocks, n_blocks, d_split_rows, n_split_rows, nullptr, 0,
+                                     stream);
+}
+
+extern "C" int fr_spmm_sparse_upstream_blocks_zero(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                                   int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
+                                                   const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2,
+                                                   float alpha, const fr_tab* A1, float beta1, const int64_t* d_blocks,
+                                                   int64_t n_blocks, const int64_t* d_split_rows, int64_t n_split_rows,
+                                                   float* d_zero, int64_t zero_floats, void* stream) {
+  return sparse_upstream_blocks_impl(d_rowptr, d_col, d_val, n_rows, n_cols, ungated, d_bits, d_X, ldx, split, Y2,
+                                     alpha, A1, beta1, d_blocks, n_blocks, d_split_rows, n_split_rows, d_zero,
+                                     zero_floats, stream);
+}
+
+static int sparse_upstream_blocks_impl(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                       int64_t n_rows, int64_t n_cols, int ungated, const uint32_t* d_bits,
+                                       const float* d_X, int64_t ldx, int64_t split, const fr_tab* Y2, float alpha,
+                                       const fr_tab* A1, float beta1, const int64_t* d_blocks, int64_t n_blocks,
+                                       const int64_t* d_split_rows, int64_t n_split_rows, float* d_zero,
+                                       int64_t zero_floats, void* stream) {
+  if (int rc = sparse_zero_check(d_zero, zero_floats)) return rc;
   FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX && n_cols >= 0 && n_cols < (int64_t)INT32_MAX,
              "n_rows / n_cols out of range");
   if (n_rows == 0) return FR_OK;
@@ -1122,7 +1166,7 @@ extern "C" int fr_spmm_sparse_upstream_blocks(const int64_t* d_rowptr, const int
   const int nwords = (int)fr::ceil_div(std::max<int64_t>(n_cols, 1), 32);
   const hipError_t e = sparse_blocks_launch(d_rowptr, d_col, d_val, n_rows, d_bits, nwords, d_X, ldx, ep, ungated != 0,
                                             d_blocks, n_blocks, d_split_rows, n_split_rows,
-                                            reinterpret_cast<hipStream_t>(stream));
+                                            reinterpret_cast<hipStream_t>(stream), d_zero, zero_floats);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_spmm_sparse_upstream_blocks: ") + hipGetErrorString(e));
   return FR_OK;
 }
@@ -1161,10 +1205,24 @@ extern "C" int fr_spmm_sparse_upstream_rect(const int64_t* d_rowptr, const int32
   return FR_OK;
 }
 
+extern "C" int fr_spmm_sparse_upstream_zero(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                            int64_t n_rows, const uint32_t* d_bits, const float* d_X, int64_t ldx,
+                                            int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1,
+                                            float beta1, float* d_zero, int64_t zero_floats, void* stream);
+
 extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
                                        int64_t n_rows, const uint32_t* d_bits, const float* d_X, int64_t ldx,
                                        int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1, float beta1,
                                        void* stream) {
+  return fr_spmm_sparse_upstream_zero(d_rowptr, d_col, d_val, n_rows, d_bits, d_X, ldx, split, Y2, alpha, A1, beta1,
+                                      nullptr, 0, stream);
+}
+
+extern "C" int fr_spmm_sparse_upstream_zero(const int64_t* d_rowptr, const int32_t* d_col, const float* d_val,
+                                            int64_t n_rows, const uint32_t* d_bits, const float* d_X, int64_t ldx,
+                                            int64_t split, const fr_tab* Y2, float alpha, const fr_tab* A1,
+                                            float beta1, float* d_zero, int64_t zero_floats, void* stream) {
+  if (int rc = sparse_zero_check(d_zero, zero_floats)) return rc;
   FR_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX, "n_rows out of range");
   if (n_rows == 0) return FR_OK;
   FR_REQUIRE(d_rowptr && d_col && d_val && d_bits && d_X && Y2 && Y2->lo, "null operand");
@@ -1179,13 +1237,15 @@ extern "C" int fr_spmm_sparse_upstream(const int64_t* d_rowptr, const int32_t* d
   // bitmask staged in LDS only while it is small next to a block's edge range: each of the
   // ceil(n / 64) blocks would copy all of it (HealthRec's UI graph: 14.3 KB per block against ~6 KB
   // of col / val; the L1-resident global lookups are 4.4 us faster per launch there)
+  float4* z4 = reinterpret_cast<float4*>(d_zero);
   if (nwords <= kSpStageWords)
     hipLaunchKernelGGL(spmm_sparse_kernel<false>, grid, dim3(256), (size_t)nwords * sizeof(uint32_t),
                        reinterpret_cast<hipStream_t>(stream), d_rowptr, d_col, d_val, n_rows, d_bits, nwords,
-                       reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
+                       reinterpret_cast<const float4*>(d_X), ldx / 4, ep, nullptr, z4, zero_floats / 4);
   else
     hipLaunchKernelGGL(spmm_sparse_kernel<true>, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_rowptr,
-                       d_col, d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep);
+                       d_col, d_val, n_rows, d_bits, nwords, reinterpret_cast<const float4*>(d_X), ldx / 4, ep, nullptr,
+                       z4, zero_floats / 4);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }

@@ -855,7 +855,9 @@ def test_spmm_sparse_upstream(cuda, frac, planned, monkeypatch):
     ref = torch.empty(n, d, device=cuda)
     ops.spmm_launch(adj, Xz, Y2=ref, alpha=0.5, A1=Xz, beta1=0.5)
     lo, hi = torch.full((split, d), 7.0, device=cuda), torch.full((n - split, d), 7.0, device=cuda)
-    ops.spmm_sparse_upstream(adj, bits, X, lo, hi, split, alpha=0.5, beta1=0.5)
+    side = torch.full((777, 64), 3.0, device=cuda)  # the launch's side job zeroes it (no memset node)
+    ops.spmm_sparse_upstream(adj, bits, X, lo, hi, split, alpha=0.5, beta1=0.5, zero=side)
+    assert not side.any()
     got = torch.cat([lo, hi])
     assert torch.isfinite(got).all()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
