@@ -461,6 +461,9 @@ int fr_adam_catch_up_slice(int n_tables, float* const* params, float* const* exp
                            const int64_t* const* d_steps, const int64_t* rows, const int32_t* row_dims,
                            int32_t* const* d_last, const float* const* d_hist, int32_t n_slices, int32_t hist_cap,
                            double beta1, double beta2, double eps, double weight_decay, void* stream);
+/* A/B switch (library state): the background slice on at most max_blocks workgroups in total, each
+ * striding over its rows (0, the default: one wave per row). */
+int fr_adam_slice_blocks(int64_t max_blocks);
 /* the same slice in n_parts launches: part p replays the p-th of n_parts even row ranges of the step's
  * slice (a step issues every part, at points of its choosing, before the optimiser's lazy kernels) */
 int fr_adam_catch_up_slice_part(int n_tables, float* const* params, float* const* exp_avg,

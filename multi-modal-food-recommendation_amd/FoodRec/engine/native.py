@@ -90,6 +90,7 @@ _SIGS = {
                                                     POINTER(FrTab), c_float, c_void_p, c_int64, c_void_p, c_int64,
                                                     c_void_p, c_int64, c_void_p]),
     "fr_spmm_sparse_block_rows": (c_int, []),
+    "fr_adam_slice_blocks": (c_int, [c_int64]),
     "fr_spmm_plan_status": (c_int, [c_int]),
     "fr_graph_bpr_finish": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                     c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -326,6 +327,9 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # FR_SLICE_BLOCKS=N: the lazy-Adam background slice on at most N workgroups (A/B; 0: one wave per row)
+        if os.environ.get("FR_SLICE_BLOCKS") is not None:
+            check(handle.fr_adam_slice_blocks(int(os.environ["FR_SLICE_BLOCKS"])), "fr_adam_slice_blocks")
         # FR_SSL_MFMA=0: the VALU forms of the dCor / InfoNCE Gram tiles (A/B of the two kernel sets)
         if os.environ.get("FR_SSL_MFMA") is not None:
             handle.fr_ssl_kernels(int(os.environ["FR_SSL_MFMA"] != "0"))

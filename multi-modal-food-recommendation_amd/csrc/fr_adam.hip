@@ -604,9 +604,9 @@ __global__ __launch_bounds__(256) void adam_catch_up_slice_kernel(CatchArgs a, i
   const int64_t s = st % nslices;
   const int64_t lo0 = R * s / nslices, hi0 = R * (s + 1) / nslices;
   const int64_t lo = lo0 + (hi0 - lo0) * part / nparts, hi = lo0 + (hi0 - lo0) * (part + 1) / nparts;
-  const int64_t r = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= hi) return;
-  catch_up_at(a.p[t], a.m[t], a.v[t], st, r, a.rshift[t], a.last[t], a.hist[t], cap, h);
+  // one wave per row; a capped grid (fr_adam_slice_blocks) strides over the slice
+  for (int64_t r = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < hi; r += (int64_t)gridDim.x * 4)
+    catch_up_at(a.p[t], a.m[t], a.v[t], st, r, a.rshift[t], a.last[t], a.hist[t], cap, h);
 }
 
 __device__ __forceinline__ void catch_up_at(float* __restrict__ P0, float* __restrict__ M0, float* __restrict__ V0,
@@ -959,6 +959,15 @@ extern "C" int fr_adam_catch_up_rows_multi(int n_tables, float* const* params, f
   return FR_OK;
 }
 
+// A/B: the background slice's grid capped at this many workgroups in total (0: one wave per row)
+static int64_t g_slice_blocks = 0;
+
+extern "C" int fr_adam_slice_blocks(int64_t max_blocks) {
+  FR_REQUIRE(max_blocks >= 0, "max_blocks must be >= 0");
+  g_slice_blocks = max_blocks;
+  return FR_OK;
+}
+
 extern "C" int fr_adam_catch_up_slice_part(int n_tables, float* const* params, float* const* exp_avg,
                                            float* const* exp_avg_sq, const int64_t* const* d_steps, const int64_t* rows,
                                            const int32_t* row_dims, int32_t* const* d_last, const float* const* d_hist,
@@ -978,7 +987,9 @@ extern "C" int fr_adam_catch_up_slice_part(int n_tables, float* const* params, f
     most = std::max<int64_t>(most, fr::ceil_div(fr::ceil_div(rows[t], (int64_t)n_slices), (int64_t)n_parts));
   if (most == 0) return FR_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(adam_catch_up_slice_kernel, dim3((unsigned)fr::ceil_div(most + 1, 4), (unsigned)n_tables),
+  int64_t gx = fr::ceil_div(most + 1, 4);
+  if (g_slice_blocks > 0) gx = std::min<int64_t>(gx, std::max<int64_t>(1, g_slice_blocks / n_tables));
+  hipLaunchKernelGGL(adam_catch_up_slice_kernel, dim3((unsigned)gx, (unsigned)n_tables),
                      dim3(256), 0, s, a, n_slices, hist_cap, h, part, n_parts);
   FR_LAUNCH_CHECK();
   return FR_OK;
