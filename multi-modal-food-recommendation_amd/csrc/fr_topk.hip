@@ -50,6 +50,12 @@ constexpr int kUsersPerWG = kWaves * 32;
 constexpr int kTile = 32;      // items per staged tile
 constexpr int kKMax = 32;      // largest k
 constexpr int kAppendDepth = 2;  // APPEND's register stages of item tiles (1 or 2)
+#ifndef FR_TOPK_PIPE
+#define FR_TOPK_PIPE 1
+#endif
+// APPEND: the candidate masks of tile t - 1 are formed between tile t's MFMAs (the matrix pipe
+// runs while the VALU compares), only the rare append passes stay outside the MFMA stream
+constexpr bool kAppendPipe = FR_TOPK_PIPE != 0;
 
 template <typename T, int D, int NB = 1>
 struct Cfg {
@@ -196,6 +202,10 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   for (int s = 0; s < NBF; ++s) asm volatile("" ::"v"(__builtin_bit_cast(i32x4, bf[s])));
   // APPEND: this user's threshold and this lane's region
   const float thr_u = MODE == kAppend && uvalid ? a.thr[slot] : -INFINITY;
+  // (read by an asm too: the counted waits are placed by the compiler, which does not see the
+  // vmcnt(0) below -- without this it waits for every load in flight, the item-tile prefetch
+  // included, before the threshold's first use in each pass of the tile loop)
+  asm volatile("" ::"v"(thr_u));
   const int64_t region = (slot * a.n_splits + sp) * 2 + h;
   int cnt = 0;
 
@@ -221,17 +231,19 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   for (int c = 0; c < NSH; ++c) {
     const int x = tid + c * kThreads;
     const int row = x / C::CPR, cc = x % C::CPR;
-    srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;  // rows past the tile never load
+    srow[c] = x < C::TILE * C::CPR ? row : 1 << 30;  // rows past the tile are never stored
     sdst[c] = (row * C::CPR + swz<T, D>(row, cc)) * 16;
-    ssrc[c] = reinterpret_cast<const char*>(It) + ((i_lo + row) * ldi) * (int64_t)sizeof(T) + cc * 16;
+    ssrc[c] = reinterpret_cast<const char*>(It) + (i_lo * ldi) * (int64_t)sizeof(T) + cc * 16;
   }
-  const int64_t tile_bytes = (int64_t)C::TILE * ldi * (int64_t)sizeof(T);
+  const uint32_t row_bytes = (uint32_t)(ldi * (int64_t)sizeof(T));
+  const int n_split = (int)(i_hi - i_lo);
 #define FR_LOAD_TILE(T_, S_)                                                                        \
   _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
     if constexpr (MODE == kAppend) {                                                                \
-      const int64_t item = i_lo + (int64_t)(T_) * C::TILE + srow[c];                                \
-      S_[c] = item < i_hi ? *reinterpret_cast<const uint4*>(ssrc[c] + (int64_t)(T_) * tile_bytes)   \
-                           : make_uint4(0, 0, 0, 0);                                                \
+      /* unconditional (rows past the split re-read its last row; their scores are dropped): */     \
+      /* with no load skipped on any path the compiler's counted waits stay exact */                \
+      const int rr = min((T_) * C::TILE + min(srow[c], C::TILE - 1), n_split - 1);                 \
+      S_[c] = __builtin_bit_cast(uint4, *reinterpret_cast<const i32x4*>(ssrc[c] + (uint64_t)(uint32_t)rr * row_bytes)); \
     } else {                                                                                        \
       const int x = tid + c * kThreads;                                                             \
       S_[c] = make_uint4(0, 0, 0, 0);                                                               \
@@ -270,25 +282,92 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   // hold the registers)
   constexpr int DEPTH = MODE == kAppend ? kAppendDepth : 1;
   uint4 stgA[C::CH], stgB[DEPTH == 2 ? C::CH : 1];
-  if (n_tiles > 0) {
+  if constexpr (MODE == kAppend) {
+    if (n_tiles <= 0) {  // an empty split: no rows to clamp to
+      if (uvalid) a.cc[region] = 0;
+      return;
+    }
     FR_LOAD_TILE(0, stgA)
     FR_STORE_TILE(0, stgA)
+    __syncthreads();
+    FR_LOAD_TILE(1, stgA)
+    if constexpr (DEPTH == 2) { FR_LOAD_TILE(2, stgB) }
+  } else {
+    if (n_tiles > 0) {
+      FR_LOAD_TILE(0, stgA)
+      FR_STORE_TILE(0, stgA)
+    }
+    __syncthreads();
+    if (n_tiles > 1) { FR_LOAD_TILE(1, stgA) }
   }
-  __syncthreads();
-  if (n_tiles > 1) { FR_LOAD_TILE(1, stgA) }
-  if constexpr (DEPTH == 2) {
-    if (n_tiles > 2) { FR_LOAD_TILE(2, stgB) }
-  }
-  // one tile: its scores and selection from LDS buffer t & 1, then the next tile (in `cur`) into the
-  // other buffer, and `cur` refilled DEPTH + 1 tiles ahead
-  auto tile_step = [&](const int t, uint4 (&cur)[C::CH]) {
+  // APPEND: the threshold of an invalid slot is NaN (no score passes any compare)
+  const float wv = uvalid ? thr_u : __builtin_nanf("");
+  // this lane's candidate bits of one block's 16 scores (branch-free: VALU only)
+  auto cand_mask = [&](const f32x16& av) __attribute__((always_inline)) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m |= av[j] >= wv ? (1u << j) : 0u;
+    return m;
+  };
+  // selection of one block (scores av, items ib + (j&3) + 8(j>>2)) given its candidate bits
+  auto select_block = [&](const f32x16& av, uint32_t mask, const int64_t ib, const float wf)
+                          __attribute__((always_inline)) {
+    if (ib + 28 >= i_hi) {  // the split's last block: drop items past its end
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
+    }
+    if (!uvalid) mask = 0u;
+    // every lane handles its next candidate in the same pass
+    while (__ballot(mask != 0u)) {
+      const bool act = mask != 0u;
+      const int j = act ? __builtin_ctz(mask) : 0;
+      mask &= mask - 1u;
+      const float v0 = (j & 1) ? av[1] : av[0], v1 = (j & 1) ? av[3] : av[2];
+      const float v2 = (j & 1) ? av[5] : av[4], v3 = (j & 1) ? av[7] : av[6];
+      const float v4 = (j & 1) ? av[9] : av[8], v5 = (j & 1) ? av[11] : av[10];
+      const float v6 = (j & 1) ? av[13] : av[12], v7 = (j & 1) ? av[15] : av[14];
+      const float w0 = (j & 2) ? v1 : v0, w1 = (j & 2) ? v3 : v2, w2 = (j & 2) ? v5 : v4, w3 = (j & 2) ? v7 : v6;
+      const float x0 = (j & 4) ? w1 : w0, x1 = (j & 4) ? w3 : w2;
+      const float sc = (j & 8) ? x1 : x0;
+      const int64_t item = (ib + (j & 3) + 8 * (j >> 2)) * a.item_mul;
+      if constexpr (MODE == kList) {
+        const uint64_t kk = ((uint64_t)fr_ord(sc) << 32) | (uint32_t)(~(uint32_t)item);
+        if (act && kk > key[KC - 1] && !ex.test(item)) {
+          // one bubble pass: the new key sinks to its place, the old minimum falls off the end
+          uint64_t x = kk;
+#pragma unroll
+          for (int q = 0; q < KC; ++q) {
+            const uint64_t cur = key[q];
+            const bool gt = x > cur;
+            key[q] = gt ? x : cur;
+            x = gt ? cur : x;
+          }
+        }
+      } else {
+        if (act) {
+          if (cnt < a.cap) {
+            a.cs[region * a.cap + cnt] = sc;
+            a.ci[region * a.cap + cnt] = (int32_t)item;
+          }
+          ++cnt;
+        }
+      }
+    }
+  };
+  constexpr bool PIPE = MODE == kAppend && kAppendPipe;
+  // one tile: its scores from LDS buffer t & 1 into `acc` -- with PIPE the previous tile's scores
+  // (`prev`) are selected after them, their masks formed between the MFMAs; without, this tile's
+  // own -- then the next tile (in `cur`) into the other buffer, and `cur` refilled DEPTH + 1 ahead
+  auto tile_step = [&](const int t, uint4 (&cur)[C::CH], f32x16 (&acc)[NB], const f32x16 (&prev)[NB])
+                       __attribute__((always_inline)) {
     // ---- scores of this tile on the matrix cores (NB independent 32-item blocks)
     const char* abuf = smem + (t & 1) * C::STAGE;
-    f32x16 acc[NB];
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
+    uint32_t pmask[NB];
     if constexpr (C::BF) {
       // the tile's A fragments are read ahead of the MFMA chains that consume them in order
       bf16x8 af[NB][C::KS];
@@ -302,15 +381,26 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[s], acc[bb], 0, 0, 0);
-      // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight)
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
+      }
+      // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight);
+      // PIPE: the previous tile's compares spread over the MFMA slots
+      constexpr int NM = NB * C::KS;
+      constexpr int VPM = PIPE ? (NB * 40 + NM - 1) / NM : 0;  // VALU per MFMA slot
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-      for (int s = 0; s < NB * C::KS - 4; ++s) {
+      for (int s = 0; s < NM - 4; ++s) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if constexpr (VPM > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      for (int s = 0; s < 4; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if constexpr (VPM > 0) __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+      }
     } else {
 #pragma unroll
       for (int sg = 0; sg < C::KS / 4; ++sg) {
@@ -323,77 +413,66 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[sg].w, acc[bb], 0, 0, 0);
         }
       }
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
+      }
     }
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
-      // ---- this lane's 16 scores of block bb: user `slot`, items ib + (j&3) + 8(j>>2) + 4h
-      const int64_t ib = i_lo + (int64_t)t * C::TILE + bb * 32 + 4 * h;
-      float wf;
-      if constexpr (MODE == kList) {
-        const uint32_t wsc = (uint32_t)(key[KC - 1] >> 32);
-        wf = wsc < 0x00800000u ? -INFINITY : fr_unord(wsc);  // the list's worst score (empty: -inf)
+      if constexpr (PIPE) {
+        // the previous tile's block bb (t - 1 < 0: its scores are NaN, no bit set)
+        select_block(prev[bb], pmask[bb], i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
       } else {
-        wf = thr_u;
-      }
-      const f32x16 av = acc[bb];
-      uint32_t mask = 0u;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) mask |= av[j] >= wf ? (1u << j) : 0u;
-      if (ib + 28 >= i_hi) {  // the split's last block: drop items past its end
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
-      }
-      if (!uvalid) mask = 0u;
-      // every lane handles its next candidate in the same pass
-      while (__ballot(mask != 0u)) {
-        const bool act = mask != 0u;
-        const int j = act ? __builtin_ctz(mask) : 0;
-        mask &= mask - 1u;
-        const float v0 = (j & 1) ? av[1] : av[0], v1 = (j & 1) ? av[3] : av[2];
-        const float v2 = (j & 1) ? av[5] : av[4], v3 = (j & 1) ? av[7] : av[6];
-        const float v4 = (j & 1) ? av[9] : av[8], v5 = (j & 1) ? av[11] : av[10];
-        const float v6 = (j & 1) ? av[13] : av[12], v7 = (j & 1) ? av[15] : av[14];
-        const float w0 = (j & 2) ? v1 : v0, w1 = (j & 2) ? v3 : v2, w2 = (j & 2) ? v5 : v4, w3 = (j & 2) ? v7 : v6;
-        const float x0 = (j & 4) ? w1 : w0, x1 = (j & 4) ? w3 : w2;
-        const float sc = (j & 8) ? x1 : x0;
-        const int64_t item = (ib + (j & 3) + 8 * (j >> 2)) * a.item_mul;
+        // ---- this lane's 16 scores of block bb: user `slot`, items ib + (j&3) + 8(j>>2) + 4h
+        const int64_t ib = i_lo + (int64_t)t * C::TILE + bb * 32 + 4 * h;
+        float wf;
         if constexpr (MODE == kList) {
-          const uint64_t kk = ((uint64_t)fr_ord(sc) << 32) | (uint32_t)(~(uint32_t)item);
-          if (act && kk > key[KC - 1] && !ex.test(item)) {
-            // one bubble pass: the new key sinks to its place, the old minimum falls off the end
-            uint64_t x = kk;
-#pragma unroll
-            for (int q = 0; q < KC; ++q) {
-              const uint64_t cur = key[q];
-              const bool gt = x > cur;
-              key[q] = gt ? x : cur;
-              x = gt ? cur : x;
-            }
-          }
+          const uint32_t wsc = (uint32_t)(key[KC - 1] >> 32);
+          wf = wsc < 0x00800000u ? -INFINITY : fr_unord(wsc);  // the list's worst score (empty: -inf)
         } else {
-          if (act) {
-            if (cnt < a.cap) {
-              a.cs[region * a.cap + cnt] = sc;
-              a.ci[region * a.cap + cnt] = (int32_t)item;
-            }
-            ++cnt;
-          }
+          wf = thr_u;
         }
+        const f32x16 av = acc[bb];
+        uint32_t mask = 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mask |= av[j] >= wf ? (1u << j) : 0u;
+        select_block(av, mask, ib, wf);
       }
     }
     // ---- next tile into the other buffer; prefetch DEPTH + 1 tiles ahead into the freed stage
-    if (t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
+    // (APPEND: unconditionally -- past the last tile the stores go to a buffer no one reads again
+    // and the loads re-read the split's last row)
+    if (MODE == kAppend || t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
     __syncthreads();
-    if (t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
+    if (MODE == kAppend || t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
   };
+  f32x16 accX[NB], accY[PIPE ? NB : 1];
+  if constexpr (PIPE) {
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) accY[bb][j] = __builtin_nanf("");
+  }
   if constexpr (DEPTH == 2) {
-    for (int t = 0; t < n_tiles; t += 2) {
-      tile_step(t, stgA);
-      if (t + 1 < n_tiles) tile_step(t + 1, stgB);
+    // an odd tile count runs one tile past the split: all its items are dropped by the i_hi test
+    int t = 0;
+    for (; t < n_tiles; t += 2) {
+      if constexpr (PIPE) {
+        tile_step(t, stgA, accX, accY);
+        tile_step(t + 1, stgB, accY, accX);
+      } else {
+        tile_step(t, stgA, accX, accX);
+        tile_step(t + 1, stgB, accX, accX);
+      }
+    }
+    if constexpr (PIPE) {  // the last tile (t - 1)
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb)
+        select_block(accY[bb], cand_mask(accY[bb]), i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
     }
   } else {
-    for (int t = 0; t < n_tiles; ++t) tile_step(t, stgA);
+    for (int t = 0; t < n_tiles; ++t) tile_step(t, stgA, accX, accX);
   }
 #undef FR_LOAD_TILE
 #undef FR_STORE_TILE
@@ -428,38 +507,75 @@ struct MergeArgs {
   int32_t* flag_list; int32_t* flag_cnt;                      // overflowed users -> exact recompute
 };
 
-// One wave per user: each lane streams a strided share of the user's candidates (all regions)
+// One wave per user: each lane streams a strided share of the user's candidates (all regions,
+// concatenated through a prefix sum of their counts in LDS; kMergeBatch loads in flight per lane)
 // into a private sorted register list (bubble insertion, as the LIST kernel), then k rounds of a
 // wave arg-max over the lanes' list heads emit the top-k in order (the winner lane pops its
 // head); finally the hit flags against the user's held-out CSR row.
+constexpr int kMergeBatch = 8;
+constexpr int kMergeMaxRegions = 128;  // 2 x the largest split count
 template <int KC>
 __global__ __launch_bounds__(256) void topk_merge_kernel(MergeArgs a) {
+  __shared__ int pre_all[4][kMergeMaxRegions + 1];
   const int lane = threadIdx.x & 63;
+  int* pre = pre_all[threadIdx.x >> 6];
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t n_users = a.d_nu ? (int64_t)*a.d_nu : a.n_users;
   if (u >= n_users) return;
   const int64_t orow = a.urows ? (int64_t)a.urows[u] : u;
   const int64_t base = u * (int64_t)a.n_regions * a.cap;
-  if (a.cnt) {
-    bool over = false;
-    for (int g = lane; g < a.n_regions; g += 64) over |= a.cnt[u * a.n_regions + g] > a.cap;
-    if (__ballot(over)) {
-      if (lane == 0) a.flag_list[atomicAdd(a.flag_cnt, 1)] = (int32_t)orow;
-      return;
+  // region counts -> exclusive prefix (pre[g] = first candidate of region g, pre[n_regions] = total)
+  bool over = false;
+  int carry = 0;
+  for (int g0 = 0; g0 < a.n_regions; g0 += 64) {
+    const int g = g0 + lane;
+    int c = g < a.n_regions ? (a.cnt ? a.cnt[u * a.n_regions + g] : a.cap) : 0;
+    over |= c > a.cap;
+    c = min(c, a.cap);
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
     }
+    if (g < a.n_regions) pre[g + 1] = carry + incl;
+    carry += __shfl(incl, 63, 64);
   }
+  if (lane == 0) pre[0] = 0;
+  if (a.cnt && __ballot(over)) {
+    if (lane == 0) a.flag_list[atomicAdd(a.flag_cnt, 1)] = (int32_t)orow;
+    return;
+  }
+  const int total = carry;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   Excl ex;
   ex.init(a.ex_ptr, a.ex_col, a.ex_base, a.uid ? a.uid[orow] : orow);
   uint64_t key[KC];
 #pragma unroll
   for (int q = 0; q < KC; ++q) key[q] = 0ull;
-  for (int g = 0; g < a.n_regions; ++g) {
-    const int c = a.cnt ? a.cnt[u * a.n_regions + g] : a.cap;
-    const int64_t rb = base + (int64_t)g * a.cap;
-    for (int e = lane; e < c; e += 64) {
-      const int i = a.pi[rb + e];
+  int g = 0;  // this lane's current region (its candidate indices only grow)
+  for (int e0 = 0; e0 < total; e0 += 64 * kMergeBatch) {
+    int ci[kMergeBatch];
+    float cs[kMergeBatch];
+#pragma unroll
+    for (int b = 0; b < kMergeBatch; ++b) {
+      const int e = e0 + 64 * b + lane;
+      ci[b] = INT32_MAX;
+      cs[b] = 0.f;
+      if (e < total) {
+        while (pre[g + 1] <= e) ++g;
+        const int64_t o = base + (int64_t)g * a.cap + (e - pre[g]);
+        ci[b] = a.pi[o];
+        cs[b] = a.ps[o];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kMergeBatch; ++b) {
+      const int i = ci[b];
       if (i == INT32_MAX) continue;
-      const uint64_t kk = ((uint64_t)fr_ord(a.ps[rb + e]) << 32) | (uint32_t)(~(uint32_t)i);
+      const uint64_t kk = ((uint64_t)fr_ord(cs[b]) << 32) | (uint32_t)(~(uint32_t)i);
       if (kk > key[KC - 1] && !ex.test(i)) {
         uint64_t x = kk;
 #pragma unroll
@@ -512,6 +628,7 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(MergeArgs a) {
 }
 
 hipError_t launch_merge(const MergeArgs& m, unsigned blocks, hipStream_t s) {
+  if (m.n_regions > kMergeMaxRegions) return hipErrorInvalidValue;  // (split_plan keeps <= 64 splits)
   auto kern = m.k <= 10 ? topk_merge_kernel<10> : (m.k <= 20 ? topk_merge_kernel<20> : topk_merge_kernel<32>);
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, m);
   return hipGetLastError();
