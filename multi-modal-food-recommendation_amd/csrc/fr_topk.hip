@@ -17,13 +17,16 @@
 //     XOR swizzle (conflict-free ds_read_b128 A fragments); item rows read once per workgroup.
 //   * XCD-aware block order: workgroups of one XCD take consecutive (user tile, split) ids, so
 //     the user tiles sharing an item range share that XCD's L2.
-// Selection, for large item counts, in three launches (exact for any data):
-//   1. LIST kernel on a strided item sample (every s-th item, s <= 64): exact per-user top-k of
-//      the sample -> the user's threshold T_u = its k-th best admissible sample score, a lower
-//      bound of the k-th best over all items.
-//   2. APPEND kernel over all items: the GEMM plus a compare against T_u; the few scores >= T_u
+// Selection, for large item counts (exact for any data):
+//   1. LIST kernel on a sparse strided sub-sample (every s0-th item, s0 = 16 s): exact per-user
+//      top-k -> T0_u = its k-th best admissible score, a lower bound of the k-th best overall.
+//   2. APPEND kernel over the sample (every s-th item, s <= 16) against T0_u, then MERGE -> T_u =
+//      the sample's k-th best admissible score (~k*16 candidates per user; a user whose regions
+//      overflow keeps T0_u, looser but still a lower bound).  (Round 5 took T_u from a LIST pass
+//      over a 64-stride sample: its per-lane insertions cost more than these two launches.)
+//   3. APPEND kernel over all items: the GEMM plus a compare against T_u; the few scores >= T_u
 //      (expected ~k*s per user) are appended to per-(user, split, lane-half) regions.
-//   3. MERGE: per user, the top-k of its admissible candidates by (score desc, item id asc); the
+//   4. MERGE: per user, the top-k of its admissible candidates by (score desc, item id asc); the
 //      exclusion (history mask) is tested here, once per candidate, off the GEMM's path.
 //   A region that overflows its capacity (adversarial score orders) flags its user; flagged users
 //   are recomputed by the LIST kernel over all items and merged again (launches that exit at once
@@ -505,6 +508,7 @@ struct MergeArgs {
   float* thr_out;                                              // write the k-th best score only
   const int64_t* ex_ptr; const int32_t* ex_col; int64_t ex_base;  // exclusion applied here (APPEND input)
   int32_t* flag_list; int32_t* flag_cnt;                      // overflowed users -> exact recompute
+  const float* thr_fb;  // threshold stage: an overflowed user keeps this (looser) lower bound instead
 };
 
 // One wave per user: each lane streams a strided share of the user's candidates (all regions,
@@ -543,7 +547,10 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(MergeArgs a) {
   }
   if (lane == 0) pre[0] = 0;
   if (a.cnt && __ballot(over)) {
-    if (lane == 0) a.flag_list[atomicAdd(a.flag_cnt, 1)] = (int32_t)orow;
+    if (lane == 0) {
+      if (a.thr_fb) a.thr_out[orow] = a.thr_fb[orow];
+      else a.flag_list[atomicAdd(a.flag_cnt, 1)] = (int32_t)orow;
+    }
     return;
   }
   const int total = carry;
@@ -673,15 +680,26 @@ void split_plan(int64_t n_users, int64_t n_items, int* n_splits, int64_t* span) 
 }
 
 constexpr int64_t kSampledMinItems = 32768;  // below this: one exact LIST pass
+#ifndef FR_TOPK_SUB
+#define FR_TOPK_SUB 16
+#endif
+constexpr int64_t kSubRatio = FR_TOPK_SUB;   // sub-sample stride / sample stride
 
 // The launch plan and the workspace carve-up (identical in the size query and the call).
 struct Plan {
   bool sampled;
-  int64_t stride, n_sample;
-  int ns1, ns2, cap;
-  int64_t span1, span2;
+  int64_t stride, n_sample, stride0, n_sub;
+  int ns0, ns1, ns2, cap1, cap;
+  int64_t span0, span1, span2;
+  int64_t off_l0, off_thr1, off_cs1, off_ci1, off_cc1;
   int64_t off_l1, off_thr, off_cs, off_ci, off_cc, off_flag, off_l2, total;
 };
+
+// region capacity: candidates per user ~ NegBinomial(k, 1/ratio) (mean k * ratio) over n_regions;
+// room for ~4x the mean plus the long tail of small k (overflow only costs time)
+int region_cap(int k, int64_t ratio, int n_regions) {
+  return (int)std::min<int64_t>(1 << 16, std::max<int64_t>(256, (4 * k + 32) * ratio / n_regions));
+}
 
 Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   Plan p{};
@@ -692,13 +710,23 @@ Plan make_plan(int64_t n_users, int64_t n_items, int k) {
     p.off_l1 = take(n_users * p.ns2 * 2 * (int64_t)k * 8);
     return p;
   }
-  p.stride = std::min<int64_t>(64, std::max<int64_t>(2, n_items / 4096));
+  // thresholds in two levels: the exact top-k of a sub-sample (every stride0-th item, LIST) bounds
+  // an APPEND pass over the sample (every stride-th item) whose merged top-k gives the threshold of
+  // the APPEND pass over all items (~k * stride candidates per user)
+  p.stride = std::min<int64_t>(16, std::max<int64_t>(2, n_items / 65536));
   p.n_sample = fr::ceil_div(n_items, p.stride);
+  p.stride0 = p.stride * kSubRatio;
+  p.n_sub = fr::ceil_div(n_items, p.stride0);
+  split_plan(n_users, p.n_sub, &p.ns0, &p.span0);
   split_plan(n_users, p.n_sample, &p.ns1, &p.span1);
-  // candidates per user ~ NegBinomial(k, 1/stride): mean k*stride, spread over 2*ns2 regions;
-  // room for ~4x the mean plus the long tail of small k (overflow only costs time: exact pass)
-  p.cap = (int)std::min<int64_t>(1 << 16, std::max<int64_t>(256, (4 * k + 32) * p.stride / (2 * p.ns2)));
-  p.off_l1 = take(n_users * p.ns1 * 2 * (int64_t)k * 8);
+  p.cap1 = region_cap(k, kSubRatio, 2 * p.ns1);
+  p.cap = region_cap(k, p.stride, 2 * p.ns2);
+  p.off_l0 = take(n_users * p.ns0 * 2 * (int64_t)k * 8);
+  p.off_thr1 = take(n_users * 4);
+  const int64_t nreg1 = n_users * p.ns1 * 2;
+  p.off_cs1 = take(nreg1 * p.cap1 * 4);
+  p.off_ci1 = take(nreg1 * p.cap1 * 4);
+  p.off_cc1 = take(nreg1 * 4);
   p.off_thr = take(n_users * 4);
   const int64_t nreg = n_users * p.ns2 * 2;
   p.off_cs = take(nreg * p.cap * 4);
@@ -706,6 +734,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   p.off_cc = take(nreg * 4);
   p.off_flag = take((n_users + 1) * 4);
   p.off_l2 = take(n_users * p.ns2 * 2 * (int64_t)k * 8);
+  p.off_l1 = p.off_l2;  // (unused)
   return p;
 }
 
@@ -756,12 +785,17 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   ma.out_s = d_out_scores; ma.out_i = d_out_items; ma.hits = d_hits;
   hipError_t e;
 
-  // exact LIST pass over `items` (stride item_mul) then a merge into the outputs or thresholds
+  // exact LIST pass over `items` (stride item_mul) then a merge into the outputs or thresholds.
+  // A threshold pass leaves the exclusion to its merge: the k-th best admissible entry of the
+  // union of the lanes' unfiltered top-k lists is still k admissible items' worst -- a lower bound
+  // of the user's k-th best admissible score (-inf if fewer remain) -- and the LIST kernel then
+  // never stalls its wave on a candidate's CSR-row bisection.
   auto list_pass = [&](const void* It, int64_t ld, int64_t n_it, int64_t mul, int ns, int64_t span, char* lists,
                        const int32_t* urows, const int32_t* d_nu, float* thr_out) -> hipError_t {
     ScoreArgs l = sa;
     l.It = It; l.ldi = ld; l.n_items = n_it; l.item_mul = mul; l.n_splits = ns; l.span = span;
     l.urows = urows; l.d_nu = d_nu;
+    if (thr_out) l.ex_ptr = nullptr;
     l.ls = reinterpret_cast<float*>(lists);
     l.li = reinterpret_cast<int32_t*>(lists + n_users * ns * 2 * (int64_t)k * 4);
     hipError_t err = launch_score<kList>(dtype, d, l, s);
@@ -769,6 +803,7 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
     MergeArgs m = ma;
     m.ps = l.ls; m.pi = l.li; m.cnt = nullptr; m.cap = k; m.n_regions = 2 * ns;
     m.d_nu = d_nu; m.urows = urows; m.thr_out = thr_out;
+    if (thr_out) { m.ex_ptr = d_ex_ptr; m.ex_col = d_ex_col; m.ex_base = ex_base; }
     return launch_merge(m, merge_blocks, s);
   };
 
@@ -777,13 +812,32 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
     if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
     return FR_OK;
   }
+  FR_REQUIRE(ldi * p.stride0 * es < INT32_MAX, "item row stride too large for the sampled passes");
+  float* thr1 = reinterpret_cast<float*>(ws + p.off_thr1);
   float* thr = reinterpret_cast<float*>(ws + p.off_thr);
   int32_t* flag_cnt = reinterpret_cast<int32_t*>(ws + p.off_flag);
   int32_t* flag_list = flag_cnt + 1;
-  // 1. thresholds from the exact top-k of every stride-th item
-  e = list_pass(d_I, ldi * p.stride, p.n_sample, p.stride, p.ns1, p.span1, ws + p.off_l1, nullptr, nullptr, thr);
+  // 1. a lower bound of every user's k-th best: the exact top-k of every stride0-th item
+  e = list_pass(d_I, ldi * p.stride0, p.n_sub, p.stride0, p.ns0, p.span0, ws + p.off_l0, nullptr, nullptr, thr1);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
-  // 2. all items: GEMM + threshold, candidates appended
+  // 2. the sample's scores above it, merged into its exact top-k: the threshold (an overflowed user
+  //    keeps the sub-sample's bound -- looser, still below its k-th best)
+  ScoreArgs as = sa;
+  as.It = d_I; as.ldi = ldi * p.stride; as.n_items = p.n_sample; as.item_mul = p.stride;
+  as.n_splits = p.ns1; as.span = p.span1;
+  as.thr = thr1; as.cap = p.cap1;
+  as.cs = reinterpret_cast<float*>(ws + p.off_cs1);
+  as.ci = reinterpret_cast<int32_t*>(ws + p.off_ci1);
+  as.cc = reinterpret_cast<int32_t*>(ws + p.off_cc1);
+  e = launch_score<kAppend>(dtype, d, as, s);
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  MergeArgs mt = ma;
+  mt.ps = as.cs; mt.pi = as.ci; mt.cnt = as.cc; mt.cap = p.cap1; mt.n_regions = 2 * p.ns1;
+  mt.ex_ptr = d_ex_ptr; mt.ex_col = d_ex_col; mt.ex_base = ex_base;
+  mt.thr_out = thr; mt.thr_fb = thr1;
+  e = launch_merge(mt, merge_blocks, s);
+  if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  // 3. all items: GEMM + threshold, candidates appended
   ScoreArgs ap = sa;
   ap.It = d_I; ap.ldi = ldi; ap.n_items = n_items; ap.item_mul = 1; ap.n_splits = p.ns2; ap.span = p.span2;
   ap.thr = thr; ap.cap = p.cap;
@@ -792,7 +846,7 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   ap.cc = reinterpret_cast<int32_t*>(ws + p.off_cc);
   e = launch_score<kAppend>(dtype, d, ap, s);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
-  // 3. merge the candidates; overflowed users are listed for the exact pass
+  // 4. merge the candidates; overflowed users are listed for the exact pass
   hipLaunchKernelGGL(topk_zero_kernel, dim3(1), dim3(64), 0, s, flag_cnt);
   FR_LAUNCH_CHECK();
   MergeArgs mc = ma;
@@ -801,7 +855,7 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   mc.ex_ptr = d_ex_ptr; mc.ex_col = d_ex_col; mc.ex_base = ex_base;
   e = launch_merge(mc, merge_blocks, s);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
-  // 4. exact LIST pass + merge for the flagged users (grid sized for all; exits when none)
+  // 5. exact LIST pass + merge for the flagged users (grid sized for all; exits when none)
   e = list_pass(d_I, ldi, n_items, 1, p.ns2, p.span2, ws + p.off_l2, flag_list, flag_cnt, nullptr);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
   return FR_OK;

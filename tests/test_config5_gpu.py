@@ -197,8 +197,9 @@ def test_full_sort_topk_matches_oracle(cuda, dtype, d, n_users, n_items, k):
     (torch.float32, 64, 300, 40000, 32),
 ])
 def test_full_sort_topk_sampled_path(cuda, dtype, d, n_users, n_items, k):
-    """n_items >= 32768: the sampled three-launch path (LIST on a strided sample -> thresholds, APPEND
-    over all items, MERGE) against the oracle's exact top-k (the small cases above take one LIST pass)."""
+    """n_items >= 32768: the sampled path (LIST on a strided sub-sample, APPEND + MERGE over the sample
+    -> thresholds, APPEND over all items, MERGE) against the oracle's exact top-k (the small cases
+    above take one LIST pass)."""
     from FoodRec.engine import ops
     rng = np.random.default_rng(d + n_users + k)
     U = rng.standard_normal((n_users, d)).astype(np.float32)
@@ -211,6 +212,24 @@ def test_full_sort_topk_sampled_path(cuda, dtype, d, n_users, n_items, k):
     s, i, _ = ops.full_sort_topk(torch.from_numpy(U).to(dtype).to(cuda), torch.from_numpy(I).to(dtype).to(cuda), k,
                                  exclude=ex)
     _check_topk(s.cpu().numpy(), i.cpu().numpy(), U, I, k, excl, 1e-5 if dtype == torch.bfloat16 else 2e-6)
+
+
+def test_full_sort_topk_overflow_paths(cuda):
+    """Adversarial score order for the sampled path: the sub-sample (multiples of 32) scores lowest,
+    the rest of the sample (even items) in the middle, odd items highest -- the sample pass's regions
+    overflow (the user keeps the sub-sample's looser threshold), then the all-items pass overflows
+    (the user is recomputed by the exact LIST pass).  Result = the exact top-k."""
+    from FoodRec.engine import ops
+    rng = np.random.default_rng(77)
+    n_users, n_items, d, k = 64, 140000, 64, 20
+    U = (rng.standard_normal((n_users, d)) + 3.0).astype(np.float32)
+    tier = np.where(np.arange(n_items) % 2 == 1, 1.0, np.where(np.arange(n_items) % 32 == 0, -1.0, 0.0))
+    I = (tier[:, None] / d + 0.01 * rng.standard_normal((n_items, d))).astype(np.float32)
+    excl = [rng.choice(n_items, size=rng.integers(0, 40), replace=False).tolist() for _ in range(n_users)]
+    ex = _excl_csr(excl, 0, cuda)
+    s, i, _ = ops.full_sort_topk(torch.from_numpy(U).to(cuda), torch.from_numpy(I).to(cuda), k, exclude=ex)
+    _check_topk(s.cpu().numpy(), i.cpu().numpy(), U, I, k, excl, 2e-6)
+    assert (i.cpu().numpy() % 2 == 1).all()
 
 
 def test_full_sort_topk_no_mask_and_permuted_ids(cuda):
