@@ -225,6 +225,7 @@ constexpr int DCOR_BP = MAXV + 2 * MAXP;  // per means-block partials: sum mean,
 struct DcorWS {
   double* S; float* row; double* mean; double* Abar; double* coef;
   float* P; float* rowm; double* bpart;
+  unsigned* ctr;  // means blocks done (zeroed by the tiles launch; the last block finalizes)
 };
 
 __host__ __device__ inline DcorWS dcor_ws(void* base, int64_t n, int V) {
@@ -241,6 +242,7 @@ __host__ __device__ inline DcorWS dcor_ws(void* base, int64_t n, int V) {
   w.P = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 128 * 4));
   w.rowm = reinterpret_cast<float*>(take((int64_t)DCOR_JS * V * n * 4));
   w.bpart = reinterpret_cast<double*>(take((n + 63) / 64 * DCOR_BP * 8));
+  w.ctr = reinterpret_cast<unsigned*>(take(4));
   return w;
 }
 
@@ -250,7 +252,7 @@ inline int64_t dcor_ws_bytes(int64_t n, int V) {
   auto r = [](int64_t b) { return (b + 255) / 256 * 256; };
   return r(nt * nt * NP * 8) + r((int64_t)V * nt * n * 4) + r((int64_t)V * n * 8) + r(MAXV * 8) +
          r(MAXP * 8) + r((int64_t)DCOR_JS * V * n * 128 * 4) + r((int64_t)DCOR_JS * V * n * 4) +
-         r((n + 63) / 64 * DCOR_BP * 8);
+         r((n + 63) / 64 * DCOR_BP * 8) + r(4);
 }
 
 // distance tile of one view: D[x][y] for the thread's 4x4 block
@@ -288,6 +290,7 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
   const int it = blockIdx.x, jt = blockIdx.y;
   const int ti = threadIdx.x >> 4, tj = threadIdx.x & 15;
   const int NP = V * (V + 1) / 2;
+  if (it == 0 && jt == 0 && threadIdx.x == 0) *ws.ctr = 0u;  // for the means launch's last block
   if (jt < it) {  // below the diagonal: the transposed tile carries it
     if (threadIdx.x < NP) ws.S[((int64_t)it * nt + jt) * NP + threadIdx.x] = 0.0;
     return;
@@ -357,35 +360,53 @@ __global__ __launch_bounds__(256) void dcor_tiles_kernel(Views v, int64_t n, int
 template <int V, int D>
 __global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n, DcorWS ws) {
   constexpr int LD = D + 4;
-  __shared__ __attribute__((aligned(16))) float At[T * LD];
-  __shared__ __attribute__((aligned(16))) float Bt[T * LD];
-  __shared__ float ra[T], rb[T];
-  __shared__ float colp[16][T];
-  __shared__ double red[4];
+  // round 6: every view's i and j tiles staged by one load phase (was one load -> barrier -> compute
+  // round trip per view), the column sums of all views behind one barrier, and all pair sums reduced
+  // together (each in the same order as block_sum_d: wave sums, then waves 0..3)
+  __shared__ __attribute__((aligned(16))) float At[V][T * LD];
+  __shared__ __attribute__((aligned(16))) float Bt[V][T * LD];
+  __shared__ float ra[V][T], rb[V][T];
+  __shared__ float colp[V][16][T];
+  constexpr int NP = V * (V + 1) / 2;
+  __shared__ double red[4][NP];
   const int64_t nt = (n + T - 1) / T;
   const int it = blockIdx.x, jt = blockIdx.y;
   const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
-  constexpr int NP = V * (V + 1) / 2;
+  if (it == 0 && jt == 0 && threadIdx.x == 0) *ws.ctr = 0u;  // for the means launch's last block
   if (jt < it) {  // below the diagonal: the transposed tile carries it
     if (threadIdx.x < NP) ws.S[((int64_t)it * nt + jt) * NP + threadIdx.x] = 0.0;
     return;
   }
   const bool off = jt > it;
+  {
+    const float* src[2 * V];
+    int64_t r0[2 * V];
+    float* dst[2 * V];
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      src[2 * a] = v.x[a]; r0[2 * a] = (int64_t)it * T; dst[2 * a] = At[a];
+      src[2 * a + 1] = v.x[a]; r0[2 * a + 1] = (int64_t)jt * T; dst[2 * a + 1] = Bt[a];
+    }
+    load_tiles_rc<D, 256, 2 * V>(src, n, r0, dst);
+  }
+  __syncthreads();
+  // squared row norms (fp32, k order): threads 0..63 the i rows, 64..127 the j rows of every view
+  if (threadIdx.x < 2 * T) {
+    const int r = threadIdx.x & (T - 1);
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      const float* X = threadIdx.x < T ? At[a] : Bt[a];
+      float sq = 0.f;
+      for (int k = 0; k < D; ++k) { const float t = X[r * LD + k]; sq = fmaf(t, t, sq); }
+      (threadIdx.x < T ? ra[a] : rb[a])[r] = sq;
+    }
+  }
+  __syncthreads();
   float Dv[V][4][4];  // [view][column tile c][row q]
 #pragma unroll
   for (int a = 0; a < V; ++a) {
-    __syncthreads();
-    load_tiles_rc<D, 256, 2>({v.x[a], v.x[a]}, n, {(int64_t)it * T, (int64_t)jt * T}, {At, Bt});
-    __syncthreads();
-    row_sq_r<D>(At, ra);
-    if (threadIdx.x >= T && threadIdx.x < 2 * T) {
-      float sq = 0.f;
-      for (int k = 0; k < D; ++k) { const float t = Bt[(threadIdx.x - T) * LD + k]; sq = fmaf(t, t, sq); }
-      rb[threadIdx.x - T] = sq;
-    }
-    __syncthreads();
     f32x4 g[4];
-    gram_mfma<D>(At, Bt, g);
+    gram_mfma<D>(At[a], Bt[a], g);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = 16 * w + 4 * h + q;
@@ -395,7 +416,7 @@ __global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n
       for (int c = 0; c < 4; ++c) {
         const int64_t gj = (int64_t)jt * T + 16 * c + i;
         // (r - 2 X X^T) + r^T, exactly the reference's evaluation order
-        const float qv = (ra[r] - 2.f * g[c][q]) + rb[16 * c + i];
+        const float qv = (ra[a][r] - 2.f * g[c][q]) + rb[a][16 * c + i];
         Dv[a][c][q] = (gi < n && gj < n) ? sqrtf(fmaxf(qv, 0.f) + 1e-8f) : 0.f;
         rs += Dv[a][c][q];
       }
@@ -404,40 +425,49 @@ __global__ __launch_bounds__(256) void dcor_tiles_mfma_kernel(Views v, int64_t n
     }
     if (off) {  // column sums = the jt rows' sums over column tile it (16 row groups, in order)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) colp[4 * w + h][16 * c + i] = ((Dv[a][c][0] + Dv[a][c][1]) + Dv[a][c][2]) + Dv[a][c][3];
-      __syncthreads();
-      if (threadIdx.x < T) {
-        float cs = 0.f;
-        for (int k = 0; k < 16; ++k) cs += colp[k][threadIdx.x];
-        const int64_t gj = (int64_t)jt * T + threadIdx.x;
-        if (gj < n) ws.row[((int64_t)a * nt + it) * n + gj] = cs;
-      }
+      for (int c = 0; c < 4; ++c) colp[a][4 * w + h][16 * c + i] = ((Dv[a][c][0] + Dv[a][c][1]) + Dv[a][c][2]) + Dv[a][c][3];
     }
   }
-  const int64_t blk = (int64_t)it * nt + jt;
+  // all unordered pair sums from the same tiles: wave sums now, the waves in order below
+  {
+    int k = 0;
 #pragma unroll
-  for (int a = 0; a < V; ++a)
+    for (int a = 0; a < V; ++a)
 #pragma unroll
-    for (int b = a; b < V; ++b) {
-      double sum = 0.0;
+      for (int b = a; b < V; ++b, ++k) {
+        double sum = 0.0;
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sum += (double)Dv[a][c][q] * (double)Dv[b][c][q];
-      sum = block_sum_d(sum, red);
-      if (threadIdx.x == 0) ws.S[blk * NP + pair_index(a, b, V)] = off ? 2.0 * sum : sum;
-    }
+          for (int q = 0; q < 4; ++q) sum += (double)Dv[a][c][q] * (double)Dv[b][c][q];
+        sum = group_sum_d<64>(sum);
+        if (lane == 0) red[w][pair_index(a, b, V)] = sum;
+      }
+  }
+  __syncthreads();
+  if (off && threadIdx.x < V * T) {
+    const int a = threadIdx.x / T, col = threadIdx.x % T;
+    float cs = 0.f;
+    for (int k = 0; k < 16; ++k) cs += colp[a][k][col];
+    const int64_t gj = (int64_t)jt * T + col;
+    if (gj < n) ws.row[((int64_t)a * nt + it) * n + gj] = cs;
+  }
+  if (threadIdx.x < NP) {
+    double sum = 0.0;
+    for (int x = 0; x < 4; ++x) sum += red[x][threadIdx.x];
+    ws.S[((int64_t)it * nt + jt) * NP + threadIdx.x] = off ? 2.0 * sum : sum;
+  }
 }
 
 // the row means and the block partials of the centred sums: one wave per 64 rows (thread i: row i of
 // every view, the j-tile row sums in fixed order), then per wave the sums of the means, of the pair
 // products of the means and of a contiguous chunk of the per-tile pair sums -> ws.bpart[block]
 template <int V>
-__global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
+__device__ __forceinline__ void dcor_means_block(int64_t n, DcorWS ws, int blk_id, int n_blk) {
   constexpr int NP = V * (V + 1) / 2;
   const int64_t nt = (n + T - 1) / T;
-  const int lane = threadIdx.x;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blk_id * 64 + lane;
   double mv[V];
   {  // every view's row sums: the loads of 8 j tiles of all views in flight together, added in j order
     double sv[V];
@@ -466,7 +496,7 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
       if (i < n) ws.mean[(int64_t)a * n + i] = mv[a];
     }
   }
-  double* bp = ws.bpart + (int64_t)blockIdx.x * DCOR_BP;
+  double* bp = ws.bpart + (int64_t)blk_id * DCOR_BP;
 #pragma unroll
   for (int a = 0; a < V; ++a) {
     const double t = group_sum_d<64>(mv[a]);
@@ -479,8 +509,8 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
       const double t = group_sum_d<64>(mv[a] * mv[b]);
       if (lane == 0) bp[MAXV + pair_index(a, b, V)] = t;
     }
-  const int64_t nblk = nt * nt, per = (nblk + gridDim.x - 1) / gridDim.x;
-  const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+  const int64_t nblk = nt * nt, per = (nblk + n_blk - 1) / n_blk;
+  const int64_t b0 = (int64_t)blk_id * per, b1 = b0 + per < nblk ? b0 + per : nblk;
   double lS[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) lS[k] = 0.0;
@@ -498,9 +528,10 @@ __global__ __launch_bounds__(64) void dcor_means_kernel(int64_t n, DcorWS ws) {
   }
 }
 
-// one wave: the block partials in block order -> Abar, centred sums, dcor values, backward coefficients
-__global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int nb, PairTab pt, DcorWS ws,
-                                                           float weight, float* out) {
+// the block partials in block order -> Abar, centred sums, dcor values, backward coefficients
+// (threads 0..DCOR_BP-1 of the workgroup; every thread reaches its barriers)
+__device__ __forceinline__ void dcor_finalize_body(int V, int64_t n, int nb, const PairTab& pt, DcorWS ws,
+                                                   float weight, float* out) {
   __shared__ double tot[DCOR_BP];
   __shared__ double Sc[MAXP];
   __shared__ double Ab[MAXV];
@@ -566,6 +597,22 @@ __global__ __launch_bounds__(64) void dcor_finalize_kernel(int V, int64_t n, int
     out[pt.n_pairs] = weight * total;  // (weight 1: the sum itself, exactly)
     for (int k = 0; k < NP; ++k) ws.coef[k] = coef[k];
   }
+}
+
+// The forward's second (and last) launch: one wave per 64 rows (the means stage); the last block
+// to finish (a device-scope counter) runs the finalize over every block's partials in block order
+// -- the same arithmetic as the round-5 means + finalize launches, so bit-identical.
+template <int V>
+__global__ __launch_bounds__(64) void dcor_means_finalize_kernel(int64_t n, int nb, PairTab pt, DcorWS ws,
+                                                                 float weight, float* out) {
+  __shared__ unsigned last;
+  dcor_means_block<V>(n, ws, blockIdx.x, nb);
+  __threadfence();  // this block's partials before its count
+  if (threadIdx.x == 0) last = atomicAdd(ws.ctr, 1u) == (unsigned)nb - 1u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every block's partials after the count
+  dcor_finalize_body(V, n, nb, pt, ws, weight, out);
 }
 
 // backward tiles: block (i-tile, j-split) accumulates P_a[i] = sum_j m_ij x_j and rowsum m
@@ -775,6 +822,151 @@ __global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_kernel(Views v, int64_t n
       load_tiles_rc<D, DB_NT>({v.x[a]}, n, {jt * T}, {Bt});
       __syncthreads();
       wx_mfma<D, NC>(Ms, Bt, acc[a], rw, NC * ch);
+    }
+  }
+  // row sums: the two column halves in order (ch 0, then 1)
+#pragma unroll
+  for (int a = 0; a < V; ++a)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i == 0) rowp[ch][a][16 * rw + 4 * h + q] = rowm[a][q];
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+    if (!v.dx[a]) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 16 * rw + 4 * h + q;
+      const int64_t gi = (int64_t)it * T + r;
+      if (gi < n) {
+        float* P = ws.P + (((int64_t)js * V + a) * n + gi) * D;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) P[16 * (NC * ch + c) + i] = acc[a][c][q];
+        if (i == 0 && ch == 0) ws.rowm[((int64_t)js * V + a) * n + gi] = rowp[0][a][r] + rowp[1][a][r];
+      }
+    }
+  }
+}
+
+// Round-6 form of dcor_bwd_mfma_kernel for V <= 3 (the LDS holds every view's i AND j tiles): the
+// i tiles, the first j tiles and the means issued in one load phase; per j tile ONE load phase for
+// all views (the round-5 kernel loaded each view's j tile twice, each behind its own barrier pair).
+// Same arithmetic in the same order.
+template <int V, int D>
+__global__ __launch_bounds__(DB_NT) void dcor_bwd_mfma_allb_kernel(Views v, int64_t n, DcorWS ws) {
+  static_assert(V <= 3, "LDS holds 2V tiles for V <= 3");
+  constexpr int LD = D + 4;
+  constexpr int NC = D / 32;  // output column tiles per wave
+  __shared__ __attribute__((aligned(16))) float Ai[V][T * LD];
+  __shared__ __attribute__((aligned(16))) float Bt[V][T * LD];
+  __shared__ float Ms[T * 65];
+  __shared__ float ra[V][T], rb[V][T];
+  __shared__ double mi[V][T], mj[V][T];
+  __shared__ float rowp[2][V][T];
+  const int64_t nt = (n + T - 1) / T;
+  const int it = blockIdx.x, js = blockIdx.y;
+  const int lane = threadIdx.x & 63, i = lane & 15, h = lane >> 4, w = threadIdx.x >> 6;
+  const int rw = w & 3, ch = w >> 2;
+  constexpr int NP = V * (V + 1) / 2;
+  double coef[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) coef[k] = ws.coef[k];
+  f32x4 acc[V][NC];
+  float rowm[V][4];
+#pragma unroll
+  for (int a = 0; a < V; ++a) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rowm[a][q] = 0.f;
+  }
+  bool first = true;
+  for (int64_t jt = js; jt < nt; jt += gridDim.y, first = false) {
+    if (!first) __syncthreads();  // every wave is done with the previous j tiles
+    if (threadIdx.x < T) {
+      const int64_t gi = (int64_t)it * T + threadIdx.x, gj = jt * T + threadIdx.x;
+      for (int a = 0; a < V; ++a) {
+        if (first) mi[a][threadIdx.x] = gi < n ? ws.mean[(int64_t)a * n + gi] : 0.0;
+        mj[a][threadIdx.x] = gj < n ? ws.mean[(int64_t)a * n + gj] : 0.0;
+      }
+    }
+    if (first) {
+      const float* src[2 * V];
+      int64_t r0[2 * V];
+      float* dst[2 * V];
+#pragma unroll
+      for (int a = 0; a < V; ++a) {
+        src[2 * a] = v.x[a]; r0[2 * a] = (int64_t)it * T; dst[2 * a] = Ai[a];
+        src[2 * a + 1] = v.x[a]; r0[2 * a + 1] = jt * T; dst[2 * a + 1] = Bt[a];
+      }
+      load_tiles_rc<D, DB_NT, 2 * V>(src, n, r0, dst);
+    } else {
+      const float* src[V];
+      int64_t r0[V];
+      float* dst[V];
+#pragma unroll
+      for (int a = 0; a < V; ++a) { src[a] = v.x[a]; r0[a] = jt * T; dst[a] = Bt[a]; }
+      load_tiles_rc<D, DB_NT, V>(src, n, r0, dst);
+    }
+    __syncthreads();
+    // squared row norms (fp32, k order): wave pairs 2a / 2a + 1 the i / j rows of view a
+    if (threadIdx.x < 2 * V * T) {
+      const int a = threadIdx.x / (2 * T), r = threadIdx.x & (T - 1);
+      const bool isj = (threadIdx.x / T) & 1;
+      if (first || isj) {
+        const float* X = isj ? Bt[a] : Ai[a];
+        float sq = 0.f;
+        for (int k = 0; k < D; ++k) { const float t = X[r * LD + k]; sq = fmaf(t, t, sq); }
+        (isj ? rb[a] : ra[a])[r] = sq;
+      }
+    }
+    __syncthreads();
+    float Dd[V][2][4], Dc[V][2][4];  // [view][column tile 2 ch + c][row q]
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      f32x4 g[2];
+      gram_mfma<D, 2>(Ai[a], Bt[a], g, rw, 2 * ch);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rw + 4 * h + q;
+        const int64_t gi = (int64_t)it * T + r;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int col = 16 * (2 * ch + c) + i;
+          const int64_t gj = jt * T + col;
+          const float qv = (ra[a][r] - 2.f * g[c][q]) + rb[a][col];
+          const float dd = sqrtf(fmaxf(qv, 0.f) + 1e-8f);
+          const float gt = qv > 0.f ? 1.f : (qv == 0.f ? 0.5f : 0.f);
+          const bool ok = gi < n && gj < n;
+          Dc[a][c][q] = ok ? (float)((double)dd - mi[a][r] - mj[a][col] + ws.Abar[a]) : 0.f;
+          Dd[a][c][q] = (ok && gi != gj) ? gt / (2.f * dd) : 0.f;  // gate(q) / (2 D), 0 off the tile / diagonal
+        }
+      }
+    }
+    bool ms_used = false;
+#pragma unroll
+    for (int a = 0; a < V; ++a) {
+      if (!v.dx[a]) continue;
+      if (ms_used) __syncthreads();  // every wave is done with Ms
+      ms_used = true;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * rw + 4 * h + q;
+        float rs = 0.f;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          double K = 2.0 * coef[pair_index(a, a, V)] * Dc[a][c][q];
+#pragma unroll
+          for (int b = 0; b < V; ++b)
+            if (b != a) K += coef[pair_index(a, b, V)] * Dc[b][c][q];
+          const float mv = (float)(K * (double)Dd[a][c][q]);
+          Ms[r * 65 + 16 * (2 * ch + c) + i] = mv;
+          rs += mv;
+        }
+        rowm[a][q] += group_sum<16>(rs);
+      }
+      __syncthreads();
+      wx_mfma<D, NC>(Ms, Bt[a], acc[a], rw, NC * ch);
     }
   }
   // row sums: the two column halves in order (ch 0, then 1)
@@ -1648,13 +1840,14 @@ extern "C" int fr_dcor_fwd_ex(const float* const* d_views, int n_views, int64_t 
   FR_LAUNCH_CHECK();
   const int nb = (int)fr::ceil_div(n, 64);
   switch (n_views) {
-    case 1: hipLaunchKernelGGL(dcor_means_kernel<1>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
-    case 2: hipLaunchKernelGGL(dcor_means_kernel<2>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
-    case 3: hipLaunchKernelGGL(dcor_means_kernel<3>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
-    default: hipLaunchKernelGGL(dcor_means_kernel<4>, dim3((unsigned)nb), dim3(64), 0, s, n, w); break;
+#define FR_DCOR_MF(VV) \
+  hipLaunchKernelGGL(dcor_means_finalize_kernel<VV>, dim3((unsigned)nb), dim3(64), 0, s, n, nb, pt, w, weight, d_out)
+    case 1: FR_DCOR_MF(1); break;
+    case 2: FR_DCOR_MF(2); break;
+    case 3: FR_DCOR_MF(3); break;
+    default: FR_DCOR_MF(4); break;
+#undef FR_DCOR_MF
   }
-  FR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dcor_finalize_kernel, dim3(1), dim3(64), 0, s, n_views, n, nb, pt, w, weight, d_out);
   FR_LAUNCH_CHECK();
   return FR_OK;
 }
@@ -1689,9 +1882,9 @@ extern "C" int fr_dcor_bwd_ex(const float* const* d_views, int n_views, int64_t 
   const dim3 grid((unsigned)nt, (unsigned)js);
   if (g_ssl_mfma && d == 64) {
     switch (n_views) {
-      case 1: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<1, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
-      case 2: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<2, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
-      case 3: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<3, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      case 1: hipLaunchKernelGGL((dcor_bwd_mfma_allb_kernel<1, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      case 2: hipLaunchKernelGGL((dcor_bwd_mfma_allb_kernel<2, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
+      case 3: hipLaunchKernelGGL((dcor_bwd_mfma_allb_kernel<3, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
       default: hipLaunchKernelGGL((dcor_bwd_mfma_kernel<4, 64>), grid, dim3(DB_NT), 0, s, v, n, w); break;
     }
     FR_LAUNCH_CHECK();

@@ -389,6 +389,35 @@ def test_dcor_three_views(cuda, n, ssl_kernels):
         assert err <= max(err32, 1e-4 * np.abs(gr).max()) + 1e-9, (err, err32, np.abs(gr).max())
 
 
+@pytest.mark.parametrize("n,nv,nograd", [(1500, 3, 1), (1500, 2, -1), (700, 4, 2), (130, 2, 0)])
+def test_dcor_views_splits_and_no_grad(cuda, n, nv, nograd, ssl_kernels):
+    """View counts 2..4 (the all-views-staged backward for <= 3, the per-view one for 4), more
+    than 16 row tiles (workgroups of the backward loop over several j tiles), and a view that needs
+    no gradient (the kernels skip its dX)."""
+    from FoodRec.engine import ops
+    d = 64
+    g = torch.Generator().manual_seed(n + nv)
+    views = [torch.randn(n, d, generator=g, dtype=torch.float64, requires_grad=True) for _ in range(nv)]
+    pairs = {1: [(0, 0)], 2: [(0, 1)], 3: [(0, 1), (0, 2), (2, 1)], 4: [(0, 1), (2, 3), (1, 3)]}[nv]
+    ref = sum(O.correlation_distance(views[a], views[b]) for a, b in pairs)
+    (0.9 * ref.sum()).backward()
+    v32 = [v.detach().float().requires_grad_(True) for v in views]
+    ref32 = sum(O.correlation_distance(v32[a], v32[b]) for a, b in pairs)
+    (0.9 * ref32.sum()).backward()
+    dv = [v.detach().float().to(cuda).requires_grad_(k != nograd) for k, v in enumerate(views)]
+    got = ops.dcor_loss(dv, pairs)
+    (0.9 * got.sum()).backward()
+    err_val, err32_val = abs(got.item() - ref.item()), abs(ref32.item() - ref.item())
+    assert err_val <= max(err32_val, 1e-5 * abs(ref.item())), (err_val, err32_val)
+    for k, (v, v3, w) in enumerate(zip(views, v32, dv)):
+        if k == nograd:
+            assert w.grad is None
+            continue
+        gr, g3, gg = v.grad.numpy(), v3.grad.numpy(), w.grad.cpu().numpy()
+        err, err32 = np.abs(gg - gr).max(), np.abs(g3 - gr).max()
+        assert err <= max(err32, 1e-4 * np.abs(gr).max()) + 1e-9, (k, err, err32, np.abs(gr).max())
+
+
 @pytest.mark.parametrize("d", [16, 32, 64, 128])
 @pytest.mark.parametrize("b", [512, 37])
 def test_infonce(cuda, b, d, ssl_kernels):

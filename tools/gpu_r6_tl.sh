@@ -1,5 +1,5 @@
 #!/bin/bash
-# (round 6) One HealthRec step's kernel timeline (steps 26-28 from the end: the last 20 feed launches are the
+# (round 6) One HealthRec step's kernel timeline (TL_KS steps from the end, default 38 40 42: the last ~20 feed launches are the
 # eager kernel pass) under rocprofv3 --kernel-trace for each "tag:ENV=V ..." spec.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,7 +14,7 @@ for spec in "$@"; do
     2> $OUT/tl_$tag.err || { echo "$tag rocprof failed"; tail -20 $OUT/tl_$tag.err; exit 1; }
   for kv in $envs; do unset "${kv%%=*}"; done
   f=$(find $OUT/tl_$tag -name "*kernel_trace.csv" | head -1)
-  for k in 26 27 28; do
+  for k in ${TL_KS:-38 40 42}; do
     python3 $R/tools/step_timeline.py "$f" $k > $OUT/step_timeline_${tag}_$k.txt && tail -1 $OUT/step_timeline_${tag}_$k.txt
   done
 done
