@@ -59,6 +59,11 @@ constexpr int kAppendDepth = 2;  // APPEND's register stages of item tiles (1 or
 // APPEND: the candidate masks of tile t - 1 are formed between tile t's MFMAs (the matrix pipe
 // runs while the VALU compares), only the rare append passes stay outside the MFMA stream
 constexpr bool kAppendPipe = FR_TOPK_PIPE != 0;
+#ifndef FR_TOPK_RING
+#define FR_TOPK_RING 2
+#endif
+// APPEND's LDS ring of staged item tiles: 2 (one barrier per tile) or 4 (two tiles per barrier)
+constexpr int kAppendRing = FR_TOPK_RING;
 
 template <typename T, int D, int NB = 1>
 struct Cfg {
@@ -160,7 +165,8 @@ enum { kList = 0, kAppend = 1 };
 template <typename T, int D, int KC, int MODE, int NB>
 __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   using C = Cfg<T, D, NB>;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  constexpr int RING = MODE == kAppend ? kAppendRing : 2;
+  __shared__ __attribute__((aligned(16))) char smem[RING * C::STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -290,11 +296,21 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
       if (uvalid) a.cc[region] = 0;
       return;
     }
-    FR_LOAD_TILE(0, stgA)
-    FR_STORE_TILE(0, stgA)
-    __syncthreads();
-    FR_LOAD_TILE(1, stgA)
-    if constexpr (DEPTH == 2) { FR_LOAD_TILE(2, stgB) }
+    if constexpr (RING == 4) {  // tiles 0, 1 staged; 2, 3 in registers
+      FR_LOAD_TILE(0, stgA)
+      FR_LOAD_TILE(1, stgB)
+      FR_STORE_TILE(0, stgA)
+      FR_STORE_TILE(1, stgB)
+      __syncthreads();
+      FR_LOAD_TILE(2, stgA)
+      FR_LOAD_TILE(3, stgB)
+    } else {
+      FR_LOAD_TILE(0, stgA)
+      FR_STORE_TILE(0, stgA)
+      __syncthreads();
+      FR_LOAD_TILE(1, stgA)
+      if constexpr (DEPTH == 2) { FR_LOAD_TILE(2, stgB) }
+    }
   } else {
     if (n_tiles > 0) {
       FR_LOAD_TILE(0, stgA)
@@ -365,7 +381,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   auto tile_step = [&](const int t, uint4 (&cur)[C::CH], f32x16 (&acc)[NB], const f32x16 (&prev)[NB])
                        __attribute__((always_inline)) {
     // ---- scores of this tile on the matrix cores (NB independent 32-item blocks)
-    const char* abuf = smem + (t & 1) * C::STAGE;
+    const char* abuf = smem + (t & (RING - 1)) * C::STAGE;
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
@@ -443,12 +459,14 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
         select_block(av, mask, ib, wf);
       }
     }
-    // ---- next tile into the other buffer; prefetch DEPTH + 1 tiles ahead into the freed stage
-    // (APPEND: unconditionally -- past the last tile the stores go to a buffer no one reads again
-    // and the loads re-read the split's last row)
-    if (MODE == kAppend || t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
-    __syncthreads();
-    if (MODE == kAppend || t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
+    if constexpr (RING == 2) {
+      // ---- next tile into the other buffer; prefetch DEPTH + 1 tiles ahead into the freed stage
+      // (APPEND: unconditionally -- past the last tile the stores go to a buffer no one reads again
+      // and the loads re-read the split's last row)
+      if (MODE == kAppend || t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
+      __syncthreads();
+      if (MODE == kAppend || t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
+    }
   };
   f32x16 accX[NB], accY[PIPE ? NB : 1];
   if constexpr (PIPE) {
@@ -467,6 +485,15 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
       } else {
         tile_step(t, stgA, accX, accX);
         tile_step(t + 1, stgB, accX, accX);
+      }
+      if constexpr (RING == 4) {
+        // tiles t + 2, t + 3 into the buffers tiles t - 2, t - 1 left (every wave passed the
+        // previous barrier after computing them), then one barrier for both, then the next pair
+        FR_STORE_TILE((t + 2) & 3, stgA)
+        FR_STORE_TILE((t + 3) & 3, stgB)
+        __syncthreads();
+        FR_LOAD_TILE(t + 4, stgA)
+        FR_LOAD_TILE(t + 5, stgB)
       }
     }
     if constexpr (PIPE) {  // the last tile (t - 1)
@@ -684,6 +711,10 @@ constexpr int64_t kSampledMinItems = 32768;  // below this: one exact LIST pass
 #define FR_TOPK_SUB 16
 #endif
 constexpr int64_t kSubRatio = FR_TOPK_SUB;   // sub-sample stride / sample stride
+#ifndef FR_TOPK_SCAP
+#define FR_TOPK_SCAP 32
+#endif
+constexpr int64_t kSampleStrideCap = FR_TOPK_SCAP;  // the sample's stride at >= 1M items
 
 // The launch plan and the workspace carve-up (identical in the size query and the call).
 struct Plan {
@@ -713,7 +744,7 @@ Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   // thresholds in two levels: the exact top-k of a sub-sample (every stride0-th item, LIST) bounds
   // an APPEND pass over the sample (every stride-th item) whose merged top-k gives the threshold of
   // the APPEND pass over all items (~k * stride candidates per user)
-  p.stride = std::min<int64_t>(16, std::max<int64_t>(2, n_items / 65536));
+  p.stride = std::min<int64_t>(kSampleStrideCap, std::max<int64_t>(2, n_items * kSampleStrideCap / (16 * 65536)));
   p.n_sample = fr::ceil_div(n_items, p.stride);
   p.stride0 = p.stride * kSubRatio;
   p.n_sub = fr::ceil_div(n_items, p.stride0);
