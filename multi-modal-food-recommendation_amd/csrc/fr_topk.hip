@@ -160,12 +160,16 @@ struct ScoreArgs {
   const float* thr; int cap; float* cs; int32_t* ci; int32_t* cc;   // APPEND: [slot][split][half][cap], counts
 };
 
-enum { kList = 0, kAppend = 1 };
+// kGmax: per lane 8 running maxima (score, item) -- one per pair of score positions (j, j + 8) of the
+// MFMA fragment -- over the lane's share of the items (APPEND's staging and schedule, no selection
+// passes): distinct items whose merged k-th best is a lower bound of the user's k-th best
+enum { kList = 0, kAppend = 1, kGmax = 2 };
 
 template <typename T, int D, int KC, int MODE, int NB>
 __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   using C = Cfg<T, D, NB>;
-  constexpr int RING = MODE == kAppend ? kAppendRing : 2;
+  constexpr bool STREAM = MODE != kList;  // APPEND / GMAX: register-held staging, pipelined epilogue
+  constexpr int RING = STREAM ? kAppendRing : 2;
   __shared__ __attribute__((aligned(16))) char smem[RING * C::STAGE];
 
   const int tid = threadIdx.x;
@@ -233,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   // item tiles: global -> registers (one tile ahead) -> LDS (double buffer, swizzled chunks).
   // APPEND keeps each staged chunk's row, LDS offset and global source (advanced one tile of rows
   // per step) in registers; the register-heavy LIST kernel recomputes them per tile.
-  constexpr int NSH = MODE == kAppend ? C::CH : 1;
+  constexpr int NSH = STREAM ? C::CH : 1;
   int srow[NSH], sdst[NSH];
   const char* ssrc[NSH];
 #pragma unroll
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   const int n_split = (int)(i_hi - i_lo);
 #define FR_LOAD_TILE(T_, S_)                                                                        \
   _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
-    if constexpr (MODE == kAppend) {                                                                \
+    if constexpr (STREAM) {                                                                         \
       /* unconditional (rows past the split re-read its last row; their scores are dropped): */     \
       /* with no load skipped on any path the compiler's counted waits stay exact */                \
       const int rr = min((T_) * C::TILE + min(srow[c], C::TILE - 1), n_split - 1);                 \
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   }
 #define FR_STORE_TILE(BUF_, S_)                                                                     \
   _Pragma("unroll") for (int c = 0; c < C::CH; ++c) {                                               \
-    if constexpr (MODE == kAppend) {                                                                \
+    if constexpr (STREAM) {                                                                         \
       if (srow[c] < C::TILE) *reinterpret_cast<uint4*>(smem + (BUF_) * C::STAGE + sdst[c]) = S_[c];  \
     } else {                                                                                        \
       const int x = tid + c * kThreads;                                                             \
@@ -280,20 +284,32 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
   // A-fragment LDS offsets of this lane (row r of each 32-item block, chunk 2s+h): held in
   // registers by the APPEND kernel, recomputed per use by the register-heavy LIST kernel
   constexpr int NA = C::BF ? C::KS : C::KS / 4;
-  constexpr int NAH = MODE == kAppend ? NA : 1;
+  constexpr int NAH = STREAM ? NA : 1;
   int aoff[NAH];
 #pragma unroll
   for (int s = 0; s < NAH; ++s) aoff[s] = a_off<T, D>(r, h, s);
-#define FR_AOFF(S_) (MODE == kAppend ? aoff[(MODE == kAppend) ? (S_) : 0] : a_off<T, D>(r, h, (S_)))
+#define FR_AOFF(S_) (STREAM ? aoff[STREAM ? (S_) : 0] : a_off<T, D>(r, h, (S_)))
 
   // register stages of the item tiles: APPEND keeps two (the global loads of tile t + 3 are issued
   // after tile t's barrier and have two tiles of MFMA work to land in), LIST one (its key lists
   // hold the registers)
-  constexpr int DEPTH = MODE == kAppend ? kAppendDepth : 1;
+  constexpr int DEPTH = STREAM ? kAppendDepth : 1;
   uint4 stgA[C::CH], stgB[DEPTH == 2 ? C::CH : 1];
-  if constexpr (MODE == kAppend) {
+  // GMAX: this lane's 8 running maxima, group g = positions g and g + 8 of every 32-item block's
+  // fragment: the score and 2 q + (position g + 8), q the block's index in the split (the item of
+  // position j is i_lo + 32 q + 4h + (j&3) + 8(j>>2)); -1: none
+  float gmx[MODE == kGmax ? 8 : 1];
+  int32_t gq[MODE == kGmax ? 8 : 1];
+#pragma unroll
+  for (int g = 0; g < (MODE == kGmax ? 8 : 1); ++g) { gmx[g] = -INFINITY; gq[g] = -1; }
+  if constexpr (STREAM) {
     if (n_tiles <= 0) {  // an empty split: no rows to clamp to
-      if (uvalid) a.cc[region] = 0;
+      if (uvalid) {
+        if constexpr (MODE == kAppend) a.cc[region] = 0;
+        else
+#pragma unroll
+          for (int g = 0; g < 8; ++g) { a.ls[region * 8 + g] = -INFINITY; a.li[region * 8 + g] = INT32_MAX; }
+      }
       return;
     }
     if constexpr (RING == 4) {  // tiles 0, 1 staged; 2, 3 in registers
@@ -374,7 +390,33 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
       }
     }
   };
-  constexpr bool PIPE = MODE == kAppend && kAppendPipe;
+  constexpr bool PIPE = STREAM && kAppendPipe;
+  static_assert(MODE != kGmax || PIPE, "the position maxima are folded between the MFMAs only");
+  // GMAX: fold one block's scores into the running maxima (strict >: the first -- lowest -- item
+  // keeps a tie; NaN never enters); `live` (wave-uniform) false skips the block
+  auto gmax_fold = [&](const f32x16& av, const int q, const bool live) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const bool hi = av[g + 8] > av[g];  // (a tie keeps the lower item)
+      const float m = hi ? av[g + 8] : av[g];
+      const bool up = live && m > gmx[g];
+      gmx[g] = up ? m : gmx[g];
+      gq[g] = up ? 2 * q + (hi ? 1 : 0) : gq[g];
+    }
+  };
+  // the same with the split's end checked (its last real tile): positions past it take no part
+  auto gmax_fold_tail = [&](const f32x16& av, const int q) __attribute__((always_inline)) {
+    const int lim = (int)(i_hi - i_lo - 32 * (int64_t)q - 4 * h);  // items of the block this lane may take
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const float lo_v = (g & 3) + 8 * (g >> 2) < lim ? av[g] : -INFINITY;
+      const bool hi = (g & 3) + 8 * (g >> 2) + 16 < lim && av[g + 8] > lo_v;
+      const float m = hi ? av[g + 8] : lo_v;
+      const bool up = m > gmx[g];
+      gmx[g] = up ? m : gmx[g];
+      gq[g] = up ? 2 * q + (hi ? 1 : 0) : gq[g];
+    }
+  };
   // one tile: its scores from LDS buffer t & 1 into `acc` -- with PIPE the previous tile's scores
   // (`prev`) are selected after them, their masks formed between the MFMAs; without, this tile's
   // own -- then the next tile (in `cur`) into the other buffer, and `cur` refilled DEPTH + 1 ahead
@@ -400,9 +442,13 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[s], acc[bb], 0, 0, 0);
-      if constexpr (PIPE) {
+      if constexpr (PIPE && MODE == kAppend) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
+      }
+      if constexpr (PIPE && MODE == kGmax) {  // (the previous tile is never the split's last here)
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) gmax_fold(prev[bb], (t - 1) * NB + bb, t - 1 < n_tiles - 1);
       }
       // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight);
       // PIPE: the previous tile's compares spread over the MFMA slots
@@ -432,14 +478,20 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[sg].w, acc[bb], 0, 0, 0);
         }
       }
-      if constexpr (PIPE) {
+      if constexpr (PIPE && MODE == kAppend) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
+      }
+      if constexpr (PIPE && MODE == kGmax) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) gmax_fold(prev[bb], (t - 1) * NB + bb, t - 1 < n_tiles - 1);
       }
     }
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
-      if constexpr (PIPE) {
+      if constexpr (PIPE && MODE == kGmax) {
+        // (folded between the MFMAs)
+      } else if constexpr (PIPE) {
         // the previous tile's block bb (t - 1 < 0: its scores are NaN, no bit set)
         select_block(prev[bb], pmask[bb], i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
       } else {
@@ -463,9 +515,9 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
       // ---- next tile into the other buffer; prefetch DEPTH + 1 tiles ahead into the freed stage
       // (APPEND: unconditionally -- past the last tile the stores go to a buffer no one reads again
       // and the loads re-read the split's last row)
-      if (MODE == kAppend || t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
+      if (STREAM || t + 1 < n_tiles) { FR_STORE_TILE((t + 1) & 1, cur) }
       __syncthreads();
-      if (MODE == kAppend || t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
+      if (STREAM || t + 1 + DEPTH < n_tiles) { FR_LOAD_TILE(t + 1 + DEPTH, cur) }
     }
   };
   f32x16 accX[NB], accY[PIPE ? NB : 1];
@@ -496,7 +548,18 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
         FR_LOAD_TILE(t + 5, stgB)
       }
     }
-    if constexpr (PIPE) {  // the last tile (t - 1)
+    if constexpr (PIPE && MODE == kGmax) {
+      // the split's last real tile n_tiles - 1 (in accY if the count is even, else in accX: the
+      // extra tile's scores in accY are dropped), folded with its end checked
+      const int q0 = (n_tiles - 1) * NB;
+      if (n_tiles & 1) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) gmax_fold_tail(accX[bb], q0 + bb);
+      } else {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) gmax_fold_tail(accY[bb], q0 + bb);
+      }
+    } else if constexpr (PIPE) {  // the last tile (t - 1)
 #pragma unroll
       for (int bb = 0; bb < NB; ++bb)
         select_block(accY[bb], cand_mask(accY[bb]), i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
@@ -520,6 +583,14 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
         a.ls[o + q] = empty ? -INFINITY : fr_unord((uint32_t)(kk >> 32));
         a.li[o + q] = empty ? INT32_MAX : (int32_t)(~(uint32_t)kk);
       }
+    }
+  } else if constexpr (MODE == kGmax) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const int j = g + 8 * (gq[g] & 1);
+      a.ls[region * 8 + g] = gmx[g];
+      a.li[region * 8 + g] = gq[g] < 0 ? INT32_MAX
+                                       : (int32_t)((i_lo + 32 * (int64_t)(gq[g] >> 1) + 4 * h + (j & 3) + 8 * (j >> 2)) * a.item_mul);
     }
   } else {
     a.cc[region] = cnt;
@@ -677,6 +748,8 @@ hipError_t launch_score_t(const ScoreArgs& a, hipStream_t s) {
   void (*kern)(ScoreArgs);
   if constexpr (MODE == kAppend) {
     kern = topk_score_kernel<T, D, 1, kAppend, 2>;
+  } else if constexpr (MODE == kGmax) {
+    kern = topk_score_kernel<T, D, 1, kGmax, 2>;
   } else {
     kern = a.k <= 10 ? topk_score_kernel<T, D, 10, kList, 1>
                      : (a.k <= 20 ? topk_score_kernel<T, D, 20, kList, 1> : topk_score_kernel<T, D, 32, kList, 1>);
@@ -711,6 +784,12 @@ constexpr int64_t kSampledMinItems = 32768;  // below this: one exact LIST pass
 #define FR_TOPK_SUB 16
 #endif
 constexpr int64_t kSubRatio = FR_TOPK_SUB;   // sub-sample stride / sample stride
+#ifndef FR_TOPK_GMAX
+#define FR_TOPK_GMAX 1
+#endif
+// thresholds from the sample's per-lane position maxima (one GMAX pass + merge) instead of the
+// two-level LIST / APPEND scheme
+constexpr bool kTopkGmax = FR_TOPK_GMAX != 0;
 #ifndef FR_TOPK_SCAP
 #define FR_TOPK_SCAP 32
 #endif
@@ -718,11 +797,11 @@ constexpr int64_t kSampleStrideCap = FR_TOPK_SCAP;  // the sample's stride at >=
 
 // The launch plan and the workspace carve-up (identical in the size query and the call).
 struct Plan {
-  bool sampled;
+  bool sampled, gmax;
   int64_t stride, n_sample, stride0, n_sub;
   int ns0, ns1, ns2, cap1, cap;
   int64_t span0, span1, span2;
-  int64_t off_l0, off_thr1, off_cs1, off_ci1, off_cc1;
+  int64_t off_l0, off_thr1, off_cs1, off_ci1, off_cc1, off_g;
   int64_t off_l1, off_thr, off_cs, off_ci, off_cc, off_flag, off_l2, total;
 };
 
@@ -752,12 +831,19 @@ Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   split_plan(n_users, p.n_sample, &p.ns1, &p.span1);
   p.cap1 = region_cap(k, kSubRatio, 2 * p.ns1);
   p.cap = region_cap(k, p.stride, 2 * p.ns2);
-  p.off_l0 = take(n_users * p.ns0 * 2 * (int64_t)k * 8);
-  p.off_thr1 = take(n_users * 4);
   const int64_t nreg1 = n_users * p.ns1 * 2;
-  p.off_cs1 = take(nreg1 * p.cap1 * 4);
-  p.off_ci1 = take(nreg1 * p.cap1 * 4);
-  p.off_cc1 = take(nreg1 * 4);
+  // the position-group maxima need enough entries per user (16 per split) to bound the k-th best
+  // tightly; with few splits (>= 128k users) the two-level scheme is kept
+  p.gmax = kTopkGmax && 16 * p.ns1 >= 3 * k;
+  if (p.gmax) {
+    p.off_g = take(nreg1 * 8 * 8);  // [region][8] scores, then [region][8] items
+  } else {
+    p.off_l0 = take(n_users * p.ns0 * 2 * (int64_t)k * 8);
+    p.off_thr1 = take(n_users * 4);
+    p.off_cs1 = take(nreg1 * p.cap1 * 4);
+    p.off_ci1 = take(nreg1 * p.cap1 * 4);
+    p.off_cc1 = take(nreg1 * 4);
+  }
   p.off_thr = take(n_users * 4);
   const int64_t nreg = n_users * p.ns2 * 2;
   p.off_cs = take(nreg * p.cap * 4);
@@ -844,10 +930,29 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
     return FR_OK;
   }
   FR_REQUIRE(ldi * p.stride0 * es < INT32_MAX, "item row stride too large for the sampled passes");
-  float* thr1 = reinterpret_cast<float*>(ws + p.off_thr1);
   float* thr = reinterpret_cast<float*>(ws + p.off_thr);
   int32_t* flag_cnt = reinterpret_cast<int32_t*>(ws + p.off_flag);
   int32_t* flag_list = flag_cnt + 1;
+  if (p.gmax) {
+    // 1-2. the sample's per-lane position-group maxima (distinct items: 8 per lane, split and half),
+    //      merged into their k-th best admissible score -- a lower bound of the user's k-th best
+    //      (-inf if fewer remain), within ~k^2 / (2 * entries) ranks of the sample's exact one
+    ScoreArgs gs = sa;
+    gs.It = d_I; gs.ldi = ldi * p.stride; gs.n_items = p.n_sample; gs.item_mul = p.stride;
+    gs.n_splits = p.ns1; gs.span = p.span1;
+    const int64_t nreg1 = n_users * p.ns1 * 2;
+    gs.ls = reinterpret_cast<float*>(ws + p.off_g);
+    gs.li = reinterpret_cast<int32_t*>(ws + p.off_g + nreg1 * 8 * 4);
+    e = launch_score<kGmax>(dtype, d, gs, s);
+    if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+    MergeArgs mg = ma;
+    mg.ps = gs.ls; mg.pi = gs.li; mg.cnt = nullptr; mg.cap = 8; mg.n_regions = 2 * p.ns1;
+    mg.ex_ptr = d_ex_ptr; mg.ex_col = d_ex_col; mg.ex_base = ex_base;
+    mg.thr_out = thr;
+    e = launch_merge(mg, merge_blocks, s);
+    if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  } else {
+  float* thr1 = reinterpret_cast<float*>(ws + p.off_thr1);
   // 1. a lower bound of every user's k-th best: the exact top-k of every stride0-th item
   e = list_pass(d_I, ldi * p.stride0, p.n_sub, p.stride0, p.ns0, p.span0, ws + p.off_l0, nullptr, nullptr, thr1);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
@@ -868,6 +973,7 @@ extern "C" int fr_topk_scores(const void* d_U, int64_t ldu, int64_t n_users, con
   mt.thr_out = thr; mt.thr_fb = thr1;
   e = launch_merge(mt, merge_blocks, s);
   if (e != hipSuccess) return fr::fail(FR_EHIP, std::string("fr_topk_scores: ") + hipGetErrorString(e));
+  }
   // 3. all items: GEMM + threshold, candidates appended
   ScoreArgs ap = sa;
   ap.It = d_I; ap.ldi = ldi; ap.n_items = n_items; ap.item_mul = 1; ap.n_splits = p.ns2; ap.span = p.span2;

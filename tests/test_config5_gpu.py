@@ -216,9 +216,11 @@ def test_full_sort_topk_sampled_path(cuda, dtype, d, n_users, n_items, k):
 
 def test_full_sort_topk_overflow_paths(cuda):
     """Adversarial score order for the sampled path: the sub-sample (multiples of 32) scores lowest,
-    the rest of the sample (even items) in the middle, odd items highest -- the sample pass's regions
-    overflow (the user keeps the sub-sample's looser threshold), then the all-items pass overflows
-    (the user is recomputed by the exact LIST pass).  Result = the exact top-k."""
+    the rest of the sample (even items) in the middle, odd items highest -- with the two-level
+    thresholds the sample pass's regions overflow (the user keeps the sub-sample's looser threshold);
+    with the position-group maxima the threshold sits at the sample's (middle) level; either way the
+    all-items pass overflows and the user is recomputed by the exact LIST pass.  Result = the exact
+    top-k."""
     from FoodRec.engine import ops
     rng = np.random.default_rng(77)
     n_users, n_items, d, k = 64, 140000, 64, 20
@@ -230,6 +232,22 @@ def test_full_sort_topk_overflow_paths(cuda):
     s, i, _ = ops.full_sort_topk(torch.from_numpy(U).to(cuda), torch.from_numpy(I).to(cuda), k, exclude=ex)
     _check_topk(s.cpu().numpy(), i.cpu().numpy(), U, I, k, excl, 2e-6)
     assert (i.cpu().numpy() % 2 == 1).all()
+
+
+def test_full_sort_topk_many_users_two_level(cuda):
+    """>= 128k users: one split per user tile, too few position-group maxima per user for the
+    threshold -- the two-level (sub-sample LIST, sample APPEND + merge) thresholds run instead.
+    Checked on a subset of users against the oracle."""
+    from FoodRec.engine import ops
+    rng = np.random.default_rng(31)
+    n_users, n_items, d, k = 140000, 33000, 64, 20
+    U = rng.standard_normal((n_users, d)).astype(np.float32)
+    I = rng.standard_normal((n_items, d)).astype(np.float32)
+    excl = [rng.choice(n_items, size=rng.integers(0, 30), replace=False).tolist() for _ in range(n_users)]
+    ex = _excl_csr(excl, 0, cuda)
+    s, i, _ = ops.full_sort_topk(torch.from_numpy(U).to(cuda), torch.from_numpy(I).to(cuda), k, exclude=ex)
+    sel = rng.choice(n_users, size=48, replace=False)
+    _check_topk(s.cpu().numpy()[sel], i.cpu().numpy()[sel], U[sel], I, k, [excl[x] for x in sel], 2e-6)
 
 
 def test_full_sort_topk_no_mask_and_permuted_ids(cuda):
