@@ -790,6 +790,10 @@ constexpr int64_t kSubRatio = FR_TOPK_SUB;   // sub-sample stride / sample strid
 // thresholds from the sample's per-lane position maxima (one GMAX pass + merge) instead of the
 // two-level LIST / APPEND scheme
 constexpr bool kTopkGmax = FR_TOPK_GMAX != 0;
+#ifndef FR_TOPK_GSPLIT
+#define FR_TOPK_GSPLIT 1
+#endif
+constexpr int kGmaxSplitMul = FR_TOPK_GSPLIT;  // the GMAX pass's splits: the plan's times this (<= 64)
 #ifndef FR_TOPK_SCAP
 #define FR_TOPK_SCAP 32
 #endif
@@ -835,8 +839,14 @@ Plan make_plan(int64_t n_users, int64_t n_items, int k) {
   // the position-group maxima need enough entries per user (16 per split) to bound the k-th best
   // tightly; with few splits (>= 128k users) the two-level scheme is kept
   p.gmax = kTopkGmax && 16 * p.ns1 >= 3 * k;
+  if (p.gmax && kGmaxSplitMul > 1) {  // more splits: more maxima per user (a tighter bound)
+    const int64_t ns = std::min<int64_t>(64, (int64_t)p.ns1 * kGmaxSplitMul);
+    p.span1 = fr::align_up(fr::ceil_div(p.n_sample, ns), 2 * kTile);
+    p.ns1 = (int)fr::ceil_div(p.n_sample, p.span1);
+  }
+  const int64_t nreg1g = n_users * p.ns1 * 2;
   if (p.gmax) {
-    p.off_g = take(nreg1 * 8 * 8);  // [region][8] scores, then [region][8] items
+    p.off_g = take(nreg1g * 8 * 8);  // [region][8] scores, then [region][8] items
   } else {
     p.off_l0 = take(n_users * p.ns0 * 2 * (int64_t)k * 8);
     p.off_thr1 = take(n_users * 4);
