@@ -59,6 +59,12 @@ constexpr int kAppendDepth = 2;  // APPEND's register stages of item tiles (1 or
 // APPEND: the candidate masks of tile t - 1 are formed between tile t's MFMAs (the matrix pipe
 // runs while the VALU compares), only the rare append passes stay outside the MFMA stream
 constexpr bool kAppendPipe = FR_TOPK_PIPE != 0;
+#ifndef FR_TOPK_PRETEST
+#define FR_TOPK_PRETEST 1
+#endif
+// APPEND: only the max of each block's 16 scores between the MFMAs; the candidate bits and the
+// append passes only for the blocks where some lane's max reaches the threshold
+constexpr bool kAppendPretest = FR_TOPK_PRETEST != 0;
 #ifndef FR_TOPK_RING
 #define FR_TOPK_RING 2
 #endif
@@ -344,13 +350,23 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
     for (int j = 0; j < 16; ++j) m |= av[j] >= wv ? (1u << j) : 0u;
     return m;
   };
+  // the largest of a block's 16 scores (v_max3 tree; a NaN score drops out -- it never passes the
+  // threshold compare either)
+  auto max16 = [&](const f32x16& av) __attribute__((always_inline)) {
+    float m0 = fmaxf(fmaxf(av[0], av[1]), av[2]), m1 = fmaxf(fmaxf(av[3], av[4]), av[5]);
+    float m2 = fmaxf(fmaxf(av[6], av[7]), av[8]), m3 = fmaxf(fmaxf(av[9], av[10]), av[11]);
+    float m4 = fmaxf(fmaxf(av[12], av[13]), av[14]);
+    return fmaxf(fmaxf(fmaxf(m0, m1), m2), fmaxf(fmaxf(m3, m4), av[15]));
+  };
   // selection of one block (scores av, items ib + (j&3) + 8(j>>2)) given its candidate bits
   auto select_block = [&](const f32x16& av, uint32_t mask, const int64_t ib, const float wf)
                           __attribute__((always_inline)) {
-    if (ib + 28 >= i_hi) {  // the split's last block: drop items past its end
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (ib + (j & 3) + 8 * (j >> 2) >= i_hi) mask &= ~(1u << j);
+    {  // the split's last block: drop items past its end -- a 32-bit offset mask (no 64-bit compares
+       // per position: if-converted, those cost ~50 VALU per block on every block)
+      const int64_t left = i_hi - ib;  // items of the block from this lane's first offset on
+      const uint32_t vb = left >= 32 ? 0xffffffffu : (left <= 0 ? 0u : (1u << (int)left) - 1u);
+      const uint32_t jm = (vb & 0xfu) | ((vb >> 4) & 0xf0u) | ((vb >> 8) & 0xf00u) | ((vb >> 12) & 0xf000u);
+      mask &= jm;  // position j <-> offset (j & 3) + 8 (j >> 2)
     }
     if (!uvalid) mask = 0u;
     // every lane handles its next candidate in the same pass
@@ -429,6 +445,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[bb][j] = 0.f;
     uint32_t pmask[NB];
+    bool pany[NB];  // APPEND pre-test: this lane's block holds a score >= the threshold
     if constexpr (C::BF) {
       // the tile's A fragments are read ahead of the MFMA chains that consume them in order
       bf16x8 af[NB][C::KS];
@@ -442,7 +459,10 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[bb][s], bf[s], acc[bb], 0, 0, 0);
-      if constexpr (PIPE && MODE == kAppend) {
+      if constexpr (PIPE && MODE == kAppend && kAppendPretest) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) pany[bb] = max16(prev[bb]) >= wv;
+      } else if constexpr (PIPE && MODE == kAppend) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
       }
@@ -453,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
       // schedule: 4 LDS reads ahead, then MFMA / next read interleaved (3-4 reads in flight);
       // PIPE: the previous tile's compares spread over the MFMA slots
       constexpr int NM = NB * C::KS;
-      constexpr int VPM = PIPE ? (NB * 40 + NM - 1) / NM : 0;  // VALU per MFMA slot
+      constexpr int VPM = PIPE ? (NB * (MODE == kAppend && kAppendPretest ? 10 : 40) + NM - 1) / NM : 0;  // VALU per MFMA slot
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
       for (int s = 0; s < NM - 4; ++s) {
@@ -478,7 +498,10 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
           acc[bb] = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf[sg].w, acc[bb], 0, 0, 0);
         }
       }
-      if constexpr (PIPE && MODE == kAppend) {
+      if constexpr (PIPE && MODE == kAppend && kAppendPretest) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) pany[bb] = max16(prev[bb]) >= wv;
+      } else if constexpr (PIPE && MODE == kAppend) {
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) pmask[bb] = cand_mask(prev[bb]);
       }
@@ -491,6 +514,10 @@ __global__ __launch_bounds__(kThreads) void topk_score_kernel(ScoreArgs a) {
     for (int bb = 0; bb < NB; ++bb) {
       if constexpr (PIPE && MODE == kGmax) {
         // (folded between the MFMAs)
+      } else if constexpr (PIPE && kAppendPretest) {
+        // the previous tile's block bb, only when some lane's pre-test passed (t - 1 < 0: NaN scores)
+        if (__ballot(pany[bb]))
+          select_block(prev[bb], cand_mask(prev[bb]), i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
       } else if constexpr (PIPE) {
         // the previous tile's block bb (t - 1 < 0: its scores are NaN, no bit set)
         select_block(prev[bb], pmask[bb], i_lo + (int64_t)(t - 1) * C::TILE + bb * 32 + 4 * h, wv);
@@ -795,7 +822,7 @@ constexpr bool kTopkGmax = FR_TOPK_GMAX != 0;
 #endif
 constexpr int kGmaxSplitMul = FR_TOPK_GSPLIT;  // the GMAX pass's splits: the plan's times this (<= 64)
 #ifndef FR_TOPK_SCAP
-#define FR_TOPK_SCAP 32
+#define FR_TOPK_SCAP 16
 #endif
 constexpr int64_t kSampleStrideCap = FR_TOPK_SCAP;  // the sample's stride at >= 1M items
 
