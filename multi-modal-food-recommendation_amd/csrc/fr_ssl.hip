@@ -1121,6 +1121,14 @@ __device__ __forceinline__ float nce_row_sumsq(const float4 (&fv)[4]) {
   return group_sum<NceRowLayout<D>::LPR>(ss);
 }
 
+// x / den rounded as fp32 division does, from one double reciprocal per row: RN32(x * RN64(1 / den)).
+// A quotient of two fp32 numbers is never within 2^-49 (relative) of an fp32 rounding boundary when
+// it is a normal number, and the double product is within 2^-52 of it, so the result is the correctly
+// rounded quotient -- 3 operations per element instead of the ~10 of the division.  (Only a quotient
+// below 2^-126, |x| < 2^-126 |den|, could land on a subnormal midpoint; normalised rows never come
+// near that.)  Both the normalize pass and the fused staging use it: Hn stays bit-identical between them.
+__device__ __forceinline__ float div_rden(float x, double rden) { return (float)((double)x * rden); }
+
 // Hn = H / max(|H|, 1e-12) and the norms, rows of every view (the staging layout above: LPR lanes per
 // row, every lane of a wave active for the DPP sum; rows past the end read zeros and store nothing)
 template <int D>
@@ -1138,11 +1146,12 @@ __global__ __launch_bounds__(256) void nce_normalize_kernel(Views vw, int V, int
   const float den = fmaxf(nr, 1e-12f);
   if (!ok) return;
   if (c0 == 0) ws.nrm[r] = nr;
+  const double rd = 1.0 / (double)den;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (c0 + q < Ly::D4)
       reinterpret_cast<float4*>(ws.Hn + r * D)[c0 + q] =
-          make_float4(fv[q].x / den, fv[q].y / den, fv[q].z / den, fv[q].w / den);
+          make_float4(div_rden(fv[q].x, rd), div_rden(fv[q].y, rd), div_rden(fv[q].z, rd), div_rden(fv[q].w, rd));
 }
 
 __device__ __forceinline__ int64_t nce_partner(int64_t i, int64_t b) { return i < b ? i + b : i - b; }
@@ -1453,6 +1462,7 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
       const int r = ps * RPP + (int)threadIdx.x / LPR, c0 = ((int)threadIdx.x % LPR) * 4;
       const float nr = sqrtf(nce_row_sumsq<D>(fv[ps]));
       const float den = fmaxf(nr, 1e-12f);
+      const double rd = 1.0 / (double)den;
       if (r < T) {
         const int64_t gr = r0 + r;
         float* hn_g = nullptr;
@@ -1466,7 +1476,7 @@ __global__ __launch_bounds__(256) void nce_lse_mfma2_kernel(int64_t b, float inv
         for (int q = 0; q < 4; ++q) {
           if (c0 + q >= D4) continue;
           const float4 x = fv[ps][q];
-          const float4 hn = make_float4(x.x / den, x.y / den, x.z / den, x.w / den);
+          const float4 hn = make_float4(div_rden(x.x, rd), div_rden(x.y, rd), div_rden(x.z, rd), div_rden(x.w, rd));
           *reinterpret_cast<float4*>(Bt + r * LD + 4 * (c0 + q)) = hn;
           if (hn_g) reinterpret_cast<float4*>(hn_g)[c0 + q] = hn;
         }
