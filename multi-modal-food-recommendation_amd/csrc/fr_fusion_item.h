@@ -134,8 +134,12 @@ __device__ __forceinline__ void fusion_item_bwd(const ItemFwd<L>& f, const Fusio
   const bool clampM = nr <= kNormEps;
   const float N = fmaxf(nr, kNormEps);
   float dM[L];
+  // the L quotients by the same N^3 through one double reciprocal: RN32(x * RN64(1 / y)) is the
+  // correctly rounded x / y for every normal quotient (fr_ssl.hip's div_rden), 3 operations each
+  const float dkN = dk / N, dkS = dk * S;
+  const double rN3 = 1.0 / (double)(N * N * N);
 #pragma unroll
-  for (int t = 0; t < L; ++t) dM[t] = clampM ? dk / N : dk / N - f.M[t] * (dk * S) / (N * N * N);
+  for (int t = 0; t < L; ++t) dM[t] = clampM ? dkN : dkN - (float)((double)(f.M[t] * dkS) * rN3);
   const float hr = sqrtf(fmaf(f.H[0], f.H[0], f.H[1] * f.H[1]));
   const bool clampH = hr <= kNormEps;
   const float hN = fmaxf(hr, kNormEps);
@@ -224,8 +228,9 @@ __device__ __forceinline__ void fusion_item_out(const ItemFwd<L>& f, float num, 
   for (int t = 0; t < L; ++t) n2 = fmaf(f.M[t], f.M[t], n2);
   const float N = fmaxf(sqrtf(n2), kNormEps);
   float s = 0.f;
+  const double rN = 1.0 / (double)N;  // (the L quotients by N through one double reciprocal, as above)
 #pragma unroll
-  for (int t = 0; t < L; ++t) s += f.M[t] / N;
+  for (int t = 0; t < L; ++t) s += (float)((double)f.M[t] * rN);
   know = s / num;
   const float hN = fmaxf(sqrtf(fmaf(f.H[0], f.H[0], f.H[1] * f.H[1])), kNormEps);
   hin = (f.H[0] / hN + f.H[1] / hN) * 0.5f;
